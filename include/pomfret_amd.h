@@ -1,0 +1,201 @@
+/*
+ * pomfret_amd.h -- C ABI of the MI355X (gfx950) implementation of Pomfret's
+ * per-window methylation-phasing hot path.
+ *
+ * Plain C, plain pointers and sizes; no HIP or torch types cross this
+ * boundary.  The library (libpomfret_amd.so) owns its device buffers; callers
+ * own every host buffer they pass in.  No entry point calls exit(): errors are
+ * returned as negative PF_ERR_* codes ("no evidence" is decision = -1, not an
+ * error), matching the reference's split between fatal exits and -1 decisions
+ * (reference blockjoin.c:1059, 1150, 4266-4270, 4313-4320).
+ *
+ * Reference interfaces replaced (all line numbers: /root/reference/<file>):
+ *
+ *   pf_methphase_windows / pf_methphase_run
+ *       replaces the per-window call haplotag_region_given_bam()
+ *       (blockjoin.c:4217-4335) as driven by the kt_for worker
+ *       blockjoin_one_chrom_callback() (blockjoin.c:4350-4426, dispatched at
+ *       blockjoin.c:4560) and by the serial report loop (blockjoin.c:5054-5077).
+ *       One call processes a whole batch of windows (gaps) from any number of
+ *       contigs; decisions land in caller-owned arrays exactly where the
+ *       reference writes ranges->decisions.a[i] (blockjoin.c:4406), and the
+ *       per-read tags the worker stores for joined windows (blockjoin.c:4408-4423)
+ *       are returned per read.
+ *
+ *   pf_haptag_reads
+ *       replaces parse_variants_for_one_read() + haptag_one_read_with_variants()
+ *       (blockjoin.c:1545-1840) as driven by pre_haplotagging_read_in_one_ref()
+ *       (blockjoin.c:1841-1898), the --bam-is-untagged (-u) pre-pass.
+ *
+ *   pf_fisher_exact
+ *       the two-sided Fisher exact test the reference borrows from htslib
+ *       (kt_fisher_exact, called at blockjoin.c:3926).
+ *
+ * Input layout ("SoA"): what the reference's BAM window loader
+ * (load_reads_given_interval, blockjoin.c:1043-1173) keeps per read after its
+ * filters, flattened:
+ *   - windows in any order; each window owns a contiguous run of reads;
+ *   - reads of a window in BAM order (the order sam_itr_next returns them);
+ *   - each read owns a contiguous run of 5mC calls in the order
+ *     get_mod_poss_on_ref() produces them (blockjoin.c:605-792).
+ */
+#ifndef POMFRET_AMD_H
+#define POMFRET_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PF_ABI_VERSION 1
+
+/* error codes */
+#define PF_OK               0
+#define PF_ERR_ARG         -1   /* bad argument / inconsistent batch */
+#define PF_ERR_HIP         -2   /* HIP runtime error (no device, launch failure) */
+#define PF_ERR_NOMEM       -3   /* device or host allocation failed */
+#define PF_ERR_UNSUPPORTED -4   /* configuration outside what this build implements */
+#define PF_ERR_LIMIT       -5   /* input exceeds a documented hard limit */
+#define PF_ERR_INTERNAL    -6
+
+/* Methmer / tagging configuration.  Mirrors mmr_config_t (blockjoin.h:7-16)
+ * plus the per-contig n_candidates_per_iter (blockjoin.c:4357-4390). */
+typedef struct pf_cfg {
+    int32_t k;                  /* methmer length, cli -k (default 3, cli.c:67)            */
+    int32_t k_span;             /* methmer base-span limit, cli -l (default 5000)          */
+    int32_t cov_for_selection;  /* site min meth AND unmeth calls (blockjoin.c:3270-3271)  */
+    int32_t cov_for_runtime;    /* min hap0+hap1 methmer count to use a site (3669-3691)   */
+    int32_t n_cand;             /* candidates scored per greedy iteration (4039-4045)      */
+    int32_t hard_cov;           /* left-side per-haplotype read minimum, 15 (1161)         */
+    int32_t flags;              /* PF_FLAG_*                                               */
+    int32_t reserved;
+} pf_cfg_t;
+
+#define PF_FLAG_NONE 0
+
+/* One batch of windows.  A "window" is one call of haplotag_region_given_bam:
+ * the gap [win_start, win_end] (blockjoin.c:4397-4398) and the reads that
+ * load_reads_given_interval fetched for [s-READBACK, e+READBACK] and kept. */
+typedef struct pf_window_batch {
+    uint32_t n_windows;
+    uint32_t n_reads;
+    uint64_t n_calls;
+    const uint32_t *win_start;     /* [n_windows] gap start s (ranges->starts.a[i])         */
+    const uint32_t *win_end;       /* [n_windows] gap end e   (ranges->ends.a[i])           */
+    const uint32_t *win_read_off;  /* [n_windows+1] reads of window w: [off[w], off[w+1])   */
+    const int32_t  *win_cov_sel;   /* [n_windows] or NULL -> cfg.cov_for_selection          */
+    const int32_t  *win_cov_rt;    /* [n_windows] or NULL -> cfg.cov_for_runtime            */
+    const int32_t  *win_n_cand;    /* [n_windows] or NULL -> cfg.n_cand                     */
+    const uint32_t *read_start;    /* [n_reads] core.pos, 0-based (blockjoin.c:1124)        */
+    const uint32_t *read_end;      /* [n_reads] bam_endpos, exclusive (blockjoin.c:1125)    */
+    const uint8_t  *read_hp;       /* [n_reads] HP-1, 254 if untagged (910-923, 1114-1122)  */
+    const uint64_t *read_call_off; /* [n_reads+1] calls of read r: [off[r], off[r+1])      */
+    const uint32_t *call_pos;      /* [n_calls] reference position of the CpG's C           */
+    const uint8_t  *call_cat;      /* [n_calls] 0 meth (q>=hi), 1 unmeth (q<lo), 2 nocall   */
+} pf_window_batch_t;
+
+/* Per-window results.  Every pointer except decision may be NULL. */
+typedef struct pf_window_out {
+    int8_t   *decision;      /* [n_windows] 0 cis, 1 trans, -1 no join (4313-4320)       */
+    uint8_t  *read_hp;       /* [n_reads] rs->a[j].hp when the window returns; these are
+                                the tags the worker stores when decision>=0 (4408-4423)   */
+    int32_t  *dir_table;     /* [n_windows*2*4] 2x2 table buf[raw][new] per direction:
+                                index (w*2+dir)*4 + raw*2 + new; dir 0 = forward
+                                (left->right, scored on right strict reads), dir 1 =
+                                backward (scored on left strict reads) (3881-3893)       */
+    int32_t  *dir_join;      /* [n_windows*2] haplotag_region2 return: 0,1,-1 (4088)     */
+    int32_t  *dir_which_way; /* [n_windows*2] evaluate_separation1 join_dir (-9 on fail) */
+    double   *dir_fisher_p;  /* [n_windows*2] two-sided p (1.0 when not reached)          */
+    float    *dir_score;     /* [n_windows*2] evaluate_separation1 return value           */
+    uint32_t *win_n_sites;   /* [n_windows] methmer sites (ms->n); 0 => window skipped     */
+    uint32_t *win_n_reads;   /* [n_windows] rs->n after the left-coverage check (1161)    */
+} pf_window_out_t;
+
+/* ------------------------------------------------------------------ */
+/* -u pre-pass: known phased variants of one contig and reads to tag.  */
+
+/* variant ops as in blockjoin.c:28-31 */
+#define PF_VAR_M 0
+#define PF_VAR_X 1
+#define PF_VAR_I 2
+#define PF_VAR_D 3
+
+typedef struct pf_known_vars {
+    uint32_t n;
+    const uint32_t *pos;       /* [n] 0-based, as insert_variant_from_vcf_line stores it (1432-1543) */
+    const uint32_t *len;       /* [n] op length                                               */
+    const uint8_t  *op;        /* [n] PF_VAR_X / PF_VAR_I / PF_VAR_D                          */
+    const uint8_t  *haptag;    /* [n] haplotype carrying REF (GT[0])                          */
+    const uint64_t *char_off;  /* [n+1] allele chars (seq_nt4 codes 0..4) of variant i        */
+    const uint8_t  *chars;
+} pf_known_vars_t;
+
+/* Reads of ONE contig in BAM order, primary mapped only (flag filter of
+ * blockjoin.c:1869-1870 already applied by the caller). */
+typedef struct pf_read_aln_batch {
+    uint32_t n_reads;
+    const uint32_t *start;      /* [n] core.pos                                  */
+    const uint32_t *end;        /* [n] bam_endpos                                */
+    const uint64_t *cigar_off;  /* [n+1] into cigar                              */
+    const uint32_t *cigar;      /* BAM encoding: len<<4 | op                     */
+    const uint64_t *seq_off;    /* [n+1] byte offsets into seq (4-bit packed)    */
+    const uint32_t *seq_len;    /* [n] l_qseq                                    */
+    const uint8_t  *seq;        /* BAM 4-bit packed SEQ                          */
+    const uint64_t *md_off;     /* [n+1] into md (no terminator needed)          */
+    const char     *md;         /* MD:Z strings, concatenated                    */
+} pf_read_aln_batch_t;
+
+/* ------------------------------------------------------------------ */
+
+typedef struct pf_ctx pf_ctx_t;        /* one device, one HIP stream          */
+typedef struct pf_dbatch pf_dbatch_t;  /* a window batch resident in HBM      */
+
+int  pf_abi_version(void);
+int  pf_device_count(void);
+const char *pf_strerror(int code);
+
+/* Context bound to one device (one process per GPU). */
+int  pf_ctx_create(int device, pf_ctx_t **out);
+void pf_ctx_destroy(pf_ctx_t *ctx);
+
+/* Upload a batch to HBM.  Validates it (offsets monotone, sizes, limits) and
+ * keeps a device copy plus the few host-side arrays the decision epilogue
+ * needs.  The caller's host arrays may be freed afterwards. */
+int  pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg,
+                     const pf_window_batch_t *batch, pf_dbatch_t **out);
+void pf_batch_free(pf_dbatch_t *db);
+uint32_t pf_batch_n_windows(const pf_dbatch_t *db);
+uint32_t pf_batch_n_reads(const pf_dbatch_t *db);
+
+/* Run the hot path on a resident batch: all kernels, then the 2x2 tables and
+ * tags come back to the host, where the Fisher test and the join decision
+ * are applied.  Synchronous. */
+int  pf_methphase_run(pf_ctx_t *ctx, pf_dbatch_t *db, pf_window_out_t *out);
+
+/* Split form of pf_methphase_run for timing: enqueue only / wait + finish. */
+int  pf_methphase_launch(pf_ctx_t *ctx, pf_dbatch_t *db);
+int  pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *db, pf_window_out_t *out);
+
+/* One-shot convenience: upload + run + free on `device`. */
+int  pf_methphase_windows(int device, const pf_cfg_t *cfg,
+                          const pf_window_batch_t *batch, pf_window_out_t *out);
+
+/* Average device time (ms) of each kernel of the last run, measured with HIP
+ * events on the library's stream.  names/ms arrays of length *n. */
+int  pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n);
+
+/* -u pre-pass: hp_out[r] in {0, 1, 254} for every read of one contig. */
+int  pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *known,
+                     const pf_read_aln_batch_t *reads, uint8_t *hp_out);
+
+/* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
+ * the observed table. */
+double pf_fisher_exact(int n11, int n12, int n21, int n22,
+                       double *left, double *right, double *two);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POMFRET_AMD_H */

@@ -1,0 +1,138 @@
+"""CPU oracle for Pomfret's methylation-phasing hot path -- TEST INFRASTRUCTURE.
+
+ctypes wrapper around oracle/build/libpf_oracle.so (plain-C restatement of the
+reference, oracle/pf_oracle.c).  Only tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py may import this package; the product
+(pomfret_amd/) never does.
+
+Parity status: window definition pinned by the reference's example fixtures;
+methylation core "parity unpinned" (reference unbuildable here: htslib absent).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+
+from pomfret_amd.abi import (Config, KnownVars, ReadAlnBatch, WindowBatch, WindowResult)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libpf_oracle.so")
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(_LIB_PATH):
+        subprocess.run(["make", "-C", _HERE], check=True, stdout=subprocess.DEVNULL)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(_LIB_PATH)
+        L.orc_methphase_windows.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_methphase_windows.restype = C.c_int
+        L.orc_methphase_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_window_sites.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int,
+                                       C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_window_methmers.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int,
+                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_long]
+        L.orc_window_methmers.restype = C.c_long
+        L.orc_fisher_exact.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_double)] * 3
+        L.orc_fisher_exact.restype = C.c_double
+        L.orc_search_arr.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_int]
+        L.orc_haptag_reads.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_vcf_gaps.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
+        _lib = L
+    return _lib
+
+
+def methphase(cfg: Config, batch: WindowBatch, n_threads: int = 1) -> WindowResult:
+    res = WindowResult.alloc(batch.n_windows, batch.n_reads)
+    c, b, o = cfg.to_c(), batch.to_c(), res.to_c()
+    rc = lib().orc_methphase_windows(C.byref(c), C.byref(b), C.byref(o), int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"oracle failed: {rc}")
+    return res
+
+
+def trace(cfg: Config, batch: WindowBatch, cap: int = 4096):
+    W = batch.n_windows
+    ids = np.zeros((W, 2, cap), np.uint32)
+    tags = np.zeros((W, 2, cap), np.uint8)
+    scores = np.zeros((W, 2, cap), np.float32)
+    counts = np.zeros((W, 2), np.uint32)
+    c, b = cfg.to_c(), batch.to_c()
+    lib().orc_methphase_trace(C.byref(c), C.byref(b), cap, ids.ctypes.data, tags.ctypes.data,
+                              scores.ctypes.data, counts.ctypes.data)
+    return ids, tags, scores, counts
+
+
+def window_sites(cfg: Config, batch: WindowBatch, w: int, direction: int):
+    ro = batch.win_read_off
+    co = batch.read_call_off
+    cap = int(co[ro[w + 1]] - co[ro[w]]) + 1
+    real = np.zeros(cap, np.uint32)
+    starts = np.zeros(cap, np.uint32)
+    lens = np.zeros(cap, np.uint8)
+    c, b = cfg.to_c(), batch.to_c()
+    n = lib().orc_window_sites(C.byref(c), C.byref(b), w, direction, real.ctypes.data,
+                               starts.ctypes.data, lens.ctypes.data)
+    return real[:n], starts[:n], lens[:n]
+
+
+def window_methmers(cfg: Config, batch: WindowBatch, w: int, direction: int, cap: int = 1 << 22):
+    ro = batch.win_read_off
+    R = int(ro[w + 1] - ro[w])
+    mmr_n = np.zeros(max(R, 1), np.uint32)
+    start_i = np.zeros(max(R, 1), np.uint32)
+    keys = np.zeros(cap, np.uint32)
+    c, b = cfg.to_c(), batch.to_c()
+    tot = lib().orc_window_methmers(C.byref(c), C.byref(b), w, direction, mmr_n.ctypes.data,
+                                    start_i.ctypes.data, keys.ctypes.data, cap)
+    if tot < 0:
+        raise RuntimeError("key buffer too small")
+    return mmr_n[:R], start_i[:R], keys[:tot]
+
+
+def fisher(n11, n12, n21, n22):
+    l, r, t = C.c_double(), C.c_double(), C.c_double()
+    q = lib().orc_fisher_exact(n11, n12, n21, n22, C.byref(l), C.byref(r), C.byref(t))
+    return q, l.value, r.value, t.value
+
+
+def search_arr(a, v, which_end=0):
+    a = np.ascontiguousarray(a, np.uint32)
+    idx = C.c_uint32(0)
+    st = lib().orc_search_arr(a.ctypes.data if len(a) else None, len(a), int(v), C.byref(idx), which_end)
+    return st, idx.value
+
+
+def haptag_reads(known: KnownVars, reads: ReadAlnBatch) -> np.ndarray:
+    out = np.zeros(max(reads.n_reads, 1), np.uint8)
+    k, r = known.to_c(), reads.to_c()
+    lib().orc_haptag_reads(C.byref(k), C.byref(r), out.ctypes.data)
+    return out[:reads.n_reads]
+
+
+def vcf_gaps(path: str, readback: int = 50_000):
+    with tempfile.NamedTemporaryFile("r", suffix=".txt", delete=True) as tf:
+        n = lib().orc_vcf_gaps(path.encode(), readback, tf.name.encode())
+        if n < 0:
+            raise RuntimeError(f"vcf_gaps failed {n}")
+        out, cur = [], None
+        for line in open(tf.name):
+            f = line.rstrip("\n").split("\t")
+            if f[0] == "contig":
+                cur = dict(name=f[1], abs_start=int(f[2]), abs_end=int(f[3]), raw=[], gaps=[], dropped=[])
+                out.append(cur)
+            else:
+                key = {"raw": "raw", "gap": "gaps", "dropped": "dropped"}[f[0]]
+                cur[key].append((int(f[1]), int(f[2])))
+        return out

@@ -1,0 +1,73 @@
+/*
+ * pf_oracle.h -- CPU oracle for the Pomfret methylation-phasing hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is a plain-C restatement of the reference
+ * algorithm (nanoporetech/pomfret v0.1-r14, /root/reference/blockjoin.c),
+ * function by function, used as the checker for the HIP implementation and as
+ * the CPU baseline leg of bench.py.  Nothing in pomfret_amd/ links or calls
+ * it; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * load it.
+ *
+ * PARITY PINNING: the reference itself cannot be built here (blockjoin.c
+ * includes htslib headers; htslib is absent from this image and stand-ins are
+ * not allowed), and the reference ships no test vectors for this path (its
+ * example BAM is missing, .MISSING_LARGE_BLOBS).  The window-definition part
+ * (VCF PS -> gaps) is pinned by the reference's example fixtures
+ * (tests/test_oracle_fixtures.py); the methylation core is "parity unpinned":
+ * it is checked only by line-by-line restatement of the reference source
+ * (each function cites the lines it follows) and by hand-worked unit cases.
+ */
+#ifndef PF_ORACLE_H
+#define PF_ORACLE_H
+#include <stdint.h>
+#include "../include/pomfret_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Whole batch, n_threads pthreads over windows (kt_for analogue). */
+int orc_methphase_windows(const pf_cfg_t *cfg, const pf_window_batch_t *b,
+                          pf_window_out_t *out, int n_threads);
+
+/* Per-(window,dir) greedy trace: for every successful iteration the tagged
+ * read (window-local index), its tag and the float score bits.  `cap` entries
+ * per (window,dir); counts[w*2+dir] = number recorded (may exceed cap). */
+int orc_methphase_trace(const pf_cfg_t *cfg, const pf_window_batch_t *b,
+                        uint32_t cap, uint32_t *read_ids, uint8_t *tags,
+                        float *scores, uint32_t *counts);
+
+/* Sites and methmers of one window (for unit tests). Returns S.  Arrays sized
+ * by the caller: sites/starts/lens >= n_calls of the window. */
+int orc_window_sites(const pf_cfg_t *cfg, const pf_window_batch_t *b, uint32_t w,
+                     int dir, uint32_t *sites_real, uint32_t *sites_starts,
+                     uint8_t *lens);
+
+/* Methmers of every read of window w in direction dir.  mmr_n[r], start_i[r]
+ * for the window's reads; keys written back to back (cap entries max).
+ * Returns total keys or -1 if cap too small. */
+long orc_window_methmers(const pf_cfg_t *cfg, const pf_window_batch_t *b,
+                         uint32_t w, int dir, uint32_t *mmr_n, uint32_t *start_i,
+                         uint32_t *keys, long cap);
+
+/* htslib kt_fisher_exact restatement. */
+double orc_fisher_exact(int n11, int n12, int n21, int n22,
+                        double *left, double *right, double *two);
+
+/* search_arr (blockjoin.c:391-421); exposed for unit tests. */
+int orc_search_arr(const uint32_t *a, uint32_t l, uint32_t v, uint32_t *idx, int which_end);
+
+/* -u pre-pass for one contig (reads in BAM order). */
+int orc_haptag_reads(const pf_known_vars_t *known, const pf_read_aln_batch_t *reads,
+                     uint8_t *hp_out);
+
+/* Window definition from a (gz) VCF: per contig the raw gaps, then
+ * merge_close_intervals(READBACK).  Results written as text lines to
+ * out_path: "contig\tabs_start\tabs_end\n" then "raw\ts\te", "gap\ts\te",
+ * "dropped\ts\te".  Returns number of contigs or <0. */
+int orc_vcf_gaps(const char *vcf_path, int readback, const char *out_path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
