@@ -1,0 +1,164 @@
+"""ctypes binding of libpomfret_amd.so (the product: HIP kernels + C ABI).
+
+The library is built in-tree (pomfret_amd/libpomfret_amd.so, see
+__graft_entry__.build()).  There is no CPU fallback: if the library or a GPU
+is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from .abi import (Config, KnownVars, PfCfg, PfKnownVars, PfReadAlnBatch, PfWindowBatch,
+                  PfWindowOut, ReadAlnBatch, WindowBatch, WindowResult)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpomfret_amd.so")
+_lib = None
+
+
+class PomfretError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PomfretError(f"{LIB_PATH} not built: run __graft_entry__.build() or "
+                               f"`make -C pomfret_amd/csrc`")
+        L = C.CDLL(LIB_PATH)
+        L.pf_abi_version.restype = C.c_int
+        L.pf_device_count.restype = C.c_int
+        L.pf_strerror.restype = C.c_char_p
+        L.pf_strerror.argtypes = [C.c_int]
+        L.pf_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.pf_ctx_destroy.argtypes = [C.c_void_p]
+        L.pf_batch_upload.argtypes = [C.c_void_p, C.POINTER(PfCfg), C.POINTER(PfWindowBatch),
+                                      C.POINTER(C.c_void_p)]
+        L.pf_batch_free.argtypes = [C.c_void_p]
+        L.pf_batch_n_windows.argtypes = [C.c_void_p]
+        L.pf_batch_n_windows.restype = C.c_uint32
+        L.pf_batch_n_reads.argtypes = [C.c_void_p]
+        L.pf_batch_n_reads.restype = C.c_uint32
+        L.pf_methphase_run.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(PfWindowOut)]
+        L.pf_methphase_launch.argtypes = [C.c_void_p, C.c_void_p]
+        L.pf_methphase_finish.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(PfWindowOut)]
+        L.pf_methphase_windows.argtypes = [C.c_int, C.POINTER(PfCfg), C.POINTER(PfWindowBatch),
+                                           C.POINTER(PfWindowOut)]
+        L.pf_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p),
+                                           C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.pf_fisher_exact.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_double)] * 3
+        L.pf_fisher_exact.restype = C.c_double
+        if hasattr(L, "pf_haptag_reads"):
+            L.pf_haptag_reads.argtypes = [C.c_void_p, C.POINTER(PfKnownVars),
+                                          C.POINTER(PfReadAlnBatch), C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise PomfretError(f"{what}: {lib().pf_strerror(rc).decode()} ({rc})")
+
+
+def device_count() -> int:
+    return int(lib().pf_device_count())
+
+
+def fisher_exact(n11, n12, n21, n22):
+    l, r, t = C.c_double(), C.c_double(), C.c_double()
+    q = lib().pf_fisher_exact(n11, n12, n21, n22, C.byref(l), C.byref(r), C.byref(t))
+    return q, l.value, r.value, t.value
+
+
+class Context:
+    """One device + one HIP stream (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(lib().pf_ctx_create(int(device), C.byref(h)), "pf_ctx_create")
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().pf_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, cfg: Config, batch: WindowBatch) -> "DeviceBatch":
+        return DeviceBatch(self, cfg, batch)
+
+    def kernel_times(self):
+        names = (C.c_char_p * 8)()
+        ms = (C.c_float * 8)()
+        n = C.c_int(8)
+        _check(lib().pf_last_kernel_times(self.handle, names, ms, C.byref(n)), "kernel_times")
+        return {names[i].decode(): float(ms[i]) for i in range(n.value)}
+
+    def haptag_reads(self, known: KnownVars, reads: ReadAlnBatch) -> np.ndarray:
+        out = np.zeros(max(reads.n_reads, 1), np.uint8)
+        k, r = known.to_c(), reads.to_c()
+        _check(lib().pf_haptag_reads(self.handle, C.byref(k), C.byref(r), out.ctypes.data),
+               "pf_haptag_reads")
+        return out[:reads.n_reads]
+
+
+class DeviceBatch:
+    """A window batch resident in HBM (pf_dbatch_t)."""
+
+    def __init__(self, ctx: Context, cfg: Config, batch: WindowBatch):
+        self.ctx = ctx
+        self.n_windows = batch.n_windows
+        self.n_reads = batch.n_reads
+        c, b = cfg.to_c(), batch.to_c()
+        h = C.c_void_p()
+        _check(lib().pf_batch_upload(ctx.handle, C.byref(c), C.byref(b), C.byref(h)),
+               "pf_batch_upload")
+        self.handle = h
+
+    def free(self):
+        if self.handle:
+            lib().pf_batch_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def run(self, out: WindowResult = None) -> WindowResult:
+        if out is None:
+            out = WindowResult.alloc(self.n_windows, self.n_reads)
+        o = out.to_c()
+        _check(lib().pf_methphase_run(self.ctx.handle, self.handle, C.byref(o)), "pf_methphase_run")
+        return out
+
+    def launch(self):
+        _check(lib().pf_methphase_launch(self.ctx.handle, self.handle), "pf_methphase_launch")
+
+    def finish(self, out: WindowResult = None) -> WindowResult:
+        if out is None:
+            out = WindowResult.alloc(self.n_windows, self.n_reads)
+        o = out.to_c()
+        _check(lib().pf_methphase_finish(self.ctx.handle, self.handle, C.byref(o)),
+               "pf_methphase_finish")
+        return out
+
+
+def methphase_windows(cfg: Config, batch: WindowBatch, device: int = 0) -> WindowResult:
+    """One-shot: upload + run + free (pf_methphase_windows)."""
+    out = WindowResult.alloc(batch.n_windows, batch.n_reads)
+    c, b, o = cfg.to_c(), batch.to_c(), out.to_c()
+    _check(lib().pf_methphase_windows(int(device), C.byref(c), C.byref(b), C.byref(o)),
+           "pf_methphase_windows")
+    return out

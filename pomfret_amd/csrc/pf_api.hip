@@ -1,0 +1,429 @@
+// pf_api.hip -- C ABI of libpomfret_amd.so (declared in include/pomfret_amd.h).
+//
+// Host driver around the three methphase kernels (pf_kernels.hip):
+//   upload  : validate the SoA batch, canonicalise per-read call order, size the
+//             HBM workspace, copy everything to the device once (resident batch);
+//   launch  : K1 sites -> K2 methmers -> K3 greedy on one HIP stream, then async
+//             D2H of the 2x2 tables, site counts and forward tags;
+//   finish  : wait, re-run with larger arenas if a device arena overflowed
+//             (deterministic: results never depend on arena sizes), then the
+//             host epilogue (Fisher test + join decision, pf_host.c).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <vector>
+#include "pf_device.h"
+#include "pf_host.h"
+#include "../../include/pomfret_amd.h"
+
+__global__ void pf_k1_sites(pf_dev_batch d);
+__global__ void pf_k2_methmers(pf_dev_batch d);
+__global__ void pf_k3_greedy(pf_dev_batch d);
+
+#define PF_NKERN 3
+static const char *k_names[PF_NKERN] = {"pf_k1_sites", "pf_k2_methmers", "pf_k3_greedy"};
+
+struct pf_ctx {
+    int device;
+    hipStream_t stream;
+    hipEvent_t ev[PF_NKERN + 1];
+    float last_ms[PF_NKERN];
+    int have_times;
+};
+
+struct pf_dbatch {
+    pf_ctx *ctx;
+    pf_cfg_t cfg;
+    uint32_t W, R;
+    uint64_t N;
+    // host copies used by the epilogue
+    std::vector<uint32_t> h_win_read_off;
+    std::vector<uint8_t> h_read_hp;
+    // device buffers (owned)
+    std::vector<void *> allocs;
+    pf_dev_batch d;
+    // host pinned result staging
+    int32_t *h_table;
+    uint32_t *h_S, *h_nreads, *h_status;
+    uint8_t *h_hp_fwd;
+    unsigned long long *h_ctr;   // keys, big, scr counters after a run
+    uint64_t site_total;
+    int launched;
+};
+
+#define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "[E::pomfret_amd] %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+    return PF_ERR_HIP; } } while (0)
+
+extern "C" int pf_abi_version(void) { return PF_ABI_VERSION; }
+
+extern "C" int pf_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" const char *pf_strerror(int code) {
+    switch (code) {
+    case PF_OK: return "ok";
+    case PF_ERR_ARG: return "invalid argument";
+    case PF_ERR_HIP: return "HIP runtime error";
+    case PF_ERR_NOMEM: return "out of memory";
+    case PF_ERR_UNSUPPORTED: return "unsupported configuration";
+    case PF_ERR_LIMIT: return "input exceeds a documented limit";
+    case PF_ERR_INTERNAL: return "internal error";
+    }
+    return "unknown";
+}
+
+extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
+    if (!out) return PF_ERR_ARG;
+    *out = nullptr;
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(device));
+    pf_ctx *c = new pf_ctx();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int i = 0; i <= PF_NKERN; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    c->have_times = 0;
+    *out = c;
+    return PF_OK;
+}
+
+extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+template <typename T>
+static int dev_alloc(pf_dbatch *b, T **p, size_t n) {
+    void *q = nullptr;
+    size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    if (hipMalloc(&q, bytes) != hipSuccess) return PF_ERR_NOMEM;
+    b->allocs.push_back(q);
+    *p = static_cast<T *>(q);
+    return PF_OK;
+}
+
+template <typename T>
+static int dev_put(pf_dbatch *b, T **p, const T *src, size_t n) {
+    int rc = dev_alloc(b, p, n);
+    if (rc) return rc;
+    if (n) HIPCHK(hipMemcpy(*p, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return PF_OK;
+}
+
+static void free_arena(pf_dbatch *b, void *p) {
+    for (size_t i = 0; i < b->allocs.size(); i++)
+        if (b->allocs[i] == p) { (void)hipFree(p); b->allocs.erase(b->allocs.begin() + i); return; }
+}
+
+extern "C" void pf_batch_free(pf_dbatch_t *b) {
+    if (!b) return;
+    (void)hipSetDevice(b->ctx->device);
+    (void)hipStreamSynchronize(b->ctx->stream);
+    for (void *p : b->allocs) (void)hipFree(p);
+    (void)hipHostFree(b->h_table);
+    (void)hipHostFree(b->h_S);
+    (void)hipHostFree(b->h_nreads);
+    (void)hipHostFree(b->h_status);
+    (void)hipHostFree(b->h_hp_fwd);
+    (void)hipHostFree(b->h_ctr);
+    delete b;
+}
+
+extern "C" uint32_t pf_batch_n_windows(const pf_dbatch_t *b) { return b ? b->W : 0; }
+extern "C" uint32_t pf_batch_n_reads(const pf_dbatch_t *b) { return b ? b->R : 0; }
+
+static int mask_words(int k) { int bits = 2 * k; return bits <= 6 ? 1 : 1 << (bits - 6); }
+
+extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_window_batch_t *in,
+                               pf_dbatch_t **out) {
+    if (!ctx || !cfg || !in || !out) return PF_ERR_ARG;
+    *out = nullptr;
+    if (cfg->k < 1 || cfg->k_span < 0) return PF_ERR_ARG;
+    if (cfg->k > 5) return PF_ERR_UNSUPPORTED;     // slot dictionary: 4^k keys per site
+    const uint32_t W = in->n_windows, R = in->n_reads;
+    const uint64_t N = in->n_calls;
+    if (W && (!in->win_start || !in->win_end || !in->win_read_off)) return PF_ERR_ARG;
+    if (R && (!in->read_start || !in->read_end || !in->read_hp || !in->read_call_off)) return PF_ERR_ARG;
+    if (N && (!in->call_pos || !in->call_cat)) return PF_ERR_ARG;
+    if (W && (in->win_read_off[0] != 0 || in->win_read_off[W] != R)) return PF_ERR_ARG;
+    if (R && (in->read_call_off[0] != 0 || in->read_call_off[R] != N)) return PF_ERR_ARG;
+    if (!W && R) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+
+    pf_dbatch *b = new pf_dbatch();
+    b->ctx = ctx;
+    b->cfg = *cfg;
+    b->W = W; b->R = R; b->N = N;
+    b->h_win_read_off.assign(in->win_read_off, in->win_read_off + (W ? W + 1 : 0));
+    b->h_read_hp.assign(in->read_hp, in->read_hp + R);
+    b->launched = 0;
+    auto fail = [&](int rc) { pf_batch_free(b); return rc; };
+
+    // ---- per-window parameters (with the clamps of blockjoin.c:4381-4390)
+    std::vector<int32_t> par(4ull * W);
+    std::vector<uint32_t> read_win(R);
+    std::vector<uint32_t> site_cap(W);
+    std::vector<uint64_t> site_off(W);
+    uint64_t site_total = 0;
+    for (uint32_t w = 0; w < W; w++) {
+        const uint32_t r0 = in->win_read_off[w], r1 = in->win_read_off[w + 1];
+        if (r1 < r0) return fail(PF_ERR_ARG);
+        if (r1 - r0 > 65535) return fail(PF_ERR_LIMIT);  // 16-bit per-haplotype counters
+        int sel = in->win_cov_sel ? in->win_cov_sel[w] : cfg->cov_for_selection;
+        int rt = in->win_cov_rt ? in->win_cov_rt[w] : cfg->cov_for_runtime;
+        int nc = in->win_n_cand ? in->win_n_cand[w] : cfg->n_cand;
+        if (sel <= 0) sel = 1;
+        if (nc <= 1) nc = 2;
+        if (nc > PF_MAX_NCAND) return fail(PF_ERR_LIMIT);
+        par[4 * w] = sel; par[4 * w + 1] = rt; par[4 * w + 2] = nc; par[4 * w + 3] = 0;
+        for (uint32_t r = r0; r < r1; r++) read_win[r] = w;
+        const uint64_t calls = in->read_call_off[r1] - in->read_call_off[r0];
+        // a site needs >= sel meth and >= sel unmeth calls
+        const uint64_t cap = calls / (2ull * (uint64_t)sel) + 1;
+        site_cap[w] = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
+        site_off[w] = site_total;
+        site_total += site_cap[w];
+    }
+    b->site_total = site_total;
+
+    // ---- reads: first/last call in the caller's order, calls sorted by (pos, cat)
+    std::vector<uint32_t> first(R), last(R);
+    const uint32_t *cpos = in->call_pos;
+    const uint8_t *ccat = in->call_cat;
+    std::vector<uint32_t> spos;
+    std::vector<uint8_t> scat;
+    bool need_sort = false;
+    for (uint32_t r = 0; r < R; r++) {
+        const uint64_t c0 = in->read_call_off[r], c1 = in->read_call_off[r + 1];
+        if (c1 < c0) return fail(PF_ERR_ARG);
+        first[r] = c1 > c0 ? cpos[c0] : 0;
+        last[r] = c1 > c0 ? cpos[c1 - 1] : 0;
+        for (uint64_t c = c0; c < c1; c++) {
+            if (cpos[c] >= (1u << 29)) return fail(PF_ERR_LIMIT);  // pos<<3 packing (blockjoin.c:3398)
+            if (ccat[c] > 2) return fail(PF_ERR_ARG);
+            if (c > c0 && (cpos[c] < cpos[c - 1] || (cpos[c] == cpos[c - 1] && ccat[c] < ccat[c - 1])))
+                need_sort = true;
+        }
+    }
+    if (need_sort) {
+        spos.assign(cpos, cpos + N);
+        scat.assign(ccat, ccat + N);
+        std::vector<uint64_t> tmp;
+        for (uint32_t r = 0; r < R; r++) {
+            const uint64_t c0 = in->read_call_off[r], c1 = in->read_call_off[r + 1];
+            tmp.resize(c1 - c0);
+            for (uint64_t c = c0; c < c1; c++) tmp[c - c0] = ((uint64_t)cpos[c] << 8) | ccat[c];
+            std::sort(tmp.begin(), tmp.end());
+            for (uint64_t c = c0; c < c1; c++) {
+                spos[c] = (uint32_t)(tmp[c - c0] >> 8);
+                scat[c] = (uint8_t)(tmp[c - c0] & 0xff);
+            }
+        }
+        cpos = spos.data();
+        ccat = scat.data();
+    }
+
+    pf_dev_batch &d = b->d;
+    memset(&d, 0, sizeof(d));
+    d.W = W; d.R = R; d.N = N;
+    d.k = cfg->k; d.k_span = cfg->k_span;
+    d.hard_cov = cfg->hard_cov > 0 ? cfg->hard_cov : 15;
+    d.mw = mask_words(cfg->k);
+    int rc = 0;
+#define PUT(field, src, n) do { rc = dev_put(b, &field, src, n); if (rc) return fail(rc); } while (0)
+#define ALLOC(field, n) do { rc = dev_alloc(b, &field, n); if (rc) return fail(rc); } while (0)
+    {
+        uint32_t *p; PUT(p, in->win_start, W); d.win_start = p;
+        PUT(p, in->win_end, W); d.win_end = p;
+        PUT(p, in->win_read_off, W + 1); d.win_read_off = p;
+        int32_t *ip; PUT(ip, par.data(), par.size()); d.win_par = ip;
+        uint64_t *up; PUT(up, site_off.data(), W); d.win_site_off = up;
+        PUT(p, site_cap.data(), W); d.win_site_cap = p;
+        PUT(p, in->read_start, R); d.read_start = p;
+        PUT(p, in->read_end, R); d.read_end = p;
+        PUT(p, first.data(), R); d.read_first = p;
+        PUT(p, last.data(), R); d.read_last = p;
+        PUT(p, read_win.data(), R); d.read_win = p;
+        uint8_t *bp; PUT(bp, in->read_hp, R); d.read_hp = bp;
+        PUT(up, in->read_call_off, R + 1); d.read_call_off = up;
+        PUT(p, cpos, N); d.call_pos = p;
+        PUT(bp, ccat, N); d.call_cat = bp;
+    }
+    ALLOC(d.call_site, N);
+    ALLOC(d.win_S, W);
+    ALLOC(d.win_nreads, W);
+    ALLOC(d.site_pos, site_total);
+    ALLOC(d.st1_pos, site_total);
+    ALLOC(d.site_q1, site_total);
+    ALLOC(d.len0, site_total);
+    ALLOC(d.len1, site_total);
+    ALLOC(d.rev_ord, R);
+    ALLOC(d.mmr_n, 2ull * R);
+    ALLOC(d.mmr_start, 2ull * R);
+    ALLOC(d.mmr_off, 2ull * R);
+    ALLOC(d.mmr_cap, R);
+    ALLOC(d.big_off, R);
+    // arenas: initial sizes; overflow is detected on device and the run repeated
+    d.keys_cap = N + (uint64_t)R * (6ull * cfg->k + 8) + 1024;
+    ALLOC(d.keys, d.keys_cap);
+    d.big_cap = 16ull << 20;
+    ALLOC(d.big, d.big_cap);
+    d.scr_cap = 64ull << 20;
+    ALLOC(d.scr, d.scr_cap);
+    {
+        unsigned long long *cp; ALLOC(cp, 3); d.keys_ctr = cp; d.big_ctr = cp + 1; d.scr_ctr = cp + 2;
+    }
+    ALLOC(d.status, 4);
+    ALLOC(d.table, 8ull * W);
+    ALLOC(d.hp_fwd, R);
+    const char *lds = getenv("PF_K3_LDS");
+    d.lds_bytes = lds ? (uint32_t)atoi(lds) : 65536u;
+    if (hipHostMalloc((void **)&b->h_table, std::max<size_t>(8ull * W, 1) * 4) != hipSuccess ||
+        hipHostMalloc((void **)&b->h_S, std::max<size_t>(W, 1) * 4) != hipSuccess ||
+        hipHostMalloc((void **)&b->h_nreads, std::max<size_t>(W, 1) * 4) != hipSuccess ||
+        hipHostMalloc((void **)&b->h_status, 16) != hipSuccess ||
+        hipHostMalloc((void **)&b->h_hp_fwd, std::max<size_t>(R, 1)) != hipSuccess ||
+        hipHostMalloc((void **)&b->h_ctr, 3 * 8) != hipSuccess)
+        return fail(PF_ERR_NOMEM);
+    *out = b;
+    return PF_OK;
+#undef PUT
+#undef ALLOC
+}
+
+static int launch_all(pf_dbatch *b) {
+    pf_ctx *c = b->ctx;
+    pf_dev_batch &d = b->d;
+    hipStream_t st = c->stream;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(d.keys_ctr, 0, 3 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(d.status, 0, 4 * sizeof(uint32_t), st));
+    if (b->W == 0) { b->launched = 1; return PF_OK; }
+    static int attr_done = 0;
+    if (!attr_done) {
+        hipError_t e = hipFuncSetAttribute((const void *)pf_k3_greedy,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes);
+        if (e != hipSuccess) {
+            fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u B dynamic LDS): %s\n", d.lds_bytes,
+                    hipGetErrorString(e));
+            (void)hipGetLastError();
+        }
+        attr_done = 1;
+    }
+    (void)hipGetLastError();
+    HIPCHK(hipEventRecord(c->ev[0], st));
+    hipLaunchKernelGGL(pf_k1_sites, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], st));
+    const uint64_t waves = 2ull * b->R;
+    const uint32_t g2 = (uint32_t)((waves + PF_K2_WAVES - 1) / PF_K2_WAVES);
+    if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], st));
+    hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[3], st));
+    HIPCHK(hipMemcpyAsync(b->h_table, d.table, 8ull * b->W * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->h_S, d.win_S, 4ull * b->W, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->h_nreads, d.win_nreads, 4ull * b->W, hipMemcpyDeviceToHost, st));
+    if (b->R) HIPCHK(hipMemcpyAsync(b->h_hp_fwd, d.hp_fwd, b->R, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->h_status, d.status, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->h_ctr, d.keys_ctr, 24, hipMemcpyDeviceToHost, st));
+    b->launched = 1;
+    return PF_OK;
+}
+
+extern "C" int pf_methphase_launch(pf_ctx_t *ctx, pf_dbatch_t *b) {
+    if (!ctx || !b || b->ctx != ctx) return PF_ERR_ARG;
+    return launch_all(b);
+}
+
+static int grow(pf_dbatch *b, uint8_t **buf, uint64_t *cap, uint64_t need) {
+    free_arena(b, *buf);
+    uint64_t ncap = std::max<uint64_t>(need + need / 4 + 1024, *cap * 2);
+    void *q = nullptr;
+    if (hipMalloc(&q, ncap) != hipSuccess) return PF_ERR_NOMEM;
+    b->allocs.push_back(q);
+    *buf = (uint8_t *)q;
+    *cap = ncap;
+    return PF_OK;
+}
+
+extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_t *out) {
+    if (!ctx || !b || !out || b->ctx != ctx || !b->launched) return PF_ERR_ARG;
+    pf_ctx *c = ctx;
+    for (int attempt = 0;; attempt++) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        b->launched = 0;
+        if (b->W) {
+            for (int i = 0; i < PF_NKERN; i++) (void)hipEventElapsedTime(&c->last_ms[i], c->ev[i], c->ev[i + 1]);
+            c->have_times = 1;
+        }
+        const uint32_t stt = b->W ? b->h_status[0] : 0;
+        if (stt == 0) break;
+        if (attempt >= 3 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF))) {
+            fprintf(stderr, "[E::pomfret_amd] device status 0x%x\n", stt);
+            return PF_ERR_INTERNAL;
+        }
+        pf_dev_batch &d = b->d;
+        int rc = 0;
+        if (stt & PF_ST_KEYS_OVF) {
+            uint8_t *p = (uint8_t *)d.keys;
+            uint64_t capb = d.keys_cap * 4;
+            rc = grow(b, &p, &capb, b->h_ctr[0] * 4);
+            d.keys = (uint32_t *)p; d.keys_cap = capb / 4;
+        }
+        if (!rc && (stt & PF_ST_BIG_OVF)) rc = grow(b, &d.big, &d.big_cap, b->h_ctr[1]);
+        if (!rc && (stt & PF_ST_SCR_OVF)) rc = grow(b, &d.scr, &d.scr_cap, b->h_ctr[2]);
+        if (rc) return rc;
+        rc = launch_all(b);
+        if (rc) return rc;
+    }
+    if (out->win_n_reads)
+        for (uint32_t w = 0; w < b->W; w++) out->win_n_reads[w] = b->h_nreads[w];
+    pf_decide_windows(b->W, b->h_win_read_off.data(), b->h_S, b->h_table, b->h_read_hp.data(),
+                      b->h_hp_fwd, out);
+    return PF_OK;
+}
+
+extern "C" int pf_methphase_run(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_t *out) {
+    int rc = pf_methphase_launch(ctx, b);
+    if (rc) return rc;
+    return pf_methphase_finish(ctx, b, out);
+}
+
+extern "C" int pf_methphase_windows(int device, const pf_cfg_t *cfg, const pf_window_batch_t *batch,
+                                    pf_window_out_t *out) {
+    pf_ctx_t *ctx = nullptr;
+    int rc = pf_ctx_create(device, &ctx);
+    if (rc) return rc;
+    pf_dbatch_t *b = nullptr;
+    rc = pf_batch_upload(ctx, cfg, batch, &b);
+    if (!rc) rc = pf_methphase_run(ctx, b, out);
+    pf_batch_free(b);
+    pf_ctx_destroy(ctx);
+    return rc;
+}
+
+extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n) {
+    if (!ctx || !n) return PF_ERR_ARG;
+    int m = *n < PF_NKERN ? *n : PF_NKERN;
+    for (int i = 0; i < m; i++) {
+        if (names) names[i] = k_names[i];
+        if (ms) ms[i] = ctx->have_times ? ctx->last_ms[i] : -1.0f;
+    }
+    *n = PF_NKERN;
+    return PF_OK;
+}

@@ -1,0 +1,73 @@
+/*
+ * pf_device.h -- device-side layout shared by the methphase kernels.
+ *
+ * HBM layout of one resident batch (all SoA, one allocation per array):
+ *   windows : win_start/win_end/win_read_off/win_par          [W]
+ *   reads   : read_start/end/first/last/win, read_hp           [R]
+ *             read_call_off                                     [R+1]
+ *   calls   : call_pos (u32), call_cat (u8), call_site (u32)    [N]
+ *             calls of a read sorted by (pos, cat)
+ *   sites   : per window a slice [site_off[w], +site_cap[w]) of
+ *             site_pos, st1_pos, site_q1 (u32) and len0, len1 (u8)
+ *   methmers: per (read, dir) a slice of the key arena (u32): methmer keys,
+ *             rewritten in place to per-site slot ids before the greedy loop
+ */
+#ifndef PF_DEVICE_H
+#define PF_DEVICE_H
+#include <stdint.h>
+
+#define PF_WAVE 64
+#define PF_K1_THREADS 1024
+#define PF_K1_TILE 32768          /* positions per dense LDS tile (128 KB of u32 counters) */
+#define PF_K2_WAVES 4
+#define PF_K2_ENT_CAP 1024        /* per-wave LDS entry buffer; larger reads use HBM scratch */
+#define PF_K3_THREADS 256
+#define PF_K3_WAVES (PF_K3_THREADS / PF_WAVE)
+#define PF_MAX_NCAND 256
+#define PF_NONE 0xFFFFFFFFu
+
+/* status bits */
+#define PF_ST_KEYS_OVF   1u
+#define PF_ST_BIG_OVF    2u
+#define PF_ST_SCR_OVF    4u
+#define PF_ST_SITE_OVF   8u
+#define PF_ST_INTERNAL  16u
+
+struct pf_dev_batch {
+    uint32_t W, R;
+    uint64_t N;
+    int32_t k, k_span, hard_cov, mw;   /* mw: 64-bit mask words per site = max(1, 4^k/64) */
+    /* windows */
+    const uint32_t *win_start, *win_end, *win_read_off;
+    const int32_t *win_par;            /* [W*4]: cov_sel, cov_rt, n_cand, 0 */
+    const uint64_t *win_site_off;
+    const uint32_t *win_site_cap;
+    /* reads */
+    const uint32_t *read_start, *read_end, *read_first, *read_last, *read_win;
+    const uint8_t *read_hp;
+    const uint64_t *read_call_off;
+    /* calls */
+    const uint32_t *call_pos;
+    const uint8_t *call_cat;
+    uint32_t *call_site;
+    /* per-window results of K1 */
+    uint32_t *win_S, *win_nreads;
+    uint32_t *site_pos, *st1_pos, *site_q1;
+    uint8_t *len0, *len1;
+    uint32_t *rev_ord;                 /* [R] window-local read index, ascending (end, idx) */
+    /* methmers */
+    uint32_t *mmr_n, *mmr_start;       /* [2R] */
+    uint64_t *mmr_off;                 /* [2R] */
+    uint32_t *mmr_cap;                 /* [R]  */
+    uint64_t *big_off;                 /* [R]  */
+    uint32_t *keys; uint64_t keys_cap; unsigned long long *keys_ctr;
+    uint8_t *big; uint64_t big_cap; unsigned long long *big_ctr;
+    uint8_t *scr; uint64_t scr_cap; unsigned long long *scr_ctr;
+    /* outputs */
+    int32_t *table;                    /* [W*2*4] */
+    uint8_t *hp_fwd;                   /* [R] */
+    uint32_t *status;
+    uint32_t lds_bytes;                /* dynamic LDS of the greedy kernel */
+};
+
+#endif
