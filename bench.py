@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X methphase hot path (BASELINE.json metric).
+
+One "step" = one pass of the hot path over one batch of windows that is already
+resident in HBM: K1 sites -> K2 methmers -> K3 greedy + 2x2 tables -> D2H ->
+host Fisher test and join decisions (pf_methphase_run).  Workload at N=1 is
+BASELINE.json configs[1] ("HG002 chr20 30x, pre-haplotagged, 1x MI355X"),
+synthesised (HG002 is not available offline): 256 chr20-like gap windows of
+50 kb at 30x, parameters as `pomfret methphase` derives them without -c
+(cov_for_selection 4, cov_for_runtime 8, n_cand 8; blockjoin.c:4373-4375).
+
+Multi-GPU (torchrun, one process per GPU): every rank owns its own shard of 256
+windows (weak scaling, no collective in the data path); after each step the
+int8 decisions are gathered to every rank over RCCL (the drop-in's only
+exchange: the host that writes VCF/GTF needs all decisions).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_HBM_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+WORKLOAD = dict(n_windows=256, coverage=30, gap=50_000)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algo_bytes(batch, stats, n_sites):
+    """Algorithmic bytes per launch of each kernel.
+
+    K1 sites   : 5 B per call read (u32 pos + u8 cat) + 9 B per site written
+    K2 methmer : per (read, dir): 5 B per call read, 4 B per site entry read
+                 (~ one per methmer) and 4 B per methmer key written
+    K3 greedy  : 12 B per methmer lookup (4 B key + 2x(2 B cnt + 2 B sum)),
+                 8 B per methmer inserted, 1 B per read visited by the scan,
+                 2 B per strict reference read in the 2x2 table
+    """
+    N = batch.n_calls
+    S = int(n_sites.sum())
+    lookups = int(stats[:, :, 0].sum())
+    inserts = int(stats[:, :, 1].sum())
+    scanned = int(stats[:, :, 3].sum())
+    mmr = int(stats[:, :, 4].sum())
+    strict = int(stats[:, :, 5].sum())
+    k1 = 5 * N + 9 * S
+    k2 = 2 * 5 * N + 8 * mmr          # calls read per direction + sites read / methmers written
+    k3 = 12 * lookups + 8 * inserts + scanned + 2 * strict
+    return {"pf_k1_sites": k1, "pf_k2_methmers": k2, "pf_k3_greedy": k3}
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    p = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("workload") != WORKLOAD:
+            return None
+        return d["kernels"].get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg, batch, reps: int, threads: int):
+    """The CPU oracle (plain-C restatement of the reference, oracle/) timed on
+    this host with `threads` pthreads over windows (kt_for analogue)."""
+    import oracle
+    oracle.methphase(cfg, batch.select(range(min(8, batch.n_windows))), n_threads=threads)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle.methphase(cfg, batch, n_threads=threads)
+    dt = time.perf_counter() - t0
+    return batch.n_reads * reps / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--windows", type=int, default=WORKLOAD["n_windows"])
+    ap.add_argument("--coverage", type=int, default=WORKLOAD["coverage"])
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group(backend="nccl")
+        dist = tdist
+
+    from pomfret_amd import Config, Context
+    from pomfret_amd.synth import SynthSpec, make_batch
+
+    wl = dict(WORKLOAD, n_windows=args.windows, coverage=args.coverage)
+    cfg = Config.from_coverage(wl["coverage"], given=False)
+    spec = SynthSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
+                     seed=1000 + rank)
+    t = time.perf_counter()
+    batch = make_batch(spec)
+    log(f"[bench] rank {rank}: generated {batch.n_windows} windows, {batch.n_reads} reads, "
+        f"{batch.n_calls} calls in {time.perf_counter() - t:.1f}s")
+
+    ctx = Context(local_rank)
+    db = ctx.upload(cfg, batch)
+    out = db.run()
+    for _ in range(args.warmup):
+        db.run(out)
+
+    if dist is not None:
+        import torch
+        dec_t = torch.empty(batch.n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
+        gathered = torch.empty(world * batch.n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
+
+    def step():
+        db.run(out)
+        if dist is not None:
+            dec_t.copy_(torch.from_numpy(out.decision))
+            dist.all_gather_into_tensor(gathered, dec_t)
+
+    if dist is not None:
+        dist.barrier()
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kern_acc = {}
+    for _ in range(args.steps):
+        step()
+        for k, v in ctx.kernel_times().items():
+            kern_acc[k] = kern_acc.get(k, 0.0) + v
+    if dist is not None:
+        torch.cuda.synchronize()
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        rt = torch.tensor([batch.n_reads], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(rt)
+        total_reads = float(rt.item()) * args.steps
+    else:
+        total_reads = float(batch.n_reads) * args.steps
+
+    value = total_reads / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    stats = db.stats()
+    kmean = {k: v / args.steps for k, v in kern_acc.items()}
+    ab = algo_bytes(batch, stats, out.win_n_sites)
+    kernels = {}
+    for k, ms in kmean.items():
+        b = ab.get(k, 0)
+        kernels[k] = {"ms": round(ms, 4), "algo_bytes": int(b),
+                      "GBps": round(b / (ms * 1e-3) / 1e9, 2) if ms > 0 else None}
+    dom = max(kmean, key=kmean.get)
+    achieved = kernels[dom]["GBps"]
+    traffic = pmc_traffic(dom)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        reps = 5
+        v_cpu, dt = cpu_baseline(cfg, batch, reps, threads)
+        cpu = {"value": round(v_cpu, 1), "unit": "reads/s", "cores": threads, "kind": "port",
+               "sample": f"the same {batch.n_windows}-window workload x{reps} "
+                         f"({batch.n_reads * reps} reads, {dt:.1f}s wall on {threads} threads), "
+                         f"oracle/pf_oracle.c"}
+
+    res = {
+        "metric": "aligned reads/sec (methphase kernel)",
+        "value": round(value, 1),
+        "unit": "reads/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32/f32",
+        "data": "synthetic (seeded chr20-like 30x pileups; HG002 not available offline)",
+        "config": {
+            "workload": f"chr20-like {wl['coverage']}x: {wl['n_windows']} gap windows x "
+                        f"{wl['gap'] // 1000} kb per GPU, pre-haplotagged (BASELINE configs[1])",
+            "windows_per_gpu": wl["n_windows"], "reads_per_gpu": batch.n_reads,
+            "calls_per_gpu": batch.n_calls, "coverage": wl["coverage"],
+            "cov_for_selection": cfg.cov_for_selection, "cov_for_runtime": cfg.cov_for_runtime,
+            "n_cand": cfg.n_cand, "k": cfg.k, "k_span": cfg.k_span,
+            "parallelism": f"windows sharded, dp{world}",
+        },
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 5) if achieved else None,
+                     "traffic": traffic},
+        "kernels": kernels,
+        "cpu_baseline": cpu,
+        "decisions": {"cis": int((out.decision == 0).sum()), "trans": int((out.decision == 1).sum()),
+                      "none": int((out.decision < 0).sum())},
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    db.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

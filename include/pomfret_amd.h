@@ -186,6 +186,24 @@ int  pf_methphase_windows(int device, const pf_cfg_t *cfg,
  * events on the library's stream.  names/ms arrays of length *n. */
 int  pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n);
 
+/* Per-(window,direction) counters of the last run, out[(w*2+dir)*8 + j]:
+ * j=0 methmer lookups (in-range methmers of every scored candidate),
+ * j=1 methmer insertions (reference reads + tagged reads), j=2 greedy
+ * iterations that scored >= 1 candidate, j=3 reads visited by the candidate
+ * scans, j=4 methmers of all reads, j=5 strict reference reads in the 2x2
+ * table, j=6 reads, j=7 sites.  n >= 16*n_windows.  These feed the
+ * algorithmic-byte model of DESIGN.md. */
+int  pf_batch_stats(pf_dbatch_t *db, uint64_t *out, uint64_t n);
+
+/* Parity/debug: run K1 only and copy window w's sites (ms->sites_real_poss,
+ * sites_starts, mmr_lens of direction dir); returns S or <0. */
+int  pf_batch_debug_sites(pf_dbatch_t *db, uint32_t w, int dir, uint32_t *real,
+                          uint32_t *starts, uint8_t *lens, uint32_t cap);
+/* Parity/debug: run K1+K2 and copy every read's methmers of direction dir
+ * (read_t.mmr_n, mmr_start_i, mmr keys back to back); returns #keys or <0. */
+int64_t pf_batch_debug_methmers(pf_dbatch_t *db, int dir, uint32_t *mmr_n,
+                                uint32_t *mmr_start, uint32_t *keys, uint64_t cap);
+
 /* -u pre-pass: hp_out[r] in {0, 1, 254} for every read of one contig. */
 int  pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *known,
                      const pf_read_aln_batch_t *reads, uint8_t *hp_out);

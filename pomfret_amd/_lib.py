@@ -50,6 +50,12 @@ def lib():
                                            C.POINTER(PfWindowOut)]
         L.pf_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p),
                                            C.POINTER(C.c_float), C.POINTER(C.c_int)]
+        L.pf_batch_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.pf_batch_debug_sites.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_uint32]
+        L.pf_batch_debug_methmers.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_uint64]
+        L.pf_batch_debug_methmers.restype = C.c_int64
         L.pf_fisher_exact.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_double)] * 3
         L.pf_fisher_exact.restype = C.c_double
         if hasattr(L, "pf_haptag_reads"):
@@ -142,6 +148,32 @@ class DeviceBatch:
         o = out.to_c()
         _check(lib().pf_methphase_run(self.ctx.handle, self.handle, C.byref(o)), "pf_methphase_run")
         return out
+
+    def stats(self) -> np.ndarray:
+        """Per-(window, dir) counters of the last run: [W, 2, 8] (see pf_batch_stats)."""
+        out = np.zeros((max(self.n_windows, 1), 2, 8), np.uint64)
+        _check(lib().pf_batch_stats(self.handle, out.ctypes.data, out.size), "pf_batch_stats")
+        return out[:self.n_windows]
+
+    def debug_sites(self, w: int, direction: int, cap: int = 1 << 22):
+        real = np.zeros(cap, np.uint32)
+        starts = np.zeros(cap, np.uint32)
+        lens = np.zeros(cap, np.uint8)
+        n = lib().pf_batch_debug_sites(self.handle, w, direction, real.ctypes.data,
+                                       starts.ctypes.data, lens.ctypes.data, cap)
+        if n < 0:
+            _check(n, "pf_batch_debug_sites")
+        return real[:n], starts[:n], lens[:n]
+
+    def debug_methmers(self, direction: int, cap: int = 1 << 26):
+        n = np.zeros(max(self.n_reads, 1), np.uint32)
+        st = np.zeros(max(self.n_reads, 1), np.uint32)
+        keys = np.zeros(cap, np.uint32)
+        tot = lib().pf_batch_debug_methmers(self.handle, direction, n.ctypes.data, st.ctypes.data,
+                                            keys.ctypes.data, cap)
+        if tot < 0:
+            _check(int(tot), "pf_batch_debug_methmers")
+        return n[:self.n_reads], st[:self.n_reads], keys[:tot]
 
     def launch(self):
         _check(lib().pf_methphase_launch(self.ctx.handle, self.handle), "pf_methphase_launch")

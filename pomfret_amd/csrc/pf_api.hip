@@ -95,6 +95,9 @@ extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
     return PF_OK;
 }
 
+extern "C" int pf_ctx_device(const pf_ctx *c) { return c->device; }
+extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c) { return c->stream; }
+
 extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -288,6 +291,8 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     ALLOC(d.status, 4);
     ALLOC(d.table, 8ull * W);
     ALLOC(d.hp_fwd, R);
+    ALLOC(d.stats, 16ull * W);
+    ALLOC(d.prof, 16ull * W);
     const char *lds = getenv("PF_K3_LDS");
     d.lds_bytes = lds ? (uint32_t)atoi(lds) : 65536u;
     if (hipHostMalloc((void **)&b->h_table, std::max<size_t>(8ull * W, 1) * 4) != hipSuccess ||
@@ -303,7 +308,7 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
 #undef ALLOC
 }
 
-static int launch_all(pf_dbatch *b) {
+static int launch_all(pf_dbatch *b, int stages = 3) {
     pf_ctx *c = b->ctx;
     pf_dev_batch &d = b->d;
     hipStream_t st = c->stream;
@@ -327,11 +332,13 @@ static int launch_all(pf_dbatch *b) {
     hipLaunchKernelGGL(pf_k1_sites, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], st));
+    if (stages < 2) { b->launched = 1; return PF_OK; }
     const uint64_t waves = 2ull * b->R;
     const uint32_t g2 = (uint32_t)((waves + PF_K2_WAVES - 1) / PF_K2_WAVES);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], st));
+    if (stages < 3) { b->launched = 1; return PF_OK; }
     hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], st));
@@ -415,6 +422,74 @@ extern "C" int pf_methphase_windows(int device, const pf_cfg_t *cfg, const pf_wi
     pf_batch_free(b);
     pf_ctx_destroy(ctx);
     return rc;
+}
+
+// ---- debug / parity entry points: run the first kernels only and copy the
+// intermediates (sites of one window; methmers of every read) to the host.
+extern "C" int pf_batch_debug_sites(pf_dbatch_t *b, uint32_t w, int dir, uint32_t *real,
+                                    uint32_t *starts, uint8_t *lens, uint32_t cap) {
+    if (!b || w >= b->W || dir < 0 || dir > 1) return PF_ERR_ARG;
+    int rc = launch_all(b, 1);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    b->launched = 0;
+    uint32_t S = 0, off_cap[1];
+    (void)off_cap;
+    HIPCHK(hipMemcpy(&S, b->d.win_S + w, 4, hipMemcpyDeviceToHost));
+    uint64_t off = 0;
+    HIPCHK(hipMemcpy(&off, b->d.win_site_off + w, 8, hipMemcpyDeviceToHost));
+    if (S > cap) return PF_ERR_ARG;
+    if (S) {
+        HIPCHK(hipMemcpy(real, b->d.site_pos + off, 4ull * S, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(starts, (dir ? b->d.st1_pos : b->d.site_pos) + off, 4ull * S, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(lens, (dir ? b->d.len1 : b->d.len0) + off, S, hipMemcpyDeviceToHost));
+    }
+    return (int)S;
+}
+
+extern "C" int64_t pf_batch_debug_methmers(pf_dbatch_t *b, int dir, uint32_t *mmr_n, uint32_t *mmr_start,
+                                           uint32_t *keys, uint64_t cap) {
+    if (!b || dir < 0 || dir > 1) return PF_ERR_ARG;
+    int rc = launch_all(b, 2);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    b->launched = 0;
+    uint32_t st = 0;
+    HIPCHK(hipMemcpy(&st, b->d.status, 4, hipMemcpyDeviceToHost));
+    if (st) return PF_ERR_INTERNAL;
+    std::vector<uint32_t> n(2ull * b->R), s0(2ull * b->R);
+    std::vector<uint64_t> off(2ull * b->R);
+    if (b->R) {
+        HIPCHK(hipMemcpy(n.data(), b->d.mmr_n, 8ull * b->R, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(s0.data(), b->d.mmr_start, 8ull * b->R, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(off.data(), b->d.mmr_off, 16ull * b->R, hipMemcpyDeviceToHost));
+    }
+    uint64_t tot = 0;
+    for (uint32_t r = 0; r < b->R; r++) {
+        const uint64_t g = 2ull * r + dir;
+        mmr_n[r] = n[g];
+        mmr_start[r] = s0[g];
+        if (tot + n[g] > cap) return PF_ERR_ARG;
+        if (n[g]) HIPCHK(hipMemcpy(keys + tot, b->d.keys + off[g], 4ull * n[g], hipMemcpyDeviceToHost));
+        tot += n[g];
+    }
+    return (int64_t)tot;
+}
+
+extern "C" int pf_batch_stats(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
+    if (!b || !out || n < 16ull * b->W) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    if (b->W) HIPCHK(hipMemcpy(out, b->d.stats, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return PF_OK;
+}
+
+extern "C" int pf_batch_prof(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
+    if (!b || !out || n < 16ull * b->W) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    if (b->W) HIPCHK(hipMemcpy(out, b->d.prof, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return PF_OK;
 }
 
 extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n) {

@@ -66,7 +66,9 @@ struct pf_dev_batch {
     /* outputs */
     int32_t *table;                    /* [W*2*4] */
     uint8_t *hp_fwd;                   /* [R] */
+    unsigned long long *stats;         /* [W*2*4] per problem: lookups, inserts, iterations, scanned */
     uint32_t *status;
+    unsigned long long *prof;          /* [W*2*8] diagnostic build only */
     uint32_t lds_bytes;                /* dynamic LDS of the greedy kernel */
 };
 

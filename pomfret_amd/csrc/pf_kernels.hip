@@ -36,6 +36,15 @@
 
 #define DEV static __device__ __forceinline__
 
+// Diagnostic build only (-DPF_K3_PROFILE): per-phase s_memtime cycle shares of
+// the greedy loop, written to d.prof.  The real kernel executes no stamp.
+#ifdef PF_K3_PROFILE
+#define K3_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
+#else
+#define K3_STAMP(i) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------------
 // small helpers
 DEV uint64_t lanemask_lt(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -122,6 +131,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
     __shared__ uint32_t tile[PF_K1_TILE];
     __shared__ uint32_t sh_scan[PF_K1_THREADS / 64 + 1];
     __shared__ uint32_t sh_misc[8];
+    __shared__ uint32_t sh_tbase[PF_K1_THREADS];
     __shared__ unsigned long long sh_base[2];
     constexpr uint32_t NT = PF_K1_THREADS, NW = NT / 64;
     const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -159,8 +169,110 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
     if (tid == 0) { sh_misc[4] = 0; d.win_nreads[w] = R; }
     __syncthreads();
 
-    // ---- dense per-position counts, tile by tile, in position order
-    for (uint64_t base = pmin; base <= pmax; base += PF_K1_TILE) {
+    // ---- fast path: LDS hash of call positions (meth/unmeth only) + a bitmap of
+    // qualifying positions over [pmin, pmin + 64*BW): a site's index (its rank in
+    // position order) is a prefix popcount, so no sort is needed.
+    constexpr uint32_t HN = 8192, HMAX = 6144, BW = 8192;
+    uint32_t *hkeys = tile, *hcnt = tile + HN;
+    uint64_t *bmap = reinterpret_cast<uint64_t *>(tile + 2 * HN);
+    bool hash_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64;
+    if (hash_ok) {
+        for (uint32_t j = tid; j < HN; j += NT) { hkeys[j] = PF_NONE; hcnt[j] = 0; }
+        for (uint32_t j = tid; j < BW; j += NT) bmap[j] = 0;
+        if (tid == 0) { sh_misc[5] = 0; sh_misc[6] = 0; }
+        __syncthreads();
+        for (uint32_t i = wid; i < R; i += NW) {
+            const uint32_t r = r0 + i;
+            const uint64_t c0 = d.read_call_off[r], c1 = d.read_call_off[r + 1];
+            for (uint64_t c = c0 + lane; c < c1; c += 64) {
+                const uint32_t cat = d.call_cat[c];
+                if (cat >= 2) continue;
+                const uint32_t pos = d.call_pos[c];
+                const uint32_t inc = cat == 0 ? 1u : 0x10000u;
+                uint32_t h = (pos * 2654435761u) >> 19;
+                for (;;) {
+                    const uint32_t k = __hip_atomic_load(&hkeys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (k == pos) { atomicAdd(&hcnt[h], inc); break; }
+                    if (k == PF_NONE) {
+                        // reserve before inserting: at most HMAX keys ever enter the
+                        // table, so probing always terminates
+                        if (atomicAdd(&sh_misc[5], 1u) >= HMAX) { sh_misc[6] = 1; break; }
+                        const uint32_t old = atomicCAS(&hkeys[h], PF_NONE, pos);
+                        if (old == PF_NONE || old == pos) { atomicAdd(&hcnt[h], inc); break; }
+                    }
+                    h = (h + 1) & (HN - 1);
+                }
+            }
+        }
+        __syncthreads();
+        hash_ok = sh_misc[6] == 0;
+    }
+    if (hash_ok) {
+        for (uint32_t j = tid; j < HN; j += NT) {
+            const uint32_t k = hkeys[j];
+            if (k == PF_NONE) continue;
+            const uint32_t v = hcnt[j];
+            if ((int)(v & 4095u) >= cov && (int)((v >> 16) & 4095u) >= cov) {
+                const uint32_t o = k - pmin;
+                atomicOr((unsigned long long *)&bmap[o >> 6], 1ull << (o & 63));
+            } else hcnt[j] = PF_NONE;
+        }
+        __syncthreads();
+        uint32_t mycount = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < BW / NT; j++) mycount += (uint32_t)__popcll(bmap[tid * (BW / NT) + j]);
+        uint32_t total;
+        const uint32_t excl = block_excl_scan<NT>(mycount, sh_scan, &total);
+        sh_tbase[tid] = excl;
+        {
+            uint32_t rank = excl;
+            for (uint32_t j = 0; j < BW / NT; j++) {
+                const uint32_t wi = tid * (BW / NT) + j;
+                uint64_t bits = bmap[wi];
+                while (bits) {
+                    const uint32_t b = __ffsll((unsigned long long)bits) - 1;
+                    bits &= bits - 1;
+                    if (rank < scap) d.site_pos[sb + rank] = pmin + wi * 64 + b;
+                    else atomicOr(d.status, PF_ST_SITE_OVF);
+                    rank++;
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < HN; j += NT) {
+            const uint32_t k = hkeys[j];
+            if (k == PF_NONE || hcnt[j] == PF_NONE) continue;
+            const uint32_t o = k - pmin, wi = o >> 6, t = wi / (BW / NT);
+            uint32_t rk = sh_tbase[t];
+            for (uint32_t q = t * (BW / NT); q < wi; q++) rk += (uint32_t)__popcll(bmap[q]);
+            rk += (uint32_t)__popcll(bmap[wi] & ((1ull << (o & 63)) - 1ull));
+            hcnt[j] = rk;
+        }
+        __syncthreads();
+        for (uint32_t i = wid; i < R; i += NW) {
+            const uint32_t r = r0 + i;
+            const uint64_t c0 = d.read_call_off[r], c1 = d.read_call_off[r + 1];
+            for (uint64_t c = c0 + lane; c < c1; c += 64) {
+                const uint32_t pos = d.call_pos[c];
+                const bool first = (c == c0) || d.call_pos[c - 1] != pos;
+                uint32_t v = PF_NONE;
+                if (first) {
+                    uint32_t h = (pos * 2654435761u) >> 19;
+                    for (;;) {
+                        const uint32_t k = hkeys[h];
+                        if (k == pos) { v = hcnt[h]; break; }
+                        if (k == PF_NONE) break;
+                        h = (h + 1) & (HN - 1);
+                    }
+                }
+                d.call_site[c] = v;
+            }
+        }
+        if (tid == 0) sh_misc[4] = total;
+        __syncthreads();
+    }
+    // ---- general path: dense per-position counts, tile by tile, in position order
+    for (uint64_t base = pmin; !hash_ok && base <= pmax; base += PF_K1_TILE) {
         const uint64_t top = base + PF_K1_TILE;
         for (uint32_t j = tid; j < PF_K1_TILE; j += NT) tile[j] = 0;
         __syncthreads();
@@ -484,7 +596,7 @@ __global__ __launch_bounds__(PF_K2_WAVES * 64) void pf_k2_methmers(pf_dev_batch 
 struct K3Ctl {
     uint32_t S, R, ntot, nc, L, done, failed, inserted, winner, tag;
     int32_t i_last;
-    uint32_t min_i, max_i, fail;
+    uint32_t min_i, max_i, fail, summ, nstrict;
     unsigned long long scr;
     unsigned long long wbest[PF_K3_WAVES];
     int32_t tab[4];
@@ -557,7 +669,7 @@ DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uin
 }
 
 struct K3Mem {
-    uint32_t *sum, *cnt, *aux, *ord;
+    uint32_t *sum, *cnt, *aux, *ord, *mn, *mst, *mo;
     uint8_t *hp, *flg;
     uint64_t *untag;
     float2 *recv;
@@ -565,21 +677,25 @@ struct K3Mem {
     uint32_t rc;        // record capacity (multiple of ncp)
 };
 
-// P2 byte layout for given sizes; returns total bytes needed for rc records
-DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint64_t off[8]) {
+#define K3_NOFF 11
+// P2 byte layout for given sizes; returns the bytes needed before the records
+DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint64_t off[K3_NOFF]) {
     const uint32_t nwords = (R + 63) >> 6;
-    off[0] = 0;                                  // sum   S*4
-    off[1] = align16(off[0] + 4ull * S);         // cnt   ntot*4
-    off[2] = align16(off[1] + 4ull * ntot);      // hp    R
-    off[3] = align16(off[2] + R);                // flg   R
-    off[4] = align16(off[3] + R);                // aux   R*4
-    off[5] = align16(off[4] + 4ull * R);         // ord   R*4 (dir 1)
+    off[0] = 0;                                        // sum   S*4
+    off[1] = align16(off[0] + 4ull * S);               // cnt   ntot*4
+    off[2] = align16(off[1] + 4ull * ntot);            // hp    R
+    off[3] = align16(off[2] + R);                      // flg   R
+    off[4] = align16(off[3] + R);                      // aux   R*4
+    off[5] = align16(off[4] + 4ull * R);               // ord   R*4 (dir 1)
     off[6] = align16(off[5] + (dir ? 4ull * R : 0));   // untag nwords*8
-    off[7] = align16(off[6] + 8ull * nwords);    // records
-    return off[7];
+    off[7] = align16(off[6] + 8ull * nwords);          // mn    R*4  methmers per read
+    off[8] = align16(off[7] + 4ull * R);               // mst   R*4  first site index
+    off[9] = align16(off[8] + 4ull * R);               // mo    R*4  key offset (window-relative)
+    off[10] = align16(off[9] + 4ull * R);              // records
+    return off[10];
 }
 
-DEV void k3_mem(uint8_t *base, const uint64_t off[8], uint32_t rc, K3Mem &m) {
+DEV void k3_mem(uint8_t *base, const uint64_t off[K3_NOFF], uint32_t rc, K3Mem &m) {
     m.sum = reinterpret_cast<uint32_t *>(base + off[0]);
     m.cnt = reinterpret_cast<uint32_t *>(base + off[1]);
     m.hp = base + off[2];
@@ -587,8 +703,11 @@ DEV void k3_mem(uint8_t *base, const uint64_t off[8], uint32_t rc, K3Mem &m) {
     m.aux = reinterpret_cast<uint32_t *>(base + off[4]);
     m.ord = reinterpret_cast<uint32_t *>(base + off[5]);
     m.untag = reinterpret_cast<uint64_t *>(base + off[6]);
-    m.recv = reinterpret_cast<float2 *>(base + off[7]);
-    m.recc = reinterpret_cast<uint32_t *>(base + off[7] + 8ull * rc);
+    m.mn = reinterpret_cast<uint32_t *>(base + off[7]);
+    m.mst = reinterpret_cast<uint32_t *>(base + off[8]);
+    m.mo = reinterpret_cast<uint32_t *>(base + off[9]);
+    m.recv = reinterpret_cast<float2 *>(base + off[10]);
+    m.recc = reinterpret_cast<uint32_t *>(base + off[10] + 8ull * rc);
     m.rc = rc;
 }
 
@@ -600,7 +719,7 @@ DEV void k3_mem(uint8_t *base, const uint64_t off[8], uint32_t rc, K3Mem &m) {
 // update_available_methmer_range (blockjoin.c:3669-3691), one wavefront
 DEV void k3_range_update(const uint32_t *sum, uint32_t S, int cov_rt, K3Ctl &ctl, uint32_t lane) {
     // left: extend down from (int)min_i while covered
-    int m0 = (int)ctl.min_i;
+    const int m0 = (int)ctl.min_i;
     if (m0 >= 0) {
         int count = 0;
         for (;;) {
@@ -635,6 +754,109 @@ DEV void k3_range_update(const uint32_t *sum, uint32_t S, int cov_rt, K3Ctl &ctl
         }
         if (count > 0 && lane == 0) ctl.max_i = (uint32_t)(M0 + count - 1);
     }
+    wave_sync();
+}
+
+// per-problem counters for the algorithmic-byte model (B_tag)
+struct K3Stats {
+    unsigned long long lookups, inserts, iters, scanned;
+};
+#define PF_NSTAT 8
+
+// step 1 of an iteration (wave 0 only): collect up to NC untagged reads in scan
+// order from i_last (:4037-4045); empty batches advance i_last (:4046-4051).
+DEV void k3_collect(const K3Mem &m, uint32_t R, uint32_t dir, uint32_t NC, uint32_t lane,
+                    K3Ctl &ctl, K3Cand &cd, K3Stats &stx) {
+    const uint32_t nwords = (R + 63) >> 6;
+    int il = ctl.i_last;
+    uint32_t failed = ctl.failed;
+    for (;;) {
+        const bool stop = dir == 0 ? il >= (int)R : il <= 0;
+        if (stop) {
+            if (lane == 0) { ctl.done = 1; ctl.i_last = il; ctl.failed = failed; }
+            wave_sync();
+            return;
+        }
+        uint32_t found = 0;
+        if (dir == 0) {
+            const uint32_t w0 = (uint32_t)il >> 6;
+            for (uint32_t wb = w0; wb < nwords && found < NC; wb += 64) {
+                const uint32_t wi = wb + lane;
+                uint64_t bits = wi < nwords ? m.untag[wi] : 0ull;
+                if (wi == w0) bits &= ~0ull << ((uint32_t)il & 63);
+                const uint32_t c = (uint32_t)__popcll(bits);
+                const uint32_t incl = wave_incl_scan(c, lane);
+                uint32_t rk = found + incl - c;
+                while (bits && rk < NC) {
+                    const uint32_t b = __ffsll((unsigned long long)bits) - 1;
+                    cd.pos[rk++] = wi * 64 + b;
+                    bits &= bits - 1;
+                }
+                found += __shfl(incl, 63, 64);
+            }
+        } else {
+            const int w0 = il >> 6;
+            for (int wb = w0; wb >= 0 && found < NC; wb -= 64) {
+                const int wi = wb - (int)lane;
+                uint64_t bits = wi >= 0 ? m.untag[wi] : 0ull;
+                if (wi == w0) {
+                    const uint32_t b = (uint32_t)il & 63;
+                    bits &= b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
+                }
+                const uint32_t c = (uint32_t)__popcll(bits);
+                const uint32_t incl = wave_incl_scan(c, lane);
+                uint32_t rk = found + incl - c;
+                while (bits && rk < NC) {
+                    const uint32_t b = 63 - __clzll((long long)bits);
+                    cd.pos[rk++] = (uint32_t)wi * 64 + b;
+                    bits &= ~(1ull << b);
+                }
+                found += __shfl(incl, 63, 64);
+            }
+        }
+        const uint32_t nc = found < NC ? found : NC;
+        wave_sync();
+        if (nc == 0) {
+            stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+            failed++;
+            if (failed > 10) {
+                if (lane == 0) { ctl.done = 1; ctl.i_last = il; ctl.failed = failed; }
+                wave_sync();
+                return;
+            }
+            il += dir == 0 ? (int)NC : -(int)NC;
+            continue;
+        }
+        if (found >= NC) {
+            const uint32_t pl = cd.pos[NC - 1];
+            stx.scanned += dir == 0 ? pl - (uint32_t)il + 1 : (uint32_t)il - pl + 1;
+        } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+        uint32_t lmax = 0, lsum = 0;
+        const uint32_t mn_ = ctl.min_i, mx_ = ctl.max_i;
+        for (uint32_t c = lane; c < nc; c += 64) {
+            const uint32_t p = cd.pos[c];
+            const uint32_t rd = dir ? m.ord[p] : p;
+            const uint32_t n = m.mn[rd], st = m.mst[rd];
+            // in-range methmers: site index in [min_i, max_i) (query_counts_of_mmrs, :3500-3501)
+            const uint64_t lo = st > mn_ ? st : mn_;
+            const uint64_t hi0 = (uint64_t)st + n;
+            const uint64_t hi = hi0 < mx_ ? hi0 : mx_;
+            const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0;
+            cd.read[c] = rd;
+            cd.site0[c] = (uint32_t)lo;
+            cd.len[c] = len;
+            cd.kofs[c] = (uint64_t)m.mo[rd] + (len ? (lo - st) : 0);
+            lmax = len > lmax ? len : lmax;
+            lsum += len;
+        }
+        lmax = wave_max_u32(lmax);
+        lsum = wave_incl_scan(lsum, lane);
+        stx.lookups += __shfl(lsum, 63, 64);
+        stx.iters++;
+        if (lane == 0) { ctl.done = 0; ctl.nc = nc; ctl.L = lmax; ctl.i_last = il; ctl.failed = failed; }
+        wave_sync();
+        return;
+    }
 }
 
 template <bool LDS2>
@@ -649,6 +871,14 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     const uint64_t sb = d.win_site_off[w];
     const uint32_t ncp = next_pow2(NC);
     const uint32_t lg = 31 - __clz(ncp);
+    const uint64_t kbase = d.mmr_off[2ull * r0];
+    const uint32_t *kb = d.keys + kbase;
+    K3Stats stx = {0, 0, 0, 0};
+    uint32_t sum_mmr = 0;
+#ifdef PF_K3_PROFILE
+    unsigned long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long prof_last = __builtin_amdgcn_s_memtime();
+#endif
 
     // ---- init tables and per-read state
     for (uint32_t j = tid; j < ntot; j += PF_K3_THREADS) m.cnt[j] = 0;
@@ -668,6 +898,11 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         m.hp[i] = d.read_hp[r];
         m.aux[i] = 0;
         if (dir) m.ord[i] = d.rev_ord[r];
+        const uint64_t g = 2ull * r + dir;
+        m.mn[i] = d.mmr_n[g];
+        sum_mmr += m.mn[i];
+        m.mst[i] = d.mmr_start[g];
+        m.mo[i] = (uint32_t)(d.mmr_off[g] - kbase);
     }
     if (tid == 0) {
         // haplotag_region1 step 1 (blockjoin.c:3976-4004)
@@ -682,17 +917,19 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         ctl.i_last = dir == 0 ? 0 : (int)R - 1;
         ctl.failed = 0;
         ctl.done = 0;
+        ctl.tab[0] = 0;
     }
     __syncthreads();
     // ---- reference reads seed the counts (insert_ref_reads_methmer_counts, :3776-3810)
     const uint32_t refbit = dir == 0 ? FLG_LEFT : FLG_RIGHT;
+    uint32_t ref_ins = 0;
     for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
         const uint32_t hp = m.hp[i];
         if (!(m.flg[i] & refbit) || hp > 1) continue;
-        const uint32_t g = 2 * (r0 + i) + dir;
-        const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
-        const uint32_t *kp = d.keys + d.mmr_off[g];
+        const uint32_t n = m.mn[i], st = m.mst[i];
+        const uint32_t *kp = kb + m.mo[i];
         const uint32_t inc = hp ? 0x10000u : 1u;
+        ref_ins += n;
         for (uint32_t t = lane; t < n; t += 64) {
             const uint32_t site = st + t;
             const uint32_t slot = kp[t];
@@ -702,6 +939,8 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             }
         }
     }
+    if (lane == 0 && ref_ins) atomicAdd((uint32_t *)&ctl.tab[0], ref_ins);
+    if (sum_mmr) atomicAdd(&ctl.summ, sum_mmr);
     __syncthreads();
     if (wid == 0) k3_range_update(m.sum, S, cov_rt, ctl, lane);
     // ---- step 1.5 (:4010-4025): all reads unphased, ref reads restored through
@@ -731,94 +970,23 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         const uint64_t b = __ballot(u);
         if (lane == 0) m.untag[j] = b;
     }
+    stx.inserts = ctl.tab[0];
     __syncthreads();
 
     // ---- step 2: greedy extension, one read per iteration (:4032-4071)
+    // Barriers per iteration: (a) candidates ready, (b) records ready, (c) keys
+    // ready.  Winner pick, insertion, range update and the next candidate scan
+    // run in wavefront 0 between (c) and the next (a).
+    K3_STAMP(0);
+    if (wid == 0) k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
+    K3_STAMP(1);
     for (;;) {
-        if (wid == 0) {
-            const int il = ctl.i_last;
-            const bool stop = dir == 0 ? il >= (int)R : il <= 0;
-            uint32_t found = 0;
-            if (!stop) {
-                if (dir == 0) {
-                    const uint32_t w0 = (uint32_t)il >> 6;
-                    for (uint32_t wb = w0; wb < nwords && found < NC; wb += 64) {
-                        const uint32_t wi = wb + lane;
-                        uint64_t bits = wi < nwords ? m.untag[wi] : 0ull;
-                        if (wi == w0) bits &= ~0ull << ((uint32_t)il & 63);
-                        const uint32_t c = (uint32_t)__popcll(bits);
-                        const uint32_t incl = wave_incl_scan(c, lane);
-                        uint32_t rk = found + incl - c;
-                        while (bits && rk < NC) {
-                            const uint32_t b = __ffsll((unsigned long long)bits) - 1;
-                            cd.pos[rk++] = wi * 64 + b;
-                            bits &= bits - 1;
-                        }
-                        found += __shfl(incl, 63, 64);
-                    }
-                } else {
-                    const int w0 = il >> 6;
-                    for (int wb = w0; wb >= 0 && found < NC; wb -= 64) {
-                        const int wi = wb - (int)lane;
-                        uint64_t bits = wi >= 0 ? m.untag[wi] : 0ull;
-                        if (wi == w0) {
-                            const uint32_t b = (uint32_t)il & 63;
-                            bits &= b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
-                        }
-                        const uint32_t c = (uint32_t)__popcll(bits);
-                        const uint32_t incl = wave_incl_scan(c, lane);
-                        uint32_t rk = found + incl - c;
-                        while (bits && rk < NC) {
-                            const uint32_t b = 63 - __clzll((long long)bits);
-                            cd.pos[rk++] = (uint32_t)wi * 64 + b;
-                            bits &= ~(1ull << b);
-                        }
-                        found += __shfl(incl, 63, 64);
-                    }
-                }
-            }
-            const uint32_t nc = found < NC ? found : NC;
-            wave_sync();
-            uint32_t lmax = 0;
-            for (uint32_t c = lane; c < nc; c += 64) {
-                const uint32_t p = cd.pos[c];
-                const uint32_t rd = dir ? m.ord[p] : p;
-                const uint32_t g = 2 * (r0 + rd) + dir;
-                const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
-                // in-range methmers: site in [min_i, max_i) (query_counts_of_mmrs, :3500-3501)
-                const uint64_t lo = st > ctl.min_i ? st : ctl.min_i;
-                const uint64_t hi0 = (uint64_t)st + n;
-                const uint64_t hi = hi0 < ctl.max_i ? hi0 : ctl.max_i;
-                const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0;
-                cd.read[c] = rd;
-                cd.site0[c] = (uint32_t)lo;
-                cd.len[c] = len;
-                cd.kofs[c] = d.mmr_off[g] + (len ? (lo - st) : 0);
-                lmax = len > lmax ? len : lmax;
-            }
-            lmax = wave_max_u32(lmax);
-            if (lane == 0) {
-                ctl.done = stop ? 1u : 0u;
-                ctl.nc = nc;
-                ctl.L = lmax;
-            }
-        }
-        __syncthreads();
+        __syncthreads();                                         // (a)
+        K3_STAMP(2);
         if (ctl.done) break;
         const uint32_t nc = ctl.nc;
-        if (nc == 0) {
-            if (tid == 0) {
-                ctl.failed++;
-                if (ctl.failed > 10) ctl.done = 1;
-                else ctl.i_last += dir == 0 ? (int)NC : -(int)NC;
-            }
-            __syncthreads();
-            if (ctl.done) break;
-            continue;
-        }
-        // ---- candidate scores: records in parallel, sums sequential per candidate
         const uint32_t L = ctl.L;
-        const uint32_t lc = m.rc >> lg;              // t-steps per record chunk
+        const uint32_t lc = m.rc >> lg;                           // t-steps per record chunk
         float s0 = 0.f, s1 = 0.f;
         uint32_t lcode = 0;
         for (uint32_t t0 = 0; t0 < L; t0 += lc) {
@@ -830,9 +998,9 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 uint32_t code = 0;
                 if (c < nc && t < cd.len[c]) {
                     const uint32_t site = cd.site0[c] + t;
-                    const uint32_t slot = d.keys[cd.kofs[c] + t];
+                    const uint32_t slot = kb[cd.kofs[c] + t];
                     const uint32_t cv = slot != PF_NONE ? m.cnt[slot] : 0u;
-                    if (cv != 0) {                           // key present at this site
+                    if (cv != 0) {                               // key present at this site
                         const uint32_t sv = m.sum[site];
                         const uint32_t h0 = sv & 0xffffu, h1 = sv >> 16;
                         if (h0) {
@@ -848,19 +1016,34 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 m.recv[idx] = make_float2(v0, v1);
                 m.recc[idx] = code;
             }
-            __syncthreads();
+            K3_STAMP(3);
+            __syncthreads();                                     // (b)
+            K3_STAMP(4);
             if (tid < nc) {
+                // sequential in methmer order; absent terms are +0.0f and leave the
+                // float sum unchanged
                 const uint32_t n = t1 - t0;
-                for (uint32_t t = 0; t < n; t++) {
-                    const float2 v = m.recv[(t << lg) + tid];
-                    s0 += v.x;                               // adding +0 for absent terms
-                    s1 += v.y;                               // leaves the float sum unchanged
-                    lcode += m.recc[(t << lg) + tid];
+                const float2 *rv = m.recv + tid;
+                const uint32_t *rcc = m.recc + tid;
+                uint32_t t = 0;
+                for (; t + 8 <= n; t += 8) {
+                    float2 v[8];
+                    uint32_t cc[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) { v[u] = rv[(t + u) << lg]; cc[u] = rcc[(t + u) << lg]; }
+#pragma unroll
+                    for (int u = 0; u < 8; u++) { s0 += v[u].x; s1 += v[u].y; lcode += cc[u]; }
+                }
+                for (; t < n; t++) {
+                    const float2 v = rv[t << lg];
+                    s0 += v.x;
+                    s1 += v.y;
+                    lcode += rcc[t << lg];
                 }
             }
-            __syncthreads();
+            if (t1 < L) __syncthreads();
         }
-        // use_mmr_count_predict_tag_for_one_read (:3637-3655) + best pick (:3744-3766)
+        // use_mmr_count_predict_tag_for_one_read (:3637-3655) + best pick (:3729-3766)
         unsigned long long key = 0;
         if (tid < nc) {
             const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
@@ -871,48 +1054,51 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         }
         key = wave_max_u64(key);
         if (lane == 0) ctl.wbest[wid] = key;
-        __syncthreads();
-        if (tid == 0) {
+        K3_STAMP(5);
+        __syncthreads();                                         // (c)
+        K3_STAMP(6);
+        if (wid == 0) {
             unsigned long long b = 0;
             for (int i = 0; i < PF_K3_WAVES; i++) b = ctl.wbest[i] > b ? ctl.wbest[i] : b;
             if (b == 0) {
-                ctl.inserted = 0;
-                ctl.failed++;
-                if (ctl.failed > 10) ctl.done = 1;
-                else ctl.i_last += dir == 0 ? (int)NC : -(int)NC;
+                // nothing could be tagged (:4064-4069)
+                const uint32_t f = ctl.failed + 1;
+                wave_sync();
+                if (lane == 0) {
+                    ctl.failed = f;
+                    if (f > 10) ctl.done = 1;
+                    else ctl.i_last += dir == 0 ? (int)NC : -(int)NC;
+                }
+                wave_sync();
             } else {
                 const uint32_t c = (uint32_t)(b & 0xffffffffu) - 1;
                 const uint32_t rd = cd.read[c];
                 const uint32_t tg = cd.tag[c];
-                ctl.failed = 0;
-                ctl.inserted = 1;
-                ctl.winner = rd;
-                ctl.tag = tg;
-                m.hp[rd] = (uint8_t)tg;
                 const uint32_t p = cd.pos[c];
-                m.untag[p >> 6] &= ~(1ull << (p & 63));
-            }
-        }
-        __syncthreads();
-        if (ctl.done) break;
-        if (ctl.inserted) {
-            const uint32_t rd = ctl.winner;
-            const uint32_t g = 2 * (r0 + rd) + dir;
-            const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
-            const uint32_t *kp = d.keys + d.mmr_off[g];
-            const uint32_t inc = ctl.tag ? 0x10000u : 1u;
-            // sites of one read are distinct: plain read-modify-write
-            for (uint32_t t = tid; t < n; t += PF_K3_THREADS) {
-                const uint32_t site = st + t;
-                const uint32_t slot = kp[t];
-                if (site < S && slot != PF_NONE) {
-                    m.cnt[slot] += inc;
-                    m.sum[site] += inc;
+                const uint32_t n = m.mn[rd], st = m.mst[rd];
+                const uint32_t *kp = kb + m.mo[rd];
+                const uint32_t inc = tg ? 0x10000u : 1u;
+                stx.inserts += n;
+                // the sites of one read are distinct: plain read-modify-write
+                for (uint32_t t = lane; t < n; t += 64) {
+                    const uint32_t site = st + t;
+                    const uint32_t slot = kp[t];
+                    if (site < S && slot != PF_NONE) {
+                        m.cnt[slot] += inc;
+                        m.sum[site] += inc;
+                    }
                 }
+                if (lane == 0) {
+                    ctl.failed = 0;
+                    m.hp[rd] = (uint8_t)tg;
+                    m.untag[p >> 6] &= ~(1ull << (p & 63));
+                }
+                wave_sync();
+                k3_range_update(m.sum, S, cov_rt, ctl, lane);
             }
-            __syncthreads();
-            if (wid == 0) k3_range_update(m.sum, S, cov_rt, ctl, lane);
-            __syncthreads();
+            K3_STAMP(7);
+            if (!ctl.done) k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
+            K3_STAMP(1);
         }
     }
 
@@ -922,6 +1108,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     const uint32_t strict = dir == 0 ? FLG_RIGHT_STRICT : FLG_LEFT_STRICT;
     for (uint32_t i = tid; i < R; i += PF_K3_THREADS) {
         if (m.flg[i] & strict) {
+            atomicAdd(&ctl.nstrict, 1u);
             const uint32_t ref = d.read_hp[r0 + i], q = m.hp[i];
             if (ref <= 1 && q <= 1) atomicAdd(&ctl.tab[ref * 2 + q], 1);
         }
@@ -929,6 +1116,15 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     }
     __syncthreads();
     if (tid < 4) d.table[((uint64_t)w * 2 + dir) * 4 + tid] = ctl.tab[tid];
+    if (tid == 0) {
+        unsigned long long *sp = d.stats + ((uint64_t)w * 2 + dir) * PF_NSTAT;
+        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
+        sp[4] = ctl.summ; sp[5] = ctl.nstrict; sp[6] = R; sp[7] = S;
+#ifdef PF_K3_PROFILE
+        unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 8;
+        for (int i = 0; i < 8; i++) pp[i] = prof_acc[i];
+#endif
+    }
 }
 
 __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
@@ -941,6 +1137,7 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     const uint32_t S = d.win_S[w];
     if (S == 0) {
         if (tid < 4) d.table[((uint64_t)w * 2 + dir) * 4 + tid] = 0;
+        if (tid < PF_NSTAT) d.stats[((uint64_t)w * 2 + dir) * PF_NSTAT + tid] = 0;
         return;
     }
     const uint32_t R = d.win_nreads[w];
@@ -954,6 +1151,8 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     const bool p1_lds = need1 <= d.lds_bytes;
     if (tid == 0) {
         ctl.fail = 0;
+        ctl.summ = 0;
+        ctl.nstrict = 0;
         if (!p1_lds) {
             const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)align16(need1));
             if (o + need1 > d.scr_cap) { ctl.fail = 1; atomicOr(d.status, PF_ST_SCR_OVF); }
@@ -973,19 +1172,20 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     const uint32_t ntot = ctl.ntot;
 
     // ---- P2: greedy
-    uint64_t off[8];
+    uint64_t off[K3_NOFF];
     const uint64_t fixed = k3_layout(S, ntot, R, dir, off);
     const uint64_t min_rec = 12ull * ncp * 8;
     const bool p2_lds = fixed + min_rec <= d.lds_bytes;
+    const uint32_t lgc = 31 - __clz(ncp);
     if (p2_lds) {
         uint32_t rc = (uint32_t)((d.lds_bytes - fixed) / 12);
-        rc = (rc >> (31 - __clz(ncp))) << (31 - __clz(ncp));
-        if (rc > ncp * 512) rc = ncp * 512;
+        rc = (rc >> lgc) << lgc;
+        if (rc > (ncp << 9)) rc = ncp << 9;
         K3Mem m;
         k3_mem(smem, off, rc, m);
         k3_greedy_body<true>(d, w, dir, r0, S, R, m, ctl, cd);
     } else {
-        const uint32_t rc = ncp * 256;
+        const uint32_t rc = ncp << 8;
         const uint64_t need2 = align16(fixed + 12ull * rc);
         __syncthreads();
         if (tid == 0) {

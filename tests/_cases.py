@@ -1,0 +1,118 @@
+"""Parity-test inputs: seeded synthetic batches plus edge cases of the
+reference's window semantics (blockjoin.c line numbers in each docstring)."""
+import numpy as np
+
+from pomfret_amd.abi import Config, WindowBatch
+from pomfret_amd.synth import SynthSpec, make_batch
+
+
+def synth(n, cov, seed, **kw):
+    return make_batch(SynthSpec(n_windows=n, coverage=cov, seed=seed, **kw))
+
+
+def report_like(n=3, seed=9):
+    """Config 5: `pomfret report --chunk-size 10000 --chunk-stride 5000` at 200x:
+    10 kb windows, parameters c/10+1, 2x, c/4+1 (blockjoin.c:5045-5051)."""
+    b = synth(n, 200, seed, gap=10_000, window_stride=400_000)
+    return b, Config.from_coverage(200, report=True)
+
+
+def with_odd_tags(b: WindowBatch, seed=3):
+    """Left/right reference reads with hp 254 and 7: the (readID<<2)|hp round
+    trip of haplotag_region1 step 1.5 (blockjoin.c:4013-4024) moves their tag
+    to readID|63 (resp. readID|1)."""
+    b = b.select(range(b.n_windows))
+    rng = np.random.default_rng(seed)
+    sel = rng.random(b.n_reads) < 0.08
+    b.read_hp[sel] = rng.choice(np.array([254, 7, 5, 2], np.uint8), sel.sum())
+    return b
+
+
+def with_unsorted_and_dup_calls(b: WindowBatch, seed=4):
+    """Some reads get a duplicated call position (another category) and a
+    swapped pair of calls: the reference takes first/last calls in array order
+    (blockjoin.c:3375-3379) and radix-sorts the rest (:3400)."""
+    b = b.select(range(b.n_windows))
+    rng = np.random.default_rng(seed)
+    pos, cat = list(b.call_pos), list(b.call_cat)
+    off = b.read_call_off.astype(np.int64)
+    new_pos, new_cat, new_off = [], [], [0]
+    for r in range(b.n_reads):
+        p = pos[off[r]:off[r + 1]]
+        c = cat[off[r]:off[r + 1]]
+        if len(p) > 6 and rng.random() < 0.15:
+            i = int(rng.integers(1, len(p) - 2))
+            p = p[:i] + [p[i]] + p[i:]                # duplicated position
+            c = c[:i] + [int((c[i] + 1) % 3)] + c[i:]
+        if len(p) > 6 and rng.random() < 0.10:
+            i = int(rng.integers(1, len(p) - 2))
+            p[i], p[i + 1] = p[i + 1], p[i]           # locally unsorted
+            c[i], c[i + 1] = c[i + 1], c[i]
+        new_pos += p
+        new_cat += c
+        new_off.append(len(new_pos))
+    return WindowBatch(win_start=b.win_start, win_end=b.win_end, win_read_off=b.win_read_off,
+                       read_start=b.read_start, read_end=b.read_end, read_hp=b.read_hp,
+                       read_call_off=np.array(new_off, np.uint64),
+                       call_pos=np.array(new_pos, np.uint32), call_cat=np.array(new_cat, np.uint8))
+
+
+def with_empty_and_starved_windows(b: WindowBatch):
+    """Window 0 keeps only its first read (left-coverage check fails,
+    blockjoin.c:1161); window 1 loses all reads (empty fetch)."""
+    keep = []
+    ro = b.win_read_off
+    for w in range(b.n_windows):
+        rs = list(range(ro[w], ro[w + 1]))
+        if w == 0:
+            rs = rs[:1]
+        elif w == 1:
+            rs = []
+        keep.append(rs)
+    reads = np.array([r for rs in keep for r in rs], np.int64)
+    co = b.read_call_off.astype(np.int64)
+    calls = np.concatenate([np.arange(co[r], co[r + 1]) for r in reads]) if len(reads) else np.zeros(0, np.int64)
+    return WindowBatch(
+        win_start=b.win_start, win_end=b.win_end,
+        win_read_off=np.concatenate([[0], np.cumsum([len(x) for x in keep])]),
+        read_start=b.read_start[reads], read_end=b.read_end[reads], read_hp=b.read_hp[reads],
+        read_call_off=np.concatenate([[0], np.cumsum(co[reads + 1] - co[reads])]),
+        call_pos=b.call_pos[calls], call_cat=b.call_cat[calls])
+
+
+def handmade():
+    """Four sites carried by two reads (see tests/test_oracle.py)."""
+    reads = []
+    for i in range(30):
+        reads.append((10, 60, i % 2, [(50, 0)]))
+    reads.append((90, 500, 254, [(100, 0), (200, 1), (300, 0), (400, 1)]))
+    reads.append((90, 500, 254, [(100, 1), (200, 0), (300, 1), (400, 0)]))
+    off = np.cumsum([0] + [len(r[3]) for r in reads])
+    return WindowBatch(
+        win_start=[60], win_end=[70], win_read_off=[0, len(reads)],
+        read_start=[r[0] for r in reads], read_end=[r[1] for r in reads],
+        read_hp=[r[2] for r in reads], read_call_off=off,
+        call_pos=[c[0] for r in reads for c in r[3]], call_cat=[c[1] for r in reads for c in r[3]])
+
+
+def cases():
+    """(name, cfg, batch) parity cases at sizes the oracle finishes in seconds."""
+    c30 = Config.from_coverage(30, given=False)
+    c60 = Config.from_coverage(60, given=True)
+    out = [
+        ("synth30", c30, synth(12, 30, 21)),
+        ("synth60", c60, synth(6, 60, 22)),
+        ("gapmix", c30, synth(8, 30, 23, gap_mix=True)),
+        ("report200", *reversed(report_like())),
+        ("oddtags", c30, with_odd_tags(synth(6, 30, 24))),
+        ("unsorted_dups", c30, with_unsorted_and_dup_calls(synth(6, 30, 25))),
+        ("starved", c30, with_empty_and_starved_windows(synth(4, 30, 26))),
+        ("k1", Config(k=1, k_span=5000, cov_for_selection=4, cov_for_runtime=8, n_cand=8), synth(4, 30, 27)),
+        ("k2_span300", Config(k=2, k_span=300, cov_for_selection=4, cov_for_runtime=8, n_cand=8), synth(4, 30, 28)),
+        ("k4", Config(k=4, k_span=5000, cov_for_selection=4, cov_for_runtime=8, n_cand=8), synth(4, 30, 29)),
+        ("ncand2", Config(k=3, k_span=5000, cov_for_selection=4, cov_for_runtime=8, n_cand=2), synth(4, 30, 30)),
+        ("ncand100", Config(k=3, k_span=5000, cov_for_selection=4, cov_for_runtime=8, n_cand=100), synth(3, 30, 31)),
+        ("cov_sel_high", Config(k=3, k_span=5000, cov_for_selection=12, cov_for_runtime=30, n_cand=8), synth(4, 30, 32)),
+        ("handmade", Config(k=3, k_span=5000, cov_for_selection=1, cov_for_runtime=2, n_cand=4), handmade()),
+    ]
+    return out

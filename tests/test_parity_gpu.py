@@ -1,0 +1,105 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Integer/byte/index outputs must be bit-identical: per-window decisions, 2x2
+tables, join/which_way, site counts, per-read tags, every intermediate site
+array and every read's methmer list.  The floating-point internals the north
+star names -- the two-sided Fisher p of each direction (FP64, blockjoin.c:3926)
+and the evaluate_separation1 score (FP32) -- must agree within 1e-6 relative;
+with the same host epilogue code they are in fact identical.
+"""
+import numpy as np
+import pytest
+
+from tests._cases import cases, synth
+
+pytestmark = pytest.mark.gpu
+
+CASES = cases()
+
+
+def _compare(ref, out, tag):
+    for name in ("decision", "dir_table", "dir_join", "dir_which_way", "win_n_sites",
+                 "win_n_reads", "read_hp"):
+        a, g = getattr(ref, name), getattr(out, name)
+        assert np.array_equal(a, g), f"{tag}: {name} differs at {np.argwhere(a != g)[:5].tolist()}"
+    np.testing.assert_allclose(out.dir_fisher_p, ref.dir_fisher_p, rtol=1e-6, atol=0, err_msg=tag)
+    np.testing.assert_allclose(out.dir_score, ref.dir_score, rtol=1e-6, atol=0, err_msg=tag)
+
+
+@pytest.mark.parametrize("name,cfg,batch", CASES, ids=[c[0] for c in CASES])
+def test_windows_parity(oracle_lib, gpu_ctx, name, cfg, batch):
+    ref = oracle_lib.methphase(cfg, batch, n_threads=8)
+    db = gpu_ctx.upload(cfg, batch)
+    out = db.run()
+    _compare(ref, out, name)
+    db.free()
+
+
+@pytest.mark.parametrize("name,cfg,batch", CASES, ids=[c[0] for c in CASES])
+def test_sites_and_methmers_parity(oracle_lib, gpu_ctx, name, cfg, batch):
+    """Intermediates: get_methmer_sites_and_ranges (both directions) and every
+    read's get_mmr_of_read output (mmr_n, mmr_start_i, keys)."""
+    db = gpu_ctx.upload(cfg, batch)
+    ro = batch.win_read_off
+    for d in (0, 1):
+        n, st, keys = db.debug_methmers(d)
+        k0 = 0
+        for w in range(batch.n_windows):
+            real, starts, lens = oracle_lib.window_sites(cfg, batch, w, d)
+            g_real, g_starts, g_lens = db.debug_sites(w, d)
+            assert np.array_equal(real, g_real), f"{name} w{w} d{d} sites"
+            assert np.array_equal(starts, g_starts), f"{name} w{w} d{d} starts"
+            assert np.array_equal(lens, g_lens), f"{name} w{w} d{d} lens"
+            on, ost, okeys = oracle_lib.window_methmers(cfg, batch, w, d)
+            gn = n[ro[w]:ro[w + 1]]
+            assert np.array_equal(on, gn), f"{name} w{w} d{d} mmr_n {np.argwhere(on != gn)[:3]}"
+            assert np.array_equal(ost, st[ro[w]:ro[w + 1]]), f"{name} w{w} d{d} mmr_start"
+            assert np.array_equal(okeys, keys[k0:k0 + len(okeys)]), f"{name} w{w} d{d} keys"
+            k0 += len(okeys)
+        assert k0 == len(keys)
+    db.free()
+
+
+def test_full_size_workload(oracle_lib, gpu_ctx):
+    """The bench workload (256 chr20-like windows at 30x): bit-exact against the
+    oracle on every window, deterministic across runs."""
+    from pomfret_amd import Config
+    cfg = Config.from_coverage(30, given=False)
+    b = synth(256, 30, 1000)
+    ref = oracle_lib.methphase(cfg, b, n_threads=16)
+    db = gpu_ctx.upload(cfg, b)
+    out1 = db.run()
+    out2 = db.run()
+    _compare(ref, out1, "full")
+    _compare(out1, out2, "rerun")
+    db.free()
+
+
+def test_sharding_invariance(gpu_ctx):
+    """Windows are independent: any sub-batch (a GPU shard) reproduces the
+    full batch's per-window results, in any window order."""
+    from pomfret_amd import Config
+    from pomfret_amd.shard import lpt_partition, window_costs
+    cfg = Config.from_coverage(30, given=False)
+    b = synth(24, 30, 77, gap_mix=True)
+    full = gpu_ctx.upload(cfg, b).run()
+    parts = lpt_partition(window_costs(b), 3)
+    for idx in parts:
+        idx = idx[::-1]
+        sub = b.select(idx)
+        res = gpu_ctx.upload(cfg, sub).run()
+        assert np.array_equal(res.decision, full.decision[idx])
+        assert np.array_equal(res.dir_table, full.dir_table[idx])
+        ro = b.win_read_off
+        hp = np.concatenate([full.read_hp[ro[w]:ro[w + 1]] for w in idx])
+        assert np.array_equal(res.read_hp, hp)
+
+
+def test_one_shot_api(oracle_lib):
+    """pf_methphase_windows (upload + run + free in one call)."""
+    from pomfret_amd import Config, methphase_windows
+    cfg = Config.from_coverage(30, given=False)
+    b = synth(4, 30, 99)
+    out = methphase_windows(cfg, b, device=0)
+    ref = oracle_lib.methphase(cfg, b)
+    _compare(ref, out, "oneshot")

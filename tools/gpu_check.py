@@ -38,9 +38,34 @@ def compare(cfg, b, tag):
     return ok and p_ok
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--timing" not in sys.argv:
     allok = True
     allok &= compare(Config.from_coverage(30, given=False), make_batch(SynthSpec(n_windows=16, coverage=30)), "30x")
     allok &= compare(Config.from_coverage(60, given=True), make_batch(SynthSpec(n_windows=16, coverage=60, seed=2)), "60x")
     allok &= compare(Config.from_coverage(30, given=False), make_batch(SynthSpec(n_windows=16, coverage=30, seed=3, gap_mix=True)), "mix")
     print("ALL_OK" if allok else "SOME_FAIL")
+
+
+def timing(n_windows=256, cov=30, reps=5):
+    cfg = Config.from_coverage(cov, given=False)
+    b = make_batch(SynthSpec(n_windows=n_windows, coverage=cov, seed=11))
+    ctx = Context(0)
+    db = ctx.upload(cfg, b)
+    out = db.run()
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        db.run(out)
+        ts.append(time.perf_counter() - t)
+    st = db.stats()
+    print(f"[timing W={n_windows} cov={cov}] R={b.n_reads} wall min={min(ts)*1e3:.3f} ms "
+          f"reads/s={b.n_reads/min(ts):.3e} kernels={ctx.kernel_times()}")
+    print("  stats sum (lookups, inserts, iters, scanned):", st.sum(axis=(0, 1)).tolist(),
+          " max iters/problem:", int(st[:, :, 2].max()))
+    db.free()
+    ctx.close()
+
+
+if __name__ == "__main__" and "--timing" in sys.argv:
+    timing(256, 30)
+    timing(256, 60)

@@ -1,0 +1,32 @@
+"""Phase breakdown of the greedy kernel from the diagnostic (-DPF_K3_PROFILE) build."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pomfret_amd._lib as L  # noqa: E402
+
+L.LIB_PATH = os.path.join(os.path.dirname(L.LIB_PATH), "libpomfret_amd_prof.so")
+from pomfret_amd import Config, Context  # noqa: E402
+from pomfret_amd.synth import SynthSpec, make_batch  # noqa: E402
+
+names = ["init", "collect", "wait_a", "fill", "wait_b", "sum+key", "wait_c", "select+ins+range"]
+for cov in (30, 60):
+    cfg = Config.from_coverage(cov, given=False)
+    b = make_batch(SynthSpec(n_windows=256, coverage=cov, seed=11))
+    ctx = Context(0)
+    db = ctx.upload(cfg, b)
+    db.run(); db.run()
+    lib = L.lib()
+    lib.pf_batch_prof.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    prof = np.zeros((256, 2, 8), np.uint64)
+    lib.pf_batch_prof(db.handle, prof.ctypes.data, prof.size)
+    st = db.stats()
+    tot = prof.sum(axis=(0, 1)).astype(float)
+    iters = st[:, :, 2].sum()
+    print(f"cov={cov} kernels={ctx.kernel_times()} iters={iters}")
+    for n, v in zip(names, tot):
+        print(f"  {n:18s} {v/tot.sum()*100:5.1f}%  {v/iters:8.0f} cyc/iter")
+    db.free(); ctx.close()
