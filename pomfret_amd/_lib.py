@@ -36,6 +36,7 @@ def lib():
         L.pf_strerror.argtypes = [C.c_int]
         L.pf_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.pf_ctx_destroy.argtypes = [C.c_void_p]
+        L.pf_selftest.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.pf_batch_upload.argtypes = [C.c_void_p, C.POINTER(PfCfg), C.POINTER(PfWindowBatch),
                                       C.POINTER(C.c_void_p)]
         L.pf_batch_free.argtypes = [C.c_void_p]
@@ -109,6 +110,13 @@ class Context:
         n = C.c_int(8)
         _check(lib().pf_last_kernel_times(self.handle, names, ms, C.byref(n)), "kernel_times")
         return {names[i].decode(): float(ms[i]) for i in range(n.value)}
+
+    def selftest(self) -> int:
+        """Mismatching (a, b) pairs of the kernels' 16-bit count division
+        against correctly rounded fp32 division (pf_selftest); 0 expected."""
+        n = C.c_uint64(0)
+        _check(lib().pf_selftest(self.handle, C.byref(n)), "pf_selftest")
+        return int(n.value)
 
     def haptag_reads(self, known: KnownVars, reads: ReadAlnBatch) -> np.ndarray:
         out = np.zeros(max(reads.n_reads, 1), np.uint8)

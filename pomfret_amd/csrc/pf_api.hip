@@ -22,6 +22,7 @@
 __global__ void pf_k1_sites(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
+__global__ void pf_selftest_div(unsigned long long *bad);
 
 #define PF_NKERN 3
 static const char *k_names[PF_NKERN] = {"pf_k1_sites", "pf_k2_methmers", "pf_k3_greedy"};
@@ -93,6 +94,25 @@ extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
     c->have_times = 0;
     *out = c;
     return PF_OK;
+}
+
+extern "C" int pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches) {
+    if (!ctx || !mismatches) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    unsigned long long *d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(*d)));
+    int rc = PF_OK;
+    unsigned long long h = 0;
+    if (hipMemsetAsync(d, 0, sizeof(*d), ctx->stream) != hipSuccess) rc = PF_ERR_HIP;
+    if (rc == PF_OK) {
+        hipLaunchKernelGGL(pf_selftest_div, dim3(65535), dim3(256), 0, ctx->stream, d);
+        if (hipGetLastError() != hipSuccess) rc = PF_ERR_HIP;
+    }
+    if (rc == PF_OK && hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) rc = PF_ERR_HIP;
+    if (rc == PF_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = PF_ERR_HIP;
+    (void)hipFree(d);
+    *mismatches = h;
+    return rc;
 }
 
 extern "C" int pf_ctx_device(const pf_ctx *c) { return c->device; }
@@ -292,9 +312,9 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     ALLOC(d.table, 8ull * W);
     ALLOC(d.hp_fwd, R);
     ALLOC(d.stats, 16ull * W);
-    ALLOC(d.prof, 16ull * W);
+    ALLOC(d.prof, 32ull * W);
     const char *lds = getenv("PF_K3_LDS");
-    d.lds_bytes = lds ? (uint32_t)atoi(lds) : 65536u;
+    d.lds_bytes = lds ? (uint32_t)atoi(lds) : 73728u;
     if (hipHostMalloc((void **)&b->h_table, std::max<size_t>(8ull * W, 1) * 4) != hipSuccess ||
         hipHostMalloc((void **)&b->h_S, std::max<size_t>(W, 1) * 4) != hipSuccess ||
         hipHostMalloc((void **)&b->h_nreads, std::max<size_t>(W, 1) * 4) != hipSuccess ||
@@ -485,10 +505,10 @@ extern "C" int pf_batch_stats(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
 }
 
 extern "C" int pf_batch_prof(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
-    if (!b || !out || n < 16ull * b->W) return PF_ERR_ARG;
+    if (!b || !out || n < 32ull * b->W) return PF_ERR_ARG;
     HIPCHK(hipSetDevice(b->ctx->device));
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    if (b->W) HIPCHK(hipMemcpy(out, b->d.prof, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (b->W) HIPCHK(hipMemcpy(out, b->d.prof, 32ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PF_OK;
 }
 

@@ -41,8 +41,10 @@
 #ifdef PF_K3_PROFILE
 #define K3_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
+#define K3_COUNT(i, v) do { prof_acc[i] += (v); } while (0)
 #else
 #define K3_STAMP(i) do { } while (0)
+#define K3_COUNT(i, v) do { } while (0)
 #endif
 
 // ------------------------------------------------------------------------
@@ -53,6 +55,14 @@ DEV void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Same, ordering global memory as well (record rows may live in HBM when the
+// problem does not fit LDS).
+DEV void wave_sync_mem() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 DEV uint32_t wave_incl_scan(uint32_t x, uint32_t lane) {
@@ -69,6 +79,53 @@ DEV uint32_t wave_max_u32(uint32_t x) {
     for (int o = 32; o > 0; o >>= 1) { uint32_t y = __shfl_xor(x, o, 64); x = y > x ? y : x; }
     return x;
 }
+
+// Wave max with DPP row ops (quad perms, half-row and row mirrors) and four
+// readlanes: no LDS round trip, unlike the shuffle butterfly above.
+DEV uint32_t dpp_max_step(uint32_t x, const int ctrl_sel) {
+    uint32_t y;
+    switch (ctrl_sel) {
+    case 0: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false); break;  // quad_perm [1,0,3,2]
+    case 1: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false); break;  // quad_perm [2,3,0,1]
+    case 2: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false); break; // row_half_mirror
+    default: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false); break; // row_mirror
+    }
+    return y > x ? y : x;
+}
+DEV uint32_t wave_max_dpp(uint32_t x) {
+    x = dpp_max_step(x, 0);
+    x = dpp_max_step(x, 1);
+    x = dpp_max_step(x, 2);
+    x = dpp_max_step(x, 3);
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), b = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), e = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    const uint32_t ab = a > b ? a : b, ce = c > e ? c : e;
+    return ab > ce ? ab : ce;
+}
+// (float)cnt/sum of query_counts_of_mmrs (blockjoin.c:3508-3509) for 16-bit
+// counts (0 <= a <= 65535, 1 <= b <= 65535), correctly
+// rounded: one Newton correction of the hardware reciprocal.  Exact here since
+// a/b is never within 2^-40 (relative) of an fp32 rounding midpoint when
+// b < 2^16, while the corrected quotient is within ~2^-46; checked on the
+// device over all 2^32 (a, b) pairs by pf_selftest (tests/test_parity_gpu.py).
+DEV float div_u16_y(float fa, float fb, float y) {
+    const float q0 = fa * y;
+    const float r = __builtin_fmaf(-q0, fb, fa);
+    return __builtin_fmaf(r, y, q0);
+}
+DEV float div_u16(uint32_t a, uint32_t b) {
+    const float fb = (float)b;
+    return div_u16_y((float)a, fb, __builtin_amdgcn_rcpf(fb));
+}
+// per-site divisor cache of the greedy kernel: (h0, h1, 1/h0, 1/h1) with a
+// zero hap total stored as (1, 0) so that 0/h evaluates to 0 without a branch
+DEV float4 site_rec(uint32_t v) {
+    const uint32_t h0 = v & 0xffffu, h1 = v >> 16;
+    const float f0 = (float)(h0 ? h0 : 1u), f1 = (float)(h1 ? h1 : 1u);
+    return make_float4(f0, f1, h0 ? __builtin_amdgcn_rcpf(f0) : 0.f, h1 ? __builtin_amdgcn_rcpf(f1) : 0.f);
+}
+
+DEV uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
 
 DEV uint64_t wave_max_u64(uint64_t x) {
 #pragma unroll
@@ -598,7 +655,6 @@ struct K3Ctl {
     int32_t i_last;
     uint32_t min_i, max_i, fail, summ, nstrict;
     unsigned long long scr;
-    unsigned long long wbest[PF_K3_WAVES];
     int32_t tab[4];
 };
 
@@ -607,7 +663,8 @@ struct K3Cand {
     uint32_t pos[PF_MAX_NCAND];
     uint32_t site0[PF_MAX_NCAND];
     uint32_t len[PF_MAX_NCAND];
-    uint64_t kofs[PF_MAX_NCAND];
+    uint32_t kofs[PF_MAX_NCAND];
+    unsigned long long key[PF_MAX_NCAND];
     uint8_t tag[PF_MAX_NCAND];
 };
 
@@ -670,45 +727,58 @@ DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uin
 
 struct K3Mem {
     uint32_t *sum, *cnt, *aux, *ord, *mn, *mst, *mo;
+    float4 *srec;            // per-site divisor cache (register variant)
     uint8_t *hp, *flg;
     uint64_t *untag;
-    float2 *recv;
+    uint16_t *sl16;          // slot lists in LDS (u16), when they fit
+    const uint32_t *kb;      // slot lists in the HBM key arena (window base)
+    float2 *recv;            // per-wave record rings
     uint32_t *recc;
-    uint32_t rc;        // record capacity (multiple of ncp)
+    uint32_t rcw;            // records per wave
 };
 
-#define K3_NOFF 11
-// P2 byte layout for given sizes; returns the bytes needed before the records
-DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint64_t off[K3_NOFF]) {
+#define K3_NOFF 13
+// P2 byte layout.  Returns the bytes needed with `rcw` records per wave;
+// slots (u16) are included only when with_slots.
+DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint32_t summ,
+                       bool with_slots, uint32_t rcw, uint64_t off[K3_NOFF]) {
     const uint32_t nwords = (R + 63) >> 6;
     off[0] = 0;                                        // sum   S*4
     off[1] = align16(off[0] + 4ull * S);               // cnt   ntot*4
     off[2] = align16(off[1] + 4ull * ntot);            // hp    R
     off[3] = align16(off[2] + R);                      // flg   R
-    off[4] = align16(off[3] + R);                      // aux   R*4
-    off[5] = align16(off[4] + 4ull * R);               // ord   R*4 (dir 1)
-    off[6] = align16(off[5] + (dir ? 4ull * R : 0));   // untag nwords*8
-    off[7] = align16(off[6] + 8ull * nwords);          // mn    R*4  methmers per read
-    off[8] = align16(off[7] + 4ull * R);               // mst   R*4  first site index
-    off[9] = align16(off[8] + 4ull * R);               // mo    R*4  key offset (window-relative)
-    off[10] = align16(off[9] + 4ull * R);              // records
-    return off[10];
+    off[4] = align16(off[3] + R);                      // ord   R*4 (dir 1)
+    off[5] = align16(off[4] + (dir ? 4ull * R : 0));   // untag nwords*8
+    off[6] = align16(off[5] + 8ull * nwords);          // mn    R*4  methmers per read
+    off[7] = align16(off[6] + 4ull * R);               // mst   R*4  first site index
+    off[8] = align16(off[7] + 4ull * R);               // mo    R*4  slot-list offset
+    off[9] = align16(off[8] + 4ull * R);               // sl16  summ*2 (optional)
+    off[10] = align16(off[9] + (with_slots ? 2ull * summ : 0));   // srec  S*16
+    off[11] = off[10] + 16ull * S;                                 // records / aux
+    const uint64_t rec = 12ull * PF_K3_WAVES * rcw;
+    const uint64_t aux = 4ull * R;
+    off[12] = off[11] + (rec > aux ? rec : aux);
+    return off[12];
 }
 
-DEV void k3_mem(uint8_t *base, const uint64_t off[K3_NOFF], uint32_t rc, K3Mem &m) {
+DEV void k3_mem(uint8_t *base, const uint64_t off[K3_NOFF], uint32_t rcw, bool with_slots,
+                const uint32_t *kb, K3Mem &m) {
     m.sum = reinterpret_cast<uint32_t *>(base + off[0]);
     m.cnt = reinterpret_cast<uint32_t *>(base + off[1]);
     m.hp = base + off[2];
     m.flg = base + off[3];
-    m.aux = reinterpret_cast<uint32_t *>(base + off[4]);
-    m.ord = reinterpret_cast<uint32_t *>(base + off[5]);
-    m.untag = reinterpret_cast<uint64_t *>(base + off[6]);
-    m.mn = reinterpret_cast<uint32_t *>(base + off[7]);
-    m.mst = reinterpret_cast<uint32_t *>(base + off[8]);
-    m.mo = reinterpret_cast<uint32_t *>(base + off[9]);
-    m.recv = reinterpret_cast<float2 *>(base + off[10]);
-    m.recc = reinterpret_cast<uint32_t *>(base + off[10] + 8ull * rc);
-    m.rc = rc;
+    m.ord = reinterpret_cast<uint32_t *>(base + off[4]);
+    m.untag = reinterpret_cast<uint64_t *>(base + off[5]);
+    m.mn = reinterpret_cast<uint32_t *>(base + off[6]);
+    m.mst = reinterpret_cast<uint32_t *>(base + off[7]);
+    m.mo = reinterpret_cast<uint32_t *>(base + off[8]);
+    m.sl16 = with_slots ? reinterpret_cast<uint16_t *>(base + off[9]) : nullptr;
+    m.kb = kb;
+    m.srec = reinterpret_cast<float4 *>(base + off[10]);
+    m.recv = reinterpret_cast<float2 *>(base + off[11]);
+    m.recc = reinterpret_cast<uint32_t *>(base + off[11] + 8ull * PF_K3_WAVES * rcw);
+    m.aux = reinterpret_cast<uint32_t *>(base + off[11]);
+    m.rcw = rcw;
 }
 
 #define FLG_LEFT 1u
@@ -718,7 +788,6 @@ DEV void k3_mem(uint8_t *base, const uint64_t off[K3_NOFF], uint32_t rc, K3Mem &
 
 // update_available_methmer_range (blockjoin.c:3669-3691), one wavefront
 DEV void k3_range_update(const uint32_t *sum, uint32_t S, int cov_rt, K3Ctl &ctl, uint32_t lane) {
-    // left: extend down from (int)min_i while covered
     const int m0 = (int)ctl.min_i;
     if (m0 >= 0) {
         int count = 0;
@@ -736,7 +805,6 @@ DEV void k3_range_update(const uint32_t *sum, uint32_t S, int cov_rt, K3Ctl &ctl
         }
         if (count > 0 && lane == 0) ctl.min_i = (uint32_t)(m0 - count + 1);
     }
-    // right: extend up from (int)max_i while covered; max_i = last covered index
     const int M0 = (int)ctl.max_i;
     if (M0 >= 0) {
         int count = 0;
@@ -757,14 +825,81 @@ DEV void k3_range_update(const uint32_t *sum, uint32_t S, int cov_rt, K3Ctl &ctl
     wave_sync();
 }
 
-// per-problem counters for the algorithmic-byte model (B_tag)
 struct K3Stats {
     unsigned long long lookups, inserts, iters, scanned;
 };
 #define PF_NSTAT 8
 
-// step 1 of an iteration (wave 0 only): collect up to NC untagged reads in scan
-// order from i_last (:4037-4045); empty batches advance i_last (:4046-4051).
+// next untagged scan position after p (dir 0: > p) / before p (dir 1: < p);
+// -1 if none.  One wavefront; no cross-lane shuffles (ballot + readlane).
+DEV int k3_next_untag(const uint64_t *untag, uint32_t nwords, int p, uint32_t dir, uint32_t lane) {
+    if (dir == 0) {
+        const int q = p + 1;
+        if (q >= (int)(nwords * 64)) return -1;
+        const uint32_t w0 = (uint32_t)q >> 6;
+        for (uint32_t wb = w0; wb < nwords; wb += 64) {
+            const uint32_t wi = wb + lane;
+            uint64_t bits = wi < nwords ? untag[wi] : 0ull;
+            if (wi == w0) bits &= ~0ull << ((uint32_t)q & 63);
+            const uint64_t bal = __ballot(bits != 0);
+            if (bal) {
+                const int src = __ffsll((unsigned long long)bal) - 1;
+                const int v = (int)(wi * 64 + (uint32_t)(__ffsll((unsigned long long)bits) - 1));
+                return __builtin_amdgcn_readlane(v, src);
+            }
+        }
+        return -1;
+    } else {
+        const int q = p - 1;
+        if (q < 0) return -1;
+        const int w0 = q >> 6;
+        for (int wb = w0; wb >= 0; wb -= 64) {
+            const int wi = wb - (int)lane;
+            uint64_t bits = wi >= 0 ? untag[wi] : 0ull;
+            if (wi == w0) {
+                const uint32_t b = (uint32_t)q & 63;
+                bits &= b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
+            }
+            const uint64_t bal = __ballot(bits != 0);
+            if (bal) {
+                const int src = __ffsll((unsigned long long)bal) - 1;
+                const int v = bits ? wi * 64 + (63 - __clzll((long long)bits)) : 0;
+                return __builtin_amdgcn_readlane(v, src);
+            }
+        }
+        return -1;
+    }
+}
+
+// per-candidate derived fields for the current range (query_counts_of_mmrs
+// only uses sites in [min_i, max_i), blockjoin.c:3500-3501); one wavefront.
+DEV void k3_cand_fields(const K3Mem &m, uint32_t nc, uint32_t dir, uint32_t lane, const K3Ctl &ctl,
+                        K3Cand &cd, K3Stats &stx) {
+    const uint32_t mn_ = ctl.min_i, mx_ = ctl.max_i;
+    uint32_t lsum = 0;
+    for (uint32_t c = lane; c < nc; c += 64) {
+        const uint32_t rd = cd.read[c];
+        const uint32_t n = m.mn[rd], st = m.mst[rd];
+        const uint64_t lo = st > mn_ ? st : mn_;
+        const uint64_t hi0 = (uint64_t)st + n;
+        const uint64_t hi = hi0 < mx_ ? hi0 : mx_;
+        const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0;
+        cd.site0[c] = (uint32_t)lo;
+        cd.len[c] = len;
+        cd.kofs[c] = m.mo[rd] + (len ? (uint32_t)(lo - st) : 0);
+        lsum += len;
+    }
+    // lookups statistic: a wave sum without shuffles (ballot bit-slices)
+    uint32_t tot = 0;
+#pragma unroll
+    for (int b = 0; b < 16; b++) tot += (uint32_t)__popcll(__ballot((lsum >> b) & 1)) << b;
+    stx.lookups += tot;
+    wave_sync();
+}
+
+// full candidate collection from i_last (:4037-4051), one wavefront: used at
+// start and after a failed iteration (i_last moves).  Returns with
+// ctl.done or a non-empty list.
 DEV void k3_collect(const K3Mem &m, uint32_t R, uint32_t dir, uint32_t NC, uint32_t lane,
                     K3Ctl &ctl, K3Cand &cd, K3Stats &stx) {
     const uint32_t nwords = (R + 63) >> 6;
@@ -777,45 +912,18 @@ DEV void k3_collect(const K3Mem &m, uint32_t R, uint32_t dir, uint32_t NC, uint3
             wave_sync();
             return;
         }
+        // first NC set bits from il (scan order), sequential over words
         uint32_t found = 0;
-        if (dir == 0) {
-            const uint32_t w0 = (uint32_t)il >> 6;
-            for (uint32_t wb = w0; wb < nwords && found < NC; wb += 64) {
-                const uint32_t wi = wb + lane;
-                uint64_t bits = wi < nwords ? m.untag[wi] : 0ull;
-                if (wi == w0) bits &= ~0ull << ((uint32_t)il & 63);
-                const uint32_t c = (uint32_t)__popcll(bits);
-                const uint32_t incl = wave_incl_scan(c, lane);
-                uint32_t rk = found + incl - c;
-                while (bits && rk < NC) {
-                    const uint32_t b = __ffsll((unsigned long long)bits) - 1;
-                    cd.pos[rk++] = wi * 64 + b;
-                    bits &= bits - 1;
-                }
-                found += __shfl(incl, 63, 64);
-            }
-        } else {
-            const int w0 = il >> 6;
-            for (int wb = w0; wb >= 0 && found < NC; wb -= 64) {
-                const int wi = wb - (int)lane;
-                uint64_t bits = wi >= 0 ? m.untag[wi] : 0ull;
-                if (wi == w0) {
-                    const uint32_t b = (uint32_t)il & 63;
-                    bits &= b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
-                }
-                const uint32_t c = (uint32_t)__popcll(bits);
-                const uint32_t incl = wave_incl_scan(c, lane);
-                uint32_t rk = found + incl - c;
-                while (bits && rk < NC) {
-                    const uint32_t b = 63 - __clzll((long long)bits);
-                    cd.pos[rk++] = (uint32_t)wi * 64 + b;
-                    bits &= ~(1ull << b);
-                }
-                found += __shfl(incl, 63, 64);
-            }
+        int p = dir == 0 ? il - 1 : il + 1;
+        while (found < NC) {
+            const int q = k3_next_untag(m.untag, nwords, p, dir, lane);
+            if (q < 0) break;
+            if (lane == 0) cd.pos[found] = (uint32_t)q;
+            found++;
+            p = q;
         }
-        const uint32_t nc = found < NC ? found : NC;
         wave_sync();
+        const uint32_t nc = found;
         if (nc == 0) {
             stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
             failed++;
@@ -827,41 +935,47 @@ DEV void k3_collect(const K3Mem &m, uint32_t R, uint32_t dir, uint32_t NC, uint3
             il += dir == 0 ? (int)NC : -(int)NC;
             continue;
         }
-        if (found >= NC) {
-            const uint32_t pl = cd.pos[NC - 1];
-            stx.scanned += dir == 0 ? pl - (uint32_t)il + 1 : (uint32_t)il - pl + 1;
-        } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
-        uint32_t lmax = 0, lsum = 0;
-        const uint32_t mn_ = ctl.min_i, mx_ = ctl.max_i;
         for (uint32_t c = lane; c < nc; c += 64) {
-            const uint32_t p = cd.pos[c];
-            const uint32_t rd = dir ? m.ord[p] : p;
-            const uint32_t n = m.mn[rd], st = m.mst[rd];
-            // in-range methmers: site index in [min_i, max_i) (query_counts_of_mmrs, :3500-3501)
-            const uint64_t lo = st > mn_ ? st : mn_;
-            const uint64_t hi0 = (uint64_t)st + n;
-            const uint64_t hi = hi0 < mx_ ? hi0 : mx_;
-            const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0;
-            cd.read[c] = rd;
-            cd.site0[c] = (uint32_t)lo;
-            cd.len[c] = len;
-            cd.kofs[c] = (uint64_t)m.mo[rd] + (len ? (lo - st) : 0);
-            lmax = len > lmax ? len : lmax;
-            lsum += len;
+            const uint32_t pp = cd.pos[c];
+            cd.read[c] = dir ? m.ord[pp] : pp;
         }
-        lmax = wave_max_u32(lmax);
-        lsum = wave_incl_scan(lsum, lane);
-        stx.lookups += __shfl(lsum, 63, 64);
-        stx.iters++;
-        if (lane == 0) { ctl.done = 0; ctl.nc = nc; ctl.L = lmax; ctl.i_last = il; ctl.failed = failed; }
+        if (lane == 0) { ctl.done = 0; ctl.nc = nc; ctl.i_last = il; ctl.failed = failed; }
         wave_sync();
         return;
     }
 }
 
-template <bool LDS2>
+// reads visited by the reference's scan this iteration (statistic only)
+DEV void k3_scanned(const K3Ctl &ctl, const K3Cand &cd, uint32_t R, uint32_t dir, uint32_t NC,
+                    K3Stats &stx) {
+    const int il = ctl.i_last;
+    const uint32_t nc = ctl.nc;
+    if (nc >= NC) {
+        const uint32_t pl = cd.pos[NC - 1];
+        stx.scanned += dir == 0 ? pl - (uint32_t)il + 1 : (uint32_t)il - pl + 1;
+    } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+    stx.iters++;
+}
+
+// raw slot-list entry: u16 (0xFFFF = none) in LDS, u32 (PF_NONE) in HBM
+template <bool SLDS>
+DEV uint32_t k3_slot_raw(const K3Mem &m, uint32_t off) {
+    if (SLDS) return m.sl16[off];
+    return m.kb[off];
+}
+
+template <bool SLDS>
+DEV uint32_t k3_slot(const K3Mem &m, uint32_t off) {
+    if (SLDS) {
+        const uint32_t v = m.sl16[off];
+        return v == 0xFFFFu ? PF_NONE : v;
+    }
+    return m.kb[off];
+}
+
+template <bool SLDS>
 DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S,
-                        uint32_t R, const K3Mem &m, K3Ctl &ctl, K3Cand &cd) {
+                        uint32_t R, const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t ntot = ctl.ntot;
     const int cov_rt = d.win_par[w * 4 + 1];
@@ -869,14 +983,12 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     const uint32_t s = d.win_start[w], e = d.win_end[w];
     const uint32_t nwords = (R + 63) >> 6;
     const uint64_t sb = d.win_site_off[w];
-    const uint32_t ncp = next_pow2(NC);
-    const uint32_t lg = 31 - __clz(ncp);
     const uint64_t kbase = d.mmr_off[2ull * r0];
     const uint32_t *kb = d.keys + kbase;
     K3Stats stx = {0, 0, 0, 0};
     uint32_t sum_mmr = 0;
 #ifdef PF_K3_PROFILE
-    unsigned long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long prof_acc[16] = {0};
     unsigned long long prof_last = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -900,24 +1012,49 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         if (dir) m.ord[i] = d.rev_ord[r];
         const uint64_t g = 2ull * r + dir;
         m.mn[i] = d.mmr_n[g];
-        sum_mmr += m.mn[i];
         m.mst[i] = d.mmr_start[g];
-        m.mo[i] = (uint32_t)(d.mmr_off[g] - kbase);
+        sum_mmr += m.mn[i];
     }
     if (tid == 0) {
-        // haplotag_region1 step 1 (blockjoin.c:3976-4004)
         const uint32_t *a = d.site_pos + sb;
         if (dir == 0) {
             ctl.min_i = 0;
-            ctl.max_i = (uint32_t)ub_u32(a, 0, S, s);            // #sites <= ref_start
+            ctl.max_i = (uint32_t)ub_u32(a, 0, S, s);            // #sites <= ref_start (:3994-3998)
         } else {
             ctl.max_i = S - 1;
-            ctl.min_i = (uint32_t)((int)ub_u32(a, 0, S, e) - 1); // may wrap to UINT32_MAX
+            ctl.min_i = (uint32_t)((int)ub_u32(a, 0, S, e) - 1); // may wrap to UINT32_MAX (:3999-4003)
         }
         ctl.i_last = dir == 0 ? 0 : (int)R - 1;
         ctl.failed = 0;
         ctl.done = 0;
         ctl.tab[0] = 0;
+    }
+    __syncthreads();
+    // slot-list offsets: LDS copy (prefix sum of mn) or the HBM arena
+    if (SLDS) {
+        uint32_t carry = 0;
+        for (uint32_t i0 = 0; i0 < R; i0 += PF_K3_THREADS) {
+            const uint32_t i = i0 + tid;
+            const uint32_t v = i < R ? m.mn[i] : 0;
+            uint32_t tot;
+            const uint32_t ex = block_excl_scan<PF_K3_THREADS>(v, sh_scan, &tot);
+            if (i < R) m.mo[i] = carry + ex;
+            carry += tot;
+        }
+        __syncthreads();
+        for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
+            const uint32_t g = 2 * (r0 + i) + dir;
+            const uint32_t *src = kb + (d.mmr_off[g] - kbase);
+            uint16_t *dst = m.sl16 + m.mo[i];
+            const uint32_t n = m.mn[i];
+            for (uint32_t t = lane; t < n; t += 64) {
+                const uint32_t v = src[t];
+                dst[t] = v == PF_NONE ? (uint16_t)0xFFFFu : (uint16_t)v;
+            }
+        }
+    } else {
+        for (uint32_t i = tid; i < R; i += PF_K3_THREADS)
+            m.mo[i] = (uint32_t)(d.mmr_off[2ull * (r0 + i) + dir] - kbase);
     }
     __syncthreads();
     // ---- reference reads seed the counts (insert_ref_reads_methmer_counts, :3776-3810)
@@ -926,13 +1063,12 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
         const uint32_t hp = m.hp[i];
         if (!(m.flg[i] & refbit) || hp > 1) continue;
-        const uint32_t n = m.mn[i], st = m.mst[i];
-        const uint32_t *kp = kb + m.mo[i];
+        const uint32_t n = m.mn[i], st = m.mst[i], mo = m.mo[i];
         const uint32_t inc = hp ? 0x10000u : 1u;
         ref_ins += n;
         for (uint32_t t = lane; t < n; t += 64) {
             const uint32_t site = st + t;
-            const uint32_t slot = kp[t];
+            const uint32_t slot = k3_slot<SLDS>(m, mo + t);
             if (site < S && slot != PF_NONE) {
                 atomicAdd(&m.cnt[slot], inc);
                 atomicAdd(&m.sum[site], inc);
@@ -942,6 +1078,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     if (lane == 0 && ref_ins) atomicAdd((uint32_t *)&ctl.tab[0], ref_ins);
     if (sum_mmr) atomicAdd(&ctl.summ, sum_mmr);
     __syncthreads();
+    for (uint32_t j = tid; j < S; j += PF_K3_THREADS) m.srec[j] = site_rec(m.sum[j]);
     if (wid == 0) k3_range_update(m.sum, S, cov_rt, ctl, lane);
     // ---- step 1.5 (:4010-4025): all reads unphased, ref reads restored through
     // the (readID<<2)|hp round trip (hp >= 4 lands on readID|(hp>>2)); the last
@@ -973,35 +1110,341 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     stx.inserts = ctl.tab[0];
     __syncthreads();
 
-    // ---- step 2: greedy extension, one read per iteration (:4032-4071)
-    // Barriers per iteration: (a) candidates ready, (b) records ready, (c) keys
-    // ready.  Winner pick, insertion, range update and the next candidate scan
-    // run in wavefront 0 between (c) and the next (a).
+    // ---- step 2: greedy extension, one read per iteration (:4032-4071), run by
+    // wavefront 0 alone (no workgroup barriers on the serial chain).  The
+    // candidate list is kept incrementally: after a tag it loses the winner and
+    // gains the next untagged read after its last entry -- exactly the
+    // reference's rescan from i_last, since tags never revert.
     K3_STAMP(0);
-    if (wid == 0) k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
+    if (wid != 0) return;
+    const uint32_t rec_cap = PF_K3_WAVES * m.rcw;
+    if (NC <= 64) {
+    // ---- register-resident variant (n_cand <= 64): lane c holds candidate c
+    // (scan position, read, methmer count/start/slot offset and the range-
+    // clipped lookup span); control state lives in scalars.
+    int il = ctl.i_last;
+    uint32_t failed = 0;
+    uint32_t umin = ctl.min_i, umax = ctl.max_i;
+    uint32_t nc = 0;
+    uint32_t c_pos = 0, c_rd = 0, c_n = 0, c_st = 0, c_mo = 0;
+    uint32_t c_lo = 0, c_len = 0, c_kofs = 0;
+    uint32_t lsum = 0;
+    bool need_collect = true;
     K3_STAMP(1);
     for (;;) {
-        __syncthreads();                                         // (a)
+        if (need_collect) {
+            // first NC untagged reads from i_last (:4037-4051); on an empty
+            // scan the failure counter advances and i_last moves by n_cand
+            bool done = false;
+            for (;;) {
+                if (dir == 0 ? il >= (int)R : il <= 0) { done = true; break; }
+                uint32_t found = 0;
+                int p = dir == 0 ? il - 1 : il + 1;
+                while (found < NC) {
+                    const int q = k3_next_untag(m.untag, nwords, p, dir, lane);
+                    if (q < 0) break;
+                    if (lane == found) c_pos = (uint32_t)q;
+                    found++;
+                    p = q;
+                }
+                if (found == 0) {
+                    stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+                    if (++failed > 10) { done = true; break; }
+                    il += dir == 0 ? (int)NC : -(int)NC;
+                    continue;
+                }
+                nc = found;
+                break;
+            }
+            if (done) break;
+            if (lane < nc) {
+                c_rd = dir ? m.ord[c_pos] : c_pos;
+                c_n = m.mn[c_rd]; c_st = m.mst[c_rd]; c_mo = m.mo[c_rd];
+            }
+            need_collect = false;
+            // span of query_counts_of_mmrs: sites in [min_i, max_i) (:3500-3501)
+            {
+                const uint64_t lo = c_st > umin ? c_st : umin;
+                const uint64_t hi0 = (uint64_t)c_st + c_n;
+                const uint64_t hi = hi0 < umax ? hi0 : umax;
+                c_len = lane < nc && hi > lo ? (uint32_t)(hi - lo) : 0;
+                c_lo = (uint32_t)lo;
+                c_kofs = c_mo + (c_len ? (uint32_t)(lo - c_st) : 0);
+                lsum += c_len;
+            }
+            if (nc >= NC) {
+                const uint32_t pl = rdl(c_pos, NC - 1);
+                stx.scanned += dir == 0 ? pl - (uint32_t)il + 1 : (uint32_t)il - pl + 1;
+            } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+            stx.iters++;
+        }
+        // the next untagged read after the last candidate (entries after it
+        // are untouched by this iteration's tag)
+        int qn = -1;
+        uint32_t q_rd = 0, q_n = 0, q_st = 0, q_mo = 0;
+        if (nc == NC) {
+            qn = k3_next_untag(m.untag, nwords, (int)rdl(c_pos, nc - 1), dir, lane);
+            if (qn >= 0) {
+                q_rd = dir ? m.ord[qn] : (uint32_t)qn;
+                q_n = m.mn[q_rd]; q_st = m.mst[q_rd]; q_mo = m.mo[q_rd];
+            }
+        }
         K3_STAMP(2);
-        if (ctl.done) break;
-        const uint32_t nc = ctl.nc;
-        const uint32_t L = ctl.L;
-        const uint32_t lc = m.rc >> lg;                           // t-steps per record chunk
+        // ---- fill: the value pair of every (candidate, methmer) lookup into
+        // per-candidate record rows; G = 64/ncp lanes per candidate take
+        // consecutive methmers.  The push/positive counts (integer, order-free)
+        // are summed in registers and reduced across the G lanes.
+        const uint32_t ncp = next_pow2(nc);
+        const uint32_t lgn = 31 - __clz(ncp);
+        const uint32_t G = 64u >> lgn;
+        const uint32_t fc = lane & (ncp - 1), fj = lane >> lgn;
+        const uint32_t f_lo = (uint32_t)__shfl((int)c_lo, (int)fc, 64);
+        const uint32_t f_len = (uint32_t)__shfl((int)c_len, (int)fc, 64);
+        const uint32_t f_kofs = (uint32_t)__shfl((int)c_kofs, (int)fc, 64);
+        const uint32_t lmax = wave_max_dpp(c_len);
+        const uint32_t P = (rec_cap >> lgn) & ~15u;              // row pitch (float2), 16 | P
+        // rows are zero-padded to a multiple of 8 terms so that the fold reads
+        // whole 8-term blocks (+0.0f leaves a non-negative sum unchanged)
+        const uint32_t lmaxp = (lmax + 7) & ~7u;
+        K3_COUNT(8, lmax);
+        K3_COUNT(9, nc);
+        K3_COUNT(10, (lmaxp + 8 * G - 1) / (8 * G));
+        const uint32_t f_lenp = (f_len + 7) & ~7u;
         float s0 = 0.f, s1 = 0.f;
         uint32_t lcode = 0;
-        for (uint32_t t0 = 0; t0 < L; t0 += lc) {
-            const uint32_t t1 = t0 + lc < L ? t0 + lc : L;
-            const uint32_t nrec = (t1 - t0) << lg;
-            for (uint32_t idx = tid; idx < nrec; idx += PF_K3_THREADS) {
-                const uint32_t t = t0 + (idx >> lg), c = idx & (ncp - 1);
+        for (uint32_t t0 = 0; t0 < lmaxp; t0 += P) {
+            const uint32_t tlim = lmaxp - t0 < P ? lmaxp - t0 : P;  // wave-uniform, 8 | tlim
+            const uint32_t tend = f_len < t0 + tlim ? f_len : t0 + tlim;
+            const uint32_t tpad = f_lenp < t0 + tlim ? f_lenp : t0 + tlim;
+            float2 *row = m.recv + fc * P - t0;
+            for (uint32_t tb = t0 + fj; tb < tpad; tb += 8 * G) {
+                // unconditional loads (out-of-span lanes read entry 0 and are
+                // masked afterwards) so that all eight rounds are in flight
+                uint32_t sl[8], cv[8];
+                float4 sr[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t t = tb + u * G;
+                    const bool ok = t < tend;
+                    sl[u] = k3_slot_raw<SLDS>(m, ok ? f_kofs + t : 0u);
+                    sr[u] = m.srec[ok ? f_lo + t : 0u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t t = tb + u * G;
+                    const bool ok = t < tend && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
+                    const uint32_t c = m.cnt[ok ? sl[u] : 0u];
+                    cv[u] = ok ? c : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t t = tb + u * G;
+                    const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
+                    // key present at this site (inserted at least once) and
+                    // sum != 0: pushed; cnt > 0: positive (:3505-3509, :3619-3624)
+                    const bool p0 = cv[u] != 0 && sr[u].z != 0.f, p1 = cv[u] != 0 && sr[u].w != 0.f;
+                    const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
+                    const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
+                    lcode += (p0 ? 1u + (a0 ? 1u : 0u) : 0u) + ((p1 ? 1u + (a1 ? 1u : 0u) : 0u) << 16);
+                    if (t < tpad) row[t] = make_float2(q0, q1);
+                }
+            }
+            wave_sync_mem();
+            K3_STAMP(3);
+            // the reference's sequential float sums (:3619-3636), one candidate
+            // per lane, 8-term blocks double-buffered
+            if (lane < nc) {
+                const uint32_t lp = (c_len + 7) & ~7u;
+                const uint32_t nt = lp > t0 ? (lp - t0 < tlim ? lp - t0 : tlim) : 0;
+                const float4 *rv4 = reinterpret_cast<const float4 *>(m.recv + lane * P);
+                const uint32_t nb = nt >> 3;
+                float4 A[4], B[4];
+                if (nb) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) A[u] = rv4[u];
+                }
+                for (uint32_t bk = 0; bk < nb; bk += 2) {
+                    if (bk + 1 < nb) {
+#pragma unroll
+                        for (int u = 0; u < 4; u++) B[u] = rv4[((bk + 1) << 2) + u];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) { s0 += A[u].x; s1 += A[u].y; s0 += A[u].z; s1 += A[u].w; }
+                    if (bk + 2 < nb) {
+#pragma unroll
+                        for (int u = 0; u < 4; u++) A[u] = rv4[((bk + 2) << 2) + u];
+                    }
+                    if (bk + 1 < nb) {
+#pragma unroll
+                        for (int u = 0; u < 4; u++) { s0 += B[u].x; s1 += B[u].y; s0 += B[u].z; s1 += B[u].w; }
+                    }
+                }
+            }
+            wave_sync_mem();
+            K3_STAMP(4);
+        }
+        for (uint32_t o = ncp; o < 64; o <<= 1) lcode += (uint32_t)__shfl_xor((int)lcode, (int)o, 64);
+        // use_mmr_count_predict_tag_for_one_read (:3637-3655) and the pick of
+        // predict_tags_of_reads (:3729-3766): max score, ties to the later
+        // candidate (stable merge sort walked from the end)
+        const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
+        const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
+        const bool elig = lane < nc && !(diff < 3.f && (l0 < 3 || l1 < 3));
+        const uint32_t hkey = elig ? __float_as_uint(diff) + 1u : 0u;
+        const uint32_t hmax = wave_max_dpp(hkey);
+        K3_STAMP(5);
+        if (hmax == 0) {
+            // nothing could be tagged (:4064-4069): move i_last, rescan
+            K3_STAMP(6);
+            if (++failed > 10) break;
+            il += dir == 0 ? (int)NC : -(int)NC;
+            need_collect = true;
+            K3_STAMP(7);
+            continue;
+        }
+        const uint64_t bal = __ballot(hkey == hmax);
+        const uint32_t cw = 63u - (uint32_t)__clzll((long long)bal);
+        const uint32_t tg = rdl(s0 > s1 ? 0u : 1u, cw);
+        const uint32_t rd = rdl(c_rd, cw), n = rdl(c_n, cw), st = rdl(c_st, cw), mo = rdl(c_mo, cw);
+        const uint32_t pw = rdl(c_pos, cw);
+        K3_STAMP(6);
+        const uint32_t inc = tg ? 0x10000u : 1u;
+        stx.inserts += n;
+        // the sites of one read are distinct: plain read-modify-write
+        for (uint32_t t = lane; t < n; t += 64) {
+            const uint32_t site = st + t;
+            const uint32_t slot = k3_slot<SLDS>(m, mo + t);
+            if (site < S && slot != PF_NONE) {
+                m.cnt[slot] += inc;
+                const uint32_t v = m.sum[site] + inc;
+                m.sum[site] = v;
+                m.srec[site] = site_rec(v);
+            }
+        }
+        if (lane == 0) {
+            m.hp[rd] = (uint8_t)tg;
+            m.untag[pw >> 6] &= ~(1ull << (pw & 63));
+        }
+        failed = 0;
+        // candidate list minus the winner, plus the prefetched next read
+        {
+            const int src = (int)lane + 1;
+            const uint32_t a0 = (uint32_t)__shfl((int)c_pos, src, 64), a1 = (uint32_t)__shfl((int)c_rd, src, 64);
+            const uint32_t a2 = (uint32_t)__shfl((int)c_n, src, 64), a3 = (uint32_t)__shfl((int)c_st, src, 64);
+            const uint32_t a4 = (uint32_t)__shfl((int)c_mo, src, 64);
+            if (lane >= cw) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; }
+        }
+        uint32_t ncn = nc - 1;
+        if (qn >= 0) {
+            if (lane == ncn) { c_pos = (uint32_t)qn; c_rd = q_rd; c_n = q_n; c_st = q_st; c_mo = q_mo; }
+            ncn++;
+        }
+        nc = ncn;
+        wave_sync();
+        // update_range (:3669-3704): both ends in one ballot, lanes 0-31 walk
+        // left from min_i, lanes 32-63 right from max_i
+        {
+            const int m0 = (int)umin, M0 = (int)umax;
+            const bool left = lane < 32;
+            const int i = left ? m0 - (int)lane : M0 + (int)(lane - 32);
+            bool cvg = false;
+            if (left ? (m0 >= 0 && i >= 0) : (M0 >= 0 && i < (int)S)) {
+                const uint32_t v = m.sum[i];
+                cvg = (int)((v & 0xffffu) + (v >> 16)) >= cov_rt;
+            }
+            const uint64_t b = __ballot(cvg);
+            const uint32_t bl = (uint32_t)b, br = (uint32_t)(b >> 32);
+            int cl = bl == ~0u ? 32 : __ffs(~bl) - 1;
+            int cr = br == ~0u ? 32 : __ffs(~br) - 1;
+            if (cl == 32) {
+                for (;;) {
+                    const int ii = m0 - cl - (int)lane;
+                    bool c2 = false;
+                    if (ii >= 0) { const uint32_t v = m.sum[ii]; c2 = (int)((v & 0xffffu) + (v >> 16)) >= cov_rt; }
+                    const uint64_t b2 = __ballot(c2);
+                    if (b2 == ~0ull) { cl += 64; continue; }
+                    cl += __ffsll((unsigned long long)~b2) - 1;
+                    break;
+                }
+            }
+            if (cr == 32) {
+                for (;;) {
+                    const int ii = M0 + cr + (int)lane;
+                    bool c2 = false;
+                    if (ii < (int)S) { const uint32_t v = m.sum[ii]; c2 = (int)((v & 0xffffu) + (v >> 16)) >= cov_rt; }
+                    const uint64_t b2 = __ballot(c2);
+                    if (b2 == ~0ull) { cr += 64; continue; }
+                    cr += __ffsll((unsigned long long)~b2) - 1;
+                    break;
+                }
+            }
+            if (m0 >= 0 && cl > 0) umin = (uint32_t)(m0 - cl + 1);
+            if (M0 >= 0 && cr > 0) umax = (uint32_t)(M0 + cr - 1);
+        }
+        if (nc == 0) {
+            // an empty batch: the failure path of the reference (:4046-4051)
+            need_collect = true;
+        } else {
+            const uint64_t lo = c_st > umin ? c_st : umin;
+            const uint64_t hi0 = (uint64_t)c_st + c_n;
+            const uint64_t hi = hi0 < umax ? hi0 : umax;
+            c_len = lane < nc && hi > lo ? (uint32_t)(hi - lo) : 0;
+            c_lo = (uint32_t)lo;
+            c_kofs = c_mo + (c_len ? (uint32_t)(lo - c_st) : 0);
+            lsum += c_len;
+            if (nc >= NC) {
+                const uint32_t pl = rdl(c_pos, NC - 1);
+                stx.scanned += dir == 0 ? pl - (uint32_t)il + 1 : (uint32_t)il - pl + 1;
+            } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+            stx.iters++;
+        }
+        K3_STAMP(7);
+    }
+    {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int bb = 0; bb < 32; bb++) tot += (uint32_t)__popcll(__ballot((lsum >> bb) & 1)) << bb;
+        stx.lookups += tot;
+    }
+    } else {
+    // ---- general variant (n_cand > 64): candidate list in LDS
+    k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
+    if (!ctl.done) {
+        k3_cand_fields(m, ctl.nc, dir, lane, ctl, cd, stx);
+        k3_scanned(ctl, cd, R, dir, NC, stx);
+    }
+    K3_STAMP(1);
+    while (!ctl.done) {
+        const uint32_t nc = ctl.nc;
+        const uint32_t ng = (nc + 63) >> 6;     // candidate groups of 64 lanes
+        uint32_t lmax = 0;
+        for (uint32_t g = 0; g < ng; g++) {
+            const uint32_t c = (g << 6) + lane;
+            const uint32_t l = c < nc ? cd.len[c] : 0u;
+            lmax = l > lmax ? l : lmax;
+        }
+        lmax = wave_max_u32(lmax);
+        // rows of `ch` records per candidate (power of two), chunked along t
+        uint32_t ch = next_pow2(lmax ? lmax : 1);
+        while (ch > 1 && ch * nc > rec_cap) ch >>= 1;
+        const uint32_t lgc = 31 - __clz(ch);
+        float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
+        uint32_t lcode[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t t0 = 0; t0 < lmax; t0 += ch) {
+            const uint32_t nrec = nc << lgc;
+            // records: value pair + push/positive code of (candidate c, methmer t0+tt)
+#pragma unroll 2
+            for (uint32_t idx = lane; idx < nrec; idx += 64) {
+                const uint32_t c = idx >> lgc, tt = idx & (ch - 1), t = t0 + tt;
                 float v0 = 0.f, v1 = 0.f;
                 uint32_t code = 0;
-                if (c < nc && t < cd.len[c]) {
+                const uint32_t len = cd.len[c];
+                if (t < len) {
                     const uint32_t site = cd.site0[c] + t;
-                    const uint32_t slot = kb[cd.kofs[c] + t];
+                    const uint32_t sv = m.sum[site];
+                    const uint32_t slot = k3_slot<SLDS>(m, cd.kofs[c] + t);
                     const uint32_t cv = slot != PF_NONE ? m.cnt[slot] : 0u;
                     if (cv != 0) {                               // key present at this site
-                        const uint32_t sv = m.sum[site];
                         const uint32_t h0 = sv & 0xffffu, h1 = sv >> 16;
                         if (h0) {
                             v0 = (float)(cv & 0xffffu) / (float)h0;
@@ -1016,113 +1459,177 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 m.recv[idx] = make_float2(v0, v1);
                 m.recc[idx] = code;
             }
+            wave_sync_mem();
             K3_STAMP(3);
-            __syncthreads();                                     // (b)
-            K3_STAMP(4);
-            if (tid < nc) {
-                // sequential in methmer order; absent terms are +0.0f and leave the
-                // float sum unchanged
-                const uint32_t n = t1 - t0;
-                const float2 *rv = m.recv + tid;
-                const uint32_t *rcc = m.recc + tid;
-                uint32_t t = 0;
-                for (; t + 8 <= n; t += 8) {
-                    float2 v[8];
-                    uint32_t cc[8];
+            // the reference's sequential float sums (:3619-3636), one candidate
+            // per lane; absent terms are +0.0f and leave the sum unchanged
+            const uint32_t n_t = lmax - t0 < ch ? lmax - t0 : ch;
 #pragma unroll
-                    for (int u = 0; u < 8; u++) { v[u] = rv[(t + u) << lg]; cc[u] = rcc[(t + u) << lg]; }
+            for (uint32_t g = 0; g < 4; g++) {
+                const uint32_t c = (g << 6) + lane;
+                if (g < ng && c < nc) {
+                    const float2 *rv = m.recv + (c << lgc);
+                    const uint32_t *rc = m.recc + (c << lgc);
+                    float a0 = s0[g], a1 = s1[g];
+                    uint32_t lc = lcode[g];
+                    uint32_t t = 0;
+                    for (; t + 8 <= n_t; t += 8) {
+                        float2 v[8];
+                        uint32_t cc[8];
 #pragma unroll
-                    for (int u = 0; u < 8; u++) { s0 += v[u].x; s1 += v[u].y; lcode += cc[u]; }
-                }
-                for (; t < n; t++) {
-                    const float2 v = rv[t << lg];
-                    s0 += v.x;
-                    s1 += v.y;
-                    lcode += rcc[t << lg];
-                }
-            }
-            if (t1 < L) __syncthreads();
-        }
-        // use_mmr_count_predict_tag_for_one_read (:3637-3655) + best pick (:3729-3766)
-        unsigned long long key = 0;
-        if (tid < nc) {
-            const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
-            const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
-            const bool untagged = diff < 3.f && (l0 < 3 || l1 < 3);
-            cd.tag[tid] = s0 > s1 ? 0 : 1;
-            if (!untagged) key = ((unsigned long long)__float_as_uint(diff) << 32) | (tid + 1);
-        }
-        key = wave_max_u64(key);
-        if (lane == 0) ctl.wbest[wid] = key;
-        K3_STAMP(5);
-        __syncthreads();                                         // (c)
-        K3_STAMP(6);
-        if (wid == 0) {
-            unsigned long long b = 0;
-            for (int i = 0; i < PF_K3_WAVES; i++) b = ctl.wbest[i] > b ? ctl.wbest[i] : b;
-            if (b == 0) {
-                // nothing could be tagged (:4064-4069)
-                const uint32_t f = ctl.failed + 1;
-                wave_sync();
-                if (lane == 0) {
-                    ctl.failed = f;
-                    if (f > 10) ctl.done = 1;
-                    else ctl.i_last += dir == 0 ? (int)NC : -(int)NC;
-                }
-                wave_sync();
-            } else {
-                const uint32_t c = (uint32_t)(b & 0xffffffffu) - 1;
-                const uint32_t rd = cd.read[c];
-                const uint32_t tg = cd.tag[c];
-                const uint32_t p = cd.pos[c];
-                const uint32_t n = m.mn[rd], st = m.mst[rd];
-                const uint32_t *kp = kb + m.mo[rd];
-                const uint32_t inc = tg ? 0x10000u : 1u;
-                stx.inserts += n;
-                // the sites of one read are distinct: plain read-modify-write
-                for (uint32_t t = lane; t < n; t += 64) {
-                    const uint32_t site = st + t;
-                    const uint32_t slot = kp[t];
-                    if (site < S && slot != PF_NONE) {
-                        m.cnt[slot] += inc;
-                        m.sum[site] += inc;
+                        for (int u = 0; u < 8; u++) { v[u] = rv[t + u]; cc[u] = rc[t + u]; }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) { a0 += v[u].x; a1 += v[u].y; lc += cc[u]; }
                     }
+                    for (; t < n_t; t++) {
+                        const float2 v = rv[t];
+                        a0 += v.x;
+                        a1 += v.y;
+                        lc += rc[t];
+                    }
+                    s0[g] = a0; s1[g] = a1; lcode[g] = lc;
                 }
-                if (lane == 0) {
-                    ctl.failed = 0;
-                    m.hp[rd] = (uint8_t)tg;
-                    m.untag[p >> 6] &= ~(1ull << (p & 63));
-                }
-                wave_sync();
-                k3_range_update(m.sum, S, cov_rt, ctl, lane);
             }
-            K3_STAMP(7);
-            if (!ctl.done) k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
-            K3_STAMP(1);
+            wave_sync_mem();
+            K3_STAMP(4);
         }
+        // use_mmr_count_predict_tag_for_one_read (:3637-3655); selection key
+        // (score, index): max wins, ties go to the later candidate = the stable
+        // merge sort + walk from the end of predict_tags_of_reads (:3729-3766)
+#pragma unroll
+        for (uint32_t g = 0; g < 4; g++) {
+            const uint32_t c = (g << 6) + lane;
+            if (g < ng && c < nc) {
+                const float diff = s0[g] > s1[g] ? s0[g] - s1[g] : s1[g] - s0[g];
+                const int l0 = (int)(lcode[g] & 0xffffu), l1 = (int)(lcode[g] >> 16);
+                const bool untagged = diff < 3.f && (l0 < 3 || l1 < 3);
+                cd.tag[c] = s0[g] > s1[g] ? 0 : 1;
+                cd.key[c] = untagged ? 0ull : (((unsigned long long)__float_as_uint(diff) << 32) | (c + 1));
+            }
+        }
+        wave_sync();
+        K3_STAMP(5);
+        unsigned long long b = 0;
+        {
+            uint32_t c = 0;
+            for (; c + 4 <= nc; c += 4) {
+                const unsigned long long k0 = cd.key[c], k1 = cd.key[c + 1], k2 = cd.key[c + 2], k3 = cd.key[c + 3];
+                const unsigned long long m01 = k0 > k1 ? k0 : k1, m23 = k2 > k3 ? k2 : k3;
+                const unsigned long long mm = m01 > m23 ? m01 : m23;
+                b = mm > b ? mm : b;
+            }
+            for (; c < nc; c++) { const unsigned long long k = cd.key[c]; b = k > b ? k : b; }
+        }
+        K3_STAMP(6);
+        if (b == 0) {
+            // nothing could be tagged (:4064-4069): move i_last, rescan
+            if (lane == 0) {
+                ctl.failed = ctl.failed + 1;
+                if (ctl.failed > 10) ctl.done = 1;
+                else ctl.i_last += dir == 0 ? (int)NC : -(int)NC;
+            }
+            wave_sync();
+            if (!ctl.done) {
+                k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
+                if (!ctl.done) {
+                    k3_cand_fields(m, ctl.nc, dir, lane, ctl, cd, stx);
+                    k3_scanned(ctl, cd, R, dir, NC, stx);
+                }
+            }
+        } else {
+            const uint32_t cw = (uint32_t)(b & 0xffffffffu) - 1;
+            const uint32_t rd = cd.read[cw];
+            const uint32_t tg = cd.tag[cw];
+            const uint32_t pw = cd.pos[cw];
+            const uint32_t n = m.mn[rd], st = m.mst[rd], mo = m.mo[rd];
+            const uint32_t inc = tg ? 0x10000u : 1u;
+            stx.inserts += n;
+            // the sites of one read are distinct: plain read-modify-write
+            for (uint32_t t = lane; t < n; t += 64) {
+                const uint32_t site = st + t;
+                const uint32_t slot = k3_slot<SLDS>(m, mo + t);
+                if (site < S && slot != PF_NONE) {
+                    m.cnt[slot] += inc;
+                    m.sum[site] += inc;
+                }
+            }
+            // candidate list minus the winner, plus the next untagged read after
+            // the last one when the list was full
+            const uint32_t last = cd.pos[nc - 1];
+            uint32_t pos_c = 0, read_c = 0;
+            for (uint32_t c0 = 0; c0 < nc; c0 += 64) {
+                const uint32_t c = c0 + lane;
+                if (c >= cw && c + 1 < nc) { pos_c = cd.pos[c + 1]; read_c = cd.read[c + 1]; }
+                wave_sync();
+                if (c >= cw && c + 1 < nc) { cd.pos[c] = pos_c; cd.read[c] = read_c; }
+                wave_sync();
+            }
+            if (lane == 0) {
+                ctl.failed = 0;
+                m.hp[rd] = (uint8_t)tg;
+                m.untag[pw >> 6] &= ~(1ull << (pw & 63));
+            }
+            wave_sync();
+            k3_range_update(m.sum, S, cov_rt, ctl, lane);
+            uint32_t ncn = nc - 1;
+            if (nc == NC) {
+                const int q = k3_next_untag(m.untag, nwords, (int)last, dir, lane);
+                if (q >= 0) {
+                    if (lane == 0) {
+                        cd.pos[ncn] = (uint32_t)q;
+                        cd.read[ncn] = dir ? m.ord[q] : (uint32_t)q;
+                    }
+                    ncn++;
+                }
+            }
+            if (lane == 0) ctl.nc = ncn;
+            wave_sync();
+            if (ncn == 0) {
+                // an empty batch: the failure path of the reference (:4046-4051)
+                k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
+                if (!ctl.done) {
+                    k3_cand_fields(m, ctl.nc, dir, lane, ctl, cd, stx);
+                    k3_scanned(ctl, cd, R, dir, NC, stx);
+                }
+            } else {
+                k3_cand_fields(m, ncn, dir, lane, ctl, cd, stx);
+                k3_scanned(ctl, cd, R, dir, NC, stx);
+            }
+        }
+        K3_STAMP(7);
+    }
     }
 
     // ---- 2x2 table on the opposite side's strict reads (evaluate_separation, :3940-3956)
-    if (tid < 4) ctl.tab[tid] = 0;
-    __syncthreads();
+    int tab0 = 0, tab1 = 0, tab2 = 0, tab3 = 0;
+    uint32_t nstrict = 0;
     const uint32_t strict = dir == 0 ? FLG_RIGHT_STRICT : FLG_LEFT_STRICT;
-    for (uint32_t i = tid; i < R; i += PF_K3_THREADS) {
+    for (uint32_t i = lane; i < R; i += 64) {
         if (m.flg[i] & strict) {
-            atomicAdd(&ctl.nstrict, 1u);
+            nstrict++;
             const uint32_t ref = d.read_hp[r0 + i], q = m.hp[i];
-            if (ref <= 1 && q <= 1) atomicAdd(&ctl.tab[ref * 2 + q], 1);
+            if (ref <= 1 && q <= 1) {
+                const uint32_t k = ref * 2 + q;
+                tab0 += k == 0; tab1 += k == 1; tab2 += k == 2; tab3 += k == 3;
+            }
         }
         if (dir == 0) d.hp_fwd[r0 + i] = m.hp[i];
     }
-    __syncthreads();
-    if (tid < 4) d.table[((uint64_t)w * 2 + dir) * 4 + tid] = ctl.tab[tid];
-    if (tid == 0) {
+    uint32_t tsum[5] = {(uint32_t)tab0, (uint32_t)tab1, (uint32_t)tab2, (uint32_t)tab3, nstrict};
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        uint32_t tot = 0;
+        for (int bb = 0; bb < 16; bb++) tot += (uint32_t)__popcll(__ballot((tsum[k] >> bb) & 1)) << bb;
+        tsum[k] = tot;
+    }
+    if (lane < 4) d.table[((uint64_t)w * 2 + dir) * 4 + lane] = (int32_t)tsum[lane];
+    if (lane == 0) {
         unsigned long long *sp = d.stats + ((uint64_t)w * 2 + dir) * PF_NSTAT;
         sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
-        sp[4] = ctl.summ; sp[5] = ctl.nstrict; sp[6] = R; sp[7] = S;
+        sp[4] = ctl.summ; sp[5] = tsum[4]; sp[6] = R; sp[7] = S;
 #ifdef PF_K3_PROFILE
-        unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 8;
-        for (int i = 0; i < 8; i++) pp[i] = prof_acc[i];
+        unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 16;
+        for (int i = 0; i < 16; i++) pp[i] = prof_acc[i];
 #endif
     }
 }
@@ -1143,8 +1650,7 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     const uint32_t R = d.win_nreads[w];
     const uint32_t r0 = d.win_read_off[w];
     const uint32_t MW = (uint32_t)d.mw;
-    const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
-    const uint32_t ncp = next_pow2(NC);
+    const uint64_t kbase = d.mmr_off[2ull * r0];
 
     // ---- P1: slot dictionary
     const uint64_t need1 = align16(8ull * S * MW) + 4ull * S;
@@ -1170,23 +1676,41 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
                        reinterpret_cast<uint32_t *>(g + align16(8ull * S * MW)), sh_scan, ctl);
     }
     const uint32_t ntot = ctl.ntot;
+    // sum of methmers over the window's reads (slot-list size)
+    uint32_t summ = 0;
+    for (uint32_t i = tid; i < R; i += PF_K3_THREADS) summ += d.mmr_n[2ull * (r0 + i) + dir];
+    uint32_t summ_tot;
+    block_excl_scan<PF_K3_THREADS>(summ, sh_scan, &summ_tot);
 
-    // ---- P2: greedy
+    // ---- P2: greedy.  Prefer everything in LDS (u16 slot lists), then LDS
+    // tables with slot lists read from the HBM arena, then all in HBM.
     uint64_t off[K3_NOFF];
-    const uint64_t fixed = k3_layout(S, ntot, R, dir, off);
-    const uint64_t min_rec = 12ull * ncp * 8;
-    const bool p2_lds = fixed + min_rec <= d.lds_bytes;
-    const uint32_t lgc = 31 - __clz(ncp);
-    if (p2_lds) {
-        uint32_t rc = (uint32_t)((d.lds_bytes - fixed) / 12);
-        rc = (rc >> lgc) << lgc;
-        if (rc > (ncp << 9)) rc = ncp << 9;
+    const uint32_t rcw_min = 256, rcw_max = 1024;
+    const bool slots_ok = ntot < 0xFFFFu;
+    uint64_t need_s = k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
+    uint64_t need_n = k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
+    const uint32_t *kb = d.keys + kbase;
+    if (slots_ok && need_s <= d.lds_bytes) {
+        uint64_t base_bytes = off[11];
+        (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
+        base_bytes = off[11];
+        uint32_t rcw = (uint32_t)((d.lds_bytes - base_bytes) / (12ull * PF_K3_WAVES));
+        rcw = rcw > rcw_max ? rcw_max : rcw;
+        (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw, off);
         K3Mem m;
-        k3_mem(smem, off, rc, m);
-        k3_greedy_body<true>(d, w, dir, r0, S, R, m, ctl, cd);
+        k3_mem(smem, off, rcw, true, kb, m);
+        k3_greedy_body<true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+    } else if (need_n <= d.lds_bytes) {
+        (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
+        uint32_t rcw = (uint32_t)((d.lds_bytes - off[11]) / (12ull * PF_K3_WAVES));
+        rcw = rcw > rcw_max ? rcw_max : rcw;
+        (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off);
+        K3Mem m;
+        k3_mem(smem, off, rcw, false, kb, m);
+        k3_greedy_body<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
     } else {
-        const uint32_t rc = ncp << 8;
-        const uint64_t need2 = align16(fixed + 12ull * rc);
+        const uint32_t rcw = rcw_min;
+        const uint64_t need2 = align16(k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off));
         __syncthreads();
         if (tid == 0) {
             const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)need2);
@@ -1197,7 +1721,20 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
         __syncthreads();
         if (ctl.fail) return;
         K3Mem m;
-        k3_mem(d.scr + ctl.scr, off, rc, m);
-        k3_greedy_body<false>(d, w, dir, r0, S, R, m, ctl, cd);
+        k3_mem(d.scr + ctl.scr, off, rcw, false, kb, m);
+        k3_greedy_body<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
     }
+}
+
+// ------------------------------------------------------------------------
+// self-test: div_u16 against the correctly rounded fp32 division over every
+// (a, b) with 0 <= a <= 65535, 1 <= b <= 65535 (block = one b)
+__global__ __launch_bounds__(256) void pf_selftest_div(unsigned long long *bad) {
+    const uint32_t b = blockIdx.x + 1;
+    uint32_t nb = 0;
+    for (uint32_t a = threadIdx.x; a < 65536u; a += 256) {
+        const float ref = (float)a / (float)b;
+        nb += __float_as_uint(div_u16(a, b)) != __float_as_uint(ref);
+    }
+    if (nb) atomicAdd(bad, (unsigned long long)nb);
 }

@@ -26,6 +26,13 @@ def _compare(ref, out, tag):
     np.testing.assert_allclose(out.dir_score, ref.dir_score, rtol=1e-6, atol=0, err_msg=tag)
 
 
+def test_division_selftest(gpu_ctx):
+    """The greedy kernel divides 16-bit counts with one Newton step on the
+    hardware reciprocal; it must equal correctly rounded fp32 division (the
+    reference's `(float)cnt/sum` of query_counts_of_mmrs, blockjoin.c:3508-3509) for every pair."""
+    assert gpu_ctx.selftest() == 0
+
+
 @pytest.mark.parametrize("name,cfg,batch", CASES, ids=[c[0] for c in CASES])
 def test_windows_parity(oracle_lib, gpu_ctx, name, cfg, batch):
     ref = oracle_lib.methphase(cfg, batch, n_threads=8)
@@ -103,3 +110,19 @@ def test_one_shot_api(oracle_lib):
     out = methphase_windows(cfg, b, device=0)
     ref = oracle_lib.methphase(cfg, b)
     _compare(ref, out, "oneshot")
+
+
+@pytest.mark.parametrize("lds", ["0", "20000"])
+def test_lds_budget_variants(oracle_lib, gpu_ctx, monkeypatch, lds):
+    """The greedy kernel's memory variants (tables and slot lists in LDS, tables
+    in LDS with slot lists in HBM, everything in the HBM scratch arena) give
+    the same bits; PF_K3_LDS caps the dynamic LDS a workgroup may take."""
+    from pomfret_amd import Config
+    monkeypatch.setenv("PF_K3_LDS", lds)
+    cfg = Config.from_coverage(30, given=False)
+    b = synth(8, 30, 41, gap_mix=True)
+    ref = oracle_lib.methphase(cfg, b, n_threads=8)
+    db = gpu_ctx.upload(cfg, b)
+    out = db.run()
+    _compare(ref, out, f"lds{lds}")
+    db.free()

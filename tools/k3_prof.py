@@ -12,7 +12,7 @@ L.LIB_PATH = os.path.join(os.path.dirname(L.LIB_PATH), "libpomfret_amd_prof.so")
 from pomfret_amd import Config, Context  # noqa: E402
 from pomfret_amd.synth import SynthSpec, make_batch  # noqa: E402
 
-names = ["init", "collect", "wait_a", "fill", "wait_b", "sum+key", "wait_c", "select+ins+range"]
+names = ["init", "setup", "prefetch", "fill", "fold", "keys", "pick", "tail"]
 for cov in (30, 60):
     cfg = Config.from_coverage(cov, given=False)
     b = make_batch(SynthSpec(n_windows=256, coverage=cov, seed=11))
@@ -21,12 +21,14 @@ for cov in (30, 60):
     db.run(); db.run()
     lib = L.lib()
     lib.pf_batch_prof.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
-    prof = np.zeros((256, 2, 8), np.uint64)
+    prof = np.zeros((256, 2, 16), np.uint64)
     lib.pf_batch_prof(db.handle, prof.ctypes.data, prof.size)
     st = db.stats()
-    tot = prof.sum(axis=(0, 1)).astype(float)
+    cnt = prof[:, :, 8:].sum(axis=(0, 1)).astype(float)
+    tot = prof[:, :, :8].sum(axis=(0, 1)).astype(float)
     iters = st[:, :, 2].sum()
     print(f"cov={cov} kernels={ctx.kernel_times()} iters={iters}")
     for n, v in zip(names, tot):
         print(f"  {n:18s} {v/tot.sum()*100:5.1f}%  {v/iters:8.0f} cyc/iter")
+    print(f"  per iter: lmax {cnt[0]/iters:.1f}  nc {cnt[1]/iters:.2f}  fill batches {cnt[2]/iters:.2f}")
     db.free(); ctx.close()
