@@ -208,10 +208,11 @@ int64_t pf_batch_debug_methmers(pf_dbatch_t *db, int dir, uint32_t *mmr_n,
 int  pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *known,
                      const pf_read_aln_batch_t *reads, uint8_t *hp_out);
 
-/* Device self-test of the arithmetic the kernels rely on for bit parity:
- * the greedy kernel's reciprocal-based division of 16-bit counts against the
- * correctly rounded fp32 division, over all 2^32 operand pairs.  Writes the
- * number of mismatching pairs (0 expected). */
+/* Device self-test of what the kernels rely on for bit parity: the greedy
+ * kernel's reciprocal-based division of 16-bit counts against the correctly
+ * rounded fp32 division over all 2^32 operand pairs, and the DPP/permlane
+ * wave scans and reductions against LDS references.  Writes the number of
+ * mismatches (0 expected). */
 int  pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches);
 
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of

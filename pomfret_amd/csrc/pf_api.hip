@@ -23,6 +23,7 @@ __global__ void pf_k1_sites(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
 __global__ void pf_selftest_div(unsigned long long *bad);
+__global__ void pf_selftest_wave(unsigned long long *bad);
 
 #define PF_NKERN 3
 static const char *k_names[PF_NKERN] = {"pf_k1_sites", "pf_k2_methmers", "pf_k3_greedy"};
@@ -106,6 +107,7 @@ extern "C" int pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches) {
     if (hipMemsetAsync(d, 0, sizeof(*d), ctx->stream) != hipSuccess) rc = PF_ERR_HIP;
     if (rc == PF_OK) {
         hipLaunchKernelGGL(pf_selftest_div, dim3(65535), dim3(256), 0, ctx->stream, d);
+        hipLaunchKernelGGL(pf_selftest_wave, dim3(1024), dim3(64), 0, ctx->stream, d);
         if (hipGetLastError() != hipSuccess) rc = PF_ERR_HIP;
     }
     if (rc == PF_OK && hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) rc = PF_ERR_HIP;

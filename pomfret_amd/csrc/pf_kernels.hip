@@ -125,6 +125,45 @@ DEV float4 site_rec(uint32_t v) {
     return make_float4(f0, f1, h0 ? __builtin_amdgcn_rcpf(f0) : 0.f, h1 ? __builtin_amdgcn_rcpf(f1) : 0.f);
 }
 
+// Inclusive wave prefix sum with DPP: row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast:15 / row_bcast:31 carry the row totals upwards.
+DEV uint32_t dpp_shr_add(uint32_t x, const int ctrl) {
+    uint32_t y;
+    switch (ctrl) {
+    case 1: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true); break;
+    case 2: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true); break;
+    case 4: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true); break;
+    case 8: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true); break;
+    case 15: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); break;
+    default: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); break;
+    }
+    return x + y;
+}
+DEV uint32_t wave_incl_scan_dpp(uint32_t x) {
+    x = dpp_shr_add(x, 1);
+    x = dpp_shr_add(x, 2);
+    x = dpp_shr_add(x, 4);
+    x = dpp_shr_add(x, 8);
+    x = dpp_shr_add(x, 15);
+    x = dpp_shr_add(x, 31);
+    return x;
+}
+// Sum over the lanes congruent modulo ncp (a power of two): row rotations for
+// strides below 16, the gfx950 permlane16/32 swaps for 16 and 32.
+template <int N>
+DEV uint32_t ror_add(uint32_t x) {
+    return x + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x120 + N, 0xF, 0xF, false);
+}
+DEV uint32_t wave_group_sum(uint32_t x, uint32_t ncp) {
+    if (ncp < 2) x = ror_add<1>(x);
+    if (ncp < 4) x = ror_add<2>(x);
+    if (ncp < 8) x = ror_add<4>(x);
+    if (ncp < 16) x = ror_add<8>(x);
+    if (ncp < 32) { const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false); x = r[0] + r[1]; }
+    if (ncp < 64) { const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false); x = r[0] + r[1]; }
+    return x;
+}
+
 DEV uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
 
 DEV uint64_t wave_max_u64(uint64_t x) {
@@ -871,6 +910,67 @@ DEV int k3_next_untag(const uint64_t *untag, uint32_t nwords, int p, uint32_t di
     }
 }
 
+// Candidate queue of the register variant: the untagged reads that follow
+// position p in scan order (dir 0: > p, dir 1: < p), up to 64, lane k holding
+// entry k with its read and methmer fields.  Reads after the last candidate
+// are untouched until they join the list, so one build serves up to 64
+// appends.  `cont` is where a further build continues; `more` whether
+// anything may lie beyond.
+DEV uint32_t k3_qbuild(const K3Mem &m, uint32_t nwords, int p, uint32_t dir, uint32_t lane, uint32_t *qbuf,
+                       uint32_t &q_pos, uint32_t &q_rd, uint32_t &q_n, uint32_t &q_st, uint32_t &q_mo,
+                       bool &more, int &cont) {
+    uint64_t bits = 0;
+    int wi, w0;
+    bool more_words;
+    if (dir == 0) {
+        const int q = p + 1;
+        if (q >= (int)(nwords * 64)) { more = false; return 0; }
+        w0 = q >> 6;
+        wi = w0 + (int)lane;
+        if (wi < (int)nwords) {
+            bits = m.untag[wi];
+            if (wi == w0) bits &= ~0ull << (q & 63);
+        }
+        more_words = w0 + 64 < (int)nwords;
+    } else {
+        const int q = p - 1;
+        if (q < 0) { more = false; return 0; }
+        w0 = q >> 6;
+        wi = w0 - (int)lane;
+        if (wi >= 0) {
+            bits = m.untag[wi];
+            if (wi == w0) {
+                const uint32_t b = (uint32_t)q & 63;
+                bits &= b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
+            }
+        }
+        more_words = w0 - 64 >= 0;
+    }
+    const uint32_t pc = (uint32_t)__popcll(bits);
+    const uint32_t incl = wave_incl_scan_dpp(pc);
+    const uint32_t tot = rdl(incl, 63);
+    uint32_t k = incl - pc;
+    while (bits != 0 && k < 64) {
+        const int b = dir == 0 ? __ffsll((unsigned long long)bits) - 1 : 63 - __clzll((long long)bits);
+        qbuf[k++] = (uint32_t)(wi * 64 + b);
+        bits &= ~(1ull << b);
+    }
+    wave_sync();
+    const uint32_t cnt = tot < 64 ? tot : 64;
+    if (lane < cnt) {
+        q_pos = qbuf[lane];
+        q_rd = dir ? m.ord[q_pos] : q_pos;
+        q_n = m.mn[q_rd];
+        q_st = m.mst[q_rd];
+        q_mo = m.mo[q_rd];
+    }
+    if (tot > 64) cont = (int)qbuf[63];
+    else cont = dir == 0 ? (w0 + 64) * 64 - 1 : (w0 - 63) * 64;
+    more = tot > 64 || more_words;
+    wave_sync();
+    return cnt;
+}
+
 // per-candidate derived fields for the current range (query_counts_of_mmrs
 // only uses sites in [min_i, max_i), blockjoin.c:3500-3501); one wavefront.
 DEV void k3_cand_fields(const K3Mem &m, uint32_t nc, uint32_t dir, uint32_t lane, const K3Ctl &ctl,
@@ -1116,7 +1216,6 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     // gains the next untagged read after its last entry -- exactly the
     // reference's rescan from i_last, since tags never revert.
     K3_STAMP(0);
-    if (wid != 0) return;
     const uint32_t rec_cap = PF_K3_WAVES * m.rcw;
     if (NC <= 64) {
     // ---- register-resident variant (n_cand <= 64): lane c holds candidate c
@@ -1128,24 +1227,43 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     uint32_t nc = 0;
     uint32_t c_pos = 0, c_rd = 0, c_n = 0, c_st = 0, c_mo = 0;
     uint32_t c_lo = 0, c_len = 0, c_kofs = 0;
+    uint32_t q_pos = 0, q_rd = 0, q_nn = 0, q_st = 0, q_mo = 0;
+    uint32_t q_cnt = 0, q_head = 0;
+    bool q_more = false;
+    int q_cont = 0;
+    uint32_t *qbuf = cd.read;
     uint32_t lsum = 0;
-    bool need_collect = true;
+    bool need_collect = true, stop = false;
+    int qn = -1;
+    uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
+    uint32_t *lcp = reinterpret_cast<uint32_t *>(cd.key);    // per-wave push/positive partials
     K3_STAMP(1);
     for (;;) {
-        if (need_collect) {
-            // first NC untagged reads from i_last (:4037-4051); on an empty
-            // scan the failure counter advances and i_last moves by n_cand
+    // wavefront 0: candidate list upkeep, then publish the lookup spans
+    if (wid == 0) {
+        if (!stop && need_collect) {
             bool done = false;
             for (;;) {
                 if (dir == 0 ? il >= (int)R : il <= 0) { done = true; break; }
-                uint32_t found = 0;
-                int p = dir == 0 ? il - 1 : il + 1;
-                while (found < NC) {
-                    const int q = k3_next_untag(m.untag, nwords, p, dir, lane);
-                    if (q < 0) break;
-                    if (lane == found) c_pos = (uint32_t)q;
-                    found++;
-                    p = q;
+                q_cnt = k3_qbuild(m, nwords, dir == 0 ? il - 1 : il + 1, dir, lane, qbuf,
+                                  q_pos, q_rd, q_nn, q_st, q_mo, q_more, q_cont);
+                const uint32_t take = q_cnt < NC ? q_cnt : NC;
+                c_pos = q_pos; c_rd = q_rd; c_n = q_nn; c_st = q_st; c_mo = q_mo;
+                q_head = take;
+                uint32_t found = take;
+                while (found < NC && q_more) {
+                    // fewer than n_cand untagged reads in the first 4096 scan
+                    // positions: continue the scan entry by entry
+                    q_cnt = k3_qbuild(m, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
+                                      q_more, q_cont);
+                    q_head = 0;
+                    while (found < NC && q_head < q_cnt) {
+                        const uint32_t a0 = rdl(q_pos, q_head), a1 = rdl(q_rd, q_head), a2 = rdl(q_nn, q_head);
+                        const uint32_t a3 = rdl(q_st, q_head), a4 = rdl(q_mo, q_head);
+                        if (lane == found) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; }
+                        found++;
+                        q_head++;
+                    }
                 }
                 if (found == 0) {
                     stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
@@ -1156,11 +1274,9 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 nc = found;
                 break;
             }
-            if (done) break;
-            if (lane < nc) {
-                c_rd = dir ? m.ord[c_pos] : c_pos;
-                c_n = m.mn[c_rd]; c_st = m.mst[c_rd]; c_mo = m.mo[c_rd];
-            }
+            if (done) stop = true;
+        }
+        if (!stop && need_collect) {
             need_collect = false;
             // span of query_counts_of_mmrs: sites in [min_i, max_i) (:3500-3501)
             {
@@ -1178,67 +1294,85 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
             stx.iters++;
         }
-        // the next untagged read after the last candidate (entries after it
-        // are untouched by this iteration's tag)
-        int qn = -1;
-        uint32_t q_rd = 0, q_n = 0, q_st = 0, q_mo = 0;
-        if (nc == NC) {
-            qn = k3_next_untag(m.untag, nwords, (int)rdl(c_pos, nc - 1), dir, lane);
-            if (qn >= 0) {
-                q_rd = dir ? m.ord[qn] : (uint32_t)qn;
-                q_n = m.mn[q_rd]; q_st = m.mst[q_rd]; q_mo = m.mo[q_rd];
+        // the next untagged read after the last candidate, from the queue
+        qn = -1;
+        if (!stop && nc == NC) {
+            if (q_head == q_cnt && q_more) {
+                q_cnt = k3_qbuild(m, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
+                                  q_more, q_cont);
+                q_head = 0;
+            }
+            if (q_head < q_cnt) {
+                qn = (int)rdl(q_pos, q_head);
+                q_rd1 = rdl(q_rd, q_head); q_n1 = rdl(q_nn, q_head);
+                q_st1 = rdl(q_st, q_head); q_mo1 = rdl(q_mo, q_head);
+                q_head++;
             }
         }
+        const uint32_t lmax0 = stop ? 0u : wave_max_dpp(c_len);
+        cd.site0[lane] = c_lo;
+        cd.len[lane] = c_len;
+        cd.kofs[lane] = c_kofs;
+        if (lane == 0) { ctl.done = stop ? 1u : 0u; ctl.nc = nc; ctl.L = lmax0; }
         K3_STAMP(2);
-        // ---- fill: the value pair of every (candidate, methmer) lookup into
-        // per-candidate record rows; G = 64/ncp lanes per candidate take
-        // consecutive methmers.  The push/positive counts (integer, order-free)
-        // are summed in registers and reduced across the G lanes.
-        const uint32_t ncp = next_pow2(nc);
+    }
+    __syncthreads();                                           // (A)
+    if (ctl.done) break;
+    {
+        // ---- fill, all four waves: the value pair of every (candidate,
+        // methmer) lookup into per-candidate record rows; G = 64/ncp lanes of
+        // each wave per candidate, the waves interleaved along the methmers.
+        // The push/positive counts (integer, order-free) are summed in
+        // registers, reduced across lanes and waves.
+        const uint32_t ncs = ctl.nc, lmax = ctl.L;
+        const uint32_t ncp = next_pow2(ncs);
         const uint32_t lgn = 31 - __clz(ncp);
         const uint32_t G = 64u >> lgn;
         const uint32_t fc = lane & (ncp - 1), fj = lane >> lgn;
-        const uint32_t f_lo = (uint32_t)__shfl((int)c_lo, (int)fc, 64);
-        const uint32_t f_len = (uint32_t)__shfl((int)c_len, (int)fc, 64);
-        const uint32_t f_kofs = (uint32_t)__shfl((int)c_kofs, (int)fc, 64);
-        const uint32_t lmax = wave_max_dpp(c_len);
-        const uint32_t P = (rec_cap >> lgn) & ~15u;              // row pitch (float2), 16 | P
+        const uint32_t J = wid * G + fj, GS = PF_K3_WAVES * G;
+        const uint32_t f_lo = cd.site0[fc], f_len = cd.len[fc], f_kofs = cd.kofs[fc];
+        // row pitch P (float2) = 4 mod 32: the fold's 16-byte row reads of up
+        // to 8 candidates and the fill's 8-lane row segments spread over the
+        // LDS banks; chunks of CHK (8 | CHK) terms
+        const uint32_t cap = rec_cap >> lgn;
+        const uint32_t P = cap >= 36 ? ((cap - 4) & ~31u) + 4 : (cap & ~7u);
+        const uint32_t CHK = P & ~7u;
         // rows are zero-padded to a multiple of 8 terms so that the fold reads
         // whole 8-term blocks (+0.0f leaves a non-negative sum unchanged)
         const uint32_t lmaxp = (lmax + 7) & ~7u;
         K3_COUNT(8, lmax);
-        K3_COUNT(9, nc);
-        K3_COUNT(10, (lmaxp + 8 * G - 1) / (8 * G));
+        K3_COUNT(9, ncs);
+        K3_COUNT(10, (lmaxp + 4 * GS - 1) / (4 * GS));
         const uint32_t f_lenp = (f_len + 7) & ~7u;
         float s0 = 0.f, s1 = 0.f;
         uint32_t lcode = 0;
-        for (uint32_t t0 = 0; t0 < lmaxp; t0 += P) {
-            const uint32_t tlim = lmaxp - t0 < P ? lmaxp - t0 : P;  // wave-uniform, 8 | tlim
+        for (uint32_t t0 = 0; t0 < lmaxp; t0 += CHK) {
+            const uint32_t tlim = lmaxp - t0 < CHK ? lmaxp - t0 : CHK;  // wave-uniform, 8 | tlim
             const uint32_t tend = f_len < t0 + tlim ? f_len : t0 + tlim;
             const uint32_t tpad = f_lenp < t0 + tlim ? f_lenp : t0 + tlim;
             float2 *row = m.recv + fc * P - t0;
-            for (uint32_t tb = t0 + fj; tb < tpad; tb += 8 * G) {
+            for (uint32_t tb = t0 + J; tb < tpad; tb += 4 * GS) {
                 // unconditional loads (out-of-span lanes read entry 0 and are
-                // masked afterwards) so that all eight rounds are in flight
-                uint32_t sl[8], cv[8];
-                float4 sr[8];
+                // masked afterwards) so that all four rounds are in flight
+                uint32_t sl[4], cv[4];
+                float4 sr[4];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const uint32_t t = tb + u * G;
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t t = tb + u * GS;
                     const bool ok = t < tend;
                     sl[u] = k3_slot_raw<SLDS>(m, ok ? f_kofs + t : 0u);
                     sr[u] = m.srec[ok ? f_lo + t : 0u];
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const uint32_t t = tb + u * G;
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t t = tb + u * GS;
                     const bool ok = t < tend && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
                     const uint32_t c = m.cnt[ok ? sl[u] : 0u];
                     cv[u] = ok ? c : 0u;
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    const uint32_t t = tb + u * G;
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t t = tb + u * GS;
                     const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
                     // key present at this site (inserted at least once) and
                     // sum != 0: pushed; cnt > 0: positive (:3505-3509, :3619-3624)
@@ -1249,11 +1383,16 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                     if (t < tpad) row[t] = make_float2(q0, q1);
                 }
             }
-            wave_sync_mem();
+            const bool last_chunk = t0 + CHK >= lmaxp;
+            if (last_chunk) {
+                const uint32_t lc = wave_group_sum(lcode, ncp);
+                if (lane < ncp) lcp[wid * 64 + lane] = lc;
+            }
+            __syncthreads();                                   // (B)
             K3_STAMP(3);
             // the reference's sequential float sums (:3619-3636), one candidate
-            // per lane, 8-term blocks double-buffered
-            if (lane < nc) {
+            // per lane of wavefront 0, 8-term blocks double-buffered
+            if (wid == 0 && lane < ncs) {
                 const uint32_t lp = (c_len + 7) & ~7u;
                 const uint32_t nt = lp > t0 ? (lp - t0 < tlim ? lp - t0 : tlim) : 0;
                 const float4 *rv4 = reinterpret_cast<const float4 *>(m.recv + lane * P);
@@ -1280,10 +1419,11 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                     }
                 }
             }
-            wave_sync_mem();
+            if (!last_chunk) __syncthreads();                  // rows reused by the next chunk
             K3_STAMP(4);
         }
-        for (uint32_t o = ncp; o < 64; o <<= 1) lcode += (uint32_t)__shfl_xor((int)lcode, (int)o, 64);
+        if (wid != 0) continue;
+        lcode = lcp[lane] + lcp[64 + lane] + lcp[128 + lane] + lcp[192 + lane];
         // use_mmr_count_predict_tag_for_one_read (:3637-3655) and the pick of
         // predict_tags_of_reads (:3729-3766): max score, ties to the later
         // candidate (stable merge sort walked from the end)
@@ -1296,9 +1436,11 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         if (hmax == 0) {
             // nothing could be tagged (:4064-4069): move i_last, rescan
             K3_STAMP(6);
-            if (++failed > 10) break;
-            il += dir == 0 ? (int)NC : -(int)NC;
-            need_collect = true;
+            if (++failed > 10) stop = true;
+            else {
+                il += dir == 0 ? (int)NC : -(int)NC;
+                need_collect = true;
+            }
             K3_STAMP(7);
             continue;
         }
@@ -1310,15 +1452,32 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         K3_STAMP(6);
         const uint32_t inc = tg ? 0x10000u : 1u;
         stx.inserts += n;
-        // the sites of one read are distinct: plain read-modify-write
-        for (uint32_t t = lane; t < n; t += 64) {
-            const uint32_t site = st + t;
-            const uint32_t slot = k3_slot<SLDS>(m, mo + t);
-            if (site < S && slot != PF_NONE) {
-                m.cnt[slot] += inc;
-                const uint32_t v = m.sum[site] + inc;
-                m.sum[site] = v;
-                m.srec[site] = site_rec(v);
+        // the sites of one read are distinct: plain read-modify-write, four
+        // rounds of loads in flight
+        for (uint32_t tb = 0; tb < n; tb += 256) {
+            uint32_t sl[4], cc[4], sv[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t t = tb + u * 64 + lane;
+                ok[u] = t < n && st + t < S;
+                sl[u] = k3_slot_raw<SLDS>(m, ok[u] ? mo + t : 0u);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t t = tb + u * 64 + lane;
+                ok[u] = ok[u] && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
+                cc[u] = m.cnt[ok[u] ? sl[u] : 0u];
+                sv[u] = m.sum[ok[u] ? st + t : 0u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (ok[u]) {
+                    const uint32_t site = st + tb + u * 64 + lane;
+                    m.cnt[sl[u]] = cc[u] + inc;
+                    m.sum[site] = sv[u] + inc;
+                    m.srec[site] = site_rec(sv[u] + inc);
+                }
             }
         }
         if (lane == 0) {
@@ -1336,7 +1495,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         }
         uint32_t ncn = nc - 1;
         if (qn >= 0) {
-            if (lane == ncn) { c_pos = (uint32_t)qn; c_rd = q_rd; c_n = q_n; c_st = q_st; c_mo = q_mo; }
+            if (lane == ncn) { c_pos = (uint32_t)qn; c_rd = q_rd1; c_n = q_n1; c_st = q_st1; c_mo = q_mo1; }
             ncn++;
         }
         nc = ncn;
@@ -1400,6 +1559,8 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         }
         K3_STAMP(7);
     }
+    }
+    if (wid != 0) return;
     {
         uint32_t tot = 0;
 #pragma unroll
@@ -1407,7 +1568,8 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         stx.lookups += tot;
     }
     } else {
-    // ---- general variant (n_cand > 64): candidate list in LDS
+    // ---- general variant (n_cand > 64): candidate list in LDS, wavefront 0
+    if (wid != 0) return;
     k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
     if (!ctl.done) {
         k3_cand_fields(m, ctl.nc, dir, lane, ctl, cd, stx);
@@ -1735,6 +1897,31 @@ __global__ __launch_bounds__(256) void pf_selftest_div(unsigned long long *bad) 
     for (uint32_t a = threadIdx.x; a < 65536u; a += 256) {
         const float ref = (float)a / (float)b;
         nb += __float_as_uint(div_u16(a, b)) != __float_as_uint(ref);
+    }
+    if (nb) atomicAdd(bad, (unsigned long long)nb);
+}
+
+// self-test of the DPP / permlane wave primitives against LDS references
+__global__ __launch_bounds__(64) void pf_selftest_wave(unsigned long long *bad) {
+    __shared__ uint32_t v[64];
+    const uint32_t lane = threadIdx.x;
+    uint32_t h = (blockIdx.x * 64 + lane) * 2654435761u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    const uint32_t x = blockIdx.x & 1 ? (h & 0xffffu) : (h & 7u);
+    v[lane] = x;
+    __syncthreads();
+    uint32_t nb = 0;
+    uint32_t ref = 0, mx = 0;
+    for (uint32_t i = 0; i <= lane; i++) ref += v[i];
+    for (uint32_t i = 0; i < 64; i++) mx = v[i] > mx ? v[i] : mx;
+    nb += wave_incl_scan_dpp(x) != ref;
+    nb += wave_max_dpp(x) != mx;
+    for (uint32_t ncp = 1; ncp <= 64; ncp <<= 1) {
+        uint32_t gs = 0;
+        for (uint32_t i = lane & (ncp - 1); i < 64; i += ncp) gs += v[i];
+        nb += wave_group_sum(x, ncp) != gs;
     }
     if (nb) atomicAdd(bad, (unsigned long long)nb);
 }

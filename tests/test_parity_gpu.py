@@ -29,7 +29,8 @@ def _compare(ref, out, tag):
 def test_division_selftest(gpu_ctx):
     """The greedy kernel divides 16-bit counts with one Newton step on the
     hardware reciprocal; it must equal correctly rounded fp32 division (the
-    reference's `(float)cnt/sum` of query_counts_of_mmrs, blockjoin.c:3508-3509) for every pair."""
+    reference's `(float)cnt/sum` of query_counts_of_mmrs, blockjoin.c:3508-3509) for every pair.
+    The DPP/permlane wave scans and group sums are checked in the same call."""
     assert gpu_ctx.selftest() == 0
 
 

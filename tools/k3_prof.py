@@ -30,5 +30,14 @@ for cov in (30, 60):
     print(f"cov={cov} kernels={ctx.kernel_times()} iters={iters}")
     for n, v in zip(names, tot):
         print(f"  {n:18s} {v/tot.sum()*100:5.1f}%  {v/iters:8.0f} cyc/iter")
+    per = prof[:, :, :8].sum(axis=2).astype(float).ravel()
+    it = st[:, :, 2].astype(float).ravel()
+    top = np.argsort(per)[::-1][:6]
+    print("  top problems (w,dir): cycles, iters, init cycles, reads, sites, lookups/iter")
+    for i in top:
+        w, d = divmod(int(i), 2)
+        print(f"    ({w},{d}) {per[i]:.3g} {it[i]:.0f} {float(prof[w, d, 0]):.3g} {st[w, d, 6]} {st[w, d, 7]} "
+              f"{st[w, d, 0] / max(it[i], 1):.0f}")
+    print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
     print(f"  per iter: lmax {cnt[0]/iters:.1f}  nc {cnt[1]/iters:.2f}  fill batches {cnt[2]/iters:.2f}")
     db.free(); ctx.close()
