@@ -692,7 +692,7 @@ __global__ __launch_bounds__(PF_K2_WAVES * 64) void pf_k2_methmers(pf_dev_batch 
 struct K3Ctl {
     uint32_t S, R, ntot, nc, L, done, failed, inserted, winner, tag;
     int32_t i_last;
-    uint32_t min_i, max_i, fail, summ, nstrict;
+    uint32_t min_i, max_i, fail, summ, nstrict, mxlen;
     unsigned long long scr;
     int32_t tab[4];
 };
@@ -1073,6 +1073,62 @@ DEV uint32_t k3_slot(const K3Mem &m, uint32_t off) {
     return m.kb[off];
 }
 
+// Fill of one lane's record-row entries t = tstart, tstart+step, ... < tpad
+// (entries t >= tend are written as zero); returns the lane's push/positive
+// count pair.  Four rounds of loads in flight.
+template <bool SLDS>
+DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32_t tstart, uint32_t tend,
+                          uint32_t tpad, uint32_t step, float2 *row) {
+    uint32_t lcode = 0;
+    for (uint32_t tb = tstart; tb < tpad; tb += 4 * step) {
+        // unconditional loads (out-of-span lanes read entry 0 and are masked
+        // afterwards)
+        uint32_t sl[4], cv[4];
+        float4 sr[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + u * step;
+            const bool ok = t < tend;
+            sl[u] = k3_slot_raw<SLDS>(m, ok ? f_kofs + t : 0u);
+            sr[u] = m.srec[ok ? f_lo + t : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + u * step;
+            const bool ok = t < tend && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
+            const uint32_t c = m.cnt[ok ? sl[u] : 0u];
+            cv[u] = ok ? c : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + u * step;
+            const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
+            // key present at this site (inserted at least once) and sum != 0:
+            // pushed; cnt > 0: positive (blockjoin.c:3505-3509, :3619-3624)
+            const bool p0 = cv[u] != 0 && sr[u].z != 0.f, p1 = cv[u] != 0 && sr[u].w != 0.f;
+            const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
+            const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
+            lcode += (p0 ? 1u + (a0 ? 1u : 0u) : 0u) + ((p1 ? 1u + (a1 ? 1u : 0u) : 0u) << 16);
+            if (t < tpad) row[t] = make_float2(q0, q1);
+        }
+    }
+    return lcode;
+}
+
+// The reference's sequential float sums (blockjoin.c:3619-3636) over one
+// record row, nb blocks of 32 terms (zero padded)
+DEV void k3_fold32(const float2 *rv, uint32_t nb, float &s0, float &s1) {
+    const float4 *r4 = reinterpret_cast<const float4 *>(rv);
+#pragma unroll 2
+    for (uint32_t b = 0; b < nb; b++) {
+        float4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = r4[b * 16 + u];
+#pragma unroll
+        for (int u = 0; u < 16; u++) { s0 += v[u].x; s1 += v[u].y; s0 += v[u].z; s1 += v[u].w; }
+    }
+}
+
 template <bool SLDS>
 DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S,
                         uint32_t R, const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
@@ -1086,7 +1142,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     const uint64_t kbase = d.mmr_off[2ull * r0];
     const uint32_t *kb = d.keys + kbase;
     K3Stats stx = {0, 0, 0, 0};
-    uint32_t sum_mmr = 0;
+    uint32_t sum_mmr = 0, mx_mmr = 0;
 #ifdef PF_K3_PROFILE
     unsigned long long prof_acc[16] = {0};
     unsigned long long prof_last = __builtin_amdgcn_s_memtime();
@@ -1114,6 +1170,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         m.mn[i] = d.mmr_n[g];
         m.mst[i] = d.mmr_start[g];
         sum_mmr += m.mn[i];
+        mx_mmr = m.mn[i] > mx_mmr ? m.mn[i] : mx_mmr;
     }
     if (tid == 0) {
         const uint32_t *a = d.site_pos + sb;
@@ -1177,6 +1234,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     }
     if (lane == 0 && ref_ins) atomicAdd((uint32_t *)&ctl.tab[0], ref_ins);
     if (sum_mmr) atomicAdd(&ctl.summ, sum_mmr);
+    if (mx_mmr) atomicMax(&ctl.mxlen, mx_mmr);
     __syncthreads();
     for (uint32_t j = tid; j < S; j += PF_K3_THREADS) m.srec[j] = site_rec(m.sum[j]);
     if (wid == 0) k3_range_update(m.sum, S, cov_rt, ctl, lane);
@@ -1233,6 +1291,17 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     int q_cont = 0;
     uint32_t *qbuf = cd.read;
     uint32_t lsum = 0;
+    // one chunk per iteration when a row can hold the longest methmer list
+    // of the window, zero-padded to 32 terms (pitch = 4 mod 32 for the banks)
+    // (the register variant keeps no push codes, so the whole 12-byte record
+    // region holds float2 terms)
+    const uint32_t rec2 = (uint32_t)((12ull * PF_K3_WAVES * m.rcw) >> 3);
+    const uint32_t L32 = (ctl.mxlen + 31) & ~31u;
+    const uint32_t P1 = L32 + 4;
+    const bool one_chunk = P1 <= (rec2 >> (31 - __clz(next_pow2(NC))));
+    K3_COUNT(11, one_chunk ? 1 : 0);
+    K3_COUNT(12, m.rcw);
+    K3_COUNT(13, ctl.mxlen);
     bool need_collect = true, stop = false;
     int qn = -1;
     uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
@@ -1309,7 +1378,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 q_head++;
             }
         }
-        const uint32_t lmax0 = stop ? 0u : wave_max_dpp(c_len);
+        const uint32_t lmax0 = stop || one_chunk ? 0u : wave_max_dpp(c_len);
         cd.site0[lane] = c_lo;
         cd.len[lane] = c_len;
         cd.kofs[lane] = c_kofs;
@@ -1324,13 +1393,29 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // each wave per candidate, the waves interleaved along the methmers.
         // The push/positive counts (integer, order-free) are summed in
         // registers, reduced across lanes and waves.
-        const uint32_t ncs = ctl.nc, lmax = ctl.L;
+        const uint32_t ncs = ctl.nc;
         const uint32_t ncp = next_pow2(ncs);
         const uint32_t lgn = 31 - __clz(ncp);
         const uint32_t G = 64u >> lgn;
         const uint32_t fc = lane & (ncp - 1), fj = lane >> lgn;
         const uint32_t J = wid * G + fj, GS = PF_K3_WAVES * G;
         const uint32_t f_lo = cd.site0[fc], f_len = cd.len[fc], f_kofs = cd.kofs[fc];
+        float s0 = 0.f, s1 = 0.f;
+        uint32_t lcode = 0;
+        // one chunk: a row holds the longest list of the window (static) or
+        // of this iteration, zero-padded to 32 terms; pitch = 4 mod 32
+        const uint32_t PI = one_chunk ? P1 : ((ctl.L + 31) & ~31u) + 4;
+        if (PI <= (rec2 >> lgn)) {
+            K3_COUNT(9, ncs);
+            lcode = k3_fill_rows<SLDS>(m, f_lo, f_kofs, J, f_len, (f_len + 31) & ~31u, GS, m.recv + fc * PI);
+            const uint32_t lc = wave_group_sum(lcode, ncp);
+            if (lane < ncp) lcp[wid * 64 + lane] = lc;
+            __syncthreads();                                   // (B)
+            K3_STAMP(3);
+            if (wid == 0 && lane < ncs) k3_fold32(m.recv + lane * PI, (c_len + 31) >> 5, s0, s1);
+            K3_STAMP(4);
+        } else {
+        const uint32_t lmax = ctl.L;
         // row pitch P (float2) = 4 mod 32: the fold's 16-byte row reads of up
         // to 8 candidates and the fill's 8-lane row segments spread over the
         // LDS banks; chunks of CHK (8 | CHK) terms
@@ -1344,45 +1429,11 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         K3_COUNT(9, ncs);
         K3_COUNT(10, (lmaxp + 4 * GS - 1) / (4 * GS));
         const uint32_t f_lenp = (f_len + 7) & ~7u;
-        float s0 = 0.f, s1 = 0.f;
-        uint32_t lcode = 0;
         for (uint32_t t0 = 0; t0 < lmaxp; t0 += CHK) {
             const uint32_t tlim = lmaxp - t0 < CHK ? lmaxp - t0 : CHK;  // wave-uniform, 8 | tlim
             const uint32_t tend = f_len < t0 + tlim ? f_len : t0 + tlim;
             const uint32_t tpad = f_lenp < t0 + tlim ? f_lenp : t0 + tlim;
-            float2 *row = m.recv + fc * P - t0;
-            for (uint32_t tb = t0 + J; tb < tpad; tb += 4 * GS) {
-                // unconditional loads (out-of-span lanes read entry 0 and are
-                // masked afterwards) so that all four rounds are in flight
-                uint32_t sl[4], cv[4];
-                float4 sr[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t t = tb + u * GS;
-                    const bool ok = t < tend;
-                    sl[u] = k3_slot_raw<SLDS>(m, ok ? f_kofs + t : 0u);
-                    sr[u] = m.srec[ok ? f_lo + t : 0u];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t t = tb + u * GS;
-                    const bool ok = t < tend && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
-                    const uint32_t c = m.cnt[ok ? sl[u] : 0u];
-                    cv[u] = ok ? c : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t t = tb + u * GS;
-                    const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
-                    // key present at this site (inserted at least once) and
-                    // sum != 0: pushed; cnt > 0: positive (:3505-3509, :3619-3624)
-                    const bool p0 = cv[u] != 0 && sr[u].z != 0.f, p1 = cv[u] != 0 && sr[u].w != 0.f;
-                    const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
-                    const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
-                    lcode += (p0 ? 1u + (a0 ? 1u : 0u) : 0u) + ((p1 ? 1u + (a1 ? 1u : 0u) : 0u) << 16);
-                    if (t < tpad) row[t] = make_float2(q0, q1);
-                }
-            }
+            lcode += k3_fill_rows<SLDS>(m, f_lo, f_kofs, t0 + J, tend, tpad, GS, m.recv + fc * P - t0);
             const bool last_chunk = t0 + CHK >= lmaxp;
             if (last_chunk) {
                 const uint32_t lc = wave_group_sum(lcode, ncp);
@@ -1421,6 +1472,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             }
             if (!last_chunk) __syncthreads();                  // rows reused by the next chunk
             K3_STAMP(4);
+        }
         }
         if (wid != 0) continue;
         lcode = lcp[lane] + lcp[64 + lane] + lcp[128 + lane] + lcp[192 + lane];
@@ -1821,6 +1873,7 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
         ctl.fail = 0;
         ctl.summ = 0;
         ctl.nstrict = 0;
+        ctl.mxlen = 0;
         if (!p1_lds) {
             const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)align16(need1));
             if (o + need1 > d.scr_cap) { ctl.fail = 1; atomicOr(d.status, PF_ST_SCR_OVF); }

@@ -33,11 +33,13 @@ for cov in (30, 60):
     per = prof[:, :, :8].sum(axis=2).astype(float).ravel()
     it = st[:, :, 2].astype(float).ravel()
     top = np.argsort(per)[::-1][:6]
-    print("  top problems (w,dir): cycles, iters, init cycles, reads, sites, lookups/iter")
+    print("  top problems (w,dir): cycles, iters, init cycles, reads, sites, lookups/iter, one_chunk, rcw, mxlen")
     for i in top:
         w, d = divmod(int(i), 2)
         print(f"    ({w},{d}) {per[i]:.3g} {it[i]:.0f} {float(prof[w, d, 0]):.3g} {st[w, d, 6]} {st[w, d, 7]} "
-              f"{st[w, d, 0] / max(it[i], 1):.0f}")
+              f"{st[w, d, 0] / max(it[i], 1):.0f} {prof[w, d, 11]} {prof[w, d, 12]} {prof[w, d, 13]}")
+    oc = prof[:, :, 11].ravel()
+    print(f"  one_chunk problems {int(oc.sum())}/{oc.size}, rcw min {prof[:, :, 12].min()} median {np.median(prof[:, :, 12])}")
     print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
     print(f"  per iter: lmax {cnt[0]/iters:.1f}  nc {cnt[1]/iters:.2f}  fill batches {cnt[2]/iters:.2f}")
     db.free(); ctx.close()
