@@ -47,6 +47,12 @@
 #define K3_COUNT(i, v) do { } while (0)
 #endif
 
+#ifdef PF_ASM_MARK
+#define K3_MARK(s) asm volatile("; MARK " s)
+#else
+#define K3_MARK(s) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------------
 // small helpers
 DEV uint64_t lanemask_lt(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -214,11 +220,7 @@ DEV uint64_t ub_u32(const uint32_t *a, uint64_t lo, uint64_t hi, uint32_t v) {
     return lo;
 }
 
-DEV uint32_t next_pow2(uint32_t x) {
-    uint32_t p = 1;
-    while (p < x) p <<= 1;
-    return p;
-}
+DEV uint32_t next_pow2(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
 
 // ========================================================================
 // K1: sites + directional methmer ranges + end-order + arena reservation
@@ -1299,9 +1301,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     const uint32_t L32 = (ctl.mxlen + 31) & ~31u;
     const uint32_t P1 = L32 + 4;
     const bool one_chunk = P1 <= (rec2 >> (31 - __clz(next_pow2(NC))));
-    K3_COUNT(11, one_chunk ? 1 : 0);
-    K3_COUNT(12, m.rcw);
-    K3_COUNT(13, ctl.mxlen);
+    K3_COUNT(15, one_chunk ? 1 : 0);
     bool need_collect = true, stop = false;
     int qn = -1;
     uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
@@ -1387,6 +1387,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     }
     __syncthreads();                                           // (A)
     if (ctl.done) break;
+    K3_STAMP(8);
     {
         // ---- fill, all four waves: the value pair of every (candidate,
         // methmer) lookup into per-candidate record rows; G = 64/ncp lanes of
@@ -1406,10 +1407,13 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // of this iteration, zero-padded to 32 terms; pitch = 4 mod 32
         const uint32_t PI = one_chunk ? P1 : ((ctl.L + 31) & ~31u) + 4;
         if (PI <= (rec2 >> lgn)) {
-            K3_COUNT(9, ncs);
+            K3_COUNT(13, ncs);
+            K3_STAMP(9);
             lcode = k3_fill_rows<SLDS>(m, f_lo, f_kofs, J, f_len, (f_len + 31) & ~31u, GS, m.recv + fc * PI);
+            K3_STAMP(10);
             const uint32_t lc = wave_group_sum(lcode, ncp);
             if (lane < ncp) lcp[wid * 64 + lane] = lc;
+            K3_STAMP(11);
             __syncthreads();                                   // (B)
             K3_STAMP(3);
             if (wid == 0 && lane < ncs) k3_fold32(m.recv + lane * PI, (c_len + 31) >> 5, s0, s1);
@@ -1425,9 +1429,9 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // rows are zero-padded to a multiple of 8 terms so that the fold reads
         // whole 8-term blocks (+0.0f leaves a non-negative sum unchanged)
         const uint32_t lmaxp = (lmax + 7) & ~7u;
-        K3_COUNT(8, lmax);
-        K3_COUNT(9, ncs);
-        K3_COUNT(10, (lmaxp + 4 * GS - 1) / (4 * GS));
+        K3_COUNT(12, lmax);
+        K3_COUNT(13, ncs);
+        K3_COUNT(14, (lmaxp + 4 * GS - 1) / (4 * GS));
         const uint32_t f_lenp = (f_len + 7) & ~7u;
         for (uint32_t t0 = 0; t0 < lmaxp; t0 += CHK) {
             const uint32_t tlim = lmaxp - t0 < CHK ? lmaxp - t0 : CHK;  // wave-uniform, 8 | tlim
@@ -1496,6 +1500,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             K3_STAMP(7);
             continue;
         }
+        K3_MARK("tail_begin");
         const uint64_t bal = __ballot(hkey == hmax);
         const uint32_t cw = 63u - (uint32_t)__clzll((long long)bal);
         const uint32_t tg = rdl(s0 > s1 ? 0u : 1u, cw);
@@ -1609,6 +1614,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
             stx.iters++;
         }
+        K3_MARK("tail_end");
         K3_STAMP(7);
     }
     }

@@ -12,7 +12,7 @@ L.LIB_PATH = os.path.join(os.path.dirname(L.LIB_PATH), "libpomfret_amd_prof.so")
 from pomfret_amd import Config, Context  # noqa: E402
 from pomfret_amd.synth import SynthSpec, make_batch  # noqa: E402
 
-names = ["init", "setup", "prefetch", "fill", "fold", "keys", "pick", "tail"]
+names = ["init", "setup", "prefetch", "barrierB", "fold", "keys", "pick", "tail", "barrierA", "fields", "fill_rows", "groupsum"]
 for cov in (30, 60):
     cfg = Config.from_coverage(cov, given=False)
     b = make_batch(SynthSpec(n_windows=256, coverage=cov, seed=11))
@@ -24,22 +24,20 @@ for cov in (30, 60):
     prof = np.zeros((256, 2, 16), np.uint64)
     lib.pf_batch_prof(db.handle, prof.ctypes.data, prof.size)
     st = db.stats()
-    cnt = prof[:, :, 8:].sum(axis=(0, 1)).astype(float)
-    tot = prof[:, :, :8].sum(axis=(0, 1)).astype(float)
+    cnt = prof[:, :, 12:].sum(axis=(0, 1)).astype(float)
+    tot = prof[:, :, :12].sum(axis=(0, 1)).astype(float)
     iters = st[:, :, 2].sum()
     print(f"cov={cov} kernels={ctx.kernel_times()} iters={iters}")
     for n, v in zip(names, tot):
         print(f"  {n:18s} {v/tot.sum()*100:5.1f}%  {v/iters:8.0f} cyc/iter")
-    per = prof[:, :, :8].sum(axis=2).astype(float).ravel()
+    per = prof[:, :, :12].sum(axis=2).astype(float).ravel()
     it = st[:, :, 2].astype(float).ravel()
     top = np.argsort(per)[::-1][:6]
-    print("  top problems (w,dir): cycles, iters, init cycles, reads, sites, lookups/iter, one_chunk, rcw, mxlen")
+    print("  top problems (w,dir): cycles, iters, init cycles, reads, sites, lookups/iter, one_chunk")
     for i in top:
         w, d = divmod(int(i), 2)
         print(f"    ({w},{d}) {per[i]:.3g} {it[i]:.0f} {float(prof[w, d, 0]):.3g} {st[w, d, 6]} {st[w, d, 7]} "
-              f"{st[w, d, 0] / max(it[i], 1):.0f} {prof[w, d, 11]} {prof[w, d, 12]} {prof[w, d, 13]}")
-    oc = prof[:, :, 11].ravel()
-    print(f"  one_chunk problems {int(oc.sum())}/{oc.size}, rcw min {prof[:, :, 12].min()} median {np.median(prof[:, :, 12])}")
+              f"{st[w, d, 0] / max(it[i], 1):.0f} {prof[w, d, 15]}")
     print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
-    print(f"  per iter: lmax {cnt[0]/iters:.1f}  nc {cnt[1]/iters:.2f}  fill batches {cnt[2]/iters:.2f}")
+    print(f"  per iter: lmax(chunked) {cnt[0]/iters:.1f}  nc(one-chunk) {cnt[1]/iters:.2f}  batches(chunked) {cnt[2]/iters:.2f}")
     db.free(); ctx.close()
