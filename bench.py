@@ -74,16 +74,22 @@ def pmc_traffic(kernel: str):
         return None
 
 
-def cpu_baseline(cfg, batch, reps: int, threads: int):
+def cpu_baseline(cfg, batch, threads: int, min_cpu_s: float = 20.0, max_reps: int = 200):
     """The CPU oracle (plain-C restatement of the reference, oracle/) timed on
-    this host with `threads` pthreads over windows (kt_for analogue)."""
+    this host with `threads` pthreads over windows (kt_for analogue): whole
+    passes over the same batch until about `min_cpu_s` seconds of CPU work
+    (wall x threads) are done -- a bounded sample, reported as reads/s."""
     import oracle
     oracle.methphase(cfg, batch.select(range(min(8, batch.n_windows))), n_threads=threads)
     t0 = time.perf_counter()
-    for _ in range(reps):
+    reps = 0
+    while reps < max_reps:
         oracle.methphase(cfg, batch, n_threads=threads)
+        reps += 1
+        if (time.perf_counter() - t0) * threads >= min_cpu_s and reps >= 3:
+            break
     dt = time.perf_counter() - t0
-    return batch.n_reads * reps / dt, dt
+    return batch.n_reads * reps / dt, dt, reps
 
 
 def main():
@@ -178,11 +184,11 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        reps = 5
-        v_cpu, dt = cpu_baseline(cfg, batch, reps, threads)
+        v_cpu, dt, reps = cpu_baseline(cfg, batch, threads)
         cpu = {"value": round(v_cpu, 1), "unit": "reads/s", "cores": threads, "kind": "port",
                "sample": f"the same {batch.n_windows}-window workload x{reps} "
-                         f"({batch.n_reads * reps} reads, {dt:.1f}s wall on {threads} threads), "
+                         f"({batch.n_reads * reps} reads, {dt:.2f}s wall x {threads} threads "
+                         f"= {dt * threads:.0f} CPU-s), "
                          f"oracle/pf_oracle.c"}
 
     res = {
