@@ -1,0 +1,65 @@
+"""Multi-process sharding on CPU (gloo, world_size 2): every rank phases its
+LPT shard of windows (the CPU oracle stands in for the device here -- the
+compute is per window and independent), then the int8 decisions are
+all-gathered into original window order (pomfret_amd.shard.gather_decisions,
+the same call the GPU path makes over RCCL).  The gathered vector must equal
+the single-process result on the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from pomfret_amd import Config
+        from pomfret_amd.shard import gather_decisions, shard
+        from pomfret_amd.synth import SynthSpec, make_batch
+        cfg = Config.from_coverage(30, given=False)
+        batch = make_batch(SynthSpec(n_windows=10, coverage=30, seed=5, gap_mix=True))
+        idx, sub = shard(batch, rank, world)
+        res = oracle.methphase(cfg, sub, n_threads=2)
+        full = gather_decisions(batch.n_windows, idx, res.decision)
+        np.save(os.path.join(out_dir, f"dec{rank}.npy"), full)
+        np.save(os.path.join(out_dir, f"idx{rank}.npy"), idx)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gather_matches_single_process(tmp_path, oracle_lib):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    from pomfret_amd import Config
+    from pomfret_amd.synth import SynthSpec, make_batch
+    cfg = Config.from_coverage(30, given=False)
+    batch = make_batch(SynthSpec(n_windows=10, coverage=30, seed=5, gap_mix=True))
+    ref = oracle_lib.methphase(cfg, batch, n_threads=4).decision
+    idx = [np.load(tmp_path / f"idx{r}.npy") for r in range(world)]
+    assert sorted(np.concatenate(idx).tolist()) == list(range(batch.n_windows))
+    assert all(len(i) > 0 for i in idx)
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"dec{r}.npy"), ref)
+
+
+def test_lpt_partition_balances():
+    from pomfret_amd.shard import lpt_partition
+    costs = np.array([9, 8, 7, 6, 5, 4, 3, 2, 1], np.float64)
+    parts = lpt_partition(costs, 3)
+    loads = [costs[p].sum() for p in parts]
+    assert max(loads) <= 4.0 / 3.0 * costs.sum() / 3   # Graham's LPT bound
+    assert sorted(np.concatenate(parts).tolist()) == list(range(9))
