@@ -40,9 +40,11 @@ def log(*a):
 def algo_bytes(batch, stats, n_sites):
     """Algorithmic bytes per launch of each kernel.
 
-    K1 sites   : 5 B per call read (u32 pos + u8 cat) + 9 B per site written
-    K2 methmer : per (read, dir): 5 B per call read, 4 B per site entry read
-                 (~ one per methmer) and 4 B per methmer key written
+    K12 sites + methmers (fused; the K2 kernel only takes fallback reads,
+                 usually none, and is credited 0 B):
+                 5 B per call read (u32 pos + u8 cat) + 9 B per site written,
+                 and per (read, dir) 5 B per call read, 4 B per site entry
+                 read (~ one per methmer) and 4 B per methmer key written
     K3 greedy  : 12 B per methmer lookup (4 B key + 2x(2 B cnt + 2 B sum)),
                  8 B per methmer inserted, 1 B per read visited by the scan,
                  2 B per strict reference read in the 2x2 table
@@ -57,7 +59,7 @@ def algo_bytes(batch, stats, n_sites):
     k1 = 5 * N + 9 * S
     k2 = 2 * 5 * N + 8 * mmr          # calls read per direction + sites read / methmers written
     k3 = 12 * lookups + 8 * inserts + scanned + 2 * strict
-    return {"pf_k1_sites": k1, "pf_k2_methmers": k2, "pf_k3_greedy": k3}
+    return {"pf_k12_sites_methmers": k1 + k2, "pf_k2_methmers": 0, "pf_k3_greedy": k3}
 
 
 def pmc_traffic(kernel: str):

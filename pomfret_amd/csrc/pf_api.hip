@@ -19,14 +19,14 @@
 #include "pf_host.h"
 #include "../../include/pomfret_amd.h"
 
-__global__ void pf_k1_sites(pf_dev_batch d);
+__global__ void pf_k12_sites_methmers(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
 __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
 #define PF_NKERN 3
-static const char *k_names[PF_NKERN] = {"pf_k1_sites", "pf_k2_methmers", "pf_k3_greedy"};
+static const char *k_names[PF_NKERN] = {"pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy"};
 
 struct pf_ctx {
     int device;
@@ -286,7 +286,8 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
         PUT(p, cpos, N); d.call_pos = p;
         PUT(bp, ccat, N); d.call_cat = bp;
     }
-    ALLOC(d.call_site, N);
+    ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
+    ALLOC(d.fb_ctr, 1);
     ALLOC(d.win_S, W);
     ALLOC(d.win_nreads, W);
     ALLOC(d.site_pos, site_total);
@@ -314,7 +315,7 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     ALLOC(d.table, 8ull * W);
     ALLOC(d.hp_fwd, R);
     ALLOC(d.stats, 16ull * W);
-    ALLOC(d.prof, 32ull * W);
+    ALLOC(d.prof, 48ull * W);
     const char *lds = getenv("PF_K3_LDS");
     d.lds_bytes = lds ? (uint32_t)atoi(lds) : 73728u;
     if (hipHostMalloc((void **)&b->h_table, std::max<size_t>(8ull * W, 1) * 4) != hipSuccess ||
@@ -337,6 +338,7 @@ static int launch_all(pf_dbatch *b, int stages = 3) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(d.keys_ctr, 0, 3 * sizeof(unsigned long long), st));
     HIPCHK(hipMemsetAsync(d.status, 0, 4 * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(d.fb_ctr, 0, sizeof(uint32_t), st));
     if (b->W == 0) { b->launched = 1; return PF_OK; }
     static int attr_done = 0;
     if (!attr_done) {
@@ -351,12 +353,13 @@ static int launch_all(pf_dbatch *b, int stages = 3) {
     }
     (void)hipGetLastError();
     HIPCHK(hipEventRecord(c->ev[0], st));
-    hipLaunchKernelGGL(pf_k1_sites, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
+    hipLaunchKernelGGL(pf_k12_sites_methmers, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], st));
     if (stages < 2) { b->launched = 1; return PF_OK; }
+    // fallback reads only (usually none): a grid-stride kernel over K12's list
     const uint64_t waves = 2ull * b->R;
-    const uint32_t g2 = (uint32_t)((waves + PF_K2_WAVES - 1) / PF_K2_WAVES);
+    const uint32_t g2 = (uint32_t)std::min<uint64_t>((waves + PF_K2_WAVES - 1) / PF_K2_WAVES, 512);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], st));
@@ -507,10 +510,10 @@ extern "C" int pf_batch_stats(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
 }
 
 extern "C" int pf_batch_prof(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
-    if (!b || !out || n < 32ull * b->W) return PF_ERR_ARG;
+    if (!b || !out || n < 48ull * b->W) return PF_ERR_ARG;
     HIPCHK(hipSetDevice(b->ctx->device));
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    if (b->W) HIPCHK(hipMemcpy(out, b->d.prof, 32ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (b->W) HIPCHK(hipMemcpy(out, b->d.prof, 48ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PF_OK;
 }
 

@@ -5,7 +5,7 @@
  *   windows : win_start/win_end/win_read_off/win_par          [W]
  *   reads   : read_start/end/first/last/win, read_hp           [R]
  *             read_call_off                                     [R+1]
- *   calls   : call_pos (u32), call_cat (u8), call_site (u32)    [N]
+ *   calls   : call_pos (u32), call_cat (u8)                     [N]
  *             calls of a read sorted by (pos, cat)
  *   sites   : per window a slice [site_off[w], +site_cap[w]) of
  *             site_pos, st1_pos, site_q1 (u32) and len0, len1 (u8)
@@ -49,7 +49,7 @@ struct pf_dev_batch {
     /* calls */
     const uint32_t *call_pos;
     const uint8_t *call_cat;
-    uint32_t *call_site;
+    uint32_t *fb_list, *fb_ctr;        /* reads left to the K2 fallback kernel */
     /* per-window results of K1 */
     uint32_t *win_S, *win_nreads;
     uint32_t *site_pos, *st1_pos, *site_q1;

@@ -42,7 +42,13 @@
 #define K3_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
 #define K3_COUNT(i, v) do { prof_acc[i] += (v); } while (0)
+#define K12_STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    d.prof[32ull * d.W + (uint64_t)blockIdx.x * 16 + (i)] = t_ - k12_t0; k12_t0 = t_; } } while (0)
+#define K2_STAMP(i) do { if (k2acc) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    k2acc[i] += t_ - k2acc[7]; k2acc[7] = t_; } } while (0)
 #else
+#define K12_STAMP(i) do { } while (0)
+#define K2_STAMP(i) do { } while (0)
 #define K3_STAMP(i) do { } while (0)
 #define K3_COUNT(i, v) do { } while (0)
 #endif
@@ -223,9 +229,343 @@ DEV uint64_t ub_u32(const uint32_t *a, uint64_t lo, uint64_t hi, uint32_t v) {
 DEV uint32_t next_pow2(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 1)); }
 
 // ========================================================================
-// K1: sites + directional methmer ranges + end-order + arena reservation
+// methmers of one read in one direction (get_mmr_of_read, blockjoin.c:3357-3451)
 // ========================================================================
-__global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
+#define PF_K12_CAPW 512          // per-wave site-entry buffer of the fused methmer phase
+#define PF_K12_SMAX 5800         // sites whose arrays fit LDS beside 16 such buffers
+
+// Methylation characters (m/u/- = 0/1/2) of read r over real-site indices
+// [qlo, qhi): the category of the read's first call at the site's position,
+// '-' when the read has no call there -- the successor of the site entry in
+// get_mmr_of_read's sorted buffer (blockjoin.c:3390-3436).  A read's calls are
+// sorted by (pos, cat), so the first call at a position has the smallest
+// category, as in the reference's radix-sorted buffer.
+DEV void k2_chars(const pf_dev_batch &d, uint64_t c0, uint64_t c1, const uint32_t *sp, uint32_t qlo,
+                  uint32_t qhi, uint32_t lane, uint8_t *chars) {
+    const uint32_t nq = qhi - qlo;
+    for (uint32_t j = lane; j < nq; j += 64) chars[j] = 2;
+    wave_sync();
+    const uint32_t plo = sp[qlo], phi = sp[qhi - 1];
+    for (uint64_t cb = c0 + lane; cb < c1; cb += 256) {
+        uint32_t pos[4], prv[4], cat[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t c = cb + 64 * u;
+            const bool ok = c < c1;
+            pos[u] = ok ? d.call_pos[c] : 0xFFFFFFFFu;
+            prv[u] = (ok && c > c0) ? d.call_pos[c - 1] : 0xFFFFFFFFu;
+            cat[u] = ok ? d.call_cat[c] : 2u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t c = cb + 64 * u;
+            const uint32_t p = pos[u];
+            if (c < c1 && (c == c0 || prv[u] != p) && p >= plo && p <= phi) {
+                uint32_t lo = qlo, hi = qhi;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (sp[mid] < p) lo = mid + 1; else hi = mid;
+                }
+                if (lo < qhi && sp[lo] == p) chars[lo - qlo] = (uint8_t)cat[u];
+            }
+        }
+    }
+    wave_sync();
+}
+
+// Lower bounds of two keys in a non-decreasing array a[0, n): lanes 0-31
+// search kA, lanes 32-63 kB, narrowing 32-fold per round (one LDS round trip
+// each instead of a dependent binary-search chain).
+DEV void wave_lb2(const uint32_t *a, uint32_t n, uint32_t kA, uint32_t kB, uint32_t lane, uint32_t &lbA,
+                  uint32_t &lbB) {
+    const uint32_t h = lane >> 5, j = lane & 31;
+    const uint32_t key = h ? kB : kA;
+    uint32_t lo = 0, hi = n;
+    for (;;) {
+        const uint32_t len = hi - lo;
+        const uint32_t step = (len + 31) >> 5;
+        const uint32_t p = lo + j * step;
+        const bool lt = len > 0 && p < hi && a[p] < key;
+        const uint64_t bal = __ballot(lt);
+        const uint32_t c = (uint32_t)__popc((uint32_t)(bal >> (32 * h)));
+        if (len > 0) {
+            if (c == 0) hi = lo;
+            else {
+                const uint32_t pn = lo + c * step;
+                lo = lo + (c - 1) * step + 1;
+                hi = pn < hi ? pn : hi;
+            }
+        }
+        if (__ballot(hi > lo) == 0) break;
+    }
+    lbA = rdl(lo, 0);
+    lbB = rdl(lo, 32);
+}
+
+// Position -> site index hash of a window's sites (LDS), entries
+// (pos - pmin) << 13 | index; positions of hash-path windows span < 2^19.
+struct K2SiteHash {
+    const uint32_t *t;
+    uint32_t mask, pmin;
+};
+DEV uint32_t k2_hash_slot(uint32_t rel) { return (rel * 2654435761u) >> 7; }
+DEV uint32_t k2_site_of(const K2SiteHash &hs, uint32_t p) {
+    const uint32_t rel = p - hs.pmin;
+    if (p < hs.pmin || rel >= (1u << 19)) return PF_NONE;
+    uint32_t h = k2_hash_slot(rel) & hs.mask;
+    for (;;) {
+        const uint32_t e = hs.t[h];
+        if (e == PF_NONE) return PF_NONE;
+        if ((e >> 13) == rel) return e & 8191u;
+        h = (h + 1) & hs.mask;
+    }
+}
+
+// Per-read scalars of the methmer walk.
+struct K2Read {
+    uint64_t c0, c1;
+    uint32_t F, L, cap, maxcall;
+};
+
+// Calls of one read held in registers (reads of up to 64*K2_CR calls): the
+// position and, for the first call at a position, its category (3 = none).
+#define K2_CR 8
+struct K2Calls {
+    uint32_t pos[K2_CR], cat[K2_CR], site[K2_CR];
+};
+
+// site index of each first call (PF_NONE if its position is not a site), once
+// per read for both directions: hash lookup, or lower bound over all sites
+DEV void k2_calls_sites(K2Calls &cl, const uint32_t *sp, uint32_t S, const K2SiteHash *hs) {
+#pragma unroll
+    for (int u = 0; u < K2_CR; u++) {
+        const uint32_t p = cl.pos[u];
+        uint32_t si = PF_NONE;
+        if (cl.cat[u] < 3u && S > 0 && p >= sp[0] && p <= sp[S - 1]) {
+            if (hs) si = k2_site_of(*hs, p);
+            else {
+                uint32_t lo = 0, hi = S;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (sp[mid] < p) lo = mid + 1; else hi = mid;
+                }
+                si = sp[lo] == p ? lo : PF_NONE;
+            }
+        }
+        cl.site[u] = si;
+    }
+}
+
+DEV void k2_load_scalars(const pf_dev_batch &d, uint32_t r, K2Read &rd) {
+    rd.c0 = d.read_call_off[r];
+    rd.c1 = d.read_call_off[r + 1];
+    rd.F = d.read_first[r];
+    rd.L = d.read_last[r];
+    rd.cap = d.mmr_cap[r];
+    rd.maxcall = 0;
+}
+
+// issue the loads of a read's calls (only when they fit the registers)
+DEV void k2_issue_calls(const pf_dev_batch &d, const K2Read &rd, uint32_t lane, uint32_t *pos, uint32_t *cat) {
+    const bool fits = rd.c1 - rd.c0 <= 64ull * K2_CR && rd.cap <= PF_K12_CAPW;
+#pragma unroll
+    for (int u = 0; u < K2_CR; u++) {
+        const uint64_t c = rd.c0 + lane + 64u * u;
+        const bool ok = fits && c < rd.c1;
+        pos[u] = ok ? d.call_pos[c] : 0xFFFFFFFFu;
+        cat[u] = ok ? (uint32_t)d.call_cat[c] : 3u;
+    }
+}
+
+// first-call flags: the previous call's position comes from the lane below
+// (DPP wave_shr:1) or, for lane 0, from lane 63 of the previous round
+DEV void k2_finish_calls(uint64_t c0, uint64_t c1, uint32_t lane, const uint32_t *pos, const uint32_t *cat,
+                         K2Calls &cl) {
+    uint32_t last = 0xFFFFFFFFu;
+#pragma unroll
+    for (int u = 0; u < K2_CR; u++) {
+        const uint64_t c = c0 + lane + 64u * u;
+        uint32_t prv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pos[u], 0x138, 0xF, 0xF, false);  // wave_shr:1
+        if (lane == 0) prv = last;
+        last = rdl(pos[u], 63);
+        cl.pos[u] = pos[u];
+        cl.cat[u] = (c < c1 && (c == c0 || prv != pos[u])) ? cat[u] : 3u;
+    }
+}
+
+// k2_chars from calls held in registers with their site indices
+DEV void k2_chars_reg(const K2Calls &cl, uint32_t qlo, uint32_t qhi, uint32_t lane, uint8_t *chars) {
+    const uint32_t nq = qhi - qlo;
+    for (uint32_t j = lane; j < nq; j += 64) chars[j] = 2;
+    wave_sync();
+#pragma unroll
+    for (int u = 0; u < K2_CR; u++) {
+        const uint32_t si = cl.site[u];
+        if (si >= qlo && si < qhi) chars[si - qlo] = (uint8_t)cl.cat[u];
+    }
+    wave_sync();
+}
+
+// One read, one direction, one wavefront.  sp = real site positions, st =
+// the direction's sites_starts, lens = its methmer lengths, q1 = dir-1 real
+// index of each start; buffers of capw entries (LDS or HBM scratch).
+DEV void k2_core(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane, uint32_t S,
+                 const uint32_t *sp, const uint32_t *st, const uint8_t *lens, const uint32_t *q1,
+                 uint8_t *chars, uint8_t *crank, uint32_t *irank, uint32_t capw, const K2Read &rd,
+                 const K2Calls *cl, uint64_t koff, unsigned long long *k2acc = nullptr) {
+    const uint32_t g = 2 * r + dir;
+    const uint64_t c0 = rd.c0, c1 = rd.c1;
+    uint32_t total = 0, start_i = PF_NONE;
+    if (S > 0 && c1 > c0) {
+        const uint32_t F = rd.F, L = rd.L;
+        const uint32_t sfirst = st[0], slast = st[S - 1];
+        // search_arr on sites_starts (blockjoin.c:3375-3384); sites_starts is
+        // non-decreasing in both directions, so search_arr1 = lower bound.
+        if (!(F > slast || L < sfirst)) {
+            uint32_t lbF, lbL;
+            wave_lb2(st, S, F, L, lane, lbF, lbL);
+            uint32_t xl, xr;
+            if (F < sfirst) xl = 0;
+            else xl = st[lbF] == F ? lbF : (lbF ? lbF - 1 : 0);
+            xr = L > slast ? S : lbL;
+            if (xl < xr) {
+                const uint32_t qlo = dir ? q1[xl] : xl;
+                const uint32_t qhi = dir ? q1[xr - 1] + 1 : xr;
+                const uint32_t nq = qhi - qlo;
+                const uint32_t cap = rd.cap;
+                if (nq > capw || xr - xl > capw) {
+                    if (lane == 0) atomicOr(d.status, PF_ST_INTERNAL);
+                } else {
+                    K2_STAMP(0);
+                    if (cl) k2_chars_reg(*cl, qlo, qhi, lane, chars);
+                    else k2_chars(d, c0, c1, sp, qlo, qhi, lane, chars);
+                    K2_STAMP(1);
+                    // buffer site entries: indices of [xl,xr) except repeats of the
+                    // previous start, with the i>1 quirk (blockjoin.c:3391)
+                    uint32_t E = 0;
+                    for (uint32_t i0 = xl; i0 < xr; i0 += 64) {
+                        const uint32_t i = i0 + lane;
+                        bool ent = false;
+                        if (i < xr) ent = !(i > 1 && st[i] == st[i - 1]);
+                        const uint64_t m = __ballot(ent);
+                        if (ent) {
+                            const uint32_t rk = E + (uint32_t)__popcll(m & lanemask_lt(lane));
+                            const uint32_t q = dir ? q1[i] : i;
+                            crank[rk] = chars[q - qlo];
+                            irank[rk] = i;
+                        }
+                        E += (uint32_t)__popcll(m);
+                    }
+                    wave_sync();
+                    K2_STAMP(2);
+                    if (E > 0) {
+                        // the buffer's last element is never a walk position (:3420)
+                        const uint32_t maxcall = rd.maxcall;
+                        const uint32_t usable = E - (st[irank[E - 1]] > maxcall ? 1u : 0u);
+                        // duplicated start at indices 0 and 1: entry 0 is followed by
+                        // another site entry, so its character is '-'
+                        if (lane == 0 && E >= 2 && irank[0] == 0 && irank[1] == 1 && st[1] == st[0])
+                            crank[0] = 2;
+                        wave_sync();
+                        uint32_t *out = d.keys + koff;
+                        const uint64_t room = d.keys_cap > koff ? d.keys_cap - koff : 0;
+                        for (uint32_t e0 = 0; e0 < E; e0 += 64) {
+                            const uint32_t e = e0 + lane;
+                            uint32_t ne = 0, fj = PF_NONE, i = 0, P = 0;
+                            if (e < E) {
+                                i = irank[e];
+                                P = st[i];
+                                for (uint32_t j = i; j < S && st[j] == P; j++) {
+                                    if (e + lens[j] <= usable) {
+                                        if (fj == PF_NONE) fj = j;
+                                        ne++;
+                                    }
+                                }
+                            }
+                            const uint32_t incl = wave_incl_scan_dpp(ne);
+                            const uint32_t tot = rdl(incl, 63);
+                            if (start_i == PF_NONE && tot > 0) {
+                                const uint64_t m = __ballot(ne > 0);
+                                const uint32_t src = (uint32_t)__ffsll((unsigned long long)m) - 1;
+                                start_i = rdl(fj, src);
+                            }
+                            if (ne) {
+                                uint32_t pos = total + incl - ne;
+                                for (uint32_t j = i; j < S && st[j] == P; j++) {
+                                    const uint32_t Lj = lens[j];
+                                    if (e + Lj <= usable) {
+                                        uint32_t key = 0;
+                                        for (uint32_t t = 0; t < Lj; t++) key = key << 2 | crank[e + t];
+                                        if (pos < cap && pos < room) out[pos] = key;
+                                        pos++;
+                                    }
+                                }
+                            }
+                            total += tot;
+                        }
+                        if (total > cap && lane == 0) atomicOr(d.status, PF_ST_KEYS_OVF);
+                        K2_STAMP(3);
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        d.mmr_n[g] = total;
+        d.mmr_start[g] = total ? start_i : 0;   // store_mmr_of_one_read (:3518-3522)
+    }
+}
+
+// Fallback for reads the fused kernel could not take (site-entry bound above
+// its wave buffer, or a window whose sites do not fit LDS): one wavefront per
+// (read, dir) from K12's list, site arrays read from HBM.
+__global__ __launch_bounds__(PF_K2_WAVES * 64) void pf_k2_methmers(pf_dev_batch d) {
+    __shared__ uint8_t s_chars[PF_K2_WAVES][PF_K2_ENT_CAP];
+    __shared__ uint8_t s_crank[PF_K2_WAVES][PF_K2_ENT_CAP];
+    __shared__ uint32_t s_irank[PF_K2_WAVES][PF_K2_ENT_CAP];
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t n = 2ull * (*d.fb_ctr);
+    for (uint64_t gw = (uint64_t)blockIdx.x * PF_K2_WAVES + wid; gw < n; gw += (uint64_t)gridDim.x * PF_K2_WAVES) {
+        const uint32_t r = d.fb_list[gw >> 1], dir = (uint32_t)(gw & 1);
+        const uint32_t w = d.read_win[r];
+        const uint32_t S = d.win_S[w];
+        const uint64_t sb = d.win_site_off[w];
+        const uint32_t *sp = d.site_pos + sb;
+        const uint32_t *st = dir ? d.st1_pos + sb : sp;
+        const uint8_t *lens = (dir ? d.len1 : d.len0) + sb;
+        const uint32_t *q1 = d.site_q1 + sb;
+        const uint64_t bo = d.big_off[r];
+        K2Read rd;
+        rd.c0 = d.read_call_off[r];
+        rd.c1 = d.read_call_off[r + 1];
+        rd.F = d.read_first[r];
+        rd.L = d.read_last[r];
+        rd.cap = d.mmr_cap[r];
+        rd.maxcall = rd.c1 > rd.c0 ? d.call_pos[rd.c1 - 1] : 0u;
+        const uint64_t koff = d.mmr_off[2ull * r + dir];
+        if (bo == ~0ull) {
+            k2_core(d, r, dir, lane, S, sp, st, lens, q1, s_chars[wid], s_crank[wid], s_irank[wid],
+                    PF_K2_ENT_CAP, rd, nullptr, koff);
+        } else {
+            // large read: HBM scratch reserved by K12, 16 bytes per bound entry:
+            // per direction [chars cap][crank cap][pad][irank 4*cap] at dir*8*cap
+            const uint32_t cap = d.mmr_cap[r];
+            if (bo + 16ull * cap > d.big_cap) {
+                if (lane == 0) { d.mmr_n[2 * r + dir] = 0; d.mmr_start[2 * r + dir] = 0; atomicOr(d.status, PF_ST_BIG_OVF); }
+                continue;
+            }
+            uint8_t *b = d.big + bo + (dir ? 8ull * cap : 0);
+            k2_core(d, r, dir, lane, S, sp, st, lens, q1, b, b + cap, reinterpret_cast<uint32_t *>(b + 4ull * cap),
+                    cap, rd, nullptr, koff);
+        }
+    }
+}
+
+// ========================================================================
+// K12: sites + directional methmer ranges + end-order + arena reservation,
+// then every read's methmers (both directions) from LDS-resident site arrays
+// ========================================================================
+__global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_batch d) {
     __shared__ uint32_t tile[PF_K1_TILE];
     __shared__ uint32_t sh_scan[PF_K1_THREADS / 64 + 1];
     __shared__ uint32_t sh_misc[8];
@@ -233,6 +573,9 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
     __shared__ unsigned long long sh_base[2];
     constexpr uint32_t NT = PF_K1_THREADS, NW = NT / 64;
     const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef PF_K3_PROFILE
+    unsigned long long k12_t0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t r0 = d.win_read_off[w], R = d.win_read_off[w + 1] - r0;
     const int cov = d.win_par[w * 4 + 0];
     const uint32_t s = d.win_start[w];
@@ -261,8 +604,17 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
                       sh_misc[2] > sh_misc[3];
     if (fail) {
         if (tid == 0) { d.win_S[w] = 0; d.win_nreads[w] = 0; }
+        for (uint32_t i = tid; i < R; i += NT) {
+            const uint32_t r = r0 + i;
+            d.mmr_n[2 * r] = 0; d.mmr_n[2 * r + 1] = 0;
+            d.mmr_start[2 * r] = 0; d.mmr_start[2 * r + 1] = 0;
+            d.mmr_off[2 * r] = 0; d.mmr_off[2 * r + 1] = 0;
+            d.mmr_cap[r] = 0;
+            d.big_off[r] = ~0ull;
+        }
         return;
     }
+    K12_STAMP(1);
     const uint32_t pmin = sh_misc[2], pmax = sh_misc[3];
     if (tid == 0) { sh_misc[4] = 0; d.win_nreads[w] = R; }
     __syncthreads();
@@ -279,13 +631,23 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
         for (uint32_t j = tid; j < BW; j += NT) bmap[j] = 0;
         if (tid == 0) { sh_misc[5] = 0; sh_misc[6] = 0; }
         __syncthreads();
-        for (uint32_t i = wid; i < R; i += NW) {
-            const uint32_t r = r0 + i;
-            const uint64_t c0 = d.read_call_off[r], c1 = d.read_call_off[r + 1];
-            for (uint64_t c = c0 + lane; c < c1; c += 64) {
-                const uint32_t cat = d.call_cat[c];
+        // the window's calls are one contiguous run: a flat pass, four
+        // independent (cat, pos) loads in flight per thread
+        const uint64_t C0 = d.read_call_off[r0], C1 = d.read_call_off[r0 + R];
+        for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
+            uint32_t cat4[4], pos4[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint64_t c = cb + (uint64_t)u * NT;
+                const bool ok = c < C1;
+                cat4[u] = ok ? d.call_cat[c] : 2u;
+                pos4[u] = ok ? d.call_pos[c] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t cat = cat4[u];
                 if (cat >= 2) continue;
-                const uint32_t pos = d.call_pos[c];
+                const uint32_t pos = pos4[u];
                 const uint32_t inc = cat == 0 ? 1u : 0x10000u;
                 uint32_t h = (pos * 2654435761u) >> 19;
                 for (;;) {
@@ -337,35 +699,6 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
             }
         }
         __syncthreads();
-        for (uint32_t j = tid; j < HN; j += NT) {
-            const uint32_t k = hkeys[j];
-            if (k == PF_NONE || hcnt[j] == PF_NONE) continue;
-            const uint32_t o = k - pmin, wi = o >> 6, t = wi / (BW / NT);
-            uint32_t rk = sh_tbase[t];
-            for (uint32_t q = t * (BW / NT); q < wi; q++) rk += (uint32_t)__popcll(bmap[q]);
-            rk += (uint32_t)__popcll(bmap[wi] & ((1ull << (o & 63)) - 1ull));
-            hcnt[j] = rk;
-        }
-        __syncthreads();
-        for (uint32_t i = wid; i < R; i += NW) {
-            const uint32_t r = r0 + i;
-            const uint64_t c0 = d.read_call_off[r], c1 = d.read_call_off[r + 1];
-            for (uint64_t c = c0 + lane; c < c1; c += 64) {
-                const uint32_t pos = d.call_pos[c];
-                const bool first = (c == c0) || d.call_pos[c - 1] != pos;
-                uint32_t v = PF_NONE;
-                if (first) {
-                    uint32_t h = (pos * 2654435761u) >> 19;
-                    for (;;) {
-                        const uint32_t k = hkeys[h];
-                        if (k == pos) { v = hcnt[h]; break; }
-                        if (k == PF_NONE) break;
-                        h = (h + 1) & (HN - 1);
-                    }
-                }
-                d.call_site[c] = v;
-            }
-        }
         if (tid == 0) sh_misc[4] = total;
         __syncthreads();
     }
@@ -410,48 +743,14 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
                 rank++;
             }
         }
-#pragma unroll 8
-        for (uint32_t jj = 0; jj < 32; jj++) {
-            const uint32_t j = (jj + tid) & 31;
-            const uint32_t below = (uint32_t)__popc(qmask & ((1u << j) - 1u));
-            tile[tid * 32 + j] = ((qmask >> j) & 1u) ? srun + excl + below : PF_NONE;
-        }
         __syncthreads();
         if (tid == 0) sh_misc[4] = srun + total;
-        // label calls with their site index (first call at a position only)
-        for (uint32_t i = wid; i < R; i += NW) {
-            const uint32_t r = r0 + i;
-            const uint64_t c0 = d.read_call_off[r], c1 = d.read_call_off[r + 1];
-            if (c1 == c0) continue;
-            if ((uint64_t)d.call_pos[c1 - 1] < base || (uint64_t)d.call_pos[c0] >= top) continue;
-            const uint64_t lo = lb_u32(d.call_pos, c0, c1, (uint32_t)base);
-            const uint64_t hi = top > 0xFFFFFFFFull ? c1 : lb_u32(d.call_pos, lo, c1, (uint32_t)top);
-            for (uint64_t c = lo + lane; c < hi; c += 64) {
-                const uint32_t pos = d.call_pos[c];
-                const bool first = (c == c0) || d.call_pos[c - 1] != pos;
-                d.call_site[c] = first ? tile[pos - (uint32_t)base] : PF_NONE;
-            }
-        }
         __syncthreads();
     }
+    K12_STAMP(2);
     uint32_t S = sh_misc[4];
     if (S > scap) S = scap;
     if (tid == 0) d.win_S[w] = S;
-
-    // ---- directional methmer lengths/starts (blockjoin.c:3307-3329)
-    const uint32_t *a = d.site_pos + sb;
-    const uint32_t k = (uint32_t)d.k, span = (uint32_t)d.k_span;
-    for (uint32_t p = tid; p < S; p += NT) {
-        const uint32_t ap = a[p];
-        uint32_t j = p + k > S - 1 ? S - 1 : p + k;
-        while (a[j] - ap > span) j--;
-        d.len0[sb + p] = (uint8_t)(j == p ? 1 : j - p);
-        uint32_t q = p > k ? p - k : 0;
-        while (ap - a[q] > span) q++;
-        d.len1[sb + p] = (uint8_t)(q == p ? 1 : p - q);
-        d.st1_pos[sb + p] = a[q];
-        d.site_q1[sb + p] = q;
-    }
 
     // ---- revbuf order: reads ascending by (end<<32 | idx) (blockjoin.c:1126, 1140)
     {
@@ -486,6 +785,36 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
         }
     }
 
+    K12_STAMP(3);
+    // ---- directional methmer lengths/starts (blockjoin.c:3307-3329), into
+    // LDS (when the window's sites fit next to the methmer phase's wave
+    // buffers) and HBM (K3 and the debug/parity hooks read them there)
+    __syncthreads();
+    const bool staged = S <= PF_K12_SMAX;
+    uint32_t *sp = tile, *st1 = tile + S, *q1s = tile + 2 * S;
+    uint8_t *l0s = reinterpret_cast<uint8_t *>(tile + 3 * S), *l1s = l0s + S;
+    const uint32_t *a = staged ? sp : d.site_pos + sb;
+    if (staged) {
+        for (uint32_t p = tid; p < S; p += NT) sp[p] = d.site_pos[sb + p];
+        __syncthreads();
+    }
+    const uint32_t k = (uint32_t)d.k, span = (uint32_t)d.k_span;
+    for (uint32_t p = tid; p < S; p += NT) {
+        const uint32_t ap = a[p];
+        uint32_t j = p + k > S - 1 ? S - 1 : p + k;
+        while (a[j] - ap > span) j--;
+        const uint8_t v0 = (uint8_t)(j == p ? 1 : j - p);
+        uint32_t q = p > k ? p - k : 0;
+        while (ap - a[q] > span) q++;
+        const uint8_t v1 = (uint8_t)(q == p ? 1 : p - q);
+        const uint32_t s1 = a[q];
+        d.len0[sb + p] = v0;
+        d.len1[sb + p] = v1;
+        d.st1_pos[sb + p] = s1;
+        d.site_q1[sb + p] = q;
+        if (staged) { l0s[p] = v0; l1s[p] = v1; st1[p] = s1; q1s[p] = q; }
+    }
+    K12_STAMP(4);
     // ---- per-read methmer capacity and arena reservation
     // bound_r = #sites in [first call, last call] + 3k + 4 >= methmers of the read
     // in either direction (entry walk: <= xr-xl + 2k+1, xr-xl <= #sites + k + 1).
@@ -543,149 +872,103 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k1_sites(pf_dev_batch d) {
         kcarry += 2ull * t1;
         bcarry += t2;
     }
-}
 
-// ========================================================================
-// K2: methmers of one read in one direction (one wavefront)
-// ========================================================================
-template <bool LDSBUF>
-DEV void k2_one(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane, uint8_t *chars,
-                uint8_t *crank, uint32_t *irank) {
-    const uint32_t g = 2 * r + dir;
-    const uint32_t w = d.read_win[r];
-    const uint32_t S = d.win_S[w];
-    const uint64_t c0 = d.read_call_off[r], c1 = d.read_call_off[r + 1];
-    uint32_t total = 0, start_i = PF_NONE;
-    if (S > 0 && c1 > c0) {
-        const uint64_t sb = d.win_site_off[w];
-        const uint32_t *st = (dir ? d.st1_pos : d.site_pos) + sb;
-        const uint8_t *lens = (dir ? d.len1 : d.len0) + sb;
-        const uint32_t *q1 = d.site_q1 + sb;
-        const uint32_t F = d.read_first[r], L = d.read_last[r];
-        const uint32_t sfirst = st[0], slast = st[S - 1];
-        // search_arr on sites_starts (blockjoin.c:3375-3384); sites_starts is
-        // non-decreasing in both directions, so search_arr1 = lower bound.
-        if (!(F > slast || L < sfirst)) {
-            uint32_t xl, xr;
-            if (F < sfirst) xl = 0;
-            else {
-                const uint32_t lb = (uint32_t)lb_u32(st, 0, S, F);
-                xl = st[lb] == F ? lb : (lb ? lb - 1 : 0);
-            }
-            xr = L > slast ? S : (uint32_t)lb_u32(st, 0, S, L);
-            if (xl < xr) {
-                const uint32_t qlo = dir ? q1[xl] : xl;
-                const uint32_t qhi = dir ? q1[xr - 1] + 1 : xr;
-                const uint32_t nq = qhi - qlo;
-                const uint32_t cap = d.mmr_cap[r];
-                if (LDSBUF && (nq > PF_K2_ENT_CAP || xr - xl > PF_K2_ENT_CAP)) {
-                    if (lane == 0) atomicOr(d.status, PF_ST_INTERNAL);
+    K12_STAMP(5);
+    // ---- methmers of every read (get_mmr_of_read, blockjoin.c:3357-3451),
+    // one wavefront per read, both directions, site arrays in LDS.  Reads
+    // whose site-entry bound exceeds the wave buffer (and every read of a
+    // window whose sites do not fit LDS) go to the K2 fallback kernel.
+    // position -> site index hash (hash-path windows whose hash fits beside
+    // the arrays and the wave buffers)
+    const uint32_t arr_b = (uint32_t)((14ull * S + 15) & ~15ull);
+    // load factor <= 1/4: most lookups are misses (calls at CpGs that are not
+    // sites), which linear probing makes long at high load
+    uint32_t HS = 1;
+    while (HS < S * 4) HS <<= 1;
+    const bool use_hash = staged && hash_ok && arr_b + 4u * HS + 16u * 6u * PF_K12_CAPW <= 4u * PF_K1_TILE;
+    uint32_t *hst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(tile) + arr_b);
+    if (use_hash) {
+        for (uint32_t j = tid; j < HS; j += NT) hst[j] = PF_NONE;
+        __syncthreads();
+        for (uint32_t p = tid; p < S; p += NT) {
+            const uint32_t rel = sp[p] - pmin;
+            uint32_t h = k2_hash_slot(rel) & (HS - 1);
+            while (atomicCAS(&hst[h], PF_NONE, (rel << 13) | p) != PF_NONE) h = (h + 1) & (HS - 1);
+        }
+    }
+    __syncthreads();
+    K2SiteHash hsd;
+    hsd.t = hst;
+    hsd.mask = HS - 1;
+    hsd.pmin = pmin;
+    const K2SiteHash *hsp = use_hash ? &hsd : nullptr;
+    if (staged) {
+        uint8_t *wb = reinterpret_cast<uint8_t *>(tile) + arr_b + (use_hash ? 4u * HS : 0u) + wid * 6ull * PF_K12_CAPW;
+        uint8_t *chars = wb, *crank = wb + PF_K12_CAPW;
+        uint32_t *irank = reinterpret_cast<uint32_t *>(wb + 2 * PF_K12_CAPW);
+#ifdef PF_K3_PROFILE
+        unsigned long long k2a[8] = {0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
+        unsigned long long *k2acc = wid == 0 ? k2a : nullptr;
+#else
+        unsigned long long *k2acc = nullptr;
+#endif
+        // software pipeline over this wave's reads i, i+NW, ...: the scalars of
+        // read i+2NW and the calls of read i+NW are in flight while read i is
+        // processed
+        K2Read rdA, rdB;
+        uint32_t pA[K2_CR], tA[K2_CR], pB[K2_CR], tB[K2_CR];
+        if (wid < R) k2_load_scalars(d, r0 + wid, rdA);
+        if (wid + NW < R) k2_load_scalars(d, r0 + wid + NW, rdB);
+        k2_issue_calls(d, wid < R ? rdA : K2Read{0, 0, 0, 0, 0, 0}, lane, pA, tA);
+        for (uint32_t i = wid; i < R; i += NW) {
+            const uint32_t r = r0 + i;
+            K2_STAMP(6);
+            K2Read rdC = {0, 0, 0, 0, 0, 0};
+            if (i + 2 * NW < R) k2_load_scalars(d, r0 + i + 2 * NW, rdC);
+            k2_issue_calls(d, i + NW < R ? rdB : K2Read{0, 0, 0, 0, 0, 0}, lane, pB, tB);
+            K2Read rd = rdA;
+            if (rd.cap > PF_K12_CAPW) {
+                if (lane == 0) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r;
+            } else {
+                const uint64_t k0 = d.mmr_off[2ull * r], k1 = d.mmr_off[2ull * r + 1];
+                const uint64_t nc = rd.c1 - rd.c0;
+                if (nc <= 64ull * K2_CR) {
+                    K2Calls cl;
+                    k2_finish_calls(rd.c0, rd.c1, lane, pA, tA, cl);
+                    // last call position (sorted order) from the registers
+                    uint32_t mc = 0;
+                    if (nc) {
+                        const uint32_t ul = (uint32_t)((nc - 1) >> 6), ll = (uint32_t)((nc - 1) & 63);
+#pragma unroll
+                        for (int u = 0; u < K2_CR; u++)
+                            if ((uint32_t)u == ul) mc = rdl(cl.pos[u], ll);
+                    }
+                    rd.maxcall = mc;
+                    k2_calls_sites(cl, sp, S, hsp);
+                    K2_STAMP(4);
+                    k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW, rd, &cl, k0, k2acc);
+                    K2_STAMP(5);
+                    k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd, &cl, k1, k2acc);
+                    K2_STAMP(5);
                 } else {
-                    // methylation character of each site for this read:
-                    // m/u/- = category of the first call at the site, or '-' (2)
-                    for (uint32_t j = lane; j < nq; j += 64) chars[j] = 2;
-                    wave_sync();
-                    for (uint64_t c = c0 + lane; c < c1; c += 64) {
-                        const uint32_t si = d.call_site[c];
-                        if (si != PF_NONE && si >= qlo && si < qhi) chars[si - qlo] = d.call_cat[c];
-                    }
-                    wave_sync();
-                    // buffer site entries: indices of [xl,xr) except repeats of the
-                    // previous start, with the i>1 quirk (blockjoin.c:3391)
-                    uint32_t E = 0;
-                    for (uint32_t i0 = xl; i0 < xr; i0 += 64) {
-                        const uint32_t i = i0 + lane;
-                        bool ent = false;
-                        if (i < xr) ent = !(i > 1 && st[i] == st[i - 1]);
-                        const uint64_t m = __ballot(ent);
-                        if (ent) {
-                            const uint32_t rk = E + (uint32_t)__popcll(m & lanemask_lt(lane));
-                            const uint32_t q = dir ? q1[i] : i;
-                            crank[rk] = chars[q - qlo];
-                            irank[rk] = i;
-                        }
-                        E += (uint32_t)__popcll(m);
-                    }
-                    wave_sync();
-                    if (E > 0) {
-                        // the buffer's last element is never a walk position (:3420)
-                        const uint32_t maxcall = d.call_pos[c1 - 1];
-                        const uint32_t usable = E - (st[irank[E - 1]] > maxcall ? 1u : 0u);
-                        // duplicated start at indices 0 and 1: entry 0 is followed by
-                        // another site entry, so its character is '-'
-                        if (lane == 0 && E >= 2 && irank[0] == 0 && irank[1] == 1 && st[1] == st[0])
-                            crank[0] = 2;
-                        wave_sync();
-                        uint32_t *out = d.keys + d.mmr_off[g];
-                        const uint64_t room = d.keys_cap > d.mmr_off[g] ? d.keys_cap - d.mmr_off[g] : 0;
-                        for (uint32_t e0 = 0; e0 < E; e0 += 64) {
-                            const uint32_t e = e0 + lane;
-                            uint32_t ne = 0, fj = PF_NONE, i = 0, P = 0;
-                            if (e < E) {
-                                i = irank[e];
-                                P = st[i];
-                                for (uint32_t j = i; j < S && st[j] == P; j++) {
-                                    if (e + lens[j] <= usable) {
-                                        if (fj == PF_NONE) fj = j;
-                                        ne++;
-                                    }
-                                }
-                            }
-                            const uint32_t incl = wave_incl_scan(ne, lane);
-                            const uint32_t tot = __shfl(incl, 63, 64);
-                            if (start_i == PF_NONE && tot > 0) {
-                                const uint64_t m = __ballot(ne > 0);
-                                const int src = __ffsll((unsigned long long)m) - 1;
-                                start_i = __shfl(fj, src, 64);
-                            }
-                            if (ne) {
-                                uint32_t pos = total + incl - ne;
-                                for (uint32_t j = i; j < S && st[j] == P; j++) {
-                                    const uint32_t Lj = lens[j];
-                                    if (e + Lj <= usable) {
-                                        uint32_t key = 0;
-                                        for (uint32_t t = 0; t < Lj; t++) key = key << 2 | crank[e + t];
-                                        if (pos < cap && pos < room) out[pos] = key;
-                                        pos++;
-                                    }
-                                }
-                            }
-                            total += tot;
-                        }
-                        if (total > cap && lane == 0) atomicOr(d.status, PF_ST_KEYS_OVF);
-                    }
+                    rd.maxcall = nc ? d.call_pos[rd.c1 - 1] : 0u;
+                    k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW, rd, nullptr, k0);
+                    k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd, nullptr, k1);
                 }
             }
+            rdA = rdB;
+            rdB = rdC;
+#pragma unroll
+            for (int u = 0; u < K2_CR; u++) { pA[u] = pB[u]; tA[u] = tB[u]; }
         }
-    }
-    if (lane == 0) {
-        d.mmr_n[g] = total;
-        d.mmr_start[g] = total ? start_i : 0;   // store_mmr_of_one_read (:3518-3522)
-    }
-}
-
-__global__ __launch_bounds__(PF_K2_WAVES * 64) void pf_k2_methmers(pf_dev_batch d) {
-    __shared__ uint8_t s_chars[PF_K2_WAVES][PF_K2_ENT_CAP];
-    __shared__ uint8_t s_crank[PF_K2_WAVES][PF_K2_ENT_CAP];
-    __shared__ uint32_t s_irank[PF_K2_WAVES][PF_K2_ENT_CAP];
-    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t gw = (uint64_t)blockIdx.x * PF_K2_WAVES + wid;
-    if (gw >= 2ull * d.R) return;
-    const uint32_t r = (uint32_t)(gw >> 1), dir = (uint32_t)(gw & 1);
-    const uint64_t bo = d.big_off[r];
-    if (bo == ~0ull) {
-        k2_one<true>(d, r, dir, lane, s_chars[wid], s_crank[wid], s_irank[wid]);
+#ifdef PF_K3_PROFILE
+        if (tid == 0) for (int j = 0; j < 7; j++) d.prof[32ull * d.W + (uint64_t)blockIdx.x * 16 + 8 + j] = k2a[j];
+#endif
     } else {
-        // large read: HBM scratch reserved by K1, 16 bytes per bound entry:
-        // per direction [chars cap][crank cap][pad][irank 4*cap] at dir*8*cap
-        const uint32_t cap = d.mmr_cap[r];
-        if (bo + 16ull * cap > d.big_cap) {
-            if (lane == 0) { d.mmr_n[2 * r + dir] = 0; d.mmr_start[2 * r + dir] = 0; atomicOr(d.status, PF_ST_BIG_OVF); }
-            return;
-        }
-        uint8_t *b = d.big + bo + (dir ? 8ull * cap : 0);
-        k2_one<false>(d, r, dir, lane, b, b + cap, reinterpret_cast<uint32_t *>(b + 4ull * cap));
+        for (uint32_t i = tid; i < R; i += NT) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r0 + i;
     }
+    __syncthreads();
+    K12_STAMP(6);
 }
 
 // ========================================================================
@@ -1976,6 +2259,10 @@ __global__ __launch_bounds__(64) void pf_selftest_wave(unsigned long long *bad) 
     for (uint32_t i = 0; i <= lane; i++) ref += v[i];
     for (uint32_t i = 0; i < 64; i++) mx = v[i] > mx ? v[i] : mx;
     nb += wave_incl_scan_dpp(x) != ref;
+    {
+        const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
+        if (lane > 0) nb += sh != v[lane - 1];
+    }
     nb += wave_max_dpp(x) != mx;
     for (uint32_t ncp = 1; ncp <= 64; ncp <<= 1) {
         uint32_t gs = 0;

@@ -21,8 +21,10 @@ for cov in (30, 60):
     db.run(); db.run()
     lib = L.lib()
     lib.pf_batch_prof.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
-    prof = np.zeros((256, 2, 16), np.uint64)
-    lib.pf_batch_prof(db.handle, prof.ctypes.data, prof.size)
+    raw = np.zeros(256 * 48, np.uint64)
+    lib.pf_batch_prof(db.handle, raw.ctypes.data, raw.size)
+    prof = raw[:256 * 32].reshape(256, 2, 16)
+    k12 = raw[256 * 32:].reshape(256, 16).astype(float)
     st = db.stats()
     cnt = prof[:, :, 12:].sum(axis=(0, 1)).astype(float)
     tot = prof[:, :, :12].sum(axis=(0, 1)).astype(float)
@@ -40,4 +42,13 @@ for cov in (30, 60):
               f"{st[w, d, 0] / max(it[i], 1):.0f} {prof[w, d, 15]}")
     print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
     print(f"  per iter: lmax(chunked) {cnt[0]/iters:.1f}  nc(one-chunk) {cnt[1]/iters:.2f}  batches(chunked) {cnt[2]/iters:.2f}")
+    names12 = ["-", "T7+range", "sites", "revbuf", "dir arrays", "reservation", "methmers", "-"]
+    mx = k12.sum(axis=1).argmax()
+    print("  K12 phases, cycles: mean over windows | slowest window")
+    for j in range(1, 7):
+        print(f"    {names12[j]:12s} {k12[:, j].mean():10.0f} | {k12[mx, j]:10.0f}")
+    k2n = ["pre->chars", "chars", "entries", "emission", "dir0 tail", "between dirs/tail", "read setup"]
+    print("  K12 methmer phase, wave 0, cycles summed over its reads: mean over windows")
+    for j in range(7):
+        print(f"    {k2n[j]:18s} {k12[:, 8 + j].mean():10.0f}")
     db.free(); ctx.close()
