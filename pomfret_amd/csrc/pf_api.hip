@@ -318,6 +318,13 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     ALLOC(d.prof, 48ull * W);
     const char *lds = getenv("PF_K3_LDS");
     d.lds_bytes = lds ? (uint32_t)atoi(lds) : 73728u;
+    // PF_K12_CAP / PF_K12_SMAX lower the fused kernel's limits (tests use them
+    // to drive reads and windows through the fallback paths)
+    const char *kc = getenv("PF_K12_CAP"), *ks = getenv("PF_K12_SMAX");
+    d.k12_capw = kc ? std::min<uint32_t>((uint32_t)atoi(kc), PF_K12_CAPW) : PF_K12_CAPW;
+    d.k12_smax = ks ? std::min<uint32_t>((uint32_t)atoi(ks), PF_K12_SMAX) : PF_K12_SMAX;
+    const char *ke = getenv("PF_K2_ENTCAP");
+    d.k2_entcap = ke ? std::min<uint32_t>((uint32_t)atoi(ke), PF_K2_ENT_CAP) : PF_K2_ENT_CAP;
     if (hipHostMalloc((void **)&b->h_table, std::max<size_t>(8ull * W, 1) * 4) != hipSuccess ||
         hipHostMalloc((void **)&b->h_S, std::max<size_t>(W, 1) * 4) != hipSuccess ||
         hipHostMalloc((void **)&b->h_nreads, std::max<size_t>(W, 1) * 4) != hipSuccess ||

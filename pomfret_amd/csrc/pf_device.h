@@ -24,6 +24,8 @@
 #define PF_K3_THREADS 256
 #define PF_K3_WAVES (PF_K3_THREADS / PF_WAVE)
 #define PF_MAX_NCAND 256
+#define PF_K12_CAPW 512           /* per-wave site-entry buffer of the fused methmer phase */
+#define PF_K12_SMAX 5800          /* sites whose arrays fit LDS beside 16 such buffers */
 #define PF_NONE 0xFFFFFFFFu
 
 /* status bits */
@@ -70,6 +72,8 @@ struct pf_dev_batch {
     uint32_t *status;
     unsigned long long *prof;          /* [W*2*8] diagnostic build only */
     uint32_t lds_bytes;                /* dynamic LDS of the greedy kernel */
+    uint32_t k12_capw, k12_smax;       /* fused methmer phase limits (test overrides) */
+    uint32_t k2_entcap;                /* fallback reads above this bound use HBM scratch */
 };
 
 #endif

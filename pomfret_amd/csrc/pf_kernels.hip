@@ -231,8 +231,6 @@ DEV uint32_t next_pow2(uint32_t x) { return x <= 1 ? 1u : 1u << (32 - __clz(x - 
 // ========================================================================
 // methmers of one read in one direction (get_mmr_of_read, blockjoin.c:3357-3451)
 // ========================================================================
-#define PF_K12_CAPW 512          // per-wave site-entry buffer of the fused methmer phase
-#define PF_K12_SMAX 5800         // sites whose arrays fit LDS beside 16 such buffers
 
 // Methylation characters (m/u/- = 0/1/2) of read r over real-site indices
 // [qlo, qhi): the category of the read's first call at the site's position,
@@ -367,7 +365,7 @@ DEV void k2_load_scalars(const pf_dev_batch &d, uint32_t r, K2Read &rd) {
 
 // issue the loads of a read's calls (only when they fit the registers)
 DEV void k2_issue_calls(const pf_dev_batch &d, const K2Read &rd, uint32_t lane, uint32_t *pos, uint32_t *cat) {
-    const bool fits = rd.c1 - rd.c0 <= 64ull * K2_CR && rd.cap <= PF_K12_CAPW;
+    const bool fits = rd.c1 - rd.c0 <= 64ull * K2_CR && rd.cap <= d.k12_capw;
 #pragma unroll
     for (int u = 0; u < K2_CR; u++) {
         const uint64_t c = rd.c0 + lane + 64u * u;
@@ -790,7 +788,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     // LDS (when the window's sites fit next to the methmer phase's wave
     // buffers) and HBM (K3 and the debug/parity hooks read them there)
     __syncthreads();
-    const bool staged = S <= PF_K12_SMAX;
+    const bool staged = S <= d.k12_smax;
     uint32_t *sp = tile, *st1 = tile + S, *q1s = tile + 2 * S;
     uint8_t *l0s = reinterpret_cast<uint8_t *>(tile + 3 * S), *l1s = l0s + S;
     const uint32_t *a = staged ? sp : d.site_pos + sb;
@@ -830,7 +828,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
                 const uint64_t lbF = lb_u32(a, 0, S, F), ubL = ub_u32(a, 0, S, L);
                 const uint32_t cnt = ubL > lbF ? (uint32_t)(ubL - lbF) : 0;
                 bound = cnt + 3 * k + 4;
-                if (bound > PF_K2_ENT_CAP) bigb = 16 * bound;
+                if (bound > d.k2_entcap) bigb = 16 * bound;
             }
             d.mmr_cap[r] = bound;
         }
@@ -858,7 +856,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
         uint32_t bound = 0, bigb = 0;
         if (i < R) {
             bound = d.mmr_cap[r0 + i];
-            if (bound > PF_K2_ENT_CAP) bigb = 16 * bound;
+            if (bound > d.k2_entcap) bigb = 16 * bound;
         }
         uint32_t t1, t2;
         const uint32_t e1 = block_excl_scan<NT>(bound, sh_scan, &t1);
@@ -927,7 +925,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
             if (i + 2 * NW < R) k2_load_scalars(d, r0 + i + 2 * NW, rdC);
             k2_issue_calls(d, i + NW < R ? rdB : K2Read{0, 0, 0, 0, 0, 0}, lane, pB, tB);
             K2Read rd = rdA;
-            if (rd.cap > PF_K12_CAPW) {
+            if (rd.cap > d.k12_capw) {
                 if (lane == 0) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r;
             } else {
                 const uint64_t k0 = d.mmr_off[2ull * r], k1 = d.mmr_off[2ull * r + 1];

@@ -127,3 +127,33 @@ def test_lds_budget_variants(oracle_lib, gpu_ctx, monkeypatch, lds):
     out = db.run()
     _compare(ref, out, f"lds{lds}")
     db.free()
+
+
+@pytest.mark.parametrize("env", [{"PF_K12_CAP": "0"}, {"PF_K12_SMAX": "0"},
+                                 {"PF_K12_CAP": "0", "PF_K2_ENTCAP": "0"}, {"PF_K12_CAP": "40"}],
+                         ids=["all_reads_fallback", "no_lds_sites", "fallback_hbm_scratch", "mixed"])
+def test_methmer_fallback_paths(oracle_lib, gpu_ctx, monkeypatch, env):
+    """Reads the fused sites+methmers kernel hands to the K2 fallback kernel
+    (site-entry bound above its wave buffer, windows whose sites do not fit
+    LDS, HBM scratch for very large reads) give the same bits, including every
+    read's methmer list."""
+    from pomfret_amd import Config
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg = Config.from_coverage(30, given=False)
+    b = synth(6, 30, 43, gap_mix=True)
+    ref = oracle_lib.methphase(cfg, b, n_threads=8)
+    db = gpu_ctx.upload(cfg, b)
+    out = db.run()
+    _compare(ref, out, str(env))
+    ro = b.win_read_off
+    for d in (0, 1):
+        n, st, keys = db.debug_methmers(d)
+        k0 = 0
+        for w in range(b.n_windows):
+            on, ost, okeys = oracle_lib.window_methmers(cfg, b, w, d)
+            assert np.array_equal(on, n[ro[w]:ro[w + 1]])
+            assert np.array_equal(ost, st[ro[w]:ro[w + 1]])
+            assert np.array_equal(okeys, keys[k0:k0 + len(okeys)])
+            k0 += len(okeys)
+    db.free()
