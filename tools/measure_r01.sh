@@ -1,6 +1,6 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/m3
+O=$R/gpurun_out/${MEAS_TAG:-m3}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 python3 $R/bench.py > $O/bench.json 2> $O/bench.err || exit 11
