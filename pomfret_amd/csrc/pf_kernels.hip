@@ -176,6 +176,40 @@ DEV uint32_t wave_group_sum(uint32_t x, uint32_t ncp) {
     return x;
 }
 
+// wave_group_sum for doubles: the same lane pattern on both 32-bit halves
+template <int N>
+DEV double ror_add_d(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, 0x120 + N, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), 0x120 + N, 0xF, 0xF, false);
+    return x + __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+DEV double swap16_add_d(double x) {
+    const long long b = __double_as_longlong(x);
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    const double a = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0]));
+    const double c = __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+    return a + c;
+}
+DEV double swap32_add_d(double x) {
+    const long long b = __double_as_longlong(x);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)b, (uint32_t)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(b >> 32), (uint32_t)(b >> 32), false, false);
+    const double a = __longlong_as_double((long long)(((uint64_t)hi[0] << 32) | lo[0]));
+    const double c = __longlong_as_double((long long)(((uint64_t)hi[1] << 32) | lo[1]));
+    return a + c;
+}
+DEV double wave_group_sum_d(double x, uint32_t ncp) {
+    if (ncp < 2) x = ror_add_d<1>(x);
+    if (ncp < 4) x = ror_add_d<2>(x);
+    if (ncp < 8) x = ror_add_d<4>(x);
+    if (ncp < 16) x = ror_add_d<8>(x);
+    if (ncp < 32) x = swap16_add_d(x);
+    if (ncp < 64) x = swap32_add_d(x);
+    return x;
+}
+
 DEV uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
 
 DEV uint64_t wave_max_u64(uint64_t x) {
@@ -1361,7 +1395,7 @@ DEV uint32_t k3_slot(const K3Mem &m, uint32_t off) {
 // count pair.  Four rounds of loads in flight.
 template <bool SLDS>
 DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32_t tstart, uint32_t tend,
-                          uint32_t tpad, uint32_t step, float2 *row) {
+                          uint32_t tpad, uint32_t step, float2 *row, double &e0, double &e1) {
     uint32_t lcode = 0;
     for (uint32_t tb = tstart; tb < tpad; tb += 4 * step) {
         // unconditional loads (out-of-span lanes read entry 0 and are masked
@@ -1393,23 +1427,82 @@ DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
             const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
             lcode += (p0 ? 1u + (a0 ? 1u : 0u) : 0u) + ((p1 ? 1u + (a1 ? 1u : 0u) : 0u) << 16);
             if (t < tpad) row[t] = make_float2(q0, q1);
+            e0 += (double)q0;                        // exact: see k3_pick_exact
+            e1 += (double)q1;
         }
     }
     return lcode;
 }
 
 // The reference's sequential float sums (blockjoin.c:3619-3636) over one
-// record row, nb blocks of 32 terms (zero padded)
-DEV void k3_fold32(const float2 *rv, uint32_t nb, float &s0, float &s1) {
+// record row of n8 terms (a multiple of 8, zero padded).  Two scalar
+// v_add_f32 chains (hap 0 / hap 1) interleaved: a dependent v_add_f32 issues
+// every ~6 cycles against ~9 for a dependent v_pk_add_f32, and the second
+// chain fills the gap.  Blocks of 32 terms, then of 8.
+#define K3_FADD(acc, x) asm("v_add_f32 %0, %0, %1" : "+v"(acc) : "v"(x))
+DEV void k3_fold(const float2 *rv, uint32_t n8, float &s0, float &s1) {
     const float4 *r4 = reinterpret_cast<const float4 *>(rv);
-#pragma unroll 2
-    for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t nq = n8 >> 1;                // float4 = two terms
+    uint32_t q = 0;
+    for (; q + 16 <= nq; q += 16) {
         float4 v[16];
 #pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = r4[b * 16 + u];
+        for (int u = 0; u < 16; u++) v[u] = r4[q + u];
 #pragma unroll
-        for (int u = 0; u < 16; u++) { s0 += v[u].x; s1 += v[u].y; s0 += v[u].z; s1 += v[u].w; }
+        for (int u = 0; u < 16; u++) {
+            K3_FADD(s0, v[u].x); K3_FADD(s1, v[u].y);
+            K3_FADD(s0, v[u].z); K3_FADD(s1, v[u].w);
+        }
     }
+    for (; q < nq; q += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = r4[q + u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            K3_FADD(s0, v[u].x); K3_FADD(s1, v[u].y);
+            K3_FADD(s0, v[u].z); K3_FADD(s1, v[u].w);
+        }
+    }
+}
+
+// Pick without the sequential fold.  S_h = exact sum of a candidate's fp32
+// terms: every nonzero term is >= 1/65535 (a multiple of 2^-39) and a row
+// holds < 2^13 terms <= 1, so the fp64 sums of the fill and of the ds_add_f64
+// reduction are exact in any order.  The reference's sequential fp32 sum s_h
+// of L non-negative terms satisfies |s_h - S_h| <= gamma_{L-1} S_h (Higham,
+// gamma_n = n u / (1 - n u), u = 2^-24), and diff = fl(|s0 - s1|) adds one
+// rounding.  With those intervals the eligibility (diff >= 3 unless l0, l1 >=
+// 3), the winner (largest diff, ties to the later candidate) and its tag (s0 >
+// s1) are decided when no interval overlaps a competitor's or the threshold;
+// otherwise pick stays 0 and the caller folds.
+DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t c_len, int l0, int l1,
+                       uint32_t &pick, uint32_t &cw, uint32_t &tg) {
+    const bool act = lane < nc;
+    const double S0 = act ? accd[lane] : 0.0, S1 = act ? accd[64 + lane] : 0.0;
+    const double lm1 = c_len > 1 ? (double)(c_len - 1) : 0.0;
+    const double gam = lm1 * 0x1p-24 / (1.0 - lm1 * 0x1p-24) * (1.0 + 0x1p-20);
+    const double E = gam * (S0 + S1);
+    const double D = S0 > S1 ? S0 - S1 : S1 - S0;
+    const bool sgn = D > E;                            // sign of s0 - s1 known
+    const double dlo = sgn ? (D - E) * (1.0 - 0x1p-20) : 0.0;
+    const double dhi = (D + E) * (1.0 + 0x1p-20) + 0x1p-60;
+    const bool rel = l0 < 3 || l1 < 3;
+    const bool el = act && (!rel || dlo >= 3.0);     // certainly eligible
+    const bool un = !act || (rel && dhi < 3.0);      // certainly untagged (or no candidate)
+    if (__ballot(!el && !un)) return;                  // eligibility undecided
+    if (__ballot(el) == 0) { pick = 2; return; }
+    // conservative fp32 images of the interval ends (non-negative: bit order = value order)
+    const float flo = el ? (float)(dlo * (1.0 - 0x1p-20)) : 0.f;
+    const float fhi = (float)(dhi * (1.0 + 0x1p-20));
+    const uint32_t M = wave_max_dpp(el ? __float_as_uint(flo) + 1u : 0u);
+    const uint32_t cs = 63u - (uint32_t)__clzll((long long)__ballot(el && __float_as_uint(flo) + 1u == M));
+    const float mf = __uint_as_float(M - 1u);
+    if (__ballot(el && lane != cs && fhi >= mf)) return;    // a competitor could reach the max
+    if (!rdl(sgn ? 1u : 0u, cs)) return;
+    pick = 1;
+    cw = cs;
+    tg = rdl(S0 > S1 ? 0u : 1u, cs);
 }
 
 template <bool SLDS>
@@ -1587,6 +1680,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     int qn = -1;
     uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
     uint32_t *lcp = reinterpret_cast<uint32_t *>(cd.key);    // per-wave push/positive partials
+    double *accd = reinterpret_cast<double *>(cd.key + 128);  // exact hap sums per candidate
     K3_STAMP(1);
     for (;;) {
     // wavefront 0: candidate list upkeep, then publish the lookup spans
@@ -1663,6 +1757,9 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         cd.site0[lane] = c_lo;
         cd.len[lane] = c_len;
         cd.kofs[lane] = c_kofs;
+        accd[lane] = 0.0;
+        accd[64 + lane] = 0.0;
+        lcp[lane] = 0u;
         if (lane == 0) { ctl.done = stop ? 1u : 0u; ctl.nc = nc; ctl.L = lmax0; }
         K3_STAMP(2);
     }
@@ -1684,20 +1781,30 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         const uint32_t f_lo = cd.site0[fc], f_len = cd.len[fc], f_kofs = cd.kofs[fc];
         float s0 = 0.f, s1 = 0.f;
         uint32_t lcode = 0;
+        bool exact_ok = false;
+        uint32_t row_pitch = 0;
         // one chunk: a row holds the longest list of the window (static) or
-        // of this iteration, zero-padded to 32 terms; pitch = 4 mod 32
+        // of this iteration, zero-padded to 8 terms; pitch = 4 mod 32
         const uint32_t PI = one_chunk ? P1 : ((ctl.L + 31) & ~31u) + 4;
         if (PI <= (rec2 >> lgn)) {
             K3_COUNT(13, ncs);
             K3_STAMP(9);
-            lcode = k3_fill_rows<SLDS>(m, f_lo, f_kofs, J, f_len, (f_len + 31) & ~31u, GS, m.recv + fc * PI);
+            double x0 = 0.0, x1 = 0.0;
+            lcode = k3_fill_rows<SLDS>(m, f_lo, f_kofs, J, f_len, (f_len + 7) & ~7u, GS, m.recv + fc * PI, x0, x1);
             K3_STAMP(10);
-            const uint32_t lc = wave_group_sum(lcode, ncp);
-            if (lane < ncp) lcp[wid * 64 + lane] = lc;
+            // every lane adds into its candidate's totals: integer counts and
+            // exact fp64 sums are order-free, and the G same-address lanes of
+            // one ds_add cost G LDS cycles, far below a DPP reduction chain
+            if (fc < ncs) {
+                atomicAdd(&lcp[fc], lcode);
+                atomicAdd(&accd[fc], x0);
+                atomicAdd(&accd[64 + fc], x1);
+            }
             K3_STAMP(11);
             __syncthreads();                                   // (B)
             K3_STAMP(3);
-            if (wid == 0 && lane < ncs) k3_fold32(m.recv + lane * PI, (c_len + 31) >> 5, s0, s1);
+            exact_ok = true;
+            row_pitch = PI;
             K3_STAMP(4);
         } else {
         const uint32_t lmax = ctl.L;
@@ -1712,13 +1819,13 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         const uint32_t lmaxp = (lmax + 7) & ~7u;
         K3_COUNT(12, lmax);
         K3_COUNT(13, ncs);
-        K3_COUNT(14, (lmaxp + 4 * GS - 1) / (4 * GS));
         const uint32_t f_lenp = (f_len + 7) & ~7u;
         for (uint32_t t0 = 0; t0 < lmaxp; t0 += CHK) {
             const uint32_t tlim = lmaxp - t0 < CHK ? lmaxp - t0 : CHK;  // wave-uniform, 8 | tlim
             const uint32_t tend = f_len < t0 + tlim ? f_len : t0 + tlim;
             const uint32_t tpad = f_lenp < t0 + tlim ? f_lenp : t0 + tlim;
-            lcode += k3_fill_rows<SLDS>(m, f_lo, f_kofs, t0 + J, tend, tpad, GS, m.recv + fc * P - t0);
+            double x0 = 0.0, x1 = 0.0;
+            lcode += k3_fill_rows<SLDS>(m, f_lo, f_kofs, t0 + J, tend, tpad, GS, m.recv + fc * P - t0, x0, x1);
             const bool last_chunk = t0 + CHK >= lmaxp;
             if (last_chunk) {
                 const uint32_t lc = wave_group_sum(lcode, ncp);
@@ -1760,17 +1867,32 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         }
         }
         if (wid != 0) continue;
-        lcode = lcp[lane] + lcp[64 + lane] + lcp[128 + lane] + lcp[192 + lane];
+        lcode = exact_ok ? lcp[lane] : lcp[lane] + lcp[64 + lane] + lcp[128 + lane] + lcp[192 + lane];
+        const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
         // use_mmr_count_predict_tag_for_one_read (:3637-3655) and the pick of
         // predict_tags_of_reads (:3729-3766): max score, ties to the later
-        // candidate (stable merge sort walked from the end)
-        const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
-        const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
-        const bool elig = lane < nc && !(diff < 3.f && (l0 < 3 || l1 < 3));
-        const uint32_t hkey = elig ? __float_as_uint(diff) + 1u : 0u;
-        const uint32_t hmax = wave_max_dpp(hkey);
+        // candidate (stable merge sort walked from the end).  First from the
+        // exact sums with rounding-error intervals; the sequential fp32 fold
+        // only when the intervals cannot decide.
+        uint32_t pick = 0;                         // 0 undecided, 1 winner, 2 none
+        uint32_t cw = 0, tg = 0;
+        if (exact_ok) k3_pick_exact(accd, lane, nc, c_len, l0, l1, pick, cw, tg);
+        K3_COUNT(14, pick == 0 ? 1u : 0u);
+        if (pick == 0) {
+            if (exact_ok && lane < nc) k3_fold(m.recv + lane * row_pitch, (c_len + 7) & ~7u, s0, s1);
+            const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
+            const bool elig = lane < nc && !(diff < 3.f && (l0 < 3 || l1 < 3));
+            const uint32_t hkey = elig ? __float_as_uint(diff) + 1u : 0u;
+            const uint32_t hmax = wave_max_dpp(hkey);
+            if (hmax == 0) pick = 2;
+            else {
+                pick = 1;
+                cw = 63u - (uint32_t)__clzll((long long)__ballot(hkey == hmax));
+                tg = rdl(s0 > s1 ? 0u : 1u, cw);
+            }
+        }
         K3_STAMP(5);
-        if (hmax == 0) {
+        if (pick == 2) {
             // nothing could be tagged (:4064-4069): move i_last, rescan
             K3_STAMP(6);
             if (++failed > 10) stop = true;
@@ -1782,9 +1904,6 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             continue;
         }
         K3_MARK("tail_begin");
-        const uint64_t bal = __ballot(hkey == hmax);
-        const uint32_t cw = 63u - (uint32_t)__clzll((long long)bal);
-        const uint32_t tg = rdl(s0 > s1 ? 0u : 1u, cw);
         const uint32_t rd = rdl(c_rd, cw), n = rdl(c_n, cw), st = rdl(c_st, cw), mo = rdl(c_mo, cw);
         const uint32_t pw = rdl(c_pos, cw);
         K3_STAMP(6);

@@ -41,7 +41,8 @@ for cov in (30, 60):
         print(f"    ({w},{d}) {per[i]:.3g} {it[i]:.0f} {float(prof[w, d, 0]):.3g} {st[w, d, 6]} {st[w, d, 7]} "
               f"{st[w, d, 0] / max(it[i], 1):.0f} {prof[w, d, 15]}")
     print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
-    print(f"  per iter: lmax(chunked) {cnt[0]/iters:.1f}  nc(one-chunk) {cnt[1]/iters:.2f}  batches(chunked) {cnt[2]/iters:.2f}")
+    print(f"  per iter: lmax(chunked) {cnt[0]/iters:.1f}  nc(one-chunk) {cnt[1]/iters:.2f}  "
+          f"picks needing the sequential fold {cnt[2]/iters*100:.2f}%")
     names12 = ["-", "T7+range", "sites", "revbuf", "dir arrays", "reservation", "methmers", "-"]
     mx = k12.sum(axis=1).argmax()
     print("  K12 phases, cycles: mean over windows | slowest window")
