@@ -1480,9 +1480,9 @@ DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t 
                        uint32_t &pick, uint32_t &cw, uint32_t &tg) {
     const bool act = lane < nc;
     const double S0 = act ? accd[lane] : 0.0, S1 = act ? accd[64 + lane] : 0.0;
-    const double lm1 = c_len > 1 ? (double)(c_len - 1) : 0.0;
-    const double gam = lm1 * 0x1p-24 / (1.0 - lm1 * 0x1p-24) * (1.0 + 0x1p-20);
-    const double E = gam * (S0 + S1);
+    // gamma_{L-1} <= (L-1) u (1 + 2^-10) for L < 2^13; margin 2^-9
+    const double g = (double)(c_len > 1 ? c_len - 1 : 0) * (0x1p-24 * (1.0 + 0x1p-9));
+    const double E = g * (S0 + S1);
     const double D = S0 > S1 ? S0 - S1 : S1 - S0;
     const bool sgn = D > E;                            // sign of s0 - s1 known
     const double dlo = sgn ? (D - E) * (1.0 - 0x1p-20) : 0.0;
@@ -1491,18 +1491,20 @@ DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t 
     const bool el = act && (!rel || dlo >= 3.0);     // certainly eligible
     const bool un = !act || (rel && dhi < 3.0);      // certainly untagged (or no candidate)
     if (__ballot(!el && !un)) return;                  // eligibility undecided
-    if (__ballot(el) == 0) { pick = 2; return; }
+    const uint64_t elb = __ballot(el);
+    if (elb == 0) { pick = 2; return; }
     // conservative fp32 images of the interval ends (non-negative: bit order = value order)
     const float flo = el ? (float)(dlo * (1.0 - 0x1p-20)) : 0.f;
     const float fhi = (float)(dhi * (1.0 + 0x1p-20));
-    const uint32_t M = wave_max_dpp(el ? __float_as_uint(flo) + 1u : 0u);
-    const uint32_t cs = 63u - (uint32_t)__clzll((long long)__ballot(el && __float_as_uint(flo) + 1u == M));
+    const uint32_t key = el ? __float_as_uint(flo) + 1u : 0u;
+    const uint32_t M = wave_max_dpp(key);
+    const uint32_t cs = 63u - (uint32_t)__clzll((long long)__ballot(key == M && el));
     const float mf = __uint_as_float(M - 1u);
     if (__ballot(el && lane != cs && fhi >= mf)) return;    // a competitor could reach the max
-    if (!rdl(sgn ? 1u : 0u, cs)) return;
+    if (!((__ballot(sgn) >> cs) & 1ull)) return;
     pick = 1;
     cw = cs;
-    tg = rdl(S0 > S1 ? 0u : 1u, cs);
+    tg = ((__ballot(S0 > S1) >> cs) & 1ull) ? 0u : 1u;
 }
 
 template <bool SLDS>
