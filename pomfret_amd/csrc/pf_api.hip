@@ -34,6 +34,8 @@ struct pf_ctx {
     hipEvent_t ev[PF_NKERN + 1];
     float last_ms[PF_NKERN];
     int have_times;
+    float haptag_ms;          /* last pf_haptag_reads kernel time */
+    int have_haptag;
 };
 
 struct pf_dbatch {
@@ -93,6 +95,7 @@ extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i <= PF_NKERN; i++) HIPCHK(hipEventCreate(&c->ev[i]));
     c->have_times = 0;
+    c->have_haptag = 0;
     *out = c;
     return PF_OK;
 }
@@ -524,13 +527,21 @@ extern "C" int pf_batch_prof(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
     return PF_OK;
 }
 
+extern "C" void pf_ctx_set_haptag_ms(pf_ctx *c, float ms) { c->haptag_ms = ms; c->have_haptag = 1; }
+
 extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n) {
     if (!ctx || !n) return PF_ERR_ARG;
-    int m = *n < PF_NKERN ? *n : PF_NKERN;
+    const int tot = PF_NKERN + (ctx->have_haptag ? 1 : 0);
+    int m = *n < tot ? *n : tot;
     for (int i = 0; i < m; i++) {
-        if (names) names[i] = k_names[i];
-        if (ms) ms[i] = ctx->have_times ? ctx->last_ms[i] : -1.0f;
+        if (i < PF_NKERN) {
+            if (names) names[i] = k_names[i];
+            if (ms) ms[i] = ctx->have_times ? ctx->last_ms[i] : -1.0f;
+        } else {
+            if (names) names[i] = "pf_k4_haptag";
+            if (ms) ms[i] = ctx->haptag_ms;
+        }
     }
-    *n = PF_NKERN;
+    *n = tot;
     return PF_OK;
 }

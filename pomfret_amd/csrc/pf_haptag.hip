@@ -79,7 +79,7 @@ static __device__ __forceinline__ int md_op(uint8_t c) {
     return 4;
 }
 
-__global__ __launch_bounds__(256) void pf_k4_haptag(pf_haptag_dev d) {
+__global__ __launch_bounds__(64) void pf_k4_haptag(pf_haptag_dev d) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= d.n_reads) return;
     if (d.n_known == 0) { d.hp_out[r] = HAPTAG_UNPHASED; return; }
@@ -259,6 +259,7 @@ __global__ __launch_bounds__(256) void pf_k4_haptag(pf_haptag_dev d) {
 struct pf_ctx;
 extern "C" int pf_ctx_device(const pf_ctx *c);
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c);
+extern "C" void pf_ctx_set_haptag_ms(pf_ctx *c, float ms);
 
 #define HCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "[E::pomfret_amd] %s: %s\n", #x, hipGetErrorString(e_)); rc = PF_ERR_HIP; goto done; } } while (0)
@@ -282,6 +283,7 @@ extern "C" int pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *K, const pf
     if (V == 0) { memset(hp_out, HAPTAG_UNPHASED, N); return PF_OK; }
     int rc = PF_OK;
     std::vector<void *> al;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     pf_haptag_dev d;
     memset(&d, 0, sizeof(d));
     // known-variant cursor chain (blockjoin.c:1716-1720) and slice ends (:1728-1729)
@@ -334,15 +336,25 @@ extern "C" int pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *K, const pf
         HCHK(put(al, &d.hp_out, (const uint8_t *)nullptr, N));
         HCHK(put(al, &d.err, (const uint32_t *)nullptr, 1));
         HCHK(hipMemsetAsync(d.err, 0, 4, st));
-        hipLaunchKernelGGL(pf_k4_haptag, dim3((N + 255) / 256), dim3(256), 0, st, d);
+        HCHK(hipEventCreate(&e0));
+        HCHK(hipEventCreate(&e1));
+        HCHK(hipEventRecord(e0, st));
+        // 64-thread workgroups: one wave per CU for small batches spreads the
+        // (divergent, latency-bound) per-read walks over more CUs
+        hipLaunchKernelGGL(pf_k4_haptag, dim3((N + 63) / 64), dim3(64), 0, st, d);
         HCHK(hipGetLastError());
+        HCHK(hipEventRecord(e1, st));
         HCHK(hipMemcpyAsync(hp_out, d.hp_out, N, hipMemcpyDeviceToHost, st));
         uint32_t err = 0;
         HCHK(hipMemcpyAsync(&err, d.err, 4, hipMemcpyDeviceToHost, st));
         HCHK(hipStreamSynchronize(st));
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess) pf_ctx_set_haptag_ms(ctx, ms);
         if (err) rc = PF_ERR_ARG;      // malformed MD (fatal exit in the reference, :1621-1624)
     }
 done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
     for (void *p : al) (void)hipFree(p);
     return rc;
 }

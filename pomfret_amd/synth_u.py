@@ -83,16 +83,18 @@ def make_u_batch(spec: USpec):
                       char_off=np.array(koff), chars=np.array(kc, np.uint8))
     var_at = {v[0]: v for v in vars_}
 
-    # --- reads
+    # --- reads, event-driven: match runs between sparse events (the read's
+    # ALT alleles and sequencing errors) are copied from the reference slab
+    var_pos = np.array(sorted(var_at), np.int64)
     starts = np.sort(rng.integers(1000, spec.ref_len - spec.mean_len * 3, spec.n_reads))
     out = dict(start=[], end=[], cig=[], cig_off=[0], seq=[], seq_off=[0], seq_len=[], md=[],
                md_off=[0], hap=[])
+    p_err = spec.sub_err + spec.indel_err
     for s in starts.tolist():
         hap = int(rng.integers(0, 2))
         L = int(rng.integers(spec.mean_len // 2, spec.mean_len * 3 // 2))
-        cig, seq, md = [], [], []
-        match_run = 0
-        mrun = 0
+        end_ref = min(s + L, spec.ref_len - 10)
+        cig, seq_parts, md = [], [], []
 
         def add_cig(op, n):
             if n <= 0:
@@ -104,53 +106,73 @@ def make_u_batch(spec: USpec):
 
         lead = int(rng.integers(1, 200)) if rng.random() < spec.clip_frac else 0
         if lead:
-            seq += BASES[rng.integers(0, 4, lead)].tolist()
+            seq_parts.append(BASES[rng.integers(0, 4, lead)])
             add_cig(4, lead)
+        # events in [s, end_ref): (pos, kind) kind 0 = variant, 1 = error
+        vlo, vhi = np.searchsorted(var_pos, [s, end_ref])
+        evs = [(int(q), 0) for q in var_pos[vlo:vhi] if var_at[int(q)][4] == hap]
+        n_span = end_ref - s
+        eq = np.nonzero(rng.random(n_span) < p_err)[0] + s
+        evs += [(int(q), 1) for q in eq]
+        evs.sort()
         p = s
-        end_ref = min(s + L, spec.ref_len - 10)
-        while p < end_ref:
-            v = var_at.get(p)
-            if v is not None and v[4] == hap:              # haplotype carries ALT here
-                _, k, ra, aa, _ = v
+        match_run = 0
+        last_op_m = False            # indel errors only right after a match
+        for q, kind in evs:
+            if q < p:
+                continue
+            if q > p:                 # match run up to the event
+                seq_parts.append(ref[p:q])
+                add_cig(0, q - p)
+                match_run += q - p
+                p = q
+                last_op_m = True
+            if kind == 0:
+                _, k, ra, aa, _ = var_at[q]
                 if k == 0:
                     md.append(str(match_run)); md.append(chr(ra[0])); match_run = 0
-                    seq.append(aa[0]); add_cig(0, 1); p += 1
-                    continue
-                # anchor base matches
-                seq.append(int(ref[p])); add_cig(0, 1); match_run += 1; p += 1
-                if k == 1:
-                    dl = len(ra) - 1
-                    md.append(str(match_run)); md.append("^" + ra[1:].decode()); match_run = 0
-                    add_cig(2, dl); p += dl
+                    seq_parts.append(np.array([aa[0]], np.uint8)); add_cig(0, 1); p += 1
                 else:
-                    il = len(aa) - 1
-                    seq += list(aa[1:]); add_cig(1, il)
+                    seq_parts.append(ref[p:p + 1]); add_cig(0, 1); match_run += 1; p += 1
+                    if k == 1:
+                        dl = len(ra) - 1
+                        md.append(str(match_run)); md.append("^" + ra[1:].decode()); match_run = 0
+                        add_cig(2, dl); p += dl
+                    else:
+                        seq_parts.append(np.frombuffer(aa[1:], np.uint8)); add_cig(1, len(aa) - 1)
+                last_op_m = k != 1 and k != 2
                 continue
-            x = rng.random()
-            if x < spec.sub_err:
+            x = rng.random() * p_err
+            if x < spec.sub_err or not last_op_m:
                 b = int(ref[p])
                 alt = int(BASES[(np.where(BASES == b)[0][0] + rng.integers(1, 4)) % 4])
                 md.append(str(match_run)); md.append(chr(b)); match_run = 0
-                seq.append(alt); add_cig(0, 1); p += 1
-            elif x < spec.sub_err + spec.indel_err / 2 and cig and (cig[-1] & 0xf) == 0:
+                seq_parts.append(np.array([alt], np.uint8)); add_cig(0, 1); p += 1
+                last_op_m = True
+            elif x < spec.sub_err + spec.indel_err / 2:
                 dl = int(rng.integers(1, 3))
                 md.append(str(match_run)); md.append("^" + bytes(ref[p:p + dl]).decode()); match_run = 0
                 add_cig(2, dl); p += dl
-            elif x < spec.sub_err + spec.indel_err and cig and (cig[-1] & 0xf) == 0:
-                il = int(rng.integers(1, 3))
-                seq += BASES[rng.integers(0, 4, il)].tolist(); add_cig(1, il)
+                last_op_m = False
             else:
-                seq.append(int(ref[p])); add_cig(0, 1); match_run += 1; p += 1
+                il = int(rng.integers(1, 3))
+                seq_parts.append(BASES[rng.integers(0, 4, il)]); add_cig(1, il)
+                last_op_m = False
+        if p < end_ref:
+            seq_parts.append(ref[p:end_ref])
+            add_cig(0, end_ref - p)
+            match_run += end_ref - p
+            p = end_ref
         md.append(str(match_run))
         if rng.random() < spec.clip_frac:
             tl = int(rng.integers(1, 200))
-            seq += BASES[rng.integers(0, 4, tl)].tolist()
+            seq_parts.append(BASES[rng.integers(0, 4, tl)])
             add_cig(4, tl)
         out["start"].append(s)
         out["end"].append(p)
         out["cig"] += cig
         out["cig_off"].append(len(out["cig"]))
-        sq = np.array(seq, np.uint8)
+        sq = np.concatenate(seq_parts).astype(np.uint8) if seq_parts else np.zeros(0, np.uint8)
         enc = _encode_seq(sq)
         out["seq"].append(enc)
         out["seq_off"].append(out["seq_off"][-1] + len(enc))
