@@ -215,6 +215,39 @@ int  pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *known,
  * mismatches (0 expected). */
 int  pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches);
 
+/* ------------------------------------------------------------------ */
+/* Window definition (host side).                                      */
+
+/* Phase-block gaps of a phased VCF, per contig in VCF order.  raw_* are the
+ * gaps as insert_vcf_line collects them (blockjoin.c:1348-1430, driven by
+ * load_intervals_from_file, :1977-2170): [last POS of a block, PS of the next
+ * block]; gap_* are the windows the methphase worker receives after
+ * merge_close_intervals(readback) (:2190-2220, called with READBACK at
+ * :4520-4521); drop_* the phased intervals that merging swallowed.  Slices of
+ * contig c: [x_off[c], x_off[c+1]). */
+typedef struct pf_gaps {
+    uint32_t n_contigs;
+    char **names;
+    uint32_t *abs_start, *abs_end;     /* ranges_t.abs_start / abs_end */
+    uint64_t *raw_off, *gap_off, *drop_off;
+    uint32_t *raw_start, *raw_end;
+    uint32_t *gap_start, *gap_end;
+    uint32_t *drop_start, *drop_end;
+} pf_gaps_t;
+
+/* Parse a (bgzipped or plain) VCF.  Returns PF_OK, PF_ERR_ARG for the
+ * reference's fatal input errors (unsorted POS, #CHROM header without 10
+ * columns), PF_ERR_NOMEM, or -1 when the file cannot be read. */
+int  pf_vcf_gaps(const char *vcf_path, int32_t readback, pf_gaps_t **out);
+void pf_gaps_free(pf_gaps_t *gaps);
+
+/* `pomfret report` chunk windows of one contig (main_methreport,
+ * blockjoin.c:4963-4991) from its raw gaps: writes up to cap windows
+ * [win_start, win_end) and returns how many there are (or < 0). */
+int64_t pf_report_windows(uint32_t abs_start, const uint32_t *gap_start, const uint32_t *gap_end,
+                          uint64_t n_gaps, uint32_t chunk_size, uint32_t chunk_stride,
+                          uint32_t *win_start, uint32_t *win_end, uint64_t cap);
+
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
  * the observed table. */
 double pf_fisher_exact(int n11, int n12, int n21, int n22,

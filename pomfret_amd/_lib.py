@@ -71,6 +71,55 @@ def _check(rc: int, what: str):
         raise PomfretError(f"{what}: {lib().pf_strerror(rc).decode()} ({rc})")
 
 
+class _PfGaps(C.Structure):
+    _fields_ = [("n_contigs", C.c_uint32), ("names", C.POINTER(C.c_char_p)),
+                ("abs_start", C.POINTER(C.c_uint32)), ("abs_end", C.POINTER(C.c_uint32)),
+                ("raw_off", C.POINTER(C.c_uint64)), ("gap_off", C.POINTER(C.c_uint64)),
+                ("drop_off", C.POINTER(C.c_uint64)),
+                ("raw_start", C.POINTER(C.c_uint32)), ("raw_end", C.POINTER(C.c_uint32)),
+                ("gap_start", C.POINTER(C.c_uint32)), ("gap_end", C.POINTER(C.c_uint32)),
+                ("drop_start", C.POINTER(C.c_uint32)), ("drop_end", C.POINTER(C.c_uint32))]
+
+
+def vcf_gaps(path: str, readback: int = 50_000):
+    """Phase-block gaps of a phased VCF per contig (pf_vcf_gaps): a list of
+    dict(name, abs_start, abs_end, raw, gaps, dropped) with (start, end) pairs."""
+    L = lib()
+    L.pf_vcf_gaps.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.POINTER(_PfGaps))]
+    L.pf_gaps_free.argtypes = [C.POINTER(_PfGaps)]
+    out = C.POINTER(_PfGaps)()
+    _check(L.pf_vcf_gaps(path.encode(), readback, C.byref(out)), "pf_vcf_gaps")
+    g = out.contents
+    res = []
+    for c in range(g.n_contigs):
+        def sl(off, a, b):
+            return [(int(a[k]), int(b[k])) for k in range(off[c], off[c + 1])]
+        res.append(dict(name=g.names[c].decode(), abs_start=int(g.abs_start[c]), abs_end=int(g.abs_end[c]),
+                        raw=sl(g.raw_off, g.raw_start, g.raw_end), gaps=sl(g.gap_off, g.gap_start, g.gap_end),
+                        dropped=sl(g.drop_off, g.drop_start, g.drop_end)))
+    L.pf_gaps_free(out)
+    return res
+
+
+def report_windows(abs_start: int, gaps, chunk_size: int, chunk_stride: int):
+    """`pomfret report` chunk windows of one contig (pf_report_windows) from
+    its raw gaps [(start, end), ...]."""
+    L = lib()
+    L.pf_report_windows.restype = C.c_int64
+    L.pf_report_windows.argtypes = [C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                    C.c_void_p, C.c_void_p, C.c_uint64]
+    gs = np.array([g[0] for g in gaps], np.uint32)
+    ge = np.array([g[1] for g in gaps], np.uint32)
+    n = L.pf_report_windows(abs_start, gs.ctypes.data, ge.ctypes.data, len(gaps), chunk_size, chunk_stride,
+                            None, None, 0)
+    _check(0 if n >= 0 else int(n), "pf_report_windows")
+    ws = np.zeros(max(n, 1), np.uint32)
+    we = np.zeros(max(n, 1), np.uint32)
+    L.pf_report_windows(abs_start, gs.ctypes.data, ge.ctypes.data, len(gaps), chunk_size, chunk_stride,
+                        ws.ctypes.data, we.ctypes.data, n)
+    return list(zip(ws[:n].tolist(), we[:n].tolist()))
+
+
 def device_count() -> int:
     return int(lib().pf_device_count())
 
