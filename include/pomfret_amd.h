@@ -248,6 +248,52 @@ int64_t pf_report_windows(uint32_t abs_start, const uint32_t *gap_start, const u
                           uint64_t n_gaps, uint32_t chunk_size, uint32_t chunk_stride,
                           uint32_t *win_start, uint32_t *win_end, uint64_t cap);
 
+/* ------------------------------------------------------------------ */
+/* Output epilogue (host side): decisions -> phase blocks -> GTF/TSV/VCF. */
+
+/* Per contig (slices [x_off[c], x_off[c+1])): the raw gaps after
+ * lift_decisions fused the joined ones (rawunphasedblocks, blockjoin.c:
+ * 2250-2310), one decision and one cumulative flip per raw gap
+ * (decisions_onraw / flips_onraw, :2312-2324), and the new phase blocks
+ * [blk_start, blk_end) of generate_new_phase_blocks(use_raw=1) (:2326-2362). */
+typedef struct pf_blocks {
+    uint32_t n_contigs;
+    uint64_t *raw_off, *dec_off, *blk_off;
+    uint32_t *raw_start, *raw_end;
+    int32_t *dec_onraw, *flip;
+    uint32_t *blk_start, *blk_end;
+} pf_blocks_t;
+
+/* decision[] holds one join decision (-1 none, 0 cis, 1 trans; the
+ * pf_window_out_t.decision of each window) per merged gap of g, contig by
+ * contig in g's order (the windows gap_*[gap_off[c] ...]).  Replaces the
+ * three calls at blockjoin.c:4685-4687. */
+int  pf_phase_blocks(const pf_gaps_t *g, const int8_t *decision, pf_blocks_t **out);
+void pf_blocks_free(pf_blocks_t *b);
+
+/* output_gtf (:2721-2756) / output_tsv (:2696-2719) to a file path. */
+int  pf_write_gtf(const pf_gaps_t *g, const pf_blocks_t *b, const char *path);
+int  pf_write_tsv(const pf_gaps_t *g, const pf_blocks_t *b, const char *path);
+
+/* Phase of the REF allele at variant sites inside dropped intervals
+ * (st->varphase_in_dropped of recover_variant_phase_in_dropped_intervals,
+ * :2618-2694), per contig of g: 0-based positions ascending in
+ * [off[c], off[c+1]), hap_of_ref 0, 1 or 254 (unphased). */
+typedef struct pf_rescue {
+    const uint64_t *off;
+    const uint32_t *pos;
+    const uint8_t *hap_of_ref;
+} pf_rescue_t;
+
+/* output_modify_vcf (:2918-2988) / alter_vcf_line (:2758-2916): rewrite
+ * vcf_in (bgzipped or plain) into vcf_out (plain text) with the new PS and
+ * flipped GTs.  rescue may be NULL (no rescued sites).  counts (optional):
+ * {lines rewritten, lines unphased by the rescue, lines read}.  Returns
+ * PF_OK, PF_ERR_ARG for a #CHROM header without 10 columns, PF_ERR_NOMEM,
+ * or -1 on an I/O error. */
+int  pf_write_vcf(const char *vcf_in, const pf_gaps_t *g, const pf_blocks_t *b, const pf_rescue_t *rescue,
+                  const char *vcf_out, int64_t *counts);
+
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
  * the observed table. */
 double pf_fisher_exact(int n11, int n12, int n21, int n22,

@@ -81,23 +81,139 @@ class _PfGaps(C.Structure):
                 ("drop_start", C.POINTER(C.c_uint32)), ("drop_end", C.POINTER(C.c_uint32))]
 
 
+def _gaps_lib():
+    L = lib()
+    if not getattr(L, "_pf_gaps_typed", False):
+        L.pf_vcf_gaps.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.POINTER(_PfGaps))]
+        L.pf_gaps_free.argtypes = [C.POINTER(_PfGaps)]
+        L.pf_phase_blocks.argtypes = [C.POINTER(_PfGaps), C.c_void_p, C.POINTER(C.POINTER(_PfBlocks))]
+        L.pf_blocks_free.argtypes = [C.POINTER(_PfBlocks)]
+        L.pf_write_gtf.argtypes = [C.POINTER(_PfGaps), C.POINTER(_PfBlocks), C.c_char_p]
+        L.pf_write_tsv.argtypes = [C.POINTER(_PfGaps), C.POINTER(_PfBlocks), C.c_char_p]
+        L.pf_write_vcf.argtypes = [C.c_char_p, C.POINTER(_PfGaps), C.POINTER(_PfBlocks), C.c_void_p,
+                                   C.c_char_p, C.POINTER(C.c_int64)]
+        L._pf_gaps_typed = True
+    return L
+
+
+class _PfBlocks(C.Structure):
+    _fields_ = [("n_contigs", C.c_uint32),
+                ("raw_off", C.POINTER(C.c_uint64)), ("dec_off", C.POINTER(C.c_uint64)),
+                ("blk_off", C.POINTER(C.c_uint64)),
+                ("raw_start", C.POINTER(C.c_uint32)), ("raw_end", C.POINTER(C.c_uint32)),
+                ("dec_onraw", C.POINTER(C.c_int32)), ("flip", C.POINTER(C.c_int32)),
+                ("blk_start", C.POINTER(C.c_uint32)), ("blk_end", C.POINTER(C.c_uint32))]
+
+
+class _PfRescue(C.Structure):
+    _fields_ = [("off", C.c_void_p), ("pos", C.c_void_p), ("hap_of_ref", C.c_void_p)]
+
+
+class Gaps:
+    """Phase-block gaps of a phased VCF (pf_vcf_gaps), owned C object."""
+
+    def __init__(self, path: str, readback: int = 50_000):
+        L = _gaps_lib()
+        self._p = C.POINTER(_PfGaps)()
+        _check(L.pf_vcf_gaps(path.encode(), readback, C.byref(self._p)), "pf_vcf_gaps")
+
+    def contigs(self):
+        g = self._p.contents
+        res = []
+        for c in range(g.n_contigs):
+            def sl(off, a, b):
+                return [(int(a[k]), int(b[k])) for k in range(off[c], off[c + 1])]
+            res.append(dict(name=g.names[c].decode(), abs_start=int(g.abs_start[c]), abs_end=int(g.abs_end[c]),
+                            raw=sl(g.raw_off, g.raw_start, g.raw_end), gaps=sl(g.gap_off, g.gap_start, g.gap_end),
+                            dropped=sl(g.drop_off, g.drop_start, g.drop_end)))
+        return res
+
+    @property
+    def n_windows(self) -> int:
+        g = self._p.contents
+        return int(g.gap_off[g.n_contigs])
+
+    def close(self):
+        if self._p:
+            _gaps_lib().pf_gaps_free(self._p)
+            self._p = C.POINTER(_PfGaps)()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Blocks:
+    """New phase blocks from the join decisions (pf_phase_blocks)."""
+
+    def __init__(self, gaps: Gaps, decision):
+        L = _gaps_lib()
+        self.gaps = gaps
+        self._dec = np.ascontiguousarray(np.asarray(decision, np.int8))
+        if self._dec.size != gaps.n_windows:
+            raise PomfretError(f"pf_phase_blocks: {self._dec.size} decisions for {gaps.n_windows} windows")
+        self._p = C.POINTER(_PfBlocks)()
+        _check(L.pf_phase_blocks(gaps._p, self._dec.ctypes.data, C.byref(self._p)), "pf_phase_blocks")
+
+    def contigs(self):
+        b = self._p.contents
+        res = []
+        for c in range(b.n_contigs):
+            res.append(dict(
+                raw=[(int(b.raw_start[k]), int(b.raw_end[k])) for k in range(b.raw_off[c], b.raw_off[c + 1])],
+                decisions=[int(b.dec_onraw[k]) for k in range(b.dec_off[c], b.dec_off[c + 1])],
+                flips=[int(b.flip[k]) for k in range(b.dec_off[c], b.dec_off[c + 1])],
+                blocks=[(int(b.blk_start[k]), int(b.blk_end[k])) for k in range(b.blk_off[c], b.blk_off[c + 1])]))
+        return res
+
+    def write_gtf(self, path: str):
+        _check(_gaps_lib().pf_write_gtf(self.gaps._p, self._p, path.encode()), "pf_write_gtf")
+
+    def write_tsv(self, path: str):
+        _check(_gaps_lib().pf_write_tsv(self.gaps._p, self._p, path.encode()), "pf_write_tsv")
+
+    def write_vcf(self, vcf_in: str, vcf_out: str, rescue=None):
+        """rescue: optional per-contig list of {pos0: hap_of_ref} dicts."""
+        L = _gaps_lib()
+        rp = None
+        keep = []
+        if rescue is not None:
+            off = np.zeros(len(rescue) + 1, np.uint64)
+            pos, hap = [], []
+            for c, m in enumerate(rescue):
+                for k in sorted(m):
+                    pos.append(k)
+                    hap.append(m[k])
+                off[c + 1] = len(pos)
+            pa = np.asarray(pos, np.uint32) if pos else np.zeros(1, np.uint32)
+            ha = np.asarray(hap, np.uint8) if hap else np.zeros(1, np.uint8)
+            keep = [off, pa, ha]
+            rp = C.byref(_PfRescue(off.ctypes.data, pa.ctypes.data, ha.ctypes.data))
+        counts = (C.c_int64 * 3)()
+        _check(L.pf_write_vcf(vcf_in.encode(), self.gaps._p, self._p, rp, vcf_out.encode(), counts), "pf_write_vcf")
+        del keep
+        return tuple(int(x) for x in counts)
+
+    def close(self):
+        if self._p:
+            _gaps_lib().pf_blocks_free(self._p)
+            self._p = C.POINTER(_PfBlocks)()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def vcf_gaps(path: str, readback: int = 50_000):
     """Phase-block gaps of a phased VCF per contig (pf_vcf_gaps): a list of
     dict(name, abs_start, abs_end, raw, gaps, dropped) with (start, end) pairs."""
-    L = lib()
-    L.pf_vcf_gaps.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.POINTER(_PfGaps))]
-    L.pf_gaps_free.argtypes = [C.POINTER(_PfGaps)]
-    out = C.POINTER(_PfGaps)()
-    _check(L.pf_vcf_gaps(path.encode(), readback, C.byref(out)), "pf_vcf_gaps")
-    g = out.contents
-    res = []
-    for c in range(g.n_contigs):
-        def sl(off, a, b):
-            return [(int(a[k]), int(b[k])) for k in range(off[c], off[c + 1])]
-        res.append(dict(name=g.names[c].decode(), abs_start=int(g.abs_start[c]), abs_end=int(g.abs_end[c]),
-                        raw=sl(g.raw_off, g.raw_start, g.raw_end), gaps=sl(g.gap_off, g.gap_start, g.gap_end),
-                        dropped=sl(g.drop_off, g.drop_start, g.drop_end)))
-    L.pf_gaps_free(out)
+    g = Gaps(path, readback)
+    res = g.contigs()
+    g.close()
     return res
 
 

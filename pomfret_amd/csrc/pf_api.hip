@@ -26,6 +26,8 @@ __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
 #define PF_NKERN 3
+#define PF_IO_HDR 64ull      // status u32[4] | arena counters u64[3] | fallback counter u32 | pad
+
 static const char *k_names[PF_NKERN] = {"pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy"};
 
 struct pf_ctx {
@@ -50,6 +52,8 @@ struct pf_dbatch {
     std::vector<void *> allocs;
     pf_dev_batch d;
     // host pinned result staging
+    uint8_t *io = nullptr, *h_io = nullptr;   // I/O block (device, pinned host), PF_IO_HDR + 40 W + R bytes
+    uint64_t io_bytes = 0;
     int32_t *h_table;
     uint32_t *h_S, *h_nreads, *h_status;
     uint8_t *h_hp_fwd;
@@ -160,12 +164,7 @@ extern "C" void pf_batch_free(pf_dbatch_t *b) {
     (void)hipSetDevice(b->ctx->device);
     (void)hipStreamSynchronize(b->ctx->stream);
     for (void *p : b->allocs) (void)hipFree(p);
-    (void)hipHostFree(b->h_table);
-    (void)hipHostFree(b->h_S);
-    (void)hipHostFree(b->h_nreads);
-    (void)hipHostFree(b->h_status);
-    (void)hipHostFree(b->h_hp_fwd);
-    (void)hipHostFree(b->h_ctr);
+    (void)hipHostFree(b->h_io);
     delete b;
 }
 
@@ -288,11 +287,36 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
         PUT(up, in->read_call_off, R + 1); d.read_call_off = up;
         PUT(p, cpos, N); d.call_pos = p;
         PUT(bp, ccat, N); d.call_cat = bp;
+        // greedy problems heaviest first (reads per window, direction 1 --
+        // the longer chains -- first on ties): the first wave of workgroups
+        // spreads the long chains over distinct CUs and pairs them with the
+        // short ones dispatched last
+        std::vector<uint32_t> ord(2ull * W);
+        for (uint32_t i = 0; i < 2 * W; i++) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t c) {
+            const uint32_t ra = in->win_read_off[(a >> 1) + 1] - in->win_read_off[a >> 1];
+            const uint32_t rc2 = in->win_read_off[(c >> 1) + 1] - in->win_read_off[c >> 1];
+            if (ra != rc2) return ra > rc2;
+            return (a & 1) > (c & 1);
+        });
+        PUT(p, ord.data(), ord.size()); d.k3_order = p;
     }
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
-    ALLOC(d.fb_ctr, 1);
-    ALLOC(d.win_S, W);
-    ALLOC(d.win_nreads, W);
+    // one I/O block: the counters zeroed before a run (status, arena
+    // counters, fallback counter) followed by everything copied back after it,
+    // so a step costs one memset and one D2H copy
+    b->io_bytes = PF_IO_HDR + 40ull * W + R;
+    ALLOC(b->io, b->io_bytes);
+    d.status = reinterpret_cast<uint32_t *>(b->io);
+    {
+        unsigned long long *cp = reinterpret_cast<unsigned long long *>(b->io + 16);
+        d.keys_ctr = cp; d.big_ctr = cp + 1; d.scr_ctr = cp + 2;
+    }
+    d.fb_ctr = reinterpret_cast<uint32_t *>(b->io + 40);
+    d.table = reinterpret_cast<int32_t *>(b->io + PF_IO_HDR);
+    d.win_S = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 32ull * W);
+    d.win_nreads = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 36ull * W);
+    d.hp_fwd = b->io + PF_IO_HDR + 40ull * W;
     ALLOC(d.site_pos, site_total);
     ALLOC(d.st1_pos, site_total);
     ALLOC(d.site_q1, site_total);
@@ -311,14 +335,8 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     ALLOC(d.big, d.big_cap);
     d.scr_cap = 64ull << 20;
     ALLOC(d.scr, d.scr_cap);
-    {
-        unsigned long long *cp; ALLOC(cp, 3); d.keys_ctr = cp; d.big_ctr = cp + 1; d.scr_ctr = cp + 2;
-    }
-    ALLOC(d.status, 4);
-    ALLOC(d.table, 8ull * W);
-    ALLOC(d.hp_fwd, R);
     ALLOC(d.stats, 16ull * W);
-    ALLOC(d.prof, 48ull * W);
+    ALLOC(d.prof, 80ull * W);
     const char *lds = getenv("PF_K3_LDS");
     d.lds_bytes = lds ? (uint32_t)atoi(lds) : 73728u;
     // PF_K12_CAP / PF_K12_SMAX lower the fused kernel's limits (tests use them
@@ -328,13 +346,17 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     d.k12_smax = ks ? std::min<uint32_t>((uint32_t)atoi(ks), PF_K12_SMAX) : PF_K12_SMAX;
     const char *ke = getenv("PF_K2_ENTCAP");
     d.k2_entcap = ke ? std::min<uint32_t>((uint32_t)atoi(ke), PF_K2_ENT_CAP) : PF_K2_ENT_CAP;
-    if (hipHostMalloc((void **)&b->h_table, std::max<size_t>(8ull * W, 1) * 4) != hipSuccess ||
-        hipHostMalloc((void **)&b->h_S, std::max<size_t>(W, 1) * 4) != hipSuccess ||
-        hipHostMalloc((void **)&b->h_nreads, std::max<size_t>(W, 1) * 4) != hipSuccess ||
-        hipHostMalloc((void **)&b->h_status, 16) != hipSuccess ||
-        hipHostMalloc((void **)&b->h_hp_fwd, std::max<size_t>(R, 1)) != hipSuccess ||
-        hipHostMalloc((void **)&b->h_ctr, 3 * 8) != hipSuccess)
-        return fail(PF_ERR_NOMEM);
+    // PF_K3_PATH=fold|rows drives every greedy pick through the sequential
+    // fold, or every iteration through the chunked record-row path (tests)
+    const char *kp = getenv("PF_K3_PATH");
+    d.k3_mode = !kp ? 0u : strcmp(kp, "fold") == 0 ? 1u : strcmp(kp, "rows") == 0 ? 2u : 0u;
+    if (hipHostMalloc((void **)&b->h_io, b->io_bytes) != hipSuccess) return fail(PF_ERR_NOMEM);
+    b->h_status = reinterpret_cast<uint32_t *>(b->h_io);
+    b->h_ctr = reinterpret_cast<unsigned long long *>(b->h_io + 16);
+    b->h_table = reinterpret_cast<int32_t *>(b->h_io + PF_IO_HDR);
+    b->h_S = reinterpret_cast<uint32_t *>(b->h_io + PF_IO_HDR + 32ull * W);
+    b->h_nreads = reinterpret_cast<uint32_t *>(b->h_io + PF_IO_HDR + 36ull * W);
+    b->h_hp_fwd = b->h_io + PF_IO_HDR + 40ull * W;
     *out = b;
     return PF_OK;
 #undef PUT
@@ -346,9 +368,7 @@ static int launch_all(pf_dbatch *b, int stages = 3) {
     pf_dev_batch &d = b->d;
     hipStream_t st = c->stream;
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemsetAsync(d.keys_ctr, 0, 3 * sizeof(unsigned long long), st));
-    HIPCHK(hipMemsetAsync(d.status, 0, 4 * sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(d.fb_ctr, 0, sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(b->io, 0, PF_IO_HDR, st));
     if (b->W == 0) { b->launched = 1; return PF_OK; }
     static int attr_done = 0;
     if (!attr_done) {
@@ -377,12 +397,7 @@ static int launch_all(pf_dbatch *b, int stages = 3) {
     hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], st));
-    HIPCHK(hipMemcpyAsync(b->h_table, d.table, 8ull * b->W * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(b->h_S, d.win_S, 4ull * b->W, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(b->h_nreads, d.win_nreads, 4ull * b->W, hipMemcpyDeviceToHost, st));
-    if (b->R) HIPCHK(hipMemcpyAsync(b->h_hp_fwd, d.hp_fwd, b->R, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(b->h_status, d.status, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(b->h_ctr, d.keys_ctr, 24, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b->h_io, b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
     b->launched = 1;
     return PF_OK;
 }
@@ -520,10 +535,10 @@ extern "C" int pf_batch_stats(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
 }
 
 extern "C" int pf_batch_prof(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
-    if (!b || !out || n < 48ull * b->W) return PF_ERR_ARG;
+    if (!b || !out || n < 80ull * b->W) return PF_ERR_ARG;
     HIPCHK(hipSetDevice(b->ctx->device));
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    if (b->W) HIPCHK(hipMemcpy(out, b->d.prof, 48ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    if (b->W) HIPCHK(hipMemcpy(out, b->d.prof, 80ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PF_OK;
 }
 

@@ -54,6 +54,7 @@ struct pf_dev_batch {
     uint32_t *fb_list, *fb_ctr;        /* reads left to the K2 fallback kernel */
     /* per-window results of K1 */
     uint32_t *win_S, *win_nreads;
+    const uint32_t *k3_order;          /* [2W] greedy problems (w<<1|dir), heaviest first */
     uint32_t *site_pos, *st1_pos, *site_q1;
     uint8_t *len0, *len1;
     uint32_t *rev_ord;                 /* [R] window-local read index, ascending (end, idx) */
@@ -74,6 +75,7 @@ struct pf_dev_batch {
     uint32_t lds_bytes;                /* dynamic LDS of the greedy kernel */
     uint32_t k12_capw, k12_smax;       /* fused methmer phase limits (test overrides) */
     uint32_t k2_entcap;                /* fallback reads above this bound use HBM scratch */
+    uint32_t k3_mode;                  /* test override: 0 exact pick, 1 always fold, 2 chunked record rows */
 };
 
 #endif

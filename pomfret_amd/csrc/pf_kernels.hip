@@ -43,7 +43,7 @@
     prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
 #define K3_COUNT(i, v) do { prof_acc[i] += (v); } while (0)
 #define K12_STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    d.prof[32ull * d.W + (uint64_t)blockIdx.x * 16 + (i)] = t_ - k12_t0; k12_t0 = t_; } } while (0)
+    d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + (i)] = t_ - k12_t0; k12_t0 = t_; } } while (0)
 #define K2_STAMP(i) do { if (k2acc) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
     k2acc[i] += t_ - k2acc[7]; k2acc[7] = t_; } } while (0)
 #else
@@ -994,7 +994,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
             for (int u = 0; u < K2_CR; u++) { pA[u] = pB[u]; tA[u] = tB[u]; }
         }
 #ifdef PF_K3_PROFILE
-        if (tid == 0) for (int j = 0; j < 7; j++) d.prof[32ull * d.W + (uint64_t)blockIdx.x * 16 + 8 + j] = k2a[j];
+        if (tid == 0) for (int j = 0; j < 7; j++) d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 8 + j] = k2a[j];
 #endif
     } else {
         for (uint32_t i = tid; i < R; i += NT) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r0 + i;
@@ -1010,6 +1010,7 @@ struct K3Ctl {
     uint32_t S, R, ntot, nc, L, done, failed, inserted, winner, tag;
     int32_t i_last;
     uint32_t min_i, max_i, fail, summ, nstrict, mxlen;
+    uint32_t ins_n, ins_st, ins_mo, ins_tg;   // register variant: winner whose insert is pending
     unsigned long long scr;
     int32_t tab[4];
 };
@@ -1434,34 +1435,114 @@ DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
     return lcode;
 }
 
-// The reference's sequential float sums (blockjoin.c:3619-3636) over one
-// record row of n8 terms (a multiple of 8, zero padded).  Two scalar
-// v_add_f32 chains (hap 0 / hap 1) interleaved: a dependent v_add_f32 issues
-// every ~6 cycles against ~9 for a dependent v_pk_add_f32, and the second
-// chain fills the gap.  Blocks of 32 terms, then of 8.
 #define K3_FADD(acc, x) asm("v_add_f32 %0, %0, %1" : "+v"(acc) : "v"(x))
-DEV void k3_fold(const float2 *rv, uint32_t n8, float &s0, float &s1) {
-    const float4 *r4 = reinterpret_cast<const float4 *>(rv);
-    const uint32_t nq = n8 >> 1;                // float4 = two terms
-    uint32_t q = 0;
-    for (; q + 16 <= nq; q += 16) {
-        float4 v[16];
+
+// insert_mmr_counts of one tagged read (hap tg) by the whole workgroup: its
+// sites are distinct, so a plain read-modify-write per site; only hap tg's
+// divisor entry changes (its total becomes >= 1, so no zero case)
+template <bool SLDS>
+DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint32_t mo, uint32_t tg) {
+    const uint32_t inc = tg ? 0x10000u : 1u, sh = tg ? 16u : 0u;
+    float *srf = reinterpret_cast<float *>(m.srec) + tg;   // (h_tg, -, 1/h_tg, -) of site 0
+    for (uint32_t tb = 0; tb < n; tb += 2 * PF_K3_THREADS) {
+        uint32_t sl[2], cc[2], sv[2];
+        bool ok[2];
 #pragma unroll
-        for (int u = 0; u < 16; u++) v[u] = r4[q + u];
+        for (int u = 0; u < 2; u++) {
+            const uint32_t t = tb + u * PF_K3_THREADS + threadIdx.x;
+            ok[u] = t < n && st + t < S;
+            sl[u] = k3_slot_raw<SLDS>(m, ok[u] ? mo + t : 0u);
+        }
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-            K3_FADD(s0, v[u].x); K3_FADD(s1, v[u].y);
-            K3_FADD(s0, v[u].z); K3_FADD(s1, v[u].w);
+        for (int u = 0; u < 2; u++) {
+            const uint32_t t = tb + u * PF_K3_THREADS + threadIdx.x;
+            ok[u] = ok[u] && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
+            cc[u] = m.cnt[ok[u] ? sl[u] : 0u];
+            sv[u] = m.sum[ok[u] ? st + t : 0u];
+        }
+        asm volatile("" ::: "memory");              // every load issued before the first store
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            if (ok[u]) {
+                const uint32_t site = st + tb + u * PF_K3_THREADS + threadIdx.x;
+                const uint32_t s2 = sv[u] + inc;
+                const float f = (float)((s2 >> sh) & 0xffffu);
+                m.cnt[sl[u]] = cc[u] + inc;
+                m.sum[site] = s2;
+                srf[4 * site] = f;
+                srf[4 * site + 2] = __builtin_amdgcn_rcpf(f);
+            }
         }
     }
-    for (; q < nq; q += 4) {
-        float4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = r4[q + u];
+}
+
+// Exact-sum fill of the register variant: the lane's terms t = tstart,
+// tstart+step, ... < tend, accumulated into the exact fp64 sums (no record
+// rows: the sequential fold, needed for 0.05-0.5 % of picks, recomputes its
+// terms with k3_fold_direct).  Returns the push/positive count pair.
+template <bool SLDS>
+DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32_t tstart, uint32_t tend,
+                          uint32_t step, double &e0, double &e1) {
+    uint32_t lcode = 0;
+    for (uint32_t tb = tstart; tb < tend; tb += 4 * step) {
+        uint32_t sl[4], cv[4];
+        float4 sr[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            K3_FADD(s0, v[u].x); K3_FADD(s1, v[u].y);
-            K3_FADD(s0, v[u].z); K3_FADD(s1, v[u].w);
+            const uint32_t t = tb + u * step;
+            const bool ok = t < tend;
+            sl[u] = k3_slot_raw<SLDS>(m, ok ? f_kofs + t : 0u);
+            sr[u] = m.srec[ok ? f_lo + t : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + u * step;
+            const bool ok = t < tend && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
+            const uint32_t c = m.cnt[ok ? sl[u] : 0u];
+            cv[u] = ok ? c : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
+            // pushed: key present (cv != 0) and hap total != 0; positive: cnt > 0
+            const bool p0 = cv[u] != 0 && sr[u].z != 0.f, p1 = cv[u] != 0 && sr[u].w != 0.f;
+            const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
+            const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
+            lcode += (p0 ? 1u + (a0 ? 1u : 0u) : 0u) + ((p1 ? 1u + (a1 ? 1u : 0u) : 0u) << 16);
+            e0 += (double)q0;
+            e1 += (double)q1;
+        }
+    }
+    return lcode;
+}
+
+// The reference's sequential float sums (blockjoin.c:3619-3636) of one
+// candidate, terms recomputed from the tables in methmer order (the rare
+// picks the exact intervals cannot decide).
+template <bool SLDS>
+DEV void k3_fold_direct(const K3Mem &m, uint32_t lo, uint32_t kofs, uint32_t len, float &s0, float &s1) {
+    for (uint32_t t0 = 0; t0 < len; t0 += 8) {
+        uint32_t sl[8];
+        float4 sr[8];
+        float q0[8], q1[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t t = t0 + u;
+            const bool ok = t < len;
+            sl[u] = k3_slot_raw<SLDS>(m, ok ? kofs + t : 0u);
+            sr[u] = m.srec[ok ? lo + t : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const bool ok = t0 + u < len && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
+            const uint32_t c = ok ? m.cnt[ok ? sl[u] : 0u] : 0u;
+            q0[u] = div_u16_y((float)(c & 0xffffu), sr[u].x, sr[u].z);
+            q1[u] = div_u16_y((float)(c >> 16), sr[u].y, sr[u].w);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            K3_FADD(s0, q0[u]);
+            K3_FADD(s1, q1[u]);
         }
     }
 }
@@ -1490,21 +1571,29 @@ DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t 
     const bool rel = l0 < 3 || l1 < 3;
     const bool el = act && (!rel || dlo >= 3.0);     // certainly eligible
     const bool un = !act || (rel && dhi < 3.0);      // certainly untagged (or no candidate)
-    if (__ballot(!el && !un)) return;                  // eligibility undecided
-    const uint64_t elb = __ballot(el);
-    if (elb == 0) { pick = 2; return; }
+    // all lane masks at once, off the dependent chain
+    const uint64_t b_und = __ballot(!el && !un), b_el = __ballot(el);
+    const uint64_t b_sgn = __ballot(sgn), b_gt = __ballot(S0 > S1);
+    if (b_und) return;                                 // eligibility undecided
+    if (b_el == 0) { pick = 2; return; }
     // conservative fp32 images of the interval ends (non-negative: bit order = value order)
     const float flo = el ? (float)(dlo * (1.0 - 0x1p-20)) : 0.f;
     const float fhi = (float)(dhi * (1.0 + 0x1p-20));
     const uint32_t key = el ? __float_as_uint(flo) + 1u : 0u;
-    const uint32_t M = wave_max_dpp(key);
-    const uint32_t cs = 63u - (uint32_t)__clzll((long long)__ballot(key == M && el));
+    // candidates sit in lanes < nc: one DPP row holds them all when nc <= 16
+    const uint32_t M = nc <= 16 ? (uint32_t)__builtin_amdgcn_readlane(
+                                      (int)dpp_max_step(dpp_max_step(dpp_max_step(dpp_max_step(key, 0), 1), 2), 3), 0)
+                                : wave_max_dpp(key);
     const float mf = __uint_as_float(M - 1u);
-    if (__ballot(el && lane != cs && fhi >= mf)) return;    // a competitor could reach the max
-    if (!((__ballot(sgn) >> cs) & 1ull)) return;
+    // the lane holding the max has fhi >= flo = mf; decided iff it is the
+    // only eligible lane whose interval reaches mf (a tie is never decided)
+    const uint64_t b_hi = __ballot(el && fhi >= mf);
+    if (__popcll(b_hi) != 1) return;
+    const uint32_t cs = (uint32_t)__ffsll((unsigned long long)b_hi) - 1u;
+    if (!((b_sgn >> cs) & 1ull)) return;
     pick = 1;
     cw = cs;
-    tg = ((__ballot(S0 > S1) >> cs) & 1ull) ? 0u : 1u;
+    tg = ((b_gt >> cs) & 1ull) ? 0u : 1u;
 }
 
 template <bool SLDS>
@@ -1522,7 +1611,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     K3Stats stx = {0, 0, 0, 0};
     uint32_t sum_mmr = 0, mx_mmr = 0;
 #ifdef PF_K3_PROFILE
-    unsigned long long prof_acc[16] = {0};
+    unsigned long long prof_acc[32] = {0};
     unsigned long long prof_last = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -1673,14 +1762,14 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     // of the window, zero-padded to 32 terms (pitch = 4 mod 32 for the banks)
     // (the register variant keeps no push codes, so the whole 12-byte record
     // region holds float2 terms)
-    const uint32_t rec2 = (uint32_t)((12ull * PF_K3_WAVES * m.rcw) >> 3);
-    const uint32_t L32 = (ctl.mxlen + 31) & ~31u;
-    const uint32_t P1 = L32 + 4;
-    const bool one_chunk = P1 <= (rec2 >> (31 - __clz(next_pow2(NC))));
-    K3_COUNT(15, one_chunk ? 1 : 0);
+    // exact sums need rows of < 2^13 terms (k3_pick_exact); longer lists
+    // take the chunked record-row path with the sequential fold
+    const bool exact_path = ctl.mxlen < 8192u && d.k3_mode != 2u;
+    K3_COUNT(15, exact_path ? 1 : 0);
     bool need_collect = true, stop = false;
     int qn = -1;
     uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
+    uint32_t p_n = 0, p_st = 0, p_mo = 0, p_tg = 0;           // pending insert (wavefront 0)
     uint32_t *lcp = reinterpret_cast<uint32_t *>(cd.key);    // per-wave push/positive partials
     double *accd = reinterpret_cast<double *>(cd.key + 128);  // exact hap sums per candidate
     K3_STAMP(1);
@@ -1722,6 +1811,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             }
             if (done) stop = true;
         }
+        K3_STAMP(16);
         if (!stop && need_collect) {
             need_collect = false;
             // span of query_counts_of_mmrs: sites in [min_i, max_i) (:3500-3501)
@@ -1755,19 +1845,31 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 q_head++;
             }
         }
-        const uint32_t lmax0 = stop || one_chunk ? 0u : wave_max_dpp(c_len);
+        K3_STAMP(17);
+        const uint32_t lmax0 = stop || exact_path ? 0u : wave_max_dpp(c_len);
         cd.site0[lane] = c_lo;
         cd.len[lane] = c_len;
         cd.kofs[lane] = c_kofs;
         accd[lane] = 0.0;
         accd[64 + lane] = 0.0;
         lcp[lane] = 0u;
-        if (lane == 0) { ctl.done = stop ? 1u : 0u; ctl.nc = nc; ctl.L = lmax0; }
+        if (lane == 0) {
+            ctl.done = stop ? 1u : 0u; ctl.nc = nc; ctl.L = lmax0;
+            ctl.ins_n = p_n; ctl.ins_st = p_st; ctl.ins_mo = p_mo; ctl.ins_tg = p_tg;
+        }
+        p_n = 0;
         K3_STAMP(2);
     }
     __syncthreads();                                           // (A)
     if (ctl.done) break;
     K3_STAMP(8);
+    // the previous winner's insert, deferred to here so that the whole
+    // workgroup shares it; wavefront 0 has already applied it virtually to
+    // its range update
+    if (ctl.ins_n) {
+        k3_insert_all<SLDS>(m, S, ctl.ins_n, ctl.ins_st, ctl.ins_mo, ctl.ins_tg);
+        __syncthreads();                                       // (A2)
+    }
     {
         // ---- fill, all four waves: the value pair of every (candidate,
         // methmer) lookup into per-candidate record rows; G = 64/ncp lanes of
@@ -1784,15 +1886,11 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         float s0 = 0.f, s1 = 0.f;
         uint32_t lcode = 0;
         bool exact_ok = false;
-        uint32_t row_pitch = 0;
-        // one chunk: a row holds the longest list of the window (static) or
-        // of this iteration, zero-padded to 8 terms; pitch = 4 mod 32
-        const uint32_t PI = one_chunk ? P1 : ((ctl.L + 31) & ~31u) + 4;
-        if (PI <= (rec2 >> lgn)) {
+        if (exact_path) {
             K3_COUNT(13, ncs);
             K3_STAMP(9);
             double x0 = 0.0, x1 = 0.0;
-            lcode = k3_fill_rows<SLDS>(m, f_lo, f_kofs, J, f_len, (f_len + 7) & ~7u, GS, m.recv + fc * PI, x0, x1);
+            lcode = k3_fill_sums<SLDS>(m, f_lo, f_kofs, J, f_len, GS, x0, x1);
             K3_STAMP(10);
             // every lane adds into its candidate's totals: integer counts and
             // exact fp64 sums are order-free, and the G same-address lanes of
@@ -1806,7 +1904,6 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             __syncthreads();                                   // (B)
             K3_STAMP(3);
             exact_ok = true;
-            row_pitch = PI;
             K3_STAMP(4);
         } else {
         const uint32_t lmax = ctl.L;
@@ -1871,6 +1968,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         if (wid != 0) continue;
         lcode = exact_ok ? lcp[lane] : lcp[lane] + lcp[64 + lane] + lcp[128 + lane] + lcp[192 + lane];
         const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
+        K3_STAMP(18);
         // use_mmr_count_predict_tag_for_one_read (:3637-3655) and the pick of
         // predict_tags_of_reads (:3729-3766): max score, ties to the later
         // candidate (stable merge sort walked from the end).  First from the
@@ -1878,10 +1976,11 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // only when the intervals cannot decide.
         uint32_t pick = 0;                         // 0 undecided, 1 winner, 2 none
         uint32_t cw = 0, tg = 0;
-        if (exact_ok) k3_pick_exact(accd, lane, nc, c_len, l0, l1, pick, cw, tg);
+        if (exact_ok && d.k3_mode == 0u) k3_pick_exact(accd, lane, nc, c_len, l0, l1, pick, cw, tg);
+        K3_STAMP(19);
         K3_COUNT(14, pick == 0 ? 1u : 0u);
         if (pick == 0) {
-            if (exact_ok && lane < nc) k3_fold(m.recv + lane * row_pitch, (c_len + 7) & ~7u, s0, s1);
+            if (exact_ok && lane < nc) k3_fold_direct<SLDS>(m, c_lo, c_kofs, c_len, s0, s1);
             const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
             const bool elig = lane < nc && !(diff < 3.f && (l0 < 3 || l1 < 3));
             const uint32_t hkey = elig ? __float_as_uint(diff) + 1u : 0u;
@@ -1909,41 +2008,16 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         const uint32_t rd = rdl(c_rd, cw), n = rdl(c_n, cw), st = rdl(c_st, cw), mo = rdl(c_mo, cw);
         const uint32_t pw = rdl(c_pos, cw);
         K3_STAMP(6);
-        const uint32_t inc = tg ? 0x10000u : 1u;
         stx.inserts += n;
-        // the sites of one read are distinct: plain read-modify-write, four
-        // rounds of loads in flight
-        for (uint32_t tb = 0; tb < n; tb += 256) {
-            uint32_t sl[4], cc[4], sv[4];
-            bool ok[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t t = tb + u * 64 + lane;
-                ok[u] = t < n && st + t < S;
-                sl[u] = k3_slot_raw<SLDS>(m, ok[u] ? mo + t : 0u);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t t = tb + u * 64 + lane;
-                ok[u] = ok[u] && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
-                cc[u] = m.cnt[ok[u] ? sl[u] : 0u];
-                sv[u] = m.sum[ok[u] ? st + t : 0u];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (ok[u]) {
-                    const uint32_t site = st + tb + u * 64 + lane;
-                    m.cnt[sl[u]] = cc[u] + inc;
-                    m.sum[site] = sv[u] + inc;
-                    m.srec[site] = site_rec(sv[u] + inc);
-                }
-            }
-        }
+        // the insert itself runs on the whole workgroup after the next barrier (A)
+        p_n = n; p_st = st; p_mo = mo; p_tg = tg;
+        K3_STAMP(20);
         if (lane == 0) {
             m.hp[rd] = (uint8_t)tg;
             m.untag[pw >> 6] &= ~(1ull << (pw & 63));
         }
         failed = 0;
+        K3_STAMP(21);
         // candidate list minus the winner, plus the prefetched next read
         {
             const int src = (int)lane + 1;
@@ -1959,17 +2033,23 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         }
         nc = ncn;
         wave_sync();
+        K3_STAMP(22);
         // update_range (:3669-3704): both ends in one ballot, lanes 0-31 walk
         // left from min_i, lanes 32-63 right from max_i
         {
             const int m0 = (int)umin, M0 = (int)umax;
             const bool left = lane < 32;
             const int i = left ? m0 - (int)lane : M0 + (int)(lane - 32);
+            // coverage after the pending insert of the winner (+1 at its sites)
+            auto cov_at = [&](int ii) -> int {
+                const uint32_t v = m.sum[ii];
+                const uint32_t t = (uint32_t)ii - st;
+                int c = (int)((v & 0xffffu) + (v >> 16));
+                if (t < n && k3_slot_raw<SLDS>(m, mo + t) != (SLDS ? 0xFFFFu : PF_NONE)) c++;
+                return c;
+            };
             bool cvg = false;
-            if (left ? (m0 >= 0 && i >= 0) : (M0 >= 0 && i < (int)S)) {
-                const uint32_t v = m.sum[i];
-                cvg = (int)((v & 0xffffu) + (v >> 16)) >= cov_rt;
-            }
+            if (left ? (m0 >= 0 && i >= 0) : (M0 >= 0 && i < (int)S)) cvg = cov_at(i) >= cov_rt;
             const uint64_t b = __ballot(cvg);
             const uint32_t bl = (uint32_t)b, br = (uint32_t)(b >> 32);
             int cl = bl == ~0u ? 32 : __ffs(~bl) - 1;
@@ -1978,7 +2058,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 for (;;) {
                     const int ii = m0 - cl - (int)lane;
                     bool c2 = false;
-                    if (ii >= 0) { const uint32_t v = m.sum[ii]; c2 = (int)((v & 0xffffu) + (v >> 16)) >= cov_rt; }
+                    if (ii >= 0) c2 = cov_at(ii) >= cov_rt;
                     const uint64_t b2 = __ballot(c2);
                     if (b2 == ~0ull) { cl += 64; continue; }
                     cl += __ffsll((unsigned long long)~b2) - 1;
@@ -1989,7 +2069,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 for (;;) {
                     const int ii = M0 + cr + (int)lane;
                     bool c2 = false;
-                    if (ii < (int)S) { const uint32_t v = m.sum[ii]; c2 = (int)((v & 0xffffu) + (v >> 16)) >= cov_rt; }
+                    if (ii < (int)S) c2 = cov_at(ii) >= cov_rt;
                     const uint64_t b2 = __ballot(c2);
                     if (b2 == ~0ull) { cr += 64; continue; }
                     cr += __ffsll((unsigned long long)~b2) - 1;
@@ -1999,6 +2079,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             if (m0 >= 0 && cl > 0) umin = (uint32_t)(m0 - cl + 1);
             if (M0 >= 0 && cr > 0) umax = (uint32_t)(M0 + cr - 1);
         }
+        K3_STAMP(23);
         if (nc == 0) {
             // an empty batch: the failure path of the reference (:4046-4051)
             need_collect = true;
@@ -2250,8 +2331,8 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
         sp[4] = ctl.summ; sp[5] = tsum[4]; sp[6] = R; sp[7] = S;
 #ifdef PF_K3_PROFILE
-        unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 16;
-        for (int i = 0; i < 16; i++) pp[i] = prof_acc[i];
+        unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 32;
+        for (int i = 0; i < 32; i++) pp[i] = prof_acc[i];
 #endif
     }
 }
@@ -2262,7 +2343,8 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     __shared__ K3Cand cd;
     __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
     const uint32_t tid = threadIdx.x;
-    const uint32_t w = blockIdx.x >> 1, dir = blockIdx.x & 1;
+    const uint32_t prob = d.k3_order[blockIdx.x];
+    const uint32_t w = prob >> 1, dir = prob & 1;
     const uint32_t S = d.win_S[w];
     if (S == 0) {
         if (tid < 4) d.table[((uint64_t)w * 2 + dir) * 4 + tid] = 0;

@@ -129,6 +129,24 @@ def test_lds_budget_variants(oracle_lib, gpu_ctx, monkeypatch, lds):
     db.free()
 
 
+@pytest.mark.parametrize("path", ["fold", "rows"])
+def test_greedy_pick_paths(oracle_lib, gpu_ctx, monkeypatch, path):
+    """The greedy pick's alternatives give the same bits as the exact-interval
+    pick: every pick through the sequential fp32 fold over terms recomputed
+    from the tables (PF_K3_PATH=fold), and every iteration through the chunked
+    record-row path with the in-LDS fold (PF_K3_PATH=rows)."""
+    from pomfret_amd import Config
+    monkeypatch.setenv("PF_K3_PATH", path)
+    for cov, seed in ((30, 47), (60, 48)):
+        cfg = Config.from_coverage(cov, given=False)
+        b = synth(6, cov, seed, gap_mix=True)
+        ref = oracle_lib.methphase(cfg, b, n_threads=8)
+        db = gpu_ctx.upload(cfg, b)
+        out = db.run()
+        _compare(ref, out, f"{path}{cov}")
+        db.free()
+
+
 @pytest.mark.parametrize("env", [{"PF_K12_CAP": "0"}, {"PF_K12_SMAX": "0"},
                                  {"PF_K12_CAP": "0", "PF_K2_ENTCAP": "0"}, {"PF_K12_CAP": "40"}],
                          ids=["all_reads_fallback", "no_lds_sites", "fallback_hbm_scratch", "mixed"])

@@ -12,7 +12,10 @@ L.LIB_PATH = os.path.join(os.path.dirname(L.LIB_PATH), "libpomfret_amd_prof.so")
 from pomfret_amd import Config, Context  # noqa: E402
 from pomfret_amd.synth import SynthSpec, make_batch  # noqa: E402
 
-names = ["init", "setup", "prefetch", "barrierB", "fold", "keys", "pick", "tail", "barrierA", "fields", "fill_rows", "groupsum"]
+names = ["init", "setup", "publish", "barrierB", "fold(chunked)", "pick fallback", "winner fields", "tail:spans",
+         "barrierA", "fields", "fill_rows", "groupsum",
+         "upkeep:collect", "upkeep:next read", "pick:lcode", "pick_exact",
+         "tail:insert", "tail:hp/untag", "tail:shift", "tail:range update"]
 for cov in (30, 60):
     cfg = Config.from_coverage(cov, given=False)
     b = make_batch(SynthSpec(n_windows=256, coverage=cov, seed=11))
@@ -21,18 +24,18 @@ for cov in (30, 60):
     db.run(); db.run()
     lib = L.lib()
     lib.pf_batch_prof.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
-    raw = np.zeros(256 * 48, np.uint64)
+    raw = np.zeros(256 * 80, np.uint64)
     lib.pf_batch_prof(db.handle, raw.ctypes.data, raw.size)
-    prof = raw[:256 * 32].reshape(256, 2, 16)
-    k12 = raw[256 * 32:].reshape(256, 16).astype(float)
+    prof = raw[:256 * 64].reshape(256, 2, 32)
+    k12 = raw[256 * 64:].reshape(256, 16).astype(float)
     st = db.stats()
-    cnt = prof[:, :, 12:].sum(axis=(0, 1)).astype(float)
-    tot = prof[:, :, :12].sum(axis=(0, 1)).astype(float)
+    cnt = prof[:, :, 12:16].sum(axis=(0, 1)).astype(float)
+    tot = np.concatenate([prof[:, :, :12], prof[:, :, 16:24]], axis=2).sum(axis=(0, 1)).astype(float)
     iters = st[:, :, 2].sum()
     print(f"cov={cov} kernels={ctx.kernel_times()} iters={iters}")
     for n, v in zip(names, tot):
         print(f"  {n:18s} {v/tot.sum()*100:5.1f}%  {v/iters:8.0f} cyc/iter")
-    per = prof[:, :, :12].sum(axis=2).astype(float).ravel()
+    per = (prof[:, :, :12].sum(axis=2) + prof[:, :, 16:24].sum(axis=2)).astype(float).ravel()
     it = st[:, :, 2].astype(float).ravel()
     top = np.argsort(per)[::-1][:6]
     print("  top problems (w,dir): cycles, iters, init cycles, reads, sites, lookups/iter, one_chunk")
