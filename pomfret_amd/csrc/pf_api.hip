@@ -22,13 +22,14 @@
 __global__ void pf_k12_sites_methmers(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
+__global__ void pf_k3_fallback(pf_dev_batch d);
 __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
-#define PF_NKERN 3
-#define PF_IO_HDR 64ull      // status u32[4] | arena counters u64[3] | fallback counter u32 | pad
+#define PF_NKERN 4
+#define PF_IO_HDR 64ull      // status u32[4] | arena counters u64[3] | K2, K3 fallback counters u32 | pad
 
-static const char *k_names[PF_NKERN] = {"pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy"};
+static const char *k_names[PF_NKERN] = {"pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy", "pf_k3_fallback"};
 
 struct pf_ctx {
     int device;
@@ -302,6 +303,7 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
         PUT(p, ord.data(), ord.size()); d.k3_order = p;
     }
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
+    ALLOC(d.k3_fb_list, std::max<uint32_t>(2 * W, 1));
     // one I/O block: the counters zeroed before a run (status, arena
     // counters, fallback counter) followed by everything copied back after it,
     // so a step costs one memset and one D2H copy
@@ -313,6 +315,7 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
         d.keys_ctr = cp; d.big_ctr = cp + 1; d.scr_ctr = cp + 2;
     }
     d.fb_ctr = reinterpret_cast<uint32_t *>(b->io + 40);
+    d.k3_fb_ctr = reinterpret_cast<uint32_t *>(b->io + 44);
     d.table = reinterpret_cast<int32_t *>(b->io + PF_IO_HDR);
     d.win_S = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 32ull * W);
     d.win_nreads = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 36ull * W);
@@ -374,6 +377,9 @@ static int launch_all(pf_dbatch *b, int stages = 3) {
     if (!attr_done) {
         hipError_t e = hipFuncSetAttribute((const void *)pf_k3_greedy,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)pf_k3_fallback, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)d.lds_bytes);
         if (e != hipSuccess) {
             fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u B dynamic LDS): %s\n", d.lds_bytes,
                     hipGetErrorString(e));
@@ -397,6 +403,11 @@ static int launch_all(pf_dbatch *b, int stages = 3) {
     hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], st));
+    // deferred problems (usually none): a grid-stride kernel over the main kernel's list
+    hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_bytes,
+                       st, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[4], st));
     HIPCHK(hipMemcpyAsync(b->h_io, b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
     b->launched = 1;
     return PF_OK;
@@ -429,6 +440,9 @@ extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_
             c->have_times = 1;
         }
         const uint32_t stt = b->W ? b->h_status[0] : 0;
+        if (getenv("PF_DEBUG_FALLBACK"))
+            fprintf(stderr, "[D::pomfret_amd] status 0x%x, K2 fallback reads %u, K3 deferred problems %u\n", stt,
+                    *reinterpret_cast<uint32_t *>(b->h_io + 40), *reinterpret_cast<uint32_t *>(b->h_io + 44));
         if (stt == 0) break;
         if (attempt >= 3 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF))) {
             fprintf(stderr, "[E::pomfret_amd] device status 0x%x\n", stt);

@@ -55,6 +55,7 @@ struct pf_dev_batch {
     /* per-window results of K1 */
     uint32_t *win_S, *win_nreads;
     const uint32_t *k3_order;          /* [2W] greedy problems (w<<1|dir), heaviest first */
+    uint32_t *k3_fb_list, *k3_fb_ctr;  /* problems the main greedy kernel defers to pf_k3_fallback */
     uint32_t *site_pos, *st1_pos, *site_q1;
     uint8_t *len0, *len1;
     uint32_t *rev_ord;                 /* [R] window-local read index, ascending (end, idx) */

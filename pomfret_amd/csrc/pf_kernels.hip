@@ -39,7 +39,16 @@
 // Diagnostic build only (-DPF_K3_PROFILE): per-phase s_memtime cycle shares of
 // the greedy loop, written to d.prof.  The real kernel executes no stamp.
 #ifdef PF_K3_PROFILE
-#define K3_STAMP(i) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+// one asm statement fenced by scheduling barriers, so no code moves across a
+// stamp and each segment owns exactly its instructions (~40 cycles per stamp)
+DEV unsigned long long k3_stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define K3_STAMP(i) do { const unsigned long long t_ = k3_stamp_now(); \
     prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
 #define K3_COUNT(i, v) do { prof_acc[i] += (v); } while (0)
 #define K12_STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
@@ -61,6 +70,12 @@
 
 // ------------------------------------------------------------------------
 // small helpers
+// a value every lane holds alike (LDS-broadcast control words, wave index),
+// moved to an SGPR so the compiler sees it as uniform: scalar branches instead
+// of exec-mask structurisation
+DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+DEV int uni_i(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
 DEV uint64_t lanemask_lt(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
 DEV void wave_sync() {
@@ -1029,7 +1044,6 @@ DEV uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
 // dictionary of methmer keys per site -> dense slot ids (replaces the per-site
 // key lists + linear search of insert_mmrs_to_counts / query_counts_of_mmrs)
-template <bool LDS1>
 DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uint32_t dir,
                  uint64_t *masks, uint32_t *base, uint32_t *sh_scan, K3Ctl &ctl) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1061,6 +1075,14 @@ DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uin
     }
     if (tid == 0) ctl.ntot = carry;
     __syncthreads();
+}
+
+// second half: rewrite every key in place into its slot id (destructive: a
+// problem is committed to a kernel before this)
+DEV void k3_dict_rewrite(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uint32_t dir,
+                         const uint64_t *masks, const uint32_t *base) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t MW = (uint32_t)d.mw;
     for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
         const uint32_t g = 2 * (r0 + i) + dir;
         const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
@@ -1596,11 +1618,11 @@ DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t 
     tg = ((b_gt >> cs) & 1ull) ? 0u : 1u;
 }
 
-template <bool SLDS>
+template <bool SLDS, bool FULL>
 DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S,
                         uint32_t R, const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t ntot = ctl.ntot;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+    const uint32_t ntot = uni(ctl.ntot);
     const int cov_rt = d.win_par[w * 4 + 1];
     const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
     const uint32_t s = d.win_start[w], e = d.win_end[w];
@@ -1612,7 +1634,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     uint32_t sum_mmr = 0, mx_mmr = 0;
 #ifdef PF_K3_PROFILE
     unsigned long long prof_acc[32] = {0};
-    unsigned long long prof_last = __builtin_amdgcn_s_memtime();
+    unsigned long long prof_last = k3_stamp_now();
 #endif
 
     // ---- init tables and per-read state
@@ -1742,13 +1764,13 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     // reference's rescan from i_last, since tags never revert.
     K3_STAMP(0);
     const uint32_t rec_cap = PF_K3_WAVES * m.rcw;
-    if (NC <= 64) {
+    if (!FULL || NC <= 64) {
     // ---- register-resident variant (n_cand <= 64): lane c holds candidate c
     // (scan position, read, methmer count/start/slot offset and the range-
     // clipped lookup span); control state lives in scalars.
-    int il = ctl.i_last;
+    int il = uni_i(ctl.i_last);
     uint32_t failed = 0;
-    uint32_t umin = ctl.min_i, umax = ctl.max_i;
+    uint32_t umin = uni(ctl.min_i), umax = uni(ctl.max_i);
     uint32_t nc = 0;
     uint32_t c_pos = 0, c_rd = 0, c_n = 0, c_st = 0, c_mo = 0;
     uint32_t c_lo = 0, c_len = 0, c_kofs = 0;
@@ -1764,7 +1786,8 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     // region holds float2 terms)
     // exact sums need rows of < 2^13 terms (k3_pick_exact); longer lists
     // take the chunked record-row path with the sequential fold
-    const bool exact_path = ctl.mxlen < 8192u && d.k3_mode != 2u;
+    // (the main kernel only takes windows of < 8192 sites: mxlen <= S)
+    const bool exact_path = !FULL || (uni(ctl.mxlen) < 8192u && d.k3_mode != 2u);
     K3_COUNT(15, exact_path ? 1 : 0);
     bool need_collect = true, stop = false;
     int qn = -1;
@@ -1776,10 +1799,12 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     for (;;) {
     // wavefront 0: candidate list upkeep, then publish the lookup spans
     if (wid == 0) {
+        K3_STAMP(28);
         if (!stop && need_collect) {
             bool done = false;
             for (;;) {
                 if (dir == 0 ? il >= (int)R : il <= 0) { done = true; break; }
+                K3_COUNT(25, 1);
                 q_cnt = k3_qbuild(m, nwords, dir == 0 ? il - 1 : il + 1, dir, lane, qbuf,
                                   q_pos, q_rd, q_nn, q_st, q_mo, q_more, q_cont);
                 const uint32_t take = q_cnt < NC ? q_cnt : NC;
@@ -1789,6 +1814,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 while (found < NC && q_more) {
                     // fewer than n_cand untagged reads in the first 4096 scan
                     // positions: continue the scan entry by entry
+                    K3_COUNT(26, 1);
                     q_cnt = k3_qbuild(m, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
                                       q_more, q_cont);
                     q_head = 0;
@@ -1834,6 +1860,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         qn = -1;
         if (!stop && nc == NC) {
             if (q_head == q_cnt && q_more) {
+                K3_COUNT(27, 1);
                 q_cnt = k3_qbuild(m, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
                                   q_more, q_cont);
                 q_head = 0;
@@ -1861,13 +1888,13 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         K3_STAMP(2);
     }
     __syncthreads();                                           // (A)
-    if (ctl.done) break;
+    if (uni(ctl.done)) break;
     K3_STAMP(8);
     // the previous winner's insert, deferred to here so that the whole
     // workgroup shares it; wavefront 0 has already applied it virtually to
     // its range update
-    if (ctl.ins_n) {
-        k3_insert_all<SLDS>(m, S, ctl.ins_n, ctl.ins_st, ctl.ins_mo, ctl.ins_tg);
+    if (const uint32_t ins_n = uni(ctl.ins_n)) {
+        k3_insert_all<SLDS>(m, S, ins_n, uni(ctl.ins_st), uni(ctl.ins_mo), uni(ctl.ins_tg));
         __syncthreads();                                       // (A2)
     }
     {
@@ -1876,7 +1903,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // each wave per candidate, the waves interleaved along the methmers.
         // The push/positive counts (integer, order-free) are summed in
         // registers, reduced across lanes and waves.
-        const uint32_t ncs = ctl.nc;
+        const uint32_t ncs = uni(ctl.nc);
         const uint32_t ncp = next_pow2(ncs);
         const uint32_t lgn = 31 - __clz(ncp);
         const uint32_t G = 64u >> lgn;
@@ -1886,7 +1913,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         float s0 = 0.f, s1 = 0.f;
         uint32_t lcode = 0;
         bool exact_ok = false;
-        if (exact_path) {
+        if (!FULL || exact_path) {
             K3_COUNT(13, ncs);
             K3_STAMP(9);
             double x0 = 0.0, x1 = 0.0;
@@ -1906,7 +1933,8 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             exact_ok = true;
             K3_STAMP(4);
         } else {
-        const uint32_t lmax = ctl.L;
+        if constexpr (FULL) {
+        const uint32_t lmax = uni(ctl.L);
         // row pitch P (float2) = 4 mod 32: the fold's 16-byte row reads of up
         // to 8 candidates and the fill's 8-lane row segments spread over the
         // LDS banks; chunks of CHK (8 | CHK) terms
@@ -1965,6 +1993,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             K3_STAMP(4);
         }
         }
+        }
         if (wid != 0) continue;
         lcode = exact_ok ? lcp[lane] : lcp[lane] + lcp[64 + lane] + lcp[128 + lane] + lcp[192 + lane];
         const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
@@ -1995,6 +2024,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         K3_STAMP(5);
         if (pick == 2) {
             // nothing could be tagged (:4064-4069): move i_last, rescan
+            K3_COUNT(24, 1);
             K3_STAMP(6);
             if (++failed > 10) stop = true;
             else {
@@ -2108,7 +2138,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         for (int bb = 0; bb < 32; bb++) tot += (uint32_t)__popcll(__ballot((lsum >> bb) & 1)) << bb;
         stx.lookups += tot;
     }
-    } else {
+    } else if constexpr (FULL) {
     // ---- general variant (n_cand > 64): candidate list in LDS, wavefront 0
     if (wid != 0) return;
     k3_collect(m, R, dir, NC, lane, ctl, cd, stx);
@@ -2337,13 +2367,18 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     }
 }
 
-__global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ K3Ctl ctl;
-    __shared__ K3Cand cd;
-    __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
+// hand a problem the main kernel does not take to pf_k3_fallback
+DEV void k3_defer(const pf_dev_batch &d, uint32_t prob) {
+    if (threadIdx.x == 0) d.k3_fb_list[atomicAdd(d.k3_fb_ctr, 1u)] = prob;
+}
+
+// One greedy problem (window w, direction dir) on one workgroup.  FULL =
+// false is the main kernel's slim build: slot dictionary and lists in LDS,
+// n_cand <= 64 (register candidate list), < 8192 sites (exact-interval pick
+// only); anything else is deferred to the FULL build.
+template <bool FULL>
+DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
     const uint32_t tid = threadIdx.x;
-    const uint32_t prob = d.k3_order[blockIdx.x];
     const uint32_t w = prob >> 1, dir = prob & 1;
     const uint32_t S = d.win_S[w];
     if (S == 0) {
@@ -2359,6 +2394,10 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     // ---- P1: slot dictionary
     const uint64_t need1 = align16(8ull * S * MW) + 4ull * S;
     const bool p1_lds = need1 <= d.lds_bytes;
+    if (!FULL && !(p1_lds && d.win_par[w * 4 + 2] <= 64 && S < 8192u && d.k3_mode == 0u)) {
+        k3_defer(d, prob);
+        return;
+    }
     if (tid == 0) {
         ctl.fail = 0;
         ctl.summ = 0;
@@ -2371,16 +2410,19 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
         }
     }
     __syncthreads();
-    if (ctl.fail) return;
-    if (p1_lds) {
-        k3_dict<true>(d, r0, R, S, dir, reinterpret_cast<uint64_t *>(smem),
-                      reinterpret_cast<uint32_t *>(smem + align16(8ull * S * MW)), sh_scan, ctl);
+    if (uni(ctl.fail)) return;
+    uint64_t *masks;
+    uint32_t *mbase;
+    if (!FULL || p1_lds) {
+        masks = reinterpret_cast<uint64_t *>(smem);
+        mbase = reinterpret_cast<uint32_t *>(smem + align16(8ull * S * MW));
     } else {
         uint8_t *g = d.scr + ctl.scr;
-        k3_dict<false>(d, r0, R, S, dir, reinterpret_cast<uint64_t *>(g),
-                       reinterpret_cast<uint32_t *>(g + align16(8ull * S * MW)), sh_scan, ctl);
+        masks = reinterpret_cast<uint64_t *>(g);
+        mbase = reinterpret_cast<uint32_t *>(g + align16(8ull * S * MW));
     }
-    const uint32_t ntot = ctl.ntot;
+    k3_dict(d, r0, R, S, dir, masks, mbase, sh_scan, ctl);
+    const uint32_t ntot = uni(ctl.ntot);
     // sum of methmers over the window's reads (slot-list size)
     uint32_t summ = 0;
     for (uint32_t i = tid; i < R; i += PF_K3_THREADS) summ += d.mmr_n[2ull * (r0 + i) + dir];
@@ -2388,32 +2430,38 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     block_excl_scan<PF_K3_THREADS>(summ, sh_scan, &summ_tot);
 
     // ---- P2: greedy.  Prefer everything in LDS (u16 slot lists), then LDS
-    // tables with slot lists read from the HBM arena, then all in HBM.
+    // tables with slot lists read from the HBM arena, then all in HBM.  The
+    // main kernel's exact-pick path keeps no record rows (rcw = 0).
     uint64_t off[K3_NOFF];
-    const uint32_t rcw_min = 256, rcw_max = 1024;
+    const uint32_t rcw_min = FULL ? 256 : 0, rcw_max = FULL ? 1024 : 0;
     const bool slots_ok = ntot < 0xFFFFu;
     uint64_t need_s = k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
     uint64_t need_n = k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
+    if (!FULL && !((slots_ok && need_s <= d.lds_bytes) || need_n <= d.lds_bytes)) {
+        k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
+        return;
+    }
+    k3_dict_rewrite(d, r0, R, S, dir, masks, mbase);
     const uint32_t *kb = d.keys + kbase;
     if (slots_ok && need_s <= d.lds_bytes) {
         uint64_t base_bytes = off[11];
         (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
         base_bytes = off[11];
-        uint32_t rcw = (uint32_t)((d.lds_bytes - base_bytes) / (12ull * PF_K3_WAVES));
+        uint32_t rcw = FULL ? (uint32_t)((d.lds_bytes - base_bytes) / (12ull * PF_K3_WAVES)) : 0u;
         rcw = rcw > rcw_max ? rcw_max : rcw;
         (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw, off);
         K3Mem m;
         k3_mem(smem, off, rcw, true, kb, m);
-        k3_greedy_body<true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        k3_greedy_body<true, FULL>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
     } else if (need_n <= d.lds_bytes) {
         (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
-        uint32_t rcw = (uint32_t)((d.lds_bytes - off[11]) / (12ull * PF_K3_WAVES));
+        uint32_t rcw = FULL ? (uint32_t)((d.lds_bytes - off[11]) / (12ull * PF_K3_WAVES)) : 0u;
         rcw = rcw > rcw_max ? rcw_max : rcw;
         (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off);
         K3Mem m;
         k3_mem(smem, off, rcw, false, kb, m);
-        k3_greedy_body<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
-    } else {
+        k3_greedy_body<false, FULL>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+    } else if constexpr (FULL) {
         const uint32_t rcw = rcw_min;
         const uint64_t need2 = align16(k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off));
         __syncthreads();
@@ -2424,10 +2472,33 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
             ctl.scr = o;
         }
         __syncthreads();
-        if (ctl.fail) return;
+        if (uni(ctl.fail)) return;
         K3Mem m;
         k3_mem(d.scr + ctl.scr, off, rcw, false, kb, m);
-        k3_greedy_body<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        k3_greedy_body<false, FULL>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+    }
+}
+
+// Main greedy kernel: every problem, heaviest first (k3_order); the slim build.
+__global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ K3Ctl ctl;
+    __shared__ K3Cand cd;
+    __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
+    k3_run<false>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan);
+}
+
+// Problems the main kernel deferred (dictionary or tables beyond the LDS
+// budget, n_cand > 64, >= 8192 sites, test overrides): all variants.
+__global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_fallback(pf_dev_batch d) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ K3Ctl ctl;
+    __shared__ K3Cand cd;
+    __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
+    const uint32_t n = *d.k3_fb_ctr;
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        k3_run<true>(d, d.k3_fb_list[i], smem, ctl, cd, sh_scan);
+        __syncthreads();
     }
 }
 

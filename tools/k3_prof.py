@@ -43,6 +43,10 @@ for cov in (30, 60):
         w, d = divmod(int(i), 2)
         print(f"    ({w},{d}) {per[i]:.3g} {it[i]:.0f} {float(prof[w, d, 0]):.3g} {st[w, d, 6]} {st[w, d, 7]} "
               f"{st[w, d, 0] / max(it[i], 1):.0f} {prof[w, d, 15]}")
+    ev = prof[:, :, 24:28].sum(axis=(0, 1)).astype(float)
+    print(f"  loop back-edge (tail end -> loop top, wave 0): {prof[:, :, 28].sum() / iters:.0f} cyc/iter")
+    print(f"  per iter: failed picks {ev[0]/iters:.3f}  collects {ev[1]/iters:.3f}  "
+          f"collect rebuilds {ev[2]/iters:.3f}  queue refills {ev[3]/iters:.3f}")
     print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
     print(f"  per iter: lmax(chunked) {cnt[0]/iters:.1f}  nc(one-chunk) {cnt[1]/iters:.2f}  "
           f"picks needing the sequential fold {cnt[2]/iters*100:.2f}%")
