@@ -1,35 +1,35 @@
 // pf_kernels.hip -- gfx950 kernels of the methphase hot path.
 //
-// Three launches per batch (reference call stack in SURVEY.md section 3.1):
+// Launches per batch (reference call stack in SURVEY.md section 3.1):
 //
-//   pf_k1_sites    one 1024-thread workgroup per window.
-//                  get_methmer_sites_and_ranges (blockjoin.c:3202-3354) for both
-//                  directions + the left-coverage check of load_reads_given_interval
-//                  (blockjoin.c:1161-1163) + the revbuf end-order (blockjoin.c:1126,1140).
-//                  Per-position meth/unmeth counts are accumulated in a dense
-//                  32768-position LDS tile (no hashing), tiles swept in position
-//                  order so sites come out sorted; every call is labelled with its
-//                  site index for the next kernel.
-//   pf_k2_methmers one wavefront per (read, direction).
-//                  get_mmr_of_read (blockjoin.c:3357-3451), restated as an
-//                  "entry walk": the merged site/call buffer the reference radix
-//                  sorts per read is never materialised; each site entry gets its
-//                  methylation character from the call labels, and each methmer is
-//                  assembled from the characters of the following entries.
-//   pf_k3_greedy   one 256-thread workgroup per (window, direction).
-//                  haplotag_region1 (blockjoin.c:3958-4080) and the 2x2 table of
-//                  evaluate_separation (blockjoin.c:3940-3956).  The per-site methmer
-//                  key lists of the reference (linear search, blockjoin.c:3453-3515)
-//                  are replaced by a dense per-site slot dictionary built once per
-//                  problem, so a lookup is one LDS load; candidate scoring runs over
-//                  (methmer, candidate) pairs in parallel and only the order-sensitive
-//                  float sums (blockjoin.c:3619-3636) run sequentially, one lane per
-//                  candidate, in methmer order.
+//   pf_k12_sites_methmers  one 1024-thread workgroup per window.
+//       Sites: the left-coverage check of load_reads_given_interval
+//       (blockjoin.c:1161-1163), get_methmer_sites_and_ranges (:3202-3354) for
+//       both directions (LDS hash of per-position meth/unmeth counts, site
+//       ranks from a bitmap prefix popcount, the u16 wrap at 4096 emulated) and
+//       the revbuf end-order (:1126, :1140).  Methmers: get_mmr_of_read
+//       (:3357-3451) for every (read, direction) by one wavefront, restated as
+//       an "entry walk" over the site arrays staged in LDS; the merged site/call
+//       buffer the reference radix-sorts per read is never materialised.
+//   pf_k2_methmers  fallback for the reads K12 hands over (site-entry bound
+//       above its wave buffer, windows whose sites do not fit LDS).
+//   pf_k3_greedy    one 256-thread workgroup per (window, direction), heaviest
+//       first.  haplotag_region1 (:3958-4080) and the 2x2 table of
+//       evaluate_separation (:3940-3956).  The per-site methmer key lists of
+//       the reference (linear search, :3453-3515) become a dense per-site slot
+//       dictionary built once per problem, so a lookup is one LDS load.  The
+//       candidate scores are exact fp64 sums of the fp32 terms; the sequential
+//       fp32 sums of the reference (:3619-3636) are only evaluated when the
+//       rounding-error intervals cannot decide the pick.
+//   pf_k3_fallback  the same greedy loop with every variant (tables or slot
+//       lists in HBM, n_cand > 64, chunked record rows) for the problems the
+//       main kernel defers.
 //
-// Bit-exactness notes: fp32 division is IEEE (no fast-math), the score sums are
-// strictly sequential in methmer order, and candidate selection reproduces the
-// stable merge sort + walk-from-end of predict_tags_of_reads (blockjoin.c:3729-3766)
-// as "max score, ties to the later candidate".
+// Bit-exactness notes: fp32 division is IEEE (no fast-math; the reciprocal
+// path is checked over all 2^32 operand pairs), the fallback fold is strictly
+// sequential in methmer order, and candidate selection reproduces the stable
+// merge sort + walk-from-end of predict_tags_of_reads (:3729-3766) as "max
+// score, ties to the later candidate".
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "pf_device.h"
