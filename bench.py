@@ -2,8 +2,9 @@
 """Benchmark of the MI355X methphase hot path (BASELINE.json metric).
 
 One "step" = one pass of the hot path over one batch of windows that is already
-resident in HBM: K1 sites -> K2 methmers -> K3 greedy + 2x2 tables -> D2H ->
-host Fisher test and join decisions (pf_methphase_run).  Workload at N=1 is
+resident in HBM: K12 sites + methmers (+ K2 fallback) -> K3 greedy + 2x2 tables
+(+ K3 fallback) -> D2H -> host Fisher test, join decisions and read tags
+(pf_methphase_launch + pf_methphase_finish, two steps in flight).  Workload at N=1 is
 BASELINE.json configs[1] ("HG002 chr20 30x, pre-haplotagged, 1x MI355X"),
 synthesised (HG002 is not available offline): 256 chr20-like gap windows of
 50 kb at 30x, parameters as `pomfret methphase` derives them without -c
@@ -134,6 +135,7 @@ def main():
     ctx = Context(local_rank)
     db = ctx.upload(cfg, batch)
     out = db.run()
+    outs = [out, db.run()]
     for _ in range(args.warmup):
         db.run(out)
 
@@ -142,10 +144,15 @@ def main():
         dec_t = torch.empty(batch.n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
         gathered = torch.empty(world * batch.n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
 
-    def step():
-        db.run(out)
+    # Steps are pipelined two deep (pf_methphase_launch / _finish): the host
+    # epilogue of step k (Fisher tests, decisions, read tags) overlaps the
+    # kernels of step k+1; every step still runs every kernel, D2H copy and
+    # epilogue inside the timed region.
+    def finish(k):
+        o = outs[k % 2]
+        db.finish(o)
         if dist is not None:
-            dec_t.copy_(torch.from_numpy(out.decision))
+            dec_t.copy_(torch.from_numpy(o.decision))
             dist.all_gather_into_tensor(gathered, dec_t)
 
     if dist is not None:
@@ -153,10 +160,14 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     kern_acc = {}
-    for _ in range(args.steps):
-        step()
-        for k, v in ctx.kernel_times().items():
-            kern_acc[k] = kern_acc.get(k, 0.0) + v
+    if args.steps:
+        db.launch()
+    for k in range(args.steps):
+        if k + 1 < args.steps:
+            db.launch()
+        finish(k)
+        for kn, v in ctx.kernel_times().items():
+            kern_acc[kn] = kern_acc.get(kn, 0.0) + v
     if dist is not None:
         torch.cuda.synchronize()
         dist.barrier()

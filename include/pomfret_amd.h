@@ -174,7 +174,11 @@ uint32_t pf_batch_n_reads(const pf_dbatch_t *db);
  * are applied.  Synchronous. */
 int  pf_methphase_run(pf_ctx_t *ctx, pf_dbatch_t *db, pf_window_out_t *out);
 
-/* Split form of pf_methphase_run for timing: enqueue only / wait + finish. */
+/* Split, pipelined form of pf_methphase_run: pf_methphase_launch enqueues a
+ * run and returns; pf_methphase_finish waits for the oldest unfinished run
+ * and does its host epilogue (Fisher tests, decisions, tags).  Up to two runs
+ * of a batch may be in flight, so the epilogue of one overlaps the kernels of
+ * the next; a third launch before a finish returns PF_ERR_ARG. */
 int  pf_methphase_launch(pf_ctx_t *ctx, pf_dbatch_t *db);
 int  pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *db, pf_window_out_t *out);
 

@@ -27,6 +27,7 @@ __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
 #define PF_NKERN 4
+#define PF_SLOTS 2
 #define PF_IO_HDR 64ull      // status u32[4] | arena counters u64[3] | K2, K3 fallback counters u32 | pad
 
 static const char *k_names[PF_NKERN] = {"pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy", "pf_k3_fallback"};
@@ -52,16 +53,41 @@ struct pf_dbatch {
     // device buffers (owned)
     std::vector<void *> allocs;
     pf_dev_batch d;
-    // host pinned result staging
-    uint8_t *io = nullptr, *h_io = nullptr;   // I/O block (device, pinned host), PF_IO_HDR + 40 W + R bytes
+    // I/O block on the device and its two pinned host slots: launches
+    // alternate between the slots, so the host epilogue of one run overlaps
+    // the kernels of the next (at most PF_SLOTS runs in flight)
+    uint8_t *io = nullptr, *h_io[PF_SLOTS] = {nullptr, nullptr};
     uint64_t io_bytes = 0;
-    int32_t *h_table;
-    uint32_t *h_S, *h_nreads, *h_status;
-    uint8_t *h_hp_fwd;
-    unsigned long long *h_ctr;   // keys, big, scr counters after a run
+    hipEvent_t ev[PF_SLOTS][PF_NKERN + 1];   // kernel boundaries per slot
+    hipEvent_t done[PF_SLOTS];               // slot's D2H complete
+    int have_ev = 0;
+    uint64_t n_launch = 0, n_finish = 0;
     uint64_t site_total;
-    int launched;
 };
+
+// views of one host slot of the I/O block
+struct IoView {
+    uint32_t *status;
+    unsigned long long *ctr;     // keys, big, scr counters after a run
+    uint32_t *fb, *k3fb;
+    int32_t *table;
+    uint32_t *S, *nreads;
+    uint8_t *hp_fwd;
+};
+static IoView io_view(const pf_dbatch *b, int slot) {
+    uint8_t *h = b->h_io[slot];
+    const uint64_t W = b->W;
+    IoView v;
+    v.status = reinterpret_cast<uint32_t *>(h);
+    v.ctr = reinterpret_cast<unsigned long long *>(h + 16);
+    v.fb = reinterpret_cast<uint32_t *>(h + 40);
+    v.k3fb = reinterpret_cast<uint32_t *>(h + 44);
+    v.table = reinterpret_cast<int32_t *>(h + PF_IO_HDR);
+    v.S = reinterpret_cast<uint32_t *>(h + PF_IO_HDR + 32ull * W);
+    v.nreads = reinterpret_cast<uint32_t *>(h + PF_IO_HDR + 36ull * W);
+    v.hp_fwd = h + PF_IO_HDR + 40ull * W;
+    return v;
+}
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "[E::pomfret_amd] %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
@@ -165,7 +191,12 @@ extern "C" void pf_batch_free(pf_dbatch_t *b) {
     (void)hipSetDevice(b->ctx->device);
     (void)hipStreamSynchronize(b->ctx->stream);
     for (void *p : b->allocs) (void)hipFree(p);
-    (void)hipHostFree(b->h_io);
+    for (int i = 0; i < PF_SLOTS; i++) (void)hipHostFree(b->h_io[i]);
+    if (b->have_ev)
+        for (int i = 0; i < PF_SLOTS; i++) {
+            for (int k = 0; k <= PF_NKERN; k++) (void)hipEventDestroy(b->ev[i][k]);
+            (void)hipEventDestroy(b->done[i]);
+        }
     delete b;
 }
 
@@ -196,7 +227,7 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     b->W = W; b->R = R; b->N = N;
     b->h_win_read_off.assign(in->win_read_off, in->win_read_off + (W ? W + 1 : 0));
     b->h_read_hp.assign(in->read_hp, in->read_hp + R);
-    b->launched = 0;
+    b->n_launch = b->n_finish = 0;
     auto fail = [&](int rc) { pf_batch_free(b); return rc; };
 
     // ---- per-window parameters (with the clamps of blockjoin.c:4381-4390)
@@ -353,26 +384,29 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     // fold, or every iteration through the chunked record-row path (tests)
     const char *kp = getenv("PF_K3_PATH");
     d.k3_mode = !kp ? 0u : strcmp(kp, "fold") == 0 ? 1u : strcmp(kp, "rows") == 0 ? 2u : 0u;
-    if (hipHostMalloc((void **)&b->h_io, b->io_bytes) != hipSuccess) return fail(PF_ERR_NOMEM);
-    b->h_status = reinterpret_cast<uint32_t *>(b->h_io);
-    b->h_ctr = reinterpret_cast<unsigned long long *>(b->h_io + 16);
-    b->h_table = reinterpret_cast<int32_t *>(b->h_io + PF_IO_HDR);
-    b->h_S = reinterpret_cast<uint32_t *>(b->h_io + PF_IO_HDR + 32ull * W);
-    b->h_nreads = reinterpret_cast<uint32_t *>(b->h_io + PF_IO_HDR + 36ull * W);
-    b->h_hp_fwd = b->h_io + PF_IO_HDR + 40ull * W;
+    for (int i = 0; i < PF_SLOTS; i++)
+        if (hipHostMalloc((void **)&b->h_io[i], b->io_bytes) != hipSuccess) return fail(PF_ERR_NOMEM);
+    for (int i = 0; i < PF_SLOTS; i++) {
+        for (int k = 0; k <= PF_NKERN; k++)
+            if (hipEventCreate(&b->ev[i][k]) != hipSuccess) return fail(PF_ERR_HIP);
+        if (hipEventCreate(&b->done[i]) != hipSuccess) return fail(PF_ERR_HIP);
+    }
+    b->have_ev = 1;
     *out = b;
     return PF_OK;
 #undef PUT
 #undef ALLOC
 }
 
-static int launch_all(pf_dbatch *b, int stages = 3) {
+// enqueue one run of the kernels on the context's stream, timing events and
+// results into host slot `slot` (stages < 3: debug runs without the D2H)
+static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     pf_ctx *c = b->ctx;
     pf_dev_batch &d = b->d;
     hipStream_t st = c->stream;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(b->io, 0, PF_IO_HDR, st));
-    if (b->W == 0) { b->launched = 1; return PF_OK; }
+    if (b->W == 0) { HIPCHK(hipEventRecord(b->done[slot], st)); return PF_OK; }
     static int attr_done = 0;
     if (!attr_done) {
         hipError_t e = hipFuncSetAttribute((const void *)pf_k3_greedy,
@@ -388,34 +422,37 @@ static int launch_all(pf_dbatch *b, int stages = 3) {
         attr_done = 1;
     }
     (void)hipGetLastError();
-    HIPCHK(hipEventRecord(c->ev[0], st));
+    HIPCHK(hipEventRecord(b->ev[slot][0], st));
     hipLaunchKernelGGL(pf_k12_sites_methmers, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], st));
-    if (stages < 2) { b->launched = 1; return PF_OK; }
+    HIPCHK(hipEventRecord(b->ev[slot][1], st));
+    if (stages < 2) return PF_OK;
     // fallback reads only (usually none): a grid-stride kernel over K12's list
     const uint64_t waves = 2ull * b->R;
     const uint32_t g2 = (uint32_t)std::min<uint64_t>((waves + PF_K2_WAVES - 1) / PF_K2_WAVES, 512);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[2], st));
-    if (stages < 3) { b->launched = 1; return PF_OK; }
+    HIPCHK(hipEventRecord(b->ev[slot][2], st));
+    if (stages < 3) return PF_OK;
     hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[3], st));
+    HIPCHK(hipEventRecord(b->ev[slot][3], st));
     // deferred problems (usually none): a grid-stride kernel over the main kernel's list
     hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_bytes,
                        st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[4], st));
-    HIPCHK(hipMemcpyAsync(b->h_io, b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
-    b->launched = 1;
+    HIPCHK(hipEventRecord(b->ev[slot][4], st));
+    HIPCHK(hipMemcpyAsync(b->h_io[slot], b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(b->done[slot], st));
     return PF_OK;
 }
 
 extern "C" int pf_methphase_launch(pf_ctx_t *ctx, pf_dbatch_t *b) {
     if (!ctx || !b || b->ctx != ctx) return PF_ERR_ARG;
-    return launch_all(b);
+    if (b->n_launch - b->n_finish >= PF_SLOTS) return PF_ERR_ARG;   // finish one first
+    const int rc = enqueue(b, (int)(b->n_launch % PF_SLOTS));
+    if (rc == PF_OK) b->n_launch++;
+    return rc;
 }
 
 static int grow(pf_dbatch *b, uint8_t **buf, uint64_t *cap, uint64_t need) {
@@ -430,42 +467,47 @@ static int grow(pf_dbatch *b, uint8_t **buf, uint64_t *cap, uint64_t need) {
 }
 
 extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_t *out) {
-    if (!ctx || !b || !out || b->ctx != ctx || !b->launched) return PF_ERR_ARG;
+    if (!ctx || !b || !out || b->ctx != ctx || b->n_finish == b->n_launch) return PF_ERR_ARG;
     pf_ctx *c = ctx;
+    const int slot = (int)(b->n_finish % PF_SLOTS);
+    const IoView v = io_view(b, slot);
+    b->n_finish++;
     for (int attempt = 0;; attempt++) {
-        HIPCHK(hipStreamSynchronize(c->stream));
-        b->launched = 0;
+        HIPCHK(hipEventSynchronize(b->done[slot]));
         if (b->W) {
-            for (int i = 0; i < PF_NKERN; i++) (void)hipEventElapsedTime(&c->last_ms[i], c->ev[i], c->ev[i + 1]);
+            for (int i = 0; i < PF_NKERN; i++)
+                (void)hipEventElapsedTime(&c->last_ms[i], b->ev[slot][i], b->ev[slot][i + 1]);
             c->have_times = 1;
         }
-        const uint32_t stt = b->W ? b->h_status[0] : 0;
+        const uint32_t stt = b->W ? v.status[0] : 0;
         if (getenv("PF_DEBUG_FALLBACK"))
             fprintf(stderr, "[D::pomfret_amd] status 0x%x, K2 fallback reads %u, K3 deferred problems %u\n", stt,
-                    *reinterpret_cast<uint32_t *>(b->h_io + 40), *reinterpret_cast<uint32_t *>(b->h_io + 44));
+                    *v.fb, *v.k3fb);
         if (stt == 0) break;
         if (attempt >= 3 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF))) {
             fprintf(stderr, "[E::pomfret_amd] device status 0x%x\n", stt);
             return PF_ERR_INTERNAL;
         }
+        // an arena overflowed: drain the stream (a later run in flight used
+        // the same arenas and re-runs itself when finished), grow, re-run
+        HIPCHK(hipStreamSynchronize(c->stream));
         pf_dev_batch &d = b->d;
         int rc = 0;
         if (stt & PF_ST_KEYS_OVF) {
             uint8_t *p = (uint8_t *)d.keys;
             uint64_t capb = d.keys_cap * 4;
-            rc = grow(b, &p, &capb, b->h_ctr[0] * 4);
+            rc = grow(b, &p, &capb, v.ctr[0] * 4);
             d.keys = (uint32_t *)p; d.keys_cap = capb / 4;
         }
-        if (!rc && (stt & PF_ST_BIG_OVF)) rc = grow(b, &d.big, &d.big_cap, b->h_ctr[1]);
-        if (!rc && (stt & PF_ST_SCR_OVF)) rc = grow(b, &d.scr, &d.scr_cap, b->h_ctr[2]);
+        if (!rc && (stt & PF_ST_BIG_OVF)) rc = grow(b, &d.big, &d.big_cap, v.ctr[1]);
+        if (!rc && (stt & PF_ST_SCR_OVF)) rc = grow(b, &d.scr, &d.scr_cap, v.ctr[2]);
         if (rc) return rc;
-        rc = launch_all(b);
+        rc = enqueue(b, slot);
         if (rc) return rc;
     }
     if (out->win_n_reads)
-        for (uint32_t w = 0; w < b->W; w++) out->win_n_reads[w] = b->h_nreads[w];
-    pf_decide_windows(b->W, b->h_win_read_off.data(), b->h_S, b->h_table, b->h_read_hp.data(),
-                      b->h_hp_fwd, out);
+        for (uint32_t w = 0; w < b->W; w++) out->win_n_reads[w] = v.nreads[w];
+    pf_decide_windows(b->W, b->h_win_read_off.data(), v.S, v.table, b->h_read_hp.data(), v.hp_fwd, out);
     return PF_OK;
 }
 
@@ -493,10 +535,10 @@ extern "C" int pf_methphase_windows(int device, const pf_cfg_t *cfg, const pf_wi
 extern "C" int pf_batch_debug_sites(pf_dbatch_t *b, uint32_t w, int dir, uint32_t *real,
                                     uint32_t *starts, uint8_t *lens, uint32_t cap) {
     if (!b || w >= b->W || dir < 0 || dir > 1) return PF_ERR_ARG;
-    int rc = launch_all(b, 1);
+    if (b->n_launch != b->n_finish) return PF_ERR_ARG;       // a run is in flight
+    int rc = enqueue(b, 0, 1);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    b->launched = 0;
     uint32_t S = 0, off_cap[1];
     (void)off_cap;
     HIPCHK(hipMemcpy(&S, b->d.win_S + w, 4, hipMemcpyDeviceToHost));
@@ -514,10 +556,10 @@ extern "C" int pf_batch_debug_sites(pf_dbatch_t *b, uint32_t w, int dir, uint32_
 extern "C" int64_t pf_batch_debug_methmers(pf_dbatch_t *b, int dir, uint32_t *mmr_n, uint32_t *mmr_start,
                                            uint32_t *keys, uint64_t cap) {
     if (!b || dir < 0 || dir > 1) return PF_ERR_ARG;
-    int rc = launch_all(b, 2);
+    if (b->n_launch != b->n_finish) return PF_ERR_ARG;       // a run is in flight
+    int rc = enqueue(b, 0, 2);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    b->launched = 0;
     uint32_t st = 0;
     HIPCHK(hipMemcpy(&st, b->d.status, 4, hipMemcpyDeviceToHost));
     if (st) return PF_ERR_INTERNAL;

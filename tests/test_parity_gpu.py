@@ -175,3 +175,26 @@ def test_methmer_fallback_paths(oracle_lib, gpu_ctx, monkeypatch, env):
             assert np.array_equal(okeys, keys[k0:k0 + len(okeys)])
             k0 += len(okeys)
     db.free()
+
+
+def test_pipelined_launch_finish(oracle_lib, gpu_ctx):
+    """Two runs in flight (pf_methphase_launch x2, then finish x2) give the
+    same bits as pf_methphase_run; a third launch or a finish with nothing in
+    flight is an argument error."""
+    from pomfret_amd import Config, PomfretError
+    cfg = Config.from_coverage(30, given=False)
+    b = synth(6, 30, 51, gap_mix=True)
+    ref = oracle_lib.methphase(cfg, b, n_threads=8)
+    db = gpu_ctx.upload(cfg, b)
+    db.launch()
+    db.launch()
+    with pytest.raises(PomfretError):
+        db.launch()
+    o1 = db.finish()
+    o2 = db.finish()
+    with pytest.raises(PomfretError):
+        db.finish()
+    _compare(ref, o1, "pipelined-1")
+    _compare(ref, o2, "pipelined-2")
+    _compare(ref, db.run(), "after")
+    db.free()
