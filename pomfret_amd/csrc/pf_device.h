@@ -25,7 +25,8 @@
 #define PF_K3_WAVES (PF_K3_THREADS / PF_WAVE)
 #define PF_MAX_NCAND 256
 #define PF_K12_CAPW 512           /* per-wave site-entry buffer of the fused methmer phase */
-#define PF_K12_SMAX 5800          /* sites whose arrays fit LDS beside 16 such buffers */
+#define PF_K12_WB 8               /* bytes per wave-buffer entry: chars, crank, u16 irank, u32 staged key */
+#define PF_K12_SMAX 4600          /* sites whose arrays (14 B/site) fit LDS beside 16 such buffers */
 #define PF_NONE 0xFFFFFFFFu
 
 /* status bits */

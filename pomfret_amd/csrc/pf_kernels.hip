@@ -51,10 +51,10 @@ DEV unsigned long long k3_stamp_now() {
 #define K3_STAMP(i) do { const unsigned long long t_ = k3_stamp_now(); \
     prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
 #define K3_COUNT(i, v) do { prof_acc[i] += (v); } while (0)
-#define K12_STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+#define K12_STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = k3_stamp_now(); \
     d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + (i)] = t_ - k12_t0; k12_t0 = t_; } } while (0)
-#define K2_STAMP(i) do { if (k2acc) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    k2acc[i] += t_ - k2acc[7]; k2acc[7] = t_; } } while (0)
+#define K2_STAMP(i) do { if (k2acc) { const unsigned long long t_ = k3_stamp_now(); \
+    k2acc[i] += t_ - k2acc[9]; k2acc[9] = t_; } } while (0)
 #else
 #define K12_STAMP(i) do { } while (0)
 #define K2_STAMP(i) do { } while (0)
@@ -383,13 +383,16 @@ struct K2Calls {
 
 // site index of each first call (PF_NONE if its position is not a site), once
 // per read for both directions: hash lookup, or lower bound over all sites
-DEV void k2_calls_sites(K2Calls &cl, const uint32_t *sp, uint32_t S, const K2SiteHash *hs) {
+// (the hash is passed by value: a pointer to a local struct would put it on
+// the scratch stack, and every reload's vmcnt wait would drain the next
+// read's prefetched calls)
+DEV void k2_calls_sites(K2Calls &cl, const uint32_t *sp, uint32_t S, const K2SiteHash hs, bool use_hash) {
 #pragma unroll
     for (int u = 0; u < K2_CR; u++) {
         const uint32_t p = cl.pos[u];
         uint32_t si = PF_NONE;
         if (cl.cat[u] < 3u && S > 0 && p >= sp[0] && p <= sp[S - 1]) {
-            if (hs) si = k2_site_of(*hs, p);
+            if (use_hash) si = k2_site_of(hs, p);
             else {
                 uint32_t lo = 0, hi = S;
                 while (lo < hi) {
@@ -456,10 +459,15 @@ DEV void k2_chars_reg(const K2Calls &cl, uint32_t qlo, uint32_t qhi, uint32_t la
 // One read, one direction, one wavefront.  sp = real site positions, st =
 // the direction's sites_starts, lens = its methmer lengths, q1 = dir-1 real
 // index of each start; buffers of capw entries (LDS or HBM scratch).
-DEV void k2_core(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane, uint32_t S,
-                 const uint32_t *sp, const uint32_t *st, const uint8_t *lens, const uint32_t *q1,
-                 uint8_t *chars, uint8_t *crank, uint32_t *irank, uint32_t capw, const K2Read &rd,
-                 const K2Calls *cl, uint64_t koff, unsigned long long *k2acc = nullptr) {
+// With kst, keys go to that LDS staging buffer (the caller copies them to the
+// arena) and the number staged is returned; otherwise straight to the arena.
+template <typename IR>
+DEV uint32_t k2_core(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane, uint32_t S,
+                     const uint32_t *sp, const uint32_t *st, const uint8_t *lens, const uint32_t *q1,
+                     uint8_t *chars, uint8_t *crank, IR *irank, uint32_t capw, const K2Read &rd,
+                     const K2Calls *cl, uint64_t koff, unsigned long long *k2acc = nullptr,
+                     uint32_t *kst = nullptr) {
+    uint32_t staged_n = 0;
     const uint32_t g = 2 * r + dir;
     const uint64_t c0 = rd.c0, c1 = rd.c1;
     uint32_t total = 0, start_i = PF_NONE;
@@ -499,7 +507,7 @@ DEV void k2_core(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane,
                             const uint32_t rk = E + (uint32_t)__popcll(m & lanemask_lt(lane));
                             const uint32_t q = dir ? q1[i] : i;
                             crank[rk] = chars[q - qlo];
-                            irank[rk] = i;
+                            irank[rk] = (IR)i;
                         }
                         E += (uint32_t)__popcll(m);
                     }
@@ -543,7 +551,10 @@ DEV void k2_core(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane,
                                     if (e + Lj <= usable) {
                                         uint32_t key = 0;
                                         for (uint32_t t = 0; t < Lj; t++) key = key << 2 | crank[e + t];
-                                        if (pos < cap && pos < room) out[pos] = key;
+                                        if (pos < cap && pos < room) {
+                                            if (kst) kst[pos] = key;
+                                            else out[pos] = key;
+                                        }
                                         pos++;
                                     }
                                 }
@@ -551,6 +562,8 @@ DEV void k2_core(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane,
                             total += tot;
                         }
                         if (total > cap && lane == 0) atomicOr(d.status, PF_ST_KEYS_OVF);
+                        staged_n = total < cap ? total : cap;
+                        staged_n = staged_n < room ? staged_n : (uint32_t)room;
                         K2_STAMP(3);
                     }
                 }
@@ -561,6 +574,13 @@ DEV void k2_core(const pf_dev_batch &d, uint32_t r, uint32_t dir, uint32_t lane,
         d.mmr_n[g] = total;
         d.mmr_start[g] = total ? start_i : 0;   // store_mmr_of_one_read (:3518-3522)
     }
+    return staged_n;
+}
+
+// copy n staged keys to the arena (lane-strided, coalesced)
+DEV void k2_flush(const pf_dev_batch &d, const uint32_t *kst, uint64_t koff, uint32_t n, uint32_t lane) {
+    uint32_t *out = d.keys + koff;
+    for (uint32_t t = lane; t < n; t += 64) out[t] = kst[t];
 }
 
 // Fallback for reads the fused kernel could not take (site-entry bound above
@@ -932,7 +952,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     // sites), which linear probing makes long at high load
     uint32_t HS = 1;
     while (HS < S * 4) HS <<= 1;
-    const bool use_hash = staged && hash_ok && arr_b + 4u * HS + 16u * 6u * PF_K12_CAPW <= 4u * PF_K1_TILE;
+    const bool use_hash = staged && hash_ok && arr_b + 4u * HS + 16u * PF_K12_WB * PF_K12_CAPW <= 4u * PF_K1_TILE;
     uint32_t *hst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(tile) + arr_b);
     if (use_hash) {
         for (uint32_t j = tid; j < HS; j += NT) hst[j] = PF_NONE;
@@ -948,13 +968,24 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     hsd.t = hst;
     hsd.mask = HS - 1;
     hsd.pmin = pmin;
-    const K2SiteHash *hsp = use_hash ? &hsd : nullptr;
+
     if (staged) {
-        uint8_t *wb = reinterpret_cast<uint8_t *>(tile) + arr_b + (use_hash ? 4u * HS : 0u) + wid * 6ull * PF_K12_CAPW;
+        // per-wave buffers: chars, crank (u8), irank (u16), key staging (u32)
+        uint8_t *wb = reinterpret_cast<uint8_t *>(tile) + arr_b + (use_hash ? 4u * HS : 0u) +
+                      wid * (uint64_t)PF_K12_WB * PF_K12_CAPW;
         uint8_t *chars = wb, *crank = wb + PF_K12_CAPW;
-        uint32_t *irank = reinterpret_cast<uint32_t *>(wb + 2 * PF_K12_CAPW);
+        uint16_t *irank = reinterpret_cast<uint16_t *>(wb + 2 * PF_K12_CAPW);
+        uint32_t *kst = reinterpret_cast<uint32_t *>(wb + 4 * PF_K12_CAPW);
+        // keys are staged in LDS and copied out at points where no prefetched
+        // load is younger than the copy: vmcnt counts loads and stores in
+        // issue order, so a load issued before a dynamic number of stores can
+        // only be waited for with vmcnt(0), which drains the stores too.  The
+        // dir-1 keys of read i are copied out after read i+1's prefetched
+        // calls have been consumed, just before read i+2's are issued.
+        uint32_t pend_n = 0;
+        uint64_t pend_off = 0;
 #ifdef PF_K3_PROFILE
-        unsigned long long k2a[8] = {0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
+        unsigned long long k2a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
         unsigned long long *k2acc = wid == 0 ? k2a : nullptr;
 #else
         unsigned long long *k2acc = nullptr;
@@ -970,32 +1001,42 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
         for (uint32_t i = wid; i < R; i += NW) {
             const uint32_t r = r0 + i;
             K2_STAMP(6);
+            K2Read rd = rdA;
+            const uint64_t nc = rd.c1 - rd.c0;
+            const bool regs = rd.cap <= d.k12_capw && nc <= 64ull * K2_CR;
+            K2Calls cl;
+            if (regs) {
+                k2_finish_calls(rd.c0, rd.c1, lane, pA, tA, cl);
+                // last call position (sorted order) from the registers
+                uint32_t mc = 0;
+                if (nc) {
+                    const uint32_t ul = (uint32_t)((nc - 1) >> 6), ll = (uint32_t)((nc - 1) & 63);
+#pragma unroll
+                    for (int u = 0; u < K2_CR; u++)
+                        if ((uint32_t)u == ul) mc = rdl(cl.pos[u], ll);
+                }
+                rd.maxcall = mc;
+                k2_calls_sites(cl, sp, S, hsd, use_hash);
+            }
+            K2_STAMP(4);
+            k2_flush(d, kst, pend_off, pend_n, lane);
+            pend_n = 0;
             K2Read rdC = {0, 0, 0, 0, 0, 0};
             if (i + 2 * NW < R) k2_load_scalars(d, r0 + i + 2 * NW, rdC);
             k2_issue_calls(d, i + NW < R ? rdB : K2Read{0, 0, 0, 0, 0, 0}, lane, pB, tB);
-            K2Read rd = rdA;
+            K2_STAMP(8);
             if (rd.cap > d.k12_capw) {
                 if (lane == 0) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r;
             } else {
                 const uint64_t k0 = d.mmr_off[2ull * r], k1 = d.mmr_off[2ull * r + 1];
-                const uint64_t nc = rd.c1 - rd.c0;
-                if (nc <= 64ull * K2_CR) {
-                    K2Calls cl;
-                    k2_finish_calls(rd.c0, rd.c1, lane, pA, tA, cl);
-                    // last call position (sorted order) from the registers
-                    uint32_t mc = 0;
-                    if (nc) {
-                        const uint32_t ul = (uint32_t)((nc - 1) >> 6), ll = (uint32_t)((nc - 1) & 63);
-#pragma unroll
-                        for (int u = 0; u < K2_CR; u++)
-                            if ((uint32_t)u == ul) mc = rdl(cl.pos[u], ll);
-                    }
-                    rd.maxcall = mc;
-                    k2_calls_sites(cl, sp, S, hsp);
-                    K2_STAMP(4);
-                    k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW, rd, &cl, k0, k2acc);
+                if (regs) {
+                    const uint32_t n0 = k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW,
+                                                rd, &cl, k0, k2acc, kst);
+                    k2_flush(d, kst, k0, n0, lane);
                     K2_STAMP(5);
-                    k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd, &cl, k1, k2acc);
+                    pend_n = k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd,
+                                     &cl, k1, k2acc, kst);
+                    pend_off = k1;
                     K2_STAMP(5);
                 } else {
                     rd.maxcall = nc ? d.call_pos[rd.c1 - 1] : 0u;
@@ -1007,9 +1048,15 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
             rdB = rdC;
 #pragma unroll
             for (int u = 0; u < K2_CR; u++) { pA[u] = pB[u]; tA[u] = tB[u]; }
+            K2_STAMP(7);
         }
+        k2_flush(d, kst, pend_off, pend_n, lane);
 #ifdef PF_K3_PROFILE
-        if (tid == 0) for (int j = 0; j < 7; j++) d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 8 + j] = k2a[j];
+        if (tid == 0) {
+            for (int j = 0; j < 7; j++) d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 8 + j] = k2a[j];
+            d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 7] = k2a[7];
+            d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 15] = k2a[8];
+        }
 #endif
     } else {
         for (uint32_t i = tid; i < R; i += NT) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r0 + i;

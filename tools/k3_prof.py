@@ -50,13 +50,16 @@ for cov in (30, 60):
     print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
     print(f"  per iter: lmax(chunked) {cnt[0]/iters:.1f}  nc(one-chunk) {cnt[1]/iters:.2f}  "
           f"picks needing the sequential fold {cnt[2]/iters*100:.2f}%")
-    names12 = ["-", "T7+range", "sites", "revbuf", "dir arrays", "reservation", "methmers", "-"]
+    names12 = ["-", "T7+range", "sites", "revbuf", "dir arrays", "reservation", "methmers"]
     mx = k12.sum(axis=1).argmax()
     print("  K12 phases, cycles: mean over windows | slowest window")
     for j in range(1, 7):
         print(f"    {names12[j]:12s} {k12[:, j].mean():10.0f} | {k12[mx, j]:10.0f}")
-    k2n = ["pre->chars", "chars", "entries", "emission", "dir0 tail", "between dirs/tail", "read setup"]
+    k2n = ["lb + ranges", "chars", "entries", "emission", "calls: flags+sites", "core tails",
+           "loop back-edge"]
     print("  K12 methmer phase, wave 0, cycles summed over its reads: mean over windows")
     for j in range(7):
         print(f"    {k2n[j]:18s} {k12[:, 8 + j].mean():10.0f}")
+    print(f"    {'loop end (moves)':18s} {k12[:, 7].mean():10.0f}")
+    print(f"    {'prefetch issue':18s} {k12[:, 15].mean():10.0f}")
     db.free(); ctx.close()
