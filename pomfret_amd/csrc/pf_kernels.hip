@@ -1665,25 +1665,22 @@ DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t 
     tg = ((b_gt >> cs) & 1ull) ? 0u : 1u;
 }
 
-template <bool SLDS, bool FULL>
-DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S,
-                        uint32_t R, const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
+// Problem set-up shared by both greedy bodies: tables zeroed, per-read
+// state, slot-list offsets (and the u16 LDS copy), reference reads seeding the
+// counts (insert_ref_reads_methmer_counts, :3776-3810), the initial range,
+// the T5 round trip and the untagged bitmask.
+template <bool SLDS>
+DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
+                 const K3Mem &m, K3Ctl &ctl, uint32_t *sh_scan, K3Stats &stx) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
     const uint32_t ntot = uni(ctl.ntot);
     const int cov_rt = d.win_par[w * 4 + 1];
-    const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
     const uint32_t s = d.win_start[w], e = d.win_end[w];
     const uint32_t nwords = (R + 63) >> 6;
     const uint64_t sb = d.win_site_off[w];
     const uint64_t kbase = d.mmr_off[2ull * r0];
     const uint32_t *kb = d.keys + kbase;
-    K3Stats stx = {0, 0, 0, 0};
     uint32_t sum_mmr = 0, mx_mmr = 0;
-#ifdef PF_K3_PROFILE
-    unsigned long long prof_acc[32] = {0};
-    unsigned long long prof_last = k3_stamp_now();
-#endif
-
     // ---- init tables and per-read state
     for (uint32_t j = tid; j < ntot; j += PF_K3_THREADS) m.cnt[j] = 0;
     for (uint32_t j = tid; j < S; j += PF_K3_THREADS) m.sum[j] = 0;
@@ -1803,6 +1800,321 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     }
     stx.inserts = ctl.tab[0];
     __syncthreads();
+}
+
+// 2x2 table, per-read tags of direction 0 and the statistics (wave 0)
+DEV void k3_finish(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
+                   const K3Mem &m, const K3Ctl &ctl, const K3Stats &stx) {
+    const uint32_t lane = threadIdx.x & 63;
+    // ---- 2x2 table on the opposite side's strict reads (evaluate_separation, :3940-3956)
+    int tab0 = 0, tab1 = 0, tab2 = 0, tab3 = 0;
+    uint32_t nstrict = 0;
+    const uint32_t strict = dir == 0 ? FLG_RIGHT_STRICT : FLG_LEFT_STRICT;
+    for (uint32_t i = lane; i < R; i += 64) {
+        if (m.flg[i] & strict) {
+            nstrict++;
+            const uint32_t ref = d.read_hp[r0 + i], q = m.hp[i];
+            if (ref <= 1 && q <= 1) {
+                const uint32_t k = ref * 2 + q;
+                tab0 += k == 0; tab1 += k == 1; tab2 += k == 2; tab3 += k == 3;
+            }
+        }
+        if (dir == 0) d.hp_fwd[r0 + i] = m.hp[i];
+    }
+    uint32_t tsum[5] = {(uint32_t)tab0, (uint32_t)tab1, (uint32_t)tab2, (uint32_t)tab3, nstrict};
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        uint32_t tot = 0;
+        for (int bb = 0; bb < 16; bb++) tot += (uint32_t)__popcll(__ballot((tsum[k] >> bb) & 1)) << bb;
+        tsum[k] = tot;
+    }
+    if (lane < 4) d.table[((uint64_t)w * 2 + dir) * 4 + lane] = (int32_t)tsum[lane];
+    if (lane == 0) {
+        unsigned long long *sp = d.stats + ((uint64_t)w * 2 + dir) * PF_NSTAT;
+        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
+        sp[4] = ctl.summ; sp[5] = tsum[4]; sp[6] = R; sp[7] = S;
+    }
+}
+
+
+// update_range (:3669-3704) on register copies of [min_i, max_i): both ends
+// in one ballot, lanes 0-31 walk left from min_i, lanes 32-63 right from max_i
+DEV void k3_range_regs(const K3Mem &m, uint32_t S, int cov_rt, uint32_t lane, uint32_t &umin, uint32_t &umax) {
+    auto cov_ok = [&](int ii) -> bool {
+        const uint32_t v = m.sum[ii];
+        return (int)((v & 0xffffu) + (v >> 16)) >= cov_rt;
+    };
+    const int m0 = (int)umin, M0 = (int)umax;
+    const bool left = lane < 32;
+    const int i = left ? m0 - (int)lane : M0 + (int)(lane - 32);
+    bool cvg = false;
+    if (left ? (m0 >= 0 && i >= 0) : (M0 >= 0 && i < (int)S)) cvg = cov_ok(i);
+    const uint64_t b = __ballot(cvg);
+    const uint32_t bl = (uint32_t)b, br = (uint32_t)(b >> 32);
+    int cl = bl == ~0u ? 32 : __ffs(~bl) - 1;
+    int cr = br == ~0u ? 32 : __ffs(~br) - 1;
+    if (cl == 32) {
+        for (;;) {
+            const int ii = m0 - cl - (int)lane;
+            const uint64_t b2 = __ballot(ii >= 0 && cov_ok(ii));
+            if (b2 == ~0ull) { cl += 64; continue; }
+            cl += __ffsll((unsigned long long)~b2) - 1;
+            break;
+        }
+    }
+    if (cr == 32) {
+        for (;;) {
+            const int ii = M0 + cr + (int)lane;
+            const uint64_t b2 = __ballot(ii < (int)S && cov_ok(ii));
+            if (b2 == ~0ull) { cr += 64; continue; }
+            cr += __ffsll((unsigned long long)~b2) - 1;
+            break;
+        }
+    }
+    if (m0 >= 0 && cl > 0) umin = (uint32_t)(m0 - cl + 1);
+    if (M0 >= 0 && cr > 0) umax = (uint32_t)(M0 + cr - 1);
+}
+
+// Greedy loop of the main kernel (register candidate list, exact pick).  All
+// four waves run the control flow of haplotag_region1 (:4032-4071)
+// redundantly -- identical register copies of the candidate list, the queue
+// and the range -- so nothing is published between waves; two barriers per
+// iteration: after the term fill (B) and after the winner's insert (X).
+template <bool SLDS>
+DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
+                        const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+    const int cov_rt = d.win_par[w * 4 + 1];
+    const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
+    const uint32_t nwords = (R + 63) >> 6;
+    K3Stats stx = {0, 0, 0, 0};
+#ifdef PF_K3_PROFILE
+    unsigned long long prof_acc[32] = {0};
+    unsigned long long prof_last = k3_stamp_now();
+#endif
+    k3_init<SLDS>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
+    K3_STAMP(0);
+    int il = uni_i(ctl.i_last);
+    uint32_t failed = 0;
+    uint32_t umin = uni(ctl.min_i), umax = uni(ctl.max_i);
+    uint32_t nc = 0;
+    uint32_t c_pos = 0, c_rd = 0, c_n = 0, c_st = 0, c_mo = 0;
+    uint32_t q_pos = 0, q_rd = 0, q_nn = 0, q_st = 0, q_mo = 0;
+    uint32_t q_cnt = 0, q_head = 0;
+    bool q_more = false;
+    int q_cont = 0;
+    uint32_t *qbuf = cd.read + 64 * wid;                 // per-wave queue scratch
+    uint32_t lsum = 0;
+    bool need_collect = true, have_win = false;
+    // per-candidate totals, double-buffered by iteration parity: exact fp64
+    // hap sums [2][128] and push/positive count pairs [2][64]
+    double *accd = reinterpret_cast<double *>(cd.key);
+    uint32_t *lcp = cd.pos;
+    accd[tid] = 0.0;
+    if (tid < 128) lcp[tid] = 0u;
+    uint32_t par = 0;
+    __syncthreads();
+    for (;;) {
+        // ---- range after the last insert (update_available_methmer_range)
+        if (have_win) k3_range_regs(m, S, cov_rt, lane, umin, umax);
+        // ---- candidate list: full collection from i_last (:4037-4051)
+        if (need_collect) {
+            bool done = false;
+            for (;;) {
+                if (dir == 0 ? il >= (int)R : il <= 0) { done = true; break; }
+                q_cnt = k3_qbuild(m, nwords, dir == 0 ? il - 1 : il + 1, dir, lane, qbuf,
+                                  q_pos, q_rd, q_nn, q_st, q_mo, q_more, q_cont);
+                const uint32_t take = q_cnt < NC ? q_cnt : NC;
+                c_pos = q_pos; c_rd = q_rd; c_n = q_nn; c_st = q_st; c_mo = q_mo;
+                q_head = take;
+                uint32_t found = take;
+                while (found < NC && q_more) {
+                    q_cnt = k3_qbuild(m, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
+                                      q_more, q_cont);
+                    q_head = 0;
+                    while (found < NC && q_head < q_cnt) {
+                        const uint32_t a0 = rdl(q_pos, q_head), a1 = rdl(q_rd, q_head), a2 = rdl(q_nn, q_head);
+                        const uint32_t a3 = rdl(q_st, q_head), a4 = rdl(q_mo, q_head);
+                        if (lane == found) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; }
+                        found++;
+                        q_head++;
+                    }
+                }
+                if (found == 0) {
+                    stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+                    if (++failed > 10) { done = true; break; }
+                    il += dir == 0 ? (int)NC : -(int)NC;
+                    continue;
+                }
+                nc = found;
+                break;
+            }
+            if (done) break;
+            need_collect = false;
+        }
+        // ---- the next untagged read after the list, for this iteration's append
+        int qn = -1;
+        uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
+        if (nc == NC) {
+            if (q_head == q_cnt && q_more) {
+                q_cnt = k3_qbuild(m, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
+                                  q_more, q_cont);
+                q_head = 0;
+            }
+            if (q_head < q_cnt) {
+                qn = (int)rdl(q_pos, q_head);
+                q_rd1 = rdl(q_rd, q_head); q_n1 = rdl(q_nn, q_head);
+                q_st1 = rdl(q_st, q_head); q_mo1 = rdl(q_mo, q_head);
+                q_head++;
+            }
+        }
+        // ---- lookup spans: sites in [min_i, max_i) (query_counts_of_mmrs, :3500-3501)
+        uint32_t c_len, c_lo, c_kofs;
+        {
+            const uint32_t lo = c_st > umin ? c_st : umin;
+            const uint32_t hi0 = c_st + c_n;
+            const uint32_t hi = hi0 < umax ? hi0 : umax;
+            c_len = lane < nc && hi > lo && umin != 0xFFFFFFFFu ? hi - lo : 0;
+            c_lo = lo;
+            c_kofs = c_mo + (c_len ? lo - c_st : 0);
+        }
+        lsum += c_len;
+        if (nc >= NC) {
+            const uint32_t pl = rdl(c_pos, NC - 1);
+            stx.scanned += dir == 0 ? pl - (uint32_t)il + 1 : (uint32_t)il - pl + 1;
+        } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+        stx.iters++;
+        K3_STAMP(2);
+        // ---- term fill: G = 64/ncp lanes of each wave per candidate, the waves
+        // interleaved along the methmers; exact fp64 sums and the integer
+        // push/positive counts per lane, reduced with LDS atomics
+        {
+            const uint32_t ncp = next_pow2(nc);
+            const uint32_t lgn = 31 - __clz(ncp);
+            const uint32_t G = 64u >> lgn;
+            const uint32_t fc = lane & (ncp - 1), fj = lane >> lgn;
+            const uint32_t J = wid * G + fj, GS = PF_K3_WAVES * G;
+            const uint32_t f_lo = (uint32_t)__shfl((int)c_lo, (int)fc, 64);
+            const uint32_t f_len = (uint32_t)__shfl((int)c_len, (int)fc, 64);
+            const uint32_t f_kofs = (uint32_t)__shfl((int)c_kofs, (int)fc, 64);
+            double x0 = 0.0, x1 = 0.0;
+            const uint32_t lcode = k3_fill_sums<SLDS>(m, f_lo, f_kofs, J, f_len, GS, x0, x1);
+            if (fc < nc) {
+                atomicAdd(&lcp[par * 64 + fc], lcode);
+                atomicAdd(&accd[par * 128 + fc], x0);
+                atomicAdd(&accd[par * 128 + 64 + fc], x1);
+            }
+            // the other parity's totals start from zero next iteration (its last
+            // readers finished before barrier X)
+            if (wid == 0) {
+                accd[(par ^ 1) * 128 + lane] = 0.0;
+                accd[(par ^ 1) * 128 + 64 + lane] = 0.0;
+                lcp[(par ^ 1) * 64 + lane] = 0u;
+            }
+        }
+        K3_STAMP(10);
+        __syncthreads();                                           // (B)
+        K3_STAMP(3);
+        // ---- pick (every wave alike): use_mmr_count_predict_tag_for_one_read
+        // (:3637-3655) and predict_tags_of_reads (:3729-3766), from the exact
+        // sums with rounding-error intervals, else the sequential fp32 fold
+        uint32_t pick = 0, cw = 0, tg = 0;
+        bool folded = false;
+        {
+            const uint32_t lcode = lcp[par * 64 + lane];
+            const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
+            k3_pick_exact(accd + par * 128, lane, nc, c_len, l0, l1, pick, cw, tg);
+            K3_COUNT(14, pick == 0 ? 1u : 0u);
+            if (pick == 0) {
+                folded = true;
+                float s0 = 0.f, s1 = 0.f;
+                if (lane < nc) k3_fold_direct<SLDS>(m, c_lo, c_kofs, c_len, s0, s1);
+                const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
+                const bool elig = lane < nc && !(diff < 3.f && (l0 < 3 || l1 < 3));
+                const uint32_t hkey = elig ? __float_as_uint(diff) + 1u : 0u;
+                const uint32_t hmax = wave_max_dpp(hkey);
+                if (hmax == 0) pick = 2;
+                else {
+                    pick = 1;
+                    cw = 63u - (uint32_t)__clzll((long long)__ballot(hkey == hmax));
+                    tg = rdl(s0 > s1 ? 0u : 1u, cw);
+                }
+            }
+        }
+        par ^= 1;
+        K3_STAMP(19);
+        if (pick == 2) {
+            // nothing could be tagged (:4064-4069): move i_last, rescan
+            if (++failed > 10) break;
+            il += dir == 0 ? (int)NC : -(int)NC;
+            need_collect = true;
+            have_win = false;
+            __syncthreads();                                       // (X): totals reused
+            continue;
+        }
+        // ---- the winner: tag, list minus the winner plus the queued read
+        const uint32_t rd = rdl(c_rd, cw), n = rdl(c_n, cw), st = rdl(c_st, cw), mo = rdl(c_mo, cw);
+        const uint32_t pw = rdl(c_pos, cw);
+        stx.inserts += n;
+        if (wid == 0 && lane == 0) {
+            m.hp[rd] = (uint8_t)tg;
+            m.untag[pw >> 6] &= ~(1ull << (pw & 63));
+        }
+        failed = 0;
+        {
+            const int src = (int)lane + 1;
+            const uint32_t a0 = (uint32_t)__shfl((int)c_pos, src, 64), a1 = (uint32_t)__shfl((int)c_rd, src, 64);
+            const uint32_t a2 = (uint32_t)__shfl((int)c_n, src, 64), a3 = (uint32_t)__shfl((int)c_st, src, 64);
+            const uint32_t a4 = (uint32_t)__shfl((int)c_mo, src, 64);
+            if (lane >= cw) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; }
+        }
+        uint32_t ncn = nc - 1;
+        if (qn >= 0) {
+            if (lane == ncn) { c_pos = (uint32_t)qn; c_rd = q_rd1; c_n = q_n1; c_st = q_st1; c_mo = q_mo1; }
+            ncn++;
+        }
+        nc = ncn;
+        if (nc == 0) need_collect = true;     // an empty batch: the failure path of the reference (:4046-4051)
+        K3_STAMP(20);
+        // ---- insert_mmr_counts of the winner, the whole workgroup (after every
+        // wave's fold, if the pick needed one, has read the tables)
+        if (folded) __syncthreads();
+        k3_insert_all<SLDS>(m, S, n, st, mo, tg);
+        have_win = true;
+        K3_STAMP(21);
+        __syncthreads();                                           // (X)
+        K3_STAMP(8);
+    }
+    {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int bb = 0; bb < 32; bb++) tot += (uint32_t)__popcll(__ballot((lsum >> bb) & 1)) << bb;
+        stx.lookups += tot;
+    }
+    if (wid != 0) return;
+    k3_finish(d, w, dir, r0, S, R, m, ctl, stx);
+#ifdef PF_K3_PROFILE
+    if (lane == 0) {
+        unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 32;
+        for (int i = 0; i < 32; i++) pp[i] = prof_acc[i];
+    }
+#endif
+}
+
+template <bool SLDS, bool FULL>
+DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S,
+                        uint32_t R, const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+    const int cov_rt = d.win_par[w * 4 + 1];
+    const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
+    const uint32_t nwords = (R + 63) >> 6;
+    K3Stats stx = {0, 0, 0, 0};
+#ifdef PF_K3_PROFILE
+    unsigned long long prof_acc[32] = {0};
+    unsigned long long prof_last = k3_stamp_now();
+#endif
+
+    k3_init<SLDS>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
 
     // ---- step 2: greedy extension, one read per iteration (:4032-4071), run by
     // wavefront 0 alone (no workgroup barriers on the serial chain).  The
@@ -2380,33 +2692,8 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     }
     }
 
-    // ---- 2x2 table on the opposite side's strict reads (evaluate_separation, :3940-3956)
-    int tab0 = 0, tab1 = 0, tab2 = 0, tab3 = 0;
-    uint32_t nstrict = 0;
-    const uint32_t strict = dir == 0 ? FLG_RIGHT_STRICT : FLG_LEFT_STRICT;
-    for (uint32_t i = lane; i < R; i += 64) {
-        if (m.flg[i] & strict) {
-            nstrict++;
-            const uint32_t ref = d.read_hp[r0 + i], q = m.hp[i];
-            if (ref <= 1 && q <= 1) {
-                const uint32_t k = ref * 2 + q;
-                tab0 += k == 0; tab1 += k == 1; tab2 += k == 2; tab3 += k == 3;
-            }
-        }
-        if (dir == 0) d.hp_fwd[r0 + i] = m.hp[i];
-    }
-    uint32_t tsum[5] = {(uint32_t)tab0, (uint32_t)tab1, (uint32_t)tab2, (uint32_t)tab3, nstrict};
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        uint32_t tot = 0;
-        for (int bb = 0; bb < 16; bb++) tot += (uint32_t)__popcll(__ballot((tsum[k] >> bb) & 1)) << bb;
-        tsum[k] = tot;
-    }
-    if (lane < 4) d.table[((uint64_t)w * 2 + dir) * 4 + lane] = (int32_t)tsum[lane];
+    k3_finish(d, w, dir, r0, S, R, m, ctl, stx);
     if (lane == 0) {
-        unsigned long long *sp = d.stats + ((uint64_t)w * 2 + dir) * PF_NSTAT;
-        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
-        sp[4] = ctl.summ; sp[5] = tsum[4]; sp[6] = R; sp[7] = S;
 #ifdef PF_K3_PROFILE
         unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 32;
         for (int i = 0; i < 32; i++) pp[i] = prof_acc[i];
@@ -2499,7 +2786,8 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
         (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw, off);
         K3Mem m;
         k3_mem(smem, off, rcw, true, kb, m);
-        k3_greedy_body<true, FULL>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        if constexpr (FULL) k3_greedy_body<true, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        else k3_greedy_slim<true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
     } else if (need_n <= d.lds_bytes) {
         (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
         uint32_t rcw = FULL ? (uint32_t)((d.lds_bytes - off[11]) / (12ull * PF_K3_WAVES)) : 0u;
@@ -2507,7 +2795,8 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
         (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off);
         K3Mem m;
         k3_mem(smem, off, rcw, false, kb, m);
-        k3_greedy_body<false, FULL>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        if constexpr (FULL) k3_greedy_body<false, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        else k3_greedy_slim<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
     } else if constexpr (FULL) {
         const uint32_t rcw = rcw_min;
         const uint64_t need2 = align16(k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off));
