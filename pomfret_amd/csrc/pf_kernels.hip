@@ -1573,11 +1573,17 @@ DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
-            // pushed: key present (cv != 0) and hap total != 0; positive: cnt > 0
-            const bool p0 = cv[u] != 0 && sr[u].z != 0.f, p1 = cv[u] != 0 && sr[u].w != 0.f;
             const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
             const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
-            lcode += (p0 ? 1u + (a0 ? 1u : 0u) : 0u) + ((p1 ? 1u + (a1 ? 1u : 0u) : 0u) << 16);
+            // push/positive counts (:3505-3509, :3619-3624): pushed = key present
+            // (cv != 0) and hap total != 0 (its cached reciprocal is then
+            // nonzero); positive = cnt > 0, which implies pushed.  Both haps
+            // packed per u32 half: min(cnt, 1) in one v_pk_min_u16.
+            uint32_t posc;
+            asm("v_pk_min_u16 %0, %1, %2" : "=v"(posc) : "v"(cv[u]), "s"(0x00010001u));
+            const uint32_t hz = __float_as_uint(sr[u].z), hw = __float_as_uint(sr[u].w);
+            const uint32_t hm = (hz < 1u ? hz : 1u) | ((hw < 1u ? hw : 1u) << 16);
+            lcode += posc + (cv[u] ? hm : 0u);
             e0 += (double)q0;
             e1 += (double)q1;
         }
