@@ -114,6 +114,48 @@ typedef struct pf_window_out {
 } pf_window_out_t;
 
 /* ------------------------------------------------------------------ */
+/* Record-level input: the BAM records each window's region query returned,
+ * decoded on the host (BGZF inflate and record split; htslib's part in the
+ * reference) and kept as raw fields.  The read filters and the 5mC
+ * extraction of load_reads_given_interval / fill_read_meth_record_from_bam_line
+ * / get_mod_poss_on_ref (blockjoin.c:1043-1173, 794-908, 605-792) run on the
+ * device (kernel K0), so the window batch above never exists on the host. */
+
+/* Loader parameters: mmr_config_t's lo/hi/readlen_threshold/min_mapq
+ * (blockjoin.h:7-16; cli defaults lo 100, hi 156, -L 15000, -q 10). */
+typedef struct pf_load_cfg {
+    int32_t min_mapq;     /* reads with core.qual < min_mapq are dropped (1082)        */
+    int32_t min_len;      /* reads with l_qseq < min_len (or < 2) are dropped (1083)   */
+    int32_t qual_lo;      /* ML < lo -> unmeth (1); passed as uint8_t (799, 876-878)   */
+    int32_t qual_hi;      /* ML >= hi -> meth (0); otherwise no-call (2)               */
+} pf_load_cfg_t;
+
+typedef struct pf_aln_batch {
+    uint32_t n_windows;
+    uint32_t n_recs;
+    const uint32_t *win_start;     /* [n_windows] gap start s                             */
+    const uint32_t *win_end;       /* [n_windows] gap end e                               */
+    const uint32_t *win_rec_off;   /* [n_windows+1] records of window w in BAM order      */
+    const int32_t  *win_cov_sel;   /* [n_windows] or NULL -> cfg.cov_for_selection        */
+    const int32_t  *win_cov_rt;    /* [n_windows] or NULL -> cfg.cov_for_runtime          */
+    const int32_t  *win_n_cand;    /* [n_windows] or NULL -> cfg.n_cand                   */
+    const uint16_t *flag;          /* [n_recs] core.flag                                  */
+    const uint8_t  *mapq;          /* [n_recs] core.qual                                  */
+    const uint32_t *pos;           /* [n_recs] core.pos (0-based)                         */
+    const uint32_t *l_qseq;        /* [n_recs] core.l_qseq                                */
+    const float    *de;            /* [n_recs] de:f value, -1 when absent (1079-1080)      */
+    const uint8_t  *hp;            /* [n_recs] get_hp_from_aln (910-923) or the -u table  */
+    const uint64_t *cigar_off;     /* [n_recs+1] into cigar                               */
+    const uint32_t *cigar;         /* BAM encoding len<<4|op                              */
+    const uint64_t *seq_off;       /* [n_recs+1] byte offsets into seq                    */
+    const uint8_t  *seq;           /* BAM 4-bit packed SEQ                                */
+    const uint64_t *mm_off;        /* [n_recs+1] MM:Z (or Mm:Z) text, no terminator       */
+    const char     *mm;
+    const uint64_t *ml_off;        /* [n_recs+1] ML:B:C values; empty = tag absent        */
+    const uint8_t  *ml;
+} pf_aln_batch_t;
+
+/* ------------------------------------------------------------------ */
 /* -u pre-pass: known phased variants of one contig and reads to tag.  */
 
 /* variant ops as in blockjoin.c:28-31 */
@@ -181,6 +223,28 @@ int  pf_methphase_run(pf_ctx_t *ctx, pf_dbatch_t *db, pf_window_out_t *out);
  * the next; a third launch before a finish returns PF_ERR_ARG. */
 int  pf_methphase_launch(pf_ctx_t *ctx, pf_dbatch_t *db);
 int  pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *db, pf_window_out_t *out);
+
+/* Upload record-level input (pf_aln_batch_t).  The records stay resident in
+ * HBM and every run of the batch starts with kernel K0, which applies the
+ * loader's filters and extracts each kept read's 5mC calls on the device;
+ * this call runs K0 once to size the batch.  The batch's reads are the kept
+ * records in record order; pf_batch_read_recs maps them back. */
+int  pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lcfg,
+                         const pf_aln_batch_t *aln, pf_dbatch_t **out);
+/* rec_of_read[i] = record index of read i (n >= pf_batch_n_reads). */
+int  pf_batch_read_recs(const pf_dbatch_t *db, uint32_t *rec_of_read, uint32_t n);
+/* Parity/debug for K0: runs it and copies every read's calls sorted by
+ * (pos, cat) as the methmer kernels consume them (call_off [R+1]), and the
+ * first and last call of each read in get_mod_poss_on_ref's order.  Returns
+ * the number of calls or < 0. */
+int64_t pf_batch_debug_calls(pf_dbatch_t *db, uint64_t *call_off, uint32_t *pos, uint8_t *cat,
+                             uint32_t *first, uint32_t *last, uint64_t cap);
+
+/* K0 counters since upload (count pass + every run), out[0..7]: records
+ * walked by the sequential path, records whose calls needed a sort, records
+ * in implicit-canonical mode, records whose MM/ML could not be decoded,
+ * emission chunks with a duplicate position.  n >= 8. */
+int  pf_batch_load_counters(pf_dbatch_t *db, uint64_t *out, int n);
 
 /* One-shot convenience: upload + run + free on `device`. */
 int  pf_methphase_windows(int device, const pf_cfg_t *cfg,

@@ -17,7 +17,8 @@ import tempfile
 
 import numpy as np
 
-from pomfret_amd.abi import (Config, KnownVars, ReadAlnBatch, WindowBatch, WindowResult)
+from pomfret_amd.abi import (AlnBatch, Config, KnownVars, LoadConfig, ReadAlnBatch, WindowBatch,
+                             WindowResult)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libpf_oracle.so")
@@ -49,6 +50,8 @@ def lib():
         L.orc_search_arr.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_int]
         L.orc_haptag_reads.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.orc_vcf_gaps.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
+        L.orc_load_reads.argtypes = [C.c_void_p, C.c_void_p] + [C.c_void_p] * 8 + [C.c_uint64, C.c_void_p]
+        L.orc_load_reads.restype = C.c_int
         _lib = L
     return _lib
 
@@ -136,3 +139,35 @@ def vcf_gaps(path: str, readback: int = 50_000):
                 key = {"raw": "raw", "gap": "gaps", "dropped": "dropped"}[f[0]]
                 cur[key].append((int(f[1]), int(f[2])))
         return out
+
+
+def load_reads(lcfg: LoadConfig, aln: AlnBatch):
+    """Window loader (a3/a4): the kept reads of every window as a WindowBatch
+    (calls in get_mod_poss_on_ref order) and rec_read[r] (read index or
+    0xFFFFFFFF for dropped records)."""
+    n = aln.n_recs
+    rec_read = np.zeros(max(n, 1), np.uint32)
+    wro = np.zeros(aln.n_windows + 1, np.uint32)
+    rs, re_ = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.uint32)
+    rh = np.zeros(max(n, 1), np.uint8)
+    co = np.zeros(n + 1, np.uint64)
+    cap = int(aln.ml_off[-1]) + int(aln.mm_off[-1]) + int(aln.l_qseq.sum()) // 2 + 16 if n else 16
+    need = C.c_uint64(0)
+    lc, a = lcfg.to_c(), aln.to_c()
+    while True:
+        cp, cc = np.zeros(cap, np.uint32), np.zeros(cap, np.uint8)
+        R = lib().orc_load_reads(C.byref(lc), C.byref(a), rec_read.ctypes.data, wro.ctypes.data, rs.ctypes.data,
+                                 re_.ctypes.data, rh.ctypes.data, co.ctypes.data, cp.ctypes.data, cc.ctypes.data,
+                                 cap, C.byref(need))
+        if R == -2:
+            cap = int(need.value) + 16
+            continue
+        if R < 0:
+            raise RuntimeError(f"oracle load_reads failed: {R}")
+        break
+    N = int(co[R])
+    b = WindowBatch(win_start=aln.win_start, win_end=aln.win_end, win_read_off=wro,
+                    read_start=rs[:R], read_end=re_[:R], read_hp=rh[:R], read_call_off=co[:R + 1],
+                    call_pos=cp[:N], call_cat=cc[:N], win_cov_sel=aln.win_cov_sel,
+                    win_cov_rt=aln.win_cov_rt, win_n_cand=aln.win_n_cand)
+    return b, rec_read[:n]

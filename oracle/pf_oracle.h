@@ -67,6 +67,16 @@ int orc_haptag_reads(const pf_known_vars_t *known, const pf_read_aln_batch_t *re
  * "dropped\ts\te".  Returns number of contigs or <0. */
 int orc_vcf_gaps(const char *vcf_path, int readback, const char *out_path);
 
+/* Window loader (pf_oracle_load.c): filters + 5mC extraction of every
+ * record (load_reads_given_interval, blockjoin.c:1043-1173).  Writes the kept
+ * reads as a pf_window_batch_t (calls in get_mod_poss_on_ref order) and
+ * rec_read[r] = read index or UINT32_MAX.  Returns the number of kept reads,
+ * -1 on a fatal CIGAR operation, -2 if call_cap is too small (*n_calls_out
+ * holds the size needed). */
+int orc_load_reads(const pf_load_cfg_t *lc, const pf_aln_batch_t *A, uint32_t *rec_read, uint32_t *win_read_off,
+                   uint32_t *read_start, uint32_t *read_end, uint8_t *read_hp, uint64_t *call_off,
+                   uint32_t *call_pos, uint8_t *call_cat, uint64_t call_cap, uint64_t *n_calls_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,12 +10,13 @@ mirror of that interface:
     res = methphase_windows(cfg, batch)             # haplotag_region_given_bam x W
     res.decision                                    # ranges->decisions.a[i]
 """
-from .abi import Config, KnownVars, ReadAlnBatch, WindowBatch, WindowResult, HAPTAG_UNPHASED
+from .abi import (AlnBatch, Config, KnownVars, LoadConfig, ReadAlnBatch, WindowBatch, WindowResult,
+                  HAPTAG_UNPHASED)
 from ._lib import (Context, DeviceBatch, PomfretError, device_count, fisher_exact, lib,
                    methphase_windows)
 
 __all__ = [
-    "Config", "KnownVars", "ReadAlnBatch", "WindowBatch", "WindowResult", "HAPTAG_UNPHASED",
+    "AlnBatch", "Config", "KnownVars", "LoadConfig", "ReadAlnBatch", "WindowBatch", "WindowResult", "HAPTAG_UNPHASED",
     "Context", "DeviceBatch", "PomfretError", "device_count", "fisher_exact", "lib",
     "methphase_windows",
 ]

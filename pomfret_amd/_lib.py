@@ -8,11 +8,12 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
-from .abi import (Config, KnownVars, PfCfg, PfKnownVars, PfReadAlnBatch, PfWindowBatch,
-                  PfWindowOut, ReadAlnBatch, WindowBatch, WindowResult)
+from .abi import (AlnBatch, Config, KnownVars, LoadConfig, PfAlnBatch, PfCfg, PfKnownVars, PfLoadCfg,
+                  PfReadAlnBatch, PfWindowBatch, PfWindowOut, ReadAlnBatch, WindowBatch, WindowResult)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libpomfret_amd.so")
@@ -59,6 +60,12 @@ def lib():
         L.pf_batch_debug_methmers.restype = C.c_int64
         L.pf_fisher_exact.argtypes = [C.c_int] * 4 + [C.POINTER(C.c_double)] * 3
         L.pf_fisher_exact.restype = C.c_double
+        L.pf_batch_upload_aln.argtypes = [C.c_void_p, C.POINTER(PfCfg), C.POINTER(PfLoadCfg),
+                                          C.POINTER(PfAlnBatch), C.POINTER(C.c_void_p)]
+        L.pf_batch_read_recs.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
+        L.pf_batch_debug_calls.argtypes = [C.c_void_p] + [C.c_void_p] * 5 + [C.c_uint64]
+        L.pf_batch_debug_calls.restype = C.c_int64
+        L.pf_batch_load_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
         if hasattr(L, "pf_haptag_reads"):
             L.pf_haptag_reads.argtypes = [C.c_void_p, C.POINTER(PfKnownVars),
                                           C.POINTER(PfReadAlnBatch), C.c_void_p]
@@ -254,8 +261,11 @@ class Context:
         _check(lib().pf_ctx_create(int(device), C.byref(h)), "pf_ctx_create")
         self.handle = h
         self.device = device
+        self._batches = weakref.WeakSet()
 
     def close(self):
+        for b in list(self._batches):      # a batch must not outlive its context
+            b.free()
         if self.handle:
             lib().pf_ctx_destroy(self.handle)
             self.handle = None
@@ -268,6 +278,11 @@ class Context:
 
     def upload(self, cfg: Config, batch: WindowBatch) -> "DeviceBatch":
         return DeviceBatch(self, cfg, batch)
+
+    def upload_aln(self, cfg: Config, aln: AlnBatch, lcfg: LoadConfig = None) -> "DeviceBatch":
+        """Record-level batch (pf_batch_upload_aln): K0 loads the reads on
+        the device in every run."""
+        return DeviceBatch(self, cfg, aln, lcfg=lcfg or LoadConfig())
 
     def kernel_times(self):
         names = (C.c_char_p * 8)()
@@ -294,15 +309,47 @@ class Context:
 class DeviceBatch:
     """A window batch resident in HBM (pf_dbatch_t)."""
 
-    def __init__(self, ctx: Context, cfg: Config, batch: WindowBatch):
+    def __init__(self, ctx: Context, cfg: Config, batch, lcfg: LoadConfig = None):
         self.ctx = ctx
         self.n_windows = batch.n_windows
-        self.n_reads = batch.n_reads
         c, b = cfg.to_c(), batch.to_c()
         h = C.c_void_p()
-        _check(lib().pf_batch_upload(ctx.handle, C.byref(c), C.byref(b), C.byref(h)),
-               "pf_batch_upload")
+        if isinstance(batch, AlnBatch):
+            lc = lcfg.to_c()
+            _check(lib().pf_batch_upload_aln(ctx.handle, C.byref(c), C.byref(lc), C.byref(b), C.byref(h)),
+                   "pf_batch_upload_aln")
+        else:
+            _check(lib().pf_batch_upload(ctx.handle, C.byref(c), C.byref(b), C.byref(h)),
+                   "pf_batch_upload")
         self.handle = h
+        self.n_reads = int(lib().pf_batch_n_reads(h))
+        ctx._batches.add(self)
+
+    def read_recs(self) -> np.ndarray:
+        """Record index of every read of the batch (identity for window batches)."""
+        out = np.zeros(max(self.n_reads, 1), np.uint32)
+        _check(lib().pf_batch_read_recs(self.handle, out.ctypes.data, out.size), "pf_batch_read_recs")
+        return out[:self.n_reads]
+
+    def debug_calls(self, cap: int = 1 << 27):
+        """K0 output: (call_off, pos, cat, first, last), calls sorted by (pos, cat) per read."""
+        R = self.n_reads
+        off = np.zeros(R + 1, np.uint64)
+        pos = np.zeros(cap, np.uint32)
+        cat = np.zeros(cap, np.uint8)
+        first = np.zeros(max(R, 1), np.uint32)
+        last = np.zeros(max(R, 1), np.uint32)
+        n = lib().pf_batch_debug_calls(self.handle, off.ctypes.data, pos.ctypes.data, cat.ctypes.data,
+                                       first.ctypes.data, last.ctypes.data, cap)
+        if n < 0:
+            _check(int(n), "pf_batch_debug_calls")
+        return off, pos[:n], cat[:n], first[:R], last[:R]
+
+    def load_counters(self) -> dict:
+        out = np.zeros(8, np.uint64)
+        _check(lib().pf_batch_load_counters(self.handle, out.ctypes.data, 8), "pf_batch_load_counters")
+        return dict(seq_path=int(out[0]), unsorted=int(out[1]), implicit=int(out[2]), bad_mm=int(out[3]),
+                    dup_chunks=int(out[4]))
 
     def free(self):
         if self.handle:

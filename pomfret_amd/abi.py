@@ -321,3 +321,97 @@ class ReadAlnBatch:
         r.seq_off, r.seq_len, r.seq = _ptr(self.seq_off), _ptr(self.seq_len), _ptr(self.seq)
         r.md_off, r.md = _ptr(self.md_off), _ptr(self.md)
         return r
+
+
+class PfLoadCfg(C.Structure):
+    """pf_load_cfg_t (mmr_config_t's loader fields, reference blockjoin.h:7-16)."""
+    _fields_ = [("min_mapq", C.c_int32), ("min_len", C.c_int32),
+                ("qual_lo", C.c_int32), ("qual_hi", C.c_int32)]
+
+
+@dataclass
+class LoadConfig:
+    """Loader parameters; defaults are the CLI's (cli.c:56-70): -q 10, -L 15000,
+    ML bands lo 100 / hi 156."""
+    min_mapq: int = 10
+    min_len: int = 15000
+    qual_lo: int = 100
+    qual_hi: int = 156
+
+    def to_c(self) -> PfLoadCfg:
+        return PfLoadCfg(self.min_mapq, self.min_len, self.qual_lo, self.qual_hi)
+
+
+class PfAlnBatch(C.Structure):
+    _fields_ = [("n_windows", C.c_uint32), ("n_recs", C.c_uint32)] + [
+        (n, C.c_void_p) for n in (
+            "win_start", "win_end", "win_rec_off", "win_cov_sel", "win_cov_rt", "win_n_cand",
+            "flag", "mapq", "pos", "l_qseq", "de", "hp", "cigar_off", "cigar", "seq_off", "seq",
+            "mm_off", "mm", "ml_off", "ml")]
+
+
+_ALN_FIELDS = {
+    "win_start": np.uint32, "win_end": np.uint32, "win_rec_off": np.uint32,
+    "flag": np.uint16, "mapq": np.uint8, "pos": np.uint32, "l_qseq": np.uint32, "de": np.float32,
+    "hp": np.uint8, "cigar_off": np.uint64, "cigar": np.uint32, "seq_off": np.uint64, "seq": np.uint8,
+    "mm_off": np.uint64, "mm": np.uint8, "ml_off": np.uint64, "ml": np.uint8,
+}
+
+
+@dataclass
+class AlnBatch:
+    """Record-level host SoA of a batch of windows (pf_aln_batch_t): the BAM
+    records each window's region query returned, in BAM order."""
+    win_start: np.ndarray
+    win_end: np.ndarray
+    win_rec_off: np.ndarray
+    flag: np.ndarray
+    mapq: np.ndarray
+    pos: np.ndarray
+    l_qseq: np.ndarray
+    de: np.ndarray
+    hp: np.ndarray
+    cigar_off: np.ndarray
+    cigar: np.ndarray
+    seq_off: np.ndarray
+    seq: np.ndarray
+    mm_off: np.ndarray
+    mm: np.ndarray
+    ml_off: np.ndarray
+    ml: np.ndarray
+    win_cov_sel: Optional[np.ndarray] = None
+    win_cov_rt: Optional[np.ndarray] = None
+    win_n_cand: Optional[np.ndarray] = None
+    meta: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        for name, dt in _ALN_FIELDS.items():
+            a = np.ascontiguousarray(getattr(self, name), dtype=dt)
+            if name in ("cigar", "seq", "mm", "ml") and a.size == 0:
+                a = np.zeros(1, dt)      # keep a valid pointer for empty arenas
+            setattr(self, name, a)
+        for name in ("win_cov_sel", "win_cov_rt", "win_n_cand"):
+            v = getattr(self, name)
+            if v is not None:
+                setattr(self, name, np.ascontiguousarray(v, dtype=np.int32))
+
+    @property
+    def n_windows(self) -> int:
+        return int(self.win_start.shape[0])
+
+    @property
+    def n_recs(self) -> int:
+        return int(self.pos.shape[0])
+
+    def to_c(self) -> PfAlnBatch:
+        b = PfAlnBatch()
+        b.n_windows = self.n_windows
+        b.n_recs = self.n_recs
+        for name in _ALN_FIELDS:
+            setattr(b, name, _ptr(getattr(self, name)))
+        for name in ("win_cov_sel", "win_cov_rt", "win_n_cand"):
+            setattr(b, name, _ptr(getattr(self, name)))
+        return b
+
+    def nbytes(self) -> int:
+        return int(sum(getattr(self, n).nbytes for n in _ALN_FIELDS))

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <vector>
 #include "pf_device.h"
+#include "pf_load.h"
 #include "pf_host.h"
 #include "../../include/pomfret_amd.h"
 
@@ -23,14 +24,16 @@ __global__ void pf_k12_sites_methmers(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
 __global__ void pf_k3_fallback(pf_dev_batch d);
+template <int MODE> __global__ void pf_k0_load(pf_load_dev d);
 __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
-#define PF_NKERN 4
+#define PF_NKERN 5
 #define PF_SLOTS 2
 #define PF_IO_HDR 64ull      // status u32[4] | arena counters u64[3] | K2, K3 fallback counters u32 | pad
 
-static const char *k_names[PF_NKERN] = {"pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy", "pf_k3_fallback"};
+static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy",
+                                        "pf_k3_fallback"};
 
 struct pf_ctx {
     int device;
@@ -63,6 +66,11 @@ struct pf_dbatch {
     int have_ev = 0;
     uint64_t n_launch = 0, n_finish = 0;
     uint64_t site_total;
+    // record-level batches (pf_batch_upload_aln): K0 runs first in every launch
+    bool has_aln = false;
+    pf_load_dev ld;
+    std::vector<uint32_t> h_rec_of_read;
+    unsigned long long *k0_ctr = nullptr;
 };
 
 // views of one host slot of the I/O block
@@ -205,6 +213,21 @@ extern "C" uint32_t pf_batch_n_reads(const pf_dbatch_t *b) { return b ? b->R : 0
 
 static int mask_words(int k) { int bits = 2 * k; return bits <= 6 ? 1 : 1 << (bits - 6); }
 
+static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t *first, const uint32_t *last,
+                       const uint32_t *cpos, const uint8_t *ccat, pf_dbatch_t **out);
+
+static int check_windows(const pf_cfg_t *cfg, const pf_window_batch_t *in) {
+    for (uint32_t w = 0; w < in->n_windows; w++) {
+        const uint32_t r0 = in->win_read_off[w], r1 = in->win_read_off[w + 1];
+        if (r1 < r0) return PF_ERR_ARG;
+        if (r1 - r0 > 65535) return PF_ERR_LIMIT;        // 16-bit per-haplotype counters
+        int nc = in->win_n_cand ? in->win_n_cand[w] : cfg->n_cand;
+        if (nc <= 1) nc = 2;
+        if (nc > PF_MAX_NCAND) return PF_ERR_LIMIT;
+    }
+    return PF_OK;
+}
+
 extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_window_batch_t *in,
                                pf_dbatch_t **out) {
     if (!ctx || !cfg || !in || !out) return PF_ERR_ARG;
@@ -230,32 +253,11 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     b->n_launch = b->n_finish = 0;
     auto fail = [&](int rc) { pf_batch_free(b); return rc; };
 
-    // ---- per-window parameters (with the clamps of blockjoin.c:4381-4390)
-    std::vector<int32_t> par(4ull * W);
-    std::vector<uint32_t> read_win(R);
-    std::vector<uint32_t> site_cap(W);
-    std::vector<uint64_t> site_off(W);
-    uint64_t site_total = 0;
-    for (uint32_t w = 0; w < W; w++) {
-        const uint32_t r0 = in->win_read_off[w], r1 = in->win_read_off[w + 1];
-        if (r1 < r0) return fail(PF_ERR_ARG);
-        if (r1 - r0 > 65535) return fail(PF_ERR_LIMIT);  // 16-bit per-haplotype counters
-        int sel = in->win_cov_sel ? in->win_cov_sel[w] : cfg->cov_for_selection;
-        int rt = in->win_cov_rt ? in->win_cov_rt[w] : cfg->cov_for_runtime;
-        int nc = in->win_n_cand ? in->win_n_cand[w] : cfg->n_cand;
-        if (sel <= 0) sel = 1;
-        if (nc <= 1) nc = 2;
-        if (nc > PF_MAX_NCAND) return fail(PF_ERR_LIMIT);
-        par[4 * w] = sel; par[4 * w + 1] = rt; par[4 * w + 2] = nc; par[4 * w + 3] = 0;
-        for (uint32_t r = r0; r < r1; r++) read_win[r] = w;
-        const uint64_t calls = in->read_call_off[r1] - in->read_call_off[r0];
-        // a site needs >= sel meth and >= sel unmeth calls
-        const uint64_t cap = calls / (2ull * (uint64_t)sel) + 1;
-        site_cap[w] = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
-        site_off[w] = site_total;
-        site_total += site_cap[w];
+    // ---- per-window limits (parameter clamps of blockjoin.c:4381-4390 in batch_build)
+    {
+        const int rc = check_windows(cfg, in);
+        if (rc) return fail(rc);
     }
-    b->site_total = site_total;
 
     // ---- reads: first/last call in the caller's order, calls sorted by (pos, cat)
     std::vector<uint32_t> first(R), last(R);
@@ -294,6 +296,41 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
         ccat = scat.data();
     }
 
+    return batch_build(b, in, first.data(), last.data(), cpos, ccat, out);
+}
+
+// Allocate and fill the device side of a batch.  read_start/read_end/first/
+// last/cpos/ccat may be NULL: the arrays are then only allocated (K0 fills
+// them on every run of a record-level batch).
+static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t *first, const uint32_t *last,
+                       const uint32_t *cpos, const uint8_t *ccat, pf_dbatch_t **out) {
+    const pf_cfg_t *cfg = &b->cfg;
+    const uint32_t W = b->W, R = b->R;
+    const uint64_t N = b->N;
+    auto fail = [&](int rc) { pf_batch_free(b); return rc; };
+    std::vector<int32_t> par(4ull * W);
+    std::vector<uint32_t> read_win(R);
+    std::vector<uint32_t> site_cap(W);
+    std::vector<uint64_t> site_off(W);
+    uint64_t site_total = 0;
+    for (uint32_t w = 0; w < W; w++) {
+        const uint32_t r0 = in->win_read_off[w], r1 = in->win_read_off[w + 1];
+        int sel = in->win_cov_sel ? in->win_cov_sel[w] : cfg->cov_for_selection;
+        int rt = in->win_cov_rt ? in->win_cov_rt[w] : cfg->cov_for_runtime;
+        int nc = in->win_n_cand ? in->win_n_cand[w] : cfg->n_cand;
+        if (sel <= 0) sel = 1;
+        if (nc <= 1) nc = 2;
+        par[4 * w] = sel; par[4 * w + 1] = rt; par[4 * w + 2] = nc; par[4 * w + 3] = 0;
+        for (uint32_t r = r0; r < r1; r++) read_win[r] = w;
+        const uint64_t calls = in->read_call_off[r1] - in->read_call_off[r0];
+        // a site needs >= sel meth and >= sel unmeth calls
+        const uint64_t cap = calls / (2ull * (uint64_t)sel) + 1;
+        site_cap[w] = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
+        site_off[w] = site_total;
+        site_total += site_cap[w];
+    }
+    b->site_total = site_total;
+
     pf_dev_batch &d = b->d;
     memset(&d, 0, sizeof(d));
     d.W = W; d.R = R; d.N = N;
@@ -303,6 +340,8 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     int rc = 0;
 #define PUT(field, src, n) do { rc = dev_put(b, &field, src, n); if (rc) return fail(rc); } while (0)
 #define ALLOC(field, n) do { rc = dev_alloc(b, &field, n); if (rc) return fail(rc); } while (0)
+#define PUTA(field, src, n) do { rc = (src) ? dev_put(b, &field, src, n) : dev_alloc(b, &field, n); \
+                                 if (rc) return fail(rc); } while (0)
     {
         uint32_t *p; PUT(p, in->win_start, W); d.win_start = p;
         PUT(p, in->win_end, W); d.win_end = p;
@@ -310,15 +349,15 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
         int32_t *ip; PUT(ip, par.data(), par.size()); d.win_par = ip;
         uint64_t *up; PUT(up, site_off.data(), W); d.win_site_off = up;
         PUT(p, site_cap.data(), W); d.win_site_cap = p;
-        PUT(p, in->read_start, R); d.read_start = p;
-        PUT(p, in->read_end, R); d.read_end = p;
-        PUT(p, first.data(), R); d.read_first = p;
-        PUT(p, last.data(), R); d.read_last = p;
+        PUTA(p, in->read_start, R); d.read_start = p;
+        PUTA(p, in->read_end, R); d.read_end = p;
+        PUTA(p, first, R); d.read_first = p;
+        PUTA(p, last, R); d.read_last = p;
         PUT(p, read_win.data(), R); d.read_win = p;
         uint8_t *bp; PUT(bp, in->read_hp, R); d.read_hp = bp;
         PUT(up, in->read_call_off, R + 1); d.read_call_off = up;
-        PUT(p, cpos, N); d.call_pos = p;
-        PUT(bp, ccat, N); d.call_cat = bp;
+        PUTA(p, cpos, N); d.call_pos = p;
+        PUTA(bp, ccat, N); d.call_cat = bp;
         // greedy problems heaviest first (reads per window, direction 1 --
         // the longer chains -- first on ties): the first wave of workgroups
         // spreads the long chains over distinct CUs and pairs them with the
@@ -395,7 +434,180 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     *out = b;
     return PF_OK;
 #undef PUT
+#undef PUTA
 #undef ALLOC
+}
+
+// ---------------------------------------------------------------------------
+// Record-level batches: raw BAM fields resident in HBM, K0 in front of K12.
+extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lc,
+                                   const pf_aln_batch_t *a, pf_dbatch_t **out) {
+    if (!ctx || !cfg || !lc || !a || !out) return PF_ERR_ARG;
+    *out = nullptr;
+    if (cfg->k < 1 || cfg->k_span < 0) return PF_ERR_ARG;
+    if (cfg->k > 5) return PF_ERR_UNSUPPORTED;
+    const uint32_t W = a->n_windows, n = a->n_recs;
+    if (W && (!a->win_start || !a->win_end || !a->win_rec_off)) return PF_ERR_ARG;
+    if (W && (a->win_rec_off[0] != 0 || a->win_rec_off[W] != n)) return PF_ERR_ARG;
+    if (!W && n) return PF_ERR_ARG;
+    if (n && (!a->flag || !a->mapq || !a->pos || !a->l_qseq || !a->de || !a->hp || !a->cigar_off || !a->cigar ||
+              !a->seq_off || !a->seq || !a->mm_off || !a->mm || !a->ml_off || !a->ml))
+        return PF_ERR_ARG;
+    for (uint32_t w = 0; w < W; w++)
+        if (a->win_rec_off[w + 1] < a->win_rec_off[w]) return PF_ERR_ARG;
+    // record slices: monotone offsets, SEQ long enough for l_qseq
+    std::vector<uint64_t> seq_off(n + 1), scr_off(n + 1);
+    uint64_t so = 0, sc = 0;
+    for (uint32_t r = 0; r < n; r++) {
+        if (a->cigar_off[r + 1] < a->cigar_off[r] || a->mm_off[r + 1] < a->mm_off[r] ||
+            a->ml_off[r + 1] < a->ml_off[r] || a->seq_off[r + 1] < a->seq_off[r])
+            return PF_ERR_ARG;
+        const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
+        if (a->seq_off[r + 1] - a->seq_off[r] < sb) return PF_ERR_ARG;
+        // htslib refuses records whose CIGAR query length differs from l_qseq
+        // (bam_read1); K0's walk relies on it to stay inside SEQ
+        if (!(a->flag[r] & 4) && a->l_qseq[r] && a->cigar_off[r + 1] > a->cigar_off[r]) {
+            uint64_t ql = 0;
+            for (uint64_t c = a->cigar_off[r]; c < a->cigar_off[r + 1]; c++) {
+                const uint32_t op = a->cigar[c] & 15u;
+                if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += a->cigar[c] >> 4;
+            }
+            if (ql != a->l_qseq[r]) return PF_ERR_ARG;
+        }
+        if (a->mm_off[r + 1] - a->mm_off[r] > 0xFFFFFFF0ull || a->ml_off[r + 1] - a->ml_off[r] > 0xFFFFFFF0ull)
+            return PF_ERR_LIMIT;
+        seq_off[r] = so;
+        so += (sb + PF_K0_SEQ_ALIGN + PF_K0_SEQ_ALIGN - 1) & ~(uint64_t)(PF_K0_SEQ_ALIGN - 1);
+        // trigger lists that may exceed the per-wave LDS list get an HBM slice
+        const uint64_t mln = a->ml_off[r + 1] - a->ml_off[r], mlen = a->mm_off[r + 1] - a->mm_off[r];
+        const uint64_t bound = mln ? mln : (mlen + 1) / 2;
+        scr_off[r] = sc;
+        if (bound > PF_K0_TCAP) sc += bound;
+    }
+    seq_off[n] = so;
+    scr_off[n] = sc;
+    HIPCHK(hipSetDevice(ctx->device));
+
+    pf_dbatch *b = new pf_dbatch();
+    b->ctx = ctx;
+    b->cfg = *cfg;
+    b->has_aln = true;
+    auto fail = [&](int rc) { pf_batch_free(b); return rc; };
+    pf_load_dev &ld = b->ld;
+    memset(&ld, 0, sizeof(ld));
+    ld.n_recs = n;
+    ld.min_mapq = (uint32_t)lc->min_mapq;
+    ld.min_len = (uint32_t)lc->min_len;
+    ld.lo = (uint8_t)lc->qual_lo;
+    ld.hi = (uint8_t)lc->qual_hi;
+    const char *fs = getenv("PF_K0_PATH");
+    ld.force_seq = fs && strcmp(fs, "seq") == 0;
+    int rc = 0;
+#define PUT(field, src, cnt) do { rc = dev_put(b, &field, src, cnt); if (rc) return fail(rc); } while (0)
+#define ALLOC(field, cnt) do { rc = dev_alloc(b, &field, cnt); if (rc) return fail(rc); } while (0)
+    {
+        uint16_t *p16; PUT(p16, a->flag, n); ld.flag = p16;
+        uint8_t *p8; PUT(p8, a->mapq, n); ld.mapq = p8;
+        uint32_t *p32; PUT(p32, a->pos, n); ld.pos = p32;
+        PUT(p32, a->l_qseq, n); ld.l_qseq = p32;
+        float *pf; PUT(pf, a->de, n); ld.de = pf;
+        uint64_t *p64; PUT(p64, a->cigar_off, n + 1); ld.cigar_off = p64;
+        PUT(p32, a->cigar, a->cigar_off[n]); ld.cigar = p32;
+        PUT(p64, a->mm_off, n + 1); ld.mm_off = p64;
+        PUT(p8, (const uint8_t *)a->mm, a->mm_off[n]); ld.mm = p8;
+        PUT(p64, a->ml_off, n + 1); ld.ml_off = p64;
+        PUT(p8, a->ml, a->ml_off[n]); ld.ml = p8;
+        PUT(p64, seq_off.data(), n + 1); ld.seq_off = p64;
+        PUT(p64, scr_off.data(), n + 1); ld.scr_off = p64;
+        ALLOC(p32, sc ? sc : 1); ld.scr = p32;
+        // SEQ repacked into 16-byte aligned, padded per-record slices
+        std::vector<uint8_t> sq(so ? so : 1, 0);
+        for (uint32_t r = 0; r < n; r++)
+            memcpy(sq.data() + seq_off[r], a->seq + a->seq_off[r], ((uint64_t)a->l_qseq[r] + 1) / 2);
+        PUT(p8, sq.data(), sq.size()); ld.seq = p8;
+        ALLOC(p32, n); ld.rec_n = p32;
+        ALLOC(p32, n); ld.rec_read = p32;
+        unsigned long long *pc; ALLOC(pc, PF_K0_NCTR); ld.ctr = pc; b->k0_ctr = pc;
+        ALLOC(p32, 1); ld.status = p32;
+    }
+    // ---- count pass: which records are kept, how many calls each
+    std::vector<uint32_t> rec_n(n);
+    uint32_t st = 0;
+    HIPCHK(hipMemsetAsync(ld.status, 0, 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(ld.ctr, 0, PF_K0_NCTR * 8, ctx->stream));
+    if (n) {
+        hipLaunchKernelGGL(pf_k0_load<0>, dim3((n + PF_K0_WAVES - 1) / PF_K0_WAVES), dim3(PF_K0_WAVES * 64), 0,
+                           ctx->stream, ld);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(rec_n.data(), ld.rec_n, 4ull * n, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCHK(hipMemcpyAsync(&st, ld.status, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (getenv("PF_DEBUG_FALLBACK")) {
+        unsigned long long c[PF_K0_NCTR];
+        HIPCHK(hipMemcpy(c, ld.ctr, sizeof(c), hipMemcpyDeviceToHost));
+        fprintf(stderr, "[D::pomfret_amd] K0: seq-path %llu, unsorted %llu, implicit %llu, bad MM %llu, dup chunks %llu\n",
+                c[0], c[1], c[2], c[3], c[4]);
+    }
+    if (st & PF_ST_FATAL_CIGAR) return fail(PF_ERR_ARG);   // the reference exits (blockjoin.c:776-779)
+    if (st & PF_ST_POS_LIMIT) return fail(PF_ERR_LIMIT);    // pos<<3 packing (3398)
+    // ---- kept reads -> the batch's read arrays (host side: offsets, tags)
+    std::vector<uint32_t> rec_read(n, PF_NONE), win_read_off(W + 1, 0);
+    std::vector<uint64_t> call_off(1, 0);
+    std::vector<uint8_t> read_hp;
+    uint32_t R = 0;
+    for (uint32_t w = 0; w < W; w++) {
+        for (uint32_t r = a->win_rec_off[w]; r < a->win_rec_off[w + 1]; r++) {
+            if (rec_n[r] == PF_NONE) continue;
+            rec_read[r] = R++;
+            b->h_rec_of_read.push_back(r);
+            read_hp.push_back(a->hp[r]);
+            call_off.push_back(call_off.back() + rec_n[r]);
+        }
+        win_read_off[w + 1] = R;
+    }
+    b->W = W; b->R = R; b->N = call_off.back();
+    b->h_win_read_off = win_read_off;
+    b->h_read_hp = read_hp;
+    b->n_launch = b->n_finish = 0;
+    {
+        uint32_t *p32; PUT(p32, rec_read.data(), n); ld.rec_read = p32;
+    }
+    pf_window_batch_t in;
+    memset(&in, 0, sizeof(in));
+    in.n_windows = W; in.n_reads = R; in.n_calls = b->N;
+    in.win_start = a->win_start; in.win_end = a->win_end; in.win_read_off = win_read_off.data();
+    in.win_cov_sel = a->win_cov_sel; in.win_cov_rt = a->win_cov_rt; in.win_n_cand = a->win_n_cand;
+    in.read_hp = read_hp.data();
+    in.read_call_off = call_off.data();
+    rc = check_windows(cfg, &in);
+    if (rc) return fail(rc);
+    pf_dbatch_t *res = nullptr;
+    rc = batch_build(b, &in, nullptr, nullptr, nullptr, nullptr, &res);
+    if (rc) return rc;                                      // batch_build freed b
+    // K0's write mode fills the batch's arrays; it shares the batch's status word
+    ld.read_call_off = b->d.read_call_off;
+    ld.call_pos = const_cast<uint32_t *>(b->d.call_pos);
+    ld.call_cat = const_cast<uint8_t *>(b->d.call_cat);
+    ld.read_start = const_cast<uint32_t *>(b->d.read_start);
+    ld.read_end = const_cast<uint32_t *>(b->d.read_end);
+    ld.read_first = const_cast<uint32_t *>(b->d.read_first);
+    ld.read_last = const_cast<uint32_t *>(b->d.read_last);
+    ld.status = b->d.status;
+    *out = res;
+    return PF_OK;
+#undef PUT
+#undef ALLOC
+}
+
+extern "C" int pf_batch_read_recs(const pf_dbatch_t *b, uint32_t *rec_of_read, uint32_t n) {
+    if (!b || !rec_of_read || n < b->R) return PF_ERR_ARG;
+    if (!b->has_aln) {
+        for (uint32_t i = 0; i < b->R; i++) rec_of_read[i] = i;
+        return PF_OK;
+    }
+    memcpy(rec_of_read, b->h_rec_of_read.data(), 4ull * b->R);
+    return PF_OK;
 }
 
 // enqueue one run of the kernels on the context's stream, timing events and
@@ -423,25 +635,33 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     }
     (void)hipGetLastError();
     HIPCHK(hipEventRecord(b->ev[slot][0], st));
+    if (b->has_aln && b->ld.n_recs) {
+        // K0: filters + 5mC extraction of every record into the batch's read/call arrays
+        hipLaunchKernelGGL(pf_k0_load<1>, dim3((b->ld.n_recs + PF_K0_WAVES - 1) / PF_K0_WAVES),
+                           dim3(PF_K0_WAVES * 64), 0, st, b->ld);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(b->ev[slot][1], st));
+    if (stages < 1) return PF_OK;
     hipLaunchKernelGGL(pf_k12_sites_methmers, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][1], st));
+    HIPCHK(hipEventRecord(b->ev[slot][2], st));
     if (stages < 2) return PF_OK;
     // fallback reads only (usually none): a grid-stride kernel over K12's list
     const uint64_t waves = 2ull * b->R;
     const uint32_t g2 = (uint32_t)std::min<uint64_t>((waves + PF_K2_WAVES - 1) / PF_K2_WAVES, 512);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][2], st));
+    HIPCHK(hipEventRecord(b->ev[slot][3], st));
     if (stages < 3) return PF_OK;
     hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][3], st));
+    HIPCHK(hipEventRecord(b->ev[slot][4], st));
     // deferred problems (usually none): a grid-stride kernel over the main kernel's list
     hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_bytes,
                        st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][4], st));
+    HIPCHK(hipEventRecord(b->ev[slot][5], st));
     HIPCHK(hipMemcpyAsync(b->h_io[slot], b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(b->done[slot], st));
     return PF_OK;
@@ -484,7 +704,7 @@ extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_
             fprintf(stderr, "[D::pomfret_amd] status 0x%x, K2 fallback reads %u, K3 deferred problems %u\n", stt,
                     *v.fb, *v.k3fb);
         if (stt == 0) break;
-        if (attempt >= 3 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF))) {
+        if (attempt >= 3 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF | PF_ST_FATAL_CIGAR | PF_ST_POS_LIMIT))) {
             fprintf(stderr, "[E::pomfret_amd] device status 0x%x\n", stt);
             return PF_ERR_INTERNAL;
         }
@@ -614,5 +834,38 @@ extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms
         }
     }
     *n = tot;
+    return PF_OK;
+}
+
+extern "C" int64_t pf_batch_debug_calls(pf_dbatch_t *b, uint64_t *call_off, uint32_t *pos, uint8_t *cat,
+                                        uint32_t *first, uint32_t *last, uint64_t cap) {
+    if (!b || !call_off || !pos || !cat || !first || !last) return PF_ERR_ARG;
+    if (b->n_launch != b->n_finish) return PF_ERR_ARG;       // a run is in flight
+    if (b->N > cap) return PF_ERR_ARG;
+    int rc = enqueue(b, 0, 0);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    uint32_t st = 0;
+    HIPCHK(hipMemcpy(&st, b->d.status, 4, hipMemcpyDeviceToHost));
+    if (st) return PF_ERR_INTERNAL;
+    HIPCHK(hipMemcpy(call_off, b->d.read_call_off, 8ull * (b->R + 1), hipMemcpyDeviceToHost));
+    if (b->N) {
+        HIPCHK(hipMemcpy(pos, b->d.call_pos, 4ull * b->N, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(cat, b->d.call_cat, b->N, hipMemcpyDeviceToHost));
+    }
+    if (b->R) {
+        HIPCHK(hipMemcpy(first, b->d.read_first, 4ull * b->R, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(last, b->d.read_last, 4ull * b->R, hipMemcpyDeviceToHost));
+    }
+    return (int64_t)b->N;
+}
+
+extern "C" int pf_batch_load_counters(pf_dbatch_t *b, uint64_t *out, int n) {
+    if (!b || !out || n < PF_K0_NCTR) return PF_ERR_ARG;
+    for (int i = 0; i < PF_K0_NCTR; i++) out[i] = 0;
+    if (!b->has_aln) return PF_OK;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    HIPCHK(hipMemcpy(out, b->k0_ctr, PF_K0_NCTR * 8, hipMemcpyDeviceToHost));
     return PF_OK;
 }

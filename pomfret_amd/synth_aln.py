@@ -1,0 +1,311 @@
+"""Seeded synthetic BAM records for the record-level path (pf_aln_batch_t).
+
+The window model is synth.py's (lognormal 30+-15 kb
+reads, CpGs every ~100 bp, 70/20/10 % methylated/unmethylated/allele-specific
+sites, 5 % no-calls, HP tags by truth haplotype and window orientation), one
+level lower: every read is a BAM record with a reference sequence, a CIGAR
+with indels and soft clips, a 4-bit SEQ with substitutions and an MM/ML pair
+in the encodings basecallers emit, so the device loader (K0) sees what
+htslib would hand the reference's load_reads_given_interval
+(blockjoin.c:1043-1173):
+
+* reference: random bases with CpGs only where planted (accidental CG broken);
+* reads: indel events at `indel_rate` per base (1-3 bases), substitutions at
+  `sub_rate`, leading/trailing soft clips on `clip_frac` of the reads;
+* calls: every CpG of the read's SEQ (the C for forward reads, the G of the
+  stored CG for reverse reads, i.e. the C of the original read), MM skip
+  counts among all C's of the original read orientation, ML from the call's
+  category band; `implicit_frac` of the reads also call a few non-CpG C's,
+  which switches the reference to its implicit-canonical mode (852-858);
+* MM layouts: "C+m?" alone, "C+h?;C+m?" (ML of h first), combined "C+hm?",
+  "C+m." and a missing ML tag, mixed when `mm_mix` is set;
+* `filt_frac` of the records fail one of the loader's filters (flags
+  4/256/2048, MAPQ, de, length).
+
+Everything is a pure function of (seed, window index).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .abi import HAPTAG_UNPHASED, AlnBatch
+from .synth import _lognormal_params
+
+_NT16 = np.array([1, 2, 4, 8], np.uint8)      # A C G T (internal codes 0..3)
+A_, C_, G_, T_ = 0, 1, 2, 3
+
+
+@dataclass
+class AlnSpec:
+    n_windows: int = 256
+    coverage: float = 30.0
+    gap: int = 50_000
+    readback: int = 50_000
+    mean_len: float = 30_000.0
+    sd_len: float = 15_000.0
+    min_len: int = 15_000
+    max_len: int = 150_000
+    cpg_rate: float = 0.01
+    nocall_frac: float = 0.05
+    untag_frac: float = 0.10
+    seed: int = 1
+    window_stride: int = 600_000
+    base: int = 1_000_000
+    gap_mix: bool = False
+    indel_rate: float = 0.004
+    sub_rate: float = 0.005
+    clip_frac: float = 0.3
+    clip_max: int = 400
+    implicit_frac: float = 0.0
+    filt_frac: float = 0.02
+    mm_mix: bool = False       # mix MM/ML layouts (tests); else "C+h?;C+m?" (dorado 5mCG_5hmCG)
+    len_scale: float = 1.0     # scales read lengths and min_len-sensitive sizes (small tests)
+
+
+def _qual_from_cat(rng, cat):
+    q = np.empty(cat.shape[0], np.uint8)
+    m = cat == 0
+    q[m] = rng.integers(200, 256, m.sum())
+    m = cat == 1
+    q[m] = rng.integers(0, 96, m.sum())
+    m = cat == 2
+    q[m] = rng.integers(100, 156, m.sum())
+    return q
+
+
+def make_aln_window(spec: AlnSpec, w: int):
+    rng = np.random.default_rng([spec.seed, w, 77])
+    gap = spec.gap
+    if spec.gap_mix:
+        gap = int(np.exp(rng.uniform(np.log(5_000), np.log(500_000))))
+    max_len = int(spec.max_len * spec.len_scale)
+    stride = max(spec.window_stride, gap + 2 * spec.readback + 2 * max_len + 10_000)
+    s = spec.base + w * stride
+    e = s + gap
+    f_lo, f_hi = max(0, s - spec.readback), e + spec.readback
+    span_lo, span_hi = f_lo - max_len, f_hi + max_len
+    L = span_hi - span_lo + 16
+
+    # reference with CpGs only where planted
+    ref = rng.integers(0, 4, L).astype(np.uint8)
+    cg = np.flatnonzero((ref[:-1] == C_) & (ref[1:] == G_))
+    ref[cg + 1] = A_
+    n_cpg = rng.poisson(spec.cpg_rate * L)
+    cpg = np.unique(rng.integers(1, L - 3, size=n_cpg))
+    cpg = cpg[np.concatenate([[True], np.diff(cpg) >= 2])]
+    ref[cpg] = C_
+    ref[cpg + 1] = G_
+    cls = rng.random(cpg.shape[0])
+    site_p = np.where(cls < 0.7, 0.95, 0.05)
+    site_asm = cls >= 0.9
+    site_hap = rng.integers(0, 2, cpg.shape[0])
+    site_of = np.full(L, -1, np.int64)
+    site_of[cpg] = np.arange(cpg.shape[0])
+
+    # reads (reference spans), tags as synth.py
+    mu, sig = _lognormal_params(spec.mean_len * spec.len_scale, spec.sd_len * spec.len_scale)
+    n_draw = int(spec.coverage * (span_hi - span_lo) / (spec.mean_len * spec.len_scale))
+    starts = rng.integers(span_lo, f_hi, size=n_draw, dtype=np.int64)
+    lens = np.clip(np.exp(rng.normal(mu, sig, n_draw)), spec.min_len * spec.len_scale, max_len).astype(np.int64)
+    ends = starts + lens
+    keep = (ends > f_lo) & (starts < f_hi) & (starts >= 0)
+    starts, ends, lens = starts[keep], ends[keep], lens[keep]
+    order = np.argsort(starts, kind="stable")
+    starts, ends, lens = starts[order], ends[order], lens[order]
+    n = starts.shape[0]
+    truth = rng.integers(0, 2, n)
+    orient = int(rng.integers(0, 2))
+    hp = np.full(n, HAPTAG_UNPHASED, np.int64)
+    tl = starts < s
+    hp[tl] = truth[tl]
+    only_right = (~tl) & (ends > e)
+    hp[only_right] = truth[only_right] ^ orient
+    hp[rng.random(n) < spec.untag_frac] = HAPTAG_UNPHASED
+    strand = (rng.random(n) < 0.5).astype(np.int64)
+    rs0 = starts - span_lo                                  # ref-relative read start
+
+    # indel events, non-overlapping, strictly inside each read
+    n_ev = rng.poisson(spec.indel_rate * lens)
+    n_ev = np.minimum(n_ev, np.maximum(lens // 8, 0))
+    ev_read = np.repeat(np.arange(n), n_ev)
+    ev_pos = rs0[ev_read] + 1 + (rng.random(ev_read.shape[0]) * (lens[ev_read] - 8)).astype(np.int64)
+    ev_len = rng.integers(1, 4, ev_read.shape[0])
+    ev_ins = rng.random(ev_read.shape[0]) < 0.5
+    o = np.lexsort((ev_pos, ev_read))
+    ev_read, ev_pos, ev_len, ev_ins = ev_read[o], ev_pos[o], ev_len[o], ev_ins[o]
+    BIG = np.int64(1) << 40
+    key = ev_read * BIG + ev_pos
+    endk = key + np.where(ev_ins, 0, ev_len)
+    prev_end = np.concatenate([[np.int64(-1)], np.maximum.accumulate(endk)[:-1]])
+    ok = key > prev_end
+    ev_read, ev_pos, ev_len, ev_ins = ev_read[ok], ev_pos[ok], ev_len[ok], ev_ins[ok]
+    n_ev = np.bincount(ev_read, minlength=n)
+    ev_first = np.concatenate([[0], np.cumsum(n_ev)])
+
+    # cursor before each event: read start or previous event's end
+    is_first = np.zeros(ev_read.shape[0], bool)
+    is_first[ev_first[:-1][n_ev > 0]] = True
+    prev_cur = np.empty(ev_read.shape[0], np.int64)
+    if ev_read.shape[0]:
+        prev_cur[1:] = ev_pos[:-1] + np.where(ev_ins[:-1], 0, ev_len[:-1])
+        prev_cur[is_first] = rs0[ev_read[is_first]]
+    m_before = ev_pos - prev_cur                           # >= 1 by construction
+    last_cur = rs0.copy()
+    has_ev = n_ev > 0
+    li = ev_first[1:][has_ev] - 1
+    last_cur[has_ev] = ev_pos[li] + np.where(ev_ins[li], 0, ev_len[li])
+    m_last = rs0 + lens - last_cur
+
+    # soft clips
+    clip = rng.random(n) < spec.clip_frac
+    c1 = np.where(clip & (rng.random(n) < 0.7), rng.integers(1, spec.clip_max, n), 0)
+    c2 = np.where(clip & (rng.random(n) < 0.7), rng.integers(1, spec.clip_max, n), 0)
+
+    # per read: ops  [S c1] (M_k, E_k)* M_last [S c2]
+    recs = []
+    ins_total = ev_len[ev_ins]
+    for r in range(n):
+        k0, k1 = ev_first[r], ev_first[r + 1]
+        ne = k1 - k0
+        core_len = np.empty(2 * ne + 1, np.int64)
+        core_op = np.empty(2 * ne + 1, np.int64)
+        core_len[0:2 * ne:2] = m_before[k0:k1]
+        core_op[0:2 * ne:2] = 0
+        core_len[1:2 * ne:2] = ev_len[k0:k1]
+        core_op[1:2 * ne:2] = np.where(ev_ins[k0:k1], 1, 2)
+        core_len[-1] = m_last[r]
+        core_op[-1] = 0
+        # SEQ: reference bases of M ops, random bases of I ops
+        ref_cur = rs0[r] + np.concatenate([[0], np.cumsum(np.where(core_op == 1, 0, core_len))[:-1]])
+        qlen = np.where(core_op == 2, 0, core_len)
+        tot = int(qlen.sum())
+        q0 = np.concatenate([[0], np.cumsum(qlen)[:-1]])
+        idx = np.repeat(ref_cur - q0, qlen) + np.arange(tot)
+        kind = np.repeat(core_op, qlen)
+        bases = ref[np.where(kind == 0, idx, 0)]
+        refpos = np.where(kind == 0, idx, -1)
+        ins_m = kind == 1
+        bases[ins_m] = rng.integers(0, 4, int(ins_m.sum()))
+        sub = (rng.random(tot) < spec.sub_rate) & ~ins_m
+        bases[sub] = (bases[sub] + rng.integers(1, 4, int(sub.sum()))) % 4
+        if c1[r] or c2[r]:
+            bases = np.concatenate([rng.integers(0, 4, c1[r]).astype(np.uint8), bases,
+                                    rng.integers(0, 4, c2[r]).astype(np.uint8)])
+            refpos = np.concatenate([np.full(c1[r], -1), refpos, np.full(c2[r], -1)])
+        ops = []
+        if c1[r]:
+            ops.append((c1[r], 4))
+        ops += list(zip(core_len.tolist(), core_op.tolist()))
+        if c2[r]:
+            ops.append((c2[r], 4))
+        cigar = np.array([(l << 4) | op for l, op in ops], np.uint32)
+        recs.append((bases, refpos, cigar))
+
+    # calls per read
+    out = []
+    for r in range(n):
+        bases, refpos, cigar = recs[r]
+        lq = bases.shape[0]
+        cgp = np.flatnonzero((bases[:-1] == C_) & (bases[1:] == G_))     # C of each CpG (stored)
+        sid = site_of[np.maximum(refpos[cgp], 0)]
+        sid[refpos[cgp] < 0] = -1
+        p = np.full(cgp.shape[0], 0.5)
+        on = sid >= 0
+        p[on] = site_p[sid[on]]
+        a = on & site_asm[np.maximum(sid, 0)]
+        p[a] = np.where(site_hap[sid[a]] == truth[r], 0.95, 0.05)
+        cat = np.where(rng.random(cgp.shape[0]) < p, 0, 1)
+        cat[rng.random(cgp.shape[0]) < spec.nocall_frac] = 2
+        called = cgp if strand[r] == 0 else cgp + 1                     # stored position of the called base
+        if spec.implicit_frac and rng.random() < spec.implicit_frac:
+            if strand[r] == 0:
+                cand = np.flatnonzero((bases[:-1] == C_) & (bases[1:] != G_))
+            else:
+                cand = 1 + np.flatnonzero((bases[1:] == G_) & (bases[:-1] != C_))
+            if cand.shape[0]:
+                extra = rng.choice(cand, size=min(cand.shape[0], int(rng.integers(1, 4))), replace=False)
+                called = np.concatenate([called, extra])
+                cat = np.concatenate([cat, rng.integers(0, 3, extra.shape[0])])
+                o = np.argsort(called, kind="stable")
+                called, cat = called[o], cat[o]
+        qual = _qual_from_cat(rng, cat)
+        # MM skip counts in the original read orientation
+        tb = C_ if strand[r] == 0 else G_
+        allt = np.flatnonzero(bases == tb)
+        rank = np.searchsorted(allt, called)
+        if strand[r]:
+            rank = allt.shape[0] - 1 - rank
+            o = np.argsort(rank, kind="stable")
+            rank, qual = rank[o], qual[o]
+        deltas = np.diff(np.concatenate([[-1], rank])) - 1
+        ds = ",".join(map(str, deltas.tolist()))
+        style = int(rng.integers(0, 5)) if spec.mm_mix else 1
+        nd = deltas.shape[0]
+        if nd == 0:
+            mm, ml = "", np.zeros(0, np.uint8)
+        elif style == 0:
+            mm, ml = f"C+m?,{ds};", qual
+        elif style == 1:
+            hq = rng.integers(0, 40, nd).astype(np.uint8)
+            mm, ml = f"C+h?,{ds};C+m?,{ds};", np.concatenate([hq, qual])
+        elif style == 2:
+            hq = rng.integers(0, 40, nd).astype(np.uint8)
+            mm, ml = f"C+hm?,{ds};", np.stack([hq, qual], 1).reshape(-1)
+        elif style == 3:
+            mm, ml = f"C+m.,{ds};", qual
+        else:
+            mm, ml = f"C+m?,{ds};", np.zeros(0, np.uint8)
+        codes = _NT16[bases]
+        if lq & 1:
+            codes = np.concatenate([codes, np.zeros(1, np.uint8)])
+        seq = (codes[0::2] << 4) | codes[1::2]
+        out.append(dict(seq=seq, l_qseq=lq, cigar=cigar, mm=np.frombuffer(mm.encode(), np.uint8), ml=ml))
+
+    flag = (strand * 16).astype(np.uint16)
+    mapq = np.full(n, 60, np.uint8)
+    de = rng.uniform(0.01, 0.08, n).astype(np.float32)
+    de[rng.random(n) < 0.1] = -1.0
+    if spec.filt_frac:
+        bad = np.flatnonzero(rng.random(n) < spec.filt_frac)
+        kind = rng.integers(0, 5, bad.shape[0])
+        flag[bad[kind == 0]] |= np.uint16(256)
+        flag[bad[kind == 1]] |= np.uint16(2048)
+        mapq[bad[kind == 2]] = 5
+        de[bad[kind == 3]] = 0.2
+        flag[bad[kind == 4]] |= np.uint16(4)
+    return dict(s=s, e=e, orient=orient, pos=starts, flag=flag, mapq=mapq, de=de, hp=hp, recs=out)
+
+
+def make_aln_batch(spec: AlnSpec, windows=None) -> AlnBatch:
+    if windows is None:
+        windows = range(spec.n_windows)
+    parts = [make_aln_window(spec, w) for w in windows]
+    recs = [r for p in parts for r in p["recs"]]
+
+    def off(key, f=lambda x: x.shape[0]):
+        return np.concatenate([[0], np.cumsum([f(r[key]) for r in recs])]).astype(np.uint64)
+
+    def cat(key, dt):
+        return np.concatenate([r[key] for r in recs]).astype(dt) if recs else np.zeros(0, dt)
+
+    rc = np.array([len(p["recs"]) for p in parts], np.int64)
+    b = AlnBatch(
+        win_start=np.array([p["s"] for p in parts], np.uint32),
+        win_end=np.array([p["e"] for p in parts], np.uint32),
+        win_rec_off=np.concatenate([[0], np.cumsum(rc)]).astype(np.uint32),
+        flag=np.concatenate([p["flag"] for p in parts]) if parts else np.zeros(0, np.uint16),
+        mapq=np.concatenate([p["mapq"] for p in parts]) if parts else np.zeros(0, np.uint8),
+        pos=np.concatenate([p["pos"] for p in parts]) if parts else np.zeros(0, np.uint32),
+        l_qseq=np.array([r["l_qseq"] for r in recs], np.uint32),
+        de=np.concatenate([p["de"] for p in parts]) if parts else np.zeros(0, np.float32),
+        hp=np.concatenate([p["hp"] for p in parts]) if parts else np.zeros(0, np.uint8),
+        cigar_off=off("cigar"), cigar=cat("cigar", np.uint32),
+        seq_off=off("seq"), seq=cat("seq", np.uint8),
+        mm_off=off("mm"), mm=cat("mm", np.uint8),
+        ml_off=off("ml"), ml=cat("ml", np.uint8),
+    )
+    b.meta["orient"] = np.array([p["orient"] for p in parts], np.int8)
+    b.meta["spec"] = spec
+    return b

@@ -1,0 +1,101 @@
+"""GPU parity of kernel K0 (the window loader on the device) against the CPU
+oracle, through the C ABI (pf_batch_upload_aln).
+
+Integer outputs must be bit-identical: which records are kept, every read's
+calls (sorted by (pos, cat), as the methmer kernels consume them), the first
+and last call in get_mod_poss_on_ref's order, read starts/ends, and then the
+whole methphase result of the record-level batch.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from tests._aln_cases import HANDMADE, LOAD_CFG_SMALL, aln_cases, handmade_batch, records_batch
+
+pytestmark = pytest.mark.gpu
+
+NONE = 0xFFFFFFFF
+CASES = aln_cases()
+
+
+def _oracle_view(oracle_lib, lcfg, aln):
+    b, rec_read = oracle_lib.load_reads(lcfg, aln)
+    co = b.read_call_off.astype(np.int64)
+    first = np.array([b.call_pos[co[r]] if co[r + 1] > co[r] else 0 for r in range(b.n_reads)], np.uint32)
+    last = np.array([b.call_pos[co[r + 1] - 1] if co[r + 1] > co[r] else 0 for r in range(b.n_reads)], np.uint32)
+    pos, cat = b.call_pos.copy(), b.call_cat.copy()
+    for r in range(b.n_reads):
+        o = np.lexsort((cat[co[r]:co[r + 1]], pos[co[r]:co[r + 1]]))
+        pos[co[r]:co[r + 1]] = pos[co[r]:co[r + 1]][o]
+        cat[co[r]:co[r + 1]] = cat[co[r]:co[r + 1]][o]
+    return b, rec_read, pos, cat, first, last
+
+
+def _check_calls(oracle_lib, gpu_ctx, cfg, lcfg, aln, tag):
+    b, rec_read, pos, cat, first, last = _oracle_view(oracle_lib, lcfg, aln)
+    db = gpu_ctx.upload_aln(cfg, aln, lcfg)
+    assert db.n_reads == b.n_reads, tag
+    assert np.array_equal(db.read_recs(), np.flatnonzero(rec_read != NONE)), tag
+    off, gpos, gcat, gfirst, glast = db.debug_calls()
+    assert np.array_equal(off, b.read_call_off), tag
+    bad = np.flatnonzero(gpos != pos)
+    assert bad.size == 0, f"{tag}: call_pos differs at {bad[:5].tolist()}"
+    assert np.array_equal(gcat, cat), f"{tag}: call_cat differs at {np.flatnonzero(gcat != cat)[:5].tolist()}"
+    assert np.array_equal(gfirst, first), tag
+    assert np.array_equal(glast, last), tag
+    return db, b
+
+
+def test_handmade_records(oracle_lib, gpu_ctx):
+    from pomfret_amd import Config
+    aln = handmade_batch()
+    db, b = _check_calls(oracle_lib, gpu_ctx, Config(), LOAD_CFG_SMALL, aln, "handmade")
+    kept = [h for h in HANDMADE if h[2] is not None]
+    assert db.n_reads == len(kept)
+    c = db.load_counters()
+    assert c["seq_path"] >= 2 and c["implicit"] >= 2 and c["bad_mm"] >= 2
+    db.free()
+
+
+def test_handmade_sequential_path(oracle_lib, gpu_ctx, monkeypatch):
+    """PF_K0_PATH=seq walks every record with the literal lane-0 loop."""
+    from pomfret_amd import Config
+    monkeypatch.setenv("PF_K0_PATH", "seq")
+    db, _ = _check_calls(oracle_lib, gpu_ctx, Config(), LOAD_CFG_SMALL, handmade_batch(), "handmade-seq")
+    db.free()
+
+
+def test_fatal_cigar_is_an_error(gpu_ctx):
+    from pomfret_amd import Config, PomfretError
+    aln = records_batch([(0, 10, [dict(seq="ACGTTCGA", cigar="6M2H", mm="C+m?,0,0;", ml=[200, 10], pos=100)])])
+    with pytest.raises(PomfretError):
+        gpu_ctx.upload_aln(Config(), aln, LOAD_CFG_SMALL)
+
+
+@pytest.mark.parametrize("name,aln", CASES, ids=[c[0] for c in CASES])
+def test_record_level_parity(oracle_lib, gpu_ctx, name, aln):
+    """K0 calls, then the whole methphase result of the record-level batch."""
+    from pomfret_amd import Config, LoadConfig
+    cfg = Config.from_coverage(30, given=False)
+    lcfg = LoadConfig()
+    db, b = _check_calls(oracle_lib, gpu_ctx, cfg, lcfg, aln, name)
+    ref = oracle_lib.methphase(cfg, b, n_threads=8)
+    out = db.run()
+    for f in ("decision", "dir_table", "dir_join", "dir_which_way", "win_n_sites", "win_n_reads", "read_hp"):
+        assert np.array_equal(getattr(ref, f), getattr(out, f)), f"{name}: {f}"
+    np.testing.assert_allclose(out.dir_fisher_p, ref.dir_fisher_p, rtol=1e-6, atol=0)
+    out2 = db.run()                                  # K0 re-runs every launch: same result
+    assert np.array_equal(out2.read_hp, out.read_hp) and np.array_equal(out2.decision, out.decision)
+    db.free()
+
+
+def test_scratch_trigger_lists(oracle_lib, gpu_ctx):
+    """Reads with more 5mC calls than the per-wave LDS list (2048) use HBM
+    scratch; aln_dense_cpg has such reads."""
+    from pomfret_amd import Config, LoadConfig
+    aln = dict(CASES)["aln_dense_cpg"]
+    big = np.diff(aln.ml_off.astype(np.int64)) > 2048
+    assert big.any()
+    db, _ = _check_calls(oracle_lib, gpu_ctx, Config.from_coverage(30, given=False), LoadConfig(), aln, "dense")
+    db.free()
