@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X methphase hot path (BASELINE.json metric).
 
-One "step" = one pass of the hot path over one batch of windows that is already
-resident in HBM: K12 sites + methmers (+ K2 fallback) -> K3 greedy + 2x2 tables
-(+ K3 fallback) -> D2H -> host Fisher test, join decisions and read tags
-(pf_methphase_launch + pf_methphase_finish, two steps in flight).  Workload at N=1 is
-BASELINE.json configs[1] ("HG002 chr20 30x, pre-haplotagged, 1x MI355X"),
-synthesised (HG002 is not available offline): 256 chr20-like gap windows of
-50 kb at 30x, parameters as `pomfret methphase` derives them without -c
-(cov_for_selection 4, cov_for_runtime 8, n_cand 8; blockjoin.c:4373-4375).
+One "step" = one pass of the hot path over one batch of windows whose BAM
+records (decoded on the host: flag, MAPQ, pos, CIGAR, 4-bit SEQ, MM/ML, de, HP)
+are already resident in HBM:
+  K0 loader (read filters + 5mC extraction of every record, blockjoin.c:
+  1043-1173 / 794-908 / 605-792) -> K12 sites + methmers (+ K2 fallback) ->
+  K3 greedy + 2x2 tables (+ K3 fallback) -> D2H -> host Fisher test, join
+  decisions and read tags (pf_methphase_launch + pf_methphase_finish, two
+  steps in flight).
+`--calls-level` times the previous boundary instead (reads and 5mC calls
+resident, no K0).  Workload at N=1 is BASELINE.json configs[1] ("HG002 chr20
+30x, pre-haplotagged, 1x MI355X"), synthesised (HG002 is not available
+offline): 256 chr20-like gap windows of 50 kb at 30x, parameters as `pomfret
+methphase` derives them without -c (cov_for_selection 4, cov_for_runtime 8,
+n_cand 8; blockjoin.c:4373-4375), loader defaults -q 10 -L 15000, ML bands
+100/156 (cli.c:52-63).
 
 Multi-GPU (torchrun, one process per GPU): every rank owns its own shard of 256
 windows (weak scaling, no collective in the data path); after each step the
@@ -65,6 +72,20 @@ def algo_bytes(batch, stats, n_sites):
     return {"pf_k12_sites_methmers": k1 + k2, "pf_k2_methmers": 0, "pf_k3_greedy": k3, "pf_k3_fallback": 0}
 
 
+def k0_bytes(aln, read_recs, n_calls):
+    """Algorithmic bytes per launch of K0: 4 B (read index) per
+    record; per kept record 55 B of fixed fields (flag, MAPQ, pos, l_qseq, de,
+    five record offsets, the read's call offset), its CIGAR (4 B/op), 4-bit SEQ
+    (l_qseq/2 B) and MM text; per call 1 B of ML read and 5 B (u32 pos + u8
+    cat) written; per kept read 16 B written (start, end, first, last)."""
+    kept = np.asarray(read_recs, np.int64)
+    cig = np.diff(aln.cigar_off.astype(np.int64))[kept]
+    mm = np.diff(aln.mm_off.astype(np.int64))[kept]
+    seq = (aln.l_qseq.astype(np.int64)[kept] + 1) // 2
+    R = kept.shape[0]
+    return int(4 * aln.n_recs + 55 * R + 4 * cig.sum() + seq.sum() + mm.sum() + 6 * n_calls + 16 * R)
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
@@ -97,6 +118,21 @@ def cpu_baseline(cfg, batch, threads: int, min_cpu_s: float = 20.0, max_reps: in
     return batch.n_reads * reps / dt, dt, reps
 
 
+def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 20.0, max_reps: int = 200):
+    """Record-level CPU path of the oracle (per window: loader + worker, the
+    reference's structure), `threads` pthreads over windows, bounded sample."""
+    import oracle
+    t0 = time.perf_counter()
+    reps = 0
+    while reps < max_reps:
+        oracle.methphase_aln(cfg, lcfg, aln, n_threads=threads)
+        reps += 1
+        if (time.perf_counter() - t0) * threads >= min_cpu_s and reps >= 2:
+            break
+    dt = time.perf_counter() - t0
+    return n_reads * reps / dt, dt, reps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,11 +142,30 @@ def main():
     ap.add_argument("--coverage", type=int, default=WORKLOAD["coverage"])
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--calls-level", action="store_true",
+                    help="time the calls-level boundary (reads + 5mC calls resident, no K0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from pomfret_amd import Config, Context, LoadConfig, WindowBatch
+    from pomfret_amd.synth import SynthSpec, make_batch
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+
+    wl = dict(WORKLOAD, n_windows=args.windows, coverage=args.coverage)
+    cfg = Config.from_coverage(wl["coverage"], given=False)
+    lcfg = LoadConfig()
+    record_level = not args.calls_level
+    t = time.perf_counter()
+    if record_level:
+        # generated (in worker processes) before anything touches the GPU
+        aln = make_aln_batch(AlnSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
+                                     seed=1000 + rank), workers=0 if world == 1 else 4)
+        log(f"[bench] rank {rank}: generated {aln.n_windows} windows, {aln.n_recs} BAM records "
+            f"({aln.nbytes() / 1e9:.2f} GB) in {time.perf_counter() - t:.1f}s")
+
     dist = None
     if world > 1:
         import torch
@@ -119,21 +174,24 @@ def main():
         torch.cuda.set_device(local_rank)
         tdist.init_process_group(backend="nccl")
         dist = tdist
-
-    from pomfret_amd import Config, Context
-    from pomfret_amd.synth import SynthSpec, make_batch
-
-    wl = dict(WORKLOAD, n_windows=args.windows, coverage=args.coverage)
-    cfg = Config.from_coverage(wl["coverage"], given=False)
-    spec = SynthSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
-                     seed=1000 + rank)
-    t = time.perf_counter()
-    batch = make_batch(spec)
-    log(f"[bench] rank {rank}: generated {batch.n_windows} windows, {batch.n_reads} reads, "
-        f"{batch.n_calls} calls in {time.perf_counter() - t:.1f}s")
-
     ctx = Context(local_rank)
-    db = ctx.upload(cfg, batch)
+    if record_level:
+        t = time.perf_counter()
+        db = ctx.upload_aln(cfg, aln, lcfg)
+        log(f"[bench] upload (validation, SEQ repack, H2D, K0 count pass): {time.perf_counter() - t:.1f}s")
+        off, cpos, ccat, _, _ = db.debug_calls()
+        rr = db.read_recs()
+        # the loaded reads as a window batch (sizes for the byte model; the rows are K0's)
+        wro = np.searchsorted(rr, aln.win_rec_off.astype(np.int64)).astype(np.uint32)
+        batch = WindowBatch(win_start=aln.win_start, win_end=aln.win_end, win_read_off=wro,
+                            read_start=np.zeros(len(rr), np.uint32), read_end=np.zeros(len(rr), np.uint32),
+                            read_hp=aln.hp[rr], read_call_off=off, call_pos=cpos, call_cat=ccat)
+    else:
+        batch = make_batch(SynthSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
+                                     seed=1000 + rank))
+        log(f"[bench] rank {rank}: generated {batch.n_windows} windows, {batch.n_reads} reads, "
+            f"{batch.n_calls} calls in {time.perf_counter() - t:.1f}s")
+        db = ctx.upload(cfg, batch)
     out = db.run()
     outs = [out, db.run()]
     for _ in range(args.warmup):
@@ -187,6 +245,10 @@ def main():
     stats = db.stats()
     kmean = {k: v / args.steps for k, v in kern_acc.items()}
     ab = algo_bytes(batch, stats, out.win_n_sites)
+    if record_level:
+        ab["pf_k0_load"] = k0_bytes(aln, rr, batch.n_calls)
+    else:
+        kmean.pop("pf_k0_load", None)
     kernels = {}
     for k, ms in kmean.items():
         b = ab.get(k, 0)
@@ -199,24 +261,30 @@ def main():
     # PCIe-inclusive rate (never `value`): the one-shot boundary call hands
     # over host buffers -- upload (validation, pinned staging, H2D), run, D2H
     t1 = time.perf_counter()
-    n_once = 3
+    n_once = 2 if record_level else 3
     for _ in range(n_once):
-        db2 = ctx.upload(cfg, batch)
+        db2 = ctx.upload_aln(cfg, aln, lcfg) if record_level else ctx.upload(cfg, batch)
         db2.run()
         db2.free()
+    what = ("upload(host BAM-record SoA: validation, SEQ repack, H2D, K0 count pass) + run + free per call"
+            if record_level else "upload(host SoA -> HBM) + run + free per call")
     pcie = {"reads_per_s": round(batch.n_reads * n_once / (time.perf_counter() - t1), 1),
             "ms_per_call": round((time.perf_counter() - t1) / n_once * 1e3, 3),
-            "what": "upload(host SoA -> HBM) + run + free per call, rank 0"}
+            "what": what + ", rank 0"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-        v_cpu, dt, reps = cpu_baseline(cfg, batch, threads)
+        if record_level:
+            v_cpu, dt, reps = cpu_baseline_aln(cfg, lcfg, aln, batch.n_reads, threads)
+            what = "per-window loader + worker over the same BAM records, oracle/pf_oracle{_load,}.c"
+        else:
+            v_cpu, dt, reps = cpu_baseline(cfg, batch, threads)
+            what = "oracle/pf_oracle.c"
         cpu = {"value": round(v_cpu, 1), "unit": "reads/s", "cores": threads, "kind": "port",
                "sample": f"the same {batch.n_windows}-window workload x{reps} "
                          f"({batch.n_reads * reps} reads, {dt:.2f}s wall x {threads} threads "
-                         f"= {dt * threads:.0f} CPU-s), "
-                         f"oracle/pf_oracle.c"}
+                         f"= {dt * threads:.0f} CPU-s), {what}"}
 
     res = {
         "metric": "aligned reads/sec (methphase kernel)",
@@ -233,7 +301,11 @@ def main():
         "data": "synthetic (seeded chr20-like 30x pileups; HG002 not available offline)",
         "config": {
             "workload": f"chr20-like {wl['coverage']}x: {wl['n_windows']} gap windows x "
-                        f"{wl['gap'] // 1000} kb per GPU, pre-haplotagged (BASELINE configs[1])",
+                        f"{wl['gap'] // 1000} kb per GPU, pre-haplotagged (BASELINE configs[1]); "
+                        + ("BAM records resident (K0 loader in the step)" if record_level
+                           else "reads + 5mC calls resident (no K0)"),
+            "boundary": "records" if record_level else "calls",
+            "records_per_gpu": aln.n_recs if record_level else None,
             "windows_per_gpu": wl["n_windows"], "reads_per_gpu": batch.n_reads,
             "calls_per_gpu": batch.n_calls, "coverage": wl["coverage"],
             "cov_for_selection": cfg.cov_for_selection, "cov_for_runtime": cfg.cov_for_runtime,

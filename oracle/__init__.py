@@ -52,6 +52,8 @@ def lib():
         L.orc_vcf_gaps.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
         L.orc_load_reads.argtypes = [C.c_void_p, C.c_void_p] + [C.c_void_p] * 8 + [C.c_uint64, C.c_void_p]
         L.orc_load_reads.restype = C.c_int
+        L.orc_methphase_aln.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_methphase_aln.restype = C.c_int
         _lib = L
     return _lib
 
@@ -171,3 +173,15 @@ def load_reads(lcfg: LoadConfig, aln: AlnBatch):
                     call_pos=cp[:N], call_cat=cc[:N], win_cov_sel=aln.win_cov_sel,
                     win_cov_rt=aln.win_cov_rt, win_n_cand=aln.win_n_cand)
     return b, rec_read[:n]
+
+
+def methphase_aln(cfg: Config, lcfg: LoadConfig, aln: AlnBatch, n_threads: int = 1) -> WindowResult:
+    """Record-level path on the CPU (per window: loader a3/a4, then the
+    methphase worker).  read_hp is left unset."""
+    res = WindowResult.alloc(aln.n_windows, 0)
+    c, lc, a, o = cfg.to_c(), lcfg.to_c(), aln.to_c(), res.to_c()
+    o.read_hp = None
+    rc = lib().orc_methphase_aln(C.byref(c), C.byref(lc), C.byref(a), C.byref(o), int(n_threads))
+    if rc != 0:
+        raise RuntimeError(f"oracle methphase_aln failed: {rc}")
+    return res

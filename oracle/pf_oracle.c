@@ -777,6 +777,44 @@ int orc_methphase_windows(const pf_cfg_t *cfg, const pf_window_batch_t *b, pf_wi
     return 0;
 }
 
+typedef struct {
+    const pf_cfg_t *cfg; const pf_load_cfg_t *lc; const pf_aln_batch_t *A; pf_window_out_t *out;
+    uint32_t next; int fatal; pthread_mutex_t mu;
+} o_ajob_t;
+
+static void *aln_worker(void *arg) {
+    o_ajob_t *j = (o_ajob_t *)arg;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        uint32_t w = j->next++;
+        pthread_mutex_unlock(&j->mu);
+        if (w >= j->A->n_windows) break;
+        orc_window_t lw;
+        if (orc_load_window(j->lc, j->A, w, &lw) < 0) {
+            pthread_mutex_lock(&j->mu); j->fatal = 1; pthread_mutex_unlock(&j->mu);
+        }
+        o_winres_t r;
+        run_window(j->cfg, &lw.b, 0, &r, NULL, NULL);
+        store_res(j->out, w, &r);
+        orc_window_free(&lw);
+    }
+    return NULL;
+}
+
+int orc_methphase_aln(const pf_cfg_t *cfg, const pf_load_cfg_t *lc, const pf_aln_batch_t *A,
+                      pf_window_out_t *out, int n_threads) {
+    if (!cfg || !lc || !A || !out) return PF_ERR_ARG;
+    o_ajob_t job = {cfg, lc, A, out, 0, 0, PTHREAD_MUTEX_INITIALIZER};
+    if (n_threads <= 1) aln_worker(&job);
+    else {
+        pthread_t *tid = malloc(sizeof(pthread_t) * n_threads);
+        for (int i = 0; i < n_threads; i++) pthread_create(&tid[i], NULL, aln_worker, &job);
+        for (int i = 0; i < n_threads; i++) pthread_join(tid[i], NULL);
+        free(tid);
+    }
+    return job.fatal ? -1 : 0;
+}
+
 int orc_methphase_trace(const pf_cfg_t *cfg, const pf_window_batch_t *b, uint32_t cap,
                         uint32_t *read_ids, uint8_t *tags, float *scores, uint32_t *counts) {
     for (uint32_t w = 0; w < b->n_windows; w++) {

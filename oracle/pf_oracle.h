@@ -77,6 +77,25 @@ int orc_load_reads(const pf_load_cfg_t *lc, const pf_aln_batch_t *A, uint32_t *r
                    uint32_t *read_start, uint32_t *read_end, uint8_t *read_hp, uint64_t *call_off,
                    uint32_t *call_pos, uint8_t *call_cat, uint64_t call_cap, uint64_t *n_calls_out);
 
+/* One window of a record-level batch loaded into a single-window batch `b`
+ * (the arrays are owned by the struct; free with orc_window_free). */
+typedef struct orc_window {
+    pf_window_batch_t b;
+    uint32_t win_start, win_end, win_read_off[2];
+    uint32_t *read_start, *read_end, *call_pos;
+    uint8_t *read_hp, *call_cat;
+    uint64_t *read_call_off;
+} orc_window_t;
+int orc_load_window(const pf_load_cfg_t *lc, const pf_aln_batch_t *A, uint32_t w, orc_window_t *o);
+void orc_window_free(orc_window_t *o);
+
+/* Record-level path on the CPU: per window load (a3/a4) then the methphase
+ * worker, n_threads pthreads over windows (the reference's per-window
+ * structure, 4217-4335).  out->read_hp is not written.  Returns 0, or -1 on a
+ * fatal CIGAR operation. */
+int orc_methphase_aln(const pf_cfg_t *cfg, const pf_load_cfg_t *lc, const pf_aln_batch_t *A,
+                      pf_window_out_t *out, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -285,3 +285,59 @@ done:
     free(tp.a); free(tq.a); free(mp.a); free(mq.a); free(cp.a); free(cq.a);
     return rc;
 }
+
+/* One window loaded into a self-owned single-window batch (the per-window
+ * load_reads_given_interval call of haplotag_region_given_bam, 4217-4240):
+ * used by orc_methphase_aln, the record-level CPU path. */
+int orc_load_window(const pf_load_cfg_t *lc, const pf_aln_batch_t *A, uint32_t w, orc_window_t *o) {
+    lv32 tp = {0}, mp = {0}, cp = {0}, rs = {0}, re = {0}, pos = {0};
+    lv8 tq = {0}, mq = {0}, cq = {0}, hp = {0}, cat = {0};
+    typedef struct { uint64_t *a; size_t n, m; } lv64;
+    lv64 off = {0};
+    const uint8_t lo = (uint8_t)lc->qual_lo, hi = (uint8_t)lc->qual_hi;
+    int rc = 0;
+    LPUSH(off, 0);
+    for (uint32_t r = A->win_rec_off[w]; r < A->win_rec_off[w + 1]; r++) {
+        const uint32_t flag = A->flag[r], mapq = A->mapq[r], len = A->l_qseq[r];
+        if ((flag & 4) || (flag & 256) || (flag & 2048)) continue;
+        if (mapq < (uint32_t)lc->min_mapq) continue;
+        if (len < 2 || len < (uint32_t)lc->min_len) continue;
+        if ((double)A->de[r] > 0.1) continue;
+        cp.n = cq.n = 0;
+        const int st = fill_read(A, r, lo, hi, &tp, &tq, &mp, &mq, &cp, &cq);
+        if (st < 0) { rc = -1; break; }
+        if (st == 0) continue;
+        LPUSH(rs, A->pos[r]);
+        LPUSH(re, bam_endpos_(A, r));
+        LPUSH(hp, A->hp[r]);
+        for (size_t i = 0; i < cp.n; i++) { LPUSH(pos, cp.a[i]); LPUSH(cat, cq.a[i]); }
+        LPUSH(off, (uint64_t)pos.n);
+    }
+    free(tp.a); free(tq.a); free(mp.a); free(mq.a); free(cp.a); free(cq.a);
+    memset(o, 0, sizeof(*o));
+    o->win_start = A->win_start[w];
+    o->win_end = A->win_end[w];
+    o->win_read_off[0] = 0;
+    o->win_read_off[1] = (uint32_t)rs.n;
+    o->read_start = rs.a; o->read_end = re.a; o->read_hp = hp.a;
+    o->read_call_off = off.a; o->call_pos = pos.a; o->call_cat = cat.a;
+    memset(&o->b, 0, sizeof(o->b));
+    o->b.n_windows = 1;
+    o->b.n_reads = (uint32_t)rs.n;
+    o->b.n_calls = pos.n;
+    o->b.win_start = &o->win_start;
+    o->b.win_end = &o->win_end;
+    o->b.win_read_off = o->win_read_off;
+    o->b.win_cov_sel = A->win_cov_sel ? A->win_cov_sel + w : NULL;
+    o->b.win_cov_rt = A->win_cov_rt ? A->win_cov_rt + w : NULL;
+    o->b.win_n_cand = A->win_n_cand ? A->win_n_cand + w : NULL;
+    o->b.read_start = rs.a; o->b.read_end = re.a; o->b.read_hp = hp.a;
+    o->b.read_call_off = off.a; o->b.call_pos = pos.a; o->b.call_cat = cat.a;
+    return rc;
+}
+
+void orc_window_free(orc_window_t *o) {
+    free(o->read_start); free(o->read_end); free(o->read_hp);
+    free((void *)o->read_call_off); free(o->call_pos); free(o->call_cat);
+    memset(o, 0, sizeof(*o));
+}

@@ -482,7 +482,8 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         const uint64_t mln = a->ml_off[r + 1] - a->ml_off[r], mlen = a->mm_off[r + 1] - a->mm_off[r];
         const uint64_t bound = mln ? mln : (mlen + 1) / 2;
         scr_off[r] = sc;
-        if (bound > PF_K0_TCAP) sc += bound;
+        if (bound > PF_K0_TCAP) sc += 2 * bound;          // ranks/triggers + K0's placement buffer
+        if (a->l_qseq[r] >= (1u << 24)) return PF_ERR_LIMIT; // K0 packs ranks into 24 bits
     }
     seq_off[n] = so;
     scr_off[n] = sc;
@@ -514,7 +515,8 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         uint64_t *p64; PUT(p64, a->cigar_off, n + 1); ld.cigar_off = p64;
         PUT(p32, a->cigar, a->cigar_off[n]); ld.cigar = p32;
         PUT(p64, a->mm_off, n + 1); ld.mm_off = p64;
-        PUT(p8, (const uint8_t *)a->mm, a->mm_off[n]); ld.mm = p8;
+        ALLOC(p8, a->mm_off[n] + 16); ld.mm = p8;            // padded: K0 stages the text with word loads
+        if (a->mm_off[n]) HIPCHK(hipMemcpy(p8, a->mm, a->mm_off[n], hipMemcpyHostToDevice));
         PUT(p64, a->ml_off, n + 1); ld.ml_off = p64;
         PUT(p8, a->ml, a->ml_off[n]); ld.ml = p8;
         PUT(p64, seq_off.data(), n + 1); ld.seq_off = p64;
@@ -526,6 +528,7 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
             memcpy(sq.data() + seq_off[r], a->seq + a->seq_off[r], ((uint64_t)a->l_qseq[r] + 1) / 2);
         PUT(p8, sq.data(), sq.size()); ld.seq = p8;
         ALLOC(p32, n); ld.rec_n = p32;
+        ALLOC(p32, n); ld.rec_nd = p32;
         ALLOC(p32, n); ld.rec_read = p32;
         unsigned long long *pc; ALLOC(pc, PF_K0_NCTR); ld.ctr = pc; b->k0_ctr = pc;
         ALLOC(p32, 1); ld.status = p32;
@@ -548,6 +551,21 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         HIPCHK(hipMemcpy(c, ld.ctr, sizeof(c), hipMemcpyDeviceToHost));
         fprintf(stderr, "[D::pomfret_amd] K0: seq-path %llu, unsorted %llu, implicit %llu, bad MM %llu, dup chunks %llu\n",
                 c[0], c[1], c[2], c[3], c[4]);
+    }
+    {
+        // write mode: scratch slices only for the C+m lists longer than the LDS list
+        std::vector<uint32_t> nd(n);
+        if (n) HIPCHK(hipMemcpy(nd.data(), ld.rec_nd, 4ull * n, hipMemcpyDeviceToHost));
+        uint64_t sc2 = 0;
+        for (uint32_t r = 0; r < n; r++) {
+            scr_off[r] = sc2;
+            if (nd[r] > PF_K0_TCAP) sc2 += 2ull * nd[r];
+        }
+        scr_off[n] = sc2;
+        free_arena(b, (void *)ld.scr);
+        free_arena(b, (void *)ld.scr_off);
+        uint32_t *p32; ALLOC(p32, sc2 ? sc2 : 1); ld.scr = p32;
+        uint64_t *p64; PUT(p64, scr_off.data(), n + 1); ld.scr_off = p64;
     }
     if (st & PF_ST_FATAL_CIGAR) return fail(PF_ERR_ARG);   // the reference exits (blockjoin.c:776-779)
     if (st & PF_ST_POS_LIMIT) return fail(PF_ERR_LIMIT);    // pos<<3 packing (3398)
@@ -861,11 +879,12 @@ extern "C" int64_t pf_batch_debug_calls(pf_dbatch_t *b, uint64_t *call_off, uint
 }
 
 extern "C" int pf_batch_load_counters(pf_dbatch_t *b, uint64_t *out, int n) {
-    if (!b || !out || n < PF_K0_NCTR) return PF_ERR_ARG;
-    for (int i = 0; i < PF_K0_NCTR; i++) out[i] = 0;
+    if (!b || !out || n < 8) return PF_ERR_ARG;
+    for (int i = 0; i < n; i++) out[i] = 0;
+    if (n > PF_K0_NCTR) n = PF_K0_NCTR;
     if (!b->has_aln) return PF_OK;
     HIPCHK(hipSetDevice(b->ctx->device));
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    HIPCHK(hipMemcpy(out, b->k0_ctr, PF_K0_NCTR * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, b->k0_ctr, 8ull * n, hipMemcpyDeviceToHost));
     return PF_OK;
 }

@@ -692,15 +692,44 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     constexpr uint32_t HN = 8192, HMAX = 6144, BW = 8192;
     uint32_t *hkeys = tile, *hcnt = tile + HN;
     uint64_t *bmap = reinterpret_cast<uint64_t *>(tile + 2 * HN);
-    bool hash_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64;
-    if (hash_ok) {
+    const bool range_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64;
+    bool hash_ok = false;
+    // the window's calls are one contiguous run: flat passes, four
+    // independent (cat, pos) loads in flight per thread
+    const uint64_t C0 = d.read_call_off[r0], C1 = d.read_call_off[r0 + R];
+    // Pass A marks in bmap the positions with >= 2 meth/unmeth calls: a site
+    // needs >= cov_sel calls of each kind, so no other position can qualify.
+    // Pass B counts only those.  Sequencing errors put CpG calls at positions
+    // that one read alone covers; with real reads they outnumber the sites, and
+    // filtering them keeps the table small and its probes short.
+    if (range_ok) {
+        {
+            uint64_t *once = reinterpret_cast<uint64_t *>(tile);   // over the hash table
+            for (uint32_t j = tid; j < BW; j += NT) { once[j] = 0; bmap[j] = 0; }
+            __syncthreads();
+            for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
+                uint32_t cat4[4], pos4[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t c = cb + (uint64_t)u * NT;
+                    const bool ok = c < C1;
+                    cat4[u] = ok ? d.call_cat[c] : 2u;
+                    pos4[u] = ok ? d.call_pos[c] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (cat4[u] >= 2) continue;
+                    const uint32_t o = pos4[u] - pmin;
+                    const unsigned long long bit = 1ull << (o & 63);
+                    if (atomicOr((unsigned long long *)&once[o >> 6], bit) & bit)
+                        atomicOr((unsigned long long *)&bmap[o >> 6], bit);
+                }
+            }
+            __syncthreads();
+        }
         for (uint32_t j = tid; j < HN; j += NT) { hkeys[j] = PF_NONE; hcnt[j] = 0; }
-        for (uint32_t j = tid; j < BW; j += NT) bmap[j] = 0;
         if (tid == 0) { sh_misc[5] = 0; sh_misc[6] = 0; }
         __syncthreads();
-        // the window's calls are one contiguous run: a flat pass, four
-        // independent (cat, pos) loads in flight per thread
-        const uint64_t C0 = d.read_call_off[r0], C1 = d.read_call_off[r0 + R];
         for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
             uint32_t cat4[4], pos4[4];
 #pragma unroll
@@ -715,6 +744,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
                 const uint32_t cat = cat4[u];
                 if (cat >= 2) continue;
                 const uint32_t pos = pos4[u];
+                if (!((bmap[(pos - pmin) >> 6] >> ((pos - pmin) & 63)) & 1ull)) continue;
                 const uint32_t inc = cat == 0 ? 1u : 0x10000u;
                 uint32_t h = (pos * 2654435761u) >> 19;
                 for (;;) {
@@ -733,6 +763,10 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
         }
         __syncthreads();
         hash_ok = sh_misc[6] == 0;
+        if (hash_ok) {                                 // bmap becomes the qualifying bitmap
+            for (uint32_t j = tid; j < BW; j += NT) bmap[j] = 0;
+            __syncthreads();
+        }
     }
     if (hash_ok) {
         for (uint32_t j = tid; j < HN; j += NT) {

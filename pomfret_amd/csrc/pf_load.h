@@ -13,8 +13,9 @@
 #include <stdint.h>
 
 #define PF_K0_WAVES 4
-#define PF_K0_TCAP 2048           /* triggers per wave kept in LDS; longer lists use HBM scratch */
-#define PF_K0_CB 512              /* read positions per emission chunk */
+#define PF_K0_TCAP 768          /* triggers per wave kept in LDS; longer lists use HBM scratch */
+#define PF_K0_MMCAP 4096          /* MM text staged in LDS; longer tags are parsed from HBM */
+#define PF_K0_CB 256              /* read positions per implicit-mode chunk */
 #define PF_K0_EC (PF_K0_CB / 2)   /* explicit / implicit calls per chunk (CpGs are >= 2 apart) */
 #define PF_K0_SEQ_ALIGN 16        /* per-record SEQ slices are 16-byte aligned and padded */
 
@@ -28,7 +29,7 @@
 #define PF_K0C_IMPLICIT 2         /* records in implicit-canonical mode */
 #define PF_K0C_BADMM    3         /* records whose MM/ML could not be decoded */
 #define PF_K0C_DUPCHUNK 4         /* emission chunks with a duplicate position */
-#define PF_K0_NCTR 8
+#define PF_K0_NCTR 16             /* [8..15]: per-phase cycles of the diagnostic build */
 
 struct pf_load_dev {
     uint32_t n_recs;
@@ -51,6 +52,7 @@ struct pf_load_dev {
     uint32_t *scr;
     /* count mode */
     uint32_t *rec_n;                 /* calls of each kept record, PF_NONE when dropped */
+    uint32_t *rec_nd;                /* 5mC skip counts of the record's C+m entry (write-mode scratch sizing) */
     /* write mode */
     const uint32_t *rec_read;        /* read index of each record or PF_NONE */
     const uint64_t *read_call_off;

@@ -1,7 +1,7 @@
 // pf_load.hip -- K0: the window loader of the methphase path on the GPU.
 //
-// One wavefront per BAM record (4 per workgroup).  Reference semantics, all
-// /root/reference/blockjoin.c:
+// One wavefront per BAM record (4 per workgroup, ~9 KB of LDS per wave so 16
+// waves share a CU).  Reference semantics, all /root/reference/blockjoin.c:
 //   filters               load_reads_given_interval 1079-1085
 //   5mC calls at CpG      fill_read_meth_record_from_bam_line 832-882
 //   reference positions   get_mod_poss_on_ref 605-792
@@ -12,24 +12,26 @@
 // the definitions on malformed input, which this kernel shares).
 //
 // Phases of one record (all wave-parallel):
-//  1. MM: find the C+m entry with ballots over 64-byte chunks, parse its skip
-//     counts (one lane per comma) and turn them into ranks with a wave scan.
-//  2. SEQ: stream the 4-bit SEQ in 1024-base chunks (16 bases per lane), count
-//     the C's (forward) or G's (reverse, ranks from the end) per lane, and
-//     resolve each rank to its read position with a 64-entry LDS search and a
-//     select-k-th-bit; the CpG context test and the ML category follow.  The
-//     result is the trigger list T (position<<2 | category), ascending.
-//  3. CIGAR: walk 64 operations per step (prefix sums of read advance and
-//     reference offset), and per 512-position chunk map the triggers that the
-//     reference's `while (i_read+length >= next_trigger)` loop assigns to each
-//     op (an op consumes every trigger up to and INCLUDING its end) and, for
-//     implicit-mode reads, the CpGs of the SEQ inside M ops that the
-//     reference's canonical scan visits.  Both lists are merged in the
-//     reference's push order and de-duplicated against the previous push
-//     (the `calls.a[n-1] == pos` tests at 681, 704, 742).
+//  1. MM: the tag text is staged in LDS (word loads); ballots over 64-byte
+//     steps find the entries, the C+m entry's skip counts are parsed one lane
+//     per comma and turned into ranks with a wave scan.
+//  2. SEQ: stream the 4-bit SEQ in 1024-base chunks (16 bases per lane, next
+//     chunk prefetched), count the C's (forward) or G's (reverse, ranks from
+//     the end) per lane, and resolve each rank to its read position with a
+//     64-entry LDS search and a select-k-th-bit; the CpG context test and the
+//     ML category follow.  Result: the trigger list T (position<<2 | category),
+//     ascending.
+//  3. CIGAR: 64 operations per step (prefix sums of read advance and reference
+//     offset); the triggers each op consumes -- the reference's
+//     `while (i_read+length >= next_trigger)` (663) takes every trigger up to
+//     and INCLUDING the op's end -- are mapped 64 at a time by an LDS search
+//     over the op ends, and pushed with the de-duplication against the previous
+//     push (`calls.a[n-1] == pos`, 704-706).  Implicit-mode reads also scan
+//     their SEQ in 256-position chunks for the CpGs the reference's canonical
+//     scan visits (666-700, 727-761) and merge both lists in push order.
 //  4. The calls are written at the read's offset; a read whose calls are not
-//     strictly increasing (rare) is sorted in place by (pos, cat), which is the
-//     order the methmer kernels consume.
+//     strictly increasing (rare) is sorted in place by (pos, cat), the order
+//     the methmer kernels consume.
 // A record whose leading soft clip swallows every trigger (the stale-trigger
 // case of 629-652) is walked by lane 0 with a literal restatement of the loop.
 #include <hip/hip_runtime.h>
@@ -39,11 +41,30 @@
 
 #define DEV static __device__ __forceinline__
 #define NT_C 2u
+
+// Diagnostic build only (-DPF_K0_PROFILE): cycles per phase summed over the
+// records into ctr[8 + phase] (s_memtime, one fenced asm statement).
+#ifdef PF_K0_PROFILE
+DEV unsigned long long k0_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define K0_STAMP(i) do { const unsigned long long t_ = k0_now(); \
+    if (d.ctr && lane == 0) atomicAdd(&d.ctr[8 + (i)], t_ - k0_t); k0_t = t_; } while (0)
+#define K0_T0 unsigned long long k0_t = k0_now()
+#else
+#define K0_STAMP(i) do { } while (0)
+#define K0_T0 do { } while (0)
+#endif
 #define NT_G 4u
 
 DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 DEV uint64_t lanemask_lt(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 DEV uint32_t popc(uint64_t m) { return (uint32_t)__popcll(m); }
+DEV uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
 
 DEV void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -51,12 +72,28 @@ DEV void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-DEV uint32_t wscan(uint32_t x, uint32_t lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
+// Inclusive wave prefix sum with DPP: row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast:15 / row_bcast:31 carry the row totals upwards (the same
+// sequence pf_selftest checks for the greedy kernel).
+DEV uint32_t dpp_shr_add(uint32_t x, const int ctrl) {
+    uint32_t y;
+    switch (ctrl) {
+    case 1: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true); break;
+    case 2: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true); break;
+    case 4: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true); break;
+    case 8: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true); break;
+    case 15: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); break;
+    default: y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); break;
     }
+    return x + y;
+}
+DEV uint32_t wscan(uint32_t x, uint32_t) {
+    x = dpp_shr_add(x, 1);
+    x = dpp_shr_add(x, 2);
+    x = dpp_shr_add(x, 4);
+    x = dpp_shr_add(x, 8);
+    x = dpp_shr_add(x, 15);
+    x = dpp_shr_add(x, 31);
     return x;
 }
 DEV uint64_t wscan64(uint64_t x, uint32_t lane) {
@@ -68,9 +105,7 @@ DEV uint64_t wscan64(uint64_t x, uint32_t lane) {
     return x;
 }
 DEV uint64_t rdl64(uint64_t x, uint32_t l) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)l);
-    return ((uint64_t)hi << 32) | lo;
+    return ((uint64_t)rdl((uint32_t)(x >> 32), l) << 32) | rdl((uint32_t)x, l);
 }
 
 DEV uint32_t nib(const uint8_t *s, uint32_t i) { return (s[i >> 1] >> ((~i & 1u) << 2)) & 0xFu; }
@@ -101,16 +136,23 @@ DEV uint32_t lb64(const uint32_t *a, uint32_t n, uint32_t v) {
     return lo;
 }
 
-struct K0W {                          // LDS of one wave (~17 KB)
-    uint32_t T[PF_K0_TCAP];           // ranks, then triggers (p<<2 | cat)
-    uint32_t lc[64];                  // per-lane rank bases of a SEQ chunk
-    uint32_t opE[64], opOff[64], opA[64];
+struct K0Merge {                      // implicit-mode chunk lists
     uint32_t eP[PF_K0_EC], eV[PF_K0_EC];
     uint32_t iP[PF_K0_EC], iV[PF_K0_EC];
     uint32_t mV[2 * PF_K0_EC];
-    uint8_t opT[64];
     uint8_t eC[PF_K0_EC];
     uint8_t mC[2 * PF_K0_EC];         // cat | 0x80 for implicit calls
+};
+struct K0W {                          // LDS of one wave (~9.6 KB)
+    uint32_t T[PF_K0_TCAP];           // ranks, then triggers (p<<2 | cat)
+    uint16_t sb[8 * 64];              // SEQ block: rank base of each (row, word pair)
+    uint8_t sc[8 * 64];               //            target count of the pair's first word
+    uint32_t opE[64], opOff[64], opA[64];
+    uint8_t opT[64];
+    union {
+        uint32_t mmw[PF_K0_MMCAP / 4 + 4];   // phase 1: the MM text
+        K0Merge mg;                          // phase 3, implicit mode
+    } u;
 };
 
 // emission state, uniform across the wave
@@ -122,11 +164,11 @@ struct K0Out {
 };
 
 // ---------------------------------------------------------------------------
-// Phase 1: MM/ML -> ranks of the called C's (original orientation) in TB.
-// Returns the number of ranks; *ok = 0 when the tags cannot be decoded.
+// Phase 1: MM/ML -> ranks of the called C's (original orientation).
 struct K0Tgt { uint32_t nd, nc, mi, th, te; uint64_t ml; };
 
-DEV bool k0_mm_entries(const uint8_t *mm, uint32_t mlen, uint32_t mln, uint32_t lane, K0Tgt &t) {
+template <typename CP>
+DEV bool k0_mm_entries(CP mm, uint32_t mlen, uint32_t mln, uint32_t lane, K0Tgt &t) {
     uint32_t i = 0;
     uint64_t ml_cur = 0;
     bool found = false;
@@ -178,8 +220,8 @@ DEV bool k0_mm_entries(const uint8_t *mm, uint32_t mlen, uint32_t mln, uint32_t 
     return true;
 }
 
-template <typename TP>
-DEV bool k0_mm_ranks(const uint8_t *mm, const K0Tgt &t, TP TB, uint32_t lane) {
+template <typename CP, typename TP>
+DEV bool k0_mm_ranks(CP mm, const K0Tgt &t, TP TB, uint32_t lane) {
     if (mm[t.th] != ',') return false;
     uint64_t carry = 0;
     uint32_t idx = 0;
@@ -197,7 +239,9 @@ DEV bool k0_mm_ranks(const uint8_t *mm, const K0Tgt &t, TP TB, uint32_t lane) {
             ok = k > q + 1 && v <= 0xFFFFFFFFull;
             if (gi + 1 < t.nd) ok = ok && k < t.te && mm[k] == ',';
         }
-        const uint64_t incl = wscan64(is_c ? v : 0ull, lane) + carry;
+        const uint64_t x = is_c ? v : 0ull;
+        const uint64_t incl = (__ballot(x >= (1ull << 26)) ? wscan64(x, lane) : (uint64_t)wscan((uint32_t)x, lane)) +
+                              carry;
         const uint64_t rank = incl + gi;
         if (is_c) {
             if (rank > 0xFFFFFFFFull) ok = false;
@@ -210,86 +254,141 @@ DEV bool k0_mm_ranks(const uint8_t *mm, const K0Tgt &t, TP TB, uint32_t lane) {
     return !bad;
 }
 
-// Phase 2: ranks -> triggers (p<<2 | cat) in ascending p, in place in TB.
-// Returns the trigger count (0 on failure); *implicit set when a 5mC call sits
-// outside CpG context (852-858).
-template <typename TP>
-DEV uint32_t k0_seq_pass(const pf_load_dev &d, const uint8_t *seq, uint32_t len, bool rev, const uint8_t *ml,
-                         uint32_t mln, const K0Tgt &t, TP TB, uint32_t *lc, uint32_t lane, bool &implicit) {
-    const uint32_t tb = rev ? NT_G : NT_C;
-    uint32_t carry = 0, ti = 0, nout = 0;
+// Phase 2: ranks -> triggers (p<<2 | cat) in ascending p, into TB.
+// On entry TB[j] = rank | ML value << 24.  Each lane owns a contiguous segment
+// of the read's 16-base words: pass 1 counts the target bases per segment (one
+// scan gives every segment its rank base), each lane then finds the triggers
+// its segment holds (two lower bounds over TB) and pass 2 walks its own words
+// to place them, test the CpG context and write them to OUT in position order;
+// a ballot compaction moves the CpG ones back to TB.  Returns the trigger
+// count (0 when a skip count runs past the read); `implicit` set when a 5mC
+// call sits outside CpG context (852-858).
+DEV uint64_t nibswap(uint64_t w) {                   // base i -> bits 4i..4i+3
+    return ((w & 0x0F0F0F0F0F0F0F0Full) << 4) | ((w >> 4) & 0x0F0F0F0F0F0F0F0Full);
+}
+DEV uint64_t zero_nibbles(uint64_t x) {             // bit 4i set iff nibble i of x == 0
+    uint64_t a = (x | (x >> 1)) & 0x5555555555555555ull;
+    a = (a | (a >> 2)) & 0x1111111111111111ull;
+    return ~a & 0x1111111111111111ull;
+}
+DEV uint64_t valid_nibbles(uint32_t nv) { return nv >= 16 ? 0x1111111111111111ull : ((1ull << (4 * nv)) - 1) & 0x1111111111111111ull; }
+
+template <typename TP, typename OP>
+DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint32_t len, bool rev, const K0Tgt &t,
+                         TP TB, OP OUT, uint32_t lane, bool &implicit) {
+    // Blocks of 1024 16-base words (16384 bases), read by 8 coalesced
+    // wave-instructions of 1 KiB (lane L holds words 2L, 2L+1 of each 128-word
+    // row i).  Target counts per word pair, one scan per row, and each pair's
+    // forward rank base (within the block) and first-word count go to LDS.  The
+    // block's triggers are then placed one per lane: row by the 8 row prefixes,
+    // pair by an LDS search, word by the first-word count, base by a select in
+    // the re-read word.  Reverse reads walk the blocks from the end (their
+    // ranks count from the end) and turn the rank into a forward one.
+    constexpr uint32_t ROWS = 8, RW = 128, BW = ROWS * RW;
+    const uint64_t pat = (rev ? (uint64_t)NT_G : (uint64_t)NT_C) * 0x1111111111111111ull;
+    const uint4 *sq4 = reinterpret_cast<const uint4 *>(seq);
+    const uint64_t *sw = reinterpret_cast<const uint64_t *>(seq);
+    const uint32_t nwords = (len + 15) / 16;
+    const uint32_t nblk = (nwords + BW - 1) / BW;
+    const uint32_t nd = t.nd;
+    uint32_t carry = 0, ti = 0;
     bool imp = false;
-    const uint32_t nch = (len + 1023) / 1024;
-    for (uint32_t ci = 0; ci < nch && ti < t.nd; ci++) {
-        const uint32_t c0 = (rev ? nch - 1 - ci : ci) * 1024u;
-        const uint32_t b0 = c0 + 16u * lane;
-        const uint32_t nv = b0 < len ? (len - b0 < 16u ? len - b0 : 16u) : 0u;
-        const uint64_t w = nv ? *reinterpret_cast<const uint64_t *>(seq + (b0 >> 1)) : 0ull;
-        const uint32_t m = match16(w, tb, nv);
-        const uint32_t cnt = (uint32_t)__builtin_popcount(m);
-        const uint32_t incl = wscan(cnt, lane);
-        const uint32_t tot = uni(__shfl(incl, 63, 64));
-        lc[lane] = rev ? carry + tot - incl : carry + incl - cnt;
-        wsync();
-        for (;;) {
-            const uint32_t j = ti + lane;
-            const uint32_t rk = j < t.nd ? TB[j] : 0xFFFFFFFFu;
-            const bool inr = j < t.nd && rk < carry + tot;
-            const uint64_t bal = __ballot(inr);
-            if (!bal) break;
-            const uint32_t nb = popc(bal);
-            // owning lane: last lane with lc <= rk (forward), first (reverse)
-            uint32_t L = 0;
-            if (rev) {
-                uint32_t lo = 0, n = 64;
-                while (n > 0) { const uint32_t h = n >> 1; if (lc[lo + h] > rk) { lo += h + 1; n -= h + 1; } else n = h; }
-                L = lo;
-            } else {
-                uint32_t lo = 0, n = 64;
-                while (n > 0) { const uint32_t h = n >> 1; if (lc[lo + h] <= rk) { lo += h + 1; n -= h + 1; } else n = h; }
-                L = lo - 1;
-            }
-            L = inr ? L : lane;
-            const uint64_t wl = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(w >> 32), (int)L, 64) << 32) |
-                                (uint32_t)__shfl((int)(uint32_t)w, (int)L, 64);
-            const uint32_t ml_ = (uint32_t)__shfl((int)m, (int)L, 64);
-            bool pass = false, hit = false;
-            uint32_t key = 0;
-            if (inr) {
-                const uint32_t k = rk - lc[L];
-                const uint32_t cL = (uint32_t)__builtin_popcount(ml_);
-                const uint32_t bit = select_bit(ml_, rev ? cL - 1 - k : k);
-                const uint32_t p = c0 + 16u * L + bit;
-                const uint32_t q = mln ? ml[t.ml + (uint64_t)j * t.nc + t.mi] : 255u;
-                if (p > 0 && p < len - 1) {
-                    const bool ctx = nibw(wl, bit) == NT_C ? nib(seq, p + 1) == NT_G : nib(seq, p - 1) == NT_C;
-                    pass = ctx;
-                    hit = !ctx;
+    for (uint32_t bb = 0; bb < nblk && ti < nd; bb++) {
+        const uint32_t b = rev ? nblk - 1 - bb : bb;
+        uint4 v[ROWS];
+#pragma unroll
+        for (uint32_t i = 0; i < ROWS; i++) {
+            const uint32_t w = b * BW + i * RW + 2 * lane;
+            v[i] = w < nwords ? sq4[w >> 1] : make_uint4(0, 0, 0, 0);
+        }
+        uint32_t pref[ROWS];
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < ROWS; i++) {
+            const uint32_t w = b * BW + i * RW + 2 * lane;
+            const uint64_t xs[2] = {((uint64_t)v[i].y << 32) | v[i].x, ((uint64_t)v[i].w << 32) | v[i].z};
+            uint32_t c[2];
+#pragma unroll
+            for (uint32_t h = 0; h < 2; h++) {
+                c[h] = 0;
+                if (w + h < nwords) {
+                    uint64_t z = zero_nibbles(xs[h] ^ pat);
+                    if ((w + h) * 16 + 16 > len) z = zero_nibbles(nibswap(xs[h]) ^ pat) & valid_nibbles(len - (w + h) * 16);
+                    c[h] = (uint32_t)__popcll(z);
                 }
-                const uint32_t cat = q < d.lo ? 1u : q >= d.hi ? 0u : 2u;
-                key = (p << 2) | cat;
             }
-            const uint64_t pb = __ballot(pass);
-            if (pass) TB[nout + popc(pb & lanemask_lt(lane))] = key;
-            if (__ballot(hit)) imp = true;
-            nout += popc(pb);
-            ti += nb;
-            wsync();
-            if (nb < 64) break;
+            const uint32_t cp = c[0] + c[1];
+            const uint32_t inc = wscan(cp, lane);
+            pref[i] = run;
+            L.sb[i * 64 + lane] = (uint16_t)(run + inc - cp);
+            L.sc[i * 64 + lane] = (uint8_t)c[0];
+            run += uni(__shfl(inc, 63, 64));
         }
-        carry += tot;
-        wsync();
-    }
-    implicit = imp;
-    if (ti < t.nd) return 0;                          // skip counts beyond the read
-    if (rev) {                                        // produced in descending p
-        for (uint32_t a = lane; a < nout / 2; a += 64) {
-            const uint32_t x = TB[a], y = TB[nout - 1 - a];
-            TB[a] = y;
-            TB[nout - 1 - a] = x;
+        const uint32_t btot = run;
+        // the block's triggers: ranks < carry + btot, from ti on
+        uint32_t tend = ti;
+        {
+            uint32_t n = nd - ti;
+            while (n > 0) {
+                const uint32_t h = n >> 1;
+                if ((TB[tend + h] & 0xFFFFFFu) < carry + btot) { tend += h + 1; n -= h + 1; } else n = h;
+            }
+            tend = uni(tend);
         }
         wsync();
+        for (uint32_t j0 = ti; j0 < tend; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            if (j < tend) {
+                const uint32_t e = TB[j];
+                const uint32_t rr = (e & 0xFFFFFFu) - carry;
+                const uint32_t f = rev ? btot - 1 - rr : rr;    // forward rank inside the block
+                uint32_t i = 0;
+#pragma unroll
+                for (uint32_t q = 1; q < ROWS; q++) i += pref[q] <= f ? 1u : 0u;
+                const uint16_t *sbi = L.sb + i * 64;
+                uint32_t lo = 0, n = 64;                        // last pair with base <= f
+                while (n > 0) { const uint32_t h = n >> 1; if (sbi[lo + h] <= f) { lo += h + 1; n -= h + 1; } else n = h; }
+                const uint32_t Lw = lo - 1;
+                uint32_t k = f - sbi[Lw];
+                const uint32_t c0 = L.sc[i * 64 + Lw];
+                uint32_t hw = 0;
+                if (k >= c0) { k -= c0; hw = 1; }
+                const uint32_t w = b * BW + i * RW + 2 * Lw + hw;
+                const uint64_t xw = nibswap(sw[w]);
+                uint64_t m = zero_nibbles(xw ^ pat);
+                for (uint32_t s2 = k; s2 > 0; s2--) m &= m - 1;
+                const uint32_t bi = (uint32_t)__builtin_ctzll(m) >> 2;
+                const uint32_t p = w * 16 + bi;
+                uint32_t key = 0xFFFFFFFFu;
+                if (p > 0 && p < len - 1) {
+                    bool ctx;
+                    if (!rev) ctx = (bi < 15 ? (uint32_t)(xw >> (4 * (bi + 1))) & 15u : nib(seq, p + 1)) == NT_G;
+                    else ctx = (bi > 0 ? (uint32_t)(xw >> (4 * (bi - 1))) & 15u : nib(seq, p - 1)) == NT_C;
+                    if (ctx) {
+                        const uint32_t q = e >> 24;
+                        key = (p << 2) | (q < d.lo ? 1u : q >= d.hi ? 0u : 2u);
+                    } else imp = true;
+                }
+                OUT[rev ? nd - 1 - j : j] = key;
+            }
+        }
+        wsync();
+        ti = tend;
+        carry += btot;
     }
+    implicit = __ballot(imp) != 0;
+    if (ti < nd) return 0;                            // skip counts beyond the read
+    wsync();
+    // compaction OUT -> TB (order kept)
+    uint32_t nout = 0;
+    for (uint32_t c0 = 0; c0 < nd; c0 += 64) {
+        const uint32_t jj = c0 + lane;
+        const uint32_t key = jj < nd ? OUT[jj] : 0xFFFFFFFFu;
+        const uint64_t pb = __ballot(key != 0xFFFFFFFFu);
+        if (key != 0xFFFFFFFFu) TB[nout + popc(pb & lanemask_lt(lane))] = key;
+        nout += popc(pb);
+    }
+    wsync();
     return nout;
 }
 
@@ -307,6 +406,46 @@ DEV void k0_emit_one(K0Out &o, uint32_t v, uint32_t cat, bool implicit) {
     if (v >= (1u << 29)) o.lim = 1;
     o.last = v;
     o.n++;
+}
+
+DEV void k0_bcast(K0Out &o, const K0Out &s) {
+    o.n = uni(s.n); o.first = uni(s.first); o.last = uni(s.last);
+    o.sorted = uni(s.sorted); o.lim = uni(s.lim);
+}
+
+// Emit up to 64 calls held one per lane (lanes with `keep`, in lane order,
+// `imp` marking implicit calls): parallel unless one repeats the previous
+// push's position, then lane 0 replays them through k0_emit_one.
+template <int MODE>
+DEV void k0_emit_lanes(const pf_load_dev &d, K0Out &o, bool keep, uint32_t v, uint32_t cat, bool imp,
+                       uint32_t lane, uint32_t *sv, uint8_t *sc) {
+    const uint64_t bk = __ballot(keep);
+    if (!bk) return;
+    const uint32_t cnt = popc(bk);
+    const uint64_t below = bk & lanemask_lt(lane);
+    const uint32_t idx = popc(below);
+    const uint32_t pl = below ? 63u - (uint32_t)__clzll(below) : lane;
+    const uint32_t vprev_l = (uint32_t)__shfl((int)v, (int)pl, 64);
+    const uint32_t vprev = below ? vprev_l : o.last;
+    const bool has_prev = below != 0 || o.n > 0;
+    if (__ballot(keep && has_prev && v == vprev)) {
+        if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_DUPCHUNK], 1ull);
+        if (keep) { sv[idx] = v; sc[idx] = (uint8_t)(cat | (imp ? 0x80u : 0u)); }
+        wsync();
+        K0Out s = o;
+        if (lane == 0)
+            for (uint32_t q = 0; q < cnt; q++) k0_emit_one<MODE>(s, sv[q], sc[q] & 3u, (sc[q] & 0x80u) != 0);
+        k0_bcast(o, s);
+        wsync();
+        return;
+    }
+    if (MODE && keep) { o.pos[o.n + idx] = v; o.cat[o.n + idx] = (uint8_t)cat; }
+    if (__ballot(keep && has_prev && v < vprev)) o.sorted = 0;
+    if (__ballot(keep && v >= (1u << 29))) o.lim = 1;
+    const uint32_t fl = (uint32_t)__ffsll((long long)bk) - 1, ll = 63u - (uint32_t)__clzll(bk);
+    if (o.n == 0) o.first = rdl(v, fl);
+    o.last = rdl(v, ll);
+    o.n += cnt;
 }
 
 // Lane 0 walks the record with the reference loop itself (605-792): used for
@@ -391,6 +530,107 @@ DEV uint32_t k0_tlb(TP TB, uint32_t n, uint32_t x) {
     return lo;
 }
 
+// Implicit mode: one chunk of read positions [c0, c0 + CB) of a CIGAR tile.
+// Explicit triggers with p <= a_end and CpGs in [a_cur, a_end) that the
+// reference's scan visits, merged in push order, then emitted.
+template <int MODE, typename TP>
+DEV void k0_chunk_implicit(const pf_load_dev &d, K0W &L, uint32_t nv, uint32_t c0, uint32_t a_cur, uint32_t a_end,
+                           uint32_t i_ref, uint32_t cgoffset, bool rev, TP TB, uint32_t nT, uint32_t &tc,
+                           const uint8_t *seq, uint32_t len, uint32_t lane, K0Out &o) {
+    K0Merge &M = L.u.mg;
+    const uint32_t c1 = c0 + PF_K0_CB;
+    uint32_t ne = 0;
+    for (;;) {
+        const uint32_t k = tc + lane;
+        const uint32_t key = k < nT ? TB[k] : 0xFFFFFFFFu;
+        const uint32_t p = key >> 2;
+        const bool in = k < nT && p < c1 && p <= a_end;
+        const uint64_t bi = __ballot(in);
+        if (!bi) break;
+        bool keep = false;
+        uint32_t v = 0;
+        if (in) {
+            const uint32_t oi = lb64<false>(L.opE, nv, p);
+            keep = L.opT[oi] == 0;
+            v = i_ref + p + cgoffset + L.opOff[oi];
+        }
+        const uint64_t bk = __ballot(keep);
+        if (keep) {
+            const uint32_t x = ne + popc(bk & lanemask_lt(lane));
+            M.eP[x] = p;
+            M.eV[x] = v;
+            M.eC[x] = (uint8_t)(key & 3u);
+        }
+        ne += popc(bk);
+        tc += popc(bi);
+        if (popc(bi) < 64) break;
+    }
+    uint32_t ni = 0;
+    if (c0 < a_end) {
+        const uint32_t lo = a_cur > c0 ? a_cur : c0;
+        const uint32_t hi = a_end < c1 ? a_end : c1;
+        const uint32_t b0 = c0 + 4u * lane;            // 4 positions per lane
+        uint32_t cm = 0;
+        if (b0 < hi && b0 + 4 > lo && b0 < len) {
+            const uint32_t w0 = *reinterpret_cast<const uint32_t *>(seq + (b0 >> 1) - ((b0 >> 1) & 3u));
+            const uint32_t w1 = *reinterpret_cast<const uint32_t *>(seq + (b0 >> 1) - ((b0 >> 1) & 3u) + 4);
+            const uint64_t w = (((uint64_t)w1 << 32) | w0) >> (8u * ((b0 >> 1) & 3u));
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t p = b0 + i;
+                if (p >= lo && p < hi && p + 1 < len && nibw(w, i) == NT_C && nibw(w, i + 1) == NT_G) cm |= 1u << i;
+            }
+        }
+        uint32_t kept = 0;
+        uint32_t vv[2], pp[2];
+        for (uint32_t mm = cm; mm; mm &= mm - 1) {
+            const uint32_t p = b0 + (uint32_t)__builtin_ctz(mm);
+            const uint32_t oi = lb64<true>(L.opE, nv, p);
+            if (oi >= nv || L.opT[oi] != 0) continue;
+            const uint32_t ao = L.opA[oi];
+            // excluded: the positions [t-1, t+1+rev) around a trigger t the same op consumed
+            uint32_t x = k0_tlb(TB, nT, p ? p - 1 : 0u);
+            bool ex = false;
+            for (; x < nT && (TB[x] >> 2) <= p + 1; x++) {
+                const uint32_t tp = TB[x] >> 2;
+                if (tp == p + 1 || (tp == p && p > ao) || (rev && tp + 1 == p && tp > ao)) ex = true;
+            }
+            if (ex) continue;
+            pp[kept] = p;
+            vv[kept] = i_ref + p + L.opOff[oi];
+            kept++;
+        }
+        const uint32_t inc = wscan(kept, lane);
+        for (uint32_t i = 0; i < kept; i++) {
+            M.iP[inc - kept + i] = pp[i];
+            M.iV[inc - kept + i] = vv[i];
+        }
+        ni = uni(__shfl(inc, 63, 64));
+    }
+    wsync();
+    const uint32_t nm = ne + ni;
+    if (nm == 0) return;
+    for (uint32_t q = lane; q < ne; q += 64) {
+        const uint32_t r = q + lb64<false>(M.iP, ni, M.eP[q]);
+        M.mV[r] = M.eV[q];
+        M.mC[r] = M.eC[q];
+    }
+    for (uint32_t q = lane; q < ni; q += 64) {
+        const uint32_t r = q + lb64<true>(M.eP, ne, M.iP[q]);
+        M.mV[r] = M.iV[q];
+        M.mC[r] = 0x80 | 1u;
+    }
+    wsync();
+    for (uint32_t q0 = 0; q0 < nm; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool keep = q < nm;
+        const uint32_t v = keep ? M.mV[q] : 0u, c = keep ? M.mC[q] : 0u;
+        wsync();
+        k0_emit_lanes<MODE>(d, o, keep, v, c & 3u, (c & 0x80u) != 0, lane, M.eP, M.eC);
+        wsync();
+    }
+}
+
 // Wave-parallel walk (phase 3).  Returns false when the CIGAR reaches a
 // fatal operation.
 template <int MODE, typename TP>
@@ -407,12 +647,14 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
         j = 1;
     }
     bool trunc = false;
-    while (j < ncig && !trunc) {
+    uint32_t cn = j + lane < ncig ? cig[j + lane] : 4u;   // next tile in flight
+    while (j < ncig && !trunc && (tc < nT || implicit)) {
         // ---- 64 CIGAR operations: read starts, reference offsets, ends
         const uint32_t g = j + lane;
-        const uint32_t c = g < ncig ? cig[g] : (4u);   // past the end acts as a stop
+        const uint32_t c = cn;
+        if (j + 64 < ncig) cn = j + 64 + lane < ncig ? cig[j + 64 + lane] : 4u;
         const uint32_t op = c & 15u, ln = c >> 4;
-        const uint64_t stop = __ballot(op == 3u || op == 4u);
+        const uint64_t stop = __ballot(op == 3u || op == 4u);     // past the end acts as a stop
         const uint64_t bad = __ballot(op > 4u && g < ncig);
         const uint32_t fs = stop ? (uint32_t)__ffsll((long long)stop) - 1 : 64u;
         const uint32_t fb = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 64u;
@@ -431,16 +673,13 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
         const uint32_t a_end = a_cur + uni(__shfl(rin, 63, 64));
         const uint32_t off_end = off_cur + uni(__shfl(din, 63, 64));
         wsync();
-        // ---- chunks of read positions: explicit p in (a_cur, a_end], implicit p in [a_cur, a_end)
-        for (uint32_t c0 = a_cur & ~7u; c0 <= a_end && (c0 < a_end || tc < nT); c0 += PF_K0_CB) {
-            const uint32_t c1 = c0 + PF_K0_CB;
-            // explicit triggers of the chunk
-            uint32_t ne = 0;
+        if (!implicit) {
+            // the triggers this tile consumes (p <= a_end), 64 at a time
             for (;;) {
                 const uint32_t k = tc + lane;
                 const uint32_t key = k < nT ? TB[k] : 0xFFFFFFFFu;
                 const uint32_t p = key >> 2;
-                const bool in = k < nT && p < c1 && p <= a_end;
+                const bool in = k < nT && p <= a_end;
                 const uint64_t bi = __ballot(in);
                 if (!bi) break;
                 bool keep = false;
@@ -450,127 +689,54 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
                     keep = L.opT[oi] == 0;
                     v = i_ref + p + cgoffset + L.opOff[oi];
                 }
-                const uint64_t bk = __ballot(keep);
-                if (keep) {
-                    const uint32_t x = ne + popc(bk & lanemask_lt(lane));
-                    L.eP[x] = p;
-                    L.eV[x] = v;
-                    L.eC[x] = (uint8_t)(key & 3u);
-                }
-                ne += popc(bk);
+                k0_emit_lanes<MODE>(d, o, keep, v, key & 3u, false, lane, L.u.mg.mV, L.u.mg.mC);
                 tc += popc(bi);
                 if (popc(bi) < 64) break;
             }
-            // implicit canonicals of the chunk (8 positions per lane)
-            uint32_t ni = 0;
-            if (implicit && c0 < a_end) {
-                const uint32_t lo = a_cur > c0 ? a_cur : c0;
-                const uint32_t hi = a_end < c1 ? a_end : c1;
-                const uint32_t b0 = c0 + 8u * lane;
-                uint32_t cm = 0;
-                if (b0 < hi && b0 + 8 > lo && b0 < len) {
-                    const uint32_t w0 = *reinterpret_cast<const uint32_t *>(seq + (b0 >> 1));
-                    const uint32_t w1 = *reinterpret_cast<const uint32_t *>(seq + (b0 >> 1) + 4);
-                    const uint64_t w = ((uint64_t)w1 << 32) | w0;
-#pragma unroll
-                    for (uint32_t i = 0; i < 8; i++) {
-                        const uint32_t p = b0 + i;
-                        if (p >= lo && p < hi && p + 1 < len && nibw(w, i) == NT_C && nibw(w, i + 1) == NT_G)
-                            cm |= 1u << i;
-                    }
-                }
-                // keep the CpGs the reference's scan visits: inside an M op,
-                // not within a consumed trigger's exclusion window
-                uint32_t kept = 0;
-                uint32_t vv[4], pp[4];
-                for (uint32_t mm = cm; mm; mm &= mm - 1) {
-                    const uint32_t p = b0 + (uint32_t)__builtin_ctz(mm);
-                    const uint32_t oi = lb64<true>(L.opE, nv, p);
-                    if (oi >= nv || L.opT[oi] != 0) continue;
-                    const uint32_t ao = L.opA[oi];
-                    uint32_t x = k0_tlb(TB, nT, p ? p - 1 : 0u);
-                    bool ex = false;
-                    for (; x < nT && (TB[x] >> 2) <= p + 1; x++) {
-                        const uint32_t tp = TB[x] >> 2;
-                        if (tp == p + 1 || (tp == p && p > ao) || (rev && tp + 1 == p && tp > ao)) ex = true;
-                    }
-                    if (ex) continue;
-                    pp[kept] = p;
-                    vv[kept] = i_ref + p + L.opOff[oi];
-                    kept++;
-                }
-                const uint32_t inc = wscan(kept, lane);
-                for (uint32_t i = 0; i < kept; i++) {
-                    L.iP[inc - kept + i] = pp[i];
-                    L.iV[inc - kept + i] = vv[i];
-                }
-                ni = uni(__shfl(inc, 63, 64));
-            }
-            wsync();
-            // ---- merge in push order (by position; explicit first on ties) and emit
-            const uint32_t nm = ne + ni;
-            if (nm == 0) continue;
-            if (ni == 0) {
-                for (uint32_t q = lane; q < ne; q += 64) { L.mV[q] = L.eV[q]; L.mC[q] = L.eC[q]; }
-            } else {
-                for (uint32_t q = lane; q < ne; q += 64) {
-                    const uint32_t r = q + lb64<false>(L.iP, ni, L.eP[q]);
-                    L.mV[r] = L.eV[q];
-                    L.mC[r] = L.eC[q];
-                }
-                for (uint32_t q = lane; q < ni; q += 64) {
-                    const uint32_t r = q + lb64<true>(L.eP, ne, L.iP[q]);
-                    L.mV[r] = L.iV[q];
-                    L.mC[r] = 0x80 | 1u;
-                }
-            }
-            wsync();
-            bool dup = false;
-            for (uint32_t q0 = 0; q0 < nm; q0 += 64) {
-                const uint32_t q = q0 + lane;
-                const uint32_t prev = q == 0 ? o.last : L.mV[q - 1];
-                if (__ballot(q < nm && (q > 0 || o.n > 0) && L.mV[q] == prev)) dup = true;
-            }
-            if (dup) {                                // rare: sequential emission with qual replacement
-                if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_DUPCHUNK], 1ull);
-                K0Out s = o;
-                if (lane == 0)
-                    for (uint32_t q = 0; q < nm; q++)
-                        k0_emit_one<MODE>(s, L.mV[q], L.mC[q] & 3u, (L.mC[q] & 0x80) != 0);
-                o.n = uni(s.n); o.first = uni(s.first); o.last = uni(s.last);
-                o.sorted = uni(s.sorted); o.lim = uni(s.lim);
-            } else {
-                bool uns = false, lim = false;
-                for (uint32_t q0 = 0; q0 < nm; q0 += 64) {
-                    const uint32_t q = q0 + lane;
-                    if (q < nm) {
-                        const uint32_t v = L.mV[q];
-                        if (MODE) { o.pos[o.n + q] = v; o.cat[o.n + q] = L.mC[q] & 3u; }
-                        const uint32_t prev = q == 0 ? o.last : L.mV[q - 1];
-                        if ((q > 0 || o.n > 0) && v < prev) uns = true;
-                        if (v >= (1u << 29)) lim = true;
-                    }
-                }
-                if (__ballot(uns)) o.sorted = 0;
-                if (__ballot(lim)) o.lim = 1;
-                if (o.n == 0) o.first = L.mV[0];
-                o.last = L.mV[nm - 1];
-                o.n += nm;
-            }
-            wsync();
+        } else {
+            for (uint32_t c0 = a_cur & ~3u; c0 <= a_end && (c0 < a_end || tc < nT); c0 += PF_K0_CB)
+                k0_chunk_implicit<MODE>(d, L, nv, c0, a_cur, a_end, i_ref, cgoffset, rev, TB, nT, tc, seq, len,
+                                        lane, o);
         }
+        wsync();
         a_cur = a_end;
         off_cur = off_end;
+        j += 64;
+    }
+    // fatal operations past the last consumed trigger are still reached
+    // by the reference's loop (it walks every op up to N/S)
+    while (j < ncig && !trunc) {
+        const uint32_t g = j + lane;
+        const uint32_t op = g < ncig ? cig[g] & 15u : 4u;
+        const uint64_t stop = __ballot(op == 3u || op == 4u);
+        const uint64_t bad = __ballot(op > 4u && g < ncig);
+        const uint32_t fs = stop ? (uint32_t)__ffsll((long long)stop) - 1 : 64u;
+        const uint32_t fb = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 64u;
+        if (fb < fs) return false;
+        trunc = fs < 64;
         j += 64;
     }
     return true;
 }
 
+// Stage the MM text in LDS with word loads (the device copy is padded, so the
+// last word may run past the text).  Returns the LDS view of the text.
+DEV const uint8_t *k0_stage_mm(const uint8_t *g, uint32_t n, uint32_t *dst, uint32_t lane) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(g);
+    const uint32_t mis = (uint32_t)(a & 3u);
+    const uint32_t *gw = reinterpret_cast<const uint32_t *>(a - mis);
+    const uint32_t nw = (n + mis + 3) / 4;
+#pragma unroll 4
+    for (uint32_t k = lane; k < nw; k += 64) dst[k] = gw[k];
+    wsync();
+    return reinterpret_cast<const uint8_t *>(dst) + mis;
+}
+
 template <int MODE, typename TP>
-DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, uint32_t cap) {
+DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, TP OUT, uint32_t cap) {
     const uint32_t len = d.l_qseq[r];
     const bool rev = (d.flag[r] & 16u) != 0;
-    const uint8_t *mm = d.mm + d.mm_off[r];
+    const uint8_t *mmg = d.mm + d.mm_off[r];
     const uint32_t mlen = (uint32_t)(d.mm_off[r + 1] - d.mm_off[r]);
     const uint8_t *ml = d.ml + d.ml_off[r];
     const uint32_t mln = (uint32_t)(d.ml_off[r + 1] - d.ml_off[r]);
@@ -579,12 +745,37 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     const uint32_t ncig = (uint32_t)(d.cigar_off[r + 1] - d.cigar_off[r]);
 
     K0Tgt t;
-    bool okmm = k0_mm_entries(mm, mlen, mln, lane, t);
+    bool okmm;
     uint32_t nT = 0;
     bool implicit = false;
-    if (okmm && t.nd > cap) okmm = false;           // only a malformed tag lists more calls than its size allows
-    if (okmm && t.nd) okmm = k0_mm_ranks(mm, t, TB, lane);
-    if (okmm && t.nd) nT = k0_seq_pass(d, seq, len, rev, ml, mln, t, TB, L.lc, lane, implicit);
+    K0_T0;
+    if (mlen <= PF_K0_MMCAP) {
+        const uint8_t *mm = k0_stage_mm(mmg, mlen, L.u.mmw, lane);
+        okmm = k0_mm_entries(mm, mlen, mln, lane, t);
+        if (okmm && t.nd > cap) okmm = false;       // only a malformed tag lists more calls than its size allows
+        if (okmm && t.nd) okmm = k0_mm_ranks(mm, t, TB, lane);
+    } else {
+        okmm = k0_mm_entries(mmg, mlen, mln, lane, t);
+        if (okmm && t.nd > cap) okmm = false;
+        if (okmm && t.nd) okmm = k0_mm_ranks(mmg, t, TB, lane);
+    }
+    if (MODE == 0 && lane == 0) d.rec_nd[r] = okmm ? t.nd : 0u;
+    wsync();
+    bool past = false;
+    if (okmm && t.nd) {                               // the C+m entry's ML values ride in the ranks' top byte
+#pragma unroll 4
+        for (uint32_t j = lane; j < t.nd; j += 64) {
+            const uint32_t q = mln ? ml[t.ml + (uint64_t)j * t.nc + t.mi] : 255u;
+            const uint32_t rk = TB[j];
+            past |= rk >= (1u << 24);                 // l_qseq < 2^24: such a rank is past the read's C's
+            TB[j] = (rk & 0xFFFFFFu) | (q << 24);
+        }
+        past = __ballot(past) != 0;
+        wsync();
+    }
+    K0_STAMP(0);
+    if (okmm && t.nd && !past) nT = k0_seq_pass(d, L, seq, len, rev, t, TB, OUT, lane, implicit);
+    K0_STAMP(1);
     if (!okmm && d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_BADMM], 1ull);
     nT = uni(nT);
 
@@ -607,12 +798,12 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
         K0Out s = o;
         bool f = false;
         if (lane == 0) k0_walk_seq<MODE>(cig, ncig, qs, rev, TB, nT, implicit ? seq : nullptr, len, s, f);
-        o.n = uni(s.n); o.first = uni(s.first); o.last = uni(s.last);
-        o.sorted = uni(s.sorted); o.lim = uni(s.lim);
+        k0_bcast(o, s);
         fatal = uni(f ? 1u : 0u) != 0;
     } else {
         fatal = !k0_walk<MODE>(d, L, cig, ncig, qs, rev, TB, nT, seq, len, implicit, lane, o);
     }
+    K0_STAMP(2);
     if (fatal) {
         if (lane == 0) atomicOr(d.status, PF_ST_FATAL_CIGAR);
         if (MODE == 0 && lane == 0) d.rec_n[r] = PF_NONE;
@@ -655,6 +846,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
         d.read_first[ri] = o.first;
         d.read_last[ri] = o.last;
     }
+    K0_STAMP(3);
 }
 
 template <int MODE>
@@ -671,12 +863,12 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) void pf_k0_load(pf_load_dev d) {
     const bool drop = (flag & 4u) || (flag & 256u) || (flag & 2048u) || (uint32_t)d.mapq[r] < d.min_mapq ||
                       d.l_qseq[r] < 2u || d.l_qseq[r] < d.min_len || (double)d.de[r] > 0.1;
     if (drop) {
-        if (MODE == 0 && lane == 0) d.rec_n[r] = PF_NONE;
+        if (MODE == 0 && lane == 0) { d.rec_n[r] = PF_NONE; d.rec_nd[r] = 0; }
         return;
     }
     const uint64_t s0 = d.scr_off[r], s1 = d.scr_off[r + 1];
-    if (s1 == s0) k0_record<MODE>(d, L, r, lane, L.T, (uint32_t)PF_K0_TCAP);
-    else k0_record<MODE>(d, L, r, lane, d.scr + s0, (uint32_t)(s1 - s0));
+    if (s1 == s0) k0_record<MODE>(d, L, r, lane, L.T, L.u.mmw, (uint32_t)PF_K0_TCAP);
+    else k0_record<MODE>(d, L, r, lane, d.scr + s0, d.scr + s0 + (s1 - s0) / 2, (uint32_t)((s1 - s0) / 2));
 }
 
 template __global__ void pf_k0_load<0>(pf_load_dev d);

@@ -26,6 +26,7 @@ Everything is a pure function of (seed, window index).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -278,10 +279,26 @@ def make_aln_window(spec: AlnSpec, w: int):
     return dict(s=s, e=e, orient=orient, pos=starts, flag=flag, mapq=mapq, de=de, hp=hp, recs=out)
 
 
-def make_aln_batch(spec: AlnSpec, windows=None) -> AlnBatch:
+def _window_job(args):
+    return make_aln_window(*args)
+
+
+def make_aln_batch(spec: AlnSpec, windows=None, workers: int = 0) -> AlnBatch:
+    """workers: processes generating windows in parallel (0: up to 16 when
+    there are many windows; every window is a pure function of its index,
+    so the result does not depend on it)."""
     if windows is None:
         windows = range(spec.n_windows)
-    parts = [make_aln_window(spec, w) for w in windows]
+    windows = list(windows)
+    if workers == 0:
+        env = os.environ.get("PF_SYNTH_WORKERS")
+        workers = int(env) if env else (min(16, os.cpu_count() or 1) if len(windows) >= 16 else 1)
+    if workers > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            parts = pool.map(_window_job, [(spec, w) for w in windows], chunksize=1)
+    else:
+        parts = [make_aln_window(spec, w) for w in windows]
     recs = [r for p in parts for r in p["recs"]]
 
     def off(key, f=lambda x: x.shape[0]):
@@ -308,4 +325,21 @@ def make_aln_batch(spec: AlnSpec, windows=None) -> AlnBatch:
     )
     b.meta["orient"] = np.array([p["orient"] for p in parts], np.int8)
     b.meta["spec"] = spec
+    return b
+
+
+_SAVE_FIELDS = ("win_start", "win_end", "win_rec_off", "flag", "mapq", "pos", "l_qseq", "de", "hp",
+                "cigar_off", "cigar", "seq_off", "seq", "mm_off", "mm", "ml_off", "ml")
+
+
+def save_aln(path: str, aln: AlnBatch) -> None:
+    """Write a record-level batch as a plain .npz (no pickled objects)."""
+    np.savez(path, orient=aln.meta.get("orient", np.zeros(0, np.int8)),
+             **{k: getattr(aln, k) for k in _SAVE_FIELDS})
+
+
+def load_aln(path: str) -> AlnBatch:
+    with np.load(path, allow_pickle=False) as z:
+        b = AlnBatch(**{k: z[k] for k in _SAVE_FIELDS})
+        b.meta["orient"] = z["orient"]
     return b

@@ -85,3 +85,16 @@ def test_record_level_path_recovers_orientation(oracle_lib):
     b, _ = oracle_lib.load_reads(LOAD_CFG_SMALL, a)
     res = oracle_lib.methphase(Config.from_coverage(30, given=False), b, n_threads=4)
     assert np.array_equal(res.decision, a.meta["orient"])
+
+
+def test_threaded_record_level_path_matches_two_step(oracle_lib):
+    """orc_methphase_aln (per-window load + worker, threaded: the CPU
+    baseline of the record-level bench) equals load_reads + methphase."""
+    from pomfret_amd import Config, LoadConfig
+    cfg = Config.from_coverage(30, given=False)
+    a = synth_aln(3, 30, 12, clip_frac=0.5, filt_frac=0.1)
+    b, _ = oracle_lib.load_reads(LoadConfig(), a)
+    ref = oracle_lib.methphase(cfg, b, n_threads=2)
+    got = oracle_lib.methphase_aln(cfg, LoadConfig(), a, n_threads=3)
+    for f in ("decision", "dir_table", "dir_join", "dir_which_way", "win_n_sites", "win_n_reads"):
+        assert np.array_equal(getattr(ref, f), getattr(got, f)), f
