@@ -482,7 +482,7 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         const uint64_t mln = a->ml_off[r + 1] - a->ml_off[r], mlen = a->mm_off[r + 1] - a->mm_off[r];
         const uint64_t bound = mln ? mln : (mlen + 1) / 2;
         scr_off[r] = sc;
-        if (bound > PF_K0_TCAP) sc += 2 * bound;          // ranks/triggers + K0's placement buffer
+        if (bound > PF_K0_TCAP) sc += bound;              // ranks, then triggers in place
         if (a->l_qseq[r] >= (1u << 24)) return PF_ERR_LIMIT; // K0 packs ranks into 24 bits
     }
     seq_off[n] = so;
@@ -559,7 +559,7 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         uint64_t sc2 = 0;
         for (uint32_t r = 0; r < n; r++) {
             scr_off[r] = sc2;
-            if (nd[r] > PF_K0_TCAP) sc2 += 2ull * nd[r];
+            if (nd[r] > PF_K0_TCAP) sc2 += nd[r];
         }
         scr_off[n] = sc2;
         free_arena(b, (void *)ld.scr);

@@ -13,9 +13,8 @@
 #include <stdint.h>
 
 #define PF_K0_WAVES 4
-#define PF_K0_TCAP 768          /* triggers per wave kept in LDS; longer lists use HBM scratch */
-#define PF_K0_MMCAP 4096          /* MM text staged in LDS; longer tags are parsed from HBM */
-#define PF_K0_CB 256              /* read positions per implicit-mode chunk */
+#define PF_K0_TCAP 640            /* triggers per wave kept in LDS; longer lists use HBM scratch */
+#define PF_K0_CB 128              /* read positions per implicit-mode chunk (4 per lane, half the wave) */
 #define PF_K0_EC (PF_K0_CB / 2)   /* explicit / implicit calls per chunk (CpGs are >= 2 apart) */
 #define PF_K0_SEQ_ALIGN 16        /* per-record SEQ slices are 16-byte aligned and padded */
 

@@ -143,15 +143,17 @@ struct K0Merge {                      // implicit-mode chunk lists
     uint8_t eC[PF_K0_EC];
     uint8_t mC[2 * PF_K0_EC];         // cat | 0x80 for implicit calls
 };
-struct K0W {                          // LDS of one wave (~9.6 KB)
-    uint32_t T[PF_K0_TCAP];           // ranks, then triggers (p<<2 | cat)
+struct K0Seq {
     uint16_t sb[8 * 64];              // SEQ block: rank base of each (row, word pair)
     uint8_t sc[8 * 64];               //            target count of the pair's first word
+};
+struct K0W {                          // LDS of one wave (5 KB: 8 waves per SIMD)
+    uint32_t T[PF_K0_TCAP];           // ranks, then triggers (p<<2 | cat)
     uint32_t opE[64], opOff[64], opA[64];
     uint8_t opT[64];
     union {
-        uint32_t mmw[PF_K0_MMCAP / 4 + 4];   // phase 1: the MM text
-        K0Merge mg;                          // phase 3, implicit mode
+        K0Seq s;                      // phase 2
+        K0Merge mg;                   // phase 3: implicit-mode lists, emission spill
     } u;
 };
 
@@ -164,29 +166,65 @@ struct K0Out {
 };
 
 // ---------------------------------------------------------------------------
-// Phase 1: MM/ML -> ranks of the called C's (original orientation).
+// Phase 1: MM/ML -> ranks of the called C's (original orientation).  The MM
+// text is read as aligned words straight from HBM/L2 (the device copy is
+// padded, so the last word may run past the text): lane k of a 64-word row
+// holds text bytes 4k - mis .. 4k - mis + 3.  ';' and ',' are found four bytes
+// per lane by per-byte flags; each comma's skip count is converted from the 7
+// bytes after it (the lane's word and the next) by a SWAR decimal parse, and
+// a count that may run past that window takes a byte loop.
 struct K0Tgt { uint32_t nd, nc, mi, th, te; uint64_t ml; };
 
-template <typename CP>
-DEV bool k0_mm_entries(CP mm, uint32_t mlen, uint32_t mln, uint32_t lane, K0Tgt &t) {
+DEV uint32_t bytes_eq(uint32_t w, uint32_t c) {      // 0x80 in each byte of w equal to c
+    const uint32_t t = w ^ (c * 0x01010101u);
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+DEV uint32_t bytes_in(int32_t b, uint32_t lo, uint32_t hi) {   // bytes with text index in [lo, hi)
+    const int32_t s = min(max((int32_t)lo - b, 0), 4), e = min(max((int32_t)hi - b, 0), 4);
+    const uint32_t ml = s >= 4 ? 0u : 0x80808080u << (8 * s);
+    const uint32_t mh = e <= 0 ? 0u : 0x80808080u >> (8 * (4 - e));
+    return ml & mh;
+}
+DEV uint32_t wsum_small(uint32_t c) {                // wave sum of per-lane values 0..7
+    return popc(__ballot(c & 1u)) + 2u * popc(__ballot(c & 2u)) + 4u * popc(__ballot(c & 4u));
+}
+DEV uint64_t nondigit_bytes(uint64_t y) {            // 0x80 in each byte of y outside '0'..'9'
+    const uint64_t hi = (y & 0xF0F0F0F0F0F0F0F0ull) ^ 0x3030303030303030ull;
+    const uint64_t hz = ~(((hi & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | hi) & 0x8080808080808080ull;
+    const uint64_t ge10 = ((y & 0x0F0F0F0F0F0F0F0Full) + 0x7676767676767676ull) & 0x8080808080808080ull;
+    return (~hz & 0x8080808080808080ull) | ge10;
+}
+DEV uint32_t swar_dec(uint64_t y, uint32_t n) {      // bytes 0..n-1 of y (n in 1..7) as decimal digits
+    uint64_t z = (y & ((1ull << (8 * n)) - 1)) << (8 * (8 - n));   // leading zeros pad to 8 digits
+    z = ((z & 0x0F0F0F0F0F0F0F0Full) * 2561u) >> 8;
+    z = ((z & 0x00FF00FF00FF00FFull) * 6553601u) >> 16;
+    return (uint32_t)(((z & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32);
+}
+
+DEV bool k0_mm_entries(const uint32_t *gw, const uint8_t *mm, uint32_t mis, uint32_t mlen, uint32_t mln,
+                       uint32_t lane, K0Tgt &t) {
     uint32_t i = 0;
     uint64_t ml_cur = 0;
     bool found = false;
     t.nd = 0;
     while (i < mlen) {
         uint32_t e = mlen, commas = 0;
-        for (uint32_t c = i; c < mlen; c += 64) {
-            const uint32_t q = c + lane;
-            const uint32_t ch = q < mlen ? mm[q] : 0u;
-            const uint64_t semi = __ballot(q < mlen && ch == ';');
-            uint64_t com = __ballot(q < mlen && ch == ',');
-            if (semi) {
-                const uint32_t s = (uint32_t)__ffsll((long long)semi) - 1;
-                e = c + s;
-                commas += popc(com & lanemask_lt(s));
+        for (uint32_t k0 = (mis + i) >> 2; 4 * k0 < mis + mlen; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            const int32_t b = (int32_t)(4 * k) - (int32_t)mis;
+            const uint32_t w = 4 * k < mis + mlen ? gw[k] : 0u;
+            const uint32_t vm = bytes_in(b, i, mlen);
+            const uint32_t sm = bytes_eq(w, ';') & vm, cm = bytes_eq(w, ',') & vm;
+            const uint64_t bs = __ballot(sm != 0);
+            if (bs) {
+                const uint32_t l0 = (uint32_t)__ffsll((long long)bs) - 1;
+                const uint32_t sb = (uint32_t)__builtin_ctz(rdl(sm, l0)) >> 3;   // byte of the first ';'
+                e = 4 * (k0 + l0) - mis + sb;
+                const uint32_t cm2 = lane < l0 ? cm : lane == l0 ? cm & ((1u << (8 * sb)) - 1u) : 0u;
+                commas += wsum_small((uint32_t)__builtin_popcount(cm2));
                 break;
             }
-            commas += popc(com);
+            commas += wsum_small((uint32_t)__builtin_popcount(cm));
         }
         e = uni(e);
         commas = uni(commas);
@@ -220,49 +258,82 @@ DEV bool k0_mm_entries(CP mm, uint32_t mlen, uint32_t mln, uint32_t lane, K0Tgt 
     return true;
 }
 
-template <typename CP, typename TP>
-DEV bool k0_mm_ranks(CP mm, const K0Tgt &t, TP TB, uint32_t lane) {
+// Ranks in TB, reversed for reverse reads (TB[nd-1-j] holds skip j's rank) so
+// that TB is in forward read order for the SEQ pass.
+template <typename TP>
+DEV bool k0_mm_ranks(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const K0Tgt &t, bool rev, TP TB,
+                     uint32_t lane) {
     if (mm[t.th] != ',') return false;
+    const uint32_t wend = mis + t.te;
     uint64_t carry = 0;
     uint32_t idx = 0;
     bool bad = false;
-    for (uint32_t c = t.th; c < t.te; c += 64) {
-        const uint32_t q = c + lane;
-        const bool is_c = q < t.te && mm[q] == ',';
-        const uint64_t com = __ballot(is_c);
-        const uint32_t gi = idx + popc(com & lanemask_lt(lane));
-        uint64_t v = 0;
+    for (uint32_t k0 = (mis + t.th) >> 2; 4 * k0 < wend; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const int32_t b = (int32_t)(4 * k) - (int32_t)mis;
+        const uint32_t w = 4 * k < wend ? gw[k] : 0u;
+        const uint32_t wn = 4 * k + 4 < wend ? gw[k + 1] : 0u;
+        const uint32_t cm = bytes_eq(w, ',') & bytes_in(b, t.th, t.te);
+        const uint32_t nl = (uint32_t)__builtin_popcount(cm);
+        const uint32_t ie = wscan(nl, lane);
+        const uint32_t gi0 = idx + ie - nl;
+        const uint64_t x = ((uint64_t)wn << 32) | w;
+        uint32_t vq[4] = {0, 0, 0, 0};
+        uint64_t lsum = 0;
         bool ok = true;
-        if (is_c) {
-            uint32_t k = q + 1;
-            while (k < t.te && is_digit(mm[k])) { v = v * 10u + (uint64_t)(mm[k] - '0'); k++; }
-            ok = k > q + 1 && v <= 0xFFFFFFFFull;
-            if (gi + 1 < t.nd) ok = ok && k < t.te && mm[k] == ',';
+        uint32_t m = cm;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            if (!__ballot(q < nl)) break;
+            if (q < nl) {
+                const uint32_t pb = (uint32_t)__builtin_ctz(m) >> 3;
+                m &= m - 1;
+                const uint32_t xc = (uint32_t)(b + (int32_t)pb);          // the comma's text index
+                const uint32_t win = 7 - pb, lim = t.te - xc - 1;        // bytes seen / bytes before te
+                const uint64_t y = x >> (8 * (pb + 1));
+                const uint32_t n = (uint32_t)__builtin_ctzll(nondigit_bytes(y)) >> 3;   // <= win: y's top bytes are 0
+                const bool last = gi0 + q + 1 >= t.nd;
+                uint64_t v;
+                if (n < win || lim <= win) {
+                    const uint32_t nv = n < lim ? n : lim;
+                    v = nv ? swar_dec(y, nv) : 0u;
+                    ok = ok && nv > 0;
+                    if (!last) ok = ok && nv < lim && (uint32_t)((y >> (8 * nv)) & 0xFFu) == ',';
+                } else {                              // a count of 7+ digits: byte loop
+                    uint32_t kk = xc + 1;
+                    v = 0;
+                    while (kk < t.te && is_digit(mm[kk])) { v = v * 10u + (uint64_t)(mm[kk] - '0'); kk++; }
+                    ok = ok && v <= 0xFFFFFFFFull;
+                    if (!last) ok = ok && kk < t.te && mm[kk] == ',';
+                }
+                vq[q] = (uint32_t)v;
+                lsum += (uint32_t)v;
+            }
         }
-        const uint64_t x = is_c ? v : 0ull;
-        const uint64_t incl = (__ballot(x >= (1ull << 26)) ? wscan64(x, lane) : (uint64_t)wscan((uint32_t)x, lane)) +
+        const uint64_t incl = (__ballot(lsum >= (1ull << 24)) ? wscan64(lsum, lane) : (uint64_t)wscan((uint32_t)lsum, lane)) +
                               carry;
-        const uint64_t rank = incl + gi;
-        if (is_c) {
-            if (rank > 0xFFFFFFFFull) ok = false;
-            if (ok) TB[gi] = (uint32_t)rank;
+        uint64_t run = incl - lsum;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+            if (q < nl) {
+                run += vq[q];
+                const uint64_t rank = run + gi0 + q;
+                if (rank > 0xFFFFFFFFull) ok = false;
+                else TB[rev ? t.nd - 1 - (gi0 + q) : gi0 + q] = (uint32_t)rank;
+            }
         }
-        if (__ballot(is_c && !ok)) { bad = true; break; }
+        if (__ballot(!ok)) { bad = true; break; }
         carry = rdl64(incl, 63);
-        idx += popc(com);
+        idx += rdl(ie, 63);
     }
     return !bad;
 }
 
-// Phase 2: ranks -> triggers (p<<2 | cat) in ascending p, into TB.
-// On entry TB[j] = rank | ML value << 24.  Each lane owns a contiguous segment
-// of the read's 16-base words: pass 1 counts the target bases per segment (one
-// scan gives every segment its rank base), each lane then finds the triggers
-// its segment holds (two lower bounds over TB) and pass 2 walks its own words
-// to place them, test the CpG context and write them to OUT in position order;
-// a ballot compaction moves the CpG ones back to TB.  Returns the trigger
-// count (0 when a skip count runs past the read); `implicit` set when a 5mC
-// call sits outside CpG context (852-858).
+// Phase 2: ranks -> triggers (p<<2 | cat) in ascending p, in place in TB.
+// On entry TB holds rank | ML value << 24 in forward read order (reversed for
+// reverse reads, whose ranks count from the end).  Returns the trigger count
+// (0 when a skip count runs past the read); `implicit` set when a 5mC call
+// sits outside CpG context (852-858).
 DEV uint64_t nibswap(uint64_t w) {                   // base i -> bits 4i..4i+3
     return ((w & 0x0F0F0F0F0F0F0F0Full) << 4) | ((w >> 4) & 0x0F0F0F0F0F0F0F0Full);
 }
@@ -273,9 +344,9 @@ DEV uint64_t zero_nibbles(uint64_t x) {             // bit 4i set iff nibble i o
 }
 DEV uint64_t valid_nibbles(uint32_t nv) { return nv >= 16 ? 0x1111111111111111ull : ((1ull << (4 * nv)) - 1) & 0x1111111111111111ull; }
 
-template <typename TP, typename OP>
+template <typename TP>
 DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint32_t len, bool rev, const K0Tgt &t,
-                         TP TB, OP OUT, uint32_t lane, bool &implicit) {
+                         TP TB, uint32_t lane, bool &implicit) {
     // Blocks of 1024 16-base words (16384 bases), read by 8 coalesced
     // wave-instructions of 1 KiB (lane L holds words 2L, 2L+1 of each 128-word
     // row i).  Target counts per word pair, one scan per row, and each pair's
@@ -283,7 +354,8 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
     // block's triggers are then placed one per lane: row by the 8 row prefixes,
     // pair by an LDS search, word by the first-word count, base by a select in
     // the re-read word.  Reverse reads walk the blocks from the end (their
-    // ranks count from the end) and turn the rank into a forward one.
+    // ranks count from the end) and turn the rank into a forward one; each
+    // trigger replaces its rank in TB.
     constexpr uint32_t ROWS = 8, RW = 128, BW = ROWS * RW;
     const uint64_t pat = (rev ? (uint64_t)NT_G : (uint64_t)NT_C) * 0x1111111111111111ull;
     const uint4 *sq4 = reinterpret_cast<const uint4 *>(seq);
@@ -291,6 +363,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
     const uint32_t nwords = (len + 15) / 16;
     const uint32_t nblk = (nwords + BW - 1) / BW;
     const uint32_t nd = t.nd;
+    auto slot = [&](uint32_t j) { return rev ? nd - 1 - j : j; };   // rank order -> TB index
     uint32_t carry = 0, ti = 0;
     bool imp = false;
     for (uint32_t bb = 0; bb < nblk && ti < nd; bb++) {
@@ -320,8 +393,8 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             const uint32_t cp = c[0] + c[1];
             const uint32_t inc = wscan(cp, lane);
             pref[i] = run;
-            L.sb[i * 64 + lane] = (uint16_t)(run + inc - cp);
-            L.sc[i * 64 + lane] = (uint8_t)c[0];
+            L.u.s.sb[i * 64 + lane] = (uint16_t)(run + inc - cp);
+            L.u.s.sc[i * 64 + lane] = (uint8_t)c[0];
             run += uni(__shfl(inc, 63, 64));
         }
         const uint32_t btot = run;
@@ -331,7 +404,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             uint32_t n = nd - ti;
             while (n > 0) {
                 const uint32_t h = n >> 1;
-                if ((TB[tend + h] & 0xFFFFFFu) < carry + btot) { tend += h + 1; n -= h + 1; } else n = h;
+                if ((TB[slot(tend + h)] & 0xFFFFFFu) < carry + btot) { tend += h + 1; n -= h + 1; } else n = h;
             }
             tend = uni(tend);
         }
@@ -339,18 +412,18 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
         for (uint32_t j0 = ti; j0 < tend; j0 += 64) {
             const uint32_t j = j0 + lane;
             if (j < tend) {
-                const uint32_t e = TB[j];
+                const uint32_t e = TB[slot(j)];
                 const uint32_t rr = (e & 0xFFFFFFu) - carry;
                 const uint32_t f = rev ? btot - 1 - rr : rr;    // forward rank inside the block
                 uint32_t i = 0;
 #pragma unroll
                 for (uint32_t q = 1; q < ROWS; q++) i += pref[q] <= f ? 1u : 0u;
-                const uint16_t *sbi = L.sb + i * 64;
+                const uint16_t *sbi = L.u.s.sb + i * 64;
                 uint32_t lo = 0, n = 64;                        // last pair with base <= f
                 while (n > 0) { const uint32_t h = n >> 1; if (sbi[lo + h] <= f) { lo += h + 1; n -= h + 1; } else n = h; }
                 const uint32_t Lw = lo - 1;
                 uint32_t k = f - sbi[Lw];
-                const uint32_t c0 = L.sc[i * 64 + Lw];
+                const uint32_t c0 = L.u.s.sc[i * 64 + Lw];
                 uint32_t hw = 0;
                 if (k >= c0) { k -= c0; hw = 1; }
                 const uint32_t w = b * BW + i * RW + 2 * Lw + hw;
@@ -369,7 +442,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                         key = (p << 2) | (q < d.lo ? 1u : q >= d.hi ? 0u : 2u);
                     } else imp = true;
                 }
-                OUT[rev ? nd - 1 - j : j] = key;
+                TB[slot(j)] = key;
             }
         }
         wsync();
@@ -379,11 +452,11 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
     implicit = __ballot(imp) != 0;
     if (ti < nd) return 0;                            // skip counts beyond the read
     wsync();
-    // compaction OUT -> TB (order kept)
+    // compaction in place (order kept)
     uint32_t nout = 0;
     for (uint32_t c0 = 0; c0 < nd; c0 += 64) {
         const uint32_t jj = c0 + lane;
-        const uint32_t key = jj < nd ? OUT[jj] : 0xFFFFFFFFu;
+        const uint32_t key = jj < nd ? TB[jj] : 0xFFFFFFFFu;
         const uint64_t pb = __ballot(key != 0xFFFFFFFFu);
         if (key != 0xFFFFFFFFu) TB[nout + popc(pb & lanemask_lt(lane))] = key;
         nout += popc(pb);
@@ -719,21 +792,8 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
     return true;
 }
 
-// Stage the MM text in LDS with word loads (the device copy is padded, so the
-// last word may run past the text).  Returns the LDS view of the text.
-DEV const uint8_t *k0_stage_mm(const uint8_t *g, uint32_t n, uint32_t *dst, uint32_t lane) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(g);
-    const uint32_t mis = (uint32_t)(a & 3u);
-    const uint32_t *gw = reinterpret_cast<const uint32_t *>(a - mis);
-    const uint32_t nw = (n + mis + 3) / 4;
-#pragma unroll 4
-    for (uint32_t k = lane; k < nw; k += 64) dst[k] = gw[k];
-    wsync();
-    return reinterpret_cast<const uint8_t *>(dst) + mis;
-}
-
 template <int MODE, typename TP>
-DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, TP OUT, uint32_t cap) {
+DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, uint32_t cap) {
     const uint32_t len = d.l_qseq[r];
     const bool rev = (d.flag[r] & 16u) != 0;
     const uint8_t *mmg = d.mm + d.mm_off[r];
@@ -749,15 +809,12 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     uint32_t nT = 0;
     bool implicit = false;
     K0_T0;
-    if (mlen <= PF_K0_MMCAP) {
-        const uint8_t *mm = k0_stage_mm(mmg, mlen, L.u.mmw, lane);
-        okmm = k0_mm_entries(mm, mlen, mln, lane, t);
+    {
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
+        const uint32_t *gw = reinterpret_cast<const uint32_t *>(mmg - mis);
+        okmm = k0_mm_entries(gw, mmg, mis, mlen, mln, lane, t);
         if (okmm && t.nd > cap) okmm = false;       // only a malformed tag lists more calls than its size allows
-        if (okmm && t.nd) okmm = k0_mm_ranks(mm, t, TB, lane);
-    } else {
-        okmm = k0_mm_entries(mmg, mlen, mln, lane, t);
-        if (okmm && t.nd > cap) okmm = false;
-        if (okmm && t.nd) okmm = k0_mm_ranks(mmg, t, TB, lane);
+        if (okmm && t.nd) okmm = k0_mm_ranks(gw, mmg, mis, t, rev, TB, lane);
     }
     if (MODE == 0 && lane == 0) d.rec_nd[r] = okmm ? t.nd : 0u;
     wsync();
@@ -766,15 +823,16 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
 #pragma unroll 4
         for (uint32_t j = lane; j < t.nd; j += 64) {
             const uint32_t q = mln ? ml[t.ml + (uint64_t)j * t.nc + t.mi] : 255u;
-            const uint32_t rk = TB[j];
+            const uint32_t sj = rev ? t.nd - 1 - j : j;
+            const uint32_t rk = TB[sj];
             past |= rk >= (1u << 24);                 // l_qseq < 2^24: such a rank is past the read's C's
-            TB[j] = (rk & 0xFFFFFFu) | (q << 24);
+            TB[sj] = (rk & 0xFFFFFFu) | (q << 24);
         }
         past = __ballot(past) != 0;
         wsync();
     }
     K0_STAMP(0);
-    if (okmm && t.nd && !past) nT = k0_seq_pass(d, L, seq, len, rev, t, TB, OUT, lane, implicit);
+    if (okmm && t.nd && !past) nT = k0_seq_pass(d, L, seq, len, rev, t, TB, lane, implicit);
     K0_STAMP(1);
     if (!okmm && d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_BADMM], 1ull);
     nT = uni(nT);
@@ -850,7 +908,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
 }
 
 template <int MODE>
-__global__ __launch_bounds__(PF_K0_WAVES * 64) void pf_k0_load(pf_load_dev d) {
+__global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_load(pf_load_dev d) {
     __shared__ K0W lds[PF_K0_WAVES];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
@@ -867,8 +925,8 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) void pf_k0_load(pf_load_dev d) {
         return;
     }
     const uint64_t s0 = d.scr_off[r], s1 = d.scr_off[r + 1];
-    if (s1 == s0) k0_record<MODE>(d, L, r, lane, L.T, L.u.mmw, (uint32_t)PF_K0_TCAP);
-    else k0_record<MODE>(d, L, r, lane, d.scr + s0, d.scr + s0 + (s1 - s0) / 2, (uint32_t)((s1 - s0) / 2));
+    if (s1 == s0) k0_record<MODE>(d, L, r, lane, L.T, (uint32_t)PF_K0_TCAP);
+    else k0_record<MODE>(d, L, r, lane, d.scr + s0, (uint32_t)(s1 - s0));
 }
 
 template __global__ void pf_k0_load<0>(pf_load_dev d);
