@@ -527,6 +527,12 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         for (uint32_t r = 0; r < n; r++)
             memcpy(sq.data() + seq_off[r], a->seq + a->seq_off[r], ((uint64_t)a->l_qseq[r] + 1) / 2);
         PUT(p8, sq.data(), sq.size()); ld.seq = p8;
+        // wave slots in decreasing read length: the long records start first
+        // and the four waves of a workgroup finish together
+        std::vector<uint32_t> ord(n);
+        for (uint32_t r = 0; r < n; r++) ord[r] = r;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return a->l_qseq[x] > a->l_qseq[y]; });
+        PUT(p32, ord.data(), n); ld.order = p32;
         ALLOC(p32, n); ld.rec_n = p32;
         ALLOC(p32, n); ld.rec_nd = p32;
         ALLOC(p32, n); ld.rec_read = p32;

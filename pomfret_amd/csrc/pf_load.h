@@ -35,6 +35,7 @@ struct pf_load_dev {
     uint32_t min_mapq, min_len;
     uint32_t lo, hi;                 /* uint8_t in the reference (799) */
     uint32_t force_seq;              /* test override: every record through the sequential path */
+    const uint32_t *order;           /* [n_recs] record of each wave slot: longest reads first */
     const uint16_t *flag;
     const uint8_t *mapq;
     const uint32_t *pos, *l_qseq;

@@ -912,8 +912,9 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_e
     __shared__ K0W lds[PF_K0_WAVES];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint32_t r = blockIdx.x * PF_K0_WAVES + wv;
-    if (r >= d.n_recs) return;
+    const uint32_t slot = blockIdx.x * PF_K0_WAVES + wv;
+    if (slot >= d.n_recs) return;
+    const uint32_t r = uni(d.order[slot]);
     K0W &L = lds[wv];
     if (MODE == 1 && d.rec_read[r] == PF_NONE) return;
     // filters (1079-1085)
