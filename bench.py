@@ -86,18 +86,32 @@ def k0_bytes(aln, read_recs, n_calls):
     return int(4 * aln.n_recs + 55 * R + 4 * cig.sum() + seq.sum() + mm.sum() + 6 * n_calls + 16 * R)
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, boundary: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py), or None."""
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py) when it was
+    collected on this workload and boundary, or None."""
     p = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") != WORKLOAD:
+        if d.get("workload") != dict(WORKLOAD, boundary=boundary):
             return None
         return d["kernels"].get(kernel, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+def record_spans(aln, recs):
+    """(pos, bam_endpos) of the records `recs`: pos + the reference-consuming
+    CIGAR lengths (M, D, N, =, X)."""
+    cig = np.asarray(aln.cigar, np.uint32)
+    ref = np.where(np.isin(cig & 15, (0, 2, 3, 7, 8)), cig >> 4, 0).astype(np.uint64)
+    cs = np.concatenate([[0], np.cumsum(ref)])
+    off = np.asarray(aln.cigar_off, np.int64)
+    recs = np.asarray(recs, np.int64)
+    start = np.asarray(aln.pos, np.uint32)[recs]
+    rlen = cs[off[recs + 1]] - cs[off[recs]]
+    return start, (start + rlen).astype(np.uint32)
 
 
 def cpu_baseline(cfg, batch, threads: int, min_cpu_s: float = 20.0, max_reps: int = 200):
@@ -181,65 +195,73 @@ def main():
         log(f"[bench] upload (validation, SEQ repack, H2D, K0 count pass): {time.perf_counter() - t:.1f}s")
         off, cpos, ccat, _, _ = db.debug_calls()
         rr = db.read_recs()
-        # the loaded reads as a window batch (sizes for the byte model; the rows are K0's)
+        # the loaded reads as a window batch (the byte model and the calls-level
+        # leg): K0's calls, and the spans of the kept records (pos, bam_endpos)
         wro = np.searchsorted(rr, aln.win_rec_off.astype(np.int64)).astype(np.uint32)
+        rs, re_ = record_spans(aln, rr)
         batch = WindowBatch(win_start=aln.win_start, win_end=aln.win_end, win_read_off=wro,
-                            read_start=np.zeros(len(rr), np.uint32), read_end=np.zeros(len(rr), np.uint32),
-                            read_hp=aln.hp[rr], read_call_off=off, call_pos=cpos, call_cat=ccat)
+                            read_start=rs, read_end=re_,
+                            read_hp=aln.hp[rr], read_call_off=off, call_pos=cpos, call_cat=ccat,
+                            win_cov_sel=aln.win_cov_sel, win_cov_rt=aln.win_cov_rt, win_n_cand=aln.win_n_cand)
     else:
         batch = make_batch(SynthSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
                                      seed=1000 + rank))
         log(f"[bench] rank {rank}: generated {batch.n_windows} windows, {batch.n_reads} reads, "
             f"{batch.n_calls} calls in {time.perf_counter() - t:.1f}s")
         db = ctx.upload(cfg, batch)
-    out = db.run()
-    outs = [out, db.run()]
-    for _ in range(args.warmup):
-        db.run(out)
-
-    if dist is not None:
-        import torch
-        dec_t = torch.empty(batch.n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
-        gathered = torch.empty(world * batch.n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
-
-    # Steps are pipelined two deep (pf_methphase_launch / _finish): the host
-    # epilogue of step k (Fisher tests, decisions, read tags) overlaps the
-    # kernels of step k+1; every step still runs every kernel, D2H copy and
-    # epilogue inside the timed region.
-    def finish(k):
-        o = outs[k % 2]
-        db.finish(o)
+    def timed(db, n_windows, n_reads):
+        """W warmup runs, then exactly K timed steps between barrier + sync
+        pairs; returns (max-over-ranks seconds, total reads, per-kernel ms
+        summed over the steps, one step's result)."""
+        out = db.run()
+        outs = [out, db.run()]
+        for _ in range(args.warmup):
+            db.run(out)
         if dist is not None:
-            dec_t.copy_(torch.from_numpy(o.decision))
-            dist.all_gather_into_tensor(gathered, dec_t)
+            import torch
+            dec_t = torch.empty(n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
+            gathered = torch.empty(world * n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
 
-    if dist is not None:
-        dist.barrier()
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    kern_acc = {}
-    if args.steps:
-        db.launch()
-    for k in range(args.steps):
-        if k + 1 < args.steps:
+        # Steps are pipelined two deep (pf_methphase_launch / _finish): the host
+        # epilogue of step k (Fisher tests, decisions, read tags) overlaps the
+        # kernels of step k+1; every step still runs every kernel, D2H copy and
+        # epilogue inside the timed region.
+        def finish(k):
+            o = outs[k % 2]
+            db.finish(o)
+            if dist is not None:
+                dec_t.copy_(torch.from_numpy(o.decision))
+                dist.all_gather_into_tensor(gathered, dec_t)
+
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        kern_acc = {}
+        if args.steps:
             db.launch()
-        finish(k)
-        for kn, v in ctx.kernel_times().items():
-            kern_acc[kn] = kern_acc.get(kn, 0.0) + v
-    if dist is not None:
-        torch.cuda.synchronize()
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        rt = torch.tensor([batch.n_reads], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(rt)
-        total_reads = float(rt.item()) * args.steps
-    else:
-        total_reads = float(batch.n_reads) * args.steps
+        for k in range(args.steps):
+            if k + 1 < args.steps:
+                db.launch()
+            finish(k)
+            for kn, v in ctx.kernel_times().items():
+                kern_acc[kn] = kern_acc.get(kn, 0.0) + v
+        if dist is not None:
+            torch.cuda.synchronize()
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+            rt = torch.tensor([n_reads], dtype=torch.float64, device=f"cuda:{local_rank}")
+            dist.all_reduce(rt)
+            total = float(rt.item()) * args.steps
+        else:
+            total = float(n_reads) * args.steps
+        return elapsed, total, kern_acc, out
 
+    elapsed, total_reads, kern_acc, out = timed(db, batch.n_windows, batch.n_reads)
     value = total_reads / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     stats = db.stats()
@@ -256,7 +278,19 @@ def main():
                       "GBps": round(b / (ms * 1e-3) / 1e9, 2) if ms > 0 else None}
     dom = max(kmean, key=kmean.get)
     achieved = kernels[dom]["GBps"]
-    traffic = pmc_traffic(dom)
+    traffic = pmc_traffic(dom, "records" if record_level else "calls")
+
+    calls_leg = None
+    if record_level:
+        # the same reads with K0's calls already resident (the calls-level
+        # boundary, pf_batch_upload): K12 + K3 + epilogue only
+        dbc = ctx.upload(cfg, batch)
+        el_c, tot_c, acc_c, out_c = timed(dbc, batch.n_windows, batch.n_reads)
+        dbc.free()
+        calls_leg = {"value": round(tot_c / el_c, 1), "ms_per_step": round(el_c / args.steps * 1e3, 4),
+                     "kernels_ms": {k: round(v / args.steps, 4) for k, v in acc_c.items() if k != "pf_k0_load"},
+                     "decisions_match": bool(np.array_equal(out_c.decision, out.decision)),
+                     "what": "same reads, calls resident in HBM (no K0): the pre-K0 boundary"}
 
     # PCIe-inclusive rate (never `value`): the one-shot boundary call hands
     # over host buffers -- upload (validation, pinned staging, H2D), run, D2H
@@ -318,6 +352,7 @@ def main():
         "kernels": kernels,
         "cpu_baseline": cpu,
         "pcie_inclusive": pcie,
+        "calls_level": calls_leg,
         "decisions": {"cis": int((out.decision == 0).sum()), "trans": int((out.decision == 1).sum()),
                       "none": int((out.decision < 0).sum())},
     }
