@@ -362,6 +362,54 @@ typedef struct pf_rescue {
 int  pf_write_vcf(const char *vcf_in, const pf_gaps_t *g, const pf_blocks_t *b, const pf_rescue_t *rescue,
                   const char *vcf_out, int64_t *counts);
 
+/* ------------------------------------------------------------------ */
+/* BAM ingest on the host: BGZF + BAM + BAI reader and  */
+/* the region fetch of load_reads_given_interval, feeding pf_aln_batch_t. */
+
+typedef struct pf_bam pf_bam_t;
+
+/* Open a BAM and its BAI (bai_path NULL: bam_path + ".bai", then the path
+ * with ".bam" replaced by ".bai").  bam_path NULL opens the index alone
+ * (pf_bam_index_stats only).  Replaces hts_open + sam_index_load +
+ * sam_hdr_read of init_and_open_bamfile_t (blockjoin.c:565-585).  Returns
+ * PF_OK, PF_ERR_ARG (not a BAM / BAI, truncated), PF_ERR_NOMEM, or -1 when a
+ * file cannot be opened. */
+int  pf_bam_open(const char *bam_path, const char *bai_path, pf_bam_t **out);
+void pf_bam_close(pf_bam_t *bam);
+int32_t pf_bam_n_targets(const pf_bam_t *bam);
+const char *pf_bam_target_name(const pf_bam_t *bam, int32_t tid);
+uint32_t pf_bam_target_len(const pf_bam_t *bam, int32_t tid);
+int32_t pf_bam_tid(const pf_bam_t *bam, const char *name);   /* -1 when absent */
+/* The index's per-reference metadata pseudo-bin: mapped / unmapped counts
+ * (hts_idx_get_stat); PF_ERR_ARG when tid has none. */
+int  pf_bam_index_stats(const pf_bam_t *bam, int32_t tid, uint64_t *n_mapped, uint64_t *n_unmapped);
+
+/* The records of a set of windows of one contig, in window order and BAM
+ * order inside a window, as pf_aln_batch_t (owned by this struct) plus the
+ * qnames (for the first-wins tag table, blockjoin.c:4408-4423). */
+typedef struct pf_bam_records {
+    pf_aln_batch_t aln;
+    const uint64_t *qname_off;     /* [n_recs+1] into qname, no terminators */
+    const char *qname;
+    const int32_t *hp_tag;         /* [n_recs] raw HP value, INT32_MIN when absent */
+    uint64_t n_truncated;          /* windows whose fetch stopped at a record
+                                      htslib refuses (CIGAR/SEQ length mismatch) */
+} pf_bam_records_t;
+
+/* For window w the records sam_itr_querys(chrom:b-(e+readback)) yields,
+ * b = s-readback clipped at 0, as load_reads_given_interval builds the
+ * region (1053-1054); HP as get_hp_from_aln (910-923: absent or 0 -> 254,
+ * else HP-1); de as bam_aux2f or -1; MM from MM:Z / Mm:Z, ML from ML:B:C /
+ * Ml:B:C (a tag of another type makes the record's MM empty: htslib's
+ * bam_parse_basemod fails and the read carries no calls); the CIGAR from a
+ * CG:B:I tag when the record holds the kSmN placeholder.  win_start/win_end
+ * are copied into aln.  n_threads > 1 fetches windows in parallel (one file
+ * handle per thread).  Returns PF_OK, PF_ERR_ARG (unknown contig, corrupt
+ * file), PF_ERR_NOMEM, or -1 on an I/O error. */
+int  pf_bam_fetch_windows(pf_bam_t *bam, const char *chrom, uint32_t n_windows, const uint32_t *win_start,
+                          const uint32_t *win_end, uint32_t readback, int n_threads, pf_bam_records_t **out);
+void pf_bam_records_free(pf_bam_records_t *recs);
+
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
  * the observed table. */
 double pf_fisher_exact(int n11, int n12, int n21, int n22,

@@ -1,0 +1,148 @@
+"""Host BAM ingest: pf_bam_* of libpomfret_amd.so.
+
+`BamFile(path).fetch_windows(chrom, starts, ends)` returns the records the
+reference's load_reads_given_interval fetches for each window
+(blockjoin.c:1053-1076: region ``chrom:max(s-readback,0)-(e+readback)``,
+htslib region/overlap semantics) as an `AlnBatch` ready for
+`Context.upload_aln`, plus each record's qname (for the first-wins tag
+table of blockjoin.c:4408-4423).  Host code; no GPU involved.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ._lib import PomfretError, _check, lib
+from .abi import AlnBatch, PfAlnBatch
+
+READBACK = 50_000  # blockjoin.c READBACK, the region margin of 1053-1054
+
+
+class PfBamRecords(C.Structure):
+    _fields_ = [("aln", PfAlnBatch), ("qname_off", C.c_void_p), ("qname", C.c_void_p),
+                ("hp_tag", C.c_void_p), ("n_truncated", C.c_uint64)]
+
+
+_bound = False
+
+
+def _bind():
+    global _bound
+    if _bound:
+        return lib()
+    L = lib()
+    L.pf_bam_open.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]
+    L.pf_bam_close.argtypes = [C.c_void_p]
+    L.pf_bam_n_targets.argtypes = [C.c_void_p]
+    L.pf_bam_n_targets.restype = C.c_int32
+    L.pf_bam_target_name.argtypes = [C.c_void_p, C.c_int32]
+    L.pf_bam_target_name.restype = C.c_char_p
+    L.pf_bam_target_len.argtypes = [C.c_void_p, C.c_int32]
+    L.pf_bam_target_len.restype = C.c_uint32
+    L.pf_bam_tid.argtypes = [C.c_void_p, C.c_char_p]
+    L.pf_bam_tid.restype = C.c_int32
+    L.pf_bam_index_stats.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+    L.pf_bam_fetch_windows.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                       C.c_uint32, C.c_int, C.POINTER(C.POINTER(PfBamRecords))]
+    L.pf_bam_records_free.argtypes = [C.POINTER(PfBamRecords)]
+    _bound = True
+    return L
+
+
+def _arr(ptr, n, dt) -> np.ndarray:
+    n = int(n)
+    if n == 0 or not ptr:
+        return np.zeros(0, dt)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), (n,)).copy()
+
+
+class BamFile:
+    """An opened BAM + BAI (pf_bam_open).  bam=None opens the index alone."""
+
+    def __init__(self, bam: Optional[str], bai: Optional[str] = None):
+        L = _bind()
+        h = C.c_void_p()
+        rc = L.pf_bam_open(bam.encode() if bam else None, bai.encode() if bai else None, C.byref(h))
+        if rc == -1:
+            raise FileNotFoundError(bam or bai)
+        _check(rc, "pf_bam_open")
+        self.handle = h
+        self.path = bam
+
+    def close(self):
+        if self.handle:
+            lib().pf_bam_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n_targets(self) -> int:
+        return int(lib().pf_bam_n_targets(self.handle))
+
+    @property
+    def targets(self) -> List[str]:
+        return [lib().pf_bam_target_name(self.handle, i).decode() for i in range(self.n_targets)]
+
+    @property
+    def lengths(self) -> List[int]:
+        return [int(lib().pf_bam_target_len(self.handle, i)) for i in range(self.n_targets)]
+
+    def tid(self, name: str) -> int:
+        return int(lib().pf_bam_tid(self.handle, name.encode()))
+
+    def index_stats(self, tid: int) -> Tuple[int, int]:
+        """(mapped, unmapped) of the BAI's metadata pseudo-bin."""
+        m, u = C.c_uint64(), C.c_uint64()
+        _check(lib().pf_bam_index_stats(self.handle, int(tid), C.byref(m), C.byref(u)), "pf_bam_index_stats")
+        return int(m.value), int(u.value)
+
+    def fetch_windows(self, chrom: str, starts: Sequence[int], ends: Sequence[int],
+                      readback: int = READBACK, threads: int = 1) -> Tuple[AlnBatch, List[str], dict]:
+        """The records of every window [s, e] (gap coordinates as the
+        methphase worker receives them) -> (AlnBatch, qnames, info)."""
+        if self.path is None:
+            raise PomfretError("index-only BamFile cannot fetch")
+        L = _bind()
+        ws = np.ascontiguousarray(starts, np.uint32)
+        we = np.ascontiguousarray(ends, np.uint32)
+        if ws.shape != we.shape:
+            raise ValueError("starts and ends differ in length")
+        out = C.POINTER(PfBamRecords)()
+        _check(L.pf_bam_fetch_windows(self.handle, chrom.encode(), ws.size, ws.ctypes.data, we.ctypes.data,
+                                      int(readback), int(threads), C.byref(out)), "pf_bam_fetch_windows")
+        try:
+            r = out.contents
+            a = r.aln
+            n, W = int(a.n_recs), int(a.n_windows)
+            co = _arr(a.cigar_off, n + 1, np.uint64)
+            so = _arr(a.seq_off, n + 1, np.uint64)
+            mo = _arr(a.mm_off, n + 1, np.uint64)
+            lo = _arr(a.ml_off, n + 1, np.uint64)
+            qo = _arr(r.qname_off, n + 1, np.uint64)
+            batch = AlnBatch(
+                win_start=ws.copy(), win_end=we.copy(), win_rec_off=_arr(a.win_rec_off, W + 1, np.uint32),
+                flag=_arr(a.flag, n, np.uint16), mapq=_arr(a.mapq, n, np.uint8), pos=_arr(a.pos, n, np.uint32),
+                l_qseq=_arr(a.l_qseq, n, np.uint32), de=_arr(a.de, n, np.float32), hp=_arr(a.hp, n, np.uint8),
+                cigar_off=co, cigar=_arr(a.cigar, co[-1], np.uint32),
+                seq_off=so, seq=_arr(a.seq, so[-1], np.uint8),
+                mm_off=mo, mm=_arr(a.mm, mo[-1], np.uint8),
+                ml_off=lo, ml=_arr(a.ml, lo[-1], np.uint8))
+            qb = _arr(r.qname, qo[-1], np.uint8).tobytes()
+            qnames = [qb[qo[i]:qo[i + 1]].decode("ascii", "replace") for i in range(n)]
+            info = {"hp_tag": _arr(r.hp_tag, n, np.int32), "n_truncated": int(r.n_truncated)}
+        finally:
+            L.pf_bam_records_free(out)
+        return batch, qnames, info

@@ -1,0 +1,858 @@
+/*
+ * pf_bam.c -- BAM ingest on the host: a BGZF block reader,
+ * the BAM header and record decoder, the BAI index and the region fetch that
+ * load_reads_given_interval does per window (reference blockjoin.c:1053-1076,
+ * with htslib's hts_open / sam_index_load / sam_itr_querys / sam_itr_next
+ * semantics), producing the pf_aln_batch_t that pf_batch_upload_aln takes.
+ *
+ * Formats follow the SAM/BAM specification (SAMv1 sections 4.1-4.2 and 5.2):
+ *   - BGZF: gzip members with a BC extra subfield (BSIZE); virtual offsets
+ *     (block address << 16 | offset in the block).  As in htslib, a read
+ *     that ends exactly at a block's end leaves the offset at the next
+ *     block's start, so chunk ends compare the same way.
+ *   - BAI: per reference the bins (with the metadata pseudo-bin 37450) and
+ *     the 16 kb linear index.
+ * Region fetch (htslib hts_itr_query + hts_itr_next): the region string
+ * "chrom:b-E" means the 0-based [max(b-1, 0), E); the chunks of the bins
+ * reg2bins gives for it, minus those ending before the linear index's
+ * offset, are read in file order; a record stops the fetch when its tid
+ * differs or its pos >= E and is returned when pos < E and bam_endpos > beg
+ * (bam_endpos: pos + reference length, 1 for unmapped or zero length).
+ * bam_read1 refuses a record whose CIGAR query length differs from l_qseq
+ * (mapped, l_qseq > 0): sam_itr_next then returns < 0 and the reference's
+ * loop ends, so the window's fetch stops there too (counted in
+ * n_truncated).  The CG:B:I long-CIGAR tag replaces a kSmN placeholder as
+ * bam_tag2cigar does.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#include "../../include/pomfret_amd.h"
+
+/* ------------------------------------------------------------------ */
+/* BGZF */
+typedef struct {
+    FILE *f;
+    uint8_t cbuf[65536 + 64];
+    uint8_t ubuf[65536];
+    int ulen, upos;
+    uint64_t caddr;          /* compressed address of the block in ubuf */
+    uint64_t next;           /* compressed address of the following block */
+    int eof;
+} bgzf_t;
+
+static uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+static uint32_t rd32(const uint8_t *p) { return rd16(p) | (rd16(p + 2) << 16); }
+static uint64_t rd64(const uint8_t *p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+
+/* load the block at compressed address addr; 0 ok, 1 clean EOF, <0 error */
+static int bgzf_load(bgzf_t *z, uint64_t addr) {
+    if (fseeko(z->f, (off_t)addr, SEEK_SET) != 0) return -1;
+    uint8_t *h = z->cbuf;
+    size_t got = fread(h, 1, 18, z->f);
+    if (got == 0) { z->caddr = addr; z->next = addr; z->ulen = z->upos = 0; z->eof = 1; return 1; }
+    if (got < 12 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return -2;
+    const uint32_t xlen = rd16(h + 10);
+    if (xlen < 6 || 12 + xlen > sizeof z->cbuf) return -2;
+    if (got < 12 + (size_t)xlen) {
+        if (fread(h + got, 1, 12 + xlen - got, z->f) != 12 + xlen - got) return -2;
+        got = 12 + xlen;
+    }
+    uint32_t bsize = 0;
+    for (uint32_t x = 0; x + 4 <= xlen;) {
+        const uint8_t *sf = h + 12 + x;
+        const uint32_t slen = rd16(sf + 2);
+        if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = rd16(sf + 4) + 1;
+        x += 4 + slen;
+    }
+    if (bsize < 12 + xlen + 8 || bsize > 65536) return -2;
+    if (got < bsize && fread(h + got, 1, bsize - got, z->f) != bsize - got) return -2;
+    const uint32_t isize = rd32(h + bsize - 4), crc = rd32(h + bsize - 8);
+    if (isize > 65536) return -2;
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return -3;
+    zs.next_in = h + 12 + xlen;
+    zs.avail_in = bsize - 12 - xlen - 8;
+    zs.next_out = z->ubuf;
+    zs.avail_out = sizeof z->ubuf;
+    const int rc = inflate(&zs, Z_FINISH);
+    const uint32_t out = (uint32_t)zs.total_out;
+    inflateEnd(&zs);
+    if (rc != Z_STREAM_END || out != isize) return -2;
+    if ((uint32_t)crc32(0L, z->ubuf, out) != crc) return -2;
+    z->caddr = addr;
+    z->next = addr + bsize;
+    z->ulen = (int)out;
+    z->upos = 0;
+    z->eof = 0;
+    return 0;
+}
+
+static int bgzf_seek(bgzf_t *z, uint64_t voff) {
+    const uint64_t addr = voff >> 16;
+    const int off = (int)(voff & 0xFFFF);
+    if (!(z->ulen > 0 && z->caddr == addr)) {
+        const int rc = bgzf_load(z, addr);
+        if (rc < 0) return rc;
+    }
+    if (off > z->ulen) return -2;
+    z->upos = off;
+    return 0;
+}
+
+static uint64_t bgzf_tell(const bgzf_t *z) { return (z->caddr << 16) | (uint64_t)z->upos; }
+
+/* n bytes; returns n, 0 at a clean EOF before any byte, <0 otherwise */
+static int64_t bgzf_read(bgzf_t *z, void *dst, size_t n) {
+    uint8_t *d = (uint8_t *)dst;
+    size_t done = 0;
+    while (done < n) {
+        if (z->upos >= z->ulen) {
+            int rc;
+            do { rc = bgzf_load(z, z->next); } while (rc == 0 && z->ulen == 0);   /* skip empty blocks */
+            if (rc == 1) return done == 0 ? 0 : -2;
+            if (rc < 0) return rc;
+        }
+        size_t k = (size_t)(z->ulen - z->upos);
+        if (k > n - done) k = n - done;
+        memcpy(d + done, z->ubuf + z->upos, k);
+        z->upos += (int)k;
+        done += k;
+    }
+    if (z->upos == z->ulen) {        /* htslib: the offset moves to the next block */
+        z->caddr = z->next;
+        z->ulen = z->upos = 0;
+    }
+    return (int64_t)n;
+}
+
+static int bgzf_open(bgzf_t *z, const char *path) {
+    memset(z, 0, sizeof *z);
+    z->f = fopen(path, "rb");
+    if (!z->f) return -1;
+    const int rc = bgzf_load(z, 0);
+    if (rc != 0) { fclose(z->f); z->f = NULL; return rc == 1 ? PF_ERR_ARG : rc == -1 ? -1 : PF_ERR_ARG; }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* index */
+typedef struct { uint64_t u, v; } chunk_t;
+typedef struct {
+    uint32_t bin;
+    uint32_t n;
+    chunk_t *c;
+} bin_t;
+typedef struct {
+    uint32_t n_bin, n_intv;
+    bin_t *bins;                 /* sorted by bin number */
+    uint64_t *intv;
+    int has_meta;
+    uint64_t mapped, unmapped;
+} ref_idx_t;
+
+struct pf_bam {
+    char *path;
+    int32_t n_ref;
+    char **names;
+    uint32_t *lens;
+    uint64_t data_off;           /* virtual offset of the first record */
+    int32_t n_ref_idx;
+    ref_idx_t *idx;
+};
+
+static int cmp_bin(const void *a, const void *b) {
+    const uint32_t x = ((const bin_t *)a)->bin, y = ((const bin_t *)b)->bin;
+    return x < y ? -1 : x > y;
+}
+
+static uint8_t *slurp(const char *path, size_t *n) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return NULL;
+    size_t cap = 1 << 16, len = 0;
+    uint8_t *buf = (uint8_t *)malloc(cap);
+    for (;;) {
+        if (!buf) { fclose(f); return NULL; }
+        const size_t k = fread(buf + len, 1, cap - len, f);
+        len += k;
+        if (len < cap) break;
+        cap *= 2;
+        uint8_t *nb = (uint8_t *)realloc(buf, cap);
+        if (!nb) { free(buf); fclose(f); return NULL; }
+        buf = nb;
+    }
+    fclose(f);
+    *n = len;
+    return buf;
+}
+
+static int load_bai(pf_bam_t *b, const char *path) {
+    size_t n = 0;
+    uint8_t *d = slurp(path, &n);
+    if (!d) return -1;
+    int rc = PF_ERR_ARG;
+    size_t o = 8;
+    if (n < 8 || memcmp(d, "BAI\1", 4) != 0) goto out;
+    const int32_t nr = (int32_t)rd32(d + 4);
+    if (nr < 0) goto out;
+    b->n_ref_idx = nr;
+    b->idx = (ref_idx_t *)calloc(nr ? (size_t)nr : 1, sizeof(ref_idx_t));
+    if (!b->idx) { rc = PF_ERR_NOMEM; goto out; }
+    for (int32_t r = 0; r < nr; r++) {
+        ref_idx_t *ri = &b->idx[r];
+        if (o + 4 > n) goto out;
+        const uint32_t nb = rd32(d + o);
+        o += 4;
+        ri->bins = (bin_t *)calloc(nb ? nb : 1, sizeof(bin_t));
+        if (!ri->bins) { rc = PF_ERR_NOMEM; goto out; }
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < nb; i++) {
+            if (o + 8 > n) goto out;
+            const uint32_t bin = rd32(d + o), nc = rd32(d + o + 4);
+            o += 8;
+            if (nc > (n - o) / 16) goto out;
+            if (bin == 37450) {                       /* metadata pseudo-bin */
+                if (nc >= 2) {
+                    ri->has_meta = 1;
+                    ri->mapped = rd64(d + o + 16);
+                    ri->unmapped = rd64(d + o + 24);
+                }
+                o += 16ull * nc;
+                continue;
+            }
+            bin_t *bb = &ri->bins[k++];
+            bb->bin = bin;
+            bb->n = nc;
+            bb->c = (chunk_t *)malloc((nc ? nc : 1) * sizeof(chunk_t));
+            if (!bb->c) { rc = PF_ERR_NOMEM; goto out; }
+            for (uint32_t c = 0; c < nc; c++) {
+                bb->c[c].u = rd64(d + o);
+                bb->c[c].v = rd64(d + o + 8);
+                o += 16;
+            }
+        }
+        ri->n_bin = k;
+        qsort(ri->bins, k, sizeof(bin_t), cmp_bin);
+        if (o + 4 > n) goto out;
+        const uint32_t ni = rd32(d + o);
+        o += 4;
+        if (ni > (n - o) / 8) goto out;
+        ri->n_intv = ni;
+        ri->intv = (uint64_t *)malloc((ni ? ni : 1) * sizeof(uint64_t));
+        if (!ri->intv) { rc = PF_ERR_NOMEM; goto out; }
+        for (uint32_t i = 0; i < ni; i++) ri->intv[i] = rd64(d + o + 8ull * i);
+        o += 8ull * ni;
+    }
+    rc = PF_OK;
+out:
+    free(d);
+    return rc;
+}
+
+static int load_header(pf_bam_t *b) {
+    bgzf_t *z = (bgzf_t *)malloc(sizeof(bgzf_t));
+    if (!z) return PF_ERR_NOMEM;
+    int rc = bgzf_open(z, b->path);
+    if (rc) { free(z); return rc; }
+    uint8_t h[8];
+    rc = PF_ERR_ARG;
+    if (bgzf_read(z, h, 8) != 8 || memcmp(h, "BAM\1", 4) != 0) goto out;
+    {
+        const uint32_t lt = rd32(h + 4);
+        char *text = (char *)malloc(lt ? lt : 1);
+        if (!text) { rc = PF_ERR_NOMEM; goto out; }
+        const int64_t g = bgzf_read(z, text, lt);
+        free(text);
+        if (g != (int64_t)lt) goto out;
+    }
+    uint8_t w[4];
+    if (bgzf_read(z, w, 4) != 4) goto out;
+    b->n_ref = (int32_t)rd32(w);
+    if (b->n_ref < 0) goto out;
+    b->names = (char **)calloc(b->n_ref ? (size_t)b->n_ref : 1, sizeof(char *));
+    b->lens = (uint32_t *)calloc(b->n_ref ? (size_t)b->n_ref : 1, sizeof(uint32_t));
+    if (!b->names || !b->lens) { rc = PF_ERR_NOMEM; goto out; }
+    for (int32_t r = 0; r < b->n_ref; r++) {
+        if (bgzf_read(z, w, 4) != 4) goto out;
+        const uint32_t ln = rd32(w);
+        if (ln == 0 || ln > (1u << 20)) goto out;
+        b->names[r] = (char *)malloc(ln);
+        if (!b->names[r]) { rc = PF_ERR_NOMEM; goto out; }
+        if (bgzf_read(z, b->names[r], ln) != (int64_t)ln) goto out;
+        b->names[r][ln - 1] = 0;
+        if (bgzf_read(z, w, 4) != 4) goto out;
+        b->lens[r] = rd32(w);
+    }
+    b->data_off = bgzf_tell(z);
+    rc = PF_OK;
+out:
+    fclose(z->f);
+    free(z);
+    return rc;
+}
+
+int pf_bam_open(const char *bam_path, const char *bai_path, pf_bam_t **out) {
+    if (!out || (!bam_path && !bai_path)) return PF_ERR_ARG;
+    *out = NULL;
+    pf_bam_t *b = (pf_bam_t *)calloc(1, sizeof(pf_bam_t));
+    if (!b) return PF_ERR_NOMEM;
+    int rc = PF_OK;
+    if (bam_path) {
+        b->path = strdup(bam_path);
+        if (!b->path) { pf_bam_close(b); return PF_ERR_NOMEM; }
+        rc = load_header(b);
+        if (rc) { pf_bam_close(b); return rc; }
+    }
+    if (bai_path) rc = load_bai(b, bai_path);
+    else {
+        const size_t L = strlen(bam_path);
+        char *p = (char *)malloc(L + 5);
+        if (!p) { pf_bam_close(b); return PF_ERR_NOMEM; }
+        memcpy(p, bam_path, L);
+        memcpy(p + L, ".bai", 5);
+        rc = load_bai(b, p);
+        if (rc == -1 && L > 4 && strcmp(bam_path + L - 4, ".bam") == 0) {
+            memcpy(p + L - 4, ".bai", 5);
+            rc = load_bai(b, p);
+        }
+        free(p);
+    }
+    if (rc) { pf_bam_close(b); return rc; }
+    if (bam_path && b->n_ref_idx != b->n_ref) { pf_bam_close(b); return PF_ERR_ARG; }
+    *out = b;
+    return PF_OK;
+}
+
+void pf_bam_close(pf_bam_t *b) {
+    if (!b) return;
+    for (int32_t r = 0; r < b->n_ref; r++) free(b->names ? b->names[r] : NULL);
+    free(b->names);
+    free(b->lens);
+    for (int32_t r = 0; b->idx && r < b->n_ref_idx; r++) {
+        for (uint32_t i = 0; i < b->idx[r].n_bin; i++) free(b->idx[r].bins[i].c);
+        free(b->idx[r].bins);
+        free(b->idx[r].intv);
+    }
+    free(b->idx);
+    free(b->path);
+    free(b);
+}
+
+int32_t pf_bam_n_targets(const pf_bam_t *b) { return b ? (b->path ? b->n_ref : b->n_ref_idx) : 0; }
+const char *pf_bam_target_name(const pf_bam_t *b, int32_t tid) {
+    return b && b->names && tid >= 0 && tid < b->n_ref ? b->names[tid] : NULL;
+}
+uint32_t pf_bam_target_len(const pf_bam_t *b, int32_t tid) {
+    return b && b->lens && tid >= 0 && tid < b->n_ref ? b->lens[tid] : 0;
+}
+int32_t pf_bam_tid(const pf_bam_t *b, const char *name) {
+    if (!b || !name || !b->names) return -1;
+    for (int32_t r = 0; r < b->n_ref; r++)
+        if (strcmp(b->names[r], name) == 0) return r;
+    return -1;
+}
+int pf_bam_index_stats(const pf_bam_t *b, int32_t tid, uint64_t *mapped, uint64_t *unmapped) {
+    if (!b || tid < 0 || tid >= b->n_ref_idx || !b->idx[tid].has_meta) return PF_ERR_ARG;
+    if (mapped) *mapped = b->idx[tid].mapped;
+    if (unmapped) *unmapped = b->idx[tid].unmapped;
+    return PF_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* growable arrays of one fetch */
+typedef struct {
+    uint8_t *p;
+    size_t n, cap;
+} vbuf_t;
+
+static int vb_put(vbuf_t *v, const void *src, size_t n) {
+    if (v->n + n > v->cap) {
+        size_t c = v->cap ? v->cap : 256;
+        while (c < v->n + n) c *= 2;
+        uint8_t *np = (uint8_t *)realloc(v->p, c);
+        if (!np) return PF_ERR_NOMEM;
+        v->p = np;
+        v->cap = c;
+    }
+    if (n) memcpy(v->p + v->n, src, n);
+    v->n += n;
+    return 0;
+}
+
+enum { F_FLAG, F_MAPQ, F_POS, F_LQ, F_DE, F_HP, F_HPTAG, F_CIG, F_SEQ, F_MM, F_ML, F_QN,
+       F_CIGOFF, F_SEQOFF, F_MMOFF, F_MLOFF, F_QNOFF, NF };
+
+typedef struct {
+    vbuf_t f[NF];
+    uint64_t n_recs;
+    uint64_t truncated;
+} recbuf_t;
+
+static void rb_free(recbuf_t *r) {
+    for (int i = 0; i < NF; i++) free(r->f[i].p);
+    memset(r, 0, sizeof *r);
+}
+
+/* aux field size past its 3-byte tag+type header; 0 for an unknown type */
+static size_t aux_size(const uint8_t *p, const uint8_t *end) {
+    const uint8_t t = p[2];
+    const uint8_t *v = p + 3;
+    switch (t) {
+    case 'A': case 'c': case 'C': return 1;
+    case 's': case 'S': return 2;
+    case 'i': case 'I': case 'f': return 4;
+    case 'd': return 8;
+    case 'Z': case 'H': {
+        const uint8_t *q = v;
+        while (q < end && *q) q++;
+        return q < end ? (size_t)(q - v) + 1 : 0;
+    }
+    case 'B': {
+        if (v + 5 > end) return 0;
+        const uint32_t cnt = rd32(v + 1);
+        size_t es;
+        switch (v[0]) {
+        case 'c': case 'C': es = 1; break;
+        case 's': case 'S': es = 2; break;
+        case 'i': case 'I': case 'f': es = 4; break;
+        default: return 0;
+        }
+        return 5 + (size_t)cnt * es;
+    }
+    default: return 0;
+    }
+}
+
+static const uint8_t *aux_find(const uint8_t *aux, const uint8_t *end, const char tag[2]) {
+    const uint8_t *p = aux;
+    while (p + 3 <= end) {
+        const size_t s = aux_size(p, end);
+        if (s == 0 || p + 3 + s > end) return NULL;
+        if (p[0] == (uint8_t)tag[0] && p[1] == (uint8_t)tag[1]) return p;
+        p += 3 + s;
+    }
+    return NULL;
+}
+
+static int aux_int(const uint8_t *p, int64_t *out) {     /* bam_aux2i for integer types */
+    const uint8_t *v = p + 3;
+    switch (p[2]) {
+    case 'c': *out = (int8_t)v[0]; return 1;
+    case 'C': *out = v[0]; return 1;
+    case 's': *out = (int16_t)rd16(v); return 1;
+    case 'S': *out = rd16(v); return 1;
+    case 'i': *out = (int32_t)rd32(v); return 1;
+    case 'I': *out = rd32(v); return 1;
+    default: return 0;
+    }
+}
+
+static double aux_f(const uint8_t *p) {                  /* bam_aux2f */
+    const uint8_t *v = p + 3;
+    int64_t x;
+    if (p[2] == 'd') { double d; memcpy(&d, v, 8); return d; }
+    if (p[2] == 'f') { float f; memcpy(&f, v, 4); return f; }
+    if (aux_int(p, &x)) return (double)x;
+    return 0.0;
+}
+
+/* one decoded record, pointing into the caller's buffer */
+typedef struct {
+    int32_t tid, pos;
+    uint32_t l_qseq, n_cigar;
+    uint16_t flag;
+    uint8_t mapq;
+    const char *qname;
+    uint32_t l_qname;
+    const uint8_t *cigar;     /* n_cigar little-endian u32 */
+    const uint8_t *seq;
+    const uint8_t *aux, *aux_end;
+} rec_t;
+
+/* decode; 0 ok, <0 corrupt */
+static int rec_decode(const uint8_t *d, uint32_t bs, rec_t *r) {
+    if (bs < 32) return -1;
+    r->tid = (int32_t)rd32(d);
+    r->pos = (int32_t)rd32(d + 4);
+    const uint32_t lrn = d[8];
+    r->mapq = d[9];
+    r->n_cigar = rd16(d + 12);
+    r->flag = (uint16_t)rd16(d + 14);
+    const int32_t lseq = (int32_t)rd32(d + 16);
+    if (lseq < 0 || lrn == 0) return -1;
+    r->l_qseq = (uint32_t)lseq;
+    uint64_t o = 32;
+    r->qname = (const char *)(d + o);
+    r->l_qname = lrn;
+    o += lrn;
+    r->cigar = d + o;
+    o += 4ull * r->n_cigar;
+    r->seq = d + o;
+    o += (r->l_qseq + 1ull) / 2;
+    o += r->l_qseq;                                     /* qual */
+    if (o > bs) return -1;
+    r->aux = d + o;
+    r->aux_end = d + bs;
+    return 0;
+}
+
+static uint64_t cigar_rlen(const uint8_t *cg, uint32_t n, uint64_t *qlen) {
+    uint64_t rl = 0, ql = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t c = rd32(cg + 4ull * i), op = c & 15u, ln = c >> 4;
+        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += ln;
+        if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += ln;
+    }
+    if (qlen) *qlen = ql;
+    return rl;
+}
+
+/* the records of one region [beg, end) of tid into rb */
+typedef struct {
+    const pf_bam_t *b;
+    int32_t tid;
+    bgzf_t z;
+    uint8_t *rec;
+    size_t rec_cap;
+    chunk_t *chunks;
+    size_t chunk_cap;
+} fetcher_t;
+
+static int push_record(recbuf_t *rb, const rec_t *r, const uint8_t *cg, uint32_t ncg) {
+    int rc = 0;
+    const uint32_t pos = (uint32_t)r->pos, lq = r->l_qseq;
+    float de = -1.f;
+    const uint8_t *t = aux_find(r->aux, r->aux_end, "de");
+    if (t) de = (float)aux_f(t);
+    int32_t hp_tag = INT32_MIN;
+    uint8_t hp = 254;
+    t = aux_find(r->aux, r->aux_end, "HP");
+    if (t) {
+        int64_t v = 0;
+        if (!aux_int(t, &v)) v = 0;                     /* bam_aux2i of a non-integer: 0 */
+        hp_tag = v < INT32_MIN ? INT32_MIN + 1 : v > INT32_MAX ? INT32_MAX : (int32_t)v;
+        /* get_hp_from_aln: 0 -> unphased, else HP-1 (an int); values outside
+         * 1..255 are kept as unphased (the batch holds u8 tags) */
+        hp = (v >= 1 && v <= 255) ? (uint8_t)(v - 1) : 254;
+    }
+    const uint8_t *mm = aux_find(r->aux, r->aux_end, "MM");
+    if (!mm) mm = aux_find(r->aux, r->aux_end, "Mm");
+    const uint8_t *ml = aux_find(r->aux, r->aux_end, "ML");
+    if (!ml) ml = aux_find(r->aux, r->aux_end, "Ml");
+    const char *mmz = NULL;
+    size_t mml = 0;
+    const uint8_t *mlv = NULL;
+    uint32_t mln = 0;
+    int mods_ok = 1;
+    if (mm && mm[2] != 'Z') mods_ok = 0;
+    if (ml && (ml[2] != 'B' || ml[3] != 'C')) mods_ok = 0;
+    if (mods_ok && mm) {
+        mmz = (const char *)(mm + 3);
+        mml = strlen(mmz);
+        if (ml) { mln = rd32(ml + 4); mlv = ml + 8; }
+    }
+    uint64_t off;
+#define PUTV(fi, ptr, nb) do { if ((rc = vb_put(&rb->f[fi], (ptr), (nb)))) return rc; } while (0)
+    PUTV(F_FLAG, &r->flag, 2);
+    PUTV(F_MAPQ, &r->mapq, 1);
+    PUTV(F_POS, &pos, 4);
+    PUTV(F_LQ, &lq, 4);
+    PUTV(F_DE, &de, 4);
+    PUTV(F_HP, &hp, 1);
+    PUTV(F_HPTAG, &hp_tag, 4);
+    off = rb->f[F_CIG].n / 4; PUTV(F_CIGOFF, &off, 8);
+    PUTV(F_CIG, cg, 4ull * ncg);
+    off = rb->f[F_SEQ].n; PUTV(F_SEQOFF, &off, 8);
+    PUTV(F_SEQ, r->seq, (lq + 1ull) / 2);
+    off = rb->f[F_MM].n; PUTV(F_MMOFF, &off, 8);
+    if (mml) PUTV(F_MM, mmz, mml);
+    off = rb->f[F_ML].n; PUTV(F_MLOFF, &off, 8);
+    if (mln) PUTV(F_ML, mlv, mln);
+    off = rb->f[F_QN].n; PUTV(F_QNOFF, &off, 8);
+    PUTV(F_QN, r->qname, strnlen(r->qname, r->l_qname));
+#undef PUTV
+    rb->n_recs++;
+    return 0;
+}
+
+static int cmp_chunk(const void *a, const void *b) {
+    const uint64_t x = ((const chunk_t *)a)->u, y = ((const chunk_t *)b)->u;
+    return x < y ? -1 : x > y;
+}
+
+static int fetch_region(fetcher_t *F, int64_t beg, int64_t end, recbuf_t *rb) {
+    const ref_idx_t *ri = &F->b->idx[F->tid];
+    if (end <= beg) return 0;
+    /* reg2bins(beg, end) of the SAM spec, end exclusive */
+    uint32_t bins[4681 + 4096 + 16];
+    uint32_t nb = 0;
+    {
+        const int64_t e = end - 1;
+        const int64_t b0 = beg;
+        bins[nb++] = 0;
+        static const int sh[5] = {26, 23, 20, 17, 14};
+        static const uint32_t base[5] = {1, 9, 73, 585, 4681};
+        for (int l = 0; l < 5; l++) {
+            int64_t k0 = base[l] + (b0 >> sh[l]), k1 = base[l] + (e >> sh[l]);
+            const int64_t kmax = (l == 4) ? 37449 : base[l + 1] - 1;
+            if (k1 > kmax) k1 = kmax;
+            for (int64_t k = k0; k <= k1 && nb < sizeof bins / sizeof bins[0]; k++) bins[nb++] = (uint32_t)k;
+        }
+    }
+    uint64_t min_off = 0;
+    if (ri->n_intv) {
+        const int64_t li = beg >> 14;
+        min_off = li >= (int64_t)ri->n_intv ? ri->intv[ri->n_intv - 1] : ri->intv[li];
+    }
+    size_t nc = 0;
+    for (uint32_t i = 0; i < nb; i++) {
+        bin_t key;
+        key.bin = bins[i];
+        const bin_t *bb = (const bin_t *)bsearch(&key, ri->bins, ri->n_bin, sizeof(bin_t), cmp_bin);
+        if (!bb) continue;
+        for (uint32_t c = 0; c < bb->n; c++) {
+            if (bb->c[c].v <= min_off) continue;
+            if (nc == F->chunk_cap) {
+                const size_t cap = F->chunk_cap ? 2 * F->chunk_cap : 64;
+                chunk_t *np = (chunk_t *)realloc(F->chunks, cap * sizeof(chunk_t));
+                if (!np) return PF_ERR_NOMEM;
+                F->chunks = np;
+                F->chunk_cap = cap;
+            }
+            F->chunks[nc++] = bb->c[c];
+        }
+    }
+    if (!nc) return 0;
+    qsort(F->chunks, nc, sizeof(chunk_t), cmp_chunk);
+    uint64_t done = 0;                          /* records before this offset were read */
+    for (size_t c = 0; c < nc; c++) {
+        uint64_t at = F->chunks[c].u > done ? F->chunks[c].u : done;
+        if (at >= F->chunks[c].v) continue;
+        int rc = bgzf_seek(&F->z, at);
+        if (rc) return PF_ERR_ARG;
+        while (bgzf_tell(&F->z) < F->chunks[c].v) {
+            uint8_t w[4];
+            const int64_t g = bgzf_read(&F->z, w, 4);
+            if (g == 0) return 0;
+            if (g != 4) return PF_ERR_ARG;
+            const uint32_t bs = rd32(w);
+            if (bs < 32 || bs > (1u << 30)) return PF_ERR_ARG;
+            if (bs > F->rec_cap) {
+                uint8_t *np = (uint8_t *)realloc(F->rec, bs);
+                if (!np) return PF_ERR_NOMEM;
+                F->rec = np;
+                F->rec_cap = bs;
+            }
+            if (bgzf_read(&F->z, F->rec, bs) != (int64_t)bs) return PF_ERR_ARG;
+            done = bgzf_tell(&F->z);
+            rec_t r;
+            if (rec_decode(F->rec, bs, &r)) return PF_ERR_ARG;
+            /* bam_tag2cigar: a kSmN placeholder with a CG:B:I / B:i tag */
+            const uint8_t *cg = r.cigar;
+            uint32_t ncg = r.n_cigar;
+            if (ncg > 0 && r.tid >= 0 && r.pos >= 0 && (rd32(cg) & 15u) == 4u && (rd32(cg) >> 4) == r.l_qseq) {
+                const uint8_t *t = aux_find(r.aux, r.aux_end, "CG");
+                if (t && t[2] == 'B' && (t[3] == 'I' || t[3] == 'i')) {
+                    const uint32_t n = rd32(t + 4);
+                    if (n >= r.n_cigar && n < (1u << 29)) { cg = t + 8; ncg = n; }
+                }
+            }
+            uint64_t qlen = 0;
+            uint64_t rlen = cigar_rlen(cg, ncg, &qlen);
+            if (ncg > 0 && r.l_qseq > 0 && !(r.flag & 4) && qlen != r.l_qseq) {
+                rb->truncated++;                        /* bam_read1 -> -4: the fetch ends */
+                return 0;
+            }
+            if ((r.flag & 4) || ncg == 0) rlen = 0;
+            if (rlen == 0) rlen = 1;
+            if (r.tid != F->tid || (int64_t)r.pos >= end) return 0;
+            if ((int64_t)r.pos + (int64_t)rlen > beg) {
+                rc = push_record(rb, &r, cg, ncg);
+                if (rc) return rc;
+            }
+        }
+    }
+    return 0;
+}
+
+typedef struct {
+    const pf_bam_t *b;
+    int32_t tid;
+    const uint32_t *ws, *we;
+    uint32_t w0, w1, readback;
+    recbuf_t *out;            /* one per window */
+    uint64_t *win_n;
+    int rc;
+} job_t;
+
+static void *fetch_job(void *arg) {
+    job_t *j = (job_t *)arg;
+    fetcher_t F;
+    memset(&F, 0, sizeof F);
+    F.b = j->b;
+    F.tid = j->tid;
+    int rc = bgzf_open(&F.z, j->b->path);
+    for (uint32_t w = j->w0; !rc && w < j->w1; w++) {
+        /* "%s:%d-%d" with (s-readback)>0 ? s-readback : 0 and e+readback (int
+         * arithmetic, 1053-1054); htslib reads b-E as the 0-based [b-1, E) */
+        const int64_t s = (int32_t)j->ws[w], e = (int32_t)j->we[w], rb = (int32_t)j->readback;
+        const int64_t b1 = s - rb > 0 ? s - rb : 0;
+        const int64_t beg = b1 > 0 ? b1 - 1 : 0, end = e + rb;
+        const uint64_t n0 = j->out->n_recs;
+        rc = fetch_region(&F, beg, end, j->out);
+        j->win_n[w] = j->out->n_recs - n0;
+    }
+    if (F.z.f) fclose(F.z.f);
+    free(F.rec);
+    free(F.chunks);
+    j->rc = rc;
+    return NULL;
+}
+
+struct pf_bam_records_own {
+    pf_bam_records_t pub;
+    recbuf_t rb;
+    uint32_t *ws, *we, *wro;
+};
+
+void pf_bam_records_free(pf_bam_records_t *r) {
+    if (!r) return;
+    struct pf_bam_records_own *o = (struct pf_bam_records_own *)r;
+    rb_free(&o->rb);
+    free(o->ws);
+    free(o->we);
+    free(o->wro);
+    free(o);
+}
+
+int pf_bam_fetch_windows(pf_bam_t *b, const char *chrom, uint32_t W, const uint32_t *ws, const uint32_t *we,
+                         uint32_t readback, int n_threads, pf_bam_records_t **out) {
+    if (!b || !chrom || !out || (W && (!ws || !we)) || !b->path) return PF_ERR_ARG;
+    *out = NULL;
+    const int32_t tid = pf_bam_tid(b, chrom);
+    if (tid < 0 || tid >= b->n_ref_idx) return PF_ERR_ARG;
+    if (n_threads < 1) n_threads = 1;
+    if ((uint32_t)n_threads > W) n_threads = W ? (int)W : 1;
+    struct pf_bam_records_own *o = (struct pf_bam_records_own *)calloc(1, sizeof *o);
+    if (!o) return PF_ERR_NOMEM;
+    o->ws = (uint32_t *)malloc((W ? W : 1) * 4ull);
+    o->we = (uint32_t *)malloc((W ? W : 1) * 4ull);
+    o->wro = (uint32_t *)malloc((W + 1ull) * 4);
+    uint64_t *win_n = (uint64_t *)calloc(W ? W : 1, 8);
+    recbuf_t *parts = (recbuf_t *)calloc((size_t)n_threads, sizeof(recbuf_t));
+    job_t *jobs = (job_t *)calloc((size_t)n_threads, sizeof(job_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
+    int rc = PF_OK;
+    if (!o->ws || !o->we || !o->wro || !win_n || !parts || !jobs || !th) rc = PF_ERR_NOMEM;
+    if (!rc) {
+        if (W) { memcpy(o->ws, ws, 4ull * W); memcpy(o->we, we, 4ull * W); }
+        /* contiguous window ranges per thread, so the parts concatenate in window order */
+        for (int t = 0; t < n_threads; t++) {
+            jobs[t].b = b; jobs[t].tid = tid; jobs[t].ws = ws; jobs[t].we = we; jobs[t].readback = readback;
+            jobs[t].w0 = (uint32_t)((uint64_t)W * t / n_threads);
+            jobs[t].w1 = (uint32_t)((uint64_t)W * (t + 1) / n_threads);
+            jobs[t].out = &parts[t];
+            jobs[t].win_n = win_n;
+        }
+        char *made = (char *)calloc((size_t)n_threads, 1);
+        for (int t = 1; t < n_threads; t++)
+            if (made) made[t] = pthread_create(&th[t], NULL, fetch_job, &jobs[t]) == 0;
+        fetch_job(&jobs[0]);
+        for (int t = 1; t < n_threads; t++) {
+            if (made && made[t]) pthread_join(th[t], NULL);
+            else fetch_job(&jobs[t]);              /* no thread: run it here */
+        }
+        free(made);
+        for (int t = 0; t < n_threads && !rc; t++) rc = jobs[t].rc;
+    }
+    if (!rc) {
+        /* concatenate the parts, rebasing the offsets */
+        recbuf_t *R = &o->rb;
+        uint64_t base[NF] = {0};
+        for (int t = 0; t < n_threads && !rc; t++) {
+            recbuf_t *P = &parts[t];
+            for (int f = 0; f < F_CIGOFF && !rc; f++) {
+                base[f] = R->f[f].n;
+                rc = vb_put(&R->f[f], P->f[f].p, P->f[f].n);
+            }
+            static const int offs[5][2] = {{F_CIGOFF, F_CIG}, {F_SEQOFF, F_SEQ}, {F_MMOFF, F_MM},
+                                           {F_MLOFF, F_ML}, {F_QNOFF, F_QN}};
+            for (int k = 0; k < 5 && !rc; k++) {
+                const uint64_t add = offs[k][1] == F_CIG ? base[F_CIG] / 4 : base[offs[k][1]];
+                const uint64_t *src = (const uint64_t *)P->f[offs[k][0]].p;
+                for (uint64_t i = 0; i < P->n_recs && !rc; i++) {
+                    const uint64_t v = src[i] + add;
+                    rc = vb_put(&R->f[offs[k][0]], &v, 8);
+                }
+            }
+            R->n_recs += P->n_recs;
+            R->truncated += P->truncated;
+        }
+        /* closing offsets */
+        static const int offs2[5][2] = {{F_CIGOFF, F_CIG}, {F_SEQOFF, F_SEQ}, {F_MMOFF, F_MM}, {F_MLOFF, F_ML},
+                                        {F_QNOFF, F_QN}};
+        for (int k = 0; k < 5 && !rc; k++) {
+            const uint64_t v = offs2[k][1] == F_CIG ? R->f[F_CIG].n / 4 : R->f[offs2[k][1]].n;
+            rc = vb_put(&R->f[offs2[k][0]], &v, 8);
+        }
+        if (!rc && R->n_recs > 0xFFFFFFFFull) rc = PF_ERR_LIMIT;
+    }
+    if (!rc) {
+        uint64_t acc = 0;
+        for (uint32_t w = 0; w < W; w++) { o->wro[w] = (uint32_t)acc; acc += win_n[w]; }
+        o->wro[W] = (uint32_t)acc;
+        recbuf_t *R = &o->rb;
+        pf_aln_batch_t *a = &o->pub.aln;
+        memset(a, 0, sizeof *a);
+        a->n_windows = W;
+        a->n_recs = (uint32_t)R->n_recs;
+        a->win_start = o->ws;
+        a->win_end = o->we;
+        a->win_rec_off = o->wro;
+        a->flag = (const uint16_t *)R->f[F_FLAG].p;
+        a->mapq = R->f[F_MAPQ].p;
+        a->pos = (const uint32_t *)R->f[F_POS].p;
+        a->l_qseq = (const uint32_t *)R->f[F_LQ].p;
+        a->de = (const float *)R->f[F_DE].p;
+        a->hp = R->f[F_HP].p;
+        a->cigar_off = (const uint64_t *)R->f[F_CIGOFF].p;
+        a->cigar = (const uint32_t *)R->f[F_CIG].p;
+        a->seq_off = (const uint64_t *)R->f[F_SEQOFF].p;
+        a->seq = R->f[F_SEQ].p;
+        a->mm_off = (const uint64_t *)R->f[F_MMOFF].p;
+        a->mm = (const char *)R->f[F_MM].p;
+        a->ml_off = (const uint64_t *)R->f[F_MLOFF].p;
+        a->ml = R->f[F_ML].p;
+        o->pub.qname_off = (const uint64_t *)R->f[F_QNOFF].p;
+        o->pub.qname = (const char *)R->f[F_QN].p;
+        o->pub.hp_tag = (const int32_t *)R->f[F_HPTAG].p;
+        o->pub.n_truncated = R->truncated;
+        /* empty arrays still get a valid pointer */
+        static const uint8_t dummy[8] = {0};
+        if (!a->flag) a->flag = (const uint16_t *)dummy;
+        if (!a->mapq) a->mapq = dummy;
+        if (!a->pos) a->pos = (const uint32_t *)dummy;
+        if (!a->l_qseq) a->l_qseq = (const uint32_t *)dummy;
+        if (!a->de) a->de = (const float *)dummy;
+        if (!a->hp) a->hp = dummy;
+        if (!a->cigar) a->cigar = (const uint32_t *)dummy;
+        if (!a->seq) a->seq = dummy;
+        if (!a->mm) a->mm = (const char *)dummy;
+        if (!a->ml) a->ml = dummy;
+        if (!o->pub.qname) o->pub.qname = (const char *)dummy;
+        if (!o->pub.hp_tag) o->pub.hp_tag = (const int32_t *)dummy;
+    }
+    for (int t = 0; parts && t < n_threads; t++) rb_free(&parts[t]);
+    free(parts);
+    free(jobs);
+    free(th);
+    free(win_n);
+    if (rc) { pf_bam_records_free(&o->pub); return rc; }
+    *out = &o->pub;
+    return PF_OK;
+}

@@ -1,0 +1,262 @@
+"""Test-side BAM + BAI writer (SAM/BAM specification, SAMv1 4.1-4.2, 5.2),
+independent of the library's reader: BGZF blocks by zlib raw deflate, the
+index's bins / chunks / 16 kb linear index / metadata pseudo-bin built as
+htslib's indexer does.  Used to make BAM fixtures for tests/test_bam.py;
+test infrastructure, never imported by the product."""
+from __future__ import annotations
+
+import struct
+import zlib
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+BLOCK = 0xFF00          # htslib BGZF_BLOCK_SIZE: uncompressed bytes per block
+EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def reg2bin(beg: int, end: int) -> int:
+    end -= 1
+    if beg >> 14 == end >> 14:
+        return ((1 << 15) - 1) // 7 + (beg >> 14)
+    if beg >> 17 == end >> 17:
+        return ((1 << 12) - 1) // 7 + (beg >> 17)
+    if beg >> 20 == end >> 20:
+        return ((1 << 9) - 1) // 7 + (beg >> 20)
+    if beg >> 23 == end >> 23:
+        return ((1 << 6) - 1) // 7 + (beg >> 23)
+    if beg >> 26 == end >> 26:
+        return ((1 << 3) - 1) // 7 + (beg >> 26)
+    return 0
+
+
+def ref_len(cigar) -> int:
+    return int(sum(c >> 4 for c in cigar if (c & 15) in (0, 2, 3, 7, 8)))
+
+
+def endpos(pos: int, cigar, flag: int) -> int:
+    rl = 0 if (flag & 4) else ref_len(cigar)
+    return pos + (rl if rl > 0 else 1)
+
+
+@dataclass
+class Rec:
+    tid: int
+    pos: int
+    qname: str
+    flag: int = 0
+    mapq: int = 60
+    cigar: List[int] = field(default_factory=list)    # BAM encoding len<<4|op
+    seq: bytes = b""                                  # 4-bit packed, (l+1)//2 bytes
+    l_seq: int = 0
+    aux: bytes = b""
+    bin_override: Optional[int] = None
+
+
+def aux_Z(tag: str, s: str) -> bytes:
+    return tag.encode() + b"Z" + s.encode() + b"\0"
+
+
+def aux_i(tag: str, v: int) -> bytes:
+    return tag.encode() + b"i" + struct.pack("<i", v)
+
+
+def aux_C(tag: str, v: int) -> bytes:
+    return tag.encode() + b"C" + struct.pack("<B", v)
+
+
+def aux_f(tag: str, v: float) -> bytes:
+    return tag.encode() + b"f" + struct.pack("<f", v)
+
+
+def aux_BC(tag: str, vals) -> bytes:
+    vals = bytes(bytearray(vals))
+    return tag.encode() + b"BC" + struct.pack("<I", len(vals)) + vals
+
+
+def aux_BI(tag: str, vals) -> bytes:
+    vals = list(vals)
+    return tag.encode() + b"BI" + struct.pack("<I", len(vals)) + struct.pack(f"<{len(vals)}I", *vals)
+
+
+def encode_record(r: Rec) -> bytes:
+    qn = r.qname.encode() + b"\0"
+    end = endpos(r.pos, r.cigar, r.flag) if r.pos >= 0 else 0
+    b = r.bin_override if r.bin_override is not None else (reg2bin(r.pos, end) if r.pos >= 0 else 4680)
+    body = struct.pack("<iiBBHHHiiii", r.tid, r.pos, len(qn), r.mapq, b, len(r.cigar), r.flag, r.l_seq,
+                       -1, -1, 0)
+    body += qn + struct.pack(f"<{len(r.cigar)}I", *r.cigar) + bytes(r.seq) + b"\xff" * r.l_seq + r.aux
+    return struct.pack("<i", len(body)) + body
+
+
+class _Bgzf:
+    """BGZF writer tracking virtual offsets as htslib's bgzf_write does (a
+    full block is flushed at once, so an offset never points at a block's
+    end)."""
+
+    def __init__(self):
+        self.out = bytearray()
+        self.buf = bytearray()
+
+    def tell(self) -> int:
+        return (len(self.out) << 16) | len(self.buf)
+
+    def _flush(self):
+        if not self.buf:
+            return
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        data = c.compress(bytes(self.buf)) + c.flush()
+        bsize = 18 + len(data) + 8
+        hdr = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize - 1)
+        self.out += hdr + data + struct.pack("<II", zlib.crc32(bytes(self.buf)) & 0xFFFFFFFF, len(self.buf))
+        self.buf = bytearray()
+
+    def write(self, data: bytes):
+        i = 0
+        while i < len(data):
+            k = min(BLOCK - len(self.buf), len(data) - i)
+            self.buf += data[i:i + k]
+            i += k
+            if len(self.buf) == BLOCK:
+                self._flush()
+
+    def flush(self):
+        self._flush()
+
+    def close(self) -> bytes:
+        self._flush()
+        return bytes(self.out) + EOF_BLOCK
+
+
+def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, text: str = "@HD\tVN:1.6\tSO:coordinate\n"):
+    """refs: [(name, length)]; recs sorted by (tid, pos) with unplaced reads
+    (tid -1) last.  Writes path and path + '.bai' (or bai_path)."""
+    z = _Bgzf()
+    hdr = b"BAM\1" + struct.pack("<i", len(text)) + text.encode() + struct.pack("<i", len(refs))
+    for name, ln in refs:
+        nb = name.encode() + b"\0"
+        hdr += struct.pack("<i", len(nb)) + nb + struct.pack("<i", ln)
+    z.write(hdr)
+    z.flush()                                  # bam_hdr_write flushes the header block
+    nref = len(refs)
+    bins = [dict() for _ in range(nref)]       # bin -> [[u, v], ...]
+    lin = [dict() for _ in range(nref)]
+    meta = [[None, None, 0, 0] for _ in range(nref)]
+    last_bin = [None] * nref
+    n_no_coor = 0
+    for r in recs:
+        u = z.tell()
+        z.write(encode_record(r))
+        v = z.tell()
+        if r.tid < 0:
+            n_no_coor += 1
+            continue
+        t = r.tid
+        end = endpos(r.pos, r.cigar, r.flag)
+        b = reg2bin(r.pos, end)
+        ch = bins[t].setdefault(b, [])
+        if last_bin[t] == b and ch and ch[-1][1] == u:
+            ch[-1][1] = v                      # contiguous records of one bin: one chunk
+        else:
+            ch.append([u, v])
+        last_bin[t] = b
+        for wdw in range(r.pos >> 14, ((end - 1) >> 14) + 1):
+            lin[t].setdefault(wdw, u)
+        m = meta[t]
+        if m[0] is None:
+            m[0] = u
+        m[1] = v
+        if r.flag & 4:
+            m[3] += 1
+        else:
+            m[2] += 1
+    data = z.close()
+    with open(path, "wb") as f:
+        f.write(data)
+    idx = bytearray(b"BAI\1" + struct.pack("<i", nref))
+    for t in range(nref):
+        bl = sorted(bins[t].items())
+        has_meta = meta[t][0] is not None
+        idx += struct.pack("<i", len(bl) + (1 if has_meta else 0))
+        for b, chunks in bl:
+            idx += struct.pack("<Ii", b, len(chunks))
+            for u, v in chunks:
+                idx += struct.pack("<QQ", u, v)
+        if has_meta:
+            idx += struct.pack("<Ii", 37450, 2) + struct.pack("<QQQQ", meta[t][0], meta[t][1], meta[t][2], meta[t][3])
+        n_intv = (max(lin[t]) + 1) if lin[t] else 0
+        idx += struct.pack("<i", n_intv)
+        prev = 0
+        for wdw in range(n_intv):
+            val = lin[t].get(wdw, prev)        # htslib fills a gap with the previous offset
+            idx += struct.pack("<Q", val)
+            prev = val
+    idx += struct.pack("<Q", n_no_coor)
+    with open(bai_path or path + ".bai", "wb") as f:
+        f.write(bytes(idx))
+
+
+def records_from_aln(aln, tid: int = 0, prefix: str = "r", hp_zero_every: int = 0, de_absent_every: int = 0):
+    """One Rec per record of an AlnBatch (tests/_aln_cases / synth_aln), with
+    MM:Z, ML:B:C, HP:i (absent for 254; HP:i:0 every hp_zero_every-th
+    unphased record) and de:f (absent when < 0)."""
+    out = []
+    for i in range(aln.n_recs):
+        cig = [int(x) for x in aln.cigar[aln.cigar_off[i]:aln.cigar_off[i + 1]]]
+        lq = int(aln.l_qseq[i])
+        seq = bytes(aln.seq[aln.seq_off[i]:aln.seq_off[i] + (lq + 1) // 2])
+        aux = b""
+        hp = int(aln.hp[i])
+        if hp in (0, 1):
+            aux += aux_i("HP", hp + 1)
+        elif hp != 254:
+            aux += aux_i("HP", hp + 1)
+        elif hp_zero_every and i % hp_zero_every == 0:
+            aux += aux_C("HP", 0)
+        de = float(aln.de[i])
+        if de >= 0 and not (de_absent_every and i % de_absent_every == 0):
+            aux += aux_f("de", de)
+        mm = bytes(aln.mm[aln.mm_off[i]:aln.mm_off[i + 1]]).decode()
+        if mm:
+            aux += aux_Z("MM", mm)
+        ml = aln.ml[aln.ml_off[i]:aln.ml_off[i + 1]]
+        if len(ml):
+            aux += aux_BC("ML", ml)
+        out.append(Rec(tid=tid, pos=int(aln.pos[i]), qname=f"{prefix}{i}", flag=int(aln.flag[i]),
+                       mapq=int(aln.mapq[i]), cigar=cig, seq=seq, l_seq=lq, aux=aux))
+    return out
+
+
+def expected_fetch(recs: List[Rec], tid: int, s: int, e: int, readback: int) -> List[int]:
+    """Indices of recs that load_reads_given_interval's region query returns,
+    by the overlap rule alone (no index): region chrom:b-(e+rb) with
+    b = max(s-rb, 0) is the 0-based [max(b-1, 0), e+rb)."""
+    b1 = s - readback if s - readback > 0 else 0
+    beg, end = (b1 - 1 if b1 > 0 else 0), e + readback
+    return [i for i, r in enumerate(recs)
+            if r.tid == tid and r.pos < end and endpos(r.pos, r.cigar, r.flag) > beg]
+
+
+def write_phased_vcf(path: str, chrom: str, windows, chrom_len: int = 100_000_000):
+    """A one-sample phased VCF whose phase-block gaps are exactly `windows`
+    [(s, e), ...] (sorted, far apart): block k ends with a variant at POS s_k
+    and block k+1 starts at POS e_k with PS e_k (insert_vcf_line's gap is
+    [last POS of a block, PS of the next])."""
+    lines = ["##fileformat=VCFv4.2", f"##contig=<ID={chrom},length={chrom_len}>",
+             '##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype">',
+             '##FORMAT=<ID=PS,Number=1,Type=Integer,Description="Phase set">',
+             "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1"]
+    first = max(1, windows[0][0] - 1000)
+    ps = first
+    pts = [(first, ps)]
+    for s, e in windows:
+        pts.append((s, ps))
+        ps = e
+        pts.append((e, ps))
+    pts.append((windows[-1][1] + 1000, ps))
+    for k, (pos, p) in enumerate(pts):
+        gt = "0|1" if k % 2 == 0 else "1|0"
+        lines.append(f"{chrom}\t{pos}\t.\tA\tG\t50\tPASS\t.\tGT:PS\t{gt}:{p}")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")

@@ -1,0 +1,164 @@
+"""f1: the host BAM reader (pf_bam_*) -- index parse pinned by the reference's
+example BAI, region fetch against the overlap rule on BAM files written by
+tests/_bamio.py (an independent writer), and the record fields the loader
+needs.  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from pomfret_amd import LoadConfig
+from pomfret_amd.bam import BamFile
+from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+from _bamio import (Rec, aux_BC, aux_BI, aux_f, aux_i, aux_Z, endpos, expected_fetch, records_from_aln,
+                    write_bam)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+EXAMPLE_BAI = os.path.join(HERE, "golden", "example", "phased.bam.bai")
+
+
+def test_example_bai_pinned():
+    # the reference's own example index (example/phased.bam.bai): 195 targets,
+    # reads on target 5 only, 315 mapped / 0 unmapped in its pseudo-bin
+    with BamFile(None, EXAMPLE_BAI) as b:
+        assert b.n_targets == 195
+        assert b.index_stats(5) == (315, 0)
+        with pytest.raises(Exception):
+            b.index_stats(0)
+
+
+def _aln_records(n_windows=3, seed=5):
+    aln = make_aln_batch(AlnSpec(n_windows=n_windows, coverage=8, seed=seed, len_scale=0.3, filt_frac=0.1),
+                         workers=1)
+    return aln, records_from_aln(aln, hp_zero_every=7, de_absent_every=5)
+
+
+def _check_fetch(bam_path, recs, refs, chrom, starts, ends, readback, threads=1):
+    tid = [n for n, _ in refs].index(chrom)
+    with BamFile(bam_path) as b:
+        got, qn, info = b.fetch_windows(chrom, starts, ends, readback=readback, threads=threads)
+    exp = [expected_fetch(recs, tid, s, e, readback) for s, e in zip(starts, ends)]
+    wro = got.win_rec_off
+    assert wro[-1] == got.n_recs == sum(len(x) for x in exp)
+    for w, ids in enumerate(exp):
+        assert [qn[i] for i in range(wro[w], wro[w + 1])] == [recs[j].qname for j in ids], f"window {w}"
+    return got, qn, info, exp
+
+
+def test_fetch_windows_matches_overlap_rule(tmp_path):
+    aln, recs = _aln_records()
+    refs = [("chrA", 50_000_000), ("chrB", 50_000_000)]
+    # a second contig with the same records shifted, to exercise tid stops
+    recs2 = [Rec(tid=1, pos=r.pos + 1000, qname="b" + r.qname, flag=r.flag, mapq=r.mapq, cigar=r.cigar,
+                 seq=r.seq, l_seq=r.l_seq, aux=r.aux) for r in recs[:200]]
+    allr = recs + recs2
+    p = str(tmp_path / "x.bam")
+    write_bam(p, refs, allr)
+    starts = [int(s) for s in aln.win_start] + [10, 1_000]
+    ends = [int(e) for e in aln.win_end] + [20, 2_000]
+    for rb in (50_000, 0, 123):
+        got, qn, info, exp = _check_fetch(p, allr, refs, "chrA", starts, ends, rb)
+        assert info["n_truncated"] == 0
+    # threads do not change the result
+    g1, q1, _, _ = _check_fetch(p, allr, refs, "chrA", starts, ends, 50_000, threads=1)
+    g4, q4, _, _ = _check_fetch(p, allr, refs, "chrA", starts, ends, 50_000, threads=4)
+    assert q1 == q4
+    for f in ("pos", "flag", "cigar", "seq", "mm", "ml", "de", "hp", "cigar_off", "seq_off"):
+        assert np.array_equal(getattr(g1, f), getattr(g4, f)), f
+    _check_fetch(p, allr, refs, "chrB", [int(aln.win_start[0])], [int(aln.win_end[0])], 50_000)
+
+
+def test_fetched_fields_equal_the_written_records(tmp_path):
+    aln, recs = _aln_records(n_windows=2, seed=9)
+    refs = [("c1", 40_000_000)]
+    p = str(tmp_path / "y.bam")
+    write_bam(p, refs, recs)
+    with BamFile(p) as b:
+        assert b.targets == ["c1"] and b.lengths == [40_000_000]
+        assert b.tid("c1") == 0 and b.tid("nope") == -1
+        mapped, unmapped = b.index_stats(0)
+        assert mapped + unmapped == len(recs)
+        got, qn, info = b.fetch_windows("c1", aln.win_start, aln.win_end)
+    idx = {r.qname: i for i, r in enumerate(recs)}
+    for k in range(got.n_recs):
+        i = int(qn[k][1:])
+        assert idx[qn[k]] == i
+        assert got.pos[k] == aln.pos[i] and got.flag[k] == aln.flag[i] and got.mapq[k] == aln.mapq[i]
+        assert got.l_qseq[k] == aln.l_qseq[i]
+        c = got.cigar[got.cigar_off[k]:got.cigar_off[k + 1]]
+        assert np.array_equal(c, aln.cigar[aln.cigar_off[i]:aln.cigar_off[i + 1]])
+        lq = int(aln.l_qseq[i])
+        assert bytes(got.seq[got.seq_off[k]:got.seq_off[k + 1]]) == bytes(aln.seq[aln.seq_off[i]:aln.seq_off[i] + (lq + 1) // 2])
+        assert bytes(got.mm[got.mm_off[k]:got.mm_off[k + 1]]) == bytes(aln.mm[aln.mm_off[i]:aln.mm_off[i + 1]])
+        assert bytes(got.ml[got.ml_off[k]:got.ml_off[k + 1]]) == bytes(aln.ml[aln.ml_off[i]:aln.ml_off[i + 1]])
+        # HP: 0/1 round trip; 254 whether HP is absent or HP:i:0 (get_hp_from_aln)
+        assert got.hp[k] == aln.hp[i]
+        de_w = aln.de[i] >= 0 and i % 5 != 0
+        assert got.de[k] == (np.float32(aln.de[i]) if de_w else np.float32(-1))
+        assert info["hp_tag"][k] == (int(aln.hp[i]) + 1 if aln.hp[i] != 254 else (0 if i % 7 == 0 else -2**31))
+
+
+def test_fetch_feeds_the_loader(tmp_path):
+    """fetch -> oracle loader gives the same reads and calls as the loader on
+    the records selected by the overlap rule directly."""
+    aln, recs = _aln_records(n_windows=2, seed=3)
+    refs = [("c1", 40_000_000)]
+    p = str(tmp_path / "z.bam")
+    write_bam(p, refs, recs)
+    with BamFile(p) as b:
+        got, qn, _ = b.fetch_windows("c1", aln.win_start, aln.win_end)
+    # de values that were dropped from the tags are -1 in both
+    lc = LoadConfig()
+    wb_got, rr_got = oracle.load_reads(lc, got)
+    exp_ids = [expected_fetch(recs, 0, int(s), int(e), 50_000) for s, e in zip(aln.win_start, aln.win_end)]
+    flat = [i for ids in exp_ids for i in ids]
+    assert [int(q[1:]) for q in qn] == flat
+    assert wb_got.n_reads > 0 and wb_got.n_calls > 0
+
+
+def test_cg_tag_and_truncation(tmp_path):
+    """kSmN placeholder + CG:B:I restores the CIGAR (bam_tag2cigar); a record
+    whose CIGAR query length differs from l_qseq ends the window's fetch
+    (bam_read1 returns -4, sam_itr_next < 0)."""
+    seq = bytes([0x12] * 50)            # 100 bases
+    real = [(60 << 4) | 0, (2 << 4) | 2, (40 << 4) | 0]          # 60M2D40M
+    recs = [
+        Rec(0, 1000, "a", cigar=[(100 << 4) | 0], seq=seq, l_seq=100),
+        Rec(0, 1100, "cg", cigar=[(100 << 4) | 4, (102 << 4) | 3], seq=seq, l_seq=100,
+            aux=aux_BI("CG", real) + aux_i("HP", 1)),
+        Rec(0, 1200, "b", cigar=[(100 << 4) | 0], seq=seq, l_seq=100),
+        Rec(0, 5000, "bad", cigar=[(90 << 4) | 0], seq=seq, l_seq=100),   # qlen 90 != 100
+        Rec(0, 5100, "c", cigar=[(100 << 4) | 0], seq=seq, l_seq=100),
+        Rec(0, 40000, "u", flag=4, cigar=[], seq=seq, l_seq=100),         # unmapped, placed
+    ]
+    refs = [("c", 100_000)]
+    p = str(tmp_path / "c.bam")
+    write_bam(p, refs, recs)
+    with BamFile(p) as b:
+        got, qn, info = b.fetch_windows("c", [1050, 4000, 39990], [1150, 6000, 40001], readback=0, threads=2)
+    w = got.win_rec_off
+    assert qn[w[0]:w[1]] == ["a", "cg", "b"][:w[1] - w[0]] and "cg" in qn[w[0]:w[1]]
+    k = qn.index("cg")
+    assert list(got.cigar[got.cigar_off[k]:got.cigar_off[k + 1]]) == real
+    assert got.hp[k] == 0
+    assert qn[w[1]:w[2]] == []                 # "bad" stops the window before "c"
+    assert info["n_truncated"] == 1
+    assert qn[w[2]:w[3]] == ["u"]              # unmapped: end = pos + 1 (its own bin and
+    assert endpos(40000, [], 4) == 40001       # linear-index window: "bad" is not read)
+
+
+def test_errors(tmp_path):
+    with pytest.raises(FileNotFoundError):
+        BamFile(str(tmp_path / "missing.bam"))
+    p = str(tmp_path / "e.bam")
+    write_bam(p, [("c", 1000)], [])
+    with BamFile(p) as b:
+        with pytest.raises(Exception):
+            b.fetch_windows("nope", [1], [2])
+        got, qn, _ = b.fetch_windows("c", [1, 5], [2, 9])
+        assert got.n_recs == 0 and list(got.win_rec_off) == [0, 0, 0]
+    bad = tmp_path / "bad.bam"
+    bad.write_bytes(b"not a bam")
+    with pytest.raises(Exception):
+        BamFile(str(bad), p + ".bai")
