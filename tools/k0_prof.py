@@ -38,3 +38,15 @@ mx = k12[:, 1:7].sum(axis=1).argmax()
 print("  K12 phases, cycles: mean over windows | slowest window")
 for j in range(1, 7):
     print(f"    {names12[j]:12s} {k12[:, j].mean():10.0f} | {k12[mx, j]:10.0f}")
+# K3: per-(window, dir) greedy cycles of the same batch
+prof = raw[:nw * 64].reshape(nw, 2, 32)
+st = db.stats()
+per = (prof[:, :, :12].sum(axis=2) + prof[:, :, 16:24].sum(axis=2)).astype(float).ravel()
+it = st[:, :, 2].astype(float).ravel()
+q = np.percentile(per, [50, 90, 99, 100])
+print(f"  K3 problem cycles p50 {q[0]:.3g} p90 {q[1]:.3g} p99 {q[2]:.3g} max {q[3]:.3g}; "
+      f"iters p50 {np.median(it):.0f} max {it.max():.0f}")
+print("  K3 top problems (w,dir): cycles, iters, reads, sites, init cycles")
+for i in np.argsort(per)[::-1][:6]:
+    w, d = divmod(int(i), 2)
+    print(f"    ({w},{d}) {per[i]:.3g} {it[i]:.0f} {st[w, d, 6]} {st[w, d, 7]} {float(prof[w, d, 0]):.3g}")
