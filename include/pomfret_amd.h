@@ -410,6 +410,35 @@ int  pf_bam_fetch_windows(pf_bam_t *bam, const char *chrom, uint32_t n_windows, 
                           const uint32_t *win_end, uint32_t readback, int n_threads, pf_bam_records_t **out);
 void pf_bam_records_free(pf_bam_records_t *recs);
 
+/* The -u pre-pass reads of one contig (pre_haplotagging_read_in_one_ref,
+ * 1841-1898: sam_itr_querys over the whole contig, flags 4/256/2048
+ * skipped), in BAM order, as pf_haptag_reads takes them, plus qnames for
+ * its first-wins table.  A primary mapped record without MD:Z returns
+ * PF_ERR_ARG (the reference asserts, 1594-1595). */
+typedef struct pf_bam_reads {
+    pf_read_aln_batch_t reads;
+    const uint64_t *qname_off;     /* [n_reads+1] */
+    const char *qname;
+    uint64_t n_truncated;          /* 1 when the fetch stopped at a record htslib refuses */
+} pf_bam_reads_t;
+int  pf_bam_fetch_contig_reads(pf_bam_t *bam, const char *chrom, pf_bam_reads_t **out);
+void pf_bam_reads_free(pf_bam_reads_t *reads);
+
+/* -u known variants of one contig: insert_variant_from_vcf_line (1432-1543)
+ * on every complete line whose CHROM equals `contig` (the variants the
+ * reference collects for a contig before pre-haplotagging its reads,
+ * 1937-1941, 2069-2080): GT "a|b" with a, b in {0,1}; SNP -> X at POS-1;
+ * ref longer -> D at POS (len ref-alt, chars ref+1); alt longer -> I at
+ * POS-1 (len alt-ref, chars alt+1); equal-length non-SNPs skipped; haptag =
+ * GT[0].  Tokens split on runs of tabs as strtok_r does.  Returns PF_OK,
+ * PF_ERR_ARG for a #CHROM header without exactly 10 columns, PF_ERR_NOMEM,
+ * or -1 when the file cannot be read. */
+typedef struct pf_known_table {
+    pf_known_vars_t vars;
+} pf_known_table_t;
+int  pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t **out);
+void pf_known_table_free(pf_known_table_t *t);
+
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
  * the observed table. */
 double pf_fisher_exact(int n11, int n12, int n21, int n22,

@@ -15,7 +15,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from ._lib import PomfretError, _check, lib
-from .abi import AlnBatch, PfAlnBatch
+from .abi import AlnBatch, KnownVars, PfAlnBatch, PfKnownVars, ReadAlnBatch
 
 READBACK = 50_000  # blockjoin.c READBACK, the region margin of 1053-1054
 
@@ -23,6 +23,20 @@ READBACK = 50_000  # blockjoin.c READBACK, the region margin of 1053-1054
 class PfBamRecords(C.Structure):
     _fields_ = [("aln", PfAlnBatch), ("qname_off", C.c_void_p), ("qname", C.c_void_p),
                 ("hp_tag", C.c_void_p), ("n_truncated", C.c_uint64)]
+
+
+class PfReadAlnBatch(C.Structure):
+    _fields_ = [("n_reads", C.c_uint32)] + [(n, C.c_void_p) for n in (
+        "start", "end", "cigar_off", "cigar", "seq_off", "seq_len", "seq", "md_off", "md")]
+
+
+class PfBamReads(C.Structure):
+    _fields_ = [("reads", PfReadAlnBatch), ("qname_off", C.c_void_p), ("qname", C.c_void_p),
+                ("n_truncated", C.c_uint64)]
+
+
+class PfKnownTable(C.Structure):
+    _fields_ = [("vars", PfKnownVars)]
 
 
 _bound = False
@@ -47,6 +61,10 @@ def _bind():
     L.pf_bam_fetch_windows.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                        C.c_uint32, C.c_int, C.POINTER(C.POINTER(PfBamRecords))]
     L.pf_bam_records_free.argtypes = [C.POINTER(PfBamRecords)]
+    L.pf_bam_fetch_contig_reads.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.POINTER(PfBamReads))]
+    L.pf_bam_reads_free.argtypes = [C.POINTER(PfBamReads)]
+    L.pf_vcf_known_vars.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.POINTER(PfKnownTable))]
+    L.pf_known_table_free.argtypes = [C.POINTER(PfKnownTable)]
     _bound = True
     return L
 
@@ -146,3 +164,49 @@ class BamFile:
         finally:
             L.pf_bam_records_free(out)
         return batch, qnames, info
+
+    def fetch_contig_reads(self, chrom: str) -> Tuple[ReadAlnBatch, List[str], dict]:
+        """The -u pre-pass reads of one contig (pf_bam_fetch_contig_reads):
+        primary mapped records with CIGAR, SEQ and MD, in BAM order."""
+        if self.path is None:
+            raise PomfretError("index-only BamFile cannot fetch")
+        L = _bind()
+        out = C.POINTER(PfBamReads)()
+        _check(L.pf_bam_fetch_contig_reads(self.handle, chrom.encode(), C.byref(out)), "pf_bam_fetch_contig_reads")
+        try:
+            r = out.contents
+            a = r.reads
+            n = int(a.n_reads)
+            co = _arr(a.cigar_off, n + 1, np.uint64)
+            so = _arr(a.seq_off, n + 1, np.uint64)
+            mo = _arr(a.md_off, n + 1, np.uint64)
+            qo = _arr(r.qname_off, n + 1, np.uint64)
+            reads = ReadAlnBatch(start=_arr(a.start, n, np.uint32), end=_arr(a.end, n, np.uint32),
+                                 cigar_off=co, cigar=_arr(a.cigar, co[-1], np.uint32),
+                                 seq_off=so, seq_len=_arr(a.seq_len, n, np.uint32), seq=_arr(a.seq, so[-1], np.uint8),
+                                 md_off=mo, md=_arr(a.md, mo[-1], np.uint8))
+            qb = _arr(r.qname, qo[-1], np.uint8).tobytes()
+            qnames = [qb[qo[i]:qo[i + 1]].decode("ascii", "replace") for i in range(n)]
+            info = {"n_truncated": int(r.n_truncated)}
+        finally:
+            L.pf_bam_reads_free(out)
+        return reads, qnames, info
+
+
+def vcf_known_vars(vcf_path: str, contig: str) -> KnownVars:
+    """The -u known-variant table of one contig (pf_vcf_known_vars)."""
+    L = _bind()
+    out = C.POINTER(PfKnownTable)()
+    rc = L.pf_vcf_known_vars(vcf_path.encode(), contig.encode(), C.byref(out))
+    if rc == -1:
+        raise FileNotFoundError(vcf_path)
+    _check(rc, "pf_vcf_known_vars")
+    try:
+        v = out.contents.vars
+        n = int(v.n)
+        off = _arr(v.char_off, n + 1, np.uint64)
+        kv = KnownVars(pos=_arr(v.pos, n, np.uint32), len=_arr(v.len, n, np.uint32), op=_arr(v.op, n, np.uint8),
+                       haptag=_arr(v.haptag, n, np.uint8), char_off=off, chars=_arr(v.chars, off[-1], np.uint8))
+    finally:
+        L.pf_known_table_free(out)
+    return kv

@@ -384,8 +384,9 @@ static int vb_put(vbuf_t *v, const void *src, size_t n) {
     return 0;
 }
 
-enum { F_FLAG, F_MAPQ, F_POS, F_LQ, F_DE, F_HP, F_HPTAG, F_CIG, F_SEQ, F_MM, F_ML, F_QN,
+enum { F_FLAG, F_MAPQ, F_POS, F_LQ, F_DE, F_HP, F_HPTAG, F_END, F_CIG, F_SEQ, F_MM, F_ML, F_QN,
        F_CIGOFF, F_SEQOFF, F_MMOFF, F_MLOFF, F_QNOFF, NF };
+/* reads mode (-u pre-pass): F_POS start, F_END bam_endpos, F_LQ l_qseq, F_MM the MD text */
 
 typedef struct {
     vbuf_t f[NF];
@@ -521,6 +522,7 @@ typedef struct {
     size_t rec_cap;
     chunk_t *chunks;
     size_t chunk_cap;
+    int reads_mode;           /* pre_haplotagging_read_in_one_ref's records (1869-1871) */
 } fetcher_t;
 
 static int push_record(recbuf_t *rb, const rec_t *r, const uint8_t *cg, uint32_t ncg) {
@@ -580,6 +582,33 @@ static int push_record(recbuf_t *rb, const rec_t *r, const uint8_t *cg, uint32_t
     return 0;
 }
 
+/* -u pre-pass record: primary mapped only, MD:Z required (the reference
+ * asserts on it, 1594-1595) */
+static int push_read(recbuf_t *rb, const rec_t *r, const uint8_t *cg, uint32_t ncg, uint32_t end) {
+    int rc = 0;
+    const uint8_t *md = aux_find(r->aux, r->aux_end, "MD");
+    if (!md || md[2] != 'Z') return PF_ERR_ARG;
+    const char *mdz = (const char *)(md + 3);
+    const size_t mdl = strlen(mdz);
+    const uint32_t pos = (uint32_t)r->pos, lq = r->l_qseq;
+    uint64_t off;
+#define PUTV(fi, ptr, nb) do { if ((rc = vb_put(&rb->f[fi], (ptr), (nb)))) return rc; } while (0)
+    PUTV(F_POS, &pos, 4);
+    PUTV(F_END, &end, 4);
+    PUTV(F_LQ, &lq, 4);
+    off = rb->f[F_CIG].n / 4; PUTV(F_CIGOFF, &off, 8);
+    PUTV(F_CIG, cg, 4ull * ncg);
+    off = rb->f[F_SEQ].n; PUTV(F_SEQOFF, &off, 8);
+    PUTV(F_SEQ, r->seq, (lq + 1ull) / 2);
+    off = rb->f[F_MM].n; PUTV(F_MMOFF, &off, 8);
+    if (mdl) PUTV(F_MM, mdz, mdl);
+    off = rb->f[F_QN].n; PUTV(F_QNOFF, &off, 8);
+    PUTV(F_QN, r->qname, strnlen(r->qname, r->l_qname));
+#undef PUTV
+    rb->n_recs++;
+    return 0;
+}
+
 static int cmp_chunk(const void *a, const void *b) {
     const uint64_t x = ((const chunk_t *)a)->u, y = ((const chunk_t *)b)->u;
     return x < y ? -1 : x > y;
@@ -588,33 +617,24 @@ static int cmp_chunk(const void *a, const void *b) {
 static int fetch_region(fetcher_t *F, int64_t beg, int64_t end, recbuf_t *rb) {
     const ref_idx_t *ri = &F->b->idx[F->tid];
     if (end <= beg) return 0;
-    /* reg2bins(beg, end) of the SAM spec, end exclusive */
-    uint32_t bins[4681 + 4096 + 16];
-    uint32_t nb = 0;
-    {
-        const int64_t e = end - 1;
-        const int64_t b0 = beg;
-        bins[nb++] = 0;
-        static const int sh[5] = {26, 23, 20, 17, 14};
-        static const uint32_t base[5] = {1, 9, 73, 585, 4681};
-        for (int l = 0; l < 5; l++) {
-            int64_t k0 = base[l] + (b0 >> sh[l]), k1 = base[l] + (e >> sh[l]);
-            const int64_t kmax = (l == 4) ? 37449 : base[l + 1] - 1;
-            if (k1 > kmax) k1 = kmax;
-            for (int64_t k = k0; k <= k1 && nb < sizeof bins / sizeof bins[0]; k++) bins[nb++] = (uint32_t)k;
-        }
-    }
+    /* the bins reg2bins(beg, end) lists are exactly the index bins whose
+     * interval overlaps [beg, end): level l bin k covers
+     * [(k - first_l) << shift_l, (k - first_l + 1) << shift_l) */
     uint64_t min_off = 0;
     if (ri->n_intv) {
         const int64_t li = beg >> 14;
         min_off = li >= (int64_t)ri->n_intv ? ri->intv[ri->n_intv - 1] : ri->intv[li];
     }
     size_t nc = 0;
-    for (uint32_t i = 0; i < nb; i++) {
-        bin_t key;
-        key.bin = bins[i];
-        const bin_t *bb = (const bin_t *)bsearch(&key, ri->bins, ri->n_bin, sizeof(bin_t), cmp_bin);
-        if (!bb) continue;
+    static const uint32_t first[6] = {0, 1, 9, 73, 585, 4681};
+    static const int shift[6] = {29, 26, 23, 20, 17, 14};
+    for (uint32_t i = 0; i < ri->n_bin; i++) {
+        const bin_t *bb = &ri->bins[i];
+        if (bb->bin > 37449) continue;
+        int l = 5;
+        while (l > 0 && bb->bin < first[l]) l--;
+        const int64_t lo = (int64_t)(bb->bin - first[l]) << shift[l], hi = lo + ((int64_t)1 << shift[l]);
+        if (!(lo < end && hi > beg)) continue;
         for (uint32_t c = 0; c < bb->n; c++) {
             if (bb->c[c].v <= min_off) continue;
             if (nc == F->chunk_cap) {
@@ -672,7 +692,8 @@ static int fetch_region(fetcher_t *F, int64_t beg, int64_t end, recbuf_t *rb) {
             if (rlen == 0) rlen = 1;
             if (r.tid != F->tid || (int64_t)r.pos >= end) return 0;
             if ((int64_t)r.pos + (int64_t)rlen > beg) {
-                rc = push_record(rb, &r, cg, ncg);
+                if (!F->reads_mode) rc = push_record(rb, &r, cg, ncg);
+                else if (!(r.flag & (4 | 256 | 2048))) rc = push_read(rb, &r, cg, ncg, (uint32_t)(r.pos + rlen));
                 if (rc) return rc;
             }
         }
@@ -853,6 +874,65 @@ int pf_bam_fetch_windows(pf_bam_t *b, const char *chrom, uint32_t W, const uint3
     free(th);
     free(win_n);
     if (rc) { pf_bam_records_free(&o->pub); return rc; }
+    *out = &o->pub;
+    return PF_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* -u pre-pass reads of one contig */
+struct pf_bam_reads_own {
+    pf_bam_reads_t pub;
+    recbuf_t rb;
+};
+
+void pf_bam_reads_free(pf_bam_reads_t *r) {
+    if (!r) return;
+    struct pf_bam_reads_own *o = (struct pf_bam_reads_own *)r;
+    rb_free(&o->rb);
+    free(o);
+}
+
+int pf_bam_fetch_contig_reads(pf_bam_t *b, const char *chrom, pf_bam_reads_t **out) {
+    if (!b || !chrom || !out || !b->path) return PF_ERR_ARG;
+    *out = NULL;
+    const int32_t tid = pf_bam_tid(b, chrom);
+    if (tid < 0 || tid >= b->n_ref_idx) return PF_ERR_ARG;
+    struct pf_bam_reads_own *o = (struct pf_bam_reads_own *)calloc(1, sizeof *o);
+    if (!o) return PF_ERR_NOMEM;
+    fetcher_t F;
+    memset(&F, 0, sizeof F);
+    F.b = b;
+    F.tid = tid;
+    F.reads_mode = 1;
+    int rc = bgzf_open(&F.z, b->path);
+    /* sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX) */
+    if (!rc) rc = fetch_region(&F, 0, INT64_MAX, &o->rb);
+    if (F.z.f) fclose(F.z.f);
+    free(F.rec);
+    free(F.chunks);
+    recbuf_t *R = &o->rb;
+    static const int offs[4][2] = {{F_CIGOFF, F_CIG}, {F_SEQOFF, F_SEQ}, {F_MMOFF, F_MM}, {F_QNOFF, F_QN}};
+    for (int k = 0; k < 4 && !rc; k++) {
+        const uint64_t v = offs[k][1] == F_CIG ? R->f[F_CIG].n / 4 : R->f[offs[k][1]].n;
+        rc = vb_put(&R->f[offs[k][0]], &v, 8);
+    }
+    if (!rc && R->n_recs > 0xFFFFFFFFull) rc = PF_ERR_LIMIT;
+    if (rc) { pf_bam_reads_free(&o->pub); return rc; }
+    static const uint8_t dummy[8] = {0};
+    pf_read_aln_batch_t *a = &o->pub.reads;
+    a->n_reads = (uint32_t)R->n_recs;
+    a->start = R->f[F_POS].p ? (const uint32_t *)R->f[F_POS].p : (const uint32_t *)dummy;
+    a->end = R->f[F_END].p ? (const uint32_t *)R->f[F_END].p : (const uint32_t *)dummy;
+    a->seq_len = R->f[F_LQ].p ? (const uint32_t *)R->f[F_LQ].p : (const uint32_t *)dummy;
+    a->cigar_off = (const uint64_t *)R->f[F_CIGOFF].p;
+    a->cigar = R->f[F_CIG].p ? (const uint32_t *)R->f[F_CIG].p : (const uint32_t *)dummy;
+    a->seq_off = (const uint64_t *)R->f[F_SEQOFF].p;
+    a->seq = R->f[F_SEQ].p ? R->f[F_SEQ].p : dummy;
+    a->md_off = (const uint64_t *)R->f[F_MMOFF].p;
+    a->md = R->f[F_MM].p ? (const char *)R->f[F_MM].p : (const char *)dummy;
+    o->pub.qname_off = (const uint64_t *)R->f[F_QNOFF].p;
+    o->pub.qname = R->f[F_QN].p ? (const char *)R->f[F_QN].p : (const char *)dummy;
+    o->pub.n_truncated = R->truncated;
     *out = &o->pub;
     return PF_OK;
 }

@@ -346,3 +346,187 @@ int64_t pf_report_windows(uint32_t abs_start, const uint32_t *gap_start, const u
     }
     return (int64_t)n;
 }
+
+/* ------------------------------------------------------------------ */
+/* pf_vcf_known_vars: the -u known-variant table of one contig
+ * (insert_variant_from_vcf_line, :1432-1543).  Quirks kept: tokens are
+ * strtok_r's (runs of tabs collapse); POS is strtoul(POS) - 1 in uint32
+ * arithmetic; GT is the FORMAT-indexed sample field and must be exactly
+ * "a|b" with a, b in {0,1}; a deletion moves POS one base right and takes
+ * its chars from REF+1, an insertion its chars from ALT+1 (a multi-allelic
+ * ALT is one string here too, commas included); chars are seq_nt4 codes
+ * (A0 C1 G2 T3, else 4).  A sample column with fewer fields than FORMAT's
+ * GT index is skipped (the reference reads uninitialised values). */
+typedef struct {
+    u32v pos, len, hp;
+    uint8_t *op;
+    size_t n_op, m_op;
+    uint8_t *ch;
+    size_t n_ch, m_ch;
+    uint64_t *off;
+    size_t n_off, m_off;
+} known_acc_t;
+
+static int grow(void **p, size_t *m, size_t need, size_t es) {
+    if (need <= *m) return 0;
+    size_t nm = *m ? *m : 64;
+    while (nm < need) nm *= 2;
+    void *q = realloc(*p, nm * es);
+    if (!q) return -1;
+    *p = q;
+    *m = nm;
+    return 0;
+}
+
+static uint8_t nt4(char c) {
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+    }
+}
+
+static int known_line(known_acc_t *K, const char *contig, const char *s, size_t l) {
+    if (l > 0 && s[0] == '#') {
+        if (l > 1 && s[1] == '#') return 0;
+        int n = 0;                                   /* strtok token count */
+        for (size_t i = 0; i < l;) {
+            while (i < l && s[i] == '\t') i++;
+            if (i >= l) break;
+            n++;
+            while (i < l && s[i] != '\t') i++;
+        }
+        return n == 10 ? 0 : PF_ERR_ARG;
+    }
+    const char *tok[10];
+    size_t tl[10];
+    int nt = 0;
+    for (size_t i = 0; i < l && nt < 10;) {
+        while (i < l && s[i] == '\t') i++;
+        if (i >= l) break;
+        tok[nt] = s + i;
+        const size_t st = i;
+        while (i < l && s[i] != '\t') i++;
+        tl[nt] = i - st;
+        nt++;
+    }
+    if (nt < 1 || tl[0] != strlen(contig) || memcmp(tok[0], contig, tl[0]) != 0) return 0;
+    if (nt < 10) return 0;
+    uint32_t pos = parse_u32(tok[1], tl[1]) - 1u;
+    const size_t ref_l = tl[3], alt_l = tl[4];
+    /* GT index in FORMAT, then that field of the sample */
+    int i_gt = -1;
+    {
+        size_t start = 0;
+        int col = 0;
+        for (size_t i = 0; i <= tl[8]; i++) {
+            if (i == tl[8] || tok[8][i] == ':') {
+                if (i - start == 2 && tok[8][start] == 'G' && tok[8][start + 1] == 'T') { i_gt = col; break; }
+                if (i == tl[8]) break;
+                start = i + 1;
+                col++;
+            }
+        }
+    }
+    if (i_gt < 0) return 0;
+    size_t fs, fl;
+    if (field_of(tok[9], tl[9], i_gt, &fs, &fl)) return 0;
+    if (fl != 3) return 0;
+    const char *gt = tok[9] + fs;
+    if (gt[1] != '|' || (gt[0] != '0' && gt[0] != '1') || (gt[2] != '0' && gt[2] != '1')) return 0;
+    uint8_t op;
+    uint32_t op_l;
+    const char *vs;
+    if (ref_l == 1 && alt_l == 1) { op = PF_VAR_X; op_l = 1; vs = tok[4]; }
+    else if (ref_l == alt_l) return 0;                    /* unhandled variant case (:1528-1532) */
+    else if (ref_l > alt_l) { op = PF_VAR_D; op_l = (uint32_t)(ref_l - alt_l); pos += 1; vs = tok[3] + 1; }
+    else { op = PF_VAR_I; op_l = (uint32_t)(alt_l - ref_l); vs = tok[4] + 1; }
+    if (u32v_push(&K->pos, pos) || u32v_push(&K->len, op_l) || u32v_push(&K->hp, (uint32_t)(gt[0] - '0')))
+        return PF_ERR_NOMEM;
+    if (grow((void **)&K->op, &K->m_op, K->n_op + 1, 1)) return PF_ERR_NOMEM;
+    K->op[K->n_op++] = op;
+    if (grow((void **)&K->ch, &K->m_ch, K->n_ch + op_l, 1)) return PF_ERR_NOMEM;
+    for (uint32_t i = 0; i < op_l; i++) K->ch[K->n_ch++] = nt4(vs[i]);
+    if (grow((void **)&K->off, &K->m_off, K->n_off + 1, 8)) return PF_ERR_NOMEM;
+    K->off[K->n_off++] = K->n_ch;
+    return 0;
+}
+
+struct pf_known_own {
+    pf_known_table_t pub;
+    known_acc_t k;
+    uint8_t *hp8;
+    uint64_t *off;
+};
+
+void pf_known_table_free(pf_known_table_t *t) {
+    if (!t) return;
+    struct pf_known_own *o = (struct pf_known_own *)t;
+    free(o->k.pos.a);
+    free(o->k.len.a);
+    free(o->k.hp.a);
+    free(o->k.op);
+    free(o->k.ch);
+    free(o->k.off);
+    free(o->hp8);
+    free(o->off);
+    free(o);
+}
+
+int pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t **out) {
+    if (!vcf_path || !contig || !out) return PF_ERR_ARG;
+    *out = NULL;
+    gzFile fp = gzopen(vcf_path, "rb");
+    if (!fp) return -1;
+    struct pf_known_own *o = (struct pf_known_own *)calloc(1, sizeof *o);
+    size_t cap = 1 << 16, len = 0;
+    char *buf = (char *)malloc(cap);
+    int rc = (buf && o) ? 0 : PF_ERR_NOMEM;
+    while (!rc) {
+        if (len == cap) {
+            char *p = (char *)realloc(buf, cap * 2);
+            if (!p) { rc = PF_ERR_NOMEM; break; }
+            buf = p;
+            cap *= 2;
+        }
+        const int nr = gzread(fp, buf + len, (unsigned)(cap - len));
+        if (nr < 0) { rc = -1; break; }
+        if (nr == 0) break;                                /* a trailing partial line is dropped */
+        len += (size_t)nr;
+        size_t start = 0;
+        for (size_t i = 0; i < len && !rc; i++) {
+            if (buf[i] == '\n') {
+                rc = known_line(&o->k, contig, buf + start, i - start);
+                start = i + 1;
+            }
+        }
+        memmove(buf, buf + start, len - start);
+        len -= start;
+    }
+    gzclose(fp);
+    free(buf);
+    if (!rc) {
+        const size_t n = o->k.pos.n;
+        o->hp8 = (uint8_t *)malloc(n ? n : 1);
+        o->off = (uint64_t *)malloc((n + 1) * 8);
+        if (!o->hp8 || !o->off) rc = PF_ERR_NOMEM;
+        else {
+            o->off[0] = 0;
+            for (size_t i = 0; i < n; i++) { o->hp8[i] = (uint8_t)o->k.hp.a[i]; o->off[i + 1] = o->k.off[i]; }
+            static const uint8_t dummy[8] = {0};
+            pf_known_vars_t *v = &o->pub.vars;
+            v->n = (uint32_t)n;
+            v->pos = n ? o->k.pos.a : (const uint32_t *)dummy;
+            v->len = n ? o->k.len.a : (const uint32_t *)dummy;
+            v->op = n ? o->k.op : dummy;
+            v->haptag = o->hp8;
+            v->char_off = o->off;
+            v->chars = o->k.n_ch ? o->k.ch : dummy;
+        }
+    }
+    if (rc) { pf_known_table_free(o ? &o->pub : NULL); return rc; }
+    *out = &o->pub;
+    return PF_OK;
+}

@@ -10,6 +10,12 @@
     f2  pf_phase_blocks, pf_write_gtf / _tsv / _vcf
                               (lift_decisions ... output_modify_vcf, 4685-4717)
 
+With untagged=True (`--bam-is-untagged`, -u) every contig's reads are first
+haplotagged on the GPU from the VCF's phased variants (pf_vcf_known_vars +
+pf_bam_fetch_contig_reads + pf_haptag_reads, the pre-pass of 1841-1898 with
+its first-wins qname table) and those tags replace the BAM's HP in the
+loader (1114-1122: a qname missing from the table is unphased).
+
 The first-wins qname -> hp table of joined windows (4408-4423) is returned
 for callers that write tags.  The dropped-interval rescue of the VCF writer
 (recover_variant_phase_in_dropped_intervals, 2618-2694) needs a read pass
@@ -24,12 +30,12 @@ import numpy as np
 
 from ._lib import Blocks, Context, Gaps
 from .abi import Config, LoadConfig
-from .bam import READBACK, BamFile
+from .bam import READBACK, BamFile, vcf_known_vars
 
 
 def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Config,
                     lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8,
-                    ctx: Optional[Context] = None) -> Dict:
+                    ctx: Optional[Context] = None, untagged: bool = False) -> Dict:
     """Run methphase over every gap of vcf_path with the reads of bam_path.
     Writes out_prefix + .mp.gtf / .mp.tsv / .mp.vcf unless out_prefix is None.
     Returns dict(decision=int8[n_gaps], contigs=[...], qname_hp={qname: hp})."""
@@ -52,6 +58,9 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
                 ws = np.array([a for a, _ in g], np.uint32)
                 we = np.array([b for _, b in g], np.uint32)
                 aln, qn, _ = bam.fetch_windows(c["name"], ws, we, readback=READBACK, threads=threads)
+                if untagged:
+                    table = _pre_haplotag(ctx, bam, vcf_path, c["name"])
+                    aln.hp = np.array([table.get(q, 254) for q in qn], np.uint8)
                 db = ctx.upload_aln(cfg, aln, lcfg)
                 try:
                     out = db.run()
@@ -81,3 +90,20 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
         gaps.close()
         if own:
             ctx.close()
+
+
+def _pre_haplotag(ctx: Context, bam: BamFile, vcf_path: str, contig: str) -> Dict[str, int]:
+    """pre_haplotagging_read_in_one_ref (1841-1898) on the GPU: qname -> hp,
+    first wins."""
+    known = vcf_known_vars(vcf_path, contig)
+    table: Dict[str, int] = {}
+    if len(known.pos) == 0:
+        return table
+    reads, qn, _ = bam.fetch_contig_reads(contig)
+    if len(qn) == 0:
+        return table
+    hp = ctx.haptag_reads(known, reads)
+    for q, h in zip(qn, hp.tolist()):
+        if q not in table:
+            table[q] = int(h)
+    return table

@@ -45,7 +45,9 @@ def _encode_seq(s: np.ndarray) -> np.ndarray:
     return (nib[0::2] << 4 | nib[1::2]).astype(np.uint8)
 
 
-def make_u_batch(spec: USpec):
+def make_u_batch(spec: USpec, with_vcf: bool = False):
+    """known table, reads, true haplotype per read; with_vcf: also the VCF
+    records [(POS 1-based, REF, ALT, GT)] the known table is loaded from."""
     rng = np.random.default_rng(spec.seed)
     ref = BASES[rng.integers(0, 4, spec.ref_len)]
     # --- phased variants (0-based REF position p of the VCF record)
@@ -187,4 +189,8 @@ def make_u_batch(spec: USpec):
         seq_off=np.array(out["seq_off"]), seq_len=np.array(out["seq_len"]),
         seq=np.concatenate(out["seq"]), md_off=np.array(out["md_off"]),
         md=np.concatenate(out["md"]))
+    if with_vcf:
+        recs = [(p + 1, ra.decode(), aa.decode(), f"{1 if h == 0 else 0}|{0 if h == 0 else 1}")
+                for p, k, ra, aa, h in vars_]
+        return known, reads, np.array(out["hap"], np.uint8), recs
     return known, reads, np.array(out["hap"], np.uint8)

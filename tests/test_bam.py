@@ -162,3 +162,134 @@ def test_errors(tmp_path):
     bad.write_bytes(b"not a bam")
     with pytest.raises(Exception):
         BamFile(str(bad), p + ".bai")
+
+
+# ---------------------------------------------------------------- -u ingest
+def _py_known(lines, contig):
+    """insert_variant_from_vcf_line (blockjoin.c:1432-1543) restated for the
+    test: strtok tokens, GT 'a|b' with a, b in {0,1}, SNP/DEL/INS rules."""
+    nt4 = {c: i for i, c in enumerate("ACGT")}
+    nt4.update({c.lower(): i for c, i in list(nt4.items())})
+    out = []
+    for s in lines:
+        if s.startswith("#"):
+            continue
+        tok = [t for t in s.split("\t") if t]
+        if not tok or tok[0] != contig or len(tok) < 10:
+            continue
+        pos = (int("".join(ch for ch in tok[1] if ch.isdigit()) or 0) - 1) & 0xFFFFFFFF
+        ref, alt = tok[3], tok[4]
+        fmt = tok[8].split(":")
+        if "GT" not in fmt:
+            continue
+        smp = tok[9].split(":")
+        i = fmt.index("GT")
+        if i >= len(smp) or len(smp[i]) != 3:
+            continue
+        gt = smp[i]
+        if gt[1] != "|" or gt[0] not in "01" or gt[2] not in "01":
+            continue
+        if len(ref) == 1 and len(alt) == 1:
+            op, ln, ch = 1, 1, alt
+        elif len(ref) == len(alt):
+            continue
+        elif len(ref) > len(alt):
+            op, ln, ch = 3, len(ref) - len(alt), ref[1:]
+            pos += 1
+        else:
+            op, ln, ch = 2, len(alt) - len(ref), alt[1:]
+        out.append((pos, ln, op, int(gt[0]), [nt4.get(c, 4) for c in ch[:ln]]))
+    return out
+
+
+def _kv_list(kv):
+    return [(int(kv.pos[i]), int(kv.len[i]), int(kv.op[i]), int(kv.haptag[i]),
+             kv.chars[kv.char_off[i]:kv.char_off[i + 1]].tolist()) for i in range(len(kv.pos))]
+
+
+def test_vcf_known_vars_rules(tmp_path):
+    from pomfret_amd.bam import vcf_known_vars
+    body = [
+        "c1\t100\t.\tA\tG\t50\tPASS\t.\tGT:PS\t0|1:100",          # SNP, haptag 0
+        "c1\t200\t.\tACGT\tA\t50\tPASS\t.\tGT\t1|0",              # DEL 3 at POS
+        "c1\t300\t.\tC\tCTTA\t50\tPASS\t.\tPS:GT\t7:0|1",         # INS 3, GT second
+        "c1\t400\t.\tAC\tGT\t50\tPASS\t.\tGT\t0|1",               # MNP: skipped
+        "c1\t500\t.\tA\tG\t50\tPASS\t.\tGT\t0/1",                 # unphased
+        "c1\t600\t.\tA\tG\t50\tPASS\t.\tGT\t.|1",
+        "c1\t700\t.\tA\tC,G\t50\tPASS\t.\tGT\t1|0",               # multi-allelic: 'INS' ",G"
+        "c2\t800\t.\tA\tG\t50\tPASS\t.\tGT\t0|1",                 # other contig
+        "c1\t\t900\t.\tT\tA\t50\tPASS\t.\tGT\t1|0",               # empty token collapses
+        "c1\t950\t.\tA\tG\t50\tPASS\t.\tGT:PS\t0|1",              # sample without PS: fine for GT
+        "c1\t990\t.\tA\tG\t50\tPASS\t.\tPS:GT\t12",               # sample shorter than GT index
+    ]
+    hdr = ["##fileformat=VCFv4.2", "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS"]
+    p = tmp_path / "k.vcf"
+    p.write_text("\n".join(hdr + body) + "\n" + "c1\t999\t.\tA\tG\t50\tPASS\t.\tGT\t0|1")  # no final newline
+    got = _kv_list(vcf_known_vars(str(p), "c1"))
+    assert got == _py_known(body, "c1")
+    assert [g[:3] for g in got] == [(99, 1, 1), (200, 3, 3), (299, 3, 2), (699, 2, 2), (899, 1, 1), (949, 1, 1)]
+    assert got[1][4] == [1, 2, 3] and got[2][4] == [3, 3, 0] and got[3][4] == [4, 2]
+    assert _kv_list(vcf_known_vars(str(p), "c2")) == _py_known(body, "c2")
+    bad = tmp_path / "b.vcf"
+    bad.write_text("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\n")
+    with pytest.raises(Exception):
+        vcf_known_vars(str(bad), "c1")
+
+
+def test_vcf_known_vars_example_fixture():
+    """the reference's example/variants.vcf.gz (bgzipped): the C loader and
+    the restatement agree on every contig it names"""
+    import gzip
+    from pomfret_amd.bam import vcf_known_vars
+    path = os.path.join(HERE, "golden", "example", "variants.vcf.gz")
+    lines = gzip.decompress(open(path, "rb").read()).decode().split("\n")[:-1]
+    contigs = sorted({l.split("\t")[0] for l in lines if l and not l.startswith("#")})
+    assert contigs
+    n = 0
+    for c in contigs:
+        got = _kv_list(vcf_known_vars(path, c))
+        assert got == _py_known(lines, c), c
+        n += len(got)
+    assert n > 0
+
+
+def _u_bam(tmp_path, spec):
+    from pomfret_amd.synth_u import make_u_batch
+    from _bamio import write_phased_vcf  # noqa: F401
+    known, reads, hap, vrecs = make_u_batch(spec, with_vcf=True)
+    recs = []
+    for i in range(len(reads.start)):
+        cig = [int(x) for x in reads.cigar[reads.cigar_off[i]:reads.cigar_off[i + 1]]]
+        lq = int(reads.seq_len[i])
+        seq = bytes(reads.seq[reads.seq_off[i]:reads.seq_off[i] + (lq + 1) // 2])
+        md = bytes(reads.md[reads.md_off[i]:reads.md_off[i + 1]]).decode()
+        recs.append(Rec(0, int(reads.start[i]), f"u{i}", cigar=cig, seq=seq, l_seq=lq, aux=aux_Z("MD", md)))
+    order = sorted(range(len(recs)), key=lambda i: (recs[i].pos, i))
+    extra = [Rec(0, recs[order[0]].pos, "sec", flag=256, cigar=recs[order[0]].cigar, seq=recs[order[0]].seq,
+                 l_seq=recs[order[0]].l_seq, aux=aux_Z("MD", "0"))]
+    bam = str(tmp_path / "u.bam")
+    write_bam(bam, [("chrU", 10_000_000)], extra + [recs[i] for i in order])
+    vcf = tmp_path / "u.vcf"
+    hdr = ["##fileformat=VCFv4.2", "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS"]
+    vcf.write_text("\n".join(hdr + [f"chrU\t{p}\t.\t{r}\t{a}\t50\tPASS\t.\tGT\t{g}" for p, r, a, g in vrecs]) + "\n")
+    return known, reads, order, bam, str(vcf)
+
+
+def test_u_ingest_round_trip(tmp_path):
+    import oracle
+    from pomfret_amd.bam import BamFile, vcf_known_vars
+    from pomfret_amd.synth_u import USpec
+    known, reads, order, bam, vcf = _u_bam(tmp_path, USpec(n_reads=120, ref_len=200_000))
+    kv = vcf_known_vars(vcf, "chrU")
+    assert _kv_list(kv) == _kv_list(known)
+    with BamFile(bam) as b:
+        got, qn, info = b.fetch_contig_reads("chrU")
+    assert info["n_truncated"] == 0
+    assert qn == [f"u{i}" for i in order]                 # the flag-256 record is skipped
+    o = np.asarray(order)
+    assert np.array_equal(got.start, reads.start[o]) and np.array_equal(got.end, reads.end[o])
+    for k, i in enumerate(order):
+        assert np.array_equal(got.md[got.md_off[k]:got.md_off[k + 1]], reads.md[reads.md_off[i]:reads.md_off[i + 1]])
+    hp_f = oracle.haptag_reads(kv, got)
+    hp_o = oracle.haptag_reads(known, reads)
+    assert np.array_equal(hp_f, hp_o[o])

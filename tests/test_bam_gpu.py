@@ -61,3 +61,18 @@ def test_pipeline_end_to_end(oracle_lib, gpu_ctx, tmp_path):
     assert (res["decision"] >= 0).any()
     for ext in (".mp.gtf", ".mp.tsv", ".mp.vcf"):
         assert os.path.getsize(str(tmp_path / "out") + ext) > 0
+
+
+def test_u_ingest_gpu(oracle_lib, gpu_ctx, tmp_path):
+    """-u pre-pass from files: VCF known variants + BAM contig reads -> K4."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_bam import _u_bam
+    from pomfret_amd.bam import BamFile, vcf_known_vars
+    from pomfret_amd.synth_u import USpec
+    known, reads, order, bam, vcf = _u_bam(tmp_path, USpec(n_reads=300, ref_len=300_000))
+    kv = vcf_known_vars(vcf, "chrU")
+    with BamFile(bam) as b:
+        got, qn, _ = b.fetch_contig_reads("chrU")
+    hp = gpu_ctx.haptag_reads(kv, got)
+    assert np.array_equal(hp, oracle_lib.haptag_reads(kv, got))
