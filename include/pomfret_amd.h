@@ -424,6 +424,36 @@ typedef struct pf_bam_reads {
 int  pf_bam_fetch_contig_reads(pf_bam_t *bam, const char *chrom, pf_bam_reads_t **out);
 void pf_bam_reads_free(pf_bam_reads_t *reads);
 
+/* qname -> tag table across the boundary (first entry of a qname wins). */
+typedef struct pf_qname_tags {
+    uint32_t n;
+    const uint64_t *off;           /* [n+1] into names */
+    const char *names;
+    const uint8_t *hp;
+} pf_qname_tags_t;
+
+/* VCF-writer rescue map of one contig: recover_variant_phase_in_dropped_
+ * intervals (2618-2694) / recover_variant_phase_in_one_interval (2475-2616).
+ * For each dropped interval [s, e] in order: the known positions in
+ * [s-1, e+1); the records of region "chrom:(s-1)-(e+1)" whose qname is in
+ * `methphased` (st->qname2haptag) and whose raw tag (`raw` table when given
+ * -- the -u table -- else the HP tag) is not unphased; their variant
+ * positions (CIGAR I, MD mismatches and closed ^-runs) voted by methphased
+ * tag 0/1 at each known position: more hap0 -> REF on hap1, more hap1 ->
+ * REF on hap0, else 254.  A known position sorted last among the interval's
+ * entries gets no vote (the loop stops at n-1).  Positions ascending, last
+ * write wins.  PF_ERR_ARG for an MD-less selected record (the reference
+ * asserts) or an invalid MD character (it exits). */
+typedef struct pf_rescue_map {
+    uint32_t n;
+    const uint32_t *pos;
+    const uint8_t *hap_of_ref;
+} pf_rescue_map_t;
+int  pf_rescue_dropped(pf_bam_t *bam, const char *chrom, uint32_t n_drop, const uint32_t *drop_start,
+                       const uint32_t *drop_end, const pf_known_vars_t *known, const pf_qname_tags_t *methphased,
+                       const pf_qname_tags_t *raw, pf_rescue_map_t **out);
+void pf_rescue_map_free(pf_rescue_map_t *map);
+
 /* -u known variants of one contig: insert_variant_from_vcf_line (1432-1543)
  * on every complete line whose CHROM equals `contig` (the variants the
  * reference collects for a contig before pre-haplotagging its reads,

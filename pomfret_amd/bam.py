@@ -10,7 +10,7 @@ table of blockjoin.c:4408-4423).  Host code; no GPU involved.
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -39,6 +39,14 @@ class PfKnownTable(C.Structure):
     _fields_ = [("vars", PfKnownVars)]
 
 
+class PfQnameTags(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("off", C.c_void_p), ("names", C.c_void_p), ("hp", C.c_void_p)]
+
+
+class PfRescueMap(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("pos", C.c_void_p), ("hap_of_ref", C.c_void_p)]
+
+
 _bound = False
 
 
@@ -65,6 +73,10 @@ def _bind():
     L.pf_bam_reads_free.argtypes = [C.POINTER(PfBamReads)]
     L.pf_vcf_known_vars.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.POINTER(PfKnownTable))]
     L.pf_known_table_free.argtypes = [C.POINTER(PfKnownTable)]
+    L.pf_rescue_dropped.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                    C.POINTER(PfKnownVars), C.POINTER(PfQnameTags), C.POINTER(PfQnameTags),
+                                    C.POINTER(C.POINTER(PfRescueMap))]
+    L.pf_rescue_map_free.argtypes = [C.POINTER(PfRescueMap)]
     _bound = True
     return L
 
@@ -210,3 +222,40 @@ def vcf_known_vars(vcf_path: str, contig: str) -> KnownVars:
     finally:
         L.pf_known_table_free(out)
     return kv
+
+
+def _qname_tags(table: Dict[str, int]):
+    """(PfQnameTags, keepalive) of a qname -> hp dict (insertion order)."""
+    names = [q.encode() for q in table]
+    off = np.zeros(len(names) + 1, np.uint64)
+    if names:
+        off[1:] = np.cumsum([len(q) for q in names])
+    buf = np.frombuffer(b"".join(names) or b"\0", np.uint8).copy()
+    hp = np.asarray([int(v) & 0xFF for v in table.values()] or [0], np.uint8)
+    t = PfQnameTags(len(names), off.ctypes.data, buf.ctypes.data, hp.ctypes.data)
+    return t, (off, buf, hp)
+
+
+def rescue_dropped(bam: BamFile, contig: str, dropped, known: KnownVars, methphased: Dict[str, int],
+                   raw: Optional[Dict[str, int]] = None) -> Dict[int, int]:
+    """pf_rescue_dropped: {0-based pos: hap_of_ref} of one contig's dropped
+    intervals [(s, e), ...] for the VCF writer (Blocks.write_vcf rescue)."""
+    L = _bind()
+    ds = np.ascontiguousarray([a for a, _ in dropped] or [0], np.uint32)
+    de = np.ascontiguousarray([b for _, b in dropped] or [0], np.uint32)
+    tm, km = _qname_tags(methphased)
+    tr, kr = _qname_tags(raw) if raw is not None else (None, None)
+    kc = known.to_c()
+    out = C.POINTER(PfRescueMap)()
+    _check(L.pf_rescue_dropped(bam.handle, contig.encode(), len(dropped), ds.ctypes.data, de.ctypes.data,
+                               C.byref(kc), C.byref(tm), C.byref(tr) if tr is not None else None, C.byref(out)),
+           "pf_rescue_dropped")
+    try:
+        m = out.contents
+        n = int(m.n)
+        pos = _arr(m.pos, n, np.uint32)
+        hap = _arr(m.hap_of_ref, n, np.uint8)
+    finally:
+        L.pf_rescue_map_free(out)
+    del km, kr
+    return {int(p): int(h) for p, h in zip(pos, hap)}

@@ -522,7 +522,8 @@ typedef struct {
     size_t rec_cap;
     chunk_t *chunks;
     size_t chunk_cap;
-    int reads_mode;           /* pre_haplotagging_read_in_one_ref's records (1869-1871) */
+    int reads_mode;           /* 1: pre_haplotagging_read_in_one_ref's records (1869-1871);
+                                 2: every record (the rescue pass, 2510-2545) */
 } fetcher_t;
 
 static int push_record(recbuf_t *rb, const rec_t *r, const uint8_t *cg, uint32_t ncg) {
@@ -600,6 +601,37 @@ static int push_read(recbuf_t *rb, const rec_t *r, const uint8_t *cg, uint32_t n
     PUTV(F_CIG, cg, 4ull * ncg);
     off = rb->f[F_SEQ].n; PUTV(F_SEQOFF, &off, 8);
     PUTV(F_SEQ, r->seq, (lq + 1ull) / 2);
+    off = rb->f[F_MM].n; PUTV(F_MMOFF, &off, 8);
+    if (mdl) PUTV(F_MM, mdz, mdl);
+    off = rb->f[F_QN].n; PUTV(F_QNOFF, &off, 8);
+    PUTV(F_QN, r->qname, strnlen(r->qname, r->l_qname));
+#undef PUTV
+    rb->n_recs++;
+    return 0;
+}
+
+/* rescue pass record: pos, get_hp_from_aln, CIGAR, MD (F_FLAG = 1 when present), qname */
+static int push_any(recbuf_t *rb, const rec_t *r, const uint8_t *cg, uint32_t ncg) {
+    int rc = 0;
+    const uint8_t *md = aux_find(r->aux, r->aux_end, "MD");
+    const uint16_t has_md = (md && md[2] == 'Z') ? 1 : 0;
+    const char *mdz = has_md ? (const char *)(md + 3) : "";
+    const size_t mdl = strlen(mdz);
+    uint8_t hp = 254;
+    const uint8_t *t = aux_find(r->aux, r->aux_end, "HP");
+    if (t) {
+        int64_t v = 0;
+        if (!aux_int(t, &v)) v = 0;
+        hp = (v >= 1 && v <= 255) ? (uint8_t)(v - 1) : 254;
+    }
+    const uint32_t pos = (uint32_t)r->pos;
+    uint64_t off;
+#define PUTV(fi, ptr, nb) do { if ((rc = vb_put(&rb->f[fi], (ptr), (nb)))) return rc; } while (0)
+    PUTV(F_POS, &pos, 4);
+    PUTV(F_FLAG, &has_md, 2);
+    PUTV(F_HP, &hp, 1);
+    off = rb->f[F_CIG].n / 4; PUTV(F_CIGOFF, &off, 8);
+    PUTV(F_CIG, cg, 4ull * ncg);
     off = rb->f[F_MM].n; PUTV(F_MMOFF, &off, 8);
     if (mdl) PUTV(F_MM, mdz, mdl);
     off = rb->f[F_QN].n; PUTV(F_QNOFF, &off, 8);
@@ -693,6 +725,7 @@ static int fetch_region(fetcher_t *F, int64_t beg, int64_t end, recbuf_t *rb) {
             if (r.tid != F->tid || (int64_t)r.pos >= end) return 0;
             if ((int64_t)r.pos + (int64_t)rlen > beg) {
                 if (!F->reads_mode) rc = push_record(rb, &r, cg, ncg);
+                else if (F->reads_mode == 2) rc = push_any(rb, &r, cg, ncg);
                 else if (!(r.flag & (4 | 256 | 2048))) rc = push_read(rb, &r, cg, ncg, (uint32_t)(r.pos + rlen));
                 if (rc) return rc;
             }
@@ -933,6 +966,262 @@ int pf_bam_fetch_contig_reads(pf_bam_t *b, const char *chrom, pf_bam_reads_t **o
     o->pub.qname_off = (const uint64_t *)R->f[F_QNOFF].p;
     o->pub.qname = R->f[F_QN].p ? (const char *)R->f[F_QN].p : (const char *)dummy;
     o->pub.n_truncated = R->truncated;
+    *out = &o->pub;
+    return PF_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* recover_variant_phase_in_dropped_intervals (2618-2694) and
+ * recover_variant_phase_in_one_interval (2475-2616) for one contig */
+
+typedef struct {                      /* open-addressing qname -> hp table */
+    uint64_t *key_off;                /* index into the caller's arrays, or ~0 */
+    uint32_t mask;
+    const pf_qname_tags_t *t;
+} qtab_t;
+
+static uint64_t fnv(const char *s, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; i++) { h ^= (uint8_t)s[i]; h *= 1099511628211ull; }
+    return h;
+}
+
+static int qtab_build(qtab_t *q, const pf_qname_tags_t *t) {
+    q->t = t;
+    uint32_t cap = 16;
+    while (cap < 2ull * t->n + 16) cap <<= 1;
+    q->mask = cap - 1;
+    q->key_off = (uint64_t *)malloc(cap * sizeof(uint64_t));
+    if (!q->key_off) return PF_ERR_NOMEM;
+    for (uint32_t i = 0; i < cap; i++) q->key_off[i] = ~0ull;
+    for (uint32_t i = 0; i < t->n; i++) {       /* first wins */
+        const char *nm = t->names + t->off[i];
+        const size_t l = t->off[i + 1] - t->off[i];
+        uint32_t h = (uint32_t)fnv(nm, l) & q->mask;
+        for (;;) {
+            const uint64_t k = q->key_off[h];
+            if (k == ~0ull) { q->key_off[h] = i; break; }
+            if (t->off[k + 1] - t->off[k] == l && memcmp(t->names + t->off[k], nm, l) == 0) break;
+            h = (h + 1) & q->mask;
+        }
+    }
+    return 0;
+}
+
+static int qtab_get(const qtab_t *q, const char *nm, size_t l) {   /* hp or -1 */
+    const pf_qname_tags_t *t = q->t;
+    uint32_t h = (uint32_t)fnv(nm, l) & q->mask;
+    for (;;) {
+        const uint64_t k = q->key_off[h];
+        if (k == ~0ull) return -1;
+        if (t->off[k + 1] - t->off[k] == l && memcmp(t->names + t->off[k], nm, l) == 0) return t->hp[k];
+        h = (h + 1) & q->mask;
+    }
+}
+
+static int md_type(uint8_t c) {       /* md_op_table (blockjoin.c:94-): digit 0, '^' 1, bases 2, else 4 */
+    if (c >= '0' && c <= '9') return 0;
+    if (c == '^') return 1;
+    switch (c) {
+    case 'A': case 'T': case 'C': case 'G': case 'a': case 't': case 'c': case 'g':
+    case 'U': case 'u': case 'N': case 'n': return 2;
+    default: return 4;
+    }
+}
+
+typedef struct { uint64_t *a; size_t n, m; } u64v_t;
+static int u64_push(u64v_t *v, uint64_t x) {
+    if (v->n == v->m) {
+        const size_t nm = v->m ? 2 * v->m : 256;
+        uint64_t *p = (uint64_t *)realloc(v->a, nm * 8);
+        if (!p) return PF_ERR_NOMEM;
+        v->a = p;
+        v->m = nm;
+    }
+    v->a[v->n++] = x;
+    return 0;
+}
+static int cmp_u64(const void *a, const void *b) {
+    const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
+/* the positions parse_variants_for_one_read (1545-1691) gives a record's
+ * variants: CIGAR I at the current reference position, MD mismatches and
+ * ^-deletion runs closed by a number; each pushed as pos<<33 | 1<<32 | hap
+ * (the vote needs only the methphased tag).  Returns PF_ERR_ARG for an MD
+ * character outside md_op_table (the reference exits, 1621-1624, or asserts
+ * on the first character, 1616). */
+static int read_var_positions(uint32_t pos0, const uint32_t *cig, uint32_t ncig, const char *md, size_t mdl,
+                              uint32_t hap, u64v_t *out) {
+    uint32_t ref = pos0;
+    int rc;
+    for (uint32_t i = 0; i < ncig; i++) {
+        const uint32_t op = cig[i] & 15u, l = cig[i] >> 4;
+        if (op == 3 || op == 0 || op == 7 || op == 8 || op == 2) ref += l;
+        else if (op == 1) { if ((rc = u64_push(out, ((uint64_t)ref << 33) | (1ull << 32) | hap))) return rc; }
+    }
+    /* md_s[0] is asserted < 4 (1616): an empty MD or a bad first character aborts */
+    if (mdl == 0 || md_type((uint8_t)md[0]) == 4) return PF_ERR_ARG;
+    ref = pos0;
+    int prev = md_type((uint8_t)md[0]);
+    size_t prev_i = 0;
+    if (prev == 2) {
+        if ((rc = u64_push(out, ((uint64_t)ref << 33) | (1ull << 32) | hap))) return rc;
+        ref++;
+        prev = -1;
+    }
+    for (size_t i = 1; i < mdl; i++) {
+        const int t = md_type((uint8_t)md[i]);
+        if (t == 4) return PF_ERR_ARG;
+        if (t == prev) continue;
+        if (prev == 0) {
+            uint32_t l = 0;                  /* natoi of the digit run */
+            for (size_t k = prev_i; k < i; k++) l = l * 10u + (uint32_t)(md[k] - '0');
+            ref += l;
+        } else if (prev == 1) {
+            if (t == 0) {
+                if ((rc = u64_push(out, ((uint64_t)ref << 33) | (1ull << 32) | hap))) return rc;
+                ref += (uint32_t)(i - prev_i - 1);
+                prev = t;
+                prev_i = i;
+            }
+            continue;
+        }
+        if (t == 2) {
+            if ((rc = u64_push(out, ((uint64_t)ref << 33) | (1ull << 32) | hap))) return rc;
+            ref++;
+            prev = -1;
+            prev_i = i;
+        } else {
+            prev = t;
+            prev_i = i;
+        }
+    }
+    return 0;
+}
+
+struct pf_rescue_own {
+    pf_rescue_map_t pub;
+    uint32_t *pos;
+    uint8_t *hap;
+};
+
+void pf_rescue_map_free(pf_rescue_map_t *m) {
+    if (!m) return;
+    struct pf_rescue_own *o = (struct pf_rescue_own *)m;
+    free(o->pos);
+    free(o->hap);
+    free(o);
+}
+
+int pf_rescue_dropped(pf_bam_t *b, const char *chrom, uint32_t n_drop, const uint32_t *drop_start,
+                      const uint32_t *drop_end, const pf_known_vars_t *known, const pf_qname_tags_t *methphased,
+                      const pf_qname_tags_t *raw, pf_rescue_map_t **out) {
+    if (!b || !chrom || !known || !methphased || !out || (n_drop && (!drop_start || !drop_end)) || !b->path)
+        return PF_ERR_ARG;
+    *out = NULL;
+    const int32_t tid = pf_bam_tid(b, chrom);
+    qtab_t qm = {0}, qr = {0};
+    u64v_t pb = {0}, res = {0};
+    fetcher_t F;
+    memset(&F, 0, sizeof F);
+    F.b = b;
+    F.tid = tid;
+    F.reads_mode = 2;
+    int rc = qtab_build(&qm, methphased);
+    if (!rc && raw) rc = qtab_build(&qr, raw);
+    if (!rc && tid >= 0 && tid < b->n_ref_idx) rc = bgzf_open(&F.z, b->path);
+    uint32_t prev_i = 0;
+    uint64_t seq = 0;
+    for (uint32_t k = 0; k < n_drop && !rc; k++) {
+        const uint32_t start = drop_start[k] - 1u, end = drop_end[k] + 1u;
+        pb.n = 0;
+        for (uint32_t i = prev_i; i < known->n; i++) {          /* 2653-2663 */
+            const uint32_t p = known->pos[i];
+            if (p >= start && p < end && (rc = u64_push(&pb, (uint64_t)p << 33))) break;
+            if (p >= end) { prev_i = i; break; }
+        }
+        if (rc) break;
+        /* "%s:%d-%d" of (start, end): htslib's 0-based [start-1, end) */
+        const int64_t b1 = (int32_t)start, e1 = (int32_t)end;
+        const int64_t beg = b1 > 0 ? b1 - 1 : 0;
+        recbuf_t rb;
+        memset(&rb, 0, sizeof rb);
+        if (tid >= 0 && tid < b->n_ref_idx) rc = fetch_region(&F, beg, e1, &rb);
+        {                                                              /* closing offsets */
+            const uint64_t vq = rb.f[F_QN].n, vc = rb.f[F_CIG].n / 4, vm = rb.f[F_MM].n;
+            if (!rc) rc = vb_put(&rb.f[F_QNOFF], &vq, 8);
+            if (!rc) rc = vb_put(&rb.f[F_CIGOFF], &vc, 8);
+            if (!rc) rc = vb_put(&rb.f[F_MMOFF], &vm, 8);
+        }
+        const size_t nk = pb.n;
+        for (uint64_t r = 0; r < rb.n_recs && !rc; r++) {
+            const uint64_t *qo = (const uint64_t *)rb.f[F_QNOFF].p;
+            const char *qn = (const char *)rb.f[F_QN].p + qo[r];
+            const size_t ql = (size_t)(qo[r + 1] - qo[r]);
+            const int hm = qtab_get(&qm, qn, ql);
+            if (hm < 0) continue;
+            int hr;
+            if (raw) { hr = qtab_get(&qr, qn, ql); if (hr < 0) continue; }
+            else hr = ((const uint8_t *)rb.f[F_HP].p)[r];
+            if (hr == 254) continue;
+            if (!((const uint16_t *)rb.f[F_FLAG].p)[r]) { rc = PF_ERR_ARG; break; }   /* assert(tagd), 1596 */
+            const uint64_t *co = (const uint64_t *)rb.f[F_CIGOFF].p, *mo = (const uint64_t *)rb.f[F_MMOFF].p;
+            rc = read_var_positions(((const uint32_t *)rb.f[F_POS].p)[r],
+                                    (const uint32_t *)rb.f[F_CIG].p + co[r], (uint32_t)(co[r + 1] - co[r]),
+                                    (const char *)rb.f[F_MM].p + mo[r], (size_t)(mo[r + 1] - mo[r]),
+                                    (uint32_t)hm & 0xFFu, &pb);
+        }
+        rb_free(&rb);
+        if (rc || nk == 0) continue;                                   /* pb.n == 0: goto done */
+        qsort(pb.a, pb.n, 8, cmp_u64);
+        /* for (i = 0; i < pb.n-1;): a known position sorted last is never visited */
+        for (size_t i = 0; i + 1 < pb.n && !rc;) {
+            if (pb.a[i] & (1ull << 32)) { i++; continue; }
+            const uint32_t rp = (uint32_t)(pb.a[i] >> 33);
+            uint32_t c[2] = {0, 0};
+            size_t j;
+            for (j = i + 1; j < pb.n; j++) {
+                if (!(pb.a[j] & (1ull << 32))) break;
+                if ((uint32_t)(pb.a[j] >> 33) != rp) break;
+                const uint32_t h = (uint32_t)pb.a[j] & 0xFFu;
+                if (h < 2) c[h]++;
+            }
+            const uint32_t hap = c[0] > c[1] ? 1u : c[1] > c[0] ? 0u : 254u;
+            rc = u64_push(&res, ((uint64_t)rp << 40) | (seq++ << 8) | hap);
+            i = j;
+        }
+    }
+    if (F.z.f) fclose(F.z.f);
+    free(F.rec);
+    free(F.chunks);
+    free(qm.key_off);
+    free(qr.key_off);
+    free(pb.a);
+    struct pf_rescue_own *o = NULL;
+    if (!rc) {
+        /* the hash keeps the last write per position */
+        qsort(res.a, res.n, 8, cmp_u64);
+        o = (struct pf_rescue_own *)calloc(1, sizeof *o);
+        if (o) { o->pos = (uint32_t *)malloc((res.n ? res.n : 1) * 4); o->hap = (uint8_t *)malloc(res.n ? res.n : 1); }
+        if (!o || !o->pos || !o->hap) rc = PF_ERR_NOMEM;
+        else {
+            uint32_t n = 0;
+            for (size_t i = 0; i < res.n; i++) {
+                const uint32_t p = (uint32_t)(res.a[i] >> 40);
+                if (i + 1 < res.n && (uint32_t)(res.a[i + 1] >> 40) == p) continue;
+                o->pos[n] = p;
+                o->hap[n] = (uint8_t)(res.a[i] & 0xFFu);
+                n++;
+            }
+            o->pub.n = n;
+            o->pub.pos = o->pos;
+            o->pub.hap_of_ref = o->hap;
+        }
+    }
+    free(res.a);
+    if (rc) { pf_rescue_map_free(o ? &o->pub : NULL); return rc; }
     *out = &o->pub;
     return PF_OK;
 }

@@ -16,11 +16,11 @@ pf_bam_fetch_contig_reads + pf_haptag_reads, the pre-pass of 1841-1898 with
 its first-wins qname table) and those tags replace the BAM's HP in the
 loader (1114-1122: a qname missing from the table is unphased).
 
-The first-wins qname -> hp table of joined windows (4408-4423) is returned
-for callers that write tags.  The dropped-interval rescue of the VCF writer
-(recover_variant_phase_in_dropped_intervals, 2618-2694) needs a read pass
-this pipeline does not make yet, so dropped intervals keep their sites as
-the VCF writer leaves them without a rescue map.
+The first-wins qname -> hp table of joined windows (4408-4423, merged across
+contigs in contig order, 4572-4590) is returned for callers that write tags,
+and drives the VCF writer's rescue of sites in dropped intervals
+(recover_variant_phase_in_dropped_intervals, 2618-2694: pf_rescue_dropped
+over the BAM).
 """
 from __future__ import annotations
 
@@ -30,14 +30,15 @@ import numpy as np
 
 from ._lib import Blocks, Context, Gaps
 from .abi import Config, LoadConfig
-from .bam import READBACK, BamFile, vcf_known_vars
+from .bam import READBACK, BamFile, rescue_dropped, vcf_known_vars
 
 
 def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Config,
                     lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8,
-                    ctx: Optional[Context] = None, untagged: bool = False) -> Dict:
+                    ctx: Optional[Context] = None, untagged: bool = False, tsv: bool = False) -> Dict:
     """Run methphase over every gap of vcf_path with the reads of bam_path.
-    Writes out_prefix + .mp.gtf / .mp.tsv / .mp.vcf unless out_prefix is None.
+    Writes out_prefix + .mp.gtf / .mp.vcf (and .mp.tsv with tsv=True, the
+    reference's --tsv) unless out_prefix is None.
     Returns dict(decision=int8[n_gaps], contigs=[...], qname_hp={qname: hp})."""
     lcfg = lcfg or LoadConfig()
     gaps = Gaps(vcf_path, READBACK)
@@ -45,9 +46,15 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
     ctx = ctx or Context(device)
     decision = []
     qname_hp: Dict[str, int] = {}
+    raw_hp: Dict[str, int] = {}
     contigs = gaps.contigs()
     try:
         with BamFile(bam_path) as bam:
+            if untagged:                         # the pre-pass tags every contig first (2069-2080)
+                for c in contigs:
+                    if bam.tid(c["name"]) >= 0:
+                        for q, h in _pre_haplotag(ctx, bam, vcf_path, c["name"]).items():
+                            raw_hp.setdefault(q, h)
             for c in contigs:
                 g = c["gaps"]
                 if not g:
@@ -59,8 +66,7 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
                 we = np.array([b for _, b in g], np.uint32)
                 aln, qn, _ = bam.fetch_windows(c["name"], ws, we, readback=READBACK, threads=threads)
                 if untagged:
-                    table = _pre_haplotag(ctx, bam, vcf_path, c["name"])
-                    aln.hp = np.array([table.get(q, 254) for q in qn], np.uint8)
+                    aln.hp = np.array([raw_hp.get(q, 254) for q in qn], np.uint8)
                 db = ctx.upload_aln(cfg, aln, lcfg)
                 try:
                     out = db.run()
@@ -81,8 +87,17 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
         blocks = Blocks(gaps, np.asarray(decision, np.int8))
         if out_prefix is not None:
             blocks.write_gtf(out_prefix + ".mp.gtf")
-            blocks.write_tsv(out_prefix + ".mp.tsv")
-            blocks.write_vcf(vcf_path, out_prefix + ".mp.vcf")
+            if tsv:
+                blocks.write_tsv(out_prefix + ".mp.tsv")
+            rescue = []
+            with BamFile(bam_path) as bam:
+                for c in contigs:
+                    if not c["dropped"] or bam.tid(c["name"]) < 0:
+                        rescue.append({})
+                        continue
+                    rescue.append(rescue_dropped(bam, c["name"], c["dropped"], vcf_known_vars(vcf_path, c["name"]),
+                                                 qname_hp, raw_hp if untagged else None))
+            blocks.write_vcf(vcf_path, out_prefix + ".mp.vcf", rescue=rescue)
         res = dict(decision=np.asarray(decision, np.int8), contigs=blocks.contigs(), qname_hp=qname_hp)
         blocks.close()
         return res

@@ -293,3 +293,138 @@ def test_u_ingest_round_trip(tmp_path):
     hp_f = oracle.haptag_reads(kv, got)
     hp_o = oracle.haptag_reads(known, reads)
     assert np.array_equal(hp_f, hp_o[o])
+
+
+# ------------------------------------------------- f2 rescue of dropped sites
+def _py_read_var_pos(pos0, cigar, md):
+    """parse_variants_for_one_read (blockjoin.c:1545-1691), positions only."""
+    out, ref = [], pos0
+    for c in cigar:
+        op, l = c & 15, c >> 4
+        if op in (0, 2, 3, 7, 8):
+            ref += l
+        elif op == 1:
+            out.append(ref)
+
+    def ty(ch):
+        if ch.isdigit():
+            return 0
+        if ch == "^":
+            return 1
+        return 2 if ch in "ATCGatcgUuNn" else 4
+    ref, prev, pi = pos0, ty(md[0]), 0
+    if prev == 2:
+        out.append(ref)
+        ref += 1
+        prev = -1
+    for i in range(1, len(md)):
+        t = ty(md[i])
+        if t == prev:
+            continue
+        if prev == 0:
+            ref += int(md[pi:i])
+        elif prev == 1:
+            if t == 0:
+                out.append(ref)
+                ref += i - pi - 1
+                prev, pi = t, i
+            continue
+        if t == 2:
+            out.append(ref)
+            ref += 1
+            prev, pi = -1, i
+        else:
+            prev, pi = t, i
+    return out
+
+
+def _py_rescue(recs, known_pos, dropped, meth, raw=None):
+    res, prev_i = {}, 0
+    for s, e in dropped:
+        start, end = (s - 1) & 0xFFFFFFFF, (e + 1) & 0xFFFFFFFF
+        poss = []
+        for i in range(prev_i, len(known_pos)):
+            p = known_pos[i]
+            if start <= p < end:
+                poss.append(p)
+            if p >= end:
+                prev_i = i
+                break
+        if not poss:
+            continue
+        pb = [(p << 33) for p in poss]
+        for j in expected_fetch(recs, 0, start, end - 0, 0):
+            r = recs[j]
+            hm = meth.get(r.qname)
+            if hm is None:
+                continue
+            if raw is not None:
+                hr = raw.get(r.qname)
+                if hr is None:
+                    continue
+            else:
+                hr = 254
+                if r.aux.startswith(b"HPi"):
+                    v = int.from_bytes(r.aux[3:7], "little", signed=True)
+                    hr = v - 1 if 1 <= v <= 255 else 254
+            if hr == 254:
+                continue
+            md = r.aux[r.aux.index(b"MDZ") + 3:].split(b"\0")[0].decode()
+            pb += [(p << 33) | (1 << 32) | hm for p in _py_read_var_pos(r.pos, r.cigar, md)]
+        pb.sort()
+        i = 0
+        while i < len(pb) - 1:
+            if pb[i] & (1 << 32):
+                i += 1
+                continue
+            rp, c, j = pb[i] >> 33, [0, 0], i + 1
+            while j < len(pb) and (pb[j] & (1 << 32)) and (pb[j] >> 33) == rp:
+                h = pb[j] & 0xFF
+                if h < 2:
+                    c[h] += 1
+                j += 1
+            res[rp] = 1 if c[0] > c[1] else 0 if c[1] > c[0] else 254
+            i = j
+    return res
+
+
+def test_rescue_dropped_matches_restatement(tmp_path):
+    from pomfret_amd.abi import KnownVars
+    from pomfret_amd.bam import BamFile, rescue_dropped
+    rng = np.random.default_rng(4)
+    seq = bytes([0x11] * 300)
+    kpos = sorted(set(int(x) for x in rng.integers(1000, 20000, 60)))
+    recs = []
+    meth = {}
+    for i in range(140):
+        p = int(rng.integers(500, 19000))
+        # a read of 600 bases with a mismatch / deletion / insertion at a known site or nearby
+        k = kpos[int(rng.integers(0, len(kpos)))]
+        off = k - p
+        if not (10 <= off < 550):
+            off = int(rng.integers(10, 500))
+        kind = int(rng.integers(0, 3))
+        if kind == 0:
+            cig, md = [(600 << 4) | 0], f"{off}A{600 - off - 1}"
+        elif kind == 1:
+            cig, md = [(off << 4) | 0, (2 << 4) | 2, ((600 - off) << 4) | 0], f"{off}^AC{600 - off}"
+        else:
+            cig, md = [(off << 4) | 0, (3 << 4) | 1, ((597 - off) << 4) | 0], f"{597}"
+        hp_tag = int(rng.integers(0, 3))                 # 0: HP absent -> unphased raw
+        aux = (aux_i("HP", hp_tag) if hp_tag else b"") + aux_Z("MD", md)
+        recs.append(Rec(0, p, f"q{i}", cigar=cig, seq=seq, l_seq=600, aux=aux))
+        if rng.random() < 0.8:
+            meth[f"q{i}"] = int(rng.integers(0, 3))
+    recs.sort(key=lambda r: r.pos)
+    p = str(tmp_path / "r.bam")
+    write_bam(p, [("c", 100_000)], recs)
+    kn = KnownVars(pos=np.array(kpos), len=np.ones(len(kpos)), op=np.ones(len(kpos)),
+                   haptag=np.zeros(len(kpos)), char_off=np.arange(len(kpos) + 1), chars=np.zeros(len(kpos)))
+    dropped = [(1200, 4000), (6000, 9000), (12000, 18000)]
+    with BamFile(p) as b:
+        got = rescue_dropped(b, "c", dropped, kn, meth)
+        raw = {f"q{i}": int(rng.integers(0, 2)) for i in range(0, 140, 2)}
+        got_raw = rescue_dropped(b, "c", dropped, kn, meth, raw)
+    exp = _py_rescue(recs, kpos, dropped, meth)
+    assert got == exp and len(got) > 5 and any(v != 254 for v in got.values())
+    assert got_raw == _py_rescue(recs, kpos, dropped, meth, raw)

@@ -53,7 +53,7 @@ def test_pipeline_end_to_end(oracle_lib, gpu_ctx, tmp_path):
     vcf = str(tmp_path / "p.vcf")
     write_phased_vcf(vcf, "chrS", wins)
     cfg = Config.from_coverage(30, given=False)
-    res = methphase_files(bam, vcf, str(tmp_path / "out"), cfg, ctx=gpu_ctx)
+    res = methphase_files(bam, vcf, str(tmp_path / "out"), cfg, ctx=gpu_ctx, tsv=True)
     with BamFile(bam) as b:
         got, qn, _ = b.fetch_windows("chrS", aln.win_start, aln.win_end)
     ref = oracle_lib.methphase_aln(cfg, LoadConfig(), got, n_threads=8)
