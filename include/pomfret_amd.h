@@ -424,6 +424,11 @@ typedef struct pf_bam_reads {
 int  pf_bam_fetch_contig_reads(pf_bam_t *bam, const char *chrom, pf_bam_reads_t **out);
 void pf_bam_reads_free(pf_bam_reads_t *reads);
 
+/* Per-contig read coverage estimate for runs without -c
+ * (estimate_read_coverage_dirtyfast, 951-1040): covs[tid] for
+ * tid < pf_bam_n_targets (n >= that).  A full sequential pass over the BAM. */
+int  pf_bam_estimate_coverage(pf_bam_t *bam, int32_t *covs, int32_t n);
+
 /* qname -> tag table across the boundary (first entry of a qname wins). */
 typedef struct pf_qname_tags {
     uint32_t n;

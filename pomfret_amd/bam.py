@@ -77,6 +77,7 @@ def _bind():
                                     C.POINTER(PfKnownVars), C.POINTER(PfQnameTags), C.POINTER(PfQnameTags),
                                     C.POINTER(C.POINTER(PfRescueMap))]
     L.pf_rescue_map_free.argtypes = [C.POINTER(PfRescueMap)]
+    L.pf_bam_estimate_coverage.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     _bound = True
     return L
 
@@ -176,6 +177,13 @@ class BamFile:
         finally:
             L.pf_bam_records_free(out)
         return batch, qnames, info
+
+    def estimate_coverage(self) -> List[int]:
+        """estimate_read_coverage_dirtyfast (blockjoin.c:951-1040): per contig."""
+        L = _bind()
+        cov = np.zeros(max(self.n_targets, 1), np.int32)
+        _check(L.pf_bam_estimate_coverage(self.handle, cov.ctypes.data, cov.size), "pf_bam_estimate_coverage")
+        return cov[:self.n_targets].tolist()
 
     def fetch_contig_reads(self, chrom: str) -> Tuple[ReadAlnBatch, List[str], dict]:
         """The -u pre-pass reads of one contig (pf_bam_fetch_contig_reads):

@@ -1225,3 +1225,102 @@ int pf_rescue_dropped(pf_bam_t *b, const char *chrom, uint32_t n_drop, const uin
     *out = &o->pub;
     return PF_OK;
 }
+
+/* ------------------------------------------------------------------ */
+/* estimate_read_coverage_dirtyfast (951-1040): every record from the first
+ * one (region "."), per contig bins of 5000 bp (target_len / 5000 of them):
+ * a record passing flag 4/256/2048, mapq >= 5, l_qseq >= 15000 and
+ * de <= 0.1 adds 1 to the bins of start, start + 5000, ... < bam_endpos;
+ * a contig's estimate is the integer mean over its bins, taken when the next
+ * contig starts and, for the last one, only when the last record read has a
+ * tid >= 0 (refID is reassigned by unplaced reads).  Counts that fall past
+ * the last whole bin are dropped (the reference writes past buf.n: they are
+ * never summed).  Contigs without reads stay 0. */
+int pf_bam_estimate_coverage(pf_bam_t *b, int32_t *covs, int32_t n) {
+    if (!b || !b->path || !covs || n < b->n_ref) return PF_ERR_ARG;
+    for (int32_t i = 0; i < n; i++) covs[i] = 0;
+    bgzf_t *z = (bgzf_t *)malloc(sizeof(bgzf_t));
+    if (!z) return PF_ERR_NOMEM;
+    int rc = bgzf_open(z, b->path);
+    if (rc) { free(z); return rc; }
+    rc = bgzf_seek(z, b->data_off) ? PF_ERR_ARG : 0;
+    uint8_t *rec = NULL;
+    size_t cap = 0;
+    uint64_t *bins = NULL;
+    size_t nb = 0, mb = 0;
+    int32_t prev = -1, refid = -1;
+    const int mod = 5000;
+    while (!rc) {
+        uint8_t w[4];
+        const int64_t g = bgzf_read(z, w, 4);
+        if (g == 0) break;
+        if (g != 4) { rc = PF_ERR_ARG; break; }
+        const uint32_t bs = rd32(w);
+        if (bs < 32 || bs > (1u << 30)) { rc = PF_ERR_ARG; break; }
+        if (bs > cap) {
+            uint8_t *np = (uint8_t *)realloc(rec, bs);
+            if (!np) { rc = PF_ERR_NOMEM; break; }
+            rec = np;
+            cap = bs;
+        }
+        if (bgzf_read(z, rec, bs) != (int64_t)bs) { rc = PF_ERR_ARG; break; }
+        rec_t r;
+        if (rec_decode(rec, bs, &r)) { rc = PF_ERR_ARG; break; }
+        const uint8_t *cg = r.cigar;
+        uint32_t ncg = r.n_cigar;
+        if (ncg > 0 && r.tid >= 0 && r.pos >= 0 && (rd32(cg) & 15u) == 4u && (rd32(cg) >> 4) == r.l_qseq) {
+            const uint8_t *t = aux_find(r.aux, r.aux_end, "CG");
+            if (t && t[2] == 'B' && (t[3] == 'I' || t[3] == 'i')) {
+                const uint32_t nn = rd32(t + 4);
+                if (nn >= r.n_cigar && nn < (1u << 29)) { cg = t + 8; ncg = nn; }
+            }
+        }
+        uint64_t qlen = 0;
+        uint64_t rlen = cigar_rlen(cg, ncg, &qlen);
+        if (ncg > 0 && r.l_qseq > 0 && !(r.flag & 4) && qlen != r.l_qseq) break;   /* sam_itr_next < 0 */
+        refid = r.tid;
+        if (refid < 0) continue;
+        if (refid > b->n_ref) continue;                 /* the reference's check is '>' */
+        if (refid == b->n_ref) continue;                /* (target_len[n_targets] is out of range) */
+        if (refid != prev) {
+            if (prev >= 0) {
+                uint64_t tot = 0;
+                for (size_t i = 0; i < nb; i++) tot += bins[i];
+                covs[prev] = nb ? (int32_t)(tot / nb) : 0;
+            }
+            nb = b->lens[refid] / (uint32_t)mod;
+            if (nb > mb) {
+                uint64_t *np = (uint64_t *)realloc(bins, nb * 8);
+                if (!np) { rc = PF_ERR_NOMEM; break; }
+                bins = np;
+                mb = nb;
+            }
+            for (size_t i = 0; i < nb; i++) bins[i] = 0;
+            prev = refid;
+        }
+        if ((r.flag & 4) || (r.flag & 256) || (r.flag & 2048)) continue;
+        if (r.mapq < 5) continue;
+        float de = -1.f;
+        const uint8_t *t = aux_find(r.aux, r.aux_end, "de");
+        if (t) de = (float)aux_f(t);
+        if (r.l_qseq < 15000) continue;
+        if ((double)de > 0.1) continue;
+        if ((r.flag & 4) || ncg == 0) rlen = 0;
+        if (rlen == 0) rlen = 1;
+        const uint32_t st = (uint32_t)r.pos, en = (uint32_t)(r.pos + rlen);
+        for (int64_t i = (int32_t)st; i < (int64_t)en; i += mod) {
+            const uint64_t k = (uint64_t)i / (uint64_t)mod;
+            if (i >= 0 && k < nb) bins[k]++;
+        }
+    }
+    if (!rc && refid >= 0 && refid < b->n_ref && prev >= 0) {
+        uint64_t tot = 0;
+        for (size_t i = 0; i < nb; i++) tot += bins[i];
+        covs[refid] = nb ? (int32_t)(tot / nb) : 0;
+    }
+    free(bins);
+    free(rec);
+    fclose(z->f);
+    free(z);
+    return rc;
+}

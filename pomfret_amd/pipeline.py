@@ -33,12 +33,14 @@ from .abi import Config, LoadConfig
 from .bam import READBACK, BamFile, rescue_dropped, vcf_known_vars
 
 
-def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Config,
+def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],
                     lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8,
                     ctx: Optional[Context] = None, untagged: bool = False, tsv: bool = False) -> Dict:
     """Run methphase over every gap of vcf_path with the reads of bam_path.
     Writes out_prefix + .mp.gtf / .mp.vcf (and .mp.tsv with tsv=True, the
     reference's --tsv) unless out_prefix is None.
+    cfg None: no -c, the per-contig parameters come from the BAM's coverage
+    estimate (estimate_read_coverage_dirtyfast + 4358-4390).
     Returns dict(decision=int8[n_gaps], contigs=[...], qname_hp={qname: hp})."""
     lcfg = lcfg or LoadConfig()
     gaps = Gaps(vcf_path, READBACK)
@@ -50,6 +52,7 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
     contigs = gaps.contigs()
     try:
         with BamFile(bam_path) as bam:
+            est = bam.estimate_coverage() if cfg is None else None
             if untagged:                         # the pre-pass tags every contig first (2069-2080)
                 for c in contigs:
                     if bam.tid(c["name"]) >= 0:
@@ -67,7 +70,8 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
                 aln, qn, _ = bam.fetch_windows(c["name"], ws, we, readback=READBACK, threads=threads)
                 if untagged:
                     aln.hp = np.array([raw_hp.get(q, 254) for q in qn], np.uint8)
-                db = ctx.upload_aln(cfg, aln, lcfg)
+                ccfg = cfg if cfg is not None else Config.from_coverage(est[bam.tid(c["name"])], given=False)
+                db = ctx.upload_aln(ccfg, aln, lcfg)
                 try:
                     out = db.run()
                     rec_of_read = db.read_recs()

@@ -428,3 +428,67 @@ def test_rescue_dropped_matches_restatement(tmp_path):
     exp = _py_rescue(recs, kpos, dropped, meth)
     assert got == exp and len(got) > 5 and any(v != 254 for v in got.values())
     assert got_raw == _py_rescue(recs, kpos, dropped, meth, raw)
+
+
+def _py_cov(recs, lens):
+    """estimate_read_coverage_dirtyfast (blockjoin.c:951-1040) restated."""
+    covs = [0] * len(lens)
+    prev, refid, bins = -1, -1, []
+    for r in recs:
+        refid = r.tid
+        if refid < 0:
+            continue
+        if refid != prev:
+            if prev >= 0:
+                covs[prev] = sum(bins) // len(bins) if bins else 0
+            bins = [0] * (lens[refid] // 5000)
+            prev = refid
+        if (r.flag & (4 | 256 | 2048)) or r.mapq < 5 or r.l_seq < 15000:
+            continue
+        de = -1.0
+        if b"def" in r.aux:
+            import struct
+            k = r.aux.index(b"def")
+            de = struct.unpack("<f", r.aux[k + 3:k + 7])[0]
+        if de > 0.1:
+            continue
+        i, e = r.pos, endpos(r.pos, r.cigar, r.flag)
+        while i < e:
+            if i // 5000 < len(bins):
+                bins[i // 5000] += 1
+            i += 5000
+    if refid >= 0:
+        covs[refid] = sum(bins) // len(bins) if bins else 0
+    return covs
+
+
+def test_estimate_coverage(tmp_path):
+    from pomfret_amd.bam import BamFile
+    rng = np.random.default_rng(8)
+    lens = [300_000, 123_456, 60_000]
+    recs = []
+    for tid in range(3):
+        for _ in range(150 if tid < 2 else 60):
+            L = int(rng.integers(5_000, 40_000))
+            p = int(rng.integers(0, max(1, lens[tid] - 1000)))
+            flag = int(rng.choice([0, 0, 0, 16, 256, 2048]))
+            aux = aux_f("de", float(rng.choice([0.01, 0.05, 0.2]))) if rng.random() < 0.7 else b""
+            recs.append(Rec(tid, p, f"t{tid}_{len(recs)}", flag=flag, mapq=int(rng.integers(0, 60)),
+                            cigar=[(L << 4) | 0], seq=b"", l_seq=L, aux=aux))
+    recs.sort(key=lambda r: (r.tid, r.pos))
+    seqfix = []
+    for r in recs:                                  # SEQ bytes sized to l_seq
+        r.seq = bytes((r.l_seq + 1) // 2)
+        seqfix.append(r)
+    p1 = str(tmp_path / "cov.bam")
+    write_bam(p1, [("a", lens[0]), ("b", lens[1]), ("c", lens[2])], seqfix)
+    with BamFile(p1) as b:
+        got = b.estimate_coverage()
+    assert got == _py_cov(seqfix, lens) and got[0] > 0
+    # an unplaced read at the end reassigns refID: the last contig keeps 0
+    un = Rec(-1, -1, "unplaced", flag=4, cigar=[], seq=bytes(50), l_seq=100)
+    p2 = str(tmp_path / "cov2.bam")
+    write_bam(p2, [("a", lens[0]), ("b", lens[1]), ("c", lens[2])], seqfix + [un])
+    with BamFile(p2) as b:
+        got2 = b.estimate_coverage()
+    assert got2[:2] == got[:2] and got[2] > 0 and got2[2] == 0
