@@ -42,7 +42,9 @@ typedef struct {
     int ulen, upos;
     uint64_t caddr;          /* compressed address of the block in ubuf */
     uint64_t next;           /* compressed address of the following block */
+    uint64_t fpos;           /* file position after the last fread */
     int eof;
+    char *iobuf;
 } bgzf_t;
 
 static uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
@@ -51,15 +53,21 @@ static uint64_t rd64(const uint8_t *p) { return (uint64_t)rd32(p) | ((uint64_t)r
 
 /* load the block at compressed address addr; 0 ok, 1 clean EOF, <0 error */
 static int bgzf_load(bgzf_t *z, uint64_t addr) {
-    if (fseeko(z->f, (off_t)addr, SEEK_SET) != 0) return -1;
+    if (addr != z->fpos) {                    /* sequential blocks keep the stdio buffer */
+        if (fseeko(z->f, (off_t)addr, SEEK_SET) != 0) return -1;
+        z->fpos = addr;
+    }
     uint8_t *h = z->cbuf;
     size_t got = fread(h, 1, 18, z->f);
+    z->fpos += got;
     if (got == 0) { z->caddr = addr; z->next = addr; z->ulen = z->upos = 0; z->eof = 1; return 1; }
     if (got < 12 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return -2;
     const uint32_t xlen = rd16(h + 10);
     if (xlen < 6 || 12 + xlen > sizeof z->cbuf) return -2;
     if (got < 12 + (size_t)xlen) {
-        if (fread(h + got, 1, 12 + xlen - got, z->f) != 12 + xlen - got) return -2;
+        const size_t k = fread(h + got, 1, 12 + xlen - got, z->f);
+        z->fpos += k;
+        if (k != 12 + xlen - got) return -2;
         got = 12 + xlen;
     }
     uint32_t bsize = 0;
@@ -70,7 +78,11 @@ static int bgzf_load(bgzf_t *z, uint64_t addr) {
         x += 4 + slen;
     }
     if (bsize < 12 + xlen + 8 || bsize > 65536) return -2;
-    if (got < bsize && fread(h + got, 1, bsize - got, z->f) != bsize - got) return -2;
+    if (got < bsize) {
+        const size_t k = fread(h + got, 1, bsize - got, z->f);
+        z->fpos += k;
+        if (k != bsize - got) return -2;
+    }
     const uint32_t isize = rd32(h + bsize - 4), crc = rd32(h + bsize - 8);
     if (isize > 65536) return -2;
     z_stream zs;
@@ -131,12 +143,27 @@ static int64_t bgzf_read(bgzf_t *z, void *dst, size_t n) {
     return (int64_t)n;
 }
 
+static void bgzf_close(bgzf_t *z) {
+    if (z->f) fclose(z->f);
+    z->f = NULL;
+    free(z->iobuf);
+    z->iobuf = NULL;
+}
+
 static int bgzf_open(bgzf_t *z, const char *path) {
     memset(z, 0, sizeof *z);
     z->f = fopen(path, "rb");
     if (!z->f) return -1;
+    z->iobuf = (char *)malloc(1 << 20);
+    if (z->iobuf) setvbuf(z->f, z->iobuf, _IOFBF, 1 << 20);
     const int rc = bgzf_load(z, 0);
-    if (rc != 0) { fclose(z->f); z->f = NULL; return rc == 1 ? PF_ERR_ARG : rc == -1 ? -1 : PF_ERR_ARG; }
+    if (rc != 0) {
+        fclose(z->f);
+        z->f = NULL;
+        free(z->iobuf);
+        z->iobuf = NULL;
+        return rc == 1 ? PF_ERR_ARG : rc == -1 ? -1 : PF_ERR_ARG;
+    }
     return 0;
 }
 
@@ -291,7 +318,7 @@ static int load_header(pf_bam_t *b) {
     b->data_off = bgzf_tell(z);
     rc = PF_OK;
 out:
-    fclose(z->f);
+    bgzf_close(z);
     free(z);
     return rc;
 }
@@ -761,7 +788,7 @@ static void *fetch_job(void *arg) {
         rc = fetch_region(&F, beg, end, j->out);
         j->win_n[w] = j->out->n_recs - n0;
     }
-    if (F.z.f) fclose(F.z.f);
+    bgzf_close(&F.z);
     free(F.rec);
     free(F.chunks);
     j->rc = rc;
@@ -940,7 +967,7 @@ int pf_bam_fetch_contig_reads(pf_bam_t *b, const char *chrom, pf_bam_reads_t **o
     int rc = bgzf_open(&F.z, b->path);
     /* sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX) */
     if (!rc) rc = fetch_region(&F, 0, INT64_MAX, &o->rb);
-    if (F.z.f) fclose(F.z.f);
+    bgzf_close(&F.z);
     free(F.rec);
     free(F.chunks);
     recbuf_t *R = &o->rb;
@@ -1193,7 +1220,7 @@ int pf_rescue_dropped(pf_bam_t *b, const char *chrom, uint32_t n_drop, const uin
             i = j;
         }
     }
-    if (F.z.f) fclose(F.z.f);
+    bgzf_close(&F.z);
     free(F.rec);
     free(F.chunks);
     free(qm.key_off);
@@ -1320,7 +1347,7 @@ int pf_bam_estimate_coverage(pf_bam_t *b, int32_t *covs, int32_t n) {
     }
     free(bins);
     free(rec);
-    fclose(z->f);
+    bgzf_close(z);
     free(z);
     return rc;
 }
