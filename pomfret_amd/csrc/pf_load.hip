@@ -342,6 +342,19 @@ DEV uint64_t zero_nibbles(uint64_t x) {             // bit 4i set iff nibble i o
     a = (a | (a >> 2)) & 0x1111111111111111ull;
     return ~a & 0x1111111111111111ull;
 }
+// index of the k-th (k < popcount) set nibble flag (bits 4i) of m, branch-free
+DEV uint32_t sel_nibble(uint64_t m, uint32_t k) {
+    uint32_t lo = (uint32_t)m, base = 0;
+    uint32_t c = (uint32_t)__builtin_popcount(lo);
+    if (k >= c) { k -= c; lo = (uint32_t)(m >> 32); base = 8; }
+    c = (uint32_t)__builtin_popcount(lo & 0xFFFFu);
+    if (k >= c) { k -= c; lo >>= 16; base += 4; }
+    c = (uint32_t)__builtin_popcount(lo & 0xFFu);
+    if (k >= c) { k -= c; lo >>= 8; base += 2; }
+    c = (uint32_t)__builtin_popcount(lo & 0xFu);
+    if (k >= c) base += 1;
+    return base;
+}
 DEV uint64_t valid_nibbles(uint32_t nv) { return nv >= 16 ? 0x1111111111111111ull : ((1ull << (4 * nv)) - 1) & 0x1111111111111111ull; }
 
 template <typename TP>
@@ -428,9 +441,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                 if (k >= c0) { k -= c0; hw = 1; }
                 const uint32_t w = b * BW + i * RW + 2 * Lw + hw;
                 const uint64_t xw = nibswap(sw[w]);
-                uint64_t m = zero_nibbles(xw ^ pat);
-                for (uint32_t s2 = k; s2 > 0; s2--) m &= m - 1;
-                const uint32_t bi = (uint32_t)__builtin_ctzll(m) >> 2;
+                const uint32_t bi = sel_nibble(zero_nibbles(xw ^ pat), k);
                 const uint32_t p = w * 16 + bi;
                 uint32_t key = 0xFFFFFFFFu;
                 if (p > 0 && p < len - 1) {
