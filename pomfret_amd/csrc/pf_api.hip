@@ -14,6 +14,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <thread>
 #include <vector>
 #include "pf_device.h"
 #include "pf_load.h"
@@ -43,6 +44,8 @@ struct pf_ctx {
     int have_times;
     float haptag_ms;          /* last pf_haptag_reads kernel time */
     int have_haptag;
+    void *pin = nullptr;      /* pinned staging for large uploads (grown on demand) */
+    size_t pin_cap = 0;
 };
 
 struct pf_dbatch {
@@ -168,6 +171,7 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     (void)hipStreamSynchronize(c->stream);
     for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
+    if (c->pin) (void)hipHostFree(c->pin);
     delete c;
 }
 
@@ -186,6 +190,69 @@ static int dev_put(pf_dbatch *b, T **p, const T *src, size_t n) {
     int rc = dev_alloc(b, p, n);
     if (rc) return rc;
     if (n) HIPCHK(hipMemcpy(*p, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return PF_OK;
+}
+
+// host-side parallel loop over [0, n): f(lo, hi) per thread (up to 16)
+template <typename F>
+static void par_for(uint64_t n, F f) {
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min(nt, 16u));
+    if (n < 4096 || nt == 1) { f(0, n); return; }
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) th.emplace_back(f, n * t / nt, n * (t + 1) / nt);
+    f(0, n / nt);
+    for (auto &x : th) x.join();
+}
+
+// large host -> device copies go through the context's pinned buffer
+// (parallel memcpy in, one DMA out) in 256 MiB pieces
+static int pinned_put(pf_ctx *c, void *dst, const void *src, size_t bytes) {
+    const size_t piece = (size_t)256 << 20;
+    if (bytes < ((size_t)4 << 20)) {
+        HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        return PF_OK;
+    }
+    const size_t want = std::min(bytes, piece);
+    if (c->pin_cap < want) {
+        if (c->pin) (void)hipHostFree(c->pin);
+        c->pin = nullptr;
+        c->pin_cap = 0;
+        if (hipHostMalloc(&c->pin, want, hipHostMallocDefault) != hipSuccess) {
+            c->pin = nullptr;
+            HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+            return PF_OK;
+        }
+        c->pin_cap = want;
+    }
+    for (size_t o = 0; o < bytes; o += c->pin_cap) {
+        const size_t k = std::min(c->pin_cap, bytes - o);
+        uint8_t *pin = (uint8_t *)c->pin;
+        const uint8_t *s8 = (const uint8_t *)src + o;
+        par_for(k, [&](uint64_t lo, uint64_t hi) { memcpy(pin + lo, s8 + lo, hi - lo); });
+        HIPCHK(hipMemcpy((uint8_t *)dst + o, pin, k, hipMemcpyHostToDevice));
+    }
+    return PF_OK;
+}
+
+// like pinned_put, but the pieces are produced by fill(buf, lo, hi) in the
+// pinned buffer itself
+template <typename F>
+static int pinned_fill(pf_ctx *c, void *dst, size_t bytes, F fill) {
+    const size_t piece = (size_t)256 << 20;
+    const size_t want = std::max<size_t>(std::min(bytes, piece), 1);
+    if (c->pin_cap < want) {
+        if (c->pin) (void)hipHostFree(c->pin);
+        c->pin = nullptr;
+        c->pin_cap = 0;
+        if (hipHostMalloc(&c->pin, want, hipHostMallocDefault) != hipSuccess) { c->pin = nullptr; return PF_ERR_NOMEM; }
+        c->pin_cap = want;
+    }
+    for (size_t o = 0; o < bytes; o += c->pin_cap) {
+        const size_t k = std::min(c->pin_cap, bytes - o);
+        fill((uint8_t *)c->pin, (uint64_t)o, (uint64_t)(o + k));
+        HIPCHK(hipMemcpy((uint8_t *)dst + o, c->pin, k, hipMemcpyHostToDevice));
+    }
     return PF_OK;
 }
 
@@ -455,35 +522,48 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         return PF_ERR_ARG;
     for (uint32_t w = 0; w < W; w++)
         if (a->win_rec_off[w + 1] < a->win_rec_off[w]) return PF_ERR_ARG;
-    // record slices: monotone offsets, SEQ long enough for l_qseq
+    // record slices: monotone offsets, SEQ long enough for l_qseq (checked
+    // per record in parallel; the slice offsets are a prefix sum)
     std::vector<uint64_t> seq_off(n + 1), scr_off(n + 1);
+    std::vector<int> prc(17, 0);
+    par_for(n, [&](uint64_t lo, uint64_t hi) {
+        int rc = 0;
+        for (uint64_t r = lo; r < hi && !rc; r++) {
+            if (a->cigar_off[r + 1] < a->cigar_off[r] || a->mm_off[r + 1] < a->mm_off[r] ||
+                a->ml_off[r + 1] < a->ml_off[r] || a->seq_off[r + 1] < a->seq_off[r]) { rc = PF_ERR_ARG; break; }
+            const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
+            if (a->seq_off[r + 1] - a->seq_off[r] < sb) { rc = PF_ERR_ARG; break; }
+            // htslib refuses records whose CIGAR query length differs from l_qseq
+            // (bam_read1); K0's walk relies on it to stay inside SEQ
+            if (!(a->flag[r] & 4) && a->l_qseq[r] && a->cigar_off[r + 1] > a->cigar_off[r]) {
+                uint64_t ql = 0;
+                for (uint64_t c = a->cigar_off[r]; c < a->cigar_off[r + 1]; c++) {
+                    const uint32_t op = a->cigar[c] & 15u;
+                    if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += a->cigar[c] >> 4;
+                }
+                if (ql != a->l_qseq[r]) { rc = PF_ERR_ARG; break; }
+            }
+            if (a->mm_off[r + 1] - a->mm_off[r] > 0xFFFFFFF0ull || a->ml_off[r + 1] - a->ml_off[r] > 0xFFFFFFF0ull)
+                rc = PF_ERR_LIMIT;
+            if (a->l_qseq[r] >= (1u << 24)) rc = PF_ERR_LIMIT;   // K0 packs ranks into 24 bits
+            // this record's slice sizes, summed below
+            seq_off[r] = (sb + PF_K0_SEQ_ALIGN + PF_K0_SEQ_ALIGN - 1) & ~(uint64_t)(PF_K0_SEQ_ALIGN - 1);
+            // trigger lists that may exceed the per-wave LDS list get an HBM slice
+            const uint64_t mln = a->ml_off[r + 1] - a->ml_off[r], mlen = a->mm_off[r + 1] - a->mm_off[r];
+            const uint64_t bound = mln ? mln : (mlen + 1) / 2;
+            scr_off[r] = bound > PF_K0_TCAP ? bound : 0;       // ranks, then triggers in place
+        }
+        if (rc) __atomic_store_n(&prc[rc == PF_ERR_LIMIT ? 1 : 0], 1, __ATOMIC_RELAXED);
+    });
+    if (prc[0]) return PF_ERR_ARG;
+    if (prc[1]) return PF_ERR_LIMIT;
     uint64_t so = 0, sc = 0;
     for (uint32_t r = 0; r < n; r++) {
-        if (a->cigar_off[r + 1] < a->cigar_off[r] || a->mm_off[r + 1] < a->mm_off[r] ||
-            a->ml_off[r + 1] < a->ml_off[r] || a->seq_off[r + 1] < a->seq_off[r])
-            return PF_ERR_ARG;
-        const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
-        if (a->seq_off[r + 1] - a->seq_off[r] < sb) return PF_ERR_ARG;
-        // htslib refuses records whose CIGAR query length differs from l_qseq
-        // (bam_read1); K0's walk relies on it to stay inside SEQ
-        if (!(a->flag[r] & 4) && a->l_qseq[r] && a->cigar_off[r + 1] > a->cigar_off[r]) {
-            uint64_t ql = 0;
-            for (uint64_t c = a->cigar_off[r]; c < a->cigar_off[r + 1]; c++) {
-                const uint32_t op = a->cigar[c] & 15u;
-                if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += a->cigar[c] >> 4;
-            }
-            if (ql != a->l_qseq[r]) return PF_ERR_ARG;
-        }
-        if (a->mm_off[r + 1] - a->mm_off[r] > 0xFFFFFFF0ull || a->ml_off[r + 1] - a->ml_off[r] > 0xFFFFFFF0ull)
-            return PF_ERR_LIMIT;
+        const uint64_t x = seq_off[r], y = scr_off[r];
         seq_off[r] = so;
-        so += (sb + PF_K0_SEQ_ALIGN + PF_K0_SEQ_ALIGN - 1) & ~(uint64_t)(PF_K0_SEQ_ALIGN - 1);
-        // trigger lists that may exceed the per-wave LDS list get an HBM slice
-        const uint64_t mln = a->ml_off[r + 1] - a->ml_off[r], mlen = a->mm_off[r + 1] - a->mm_off[r];
-        const uint64_t bound = mln ? mln : (mlen + 1) / 2;
         scr_off[r] = sc;
-        if (bound > PF_K0_TCAP) sc += bound;              // ranks, then triggers in place
-        if (a->l_qseq[r] >= (1u << 24)) return PF_ERR_LIMIT; // K0 packs ranks into 24 bits
+        so += x;
+        sc += y;
     }
     seq_off[n] = so;
     scr_off[n] = sc;
@@ -513,20 +593,44 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         PUT(p32, a->l_qseq, n); ld.l_qseq = p32;
         float *pf; PUT(pf, a->de, n); ld.de = pf;
         uint64_t *p64; PUT(p64, a->cigar_off, n + 1); ld.cigar_off = p64;
-        PUT(p32, a->cigar, a->cigar_off[n]); ld.cigar = p32;
+        ALLOC(p32, a->cigar_off[n]); ld.cigar = p32;
+        if ((rc = pinned_put(ctx, p32, a->cigar, 4ull * a->cigar_off[n]))) return fail(rc);
         PUT(p64, a->mm_off, n + 1); ld.mm_off = p64;
         ALLOC(p8, a->mm_off[n] + 16); ld.mm = p8;            // padded: K0 stages the text with word loads
-        if (a->mm_off[n]) HIPCHK(hipMemcpy(p8, a->mm, a->mm_off[n], hipMemcpyHostToDevice));
+        if (a->mm_off[n] && (rc = pinned_put(ctx, p8, a->mm, a->mm_off[n]))) return fail(rc);
         PUT(p64, a->ml_off, n + 1); ld.ml_off = p64;
-        PUT(p8, a->ml, a->ml_off[n]); ld.ml = p8;
+        ALLOC(p8, a->ml_off[n]); ld.ml = p8;
+        if ((rc = pinned_put(ctx, p8, a->ml, a->ml_off[n]))) return fail(rc);
         PUT(p64, seq_off.data(), n + 1); ld.seq_off = p64;
         PUT(p64, scr_off.data(), n + 1); ld.scr_off = p64;
         ALLOC(p32, sc ? sc : 1); ld.scr = p32;
-        // SEQ repacked into 16-byte aligned, padded per-record slices
-        std::vector<uint8_t> sq(so ? so : 1, 0);
-        for (uint32_t r = 0; r < n; r++)
-            memcpy(sq.data() + seq_off[r], a->seq + a->seq_off[r], ((uint64_t)a->l_qseq[r] + 1) / 2);
-        PUT(p8, sq.data(), sq.size()); ld.seq = p8;
+        // SEQ repacked into 16-byte aligned, padded per-record slices, built
+        // piece by piece in the pinned buffer (no pageable copy of 1 GB)
+        ALLOC(p8, so ? so : 1); ld.seq = p8;
+        rc = pinned_fill(ctx, p8, so, [&](uint8_t *buf, uint64_t lo, uint64_t hi) {
+            const uint64_t r0 = (uint64_t)(std::upper_bound(seq_off.begin(), seq_off.begin() + n + 1, lo) -
+                                           seq_off.begin()) - 1;
+            uint64_t r1 = r0;
+            while (r1 < n && seq_off[r1] < hi) r1++;
+            par_for(r1 - r0, [&](uint64_t a0, uint64_t a1) {
+                for (uint64_t r = r0 + a0; r < r0 + a1; r++) {
+                    const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
+                    const uint64_t x0 = std::max(seq_off[r], lo), x1 = std::min(seq_off[r + 1], hi);
+                    for (uint64_t x = x0; x < x1;) {               // data part, then the zero pad
+                        const uint64_t rel = x - seq_off[r];
+                        if (rel < sb) {
+                            const uint64_t k = std::min(sb - rel, x1 - x);
+                            memcpy(buf + (x - lo), a->seq + a->seq_off[r] + rel, k);
+                            x += k;
+                        } else {
+                            memset(buf + (x - lo), 0, x1 - x);
+                            x = x1;
+                        }
+                    }
+                }
+            });
+        });
+        if (rc) return fail(rc);
         // wave slots in decreasing read length: the long records start first
         // and the four waves of a workgroup finish together
         std::vector<uint32_t> ord(n);
