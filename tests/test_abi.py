@@ -87,3 +87,23 @@ def test_host_epilogue_decisions():
     assert ev([20, 6, 0, 18])[1] == -9    # contamination > 5 in one row
     assert ev([5, 2, 0, 9])[1] == -9      # ratio 5/2 < 3
     assert ev([3, 0, 0, 3])[3] == -1      # not significant (p >= 0.001)
+
+
+def test_ingest_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors of the host-ingest structs (pomfret_amd/bam.py) against
+    the C compiler's sizeof / offsetof of include/pomfret_amd.h."""
+    import subprocess
+    from pomfret_amd.abi import PfAlnBatch
+    from pomfret_amd.bam import PfBamReads, PfBamRecords, PfKnownTable, PfQnameTags, PfRescueMap
+    src = tmp_path / "l.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "pomfret_amd.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(pf_aln_batch_t),'
+                   'sizeof(pf_bam_records_t), offsetof(pf_bam_records_t, n_truncated), sizeof(pf_bam_reads_t),'
+                   'sizeof(pf_known_table_t), sizeof(pf_qname_tags_t), sizeof(pf_rescue_map_t),'
+                   'offsetof(pf_bam_reads_t, qname));return 0;}\n')
+    exe = tmp_path / "l"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    exp = [C.sizeof(PfAlnBatch), C.sizeof(PfBamRecords), PfBamRecords.n_truncated.offset, C.sizeof(PfBamReads),
+           C.sizeof(PfKnownTable), C.sizeof(PfQnameTags), C.sizeof(PfRescueMap), PfBamReads.qname.offset]
+    assert got == exp
