@@ -415,3 +415,35 @@ class AlnBatch:
 
     def nbytes(self) -> int:
         return int(sum(getattr(self, n).nbytes for n in _ALN_FIELDS))
+
+    def select(self, windows) -> "AlnBatch":
+        """Sub-batch with the given window indices (records re-packed)."""
+        windows = np.asarray(windows, dtype=np.int64)
+        wo = self.win_rec_off.astype(np.int64)
+        recs = [np.arange(wo[w], wo[w + 1]) for w in windows]
+        recs = np.concatenate(recs) if recs else np.zeros(0, np.int64)
+        cnt = np.array([wo[w + 1] - wo[w] for w in windows], dtype=np.int64)
+
+        def gather(off, data):
+            off = np.asarray(off, np.int64)
+            lo, hi = off[recs], off[recs + 1]
+            sizes = hi - lo
+            noff = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+            parts = [data[a:b] for a, b in zip(lo.tolist(), hi.tolist())]
+            return noff, (np.concatenate(parts) if parts else data[:0])
+
+        co, cg = gather(self.cigar_off, self.cigar)
+        lq = self.l_qseq.astype(np.int64)
+        so = np.asarray(self.seq_off, np.int64)
+        sparts = [self.seq[so[r]:so[r] + (lq[r] + 1) // 2] for r in recs.tolist()]
+        sq = np.concatenate(sparts) if sparts else self.seq[:0]
+        soff = np.concatenate([[0], np.cumsum([(lq[r] + 1) // 2 for r in recs.tolist()])]).astype(np.uint64)
+        mo, mm = gather(self.mm_off, self.mm)
+        lo_, ml = gather(self.ml_off, self.ml)
+        opt = {n: (None if getattr(self, n) is None else getattr(self, n)[windows])
+               for n in ("win_cov_sel", "win_cov_rt", "win_n_cand")}
+        return AlnBatch(win_start=self.win_start[windows], win_end=self.win_end[windows],
+                        win_rec_off=np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32),
+                        flag=self.flag[recs], mapq=self.mapq[recs], pos=self.pos[recs], l_qseq=self.l_qseq[recs],
+                        de=self.de[recs], hp=self.hp[recs], cigar_off=co, cigar=cg, seq_off=soff, seq=sq,
+                        mm_off=mo, mm=mm, ml_off=lo_, ml=ml, **opt)

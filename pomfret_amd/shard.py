@@ -46,6 +46,21 @@ def shard(batch: WindowBatch, rank: int, world: int):
     return idx, batch.select(idx)
 
 
+def aln_window_costs(aln) -> np.ndarray:
+    """Record-level cost of each window: its SEQ + MM bytes (K0's work)."""
+    wo = aln.win_rec_off.astype(np.int64)
+    per = (aln.l_qseq.astype(np.int64) + 1) // 2 + np.diff(aln.mm_off.astype(np.int64))
+    cs = np.concatenate([[0], np.cumsum(per)])
+    return (cs[wo[1:]] - cs[wo[:-1]]).astype(np.float64)
+
+
+def shard_aln(aln, rank: int, world: int):
+    """(window indices, record-level sub-batch) owned by `rank`."""
+    parts = lpt_partition(aln_window_costs(aln), world)
+    idx = parts[rank]
+    return idx, aln.select(idx)
+
+
 def gather_decisions(n_windows: int, idx: np.ndarray, decision: np.ndarray, group=None):
     """All-gather per-window decisions into original window order.
 

@@ -63,3 +63,44 @@ def test_lpt_partition_balances():
     loads = [costs[p].sum() for p in parts]
     assert max(loads) <= 4.0 / 3.0 * costs.sum() / 3   # Graham's LPT bound
     assert sorted(np.concatenate(parts).tolist()) == list(range(9))
+
+
+def _aln_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from pomfret_amd import Config, LoadConfig
+        from pomfret_amd.shard import gather_decisions, shard_aln
+        from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+        cfg = Config.from_coverage(30, given=False)
+        aln = make_aln_batch(AlnSpec(n_windows=6, coverage=20, seed=9, len_scale=0.4), workers=1)
+        idx, sub = shard_aln(aln, rank, world)
+        res = oracle.methphase_aln(cfg, LoadConfig(), sub, n_threads=2)
+        full = gather_decisions(aln.n_windows, idx, res.decision)
+        np.save(os.path.join(out_dir, f"adec{rank}.npy"), full)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_record_level_shards(tmp_path, oracle_lib):
+    """Record-level batches shard by window (AlnBatch.select + LPT on SEQ/MM
+    bytes); the gathered decisions equal the whole batch's."""
+    world = 2
+    mp.spawn(_aln_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    from pomfret_amd import Config, LoadConfig
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    aln = make_aln_batch(AlnSpec(n_windows=6, coverage=20, seed=9, len_scale=0.4), workers=1)
+    ref = oracle_lib.methphase_aln(Config.from_coverage(30, given=False), LoadConfig(), aln, n_threads=4).decision
+    for r in range(world):
+        assert np.array_equal(np.load(tmp_path / f"adec{r}.npy"), ref)
+    # select() keeps every field of the chosen windows' records
+    sub = aln.select([4, 1])
+    w4 = slice(int(aln.win_rec_off[4]), int(aln.win_rec_off[5]))
+    n4 = int(aln.win_rec_off[5] - aln.win_rec_off[4])
+    assert np.array_equal(sub.pos[:n4], aln.pos[w4]) and sub.n_windows == 2
+    r0 = int(aln.win_rec_off[4])
+    assert bytes(sub.mm[sub.mm_off[0]:sub.mm_off[1]]) == bytes(aln.mm[aln.mm_off[r0]:aln.mm_off[r0 + 1]])
+    lq = int(aln.l_qseq[r0])
+    assert bytes(sub.seq[:(lq + 1) // 2]) == bytes(aln.seq[aln.seq_off[r0]:aln.seq_off[r0] + (lq + 1) // 2])
