@@ -38,7 +38,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 PEAK_HBM_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-WORKLOAD = dict(n_windows=256, coverage=30, gap=50_000)
+# N=1 headline: BASELINE.json's target is quoted on HG002 60x at 1 GPU
+WORKLOAD = dict(n_windows=1024, coverage=60, gap=50_000)
+CPU_SHARE = 16           # host cores per GPU on the MI355X boxes (OMP_NUM_THREADS there)
 
 
 def log(*a):
@@ -73,28 +75,36 @@ def algo_bytes(batch, stats, n_sites):
 
 
 def k0_bytes(aln, read_recs, n_calls):
-    """Algorithmic bytes per launch of K0: 4 B (read index) per
-    record; per kept record 55 B of fixed fields (flag, MAPQ, pos, l_qseq, de,
-    five record offsets, the read's call offset), its CIGAR (4 B/op), 4-bit SEQ
-    (l_qseq/2 B) and MM text; per call 1 B of ML read and 5 B (u32 pos + u8
-    cat) written; per kept read 16 B written (start, end, first, last)."""
+    """Algorithmic bytes per launch of K0: per record 15 B of
+    filter fields (wave-slot index, flag, MAPQ, l_qseq, de) read and 4 B
+    (rec_n) written; per kept record 55 B of fixed fields (pos, the record's
+    offsets), its CIGAR (4 B/op), 4-bit SEQ (l_qseq/2 B) and MM text read and
+    24 B written (start, end, first, last, staging offset); per call 1 B of ML
+    read and 5 B (u32 pos + u8 cat) written to its staging slice."""
     kept = np.asarray(read_recs, np.int64)
     cig = np.diff(aln.cigar_off.astype(np.int64))[kept]
     mm = np.diff(aln.mm_off.astype(np.int64))[kept]
     seq = (aln.l_qseq.astype(np.int64)[kept] + 1) // 2
     R = kept.shape[0]
-    return int(4 * aln.n_recs + 55 * R + 4 * cig.sum() + seq.sum() + mm.sum() + 6 * n_calls + 16 * R)
+    return int(19 * aln.n_recs + 79 * R + 4 * cig.sum() + seq.sum() + mm.sum() + 6 * n_calls)
 
 
-def pmc_traffic(kernel: str, boundary: str):
+def pack_bytes(n_recs, R, n_calls):
+    """scan + pack: 4 B (rec_n) per record; per kept read 25 B read (record
+    fields, staging offset, HP) and 34 B written (read fields, record index,
+    two tag copies, call offset); per call 5 B read + 5 B written."""
+    return int(4 * n_recs + 59 * R + 10 * n_calls)
+
+
+def pmc_traffic(kernel: str, wl: dict, boundary: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py) when it was
-    collected on this workload and boundary, or None."""
+    collected on this run's workload `wl` and boundary, or None."""
     p = os.path.join(HERE, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
             d = json.load(f)
-        if d.get("workload") != dict(WORKLOAD, boundary=boundary):
+        if d.get("workload") != dict(wl, boundary=boundary):
             return None
         return d["kernels"].get(kernel, {}).get("hbm_bytes_per_launch")
     except Exception:
@@ -150,11 +160,14 @@ def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 2
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--windows", type=int, default=WORKLOAD["n_windows"])
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--windows", type=int, default=WORKLOAD["n_windows"],
+                    help="windows of the job (strong scaling, dealt over the ranks); per rank with --weak")
     ap.add_argument("--coverage", type=int, default=WORKLOAD["coverage"])
+    ap.add_argument("--weak", action="store_true", help="every rank owns --windows windows of its own")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-legs", action="store_true", help="skip the calls-level and PCIe-inclusive legs")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--calls-level", action="store_true",
                     help="time the calls-level boundary (reads + 5mC calls resident, no K0)")
@@ -172,11 +185,21 @@ def main():
     cfg = Config.from_coverage(wl["coverage"], given=False)
     lcfg = LoadConfig()
     record_level = not args.calls_level
+    # Strong scaling (default): one job of wl["n_windows"] windows, dealt
+    # round-robin to the ranks (the synthetic windows are i.i.d.; the product's
+    # sharder, pomfret_amd.shard, balances real windows by LPT on their bytes).
+    # --weak: every rank owns wl["n_windows"] windows of its own.
+    if args.weak:
+        mine = list(range(wl["n_windows"]))
+        seed = 1000 + rank
+    else:
+        mine = list(range(rank, wl["n_windows"], world))
+        seed = 1000
     t = time.perf_counter()
     if record_level:
         # generated (in worker processes) before anything touches the GPU
-        aln = make_aln_batch(AlnSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
-                                     seed=1000 + rank), workers=0 if world == 1 else 4)
+        aln = make_aln_batch(AlnSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"], seed=seed),
+                             windows=mine, workers=0 if world == 1 else max(1, CPU_SHARE // 2))
         log(f"[bench] rank {rank}: generated {aln.n_windows} windows, {aln.n_recs} BAM records "
             f"({aln.nbytes() / 1e9:.2f} GB) in {time.perf_counter() - t:.1f}s")
 
@@ -192,7 +215,7 @@ def main():
     if record_level:
         t = time.perf_counter()
         db = ctx.upload_aln(cfg, aln, lcfg)
-        log(f"[bench] upload (validation, SEQ repack, H2D, K0 count pass): {time.perf_counter() - t:.1f}s")
+        log(f"[bench] upload (validation, SEQ repack, H2D; no device work): {time.perf_counter() - t:.1f}s")
         off, cpos, ccat, _, _ = db.debug_calls()
         rr = db.read_recs()
         # the loaded reads as a window batch (the byte model and the calls-level
@@ -203,12 +226,14 @@ def main():
                             read_start=rs, read_end=re_,
                             read_hp=aln.hp[rr], read_call_off=off, call_pos=cpos, call_cat=ccat,
                             win_cov_sel=aln.win_cov_sel, win_cov_rt=aln.win_cov_rt, win_n_cand=aln.win_n_cand)
+        del off, cpos, ccat
     else:
         batch = make_batch(SynthSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
-                                     seed=1000 + rank))
+                                     seed=seed)).select(mine)
         log(f"[bench] rank {rank}: generated {batch.n_windows} windows, {batch.n_reads} reads, "
             f"{batch.n_calls} calls in {time.perf_counter() - t:.1f}s")
         db = ctx.upload(cfg, batch)
+
     def timed(db, n_windows, n_reads):
         """W warmup runs, then exactly K timed steps between barrier + sync
         pairs; returns (max-over-ranks seconds, total reads, per-kernel ms
@@ -219,18 +244,20 @@ def main():
             db.run(out)
         if dist is not None:
             import torch
-            dec_t = torch.empty(n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
-            gathered = torch.empty(world * n_windows, dtype=torch.int8, device=f"cuda:{local_rank}")
+            n_max = torch.tensor([n_windows], dtype=torch.int64, device=f"cuda:{local_rank}")
+            dist.all_reduce(n_max, op=dist.ReduceOp.MAX)
+            dec_t = torch.full((int(n_max.item()),), -2, dtype=torch.int8, device=f"cuda:{local_rank}")
+            gathered = torch.empty(world * dec_t.numel(), dtype=torch.int8, device=f"cuda:{local_rank}")
 
         # Steps are pipelined two deep (pf_methphase_launch / _finish): the host
         # epilogue of step k (Fisher tests, decisions, read tags) overlaps the
-        # kernels of step k+1; every step still runs every kernel, D2H copy and
-        # epilogue inside the timed region.
+        # kernels of step k+1; every step runs every kernel (K0 loader, scan +
+        # pack, K12, K2, K3), the D2H copy and the epilogue inside the timed region.
         def finish(k):
             o = outs[k % 2]
             db.finish(o)
             if dist is not None:
-                dec_t.copy_(torch.from_numpy(o.decision))
+                dec_t[:n_windows].copy_(torch.from_numpy(o.decision))
                 dist.all_gather_into_tensor(gathered, dec_t)
 
         if dist is not None:
@@ -269,8 +296,10 @@ def main():
     ab = algo_bytes(batch, stats, out.win_n_sites)
     if record_level:
         ab["pf_k0_load"] = k0_bytes(aln, rr, batch.n_calls)
+        ab["pf_k0_pack"] = pack_bytes(aln.n_recs, batch.n_reads, batch.n_calls)
     else:
         kmean.pop("pf_k0_load", None)
+        kmean.pop("pf_k0_pack", None)
     kernels = {}
     for k, ms in kmean.items():
         b = ab.get(k, 0)
@@ -278,48 +307,61 @@ def main():
                       "GBps": round(b / (ms * 1e-3) / 1e9, 2) if ms > 0 else None}
     dom = max(kmean, key=kmean.get)
     achieved = kernels[dom]["GBps"]
-    traffic = pmc_traffic(dom, "records" if record_level else "calls")
+    boundary = "records" if record_level else "calls"
+    traffic = pmc_traffic(dom, dict(wl, windows_per_gpu=batch.n_windows), boundary)
 
     calls_leg = None
-    if record_level:
+    if record_level and not args.no_legs:
         # the same reads with K0's calls already resident (the calls-level
         # boundary, pf_batch_upload): K12 + K3 + epilogue only
         dbc = ctx.upload(cfg, batch)
         el_c, tot_c, acc_c, out_c = timed(dbc, batch.n_windows, batch.n_reads)
         dbc.free()
         calls_leg = {"value": round(tot_c / el_c, 1), "ms_per_step": round(el_c / args.steps * 1e3, 4),
-                     "kernels_ms": {k: round(v / args.steps, 4) for k, v in acc_c.items() if k != "pf_k0_load"},
+                     "kernels_ms": {k: round(v / args.steps, 4) for k, v in acc_c.items()
+                                    if k not in ("pf_k0_load", "pf_k0_pack")},
                      "decisions_match": bool(np.array_equal(out_c.decision, out.decision)),
                      "what": "same reads, calls resident in HBM (no K0): the pre-K0 boundary"}
 
     # PCIe-inclusive rate (never `value`): the one-shot boundary call hands
     # over host buffers -- upload (validation, pinned staging, H2D), run, D2H
-    t1 = time.perf_counter()
-    n_once = 2 if record_level else 3
-    for _ in range(n_once):
-        db2 = ctx.upload_aln(cfg, aln, lcfg) if record_level else ctx.upload(cfg, batch)
-        db2.run()
-        db2.free()
-    what = ("upload(host BAM-record SoA: validation, SEQ repack, H2D, K0 count pass) + run + free per call"
-            if record_level else "upload(host SoA -> HBM) + run + free per call")
-    pcie = {"reads_per_s": round(batch.n_reads * n_once / (time.perf_counter() - t1), 1),
-            "ms_per_call": round((time.perf_counter() - t1) / n_once * 1e3, 3),
-            "what": what + ", rank 0"}
+    pcie = None
+    if not args.no_legs:
+        t1 = time.perf_counter()
+        n_once = 2
+        for _ in range(n_once):
+            db2 = ctx.upload_aln(cfg, aln, lcfg) if record_level else ctx.upload(cfg, batch)
+            db2.run()
+            db2.free()
+        what = ("upload(host BAM-record SoA: validation, SEQ repack, H2D) + run + free per call"
+                if record_level else "upload(host SoA -> HBM) + run + free per call")
+        pcie = {"reads_per_s": round(batch.n_reads * n_once / (time.perf_counter() - t1), 1),
+                "ms_per_call": round((time.perf_counter() - t1) / n_once * 1e3, 3),
+                "what": what + ", rank 0"}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+        # the box's CPU share per GPU (OMP_NUM_THREADS there); the reference's
+        # kt_for scales with threads, so the -t 32 figure of BASELINE's target
+        # would be at most twice this
+        threads = args.cpu_threads or min(CPU_SHARE, len(os.sched_getaffinity(0)))
+        sub = list(range(min(64, batch.n_windows)))
         if record_level:
-            v_cpu, dt, reps = cpu_baseline_aln(cfg, lcfg, aln, batch.n_reads, threads)
+            a_sub = aln.select(sub)
+            n_sub = int(batch.win_read_off[len(sub)])
+            v_cpu, dt, reps = cpu_baseline_aln(cfg, lcfg, a_sub, n_sub, threads)
             what = "per-window loader + worker over the same BAM records, oracle/pf_oracle{_load,}.c"
         else:
-            v_cpu, dt, reps = cpu_baseline(cfg, batch, threads)
+            b_sub = batch.select(sub)
+            n_sub = b_sub.n_reads
+            v_cpu, dt, reps = cpu_baseline(cfg, b_sub, threads)
             what = "oracle/pf_oracle.c"
         cpu = {"value": round(v_cpu, 1), "unit": "reads/s", "cores": threads, "kind": "port",
-               "sample": f"the same {batch.n_windows}-window workload x{reps} "
-                         f"({batch.n_reads * reps} reads, {dt:.2f}s wall x {threads} threads "
+               "sample": f"the first {len(sub)} windows of the workload x{reps} "
+                         f"({n_sub * reps} reads, {dt:.2f}s wall x {threads} threads "
                          f"= {dt * threads:.0f} CPU-s), {what}"}
 
+    par = f"windows dealt over dp{world}" + (" (weak: per-rank batches)" if args.weak else " (strong: one job)")
     res = {
         "metric": "aligned reads/sec (methphase kernel)",
         "value": round(value, 1),
@@ -329,28 +371,30 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.weak else "strong",
         "vs_baseline": None,
         "dtype": "u32/f32",
-        "data": "synthetic (seeded chr20-like 30x pileups; HG002 not available offline)",
+        "data": f"synthetic (seeded {wl['coverage']}x long-read pileups, HG002-like; HG002 not available offline)",
         "config": {
-            "workload": f"chr20-like {wl['coverage']}x: {wl['n_windows']} gap windows x "
-                        f"{wl['gap'] // 1000} kb per GPU, pre-haplotagged (BASELINE configs[1]); "
-                        + ("BAM records resident (K0 loader in the step)" if record_level
-                           else "reads + 5mC calls resident (no K0)"),
-            "boundary": "records" if record_level else "calls",
+            "workload": (f"HG002-like {wl['coverage']}x pre-haplotagged: "
+                         f"{wl['n_windows'] * (world if args.weak else 1)} gap windows x {wl['gap'] // 1000} kb "
+                         f"in the job, {batch.n_windows} on this GPU; "
+                         + ("BAM records resident (every per-batch kernel in the step: K0 loader, scan + pack, "
+                            "K12, K2, K3)" if record_level else "reads + 5mC calls resident (no K0)")),
+            "boundary": boundary,
             "records_per_gpu": aln.n_recs if record_level else None,
-            "windows_per_gpu": wl["n_windows"], "reads_per_gpu": batch.n_reads,
+            "windows_per_gpu": batch.n_windows, "reads_per_gpu": batch.n_reads,
             "calls_per_gpu": batch.n_calls, "coverage": wl["coverage"],
             "cov_for_selection": cfg.cov_for_selection, "cov_for_runtime": cfg.cov_for_runtime,
             "n_cand": cfg.n_cand, "k": cfg.k, "k_span": cfg.k_span,
-            "parallelism": f"windows sharded, dp{world}",
+            "parallelism": par,
         },
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 5) if achieved else None,
                      "traffic": traffic},
         "kernels": kernels,
         "cpu_baseline": cpu,
+        "vs_cpu_baseline": round(value / cpu["value"], 2) if cpu else None,
         "pcie_inclusive": pcie,
         "calls_level": calls_leg,
         "decisions": {"cis": int((out.decision == 0).sum()), "trans": int((out.decision == 1).sum()),

@@ -210,6 +210,8 @@ int  pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg,
 void pf_batch_free(pf_dbatch_t *db);
 uint32_t pf_batch_n_windows(const pf_dbatch_t *db);
 uint32_t pf_batch_n_reads(const pf_dbatch_t *db);
+/* Calls of the batch (record level: of the last finished run, 0 before). */
+uint64_t pf_batch_n_calls(const pf_dbatch_t *db);
 
 /* Run the hot path on a resident batch: all kernels, then the 2x2 tables and
  * tags come back to the host, where the Fisher test and the join decision

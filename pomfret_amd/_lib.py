@@ -45,6 +45,8 @@ def lib():
         L.pf_batch_n_windows.restype = C.c_uint32
         L.pf_batch_n_reads.argtypes = [C.c_void_p]
         L.pf_batch_n_reads.restype = C.c_uint32
+        L.pf_batch_n_calls.argtypes = [C.c_void_p]
+        L.pf_batch_n_calls.restype = C.c_uint64
         L.pf_methphase_run.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(PfWindowOut)]
         L.pf_methphase_launch.argtypes = [C.c_void_p, C.c_void_p]
         L.pf_methphase_finish.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(PfWindowOut)]
@@ -322,28 +324,50 @@ class DeviceBatch:
             _check(lib().pf_batch_upload(ctx.handle, C.byref(c), C.byref(b), C.byref(h)),
                    "pf_batch_upload")
         self.handle = h
-        self.n_reads = int(lib().pf_batch_n_reads(h))
+        self.record_level = isinstance(batch, AlnBatch)
         ctx._batches.add(self)
 
-    def read_recs(self) -> np.ndarray:
-        """Record index of every read of the batch (identity for window batches)."""
-        out = np.zeros(max(self.n_reads, 1), np.uint32)
-        _check(lib().pf_batch_read_recs(self.handle, out.ctypes.data, out.size), "pf_batch_read_recs")
-        return out[:self.n_reads]
+    @property
+    def n_reads(self) -> int:
+        """Reads of the batch.  Record level: the kept records of the last
+        finished run (K0 sizes the batch on the device in every run); before
+        any run, the record count (an upper bound)."""
+        return int(lib().pf_batch_n_reads(self.handle))
 
-    def debug_calls(self, cap: int = 1 << 27):
-        """K0 output: (call_off, pos, cat, first, last), calls sorted by (pos, cat) per read."""
+    def read_recs(self) -> np.ndarray:
+        """Record index of every read of the batch (identity for window
+        batches).  Record level: runs the loader first if no run has finished."""
+        R = self.n_reads
+        out = np.zeros(max(R, 1), np.uint32)
+        rc = lib().pf_batch_read_recs(self.handle, out.ctypes.data, out.size)
+        if rc != 0 and self.record_level:           # no run has finished yet: load once
+            self.debug_calls(cap=0, probe=True)
+            R = self.n_reads
+            rc = lib().pf_batch_read_recs(self.handle, out.ctypes.data, out.size)
+        _check(rc, "pf_batch_read_recs")
+        return out[:R]
+
+    def debug_calls(self, cap: int = None, probe: bool = False):
+        """K0 output: (call_off, pos, cat, first, last), calls sorted by (pos, cat) per read.
+        probe=True only runs the loader (sizes the batch)."""
+        if cap is None:
+            if self.record_level and not lib().pf_batch_n_calls(self.handle):
+                self.debug_calls(cap=0, probe=True)
+            cap = int(lib().pf_batch_n_calls(self.handle))
         R = self.n_reads
         off = np.zeros(R + 1, np.uint64)
-        pos = np.zeros(cap, np.uint32)
-        cat = np.zeros(cap, np.uint8)
+        pos = np.zeros(max(cap, 1), np.uint32)
+        cat = np.zeros(max(cap, 1), np.uint8)
         first = np.zeros(max(R, 1), np.uint32)
         last = np.zeros(max(R, 1), np.uint32)
         n = lib().pf_batch_debug_calls(self.handle, off.ctypes.data, pos.ctypes.data, cat.ctypes.data,
                                        first.ctypes.data, last.ctypes.data, cap)
+        if probe:
+            return None
         if n < 0:
             _check(int(n), "pf_batch_debug_calls")
-        return off, pos[:n], cat[:n], first[:R], last[:R]
+        R = self.n_reads
+        return off[:R + 1], pos[:n], cat[:n], first[:R], last[:R]
 
     def load_counters(self) -> dict:
         out = np.zeros(8, np.uint64)
@@ -363,10 +387,13 @@ class DeviceBatch:
             pass
 
     def run(self, out: WindowResult = None) -> WindowResult:
-        if out is None:
+        fresh = out is None
+        if fresh:
             out = WindowResult.alloc(self.n_windows, self.n_reads)
         o = out.to_c()
         _check(lib().pf_methphase_run(self.ctx.handle, self.handle, C.byref(o)), "pf_methphase_run")
+        if fresh:
+            out.read_hp = out.read_hp[:self.n_reads]
         return out
 
     def stats(self) -> np.ndarray:
@@ -399,11 +426,14 @@ class DeviceBatch:
         _check(lib().pf_methphase_launch(self.ctx.handle, self.handle), "pf_methphase_launch")
 
     def finish(self, out: WindowResult = None) -> WindowResult:
-        if out is None:
+        fresh = out is None
+        if fresh:
             out = WindowResult.alloc(self.n_windows, self.n_reads)
         o = out.to_c()
         _check(lib().pf_methphase_finish(self.ctx.handle, self.handle, C.byref(o)),
                "pf_methphase_finish")
+        if fresh:
+            out.read_hp = out.read_hp[:self.n_reads]
         return out
 
 

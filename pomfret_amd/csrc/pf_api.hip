@@ -25,16 +25,23 @@ __global__ void pf_k12_sites_methmers(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
 __global__ void pf_k3_fallback(pf_dev_batch d);
-template <int MODE> __global__ void pf_k0_load(pf_load_dev d);
+__global__ void pf_k0_load(pf_load_dev d);
+__global__ void pf_k0_scan(pf_load_dev d);
+__global__ void pf_k0_pack(pf_load_dev d);
 __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
-#define PF_NKERN 5
+#define PF_NKERN 6
 #define PF_SLOTS 2
-#define PF_IO_HDR 64ull      // status u32[4] | arena counters u64[3] | K2, K3 fallback counters u32 | pad
+// I/O block header: status u32[4] | arena counters u64[3] (16) | K2, K3
+// fallback counters u32 (40, 44) | record level: staging bump pointer u64
+// (48), kept reads u32 (56), calls u64 (64), site slots u64 (72) | pad
+#define PF_IO_HDR 128ull
 
-static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k12_sites_methmers", "pf_k2_methmers", "pf_k3_greedy",
-                                        "pf_k3_fallback"};
+// kernel timing slots: "pf_k0_pack" is the scan + pack pair
+static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k0_pack", "pf_k12_sites_methmers", "pf_k2_methmers",
+                                        "pf_k3_greedy", "pf_k3_fallback"};
+#define PF_GROWABLE (PF_ST_KEYS_OVF | PF_ST_BIG_OVF | PF_ST_SCR_OVF | PF_ST_STAGE_OVF | PF_ST_CALL_OVF | PF_ST_SITES_OVF)
 
 struct pf_ctx {
     int device;
@@ -46,6 +53,7 @@ struct pf_ctx {
     int have_haptag;
     void *pin = nullptr;      /* pinned staging for large uploads (grown on demand) */
     size_t pin_cap = 0;
+    uint32_t k3_lds_set = 0;  /* dynamic LDS limit set on the greedy kernels of this device */
 };
 
 struct pf_dbatch {
@@ -69,8 +77,16 @@ struct pf_dbatch {
     int have_ev = 0;
     uint64_t n_launch = 0, n_finish = 0;
     uint64_t site_total;
-    // record-level batches (pf_batch_upload_aln): K0 runs first in every launch
+    // I/O block layout after the header (byte offsets): 2x2 tables, site
+    // counts, read counts, then (record level) the window read offsets and
+    // each read's record, then the forward tags and (record level) raw tags
+    uint64_t o_wro = 0, o_rrec = 0, o_hpfwd = 0, o_hpraw = 0;
+    // record-level batches (pf_batch_upload_aln): K0 + scan + pack run first
+    // in every launch and size the batch on the device; R is the record count
+    // (an upper bound) until a run has finished
     bool has_aln = false;
+    uint32_t n_recs = 0;
+    bool have_map = false;
     pf_load_dev ld;
     std::vector<uint32_t> h_rec_of_read;
     unsigned long long *k0_ctr = nullptr;
@@ -81,24 +97,35 @@ struct IoView {
     uint32_t *status;
     unsigned long long *ctr;     // keys, big, scr counters after a run
     uint32_t *fb, *k3fb;
+    uint64_t stage, N, sites;    // record level: the staging arena, calls and site slots needed
+    uint32_t R;
     int32_t *table;
     uint32_t *S, *nreads;
-    uint8_t *hp_fwd;
+    uint32_t *wro, *rrec;        // record level: window read offsets, record of each read
+    uint8_t *hp_fwd, *hp_raw;
 };
-static IoView io_view(const pf_dbatch *b, int slot) {
-    uint8_t *h = b->h_io[slot];
+static IoView io_view(const pf_dbatch *b, const uint8_t *h) {
+    uint8_t *hh = const_cast<uint8_t *>(h);
     const uint64_t W = b->W;
     IoView v;
-    v.status = reinterpret_cast<uint32_t *>(h);
-    v.ctr = reinterpret_cast<unsigned long long *>(h + 16);
-    v.fb = reinterpret_cast<uint32_t *>(h + 40);
-    v.k3fb = reinterpret_cast<uint32_t *>(h + 44);
-    v.table = reinterpret_cast<int32_t *>(h + PF_IO_HDR);
-    v.S = reinterpret_cast<uint32_t *>(h + PF_IO_HDR + 32ull * W);
-    v.nreads = reinterpret_cast<uint32_t *>(h + PF_IO_HDR + 36ull * W);
-    v.hp_fwd = h + PF_IO_HDR + 40ull * W;
+    v.status = reinterpret_cast<uint32_t *>(hh);
+    v.ctr = reinterpret_cast<unsigned long long *>(hh + 16);
+    v.fb = reinterpret_cast<uint32_t *>(hh + 40);
+    v.k3fb = reinterpret_cast<uint32_t *>(hh + 44);
+    memcpy(&v.stage, hh + PF_IO_STAGE, 8);
+    memcpy(&v.R, hh + PF_IO_R, 4);
+    memcpy(&v.N, hh + PF_IO_N, 8);
+    memcpy(&v.sites, hh + PF_IO_SITES, 8);
+    v.table = reinterpret_cast<int32_t *>(hh + PF_IO_HDR);
+    v.S = reinterpret_cast<uint32_t *>(hh + PF_IO_HDR + 32ull * W);
+    v.nreads = reinterpret_cast<uint32_t *>(hh + PF_IO_HDR + 36ull * W);
+    v.wro = b->has_aln ? reinterpret_cast<uint32_t *>(hh + b->o_wro) : nullptr;
+    v.rrec = b->has_aln ? reinterpret_cast<uint32_t *>(hh + b->o_rrec) : nullptr;
+    v.hp_fwd = hh + b->o_hpfwd;
+    v.hp_raw = b->has_aln ? hh + b->o_hpraw : nullptr;
     return v;
 }
+static IoView io_view(const pf_dbatch *b, int slot) { return io_view(b, b->h_io[slot]); }
 
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "[E::pomfret_amd] %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
@@ -277,11 +304,12 @@ extern "C" void pf_batch_free(pf_dbatch_t *b) {
 
 extern "C" uint32_t pf_batch_n_windows(const pf_dbatch_t *b) { return b ? b->W : 0; }
 extern "C" uint32_t pf_batch_n_reads(const pf_dbatch_t *b) { return b ? b->R : 0; }
+extern "C" uint64_t pf_batch_n_calls(const pf_dbatch_t *b) { return b ? b->N : 0; }
 
 static int mask_words(int k) { int bits = 2 * k; return bits <= 6 ? 1 : 1 << (bits - 6); }
 
 static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t *first, const uint32_t *last,
-                       const uint32_t *cpos, const uint8_t *ccat, pf_dbatch_t **out);
+                       const uint32_t *cpos, const uint8_t *ccat, const uint64_t *win_calls, pf_dbatch_t **out);
 
 static int check_windows(const pf_cfg_t *cfg, const pf_window_batch_t *in) {
     for (uint32_t w = 0; w < in->n_windows; w++) {
@@ -363,20 +391,24 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
         ccat = scat.data();
     }
 
-    return batch_build(b, in, first.data(), last.data(), cpos, ccat, out);
+    return batch_build(b, in, first.data(), last.data(), cpos, ccat, nullptr, out);
 }
 
-// Allocate and fill the device side of a batch.  read_start/read_end/first/
-// last/cpos/ccat may be NULL: the arrays are then only allocated (K0 fills
-// them on every run of a record-level batch).
+// Allocate and fill the device side of a batch.  Calls level: everything from
+// `in`.  Record level (win_calls != NULL): `in` holds the windows' records
+// (win_read_off = records per window, which also orders the greedy problems)
+// and b->R / b->N are capacities; the read, call and site arrays are only
+// allocated -- K0, scan and pack fill them on every run -- and the site
+// slots are sized from win_calls, an upper bound of each window's calls.
 static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t *first, const uint32_t *last,
-                       const uint32_t *cpos, const uint8_t *ccat, pf_dbatch_t **out) {
+                       const uint32_t *cpos, const uint8_t *ccat, const uint64_t *win_calls, pf_dbatch_t **out) {
     const pf_cfg_t *cfg = &b->cfg;
+    const bool aln = win_calls != nullptr;
     const uint32_t W = b->W, R = b->R;
     const uint64_t N = b->N;
     auto fail = [&](int rc) { pf_batch_free(b); return rc; };
     std::vector<int32_t> par(4ull * W);
-    std::vector<uint32_t> read_win(R);
+    std::vector<uint32_t> read_win(aln ? 0 : R);
     std::vector<uint32_t> site_cap(W);
     std::vector<uint64_t> site_off(W);
     uint64_t site_total = 0;
@@ -388,8 +420,9 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         if (sel <= 0) sel = 1;
         if (nc <= 1) nc = 2;
         par[4 * w] = sel; par[4 * w + 1] = rt; par[4 * w + 2] = nc; par[4 * w + 3] = 0;
-        for (uint32_t r = r0; r < r1; r++) read_win[r] = w;
-        const uint64_t calls = in->read_call_off[r1] - in->read_call_off[r0];
+        if (!aln)
+            for (uint32_t r = r0; r < r1; r++) read_win[r] = w;
+        const uint64_t calls = aln ? win_calls[w] : in->read_call_off[r1] - in->read_call_off[r0];
         // a site needs >= sel meth and >= sel unmeth calls
         const uint64_t cap = calls / (2ull * (uint64_t)sel) + 1;
         site_cap[w] = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFF0ull);
@@ -412,17 +445,17 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     {
         uint32_t *p; PUT(p, in->win_start, W); d.win_start = p;
         PUT(p, in->win_end, W); d.win_end = p;
-        PUT(p, in->win_read_off, W + 1); d.win_read_off = p;
+        PUTA(p, aln ? nullptr : in->win_read_off, W + 1); d.win_read_off = p;
         int32_t *ip; PUT(ip, par.data(), par.size()); d.win_par = ip;
-        uint64_t *up; PUT(up, site_off.data(), W); d.win_site_off = up;
-        PUT(p, site_cap.data(), W); d.win_site_cap = p;
+        uint64_t *up; PUTA(up, aln ? nullptr : site_off.data(), W); d.win_site_off = up;
+        PUTA(p, aln ? nullptr : site_cap.data(), W); d.win_site_cap = p;
         PUTA(p, in->read_start, R); d.read_start = p;
         PUTA(p, in->read_end, R); d.read_end = p;
         PUTA(p, first, R); d.read_first = p;
         PUTA(p, last, R); d.read_last = p;
-        PUT(p, read_win.data(), R); d.read_win = p;
-        uint8_t *bp; PUT(bp, in->read_hp, R); d.read_hp = bp;
-        PUT(up, in->read_call_off, R + 1); d.read_call_off = up;
+        PUTA(p, aln ? nullptr : read_win.data(), R); d.read_win = p;
+        uint8_t *bp; PUTA(bp, in->read_hp, R); d.read_hp = bp;
+        PUTA(up, in->read_call_off, R + 1); d.read_call_off = up;
         PUTA(p, cpos, N); d.call_pos = p;
         PUTA(bp, ccat, N); d.call_cat = bp;
         // greedy problems heaviest first (reads per window, direction 1 --
@@ -444,7 +477,11 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     // one I/O block: the counters zeroed before a run (status, arena
     // counters, fallback counter) followed by everything copied back after it,
     // so a step costs one memset and one D2H copy
-    b->io_bytes = PF_IO_HDR + 40ull * W + R;
+    b->o_wro = PF_IO_HDR + 40ull * W;
+    b->o_rrec = b->o_wro + (aln ? 4ull * (W + 1) : 0ull);
+    b->o_hpfwd = b->o_rrec + (aln ? 4ull * R : 0ull);
+    b->o_hpraw = b->o_hpfwd + R;
+    b->io_bytes = b->o_hpraw + (aln ? R : 0ull);
     ALLOC(b->io, b->io_bytes);
     d.status = reinterpret_cast<uint32_t *>(b->io);
     {
@@ -456,7 +493,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     d.table = reinterpret_cast<int32_t *>(b->io + PF_IO_HDR);
     d.win_S = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 32ull * W);
     d.win_nreads = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 36ull * W);
-    d.hp_fwd = b->io + PF_IO_HDR + 40ull * W;
+    d.hp_fwd = b->io + b->o_hpfwd;
     ALLOC(d.site_pos, site_total);
     ALLOC(d.st1_pos, site_total);
     ALLOC(d.site_q1, site_total);
@@ -524,7 +561,7 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         if (a->win_rec_off[w + 1] < a->win_rec_off[w]) return PF_ERR_ARG;
     // record slices: monotone offsets, SEQ long enough for l_qseq (checked
     // per record in parallel; the slice offsets are a prefix sum)
-    std::vector<uint64_t> seq_off(n + 1), scr_off(n + 1);
+    std::vector<uint64_t> seq_off(n + 1), scr_off(n + 1), tbound(n);
     std::vector<int> prc(17, 0);
     par_for(n, [&](uint64_t lo, uint64_t hi) {
         int rc = 0;
@@ -552,6 +589,7 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
             const uint64_t mln = a->ml_off[r + 1] - a->ml_off[r], mlen = a->mm_off[r + 1] - a->mm_off[r];
             const uint64_t bound = mln ? mln : (mlen + 1) / 2;
             scr_off[r] = bound > PF_K0_TCAP ? bound : 0;       // ranks, then triggers in place
+            tbound[r] = bound;                                 // >= the record's triggers (and explicit calls)
         }
         if (rc) __atomic_store_n(&prc[rc == PF_ERR_LIMIT ? 1 : 0], 1, __ATOMIC_RELAXED);
     });
@@ -637,91 +675,90 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         for (uint32_t r = 0; r < n; r++) ord[r] = r;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return a->l_qseq[x] > a->l_qseq[y]; });
         PUT(p32, ord.data(), n); ld.order = p32;
+        PUT(p8, a->hp, n); ld.hp = p8;
+        // K0's per-record output
         ALLOC(p32, n); ld.rec_n = p32;
-        ALLOC(p32, n); ld.rec_nd = p32;
-        ALLOC(p32, n); ld.rec_read = p32;
+        ALLOC(p64, n); ld.rec_coff = p64;
+        ALLOC(p32, n); ld.rec_start = p32;
+        ALLOC(p32, n); ld.rec_end = p32;
+        ALLOC(p32, n); ld.rec_first = p32;
+        ALLOC(p32, n); ld.rec_last = p32;
+        // window of each record, records per window, per-window totals (kept
+        // then calls: one memset per run)
+        std::vector<uint32_t> rw(n);
+        for (uint32_t w = 0; w < W; w++)
+            for (uint32_t r = a->win_rec_off[w]; r < a->win_rec_off[w + 1]; r++) rw[r] = w;
+        PUT(p32, rw.data(), n); ld.rec_win = p32;
+        PUT(p32, a->win_rec_off, W + 1); ld.win_rec_off = p32;
+        ALLOC(p32, 2ull * W); ld.win_kept = p32; ld.win_calls = p32 + W;
+        ALLOC(p64, W + 1); ld.win_call_off = p64;
         unsigned long long *pc; ALLOC(pc, PF_K0_NCTR); ld.ctr = pc; b->k0_ctr = pc;
-        ALLOC(p32, 1); ld.status = p32;
+        if (hipMemset(pc, 0, PF_K0_NCTR * 8) != hipSuccess) return fail(PF_ERR_HIP);
     }
-    // ---- count pass: which records are kept, how many calls each
-    std::vector<uint32_t> rec_n(n);
-    uint32_t st = 0;
-    HIPCHK(hipMemsetAsync(ld.status, 0, 4, ctx->stream));
-    HIPCHK(hipMemsetAsync(ld.ctr, 0, PF_K0_NCTR * 8, ctx->stream));
-    if (n) {
-        hipLaunchKernelGGL(pf_k0_load<0>, dim3((n + PF_K0_WAVES - 1) / PF_K0_WAVES), dim3(PF_K0_WAVES * 64), 0,
-                           ctx->stream, ld);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(rec_n.data(), ld.rec_n, 4ull * n, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    HIPCHK(hipMemcpyAsync(&st, ld.status, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    if (getenv("PF_DEBUG_FALLBACK")) {
-        unsigned long long c[PF_K0_NCTR];
-        HIPCHK(hipMemcpy(c, ld.ctr, sizeof(c), hipMemcpyDeviceToHost));
-        fprintf(stderr, "[D::pomfret_amd] K0: seq-path %llu, unsorted %llu, implicit %llu, bad MM %llu, dup chunks %llu\n",
-                c[0], c[1], c[2], c[3], c[4]);
-    }
-    {
-        // write mode: scratch slices only for the C+m lists longer than the LDS list
-        std::vector<uint32_t> nd(n);
-        if (n) HIPCHK(hipMemcpy(nd.data(), ld.rec_nd, 4ull * n, hipMemcpyDeviceToHost));
-        uint64_t sc2 = 0;
-        for (uint32_t r = 0; r < n; r++) {
-            scr_off[r] = sc2;
-            if (nd[r] > PF_K0_TCAP) sc2 += nd[r];
-        }
-        scr_off[n] = sc2;
-        free_arena(b, (void *)ld.scr);
-        free_arena(b, (void *)ld.scr_off);
-        uint32_t *p32; ALLOC(p32, sc2 ? sc2 : 1); ld.scr = p32;
-        uint64_t *p64; PUT(p64, scr_off.data(), n + 1); ld.scr_off = p64;
-    }
-    if (st & PF_ST_FATAL_CIGAR) return fail(PF_ERR_ARG);   // the reference exits (blockjoin.c:776-779)
-    if (st & PF_ST_POS_LIMIT) return fail(PF_ERR_LIMIT);    // pos<<3 packing (3398)
-    // ---- kept reads -> the batch's read arrays (host side: offsets, tags)
-    std::vector<uint32_t> rec_read(n, PF_NONE), win_read_off(W + 1, 0);
-    std::vector<uint64_t> call_off(1, 0);
-    std::vector<uint8_t> read_hp;
-    uint32_t R = 0;
+    // ---- capacities: reads <= records; calls <= the records' trigger bounds
+    // (implicit-canonical reads may add more: the arenas grow on overflow)
+    std::vector<uint64_t> win_calls(W, 0);
+    uint64_t tb_total = 0;
     for (uint32_t w = 0; w < W; w++) {
-        for (uint32_t r = a->win_rec_off[w]; r < a->win_rec_off[w + 1]; r++) {
-            if (rec_n[r] == PF_NONE) continue;
-            rec_read[r] = R++;
-            b->h_rec_of_read.push_back(r);
-            read_hp.push_back(a->hp[r]);
-            call_off.push_back(call_off.back() + rec_n[r]);
-        }
-        win_read_off[w + 1] = R;
+        for (uint32_t r = a->win_rec_off[w]; r < a->win_rec_off[w + 1]; r++) win_calls[w] += tbound[r];
+        tb_total += win_calls[w];
     }
-    b->W = W; b->R = R; b->N = call_off.back();
-    b->h_win_read_off = win_read_off;
-    b->h_read_hp = read_hp;
-    b->n_launch = b->n_finish = 0;
+    // static staging slices (the trigger bounds), then a bump-allocated tail
+    // for implicit-canonical reads
+    std::vector<uint64_t> so_(n + 1, 0);
+    for (uint32_t r = 0; r < n; r++) so_[r + 1] = so_[r] + tbound[r];
+    uint64_t tail = 65536 + tb_total / 64;
+    uint64_t call_cap = tb_total + 4096;
+    if (getenv("PF_TEST_TIGHT")) {              // tests: every array starts too small, grows, re-runs
+        tail = 16;
+        call_cap = 64;
+        std::fill(win_calls.begin(), win_calls.end(), 0ull);
+        std::fill(so_.begin(), so_.end(), 0ull);        // every record takes the bump path
+    }
+    ld.stage_cap = so_[n] + tail;
     {
-        uint32_t *p32; PUT(p32, rec_read.data(), n); ld.rec_read = p32;
+        uint64_t *p64; PUT(p64, so_.data(), n + 1); ld.stage_off = p64;
+        uint32_t *p32; ALLOC(p32, ld.stage_cap); ld.stage_pos = p32;
+        uint8_t *p8; ALLOC(p8, ld.stage_cap); ld.stage_cat = p8;
     }
+    b->W = W; b->R = n; b->N = call_cap;
+    b->n_recs = n;
+    b->n_launch = b->n_finish = 0;
     pf_window_batch_t in;
     memset(&in, 0, sizeof(in));
-    in.n_windows = W; in.n_reads = R; in.n_calls = b->N;
-    in.win_start = a->win_start; in.win_end = a->win_end; in.win_read_off = win_read_off.data();
+    in.n_windows = W; in.n_reads = n; in.n_calls = b->N;
+    in.win_start = a->win_start; in.win_end = a->win_end; in.win_read_off = a->win_rec_off;
     in.win_cov_sel = a->win_cov_sel; in.win_cov_rt = a->win_cov_rt; in.win_n_cand = a->win_n_cand;
-    in.read_hp = read_hp.data();
-    in.read_call_off = call_off.data();
-    rc = check_windows(cfg, &in);
+    rc = check_windows(cfg, &in);                  // records per window bound the reads per window
     if (rc) return fail(rc);
     pf_dbatch_t *res = nullptr;
-    rc = batch_build(b, &in, nullptr, nullptr, nullptr, nullptr, &res);
+    rc = batch_build(b, &in, nullptr, nullptr, nullptr, nullptr, win_calls.data(), &res);
     if (rc) return rc;                                      // batch_build freed b
-    // K0's write mode fills the batch's arrays; it shares the batch's status word
-    ld.read_call_off = b->d.read_call_off;
-    ld.call_pos = const_cast<uint32_t *>(b->d.call_pos);
-    ld.call_cat = const_cast<uint8_t *>(b->d.call_cat);
-    ld.read_start = const_cast<uint32_t *>(b->d.read_start);
-    ld.read_end = const_cast<uint32_t *>(b->d.read_end);
-    ld.read_first = const_cast<uint32_t *>(b->d.read_first);
-    ld.read_last = const_cast<uint32_t *>(b->d.read_last);
-    ld.status = b->d.status;
+    // scan + pack fill the batch's arrays; K0 shares the batch's status word
+    pf_dev_batch &d = b->d;
+    ld.n_windows = W;
+    ld.status = d.status;
+    ld.io = b->io;
+    ld.call_cap = b->N;
+    ld.sites_cap = b->site_total;
+    ld.win_read_off = const_cast<uint32_t *>(d.win_read_off);
+    ld.io_win_read_off = reinterpret_cast<uint32_t *>(b->io + b->o_wro);
+    ld.win_site_off = const_cast<uint64_t *>(d.win_site_off);
+    ld.win_site_cap = const_cast<uint32_t *>(d.win_site_cap);
+    ld.win_par = d.win_par;
+    ld.read_start = const_cast<uint32_t *>(d.read_start);
+    ld.read_end = const_cast<uint32_t *>(d.read_end);
+    ld.read_first = const_cast<uint32_t *>(d.read_first);
+    ld.read_last = const_cast<uint32_t *>(d.read_last);
+    ld.read_win = const_cast<uint32_t *>(d.read_win);
+    ld.read_rec = reinterpret_cast<uint32_t *>(b->io + b->o_rrec);
+    ld.read_hp = const_cast<uint8_t *>(d.read_hp);
+    ld.hp_raw = b->io + b->o_hpraw;
+    ld.read_call_off = const_cast<uint64_t *>(d.read_call_off);
+    ld.call_pos = const_cast<uint32_t *>(d.call_pos);
+    ld.call_cat = const_cast<uint8_t *>(d.call_cat);
+    ld.stage_ctr = reinterpret_cast<unsigned long long *>(b->io + PF_IO_STAGE);
+    b->N = 0;                                   // calls: known once a run has finished
     *out = res;
     return PF_OK;
 #undef PUT
@@ -734,12 +771,14 @@ extern "C" int pf_batch_read_recs(const pf_dbatch_t *b, uint32_t *rec_of_read, u
         for (uint32_t i = 0; i < b->R; i++) rec_of_read[i] = i;
         return PF_OK;
     }
+    if (!b->have_map) return PF_ERR_ARG;             // known once a run has finished
     memcpy(rec_of_read, b->h_rec_of_read.data(), 4ull * b->R);
     return PF_OK;
 }
 
 // enqueue one run of the kernels on the context's stream, timing events and
-// results into host slot `slot` (stages < 3: debug runs without the D2H)
+// results into host slot `slot`.  stages < 3 are debug runs without the D2H:
+// 0 stops after the loader (K0, scan, pack), 1 after K12, 2 after K2.
 static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     pf_ctx *c = b->ctx;
     pf_dev_batch &d = b->d;
@@ -747,8 +786,8 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(b->io, 0, PF_IO_HDR, st));
     if (b->W == 0) { HIPCHK(hipEventRecord(b->done[slot], st)); return PF_OK; }
-    static int attr_done = 0;
-    if (!attr_done) {
+    // the greedy kernels' dynamic LDS limit, raised per context when a batch needs more
+    if (d.lds_bytes > c->k3_lds_set) {
         hipError_t e = hipFuncSetAttribute((const void *)pf_k3_greedy,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes);
         if (e == hipSuccess)
@@ -758,38 +797,48 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
             fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u B dynamic LDS): %s\n", d.lds_bytes,
                     hipGetErrorString(e));
             (void)hipGetLastError();
-        }
-        attr_done = 1;
+        } else c->k3_lds_set = d.lds_bytes;
     }
     (void)hipGetLastError();
     HIPCHK(hipEventRecord(b->ev[slot][0], st));
-    if (b->has_aln && b->ld.n_recs) {
-        // K0: filters + 5mC extraction of every record into the batch's read/call arrays
-        hipLaunchKernelGGL(pf_k0_load<1>, dim3((b->ld.n_recs + PF_K0_WAVES - 1) / PF_K0_WAVES),
-                           dim3(PF_K0_WAVES * 64), 0, st, b->ld);
-        HIPCHK(hipGetLastError());
+    if (b->has_aln) {
+        // K0: filters + 5mC extraction of every record into staging slices
+        HIPCHK(hipMemsetAsync(b->ld.win_kept, 0, 8ull * b->W, st));
+        if (b->ld.n_recs) {
+            hipLaunchKernelGGL(pf_k0_load, dim3((b->ld.n_recs + PF_K0_WAVES - 1) / PF_K0_WAVES),
+                               dim3(PF_K0_WAVES * 64), 0, st, b->ld);
+            HIPCHK(hipGetLastError());
+        }
     }
     HIPCHK(hipEventRecord(b->ev[slot][1], st));
+    if (b->has_aln) {
+        // window offsets, then the batch's read and call arrays
+        hipLaunchKernelGGL(pf_k0_scan, dim3(1), dim3(PF_SCAN_THREADS), 0, st, b->ld);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(pf_k0_pack, dim3(b->W), dim3(PF_PACK_THREADS), 0, st, b->ld);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(b->ev[slot][2], st));
     if (stages < 1) return PF_OK;
     hipLaunchKernelGGL(pf_k12_sites_methmers, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][2], st));
+    HIPCHK(hipEventRecord(b->ev[slot][3], st));
     if (stages < 2) return PF_OK;
     // fallback reads only (usually none): a grid-stride kernel over K12's list
     const uint64_t waves = 2ull * b->R;
     const uint32_t g2 = (uint32_t)std::min<uint64_t>((waves + PF_K2_WAVES - 1) / PF_K2_WAVES, 512);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][3], st));
+    HIPCHK(hipEventRecord(b->ev[slot][4], st));
     if (stages < 3) return PF_OK;
     hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][4], st));
+    HIPCHK(hipEventRecord(b->ev[slot][5], st));
     // deferred problems (usually none): a grid-stride kernel over the main kernel's list
     hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_bytes,
                        st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][5], st));
+    HIPCHK(hipEventRecord(b->ev[slot][6], st));
     HIPCHK(hipMemcpyAsync(b->h_io[slot], b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(b->done[slot], st));
     return PF_OK;
@@ -814,14 +863,92 @@ static int grow(pf_dbatch *b, uint8_t **buf, uint64_t *cap, uint64_t need) {
     return PF_OK;
 }
 
+// replace a typed device array by a larger one (contents are not kept: every
+// run rewrites the arrays that grow)
+template <typename T>
+static int realloc_arr(pf_dbatch *b, T **p, uint64_t n) {
+    free_arena(b, (void *)*p);
+    *p = nullptr;
+    return dev_alloc(b, p, n);
+}
+
+// grow what a run found too small (status bits) to what it needed
+static int grow_for(pf_dbatch *b, uint32_t stt, const IoView &v) {
+    pf_dev_batch &d = b->d;
+    pf_load_dev &ld = b->ld;
+    int rc = 0;
+    if (stt & PF_ST_KEYS_OVF) {
+        uint8_t *p = (uint8_t *)d.keys;
+        uint64_t capb = d.keys_cap * 4;
+        rc = grow(b, &p, &capb, v.ctr[0] * 4);
+        d.keys = (uint32_t *)p; d.keys_cap = capb / 4;
+    }
+    if (!rc && (stt & PF_ST_BIG_OVF)) rc = grow(b, &d.big, &d.big_cap, v.ctr[1]);
+    if (!rc && (stt & PF_ST_SCR_OVF)) rc = grow(b, &d.scr, &d.scr_cap, v.ctr[2]);
+    if (!rc && (stt & PF_ST_STAGE_OVF)) {
+        // v.stage: the bump-allocated tail the run needed, after the static slices
+        uint64_t base = 0;
+        if (hipMemcpy(&base, ld.stage_off + ld.n_recs, 8, hipMemcpyDeviceToHost) != hipSuccess) return PF_ERR_HIP;
+        const uint64_t need = base + v.stage;
+        const uint64_t cap = std::max<uint64_t>(need + v.stage / 8 + 4096, ld.stage_cap + (ld.stage_cap - base));
+        rc = realloc_arr(b, &ld.stage_pos, cap);
+        if (!rc) rc = realloc_arr(b, &ld.stage_cat, cap);
+        if (!rc) ld.stage_cap = cap;
+    }
+    if (!rc && (stt & PF_ST_CALL_OVF)) {
+        const uint64_t cap = v.N + v.N / 8 + 4096;
+        rc = realloc_arr(b, &ld.call_pos, cap);
+        if (!rc) rc = realloc_arr(b, &ld.call_cat, cap);
+        if (!rc) { d.call_pos = ld.call_pos; d.call_cat = ld.call_cat; ld.call_cap = cap; }
+    }
+    if (!rc && (stt & PF_ST_SITES_OVF)) {
+        const uint64_t cap = v.sites + v.sites / 8 + 1024;
+        rc = realloc_arr(b, &d.site_pos, cap);
+        if (!rc) rc = realloc_arr(b, &d.st1_pos, cap);
+        if (!rc) rc = realloc_arr(b, &d.site_q1, cap);
+        if (!rc) rc = realloc_arr(b, &d.len0, cap);
+        if (!rc) rc = realloc_arr(b, &d.len1, cap);
+        if (!rc) { b->site_total = cap; ld.sites_cap = cap; }
+    }
+    return rc;
+}
+
+// One finished run's status: 0 done, 1 grown (run it again), < 0 an error.
+static int settle_status(pf_dbatch *b, uint32_t stt, const IoView &v, int attempt) {
+    if (stt == 0) return 0;
+    if (stt & PF_ST_FATAL_CIGAR) return PF_ERR_ARG;   // the reference exits (blockjoin.c:776-779)
+    if (stt & PF_ST_POS_LIMIT) return PF_ERR_LIMIT;    // pos<<3 packing (3398)
+    if (attempt >= 6 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF)) || !(stt & PF_GROWABLE)) {
+        fprintf(stderr, "[E::pomfret_amd] device status 0x%x\n", stt);
+        return PF_ERR_INTERNAL;
+    }
+    // an array overflowed: drain the stream (a later run in flight used the
+    // same arrays and re-runs itself when finished), grow, re-run
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    const int rc = grow_for(b, stt, v);
+    return rc ? rc : 1;
+}
+
+// the run's sizes (record level: reads, calls and the read -> record map)
+static void note_sizes(pf_dbatch *b, const IoView &v) {
+    if (!b->has_aln) return;
+    b->R = v.R;
+    b->N = v.N;
+    if (!b->have_map) {
+        b->h_rec_of_read.assign(v.rrec, v.rrec + v.R);
+        b->have_map = true;
+    }
+}
+
 extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_t *out) {
     if (!ctx || !b || !out || b->ctx != ctx || b->n_finish == b->n_launch) return PF_ERR_ARG;
     pf_ctx *c = ctx;
     const int slot = (int)(b->n_finish % PF_SLOTS);
-    const IoView v = io_view(b, slot);
+    IoView v;
     b->n_finish++;
     for (int attempt = 0;; attempt++) {
         HIPCHK(hipEventSynchronize(b->done[slot]));
+        v = io_view(b, slot);                      // the header's sizes are read here
         if (b->W) {
             for (int i = 0; i < PF_NKERN; i++)
                 (void)hipEventElapsedTime(&c->last_ms[i], b->ev[slot][i], b->ev[slot][i + 1]);
@@ -831,32 +958,49 @@ extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_
         if (getenv("PF_DEBUG_FALLBACK"))
             fprintf(stderr, "[D::pomfret_amd] status 0x%x, K2 fallback reads %u, K3 deferred problems %u\n", stt,
                     *v.fb, *v.k3fb);
-        if (stt == 0) break;
-        if (attempt >= 3 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF | PF_ST_FATAL_CIGAR | PF_ST_POS_LIMIT))) {
-            fprintf(stderr, "[E::pomfret_amd] device status 0x%x\n", stt);
-            return PF_ERR_INTERNAL;
-        }
-        // an arena overflowed: drain the stream (a later run in flight used
-        // the same arenas and re-runs itself when finished), grow, re-run
-        HIPCHK(hipStreamSynchronize(c->stream));
-        pf_dev_batch &d = b->d;
-        int rc = 0;
-        if (stt & PF_ST_KEYS_OVF) {
-            uint8_t *p = (uint8_t *)d.keys;
-            uint64_t capb = d.keys_cap * 4;
-            rc = grow(b, &p, &capb, v.ctr[0] * 4);
-            d.keys = (uint32_t *)p; d.keys_cap = capb / 4;
-        }
-        if (!rc && (stt & PF_ST_BIG_OVF)) rc = grow(b, &d.big, &d.big_cap, v.ctr[1]);
-        if (!rc && (stt & PF_ST_SCR_OVF)) rc = grow(b, &d.scr, &d.scr_cap, v.ctr[2]);
-        if (rc) return rc;
-        rc = enqueue(b, slot);
+        const int s = settle_status(b, stt, v, attempt);
+        if (s < 0) return s;
+        if (s == 0) break;
+        const int rc = enqueue(b, slot);
         if (rc) return rc;
     }
+    if (b->W == 0) return PF_OK;
+    note_sizes(b, v);
     if (out->win_n_reads)
         for (uint32_t w = 0; w < b->W; w++) out->win_n_reads[w] = v.nreads[w];
-    pf_decide_windows(b->W, b->h_win_read_off.data(), v.S, v.table, b->h_read_hp.data(), v.hp_fwd, out);
+    if (b->has_aln) pf_decide_windows(b->W, v.wro, v.S, v.table, v.hp_raw, v.hp_fwd, out);
+    else pf_decide_windows(b->W, b->h_win_read_off.data(), v.S, v.table, b->h_read_hp.data(), v.hp_fwd, out);
     return PF_OK;
+}
+
+// A synchronous debug run up to `stages` (see enqueue), re-run until no array
+// overflows; the header's sizes are noted.
+static int run_debug(pf_dbatch *b, int stages) {
+    if (b->n_launch != b->n_finish) return PF_ERR_ARG;       // a run is in flight
+    std::vector<uint8_t> hdr(PF_IO_HDR);
+    for (int attempt = 0;; attempt++) {
+        int rc = enqueue(b, 0, stages);
+        if (rc) return rc;
+        HIPCHK(hipStreamSynchronize(b->ctx->stream));
+        if (b->W == 0) return PF_OK;
+        HIPCHK(hipMemcpy(hdr.data(), b->io, PF_IO_HDR, hipMemcpyDeviceToHost));
+        const IoView v = io_view(b, hdr.data());
+        const int s = settle_status(b, v.status[0], v, attempt);
+        if (s < 0) return s;
+        if (s == 0) {
+            if (b->has_aln) {
+                b->R = v.R;
+                b->N = v.N;
+                if (!b->have_map && b->R) {
+                    b->h_rec_of_read.resize(b->R);
+                    HIPCHK(hipMemcpy(b->h_rec_of_read.data(), b->io + b->o_rrec, 4ull * b->R, hipMemcpyDeviceToHost));
+                    b->have_map = true;
+                }
+                if (!b->R) b->have_map = true;
+            }
+            return PF_OK;
+        }
+    }
 }
 
 extern "C" int pf_methphase_run(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_t *out) {
@@ -883,12 +1027,9 @@ extern "C" int pf_methphase_windows(int device, const pf_cfg_t *cfg, const pf_wi
 extern "C" int pf_batch_debug_sites(pf_dbatch_t *b, uint32_t w, int dir, uint32_t *real,
                                     uint32_t *starts, uint8_t *lens, uint32_t cap) {
     if (!b || w >= b->W || dir < 0 || dir > 1) return PF_ERR_ARG;
-    if (b->n_launch != b->n_finish) return PF_ERR_ARG;       // a run is in flight
-    int rc = enqueue(b, 0, 1);
+    const int rc = run_debug(b, 1);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    uint32_t S = 0, off_cap[1];
-    (void)off_cap;
+    uint32_t S = 0;
     HIPCHK(hipMemcpy(&S, b->d.win_S + w, 4, hipMemcpyDeviceToHost));
     uint64_t off = 0;
     HIPCHK(hipMemcpy(&off, b->d.win_site_off + w, 8, hipMemcpyDeviceToHost));
@@ -904,13 +1045,8 @@ extern "C" int pf_batch_debug_sites(pf_dbatch_t *b, uint32_t w, int dir, uint32_
 extern "C" int64_t pf_batch_debug_methmers(pf_dbatch_t *b, int dir, uint32_t *mmr_n, uint32_t *mmr_start,
                                            uint32_t *keys, uint64_t cap) {
     if (!b || dir < 0 || dir > 1) return PF_ERR_ARG;
-    if (b->n_launch != b->n_finish) return PF_ERR_ARG;       // a run is in flight
-    int rc = enqueue(b, 0, 2);
+    const int rc = run_debug(b, 2);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    uint32_t st = 0;
-    HIPCHK(hipMemcpy(&st, b->d.status, 4, hipMemcpyDeviceToHost));
-    if (st) return PF_ERR_INTERNAL;
     std::vector<uint32_t> n(2ull * b->R), s0(2ull * b->R);
     std::vector<uint64_t> off(2ull * b->R);
     if (b->R) {
@@ -968,14 +1104,10 @@ extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms
 extern "C" int64_t pf_batch_debug_calls(pf_dbatch_t *b, uint64_t *call_off, uint32_t *pos, uint8_t *cat,
                                         uint32_t *first, uint32_t *last, uint64_t cap) {
     if (!b || !call_off || !pos || !cat || !first || !last) return PF_ERR_ARG;
-    if (b->n_launch != b->n_finish) return PF_ERR_ARG;       // a run is in flight
-    if (b->N > cap) return PF_ERR_ARG;
-    int rc = enqueue(b, 0, 0);
+    const int rc = run_debug(b, 0);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(b->ctx->stream));
-    uint32_t st = 0;
-    HIPCHK(hipMemcpy(&st, b->d.status, 4, hipMemcpyDeviceToHost));
-    if (st) return PF_ERR_INTERNAL;
+    if (b->N > cap) return PF_ERR_ARG;
+    if (b->R == 0) { call_off[0] = 0; return 0; }
     HIPCHK(hipMemcpy(call_off, b->d.read_call_off, 8ull * (b->R + 1), hipMemcpyDeviceToHost));
     if (b->N) {
         HIPCHK(hipMemcpy(pos, b->d.call_pos, 4ull * b->N, hipMemcpyDeviceToHost));

@@ -953,6 +953,19 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
         sh_base[1] = bb;
     }
     __syncthreads();
+    if (sh_base[0] + 2ull * tot_keys > d.keys_cap) {
+        // the key arena is full (status set above; the host grows it and
+        // re-runs): this window writes no keys and K3 skips it (S = 0)
+        for (uint32_t i = tid; i < R; i += NT) {
+            const uint32_t r = r0 + i;
+            d.mmr_n[2 * r] = 0; d.mmr_n[2 * r + 1] = 0;
+            d.mmr_start[2 * r] = 0; d.mmr_start[2 * r + 1] = 0;
+            d.mmr_off[2 * r] = 0; d.mmr_off[2 * r + 1] = 0;
+            d.big_off[r] = ~0ull;
+        }
+        if (tid == 0) d.win_S[w] = 0;
+        return;
+    }
     uint64_t kcarry = sh_base[0], bcarry = sh_base[1];
     for (uint32_t i0 = 0; i0 < R; i0 += NT) {
         const uint32_t i = i0 + tid;

@@ -1,12 +1,24 @@
 /*
- * pf_load.h -- device-side layout of kernel K0 (the window loader on the GPU).
+ * pf_load.h -- device-side layout of kernel K0 (the window loader on the GPU)
+ * and of its pack step.
  *
  * K0 applies load_reads_given_interval's read filters (blockjoin.c:1079-1085),
  * decodes the 5mC calls of the MM/ML tags (fill_read_meth_record_from_bam_line,
  * 794-908) and maps them to the reference through the CIGAR, including the
  * implicit-canonical calls (get_mod_poss_on_ref, 605-792).  One wavefront per
- * BAM record.  Count mode sizes the batch at upload; write mode fills the
- * resident batch's read and call arrays on every run.
+ * BAM record.  Every run of a record-level batch sizes itself on the device:
+ *   K0    decodes each record once; a kept record bump-allocates its call
+ *         slice in the staging arena (exactly its trigger count, plus one
+ *         position per two read bases for implicit-canonical reads) and adds
+ *         itself to its window's kept/call totals;
+ *   scan  one workgroup: window totals -> window read / call / site offsets
+ *         (capacity checks; on overflow every window is emptied and the host
+ *         grows the arrays and re-runs);
+ *   pack  one workgroup per window: kept records -> read indices in record
+ *         order (the reference's rs->a order), the batch's read arrays, and
+ *         each read's calls copied from its staging slice to the window's
+ *         contiguous run.
+ * No count pass and no host round trip sit between the records and K12.
  */
 #ifndef PF_LOAD_H
 #define PF_LOAD_H
@@ -17,10 +29,16 @@
 #define PF_K0_CB 128              /* read positions per implicit-mode chunk (4 per lane, half the wave) */
 #define PF_K0_EC (PF_K0_CB / 2)   /* explicit / implicit calls per chunk (CpGs are >= 2 apart) */
 #define PF_K0_SEQ_ALIGN 16        /* per-record SEQ slices are 16-byte aligned and padded */
+#define PF_PACK_THREADS 1024
+#define PF_SCAN_THREADS 1024
 
-/* status bits of K0 (share the batch status word with pf_device.h's) */
+/* status bits of K0 and the pack step (share the batch status word with
+ * pf_device.h's) */
 #define PF_ST_FATAL_CIGAR 32u     /* H/=/X/P/... reached in the CIGAR walk: exit(1) at 776-779 */
 #define PF_ST_POS_LIMIT   64u     /* a call position >= 2^29 */
+#define PF_ST_STAGE_OVF  128u     /* K0's call staging arena is too small (grow, re-run) */
+#define PF_ST_CALL_OVF   256u     /* the batch call arrays are too small (grow, re-run) */
+#define PF_ST_SITES_OVF  512u     /* the batch site arrays are too small (grow, re-run) */
 
 /* counters (ctr[]) */
 #define PF_K0C_SEQPATH  0         /* records walked by the sequential path */
@@ -30,16 +48,26 @@
 #define PF_K0C_DUPCHUNK 4         /* emission chunks with a duplicate position */
 #define PF_K0_NCTR 16             /* [8..15]: per-phase cycles of the diagnostic build */
 
+/* I/O block header fields of the record-level path (byte offsets; the
+ * header layout is in pf_api.hip) */
+#define PF_IO_STAGE 48            /* u64 staging arena bump pointer (K0)   */
+#define PF_IO_R     56            /* u32 kept reads (scan)                   */
+#define PF_IO_N     64            /* u64 calls (scan)                        */
+#define PF_IO_SITES 72            /* u64 site slots the windows need (scan)  */
+
 struct pf_load_dev {
-    uint32_t n_recs;
+    uint32_t n_recs, n_windows;
     uint32_t min_mapq, min_len;
     uint32_t lo, hi;                 /* uint8_t in the reference (799) */
     uint32_t force_seq;              /* test override: every record through the sequential path */
     const uint32_t *order;           /* [n_recs] record of each wave slot: longest reads first */
+    const uint32_t *rec_win;         /* [n_recs] window of each record */
+    const uint32_t *win_rec_off;     /* [W+1] records of each window */
     const uint16_t *flag;
     const uint8_t *mapq;
     const uint32_t *pos, *l_qseq;
     const float *de;
+    const uint8_t *hp;               /* [n_recs] get_hp_from_aln (910-923) or the -u table */
     const uint64_t *cigar_off;
     const uint32_t *cigar;
     const uint64_t *seq_off;         /* 16-byte aligned device offsets */
@@ -50,17 +78,33 @@ struct pf_load_dev {
     const uint8_t *ml;
     const uint64_t *scr_off;         /* [n_recs+1] trigger-list scratch slices (u32 units); empty = LDS */
     uint32_t *scr;
-    /* count mode */
+    /* K0 output, per record */
     uint32_t *rec_n;                 /* calls of each kept record, PF_NONE when dropped */
-    uint32_t *rec_nd;                /* 5mC skip counts of the record's C+m entry (write-mode scratch sizing) */
-    /* write mode */
-    const uint32_t *rec_read;        /* read index of each record or PF_NONE */
-    const uint64_t *read_call_off;
-    uint32_t *call_pos;
-    uint8_t *call_cat;
-    uint32_t *read_start, *read_end, *read_first, *read_last;
+    uint64_t *rec_coff;              /* its slice of the staging arena */
+    uint32_t *rec_start, *rec_end, *rec_first, *rec_last;
+    uint32_t *stage_pos;             /* staging arena: per-record call slices */
+    uint8_t *stage_cat;
+    const uint64_t *stage_off;       /* [n_recs+1] static slices: each record's trigger bound */
+    uint64_t stage_cap;              /* slots; [stage_off[n_recs], stage_cap) is bump-allocated */
+    unsigned long long *stage_ctr;   /* bump pointer of that tail (I/O block header, zeroed per run) */
+    uint32_t *win_kept, *win_calls;  /* [W] per-window totals (atomics, zeroed per run) */
     uint32_t *status;
     unsigned long long *ctr;         /* PF_K0_NCTR */
+    /* scan + pack output: the batch's window / read / call arrays */
+    uint8_t *io;                     /* I/O block (header totals, bump pointer) */
+    uint64_t call_cap, sites_cap;
+    uint32_t *win_read_off;          /* [W+1] device copy the kernels read */
+    uint32_t *io_win_read_off;       /* [W+1] I/O block copy for the host epilogue */
+    uint64_t *win_site_off;          /* [W] */
+    uint32_t *win_site_cap;          /* [W] */
+    const int32_t *win_par;          /* [W*4] cov_sel first */
+    uint64_t *win_call_off;          /* [W+1] scratch */
+    uint32_t *read_start, *read_end, *read_first, *read_last, *read_win;
+    uint32_t *read_rec;              /* [R] record of each read (I/O block) */
+    uint8_t *read_hp, *hp_raw;       /* read_hp: the kernels' copy; hp_raw: the I/O block's */
+    uint64_t *read_call_off;         /* [R+1] */
+    uint32_t *call_pos;
+    uint8_t *call_cat;
 };
 
 #endif

@@ -803,7 +803,7 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
     return true;
 }
 
-template <int MODE, typename TP>
+template <typename TP>
 DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, uint32_t cap) {
     const uint32_t len = d.l_qseq[r];
     const bool rev = (d.flag[r] & 16u) != 0;
@@ -827,7 +827,6 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
         if (okmm && t.nd > cap) okmm = false;       // only a malformed tag lists more calls than its size allows
         if (okmm && t.nd) okmm = k0_mm_ranks(gw, mmg, mis, t, rev, TB, lane);
     }
-    if (MODE == 0 && lane == 0) d.rec_nd[r] = okmm ? t.nd : 0u;
     wsync();
     bool past = false;
     if (okmm && t.nd) {                               // the C+m entry's ML values ride in the ranks' top byte
@@ -849,14 +848,32 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     nT = uni(nT);
 
     if (ncig == 0 || nT == 0) {                       // get_mod_poss_on_ref returns 0: read dropped
-        if (MODE == 0 && lane == 0) d.rec_n[r] = PF_NONE;
+        if (lane == 0) d.rec_n[r] = PF_NONE;
         return;
     }
-    const uint32_t ri = MODE ? d.rec_read[r] : 0;
+    // The record's call slice in the staging arena: its static slice (the
+    // upload's trigger bound; each trigger pushes at most once), or, for an
+    // implicit-canonical read -- which also pushes the CpGs the canonical scan
+    // adds, CpG C's being >= 2 read bases apart -- a slice bump-allocated from
+    // the arena's tail.  A full tail flags the batch: the bump pointer keeps
+    // counting, so it ends at the size the run needs, and the host grows the
+    // arena to that and re-runs.
+    const uint64_t s_lo = d.stage_off[r], s_hi = d.stage_off[r + 1];
+    uint64_t cb = s_lo;
+    if (implicit || (uint64_t)nT > s_hi - s_lo) {
+        const uint64_t need = (uint64_t)nT + (uint64_t)(len + 1) / 2;
+        unsigned long long t = 0;
+        if (lane == 0) t = atomicAdd(d.stage_ctr, (unsigned long long)need);
+        cb = d.stage_off[d.n_recs] + (((uint64_t)uni((uint32_t)(t >> 32)) << 32) | uni((uint32_t)t));
+        if (cb + need > d.stage_cap) {
+            if (lane == 0) { atomicOr(d.status, PF_ST_STAGE_OVF); d.rec_n[r] = PF_NONE; }
+            return;
+        }
+    }
     K0Out o;
     o.n = 0; o.first = 0; o.last = 0; o.sorted = 1; o.lim = 0;
-    o.pos = MODE ? d.call_pos + d.read_call_off[ri] : nullptr;
-    o.cat = MODE ? d.call_cat + d.read_call_off[ri] : nullptr;
+    o.pos = d.stage_pos + cb;
+    o.cat = d.stage_cat + cb;
     if (implicit && d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_IMPLICIT], 1ull);
 
     const uint32_t qs = d.pos[r];
@@ -866,24 +883,19 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
         if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_SEQPATH], 1ull);
         K0Out s = o;
         bool f = false;
-        if (lane == 0) k0_walk_seq<MODE>(cig, ncig, qs, rev, TB, nT, implicit ? seq : nullptr, len, s, f);
+        if (lane == 0) k0_walk_seq<1>(cig, ncig, qs, rev, TB, nT, implicit ? seq : nullptr, len, s, f);
         k0_bcast(o, s);
         fatal = uni(f ? 1u : 0u) != 0;
     } else {
-        fatal = !k0_walk<MODE>(d, L, cig, ncig, qs, rev, TB, nT, seq, len, implicit, lane, o);
+        fatal = !k0_walk<1>(d, L, cig, ncig, qs, rev, TB, nT, seq, len, implicit, lane, o);
     }
     K0_STAMP(2);
     if (fatal) {
-        if (lane == 0) atomicOr(d.status, PF_ST_FATAL_CIGAR);
-        if (MODE == 0 && lane == 0) d.rec_n[r] = PF_NONE;
+        if (lane == 0) { atomicOr(d.status, PF_ST_FATAL_CIGAR); d.rec_n[r] = PF_NONE; }
         return;
     }
     if (o.lim && lane == 0) atomicOr(d.status, PF_ST_POS_LIMIT);
-    if (MODE == 0) {
-        if (lane == 0) d.rec_n[r] = o.n;
-        return;
-    }
-    // ---- write mode: sort if needed, then the read's scalars
+    // ---- the calls in (pos, cat) order, then the record's scalars
     if (!o.sorted && o.n > 1) {
         if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_UNSORTED], 1ull);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -910,15 +922,19 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     }
     rlen = wscan(rlen, lane);
     if (lane == 63) {
-        d.read_start[ri] = qs;
-        d.read_end[ri] = qs + rlen;
-        d.read_first[ri] = o.first;
-        d.read_last[ri] = o.last;
+        d.rec_start[r] = qs;
+        d.rec_end[r] = qs + rlen;
+        d.rec_first[r] = o.first;
+        d.rec_last[r] = o.last;
+        d.rec_coff[r] = cb;
+        d.rec_n[r] = o.n;
+        const uint32_t w = d.rec_win[r];
+        atomicAdd(&d.win_kept[w], 1u);
+        atomicAdd(&d.win_calls[w], o.n);
     }
     K0_STAMP(3);
 }
 
-template <int MODE>
 __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_load(pf_load_dev d) {
     __shared__ K0W lds[PF_K0_WAVES];
     const uint32_t lane = threadIdx.x & 63u;
@@ -927,19 +943,171 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_e
     if (slot >= d.n_recs) return;
     const uint32_t r = uni(d.order[slot]);
     K0W &L = lds[wv];
-    if (MODE == 1 && d.rec_read[r] == PF_NONE) return;
     // filters (1079-1085)
     const uint32_t flag = d.flag[r];
     const bool drop = (flag & 4u) || (flag & 256u) || (flag & 2048u) || (uint32_t)d.mapq[r] < d.min_mapq ||
                       d.l_qseq[r] < 2u || d.l_qseq[r] < d.min_len || (double)d.de[r] > 0.1;
     if (drop) {
-        if (MODE == 0 && lane == 0) { d.rec_n[r] = PF_NONE; d.rec_nd[r] = 0; }
+        if (lane == 0) d.rec_n[r] = PF_NONE;
         return;
     }
     const uint64_t s0 = d.scr_off[r], s1 = d.scr_off[r + 1];
-    if (s1 == s0) k0_record<MODE>(d, L, r, lane, L.T, (uint32_t)PF_K0_TCAP);
-    else k0_record<MODE>(d, L, r, lane, d.scr + s0, (uint32_t)(s1 - s0));
+    if (s1 == s0) k0_record(d, L, r, lane, L.T, (uint32_t)PF_K0_TCAP);
+    else k0_record(d, L, r, lane, d.scr + s0, (uint32_t)(s1 - s0));
 }
 
-template __global__ void pf_k0_load<0>(pf_load_dev d);
-template __global__ void pf_k0_load<1>(pf_load_dev d);
+// ---------------------------------------------------------------------------
+// scan: window totals -> offsets of the batch's reads, calls and site slots
+// (one workgroup).  Site slots per window: calls / (2 cov_sel) + 1 (a site
+// needs >= cov_sel meth and >= cov_sel unmeth calls).  When K0's arena or
+// the batch arrays are too small every window is emptied (no later kernel
+// touches the arrays) and the needs go to the I/O header.
+template <uint32_t NT, typename T>
+DEV T blk_excl_scan(T v, T *sh, T &total) {
+    static_assert(NT % 64 == 0 && NT <= 4096, "block of whole waves");
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    constexpr uint32_t NW = NT / 64;
+    T x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        T s = lane < NW ? sh[lane] : (T)0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const T y = __shfl_up(s, o, 64);
+            if (lane >= (uint32_t)o) s += y;
+        }
+        if (lane < NW) sh[NW + lane] = s;
+    }
+    __syncthreads();
+    const T base = wid ? sh[NW + wid - 1] : (T)0;
+    total = sh[2 * NW - 1];
+    __syncthreads();
+    return base + x - v;
+}
+
+__global__ __launch_bounds__(PF_SCAN_THREADS) void pf_k0_scan(pf_load_dev d) {
+    __shared__ uint64_t sh[2 * (PF_SCAN_THREADS / 64)];
+    __shared__ uint32_t sh32[2 * (PF_SCAN_THREADS / 64)];
+    const uint32_t tid = threadIdx.x, W = d.n_windows;
+    uint32_t rc = 0;
+    uint64_t cc = 0, sc = 0;
+    for (uint32_t w0 = 0; w0 < W; w0 += PF_SCAN_THREADS) {
+        const uint32_t w = w0 + tid;
+        const uint32_t kept = w < W ? d.win_kept[w] : 0u;
+        const uint64_t calls = w < W ? (uint64_t)d.win_calls[w] : 0ull;
+        const int32_t sel = w < W ? max(d.win_par[4ull * w], 1) : 1;
+        const uint64_t slots = w < W ? calls / (2ull * (uint64_t)sel) + 1ull : 0ull;
+        uint32_t tk;
+        uint64_t tcl, ts;
+        const uint32_t ek = blk_excl_scan<PF_SCAN_THREADS, uint32_t>(kept, sh32, tk);
+        const uint64_t ec = blk_excl_scan<PF_SCAN_THREADS, uint64_t>(calls, sh, tcl);
+        const uint64_t es = blk_excl_scan<PF_SCAN_THREADS, uint64_t>(slots, sh, ts);
+        if (w < W) {
+            d.win_read_off[w] = rc + ek;
+            d.win_call_off[w] = cc + ec;
+            d.win_site_off[w] = sc + es;
+            d.win_site_cap[w] = (uint32_t)min(slots, (uint64_t)0xFFFFFFF0u);
+        }
+        rc += tk;
+        cc += tcl;
+        sc += ts;
+    }
+    const uint32_t st = __hip_atomic_load(d.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool c_ovf = cc > d.call_cap, s_ovf = sc > d.sites_cap;
+    const bool empty = c_ovf || s_ovf || (st & (PF_ST_STAGE_OVF | PF_ST_FATAL_CIGAR | PF_ST_POS_LIMIT));
+    if (tid == 0) {
+        d.win_read_off[W] = rc;
+        d.win_call_off[W] = cc;
+        *reinterpret_cast<uint32_t *>(d.io + PF_IO_R) = rc;
+        *reinterpret_cast<uint64_t *>(d.io + PF_IO_N) = cc;
+        *reinterpret_cast<uint64_t *>(d.io + PF_IO_SITES) = sc;
+        if (c_ovf) atomicOr(d.status, PF_ST_CALL_OVF);
+        if (s_ovf) atomicOr(d.status, PF_ST_SITES_OVF);
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w <= W; w += PF_SCAN_THREADS) {
+        if (empty) {
+            d.win_read_off[w] = 0;
+            if (w < W) d.win_site_cap[w] = 0;
+        }
+        d.io_win_read_off[w] = d.win_read_off[w];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// pack: one workgroup per window.  Kept records become reads in record
+// order; their scalars move to the read arrays and their calls from the
+// staging slices to the window's contiguous run (one wave per read).
+__global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
+    constexpr uint32_t NT = PF_PACK_THREADS, NW = NT / 64;
+    __shared__ uint32_t sh32[2 * NW];
+    __shared__ uint32_t l_n[NT];
+    __shared__ uint64_t l_src[NT], l_dst[NT];
+    const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t rb = d.win_read_off[w], re = d.win_read_off[w + 1];
+    const bool last = w + 1 == d.n_windows;
+    if (re == rb) {
+        if (last && tid == 0) d.read_call_off[re] = re ? d.win_call_off[d.n_windows] : 0ull;
+        return;
+    }
+    const uint32_t rec0 = d.win_rec_off[w], rec1 = d.win_rec_off[w + 1];
+    uint32_t kc = 0, ccarry = 0;
+    const uint64_t cb = d.win_call_off[w];
+    for (uint32_t i0 = rec0; i0 < rec1; i0 += NT) {
+        const uint32_t r = i0 + tid;
+        const uint32_t n = r < rec1 ? d.rec_n[r] : PF_NONE;
+        const bool keep = n != PF_NONE;
+        uint32_t tk, tc;
+        const uint32_t ek = blk_excl_scan<NT, uint32_t>(keep ? 1u : 0u, sh32, tk);
+        // per-window calls fit u32 (the window totals are u32 atomics)
+        const uint32_t ec = blk_excl_scan<NT, uint32_t>(keep ? n : 0u, sh32, tc);
+        if (keep) {
+            const uint32_t ri = rb + kc + ek;
+            const uint64_t co = cb + ccarry + ec;
+            d.read_start[ri] = d.rec_start[r];
+            d.read_end[ri] = d.rec_end[r];
+            d.read_first[ri] = d.rec_first[r];
+            d.read_last[ri] = d.rec_last[r];
+            d.read_win[ri] = w;
+            d.read_rec[ri] = r;
+            const uint8_t h = d.hp[r];
+            d.read_hp[ri] = h;
+            d.hp_raw[ri] = h;
+            d.read_call_off[ri] = co;
+            l_n[ek] = n;
+            l_src[ek] = d.rec_coff[r];
+            l_dst[ek] = co;
+        }
+        __syncthreads();
+        // one wave per read, 8 calls per lane in flight (loads before stores)
+        for (uint32_t j = wid; j < tk; j += NW) {
+            const uint32_t cn = l_n[j];
+            const uint64_t s = l_src[j], t = l_dst[j];
+            for (uint32_t c0 = 0; c0 < cn; c0 += 8 * 64) {
+                uint32_t pv[8];
+                uint8_t cv[8];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t c = c0 + u * 64 + lane;
+                    pv[u] = c < cn ? d.stage_pos[s + c] : 0u;
+                    cv[u] = c < cn ? d.stage_cat[s + c] : (uint8_t)0;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t c = c0 + u * 64 + lane;
+                    if (c < cn) { d.call_pos[t + c] = pv[u]; d.call_cat[t + c] = cv[u]; }
+                }
+            }
+        }
+        __syncthreads();
+        kc += tk;
+        ccarry += tc;
+    }
+    if (last && tid == 0) d.read_call_off[re] = d.win_call_off[d.n_windows];
+}

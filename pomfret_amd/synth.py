@@ -60,7 +60,8 @@ def make_window(spec: SynthSpec, w: int):
     if spec.gap_mix:
         gap = int(np.exp(rng.uniform(np.log(5_000), np.log(500_000))))
     stride = max(spec.window_stride, gap + 2 * spec.readback + 2 * spec.max_len + 10_000)
-    s = spec.base + w * stride
+    # windows are independent: the layout wraps below the 2^29 position limit
+    s = spec.base + (w % max(1, (400_000_000 - spec.base) // stride)) * stride
     e = s + gap
     f_lo, f_hi = max(0, s - spec.readback), e + spec.readback
     span_lo, span_hi = f_lo - spec.max_len, f_hi + spec.max_len

@@ -83,7 +83,9 @@ def make_aln_window(spec: AlnSpec, w: int):
         gap = int(np.exp(rng.uniform(np.log(5_000), np.log(500_000))))
     max_len = int(spec.max_len * spec.len_scale)
     stride = max(spec.window_stride, gap + 2 * spec.readback + 2 * max_len + 10_000)
-    s = spec.base + w * stride
+    # windows are independent: the layout wraps so that every position stays
+    # below the 2^29 limit of the call packing (a human chromosome is < 2^28)
+    s = spec.base + (w % max(1, (400_000_000 - spec.base) // stride)) * stride
     e = s + gap
     f_lo, f_hi = max(0, s - spec.readback), e + spec.readback
     span_lo, span_hi = f_lo - max_len, f_hi + max_len

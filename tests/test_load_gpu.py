@@ -35,9 +35,9 @@ def _oracle_view(oracle_lib, lcfg, aln):
 def _check_calls(oracle_lib, gpu_ctx, cfg, lcfg, aln, tag):
     b, rec_read, pos, cat, first, last = _oracle_view(oracle_lib, lcfg, aln)
     db = gpu_ctx.upload_aln(cfg, aln, lcfg)
+    off, gpos, gcat, gfirst, glast = db.debug_calls()      # K0 sizes the batch on the device
     assert db.n_reads == b.n_reads, tag
     assert np.array_equal(db.read_recs(), np.flatnonzero(rec_read != NONE)), tag
-    off, gpos, gcat, gfirst, glast = db.debug_calls()
     assert np.array_equal(off, b.read_call_off), tag
     bad = np.flatnonzero(gpos != pos)
     assert bad.size == 0, f"{tag}: call_pos differs at {bad[:5].tolist()}"
@@ -68,9 +68,35 @@ def test_handmade_sequential_path(oracle_lib, gpu_ctx, monkeypatch):
 
 def test_fatal_cigar_is_an_error(gpu_ctx):
     from pomfret_amd import Config, PomfretError
+    # a CIGAR whose query length differs from SEQ is refused at upload (htslib's bam_read1 check)
     aln = records_batch([(0, 10, [dict(seq="ACGTTCGA", cigar="6M2H", mm="C+m?,0,0;", ml=[200, 10], pos=100)])])
     with pytest.raises(PomfretError):
         gpu_ctx.upload_aln(Config(), aln, LOAD_CFG_SMALL)
+    # an X op the walk reaches is the reference's exit(1) (776-779): an error of the run
+    aln = records_batch([(0, 10, [dict(seq="ACGTTCGA", cigar="6M2X", mm="C+m?,0,0;", ml=[200, 10], pos=100)])])
+    db = gpu_ctx.upload_aln(Config(), aln, LOAD_CFG_SMALL)   # the loader runs in every run, not at upload
+    with pytest.raises(PomfretError):
+        db.run()
+    with pytest.raises(PomfretError):
+        db.debug_calls()
+    db.free()
+
+
+def test_arrays_grow_and_rerun(oracle_lib, gpu_ctx, monkeypatch):
+    """Staging arena, call arrays and site slots sized too small at upload
+    (PF_TEST_TIGHT) overflow, grow and re-run with identical results."""
+    from pomfret_amd import Config, LoadConfig
+    name, aln = CASES[0]
+    cfg, lcfg = Config.from_coverage(30, given=False), LoadConfig()
+    ref = gpu_ctx.upload_aln(cfg, aln, lcfg)
+    out_ref = ref.run()
+    ref.free()
+    monkeypatch.setenv("PF_TEST_TIGHT", "1")
+    db = gpu_ctx.upload_aln(cfg, aln, lcfg)
+    out = db.run()
+    for f in ("decision", "dir_table", "win_n_sites", "win_n_reads", "read_hp"):
+        assert np.array_equal(getattr(out_ref, f), getattr(out, f)), f
+    db.free()
 
 
 @pytest.mark.parametrize("name,aln", CASES, ids=[c[0] for c in CASES])
