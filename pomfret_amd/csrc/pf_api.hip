@@ -53,7 +53,8 @@ struct pf_ctx {
     int have_haptag;
     void *pin = nullptr;      /* pinned staging for large uploads (grown on demand) */
     size_t pin_cap = 0;
-    uint32_t k3_lds_set = 0;  /* dynamic LDS limit set on the greedy kernels of this device */
+    uint32_t k3_lds_set = 0;  /* dynamic LDS limits set on the greedy kernels of this device */
+    uint32_t k3_lds_fb_set = 0;
 };
 
 struct pf_dbatch {
@@ -514,8 +515,24 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     ALLOC(d.scr, d.scr_cap);
     ALLOC(d.stats, 16ull * W);
     ALLOC(d.prof, 80ull * W);
-    const char *lds = getenv("PF_K3_LDS");
-    d.lds_bytes = lds ? (uint32_t)atoi(lds) : 73728u;
+    // greedy kernels' dynamic LDS.  40 KB (+ ~6 KB static) fits three
+    // workgroups per CU, 72 KB two; a problem the main kernel cannot fit runs
+    // in the fallback kernel after it.  Small windows (90 % of the windows
+    // with <= 400 reads, ~30x) nearly all fit 40 KB, and the higher occupancy
+    // pays (30x: K3 2.43 -> 1.95 ms); for larger windows (60x) the heaviest
+    // problems would be deferred to a serial tail, so 72 KB
+    // (profiles/r02/k3_lds_sweep).  PF_K3_LDS (tests, tuning) sets both.
+    uint32_t lds_auto = 73728u;
+    if (W) {
+        std::vector<uint32_t> rw(W);
+        for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
+        std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
+        if (rw[(W * 9) / 10] <= 400) lds_auto = 40960u;
+    }
+    const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB");
+    d.lds_bytes = lds ? (uint32_t)atoi(lds) : lds_auto;
+    d.lds_fb = ldf ? (uint32_t)atoi(ldf) : lds ? d.lds_bytes : 73728u;
+    if (d.lds_fb < d.lds_bytes) d.lds_fb = d.lds_bytes;
     // PF_K12_CAP / PF_K12_SMAX lower the fused kernel's limits (tests use them
     // to drive reads and windows through the fallback paths)
     const char *kc = getenv("PF_K12_CAP"), *ks = getenv("PF_K12_SMAX");
@@ -786,18 +803,21 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(b->io, 0, PF_IO_HDR, st));
     if (b->W == 0) { HIPCHK(hipEventRecord(b->done[slot], st)); return PF_OK; }
-    // the greedy kernels' dynamic LDS limit, raised per context when a batch needs more
-    if (d.lds_bytes > c->k3_lds_set) {
+    // the greedy kernels' dynamic LDS limits, raised per context when a batch needs more
+    if (d.lds_bytes > c->k3_lds_set || d.lds_fb > c->k3_lds_fb_set) {
         hipError_t e = hipFuncSetAttribute((const void *)pf_k3_greedy,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes);
         if (e == hipSuccess)
             e = hipFuncSetAttribute((const void *)pf_k3_fallback, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)d.lds_bytes);
+                                    (int)d.lds_fb);
         if (e != hipSuccess) {
-            fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u B dynamic LDS): %s\n", d.lds_bytes,
-                    hipGetErrorString(e));
+            fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u / %u B dynamic LDS): %s\n", d.lds_bytes,
+                    d.lds_fb, hipGetErrorString(e));
             (void)hipGetLastError();
-        } else c->k3_lds_set = d.lds_bytes;
+        } else {
+            c->k3_lds_set = d.lds_bytes;
+            c->k3_lds_fb_set = d.lds_fb;
+        }
     }
     (void)hipGetLastError();
     HIPCHK(hipEventRecord(b->ev[slot][0], st));
@@ -835,7 +855,7 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][5], st));
     // deferred problems (usually none): a grid-stride kernel over the main kernel's list
-    hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_bytes,
+    hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_fb,
                        st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][6], st));

@@ -2764,7 +2764,8 @@ DEV void k3_defer(const pf_dev_batch &d, uint32_t prob) {
 // n_cand <= 64 (register candidate list), < 8192 sites (exact-interval pick
 // only); anything else is deferred to the FULL build.
 template <bool FULL>
-DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
+DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan,
+                const uint32_t lds) {
     const uint32_t tid = threadIdx.x;
     const uint32_t w = prob >> 1, dir = prob & 1;
     const uint32_t S = d.win_S[w];
@@ -2780,8 +2781,11 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
 
     // ---- P1: slot dictionary
     const uint64_t need1 = align16(8ull * S * MW) + 4ull * S;
-    const bool p1_lds = need1 <= d.lds_bytes;
-    if (!FULL && !(p1_lds && d.win_par[w * 4 + 2] <= 64 && S < 8192u && d.k3_mode == 0u)) {
+    const bool p1_lds = need1 <= lds;
+    // the slim loop: register candidate list (n_cand <= 64), exact-interval
+    // pick (< 8192 sites), dictionary in LDS
+    const bool slim_ok = p1_lds && d.win_par[w * 4 + 2] <= 64 && S < 8192u && d.k3_mode == 0u;
+    if (!FULL && !slim_ok) {
         k3_defer(d, prob);
         return;
     }
@@ -2818,53 +2822,69 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
 
     // ---- P2: greedy.  Prefer everything in LDS (u16 slot lists), then LDS
     // tables with slot lists read from the HBM arena, then all in HBM.  The
-    // main kernel's exact-pick path keeps no record rows (rcw = 0).
+    // slim loop keeps no record rows (rcw = 0): either kernel runs it when the
+    // problem fits this launch's LDS; the fallback kernel's general loop
+    // takes the rest.
     uint64_t off[K3_NOFF];
-    const uint32_t rcw_min = FULL ? 256 : 0, rcw_max = FULL ? 1024 : 0;
     const bool slots_ok = ntot < 0xFFFFu;
-    uint64_t need_s = k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
-    uint64_t need_n = k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
-    if (!FULL && !((slots_ok && need_s <= d.lds_bytes) || need_n <= d.lds_bytes)) {
+    const uint64_t slim_s = k3_layout(S, ntot, R, dir, summ_tot, true, 0, off);
+    const uint64_t slim_n = k3_layout(S, ntot, R, dir, summ_tot, false, 0, off);
+    const bool slim_fit = slim_ok && ((slots_ok && slim_s <= lds) || slim_n <= lds);
+    if (!FULL && !slim_fit) {
         k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
         return;
     }
     k3_dict_rewrite(d, r0, R, S, dir, masks, mbase);
     const uint32_t *kb = d.keys + kbase;
-    if (slots_ok && need_s <= d.lds_bytes) {
-        uint64_t base_bytes = off[11];
-        (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
-        base_bytes = off[11];
-        uint32_t rcw = FULL ? (uint32_t)((d.lds_bytes - base_bytes) / (12ull * PF_K3_WAVES)) : 0u;
-        rcw = rcw > rcw_max ? rcw_max : rcw;
-        (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw, off);
+    if (slim_fit) {
         K3Mem m;
-        k3_mem(smem, off, rcw, true, kb, m);
-        if constexpr (FULL) k3_greedy_body<true, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
-        else k3_greedy_slim<true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
-    } else if (need_n <= d.lds_bytes) {
-        (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
-        uint32_t rcw = FULL ? (uint32_t)((d.lds_bytes - off[11]) / (12ull * PF_K3_WAVES)) : 0u;
-        rcw = rcw > rcw_max ? rcw_max : rcw;
-        (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off);
-        K3Mem m;
-        k3_mem(smem, off, rcw, false, kb, m);
-        if constexpr (FULL) k3_greedy_body<false, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
-        else k3_greedy_slim<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
-    } else if constexpr (FULL) {
-        const uint32_t rcw = rcw_min;
-        const uint64_t need2 = align16(k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off));
-        __syncthreads();
-        if (tid == 0) {
-            const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)need2);
-            ctl.fail = 0;
-            if (o + need2 > d.scr_cap) { ctl.fail = 1; atomicOr(d.status, PF_ST_SCR_OVF); }
-            ctl.scr = o;
+        if (slots_ok && slim_s <= lds) {
+            (void)k3_layout(S, ntot, R, dir, summ_tot, true, 0, off);
+            k3_mem(smem, off, 0, true, kb, m);
+            k3_greedy_slim<true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        } else {
+            (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off);
+            k3_mem(smem, off, 0, false, kb, m);
+            k3_greedy_slim<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
         }
-        __syncthreads();
-        if (uni(ctl.fail)) return;
-        K3Mem m;
-        k3_mem(d.scr + ctl.scr, off, rcw, false, kb, m);
-        k3_greedy_body<false, FULL>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        return;
+    }
+    if constexpr (FULL) {
+        const uint32_t rcw_min = 256, rcw_max = 1024;
+        const uint64_t need_s = k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
+        const uint64_t need_n = k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
+        if (slots_ok && need_s <= lds) {
+            (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw_min, off);
+            uint32_t rcw = (uint32_t)((lds - off[11]) / (12ull * PF_K3_WAVES));
+            rcw = rcw > rcw_max ? rcw_max : rcw;
+            (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw, off);
+            K3Mem m;
+            k3_mem(smem, off, rcw, true, kb, m);
+            k3_greedy_body<true, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        } else if (need_n <= lds) {
+            (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
+            uint32_t rcw = (uint32_t)((lds - off[11]) / (12ull * PF_K3_WAVES));
+            rcw = rcw > rcw_max ? rcw_max : rcw;
+            (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off);
+            K3Mem m;
+            k3_mem(smem, off, rcw, false, kb, m);
+            k3_greedy_body<false, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        } else {
+            const uint32_t rcw = rcw_min;
+            const uint64_t need2 = align16(k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off));
+            __syncthreads();
+            if (tid == 0) {
+                const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)need2);
+                ctl.fail = 0;
+                if (o + need2 > d.scr_cap) { ctl.fail = 1; atomicOr(d.status, PF_ST_SCR_OVF); }
+                ctl.scr = o;
+            }
+            __syncthreads();
+            if (uni(ctl.fail)) return;
+            K3Mem m;
+            k3_mem(d.scr + ctl.scr, off, rcw, false, kb, m);
+            k3_greedy_body<false, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+        }
     }
 }
 
@@ -2874,7 +2894,7 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     __shared__ K3Ctl ctl;
     __shared__ K3Cand cd;
     __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
-    k3_run<false>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan);
+    k3_run<false>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes);
 }
 
 // Problems the main kernel deferred (dictionary or tables beyond the LDS
@@ -2886,7 +2906,7 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_fallback(pf_dev_batch d) 
     __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
     const uint32_t n = *d.k3_fb_ctr;
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-        k3_run<true>(d, d.k3_fb_list[i], smem, ctl, cd, sh_scan);
+        k3_run<true>(d, d.k3_fb_list[i], smem, ctl, cd, sh_scan, d.lds_fb);
         __syncthreads();
     }
 }
