@@ -63,6 +63,9 @@ class AlnSpec:
     filt_frac: float = 0.02
     mm_mix: bool = False       # mix MM/ML layouts (tests); else "C+h?;C+m?" (dorado 5mCG_5hmCG)
     len_scale: float = 1.0     # scales read lengths and min_len-sensitive sizes (small tests)
+    het_snv_rate: float = 0.0  # > 0: het SNVs outside the gap, alt on one truth haplotype, and MD:Z per record
+    windows_at: tuple = ()     # explicit (s, e) per window index instead of the strided layout
+    orient_at: tuple = ()      # explicit cis (0) / trans (1) per window index
 
 
 def _qual_from_cat(rng, cat):
@@ -87,6 +90,8 @@ def make_aln_window(spec: AlnSpec, w: int):
     # below the 2^29 limit of the call packing (a human chromosome is < 2^28)
     s = spec.base + (w % max(1, (400_000_000 - spec.base) // stride)) * stride
     e = s + gap
+    if spec.windows_at:
+        s, e = (int(x) for x in spec.windows_at[w])
     f_lo, f_hi = max(0, s - spec.readback), e + spec.readback
     span_lo, span_hi = f_lo - max_len, f_hi + max_len
     L = span_hi - span_lo + 16
@@ -106,6 +111,7 @@ def make_aln_window(spec: AlnSpec, w: int):
     site_hap = rng.integers(0, 2, cpg.shape[0])
     site_of = np.full(L, -1, np.int64)
     site_of[cpg] = np.arange(cpg.shape[0])
+    snv = _plant_snvs(spec, w, ref, cpg, span_lo, s, e) if spec.het_snv_rate > 0 else None
 
     # reads (reference spans), tags as synth.py
     mu, sig = _lognormal_params(spec.mean_len * spec.len_scale, spec.sd_len * spec.len_scale)
@@ -120,6 +126,8 @@ def make_aln_window(spec: AlnSpec, w: int):
     n = starts.shape[0]
     truth = rng.integers(0, 2, n)
     orient = int(rng.integers(0, 2))
+    if spec.orient_at:
+        orient = int(spec.orient_at[w])
     hp = np.full(n, HAPTAG_UNPHASED, np.int64)
     tl = starts < s
     hp[tl] = truth[tl]
@@ -189,6 +197,10 @@ def make_aln_window(spec: AlnSpec, w: int):
         kind = np.repeat(core_op, qlen)
         bases = ref[np.where(kind == 0, idx, 0)]
         refpos = np.where(kind == 0, idx, -1)
+        if snv is not None:                                   # het SNV alleles of the read's haplotype
+            on = (kind == 0) & (snv["alt_of"][np.maximum(idx, 0)] >= 0)
+            on &= snv["halt_of"][np.maximum(idx, 0)] == truth[r]
+            bases[on] = snv["alt_of"][idx[on]]
         ins_m = kind == 1
         bases[ins_m] = rng.integers(0, 4, int(ins_m.sum()))
         sub = (rng.random(tot) < spec.sub_rate) & ~ins_m
@@ -204,12 +216,13 @@ def make_aln_window(spec: AlnSpec, w: int):
         if c2[r]:
             ops.append((c2[r], 4))
         cigar = np.array([(l << 4) | op for l, op in ops], np.uint32)
-        recs.append((bases, refpos, cigar))
+        md = _md_string(bases[c1[r]:], ref, rs0[r], core_op, core_len) if snv is not None else None
+        recs.append((bases, refpos, cigar, md))
 
     # calls per read
     out = []
     for r in range(n):
-        bases, refpos, cigar = recs[r]
+        bases, refpos, cigar, md_s = recs[r]
         lq = bases.shape[0]
         cgp = np.flatnonzero((bases[:-1] == C_) & (bases[1:] == G_))     # C of each CpG (stored)
         sid = site_of[np.maximum(refpos[cgp], 0)]
@@ -265,6 +278,8 @@ def make_aln_window(spec: AlnSpec, w: int):
             codes = np.concatenate([codes, np.zeros(1, np.uint8)])
         seq = (codes[0::2] << 4) | codes[1::2]
         out.append(dict(seq=seq, l_qseq=lq, cigar=cigar, mm=np.frombuffer(mm.encode(), np.uint8), ml=ml))
+        if md_s is not None:
+            out[-1]["md"] = md_s
 
     flag = (strand * 16).astype(np.uint16)
     mapq = np.full(n, 60, np.uint8)
@@ -278,7 +293,67 @@ def make_aln_window(spec: AlnSpec, w: int):
         mapq[bad[kind == 2]] = 5
         de[bad[kind == 3]] = 0.2
         flag[bad[kind == 4]] |= np.uint16(4)
-    return dict(s=s, e=e, orient=orient, pos=starts, flag=flag, mapq=mapq, de=de, hp=hp, recs=out)
+    res = dict(s=s, e=e, orient=orient, pos=starts, flag=flag, mapq=mapq, de=de, hp=hp, recs=out)
+    if snv is not None:
+        res["snv"] = dict(pos=snv["pos"] + span_lo, ref=snv["ref"], alt=snv["alt"], h_alt=snv["h_alt"])
+    return res
+
+
+def _plant_snvs(spec: AlnSpec, w: int, ref: np.ndarray, cpg: np.ndarray, span_lo: int, s: int, e: int):
+    """Het SNVs for the -u path (a separate stream: the records of a spec
+    without SNVs do not change).  Poisson at het_snv_rate outside the gap,
+    plus one at each gap end (0-based s-1 and e-1: the last variant of the
+    left phase block at POS s and the first of the right one at POS e, so
+    that insert_vcf_line's gap is exactly [s, e]); never on a planted CpG.
+    The ALT allele sits on truth haplotype h_alt."""
+    rng = np.random.default_rng([spec.seed, w, 78])
+    L = ref.shape[0]
+    n = rng.poisson(spec.het_snv_rate * L)
+    cand = np.unique(np.concatenate([rng.integers(2, L - 2, n), [s - 1 - span_lo, e - 1 - span_lo]]))
+    g = cand + span_lo
+    cand = cand[(g < s) | (g >= e - 1)]
+    bad = np.zeros(L, bool)
+    bad[cpg] = True
+    bad[cpg + 1] = True
+    keep = ~bad[cand] | np.isin(cand + span_lo, [s - 1, e - 1])   # the gap ends stay, CpG or not
+    cand = cand[keep]
+    refb = ref[cand].copy()
+    alt = ((refb + rng.integers(1, 4, cand.shape[0])) % 4).astype(np.uint8)
+    h_alt = rng.integers(0, 2, cand.shape[0]).astype(np.int64)
+    alt_of = np.full(L, -1, np.int16)
+    halt_of = np.full(L, -1, np.int16)
+    alt_of[cand] = alt
+    halt_of[cand] = h_alt
+    return dict(pos=cand, ref=refb, alt=alt, h_alt=h_alt, alt_of=alt_of, halt_of=halt_of)
+
+
+_ACGT = "ACGT"
+
+
+def _md_string(core: np.ndarray, ref: np.ndarray, rs0: int, ops: np.ndarray, lens: np.ndarray) -> str:
+    """SAM MD:Z of an alignment whose query (without the leading clip) is
+    `core` against `ref` from ref index rs0, ops M/I/D only."""
+    parts, run, q, rc = [], 0, 0, int(rs0)
+    for op, ln in zip(ops.tolist(), lens.tolist()):
+        if op == 0:
+            mis = np.flatnonzero(core[q:q + ln] != ref[rc:rc + ln])
+            last = 0
+            for m in mis.tolist():
+                parts.append(str(run + m - last))
+                parts.append(_ACGT[int(ref[rc + m])])
+                run, last = 0, m + 1
+            run += ln - last
+            q += ln
+            rc += ln
+        elif op == 1:
+            q += ln
+        elif op == 2:
+            parts.append(str(run))
+            parts.append("^" + "".join(_ACGT[int(b)] for b in ref[rc:rc + ln]))
+            run = 0
+            rc += ln
+    parts.append(str(run))
+    return "".join(parts)
 
 
 def _window_job(args):
@@ -327,6 +402,9 @@ def make_aln_batch(spec: AlnSpec, windows=None, workers: int = 0) -> AlnBatch:
     )
     b.meta["orient"] = np.array([p["orient"] for p in parts], np.int8)
     b.meta["spec"] = spec
+    if spec.het_snv_rate > 0:
+        b.meta["md"] = [r["md"] for r in recs]
+        b.meta["snv"] = [p["snv"] for p in parts]
     return b
 
 

@@ -199,7 +199,7 @@ def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, 
 
 def records_from_aln(aln, tid: int = 0, prefix: str = "r", hp_zero_every: int = 0, de_absent_every: int = 0):
     """One Rec per record of an AlnBatch (tests/_aln_cases / synth_aln), with
-    MM:Z, ML:B:C, HP:i (absent for 254; HP:i:0 every hp_zero_every-th
+    MM:Z, ML:B:C, MD:Z (when the generator made one), HP:i (absent for 254; HP:i:0 every hp_zero_every-th
     unphased record) and de:f (absent when < 0)."""
     out = []
     for i in range(aln.n_recs):
@@ -223,6 +223,8 @@ def records_from_aln(aln, tid: int = 0, prefix: str = "r", hp_zero_every: int = 
         ml = aln.ml[aln.ml_off[i]:aln.ml_off[i + 1]]
         if len(ml):
             aux += aux_BC("ML", ml)
+        if "md" in aln.meta:
+            aux += aux_Z("MD", aln.meta["md"][i])
         out.append(Rec(tid=tid, pos=int(aln.pos[i]), qname=f"{prefix}{i}", flag=int(aln.flag[i]),
                        mapq=int(aln.mapq[i]), cigar=cig, seq=seq, l_seq=lq, aux=aux))
     return out
@@ -258,5 +260,37 @@ def write_phased_vcf(path: str, chrom: str, windows, chrom_len: int = 100_000_00
     for k, (pos, p) in enumerate(pts):
         gt = "0|1" if k % 2 == 0 else "1|0"
         lines.append(f"{chrom}\t{pos}\t.\tA\tG\t50\tPASS\t.\tGT:PS\t{gt}:{p}")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def write_u_vcf(path: str, chrom: str, aln, chrom_len: int = 400_000_000):
+    """The phased VCF of a synth_aln batch made with het SNVs: every window's
+    SNVs, the left side (POS <= s) in the block that ends at the gap, the
+    right side (POS >= e) in the block that starts there with PS e, so
+    insert_vcf_line's gaps are exactly the windows.  GT "a|b" puts ALT on the
+    block haplotype that carries it: h_alt left of the gap, h_alt ^ orient
+    right of it (the generator's HP convention: right-side reads carry
+    truth ^ orient)."""
+    lines = ["##fileformat=VCFv4.2", f"##contig=<ID={chrom},length={chrom_len}>",
+             '##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype">',
+             '##FORMAT=<ID=PS,Number=1,Type=Integer,Description="Phase set">',
+             "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1"]
+    ps = None
+    for w in range(aln.n_windows):
+        sv = aln.meta["snv"][w]
+        s, e, orient = int(aln.win_start[w]), int(aln.win_end[w]), int(aln.meta["orient"][w])
+        for p0, r, a, h in zip(sv["pos"].tolist(), sv["ref"].tolist(), sv["alt"].tolist(), sv["h_alt"].tolist()):
+            pos = p0 + 1
+            if pos <= s:
+                hb = h
+                if ps is None:
+                    ps = pos
+            else:
+                hb = h ^ orient
+                if pos == e:
+                    ps = e
+            gt = "0|1" if hb == 1 else "1|0"
+            lines.append(f"{chrom}\t{pos}\t.\t{'ACGT'[r]}\t{'ACGT'[a]}\t50\tPASS\t.\tGT:PS\t{gt}:{ps}")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")

@@ -116,3 +116,69 @@ def cases():
         ("handmade", Config(k=3, k_span=5000, cov_for_selection=1, cov_for_runtime=2, n_cand=4), handmade()),
     ]
     return out
+
+
+def _batch_from_reads(s, e, reads):
+    """One window [s, e] from [(start, end, hp, [(pos, cat), ...]), ...]."""
+    off = np.cumsum([0] + [len(r[3]) for r in reads])
+    return WindowBatch(
+        win_start=[s], win_end=[e], win_read_off=[0, len(reads)],
+        read_start=[r[0] for r in reads], read_end=[r[1] for r in reads],
+        read_hp=[r[2] for r in reads], read_call_off=off,
+        call_pos=[c[0] for r in reads for c in r[3]], call_cat=[c[1] for r in reads for c in r[3]])
+
+
+# T8 positions and their (meth, unmeth) call counts; the reference's per-site
+# counters are u16 with the count in the top 12 bits (cnt += 1<<4,
+# blockjoin.c:3210-3238), so a count is n mod 4096.
+T8_COUNTS = {100_100: (4100, 20),     # meth wraps to 4  < cov_sel 5: not a site
+             100_200: (4101, 20),     # meth wraps to 5 >= 5: a site
+             100_300: (4096, 20),     # meth wraps to 0: not a site
+             100_400: (20, 20),       # ordinary site
+             100_500: (10, 4096)}     # unmeth wraps to 0: not a site
+T8_SITES = [100_200, 100_400]         # worked by hand from the rule above
+T8_CFG = Config(k=3, k_span=5000, cov_for_selection=5, cov_for_runtime=10, n_cand=8)
+
+
+def t8_counter_wrap():
+    """A window of 4,200 reads, all left-side references (start <= s, hp
+    alternating 0/1, so the left-coverage check passes), whose calls give
+    every T8 position the counts of T8_COUNTS (read i makes a meth call at
+    a position while i < n_meth, an unmeth call while i < n_meth + n_unmeth)."""
+    n = 4200
+    reads = []
+    for i in range(n):
+        calls = []
+        for p, (nm, nu) in T8_COUNTS.items():
+            if i < nm:
+                calls.append((p, 0))
+            elif i < nm + nu:
+                calls.append((p, 1))
+        reads.append((50_000, 200_000, i % 2, calls))
+    return _batch_from_reads(100_000, 150_000, reads)
+
+
+def t6_range_wrap():
+    """Every site lies right of the gap end e.  Direction 1 starts with
+    mmr_min_i = n-1 and decrements it once per site > e
+    (haplotag_region1, blockjoin.c:3999-4003): past site 0 the u32 wraps to
+    UINT32_MAX, the range update's `int i = mmr_min_i` loop never runs
+    (3671) and no site is ever inside [mmr_min_i, mmr_max_i), so direction 1
+    tags no read and its join is -1; direction 0 (range from 0 upwards) tags
+    normally.  A clamped (non-wrapping) min_i would let direction 1 query
+    sites and tag reads."""
+    rng = np.random.default_rng(61)
+    s, e = 100_000, 150_000
+    sites = np.arange(160_000, 190_000, 400)
+    meth = rng.random(sites.shape[0]) < 0.5        # allele-specific: hap 0 meth at `meth` sites
+    reads = []
+    for i in range(40):                            # left references, hp 0/1
+        h = i % 2
+        reads.append((60_000, 195_000, h, [(int(p), int(meth[k] ^ h)) for k, p in enumerate(sites)]))
+    for i in range(40):                            # untagged reads inside the gap, spanning the sites
+        h = int(rng.integers(0, 2))
+        reads.append((110_000 + 500 * i, 196_000, 254, [(int(p), int(meth[k] ^ h)) for k, p in enumerate(sites)]))
+    for i in range(30):                            # right references (start > s, end >= e), hp 0/1
+        h = i % 2
+        reads.append((120_000 + 700 * i, 198_000, h, [(int(p), int(meth[k] ^ h)) for k, p in enumerate(sites)]))
+    return _batch_from_reads(s, e, reads)

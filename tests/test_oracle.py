@@ -207,3 +207,28 @@ def test_golden_synth_vectors(oracle_lib):
         assert np.array_equal(res.dir_table, g[f"{tag}_table"])
         assert np.array_equal(res.win_n_sites, g[f"{tag}_sites"])
         assert np.array_equal(res.read_hp, g[f"{tag}_hp"])
+
+
+def test_t8_site_counter_wrap(oracle_lib):
+    """T8: a site's meth/unmeth counts wrap at 4096 (u16 counters, 12-bit
+    count, blockjoin.c:3210-3238); the sites of tests/_cases.t8_counter_wrap
+    worked out by hand."""
+    from tests._cases import T8_CFG, T8_SITES, t8_counter_wrap
+    b = t8_counter_wrap()
+    for d in (0, 1):
+        real, _, _ = oracle_lib.window_sites(T8_CFG, b, 0, d)
+        assert real.tolist() == T8_SITES          # dir 1 is reversed back after its ranges (3307-3329)
+    assert oracle_lib.methphase(T8_CFG, b).win_n_sites.tolist() == [len(T8_SITES)]
+
+
+def test_t6_range_index_wrap(oracle_lib):
+    """T6: with every site right of e, direction 1's mmr_min_i wraps to
+    UINT32_MAX (blockjoin.c:3999-4003) and no read is ever tagged in that
+    direction; direction 0 tags reads (tests/_cases.t6_range_wrap)."""
+    from tests._cases import t6_range_wrap
+    cfg = Config(k=3, k_span=5000, cov_for_selection=4, cov_for_runtime=8, n_cand=8)
+    b = t6_range_wrap()
+    ids, tags, scores, counts = oracle_lib.trace(cfg, b)
+    assert counts[0, 1] == 0 and counts[0, 0] > 0
+    res = oracle_lib.methphase(cfg, b)
+    assert res.dir_join[0, 1] == -1 and res.decision[0] == -1
