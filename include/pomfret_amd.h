@@ -209,6 +209,8 @@ int  pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg,
                      const pf_window_batch_t *batch, pf_dbatch_t **out);
 void pf_batch_free(pf_dbatch_t *db);
 uint32_t pf_batch_n_windows(const pf_dbatch_t *db);
+/* Reads of the batch (record level: the kept records of the last finished
+ * run -- K0 sizes the batch on the device -- bounded by the record count). */
 uint32_t pf_batch_n_reads(const pf_dbatch_t *db);
 /* Calls of the batch (record level: of the last finished run, 0 before). */
 uint64_t pf_batch_n_calls(const pf_dbatch_t *db);
@@ -475,6 +477,130 @@ typedef struct pf_known_table {
 } pf_known_table_t;
 int  pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t **out);
 void pf_known_table_free(pf_known_table_t *t);
+
+/* ------------------------------------------------------------------ */
+/* qname -> haplotag tables (the reference's htstri_t: st->qname2haptag,  */
+/* st->qname2haptag_raw), first entry of a qname wins.                    */
+
+typedef struct pf_tags pf_tags_t;
+pf_tags_t *pf_tags_new(void);
+void     pf_tags_free(pf_tags_t *t);
+uint64_t pf_tags_size(const pf_tags_t *t);
+/* Insert every (names[off[i]:off[i+1]], hp[i]) whose qname is absent, in
+ * order (kh_put + "if (absent)", blockjoin.c:4412-4421).  Returns the number
+ * inserted or < 0. */
+int64_t  pf_tags_put_first(pf_tags_t *t, uint32_t n, const uint64_t *off, const char *names, const uint8_t *hp);
+/* hp_out[i] = tag of qname i, or dflt when absent; returns how many were found. */
+int64_t  pf_tags_get(const pf_tags_t *t, uint32_t n, const uint64_t *off, const char *names, uint8_t dflt,
+                     uint8_t *hp_out);
+/* The entries in insertion order (valid until the next insertion). */
+int      pf_tags_view(const pf_tags_t *t, pf_qname_tags_t *out);
+
+/* ------------------------------------------------------------------ */
+/* Pipeline driver: `pomfret methphase` (main_blockjoin, blockjoin.c:    */
+/* 4643-4736) and `pomfret report` (main_methreport, 4901-5089) from     */
+/* files, on one or more GPUs.                                           */
+
+#define PF_READBACK 50000          /* blockjoin.c READBACK, the fetch margin of 1053-1054 */
+#define PF_MODE_METHPHASE 0
+#define PF_MODE_REPORT    1
+#define PF_JOB_WINDOWS 0           /* a run of consecutive windows of one contig */
+#define PF_JOB_HAPTAG  1           /* the -u pre-pass of one contig (1841-1898) */
+
+typedef struct pf_methphase_opts {
+    int32_t mode;                  /* PF_MODE_*                                                */
+    const char *bam_path;          /* positional bam (sorted, indexed)                         */
+    const char *vcf_path;          /* --vcf                                                    */
+    const char *out_prefix;        /* -o; NULL: nothing written                                */
+    /* methphase: cliopt->cov_for_selection / n_candidates_per_iter as the
+     * CLI leaves them (-c C sets C/10 and C/4, -n sets n_cand; <= 0: per
+     * contig from the coverage estimate, 4357-4374); cov_for_runtime <= 0
+     * means 2*cov_for_selection (4655).  report: cov is -c (<= 0: the
+     * estimate), parameters cov/10+1, 2x, cov/4+1 (5045-5051). */
+    int32_t cov_for_selection, cov_for_runtime, n_cand, cov;
+    int32_t k, k_span;             /* -k, -l (<= 0: 3, 5000)                                   */
+    pf_load_cfg_t load;            /* -q, -L, --lo, --hi                                       */
+    int32_t untagged;              /* -u, --bam-is-untagged                                    */
+    int32_t write_tsv;             /* --output-tsv: {prefix}.mp.tsv                            */
+    int32_t write_bam;             /* --write-bam (PF_ERR_UNSUPPORTED in pf_methphase_main)    */
+    int32_t chunk_size, chunk_stride;  /* report: --chunk-size, --chunk-stride                 */
+    int32_t threads;               /* host threads fetching one job's windows (-t)             */
+    int32_t n_devices;             /* GPUs to drive from this process (0: all visible)         */
+    const int32_t *devices;        /* their ids (NULL: 0..n_devices-1)                         */
+    pf_ctx_t *const *ctxs;         /* or caller-owned contexts, one per device thread          */
+    int32_t n_ctxs;
+    int32_t rank, world;           /* multi-process runs: this process runs the jobs the static
+                                      LPT partition gives `rank` (world <= 1: all of them)      */
+    uint32_t job_windows;          /* max windows per job (0: 1024)                            */
+    int32_t verbose;               /* < 0: no progress messages                                */
+} pf_methphase_opts_t;
+
+typedef struct pf_mp_plan pf_mp_plan_t;
+
+/* Whole run in this process: plan, (-u) pre-pass jobs on the devices, window
+ * jobs on the devices (one host thread per GPU; the next job's BAM fetch
+ * overlaps the current job's kernels), merge and outputs:
+ * {prefix}.mp.gtf, .mp.vcf (and .mp.tsv), or {prefix}.report.tsv plus the
+ * running totals on stdout.  On success *out holds the finished plan
+ * (decisions, tables, blocks) until pf_mp_free. */
+int  pf_methphase_main(const pf_methphase_opts_t *o, pf_mp_plan_t **out);
+
+/* The same run split into steps, for one process per GPU: every rank builds
+ * the same plan (deterministic), runs its jobs, exports their results; the
+ * writer rank imports every rank's results and finishes. */
+int  pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out);
+void pf_mp_free(pf_mp_plan_t *p);
+uint32_t pf_mp_n_jobs(const pf_mp_plan_t *p, int kind);
+
+typedef struct pf_mp_job_info {
+    uint32_t contig;               /* index into the plan's gaps                    */
+    const char *contig_name;
+    uint32_t w0, w1;               /* windows [w0, w1) of pf_mp_windows             */
+    int32_t rank;                  /* static LPT owner                              */
+    uint32_t lpt_pos;              /* position in the longest-first order           */
+    double cost;                   /* fetch span (bases) / contig length (-u)       */
+    int32_t done;
+    pf_cfg_t cfg;                  /* the contig's parameters (4357-4390)           */
+} pf_mp_job_info_t;
+int  pf_mp_job_info(const pf_mp_plan_t *p, int kind, uint32_t j, pf_mp_job_info_t *info);
+/* All windows in (contig, window) order; contig c owns [off[c], off[c+1]). */
+int  pf_mp_windows(const pf_mp_plan_t *p, const uint32_t **win_start, const uint32_t **win_end,
+                   const uint64_t **contig_win_off, uint32_t *n_windows);
+
+/* Run jobs of `kind` owned by run_opts->rank (all when world <= 1) on the
+ * devices run_opts names (n_devices / devices / ctxs). */
+int  pf_mp_run_mine(pf_mp_plan_t *p, const pf_methphase_opts_t *run_opts, int kind);
+int  pf_mp_run_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j);          /* one window job */
+int  pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j);   /* one -u job     */
+/* After every -u job has a result: the merged table (contig order, first
+ * wins) that replaces HP in the window jobs (1114-1122). */
+int  pf_mp_merge_raw(pf_mp_plan_t *p);
+
+/* A job's result: decisions of its windows and the (qname, tag) entries of
+ * its joined windows, window by window in read order (tag_off[w] ..
+ * tag_off[w+1]); -u jobs: no windows, the contig's first-wins table in BAM
+ * order.  get returns views into the plan; set copies. */
+typedef struct pf_mp_job_result {
+    uint32_t n_windows;
+    const int8_t *decision;
+    const uint64_t *tag_off;
+    pf_qname_tags_t tags;
+    uint32_t n_limit;              /* windows left undecided for a device limit */
+} pf_mp_job_result_t;
+int  pf_mp_get_job_result(const pf_mp_plan_t *p, int kind, uint32_t j, pf_mp_job_result_t *r);
+int  pf_mp_set_job_result(pf_mp_plan_t *p, int kind, uint32_t j, const pf_mp_job_result_t *r);
+
+/* Merge every job's result in (contig, window) order -- decisions, and the
+ * joined windows' tags first-wins (4408-4423 then 4579-4595) -- then the
+ * phase blocks and, with an output prefix, the files. */
+int  pf_mp_finish(pf_mp_plan_t *p);
+int  pf_mp_decisions(const pf_mp_plan_t *p, const int8_t **decision, uint32_t *n, uint32_t *n_limit);
+const pf_gaps_t   *pf_mp_gaps(const pf_mp_plan_t *p);
+const pf_blocks_t *pf_mp_blocks(const pf_mp_plan_t *p);
+const pf_tags_t   *pf_mp_qname_hp(const pf_mp_plan_t *p);
+const pf_tags_t   *pf_mp_raw_hp(const pf_mp_plan_t *p);     /* NULL without -u */
+/* report: {correct, switch, fail} */
+int  pf_mp_report_counts(const pf_mp_plan_t *p, double *counts3);
 
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
  * the observed table. */

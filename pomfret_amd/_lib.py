@@ -114,6 +114,32 @@ class _PfBlocks(C.Structure):
                 ("blk_start", C.POINTER(C.c_uint32)), ("blk_end", C.POINTER(C.c_uint32))]
 
 
+def _gaps_contigs(p):
+    """pf_gaps_t* -> [dict(name, abs_start, abs_end, raw, gaps, dropped)]."""
+    g = p.contents
+    res = []
+    for c in range(g.n_contigs):
+        def sl(off, a, b):
+            return [(int(a[k]), int(b[k])) for k in range(off[c], off[c + 1])]
+        res.append(dict(name=g.names[c].decode(), abs_start=int(g.abs_start[c]), abs_end=int(g.abs_end[c]),
+                        raw=sl(g.raw_off, g.raw_start, g.raw_end), gaps=sl(g.gap_off, g.gap_start, g.gap_end),
+                        dropped=sl(g.drop_off, g.drop_start, g.drop_end)))
+    return res
+
+
+def _blocks_contigs(p):
+    """pf_blocks_t* -> [dict(raw, decisions, flips, blocks)] per contig."""
+    b = p.contents
+    res = []
+    for c in range(b.n_contigs):
+        res.append(dict(
+            raw=[(int(b.raw_start[k]), int(b.raw_end[k])) for k in range(b.raw_off[c], b.raw_off[c + 1])],
+            decisions=[int(b.dec_onraw[k]) for k in range(b.dec_off[c], b.dec_off[c + 1])],
+            flips=[int(b.flip[k]) for k in range(b.dec_off[c], b.dec_off[c + 1])],
+            blocks=[(int(b.blk_start[k]), int(b.blk_end[k])) for k in range(b.blk_off[c], b.blk_off[c + 1])]))
+    return res
+
+
 class _PfRescue(C.Structure):
     _fields_ = [("off", C.c_void_p), ("pos", C.c_void_p), ("hap_of_ref", C.c_void_p)]
 
@@ -127,15 +153,7 @@ class Gaps:
         _check(L.pf_vcf_gaps(path.encode(), readback, C.byref(self._p)), "pf_vcf_gaps")
 
     def contigs(self):
-        g = self._p.contents
-        res = []
-        for c in range(g.n_contigs):
-            def sl(off, a, b):
-                return [(int(a[k]), int(b[k])) for k in range(off[c], off[c + 1])]
-            res.append(dict(name=g.names[c].decode(), abs_start=int(g.abs_start[c]), abs_end=int(g.abs_end[c]),
-                            raw=sl(g.raw_off, g.raw_start, g.raw_end), gaps=sl(g.gap_off, g.gap_start, g.gap_end),
-                            dropped=sl(g.drop_off, g.drop_start, g.drop_end)))
-        return res
+        return _gaps_contigs(self._p)
 
     @property
     def n_windows(self) -> int:
@@ -167,15 +185,7 @@ class Blocks:
         _check(L.pf_phase_blocks(gaps._p, self._dec.ctypes.data, C.byref(self._p)), "pf_phase_blocks")
 
     def contigs(self):
-        b = self._p.contents
-        res = []
-        for c in range(b.n_contigs):
-            res.append(dict(
-                raw=[(int(b.raw_start[k]), int(b.raw_end[k])) for k in range(b.raw_off[c], b.raw_off[c + 1])],
-                decisions=[int(b.dec_onraw[k]) for k in range(b.dec_off[c], b.dec_off[c + 1])],
-                flips=[int(b.flip[k]) for k in range(b.dec_off[c], b.dec_off[c + 1])],
-                blocks=[(int(b.blk_start[k]), int(b.blk_end[k])) for k in range(b.blk_off[c], b.blk_off[c + 1])]))
-        return res
+        return _blocks_contigs(self._p)
 
     def write_gtf(self, path: str):
         _check(_gaps_lib().pf_write_gtf(self.gaps._p, self._p, path.encode()), "pf_write_gtf")

@@ -1,0 +1,1151 @@
+/*
+ * pf_pipeline.c -- `pomfret methphase` / `pomfret report` end to end in host C
+ * around the device hot path (f1-f3 glue).
+ *
+ * Reference structure (line numbers: /root/reference/blockjoin.c):
+ *   main_blockjoin (4643-4736) -> blockjoin_parallel (4427-4641):
+ *     load_intervals_from_file + merge_close_intervals      -> pf_vcf_gaps
+ *     (-u) pre_haplotagging_read_in_one_ref per contig (1841-1898),
+ *          qname first-wins per contig, merged in contig order     -> K4 jobs
+ *     estimate_read_coverage_dirtyfast when -c is absent (4547)     -> pf_bam_estimate_coverage
+ *     kt_for(blockjoin_one_chrom_callback) over contigs (4560):
+ *       per-contig parameters and clamps (4357-4390), one
+ *       haplotag_region_given_bam per merged gap, and for a joined gap
+ *       every read's tag into the contig's qname table, first wins
+ *       (4396-4423)                                                  -> window jobs on the devices
+ *     per-contig tables merged into st->qname2haptag in contig order,
+ *     first wins (4571-4595)                                         -> pf_mp_finish
+ *   lift_decisions .. output_modify_vcf (4685-4717)                  -> pf_phase_blocks, pf_write_*,
+ *                                                                       pf_rescue_dropped
+ *   main_methreport (4901-5089): chunk windows of the raw gaps, one
+ *     haplotag_region_given_bam each, report.tsv rows and the running
+ *     correct/switch/fail totals                                      -> mode PF_MODE_REPORT
+ *
+ * MI355X-first shape.  The reference fans contigs out to CPU threads and
+ * re-opens the BAM per gap.  Here the windows of all contigs are cut into
+ * jobs (runs of consecutive windows of one contig), ordered by
+ * longest-processing-time first on their fetch span, and consumed by one
+ * host thread per GPU: the thread fetches a job's records on the host
+ * (pf_bam_fetch_windows, threaded) while its device runs the previous job
+ * (K0..K3, pf_methphase_run), so host ingest and device compute overlap.
+ * Within one process the device threads share a work queue; across
+ * processes (one per GPU, torch.distributed) `rank/world` picks a static
+ * LPT shard and the job results -- per-window decisions plus the joined
+ * windows' (qname, tag) lists -- are exported, gathered and imported on the
+ * writer rank, whose merge in (contig, window) order reproduces the
+ * reference's first-wins tables exactly.
+ *
+ * Windows whose record count exceeds the device limit (65,535 reads per
+ * window) are left undecided (-1) with a warning instead of failing the run.
+ */
+#include <errno.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/pomfret_amd.h"
+
+#define PF_JOB_WINDOWS_DEFAULT 1024u
+#define PF_MAX_WIN_RECS 65535u
+
+/* ------------------------------------------------------------------ */
+/* qname -> hp, first wins (htstri_t of the reference)                  */
+
+struct pf_tags {
+    uint64_t *slot;        /* entry index + 1, 0 = empty */
+    uint64_t mask;
+    uint64_t n, cap;       /* entries */
+    uint64_t *off;         /* [cap+1] name offsets */
+    char *names;
+    uint64_t names_n, names_cap;
+    uint8_t *hp;
+};
+
+static uint64_t fnv1a(const char *s, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; i++) { h ^= (uint8_t)s[i]; h *= 1099511628211ull; }
+    return h ^ (h >> 29);
+}
+
+pf_tags_t *pf_tags_new(void) {
+    pf_tags_t *t = (pf_tags_t *)calloc(1, sizeof *t);
+    if (!t) return NULL;
+    t->mask = 1023;
+    t->slot = (uint64_t *)calloc(t->mask + 1, sizeof(uint64_t));
+    t->cap = 256;
+    t->off = (uint64_t *)calloc(t->cap + 1, sizeof(uint64_t));
+    t->hp = (uint8_t *)malloc(t->cap);
+    t->names_cap = 4096;
+    t->names = (char *)malloc(t->names_cap);
+    if (!t->slot || !t->off || !t->hp || !t->names) { pf_tags_free(t); return NULL; }
+    return t;
+}
+
+void pf_tags_free(pf_tags_t *t) {
+    if (!t) return;
+    free(t->slot); free(t->off); free(t->hp); free(t->names);
+    free(t);
+}
+
+uint64_t pf_tags_size(const pf_tags_t *t) { return t ? t->n : 0; }
+
+static int64_t tags_find(const pf_tags_t *t, const char *nm, size_t l, uint64_t *slot_out) {
+    uint64_t h = fnv1a(nm, l) & t->mask;
+    for (;;) {
+        const uint64_t s = t->slot[h];
+        if (!s) { if (slot_out) *slot_out = h; return -1; }
+        const uint64_t k = s - 1;
+        if (t->off[k + 1] - t->off[k] == l && memcmp(t->names + t->off[k], nm, l) == 0) return (int64_t)k;
+        h = (h + 1) & t->mask;
+    }
+}
+
+static int tags_rehash(pf_tags_t *t) {
+    const uint64_t nm = (t->mask + 1) * 2 - 1;
+    uint64_t *ns = (uint64_t *)calloc(nm + 1, sizeof(uint64_t));
+    if (!ns) return PF_ERR_NOMEM;
+    for (uint64_t k = 0; k < t->n; k++) {
+        uint64_t h = fnv1a(t->names + t->off[k], t->off[k + 1] - t->off[k]) & nm;
+        while (ns[h]) h = (h + 1) & nm;
+        ns[h] = k + 1;
+    }
+    free(t->slot);
+    t->slot = ns;
+    t->mask = nm;
+    return PF_OK;
+}
+
+/* insert (nm, hp) unless present; 1 inserted, 0 present, < 0 error */
+static int tags_put(pf_tags_t *t, const char *nm, size_t l, uint8_t hp) {
+    uint64_t slot;
+    if (tags_find(t, nm, l, &slot) >= 0) return 0;
+    if (2 * (t->n + 1) > t->mask + 1) {
+        int rc = tags_rehash(t);
+        if (rc) return rc;
+        (void)tags_find(t, nm, l, &slot);
+    }
+    if (t->n + 1 > t->cap) {
+        const uint64_t nc = t->cap * 2;
+        uint64_t *no = (uint64_t *)realloc(t->off, (nc + 1) * sizeof(uint64_t));
+        if (!no) return PF_ERR_NOMEM;
+        t->off = no;
+        uint8_t *nh = (uint8_t *)realloc(t->hp, nc);
+        if (!nh) return PF_ERR_NOMEM;
+        t->hp = nh;
+        t->cap = nc;
+    }
+    if (t->names_n + l > t->names_cap) {
+        uint64_t nc = t->names_cap * 2;
+        while (nc < t->names_n + l) nc *= 2;
+        char *nn = (char *)realloc(t->names, nc);
+        if (!nn) return PF_ERR_NOMEM;
+        t->names = nn;
+        t->names_cap = nc;
+    }
+    memcpy(t->names + t->names_n, nm, l);
+    t->names_n += l;
+    t->hp[t->n] = hp;
+    t->n++;
+    t->off[t->n] = t->names_n;
+    t->slot[slot] = t->n;
+    return 1;
+}
+
+int64_t pf_tags_put_first(pf_tags_t *t, uint32_t n, const uint64_t *off, const char *names, const uint8_t *hp) {
+    if (!t || (n && (!off || !names || !hp))) return PF_ERR_ARG;
+    int64_t ins = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (off[i + 1] < off[i]) return PF_ERR_ARG;
+        const int rc = tags_put(t, names + off[i], (size_t)(off[i + 1] - off[i]), hp[i]);
+        if (rc < 0) return rc;
+        ins += rc;
+    }
+    return ins;
+}
+
+int64_t pf_tags_get(const pf_tags_t *t, uint32_t n, const uint64_t *off, const char *names, uint8_t dflt,
+                    uint8_t *hp_out) {
+    if (!t || (n && (!off || !names || !hp_out))) return PF_ERR_ARG;
+    int64_t found = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const int64_t k = tags_find(t, names + off[i], (size_t)(off[i + 1] - off[i]), NULL);
+        hp_out[i] = k >= 0 ? t->hp[k] : dflt;
+        found += k >= 0;
+    }
+    return found;
+}
+
+int pf_tags_view(const pf_tags_t *t, pf_qname_tags_t *out) {
+    if (!t || !out) return PF_ERR_ARG;
+    if (t->n > UINT32_MAX) return PF_ERR_LIMIT;
+    out->n = (uint32_t)t->n;
+    out->off = t->off;
+    out->names = t->names;
+    out->hp = t->hp;
+    return PF_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* plan                                                                 */
+
+typedef struct {
+    uint32_t contig, w0, w1;   /* windows [w0, w1) of the plan's global window list */
+    double cost;
+    int32_t rank;
+    int done;
+    /* result */
+    int8_t *dec;               /* [w1-w0] */
+    uint64_t *tag_off;         /* [w1-w0+1] entry ranges per window */
+    uint64_t n_ent;
+    uint64_t *name_off;        /* [n_ent+1] */
+    char *names;
+    uint8_t *hp;
+    uint32_t n_limit;          /* windows left undecided for a device limit */
+} job_t;
+
+struct pf_mp_plan {
+    pf_methphase_opts_t o;
+    char *bam_path, *vcf_path, *out_prefix;
+    pf_gaps_t *gaps;
+    uint32_t n_contigs;
+    int32_t *tid;              /* [n_contigs] BAM tid or -1 */
+    pf_cfg_t *cfg;             /* [n_contigs] */
+    uint32_t n_windows;
+    uint64_t *win_off;         /* [n_contigs+1] */
+    uint32_t *win_start, *win_end;
+    uint32_t n_jobs, n_ujobs;
+    job_t *jobs, *ujobs;       /* window jobs; -u pre-pass jobs (one per contig, w0=w1=0) */
+    uint32_t *order, *uorder;  /* LPT order */
+    pf_tags_t *raw;            /* merged -u table */
+    int raw_merged;
+    int8_t *decision;          /* [n_windows] after finish */
+    pf_tags_t *qname_hp;
+    pf_blocks_t *blocks;
+    int finished;
+    uint32_t n_limit;
+    double report_counts[3];   /* correct, switch, fail */
+};
+
+static char *dupstr(const char *s) {
+    if (!s) return NULL;
+    const size_t l = strlen(s);
+    char *d = (char *)malloc(l + 1);
+    if (d) memcpy(d, s, l + 1);
+    return d;
+}
+
+static void job_clear(job_t *j) {
+    free(j->dec); free(j->tag_off); free(j->name_off); free(j->names); free(j->hp);
+    j->dec = NULL; j->tag_off = NULL; j->name_off = NULL; j->names = NULL; j->hp = NULL;
+    j->n_ent = 0;
+    j->done = 0;
+}
+
+void pf_mp_free(pf_mp_plan_t *p) {
+    if (!p) return;
+    for (uint32_t j = 0; j < p->n_jobs; j++) job_clear(&p->jobs[j]);
+    for (uint32_t j = 0; j < p->n_ujobs; j++) job_clear(&p->ujobs[j]);
+    free(p->jobs); free(p->ujobs); free(p->order); free(p->uorder);
+    free(p->tid); free(p->cfg); free(p->win_off); free(p->win_start); free(p->win_end);
+    free(p->decision);
+    pf_tags_free(p->raw);
+    pf_tags_free(p->qname_hp);
+    if (p->blocks) pf_blocks_free(p->blocks);
+    if (p->gaps) pf_gaps_free(p->gaps);
+    free(p->bam_path); free(p->vcf_path); free(p->out_prefix);
+    free(p);
+}
+
+static int cmp_cost_desc(const void *a, const void *b, void *ctx) {
+    const job_t *J = (const job_t *)ctx;
+    const uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    const double cx = J[x].cost, cy = J[y].cost;
+    if (cx != cy) return cx > cy ? -1 : 1;
+    return x < y ? -1 : x > y;
+}
+
+/* LPT order and static rank assignment */
+static int lpt(job_t *J, uint32_t n, int32_t world, uint32_t **order_out) {
+    uint32_t *ord = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    double *load = (double *)calloc(world > 0 ? world : 1, sizeof(double));
+    if (!ord || !load) { free(ord); free(load); return PF_ERR_NOMEM; }
+    for (uint32_t i = 0; i < n; i++) ord[i] = i;
+    qsort_r(ord, n, sizeof(uint32_t), cmp_cost_desc, J);
+    const int32_t W = world > 0 ? world : 1;
+    for (uint32_t i = 0; i < n; i++) {
+        int32_t best = 0;
+        for (int32_t r = 1; r < W; r++) if (load[r] < load[best]) best = r;
+        J[ord[i]].rank = best;
+        load[best] += J[ord[i]].cost;
+    }
+    free(load);
+    *order_out = ord;
+    return PF_OK;
+}
+
+static void mp_log(const pf_mp_plan_t *p, const char *fmt, const char *a, long x, long y) {
+    if (p->o.verbose) { fprintf(stderr, fmt, a, x, y); fputc('\n', stderr); }
+}
+
+int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
+    if (!o || !out || !o->bam_path || !o->vcf_path) return PF_ERR_ARG;
+    if (o->mode != PF_MODE_METHPHASE && o->mode != PF_MODE_REPORT) return PF_ERR_ARG;
+    if (o->mode == PF_MODE_REPORT && (o->chunk_size <= 0 || o->chunk_stride <= 0)) return PF_ERR_ARG;
+    *out = NULL;
+    pf_mp_plan_t *p = (pf_mp_plan_t *)calloc(1, sizeof *p);
+    if (!p) return PF_ERR_NOMEM;
+    p->o = *o;
+    p->bam_path = dupstr(o->bam_path);
+    p->vcf_path = dupstr(o->vcf_path);
+    p->out_prefix = dupstr(o->out_prefix);
+    p->o.bam_path = p->bam_path;
+    p->o.vcf_path = p->vcf_path;
+    p->o.out_prefix = p->out_prefix;
+    p->o.ctxs = NULL;
+    p->o.n_ctxs = 0;
+    int rc = pf_vcf_gaps(o->vcf_path, PF_READBACK, &p->gaps);
+    if (rc) { pf_mp_free(p); return rc; }
+    const pf_gaps_t *g = p->gaps;
+    const uint32_t C = g->n_contigs;
+    p->n_contigs = C;
+    p->tid = (int32_t *)calloc(C ? C : 1, sizeof(int32_t));
+    p->cfg = (pf_cfg_t *)calloc(C ? C : 1, sizeof(pf_cfg_t));
+    p->win_off = (uint64_t *)calloc(C + 1, sizeof(uint64_t));
+    if (!p->tid || !p->cfg || !p->win_off) { pf_mp_free(p); return PF_ERR_NOMEM; }
+
+    pf_bam_t *bam = NULL;
+    rc = pf_bam_open(o->bam_path, NULL, &bam);
+    if (rc) { pf_mp_free(p); return rc; }
+    const int32_t nt = pf_bam_n_targets(bam);
+    int32_t *covs = NULL;
+    const int need_est = o->mode == PF_MODE_METHPHASE ? o->cov_for_selection <= 0 : o->cov <= 0;
+    if (need_est) {
+        covs = (int32_t *)calloc(nt > 0 ? nt : 1, sizeof(int32_t));
+        if (!covs) rc = PF_ERR_NOMEM;
+        if (!rc) rc = pf_bam_estimate_coverage(bam, covs, nt > 0 ? nt : 1);
+    }
+    /* windows: merged gaps (methphase) or report chunks of the raw gaps */
+    uint64_t nw = 0, cap = 0;
+    for (uint32_t c = 0; c < C && !rc; c++) {
+        p->tid[c] = pf_bam_tid(bam, g->names[c]);
+        pf_cfg_t *cf = &p->cfg[c];
+        cf->k = o->k > 0 ? o->k : 3;
+        cf->k_span = o->k_span > 0 ? o->k_span : 5000;
+        cf->hard_cov = 15;
+        if (o->mode == PF_MODE_METHPHASE) {
+            int sel = o->cov_for_selection, nc = o->n_cand, rt = o->cov_for_runtime;
+            if (sel <= 0) {                                   /* 4357-4374 */
+                const int cov = (p->tid[c] >= 0 && p->tid[c] < nt) ? covs[p->tid[c]] : 0;
+                sel = cov / 10 + 1;
+                rt = 2 * sel;
+                nc = cov / 4 + 1;
+            } else if (rt <= 0) {
+                rt = 2 * sel;                                  /* config.cov_for_runtime, 4655 */
+            }
+            if (sel <= 0) sel = 1;                             /* clamps, 4381-4390 */
+            if (nc <= 1) nc = 2;
+            cf->cov_for_selection = sel; cf->cov_for_runtime = rt; cf->n_cand = nc;
+        } else {                                               /* 5045-5051: no clamps */
+            /* covs is indexed by the VCF contig index here, as the reference
+             * does (covs[i_ref], 5046); out of range reads as 0 */
+            const int cov = o->cov > 0 ? o->cov : ((int32_t)c < nt ? covs[c] : 0);
+            cf->cov_for_selection = cov / 10 + 1;
+            cf->cov_for_runtime = 2 * cf->cov_for_selection;
+            cf->n_cand = cov / 4 + 1;
+        }
+        uint64_t n_c;
+        if (o->mode == PF_MODE_METHPHASE) {
+            n_c = g->gap_off[c + 1] - g->gap_off[c];
+        } else {
+            const int64_t r = pf_report_windows(g->abs_start[c], g->raw_start + g->raw_off[c], g->raw_end + g->raw_off[c],
+                                                g->raw_off[c + 1] - g->raw_off[c], (uint32_t)o->chunk_size,
+                                                (uint32_t)o->chunk_stride, NULL, NULL, 0);
+            if (r < 0) { rc = (int)r; break; }
+            n_c = (uint64_t)r;
+        }
+        if (nw + n_c > cap) {
+            uint64_t nc2 = cap ? cap : 1024;
+            while (nc2 < nw + n_c) nc2 *= 2;
+            uint32_t *a = (uint32_t *)realloc(p->win_start, nc2 * sizeof(uint32_t));
+            if (!a) { rc = PF_ERR_NOMEM; break; }
+            p->win_start = a;
+            a = (uint32_t *)realloc(p->win_end, nc2 * sizeof(uint32_t));
+            if (!a) { rc = PF_ERR_NOMEM; break; }
+            p->win_end = a;
+            cap = nc2;
+        }
+        if (o->mode == PF_MODE_METHPHASE) {
+            memcpy(p->win_start + nw, g->gap_start + g->gap_off[c], n_c * sizeof(uint32_t));
+            memcpy(p->win_end + nw, g->gap_end + g->gap_off[c], n_c * sizeof(uint32_t));
+        } else if (n_c) {
+            const int64_t r = pf_report_windows(g->abs_start[c], g->raw_start + g->raw_off[c], g->raw_end + g->raw_off[c],
+                                                g->raw_off[c + 1] - g->raw_off[c], (uint32_t)o->chunk_size,
+                                                (uint32_t)o->chunk_stride, p->win_start + nw, p->win_end + nw, n_c);
+            if (r != (int64_t)n_c) { rc = PF_ERR_INTERNAL; break; }
+        }
+        nw += n_c;
+        p->win_off[c + 1] = nw;
+        if (o->mode == PF_MODE_REPORT && o->verbose >= 0)
+            fprintf(stderr, "[M::%s] %s has %d intervals\n", "main_methreport", g->names[c], (int)n_c);
+    }
+    free(covs);
+    pf_bam_close(bam);
+    if (rc) { pf_mp_free(p); return rc; }
+    if (nw > UINT32_MAX) { pf_mp_free(p); return PF_ERR_LIMIT; }
+    p->n_windows = (uint32_t)nw;
+
+    /* window jobs: runs of consecutive windows of one contig, at most
+     * job_windows windows and, with several devices or ranks, small enough
+     * that every one gets several jobs */
+    const uint32_t jw = o->job_windows ? o->job_windows : PF_JOB_WINDOWS_DEFAULT;
+    double tot_span = 0;
+    for (uint64_t w = 0; w < nw; w++) tot_span += (double)(p->win_end[w] - p->win_start[w]) + 2.0 * PF_READBACK;
+    const int32_t par = (o->world > 1 ? o->world : 1) * (o->n_devices > 1 ? o->n_devices : 1);
+    const double span_cap = par > 1 ? tot_span / (4.0 * par) : 1e300;
+    uint32_t nj = 0, jcap = 64;
+    p->jobs = (job_t *)calloc(jcap, sizeof(job_t));
+    if (!p->jobs) { pf_mp_free(p); return PF_ERR_NOMEM; }
+    for (uint32_t c = 0; c < C; c++) {
+        uint64_t w = p->win_off[c];
+        while (w < p->win_off[c + 1]) {
+            const uint64_t w0 = w;
+            double span = 0;
+            while (w < p->win_off[c + 1] && w - w0 < jw && (w == w0 || span < span_cap)) {
+                span += (double)(p->win_end[w] - p->win_start[w]) + 2.0 * PF_READBACK;
+                w++;
+            }
+            if (nj == jcap) {
+                job_t *nj2 = (job_t *)realloc(p->jobs, 2 * jcap * sizeof(job_t));
+                if (!nj2) { pf_mp_free(p); return PF_ERR_NOMEM; }
+                memset(nj2 + jcap, 0, jcap * sizeof(job_t));
+                p->jobs = nj2;
+                jcap *= 2;
+            }
+            job_t *J = &p->jobs[nj++];
+            J->contig = c; J->w0 = (uint32_t)w0; J->w1 = (uint32_t)w; J->cost = span;
+        }
+    }
+    p->n_jobs = nj;
+    rc = lpt(p->jobs, nj, o->world, &p->order);
+    /* -u pre-pass jobs: one per contig present in the BAM (cost: contig length) */
+    if (!rc && o->untagged) {
+        p->ujobs = (job_t *)calloc(C ? C : 1, sizeof(job_t));
+        if (!p->ujobs) rc = PF_ERR_NOMEM;
+        uint32_t nu = 0;
+        pf_bam_t *b2 = NULL;
+        if (!rc) rc = pf_bam_open(o->bam_path, NULL, &b2);
+        for (uint32_t c = 0; c < C && !rc; c++) {
+            if (p->tid[c] < 0) continue;
+            job_t *J = &p->ujobs[nu++];
+            J->contig = c;
+            J->cost = (double)pf_bam_target_len(b2, p->tid[c]);
+        }
+        if (b2) pf_bam_close(b2);
+        p->n_ujobs = nu;
+        if (!rc) rc = lpt(p->ujobs, nu, o->world, &p->uorder);
+    }
+    p->raw = pf_tags_new();
+    p->qname_hp = pf_tags_new();
+    if (!rc && (!p->raw || !p->qname_hp)) rc = PF_ERR_NOMEM;
+    if (rc) { pf_mp_free(p); return rc; }
+    mp_log(p, "[M::pf_mp_plan] %s: %ld windows in %ld jobs", o->mode == PF_MODE_REPORT ? "report" : "methphase",
+           (long)p->n_windows, (long)p->n_jobs);
+    *out = p;
+    return PF_OK;
+}
+
+uint32_t pf_mp_n_jobs(const pf_mp_plan_t *p, int kind) {
+    if (!p) return 0;
+    return kind == PF_JOB_HAPTAG ? p->n_ujobs : p->n_jobs;
+}
+
+static job_t *job_of(const pf_mp_plan_t *p, int kind, uint32_t j) {
+    if (!p) return NULL;
+    if (kind == PF_JOB_HAPTAG) return j < p->n_ujobs ? &p->ujobs[j] : NULL;
+    return j < p->n_jobs ? &p->jobs[j] : NULL;
+}
+
+int pf_mp_job_info(const pf_mp_plan_t *p, int kind, uint32_t j, pf_mp_job_info_t *info) {
+    const job_t *J = job_of(p, kind, j);
+    if (!J || !info) return PF_ERR_ARG;
+    const uint32_t *ord = kind == PF_JOB_HAPTAG ? p->uorder : p->order;
+    const uint32_t n = kind == PF_JOB_HAPTAG ? p->n_ujobs : p->n_jobs;
+    uint32_t pos = 0;
+    for (uint32_t i = 0; i < n; i++) if (ord[i] == j) { pos = i; break; }
+    info->contig = J->contig;
+    info->contig_name = p->gaps->names[J->contig];
+    info->w0 = J->w0;
+    info->w1 = J->w1;
+    info->rank = J->rank;
+    info->lpt_pos = pos;
+    info->cost = J->cost;
+    info->done = J->done;
+    info->cfg = p->cfg[J->contig];
+    return PF_OK;
+}
+
+int pf_mp_windows(const pf_mp_plan_t *p, const uint32_t **win_start, const uint32_t **win_end,
+                  const uint64_t **contig_win_off, uint32_t *n_windows) {
+    if (!p) return PF_ERR_ARG;
+    if (win_start) *win_start = p->win_start;
+    if (win_end) *win_end = p->win_end;
+    if (contig_win_off) *contig_win_off = p->win_off;
+    if (n_windows) *n_windows = p->n_windows;
+    return PF_OK;
+}
+
+const pf_gaps_t *pf_mp_gaps(const pf_mp_plan_t *p) { return p ? p->gaps : NULL; }
+const pf_blocks_t *pf_mp_blocks(const pf_mp_plan_t *p) { return p ? p->blocks : NULL; }
+const pf_tags_t *pf_mp_qname_hp(const pf_mp_plan_t *p) { return p ? p->qname_hp : NULL; }
+const pf_tags_t *pf_mp_raw_hp(const pf_mp_plan_t *p) { return p && p->o.untagged ? p->raw : NULL; }
+
+int pf_mp_decisions(const pf_mp_plan_t *p, const int8_t **dec, uint32_t *n, uint32_t *n_limit) {
+    if (!p || !p->finished) return PF_ERR_ARG;
+    if (dec) *dec = p->decision;
+    if (n) *n = p->n_windows;
+    if (n_limit) *n_limit = p->n_limit;
+    return PF_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* job results                                                          */
+
+int pf_mp_get_job_result(const pf_mp_plan_t *p, int kind, uint32_t j, pf_mp_job_result_t *r) {
+    const job_t *J = job_of(p, kind, j);
+    if (!J || !r) return PF_ERR_ARG;
+    if (!J->done) return PF_ERR_ARG;
+    if (J->n_ent > UINT32_MAX) return PF_ERR_LIMIT;
+    r->n_windows = J->w1 - J->w0;
+    r->decision = J->dec;
+    r->tag_off = J->tag_off;
+    r->tags.n = (uint32_t)J->n_ent;
+    r->tags.off = J->name_off;
+    r->tags.names = J->names;
+    r->tags.hp = J->hp;
+    r->n_limit = J->n_limit;
+    return PF_OK;
+}
+
+static int job_store(job_t *J, uint32_t n_win, const int8_t *dec, const uint64_t *tag_off, uint64_t n_ent,
+                     const uint64_t *name_off, const char *names, const uint8_t *hp, uint32_t n_limit) {
+    job_clear(J);
+    J->dec = (int8_t *)malloc(n_win ? n_win : 1);
+    J->tag_off = (uint64_t *)malloc((n_win + 1) * sizeof(uint64_t));
+    J->name_off = (uint64_t *)malloc((n_ent + 1) * sizeof(uint64_t));
+    const uint64_t nb = n_ent ? name_off[n_ent] - name_off[0] : 0;
+    J->names = (char *)malloc(nb ? nb : 1);
+    J->hp = (uint8_t *)malloc(n_ent ? n_ent : 1);
+    if (!J->dec || !J->tag_off || !J->name_off || !J->names || !J->hp) { job_clear(J); return PF_ERR_NOMEM; }
+    if (n_win) memcpy(J->dec, dec, n_win);
+    if (tag_off) for (uint32_t w = 0; w <= n_win; w++) J->tag_off[w] = tag_off[w] - tag_off[0];
+    else for (uint32_t w = 0; w <= n_win; w++) J->tag_off[w] = 0;
+    for (uint64_t i = 0; i <= n_ent; i++) J->name_off[i] = n_ent ? name_off[i] - name_off[0] : 0;
+    if (nb) memcpy(J->names, names + name_off[0], nb);
+    if (n_ent) memcpy(J->hp, hp, n_ent);
+    J->n_ent = n_ent;
+    J->n_limit = n_limit;
+    J->done = 1;
+    return PF_OK;
+}
+
+int pf_mp_set_job_result(pf_mp_plan_t *p, int kind, uint32_t j, const pf_mp_job_result_t *r) {
+    job_t *J = job_of(p, kind, j);
+    if (!J || !r) return PF_ERR_ARG;
+    if (r->n_windows != J->w1 - J->w0) return PF_ERR_ARG;
+    if (r->n_windows && !r->decision) return PF_ERR_ARG;
+    if (r->tags.n && (!r->tags.off || !r->tags.names || !r->tags.hp)) return PF_ERR_ARG;
+    if (kind != PF_JOB_HAPTAG && r->tag_off && r->tag_off[r->n_windows] - r->tag_off[0] != r->tags.n)
+        return PF_ERR_ARG;
+    if (kind != PF_JOB_HAPTAG && r->tags.n && !r->tag_off) return PF_ERR_ARG;
+    static const uint64_t zero = 0;
+    return job_store(J, r->n_windows, r->decision, kind == PF_JOB_HAPTAG ? NULL : r->tag_off, r->tags.n,
+                     r->tags.n ? r->tags.off : &zero, r->tags.names, r->tags.hp, r->n_limit);
+}
+
+/* ------------------------------------------------------------------ */
+/* running jobs on a device                                             */
+
+typedef struct {                /* a growable (qname, hp) list */
+    uint64_t n, cap;
+    uint64_t *off;
+    char *names;
+    uint64_t nb, nbcap;
+    uint8_t *hp;
+} entlist_t;
+
+static void ent_free(entlist_t *e) { free(e->off); free(e->names); free(e->hp); memset(e, 0, sizeof *e); }
+
+static int ent_push(entlist_t *e, const char *nm, size_t l, uint8_t hp) {
+    if (!e->off) {
+        e->cap = 1024;
+        e->off = (uint64_t *)malloc((e->cap + 1) * sizeof(uint64_t));
+        e->hp = (uint8_t *)malloc(e->cap);
+        e->nbcap = 16384;
+        e->names = (char *)malloc(e->nbcap);
+        if (!e->off || !e->hp || !e->names) return PF_ERR_NOMEM;
+        e->off[0] = 0;
+    }
+    if (e->n + 1 > e->cap) {
+        e->cap *= 2;
+        uint64_t *o = (uint64_t *)realloc(e->off, (e->cap + 1) * sizeof(uint64_t));
+        uint8_t *h = o ? (uint8_t *)realloc(e->hp, e->cap) : NULL;
+        if (o) e->off = o;
+        if (!o || !h) return PF_ERR_NOMEM;
+        e->hp = h;
+    }
+    if (e->nb + l > e->nbcap) {
+        while (e->nb + l > e->nbcap) e->nbcap *= 2;
+        char *s = (char *)realloc(e->names, e->nbcap);
+        if (!s) return PF_ERR_NOMEM;
+        e->names = s;
+    }
+    memcpy(e->names + e->nb, nm, l);
+    e->nb += l;
+    e->hp[e->n++] = hp;
+    e->off[e->n] = e->nb;
+    return PF_OK;
+}
+
+int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
+    job_t *J = job_of(p, PF_JOB_HAPTAG, j);
+    if (!J || !ctx) return PF_ERR_ARG;
+    const char *contig = p->gaps->names[J->contig];
+    pf_known_table_t *kt = NULL;
+    pf_bam_t *bam = NULL;
+    pf_bam_reads_t *rd = NULL;
+    uint8_t *hp = NULL;
+    entlist_t e = {0};
+    pf_tags_t *seen = NULL;
+    int rc = pf_vcf_known_vars(p->vcf_path, contig, &kt);
+    if (!rc && kt->vars.n) rc = pf_bam_open(p->bam_path, NULL, &bam);
+    if (!rc && kt->vars.n) rc = pf_bam_fetch_contig_reads(bam, contig, &rd);
+    if (!rc && rd && rd->reads.n_reads) {
+        hp = (uint8_t *)malloc(rd->reads.n_reads);
+        seen = pf_tags_new();
+        if (!hp || !seen) rc = PF_ERR_NOMEM;
+        if (!rc) rc = pf_haptag_reads(ctx, &kt->vars, &rd->reads, hp);
+        /* the contig's table, first wins (1880-1889), kept in BAM order */
+        for (uint32_t r = 0; r < rd->reads.n_reads && !rc; r++) {
+            const char *nm = rd->qname + rd->qname_off[r];
+            const size_t l = (size_t)(rd->qname_off[r + 1] - rd->qname_off[r]);
+            const int ins = tags_put(seen, nm, l, hp[r]);
+            if (ins < 0) rc = ins;
+            else if (ins) rc = ent_push(&e, nm, l, hp[r]);
+        }
+    }
+    if (!rc) {
+        static const uint64_t zero = 0;
+        rc = job_store(J, 0, NULL, NULL, e.n, e.off ? e.off : &zero, e.names, e.hp, 0);
+    }
+    ent_free(&e);
+    pf_tags_free(seen);
+    free(hp);
+    if (rd) pf_bam_reads_free(rd);
+    if (bam) pf_bam_close(bam);
+    if (kt) pf_known_table_free(kt);
+    return rc;
+}
+
+int pf_mp_merge_raw(pf_mp_plan_t *p) {
+    if (!p) return PF_ERR_ARG;
+    if (!p->o.untagged) { p->raw_merged = 1; return PF_OK; }
+    /* contig order, first wins across contigs (the -u table is one hash
+     * filled contig by contig, 2069-2080) */
+    uint32_t *by_contig = (uint32_t *)malloc((p->n_contigs ? p->n_contigs : 1) * sizeof(uint32_t));
+    if (!by_contig) return PF_ERR_NOMEM;
+    for (uint32_t c = 0; c < p->n_contigs; c++) by_contig[c] = UINT32_MAX;
+    for (uint32_t j = 0; j < p->n_ujobs; j++) {
+        if (!p->ujobs[j].done) { free(by_contig); return PF_ERR_ARG; }
+        by_contig[p->ujobs[j].contig] = j;
+    }
+    int rc = PF_OK;
+    for (uint32_t c = 0; c < p->n_contigs && !rc; c++) {
+        if (by_contig[c] == UINT32_MAX) continue;
+        const job_t *J = &p->ujobs[by_contig[c]];
+        if (J->n_ent > UINT32_MAX) { rc = PF_ERR_LIMIT; break; }
+        const int64_t r = pf_tags_put_first(p->raw, (uint32_t)J->n_ent, J->name_off, J->names, J->hp);
+        if (r < 0) rc = (int)r;
+    }
+    free(by_contig);
+    if (!rc) p->raw_merged = 1;
+    return rc;
+}
+
+/* fetch of one job (host), separate from the device part so that the next
+ * job's fetch overlaps this job's kernels */
+typedef struct {
+    pf_bam_records_t *recs;
+    int rc;
+} fetch_t;
+
+static int job_fetch(const pf_mp_plan_t *p, pf_bam_t *bam, const job_t *J, fetch_t *f) {
+    f->recs = NULL;
+    f->rc = PF_OK;
+    if (p->tid[J->contig] < 0) return PF_OK;
+    f->rc = pf_bam_fetch_windows(bam, p->gaps->names[J->contig], J->w1 - J->w0, p->win_start + J->w0,
+                                 p->win_end + J->w0, PF_READBACK, p->o.threads > 0 ? p->o.threads : 1, &f->recs);
+    if (!f->rc && p->o.untagged) {              /* the -u table replaces HP (1114-1122) */
+        pf_aln_batch_t *a = &f->recs->aln;
+        f->rc = (int)pf_tags_get(p->raw, a->n_recs, f->recs->qname_off, f->recs->qname, 254, (uint8_t *)a->hp);
+        if (f->rc > 0) f->rc = 0;
+    }
+    return f->rc;
+}
+
+/* upload + run a sub-batch of windows [a, b) of the fetched records */
+static int run_windows(const pf_mp_plan_t *p, pf_ctx_t *ctx, const job_t *J, const pf_bam_records_t *R,
+                       const uint32_t *sel, uint32_t n_sel, int8_t *dec, entlist_t *ent, uint64_t *win_ent) {
+    const pf_aln_batch_t *A = &R->aln;
+    const pf_cfg_t *cf = &p->cfg[J->contig];
+    pf_load_cfg_t lc = p->o.load;
+    /* gather the selected windows (usually all of them, in order) */
+    pf_aln_batch_t a = *A;
+    uint32_t *wro = NULL;
+    int all = n_sel == A->n_windows;
+    for (uint32_t i = 0; all && i < n_sel; i++) all = sel[i] == i;
+    if (!all) {
+        /* a single window: slice the arrays (offsets stay absolute) */
+        if (n_sel != 1) return PF_ERR_INTERNAL;
+        const uint32_t w = sel[0];
+        const uint32_t r0 = A->win_rec_off[w], r1 = A->win_rec_off[w + 1];
+        wro = (uint32_t *)malloc(2 * sizeof(uint32_t));
+        if (!wro) return PF_ERR_NOMEM;
+        wro[0] = 0; wro[1] = r1 - r0;
+        a.n_windows = 1; a.n_recs = r1 - r0;
+        a.win_start = A->win_start + w; a.win_end = A->win_end + w; a.win_rec_off = wro;
+        a.flag = A->flag + r0; a.mapq = A->mapq + r0; a.pos = A->pos + r0; a.l_qseq = A->l_qseq + r0;
+        a.de = A->de + r0; a.hp = A->hp + r0;
+        a.cigar_off = A->cigar_off + r0; a.seq_off = A->seq_off + r0; a.mm_off = A->mm_off + r0;
+        a.ml_off = A->ml_off + r0;
+    }
+    pf_dbatch_t *db = NULL;
+    int rc = pf_batch_upload_aln(ctx, cf, &lc, &a, &db);
+    /* the kept reads are known after a run (K0 sizes the batch on the
+     * device); the records bound them */
+    const uint32_t W = a.n_windows, cap = a.n_recs ? a.n_recs : 1;
+    uint32_t R_ = 0;
+    uint32_t *rec_of = NULL;
+    uint8_t *rhp = NULL;
+    int8_t *d = NULL;
+    if (!rc) {
+        rec_of = (uint32_t *)malloc(cap * sizeof(uint32_t));
+        rhp = (uint8_t *)malloc(cap);
+        d = (int8_t *)malloc(W ? W : 1);
+        if (!rec_of || !rhp || !d) rc = PF_ERR_NOMEM;
+    }
+    if (!rc) {
+        pf_window_out_t o;
+        memset(&o, 0, sizeof o);
+        o.decision = d;
+        o.read_hp = rhp;
+        rc = pf_methphase_run(ctx, db, &o);
+    }
+    if (!rc) {
+        R_ = pf_batch_n_reads(db);
+        if (R_ > cap) rc = PF_ERR_INTERNAL;
+    }
+    if (!rc) rc = pf_batch_read_recs(db, rec_of, cap);
+    if (!rc) {
+        /* reads are the kept records in record order; window w's reads are
+         * those whose record lies in [win_rec_off[w], win_rec_off[w+1]) */
+        const uint64_t rbase = a.win_rec_off == wro ? A->win_rec_off[sel[0]] : 0;
+        uint32_t i = 0;
+        for (uint32_t w = 0; w < W && !rc; w++) {
+            const uint32_t gw = all ? w : sel[0];
+            dec[gw] = d[w];
+            const uint32_t rend = a.win_rec_off[w + 1];
+            const uint64_t e0 = ent->n;
+            for (; i < R_ && rec_of[i] < rend; i++) {
+                if (d[w] < 0 || p->o.mode == PF_MODE_REPORT) continue;
+                const uint64_t rec = rbase + rec_of[i];
+                rc = ent_push(ent, R->qname + R->qname_off[rec], (size_t)(R->qname_off[rec + 1] - R->qname_off[rec]),
+                              rhp[i]);
+                if (rc) break;
+            }
+            win_ent[gw] = ent->n - e0;
+        }
+    }
+    if (db) pf_batch_free(db);
+    free(rec_of); free(rhp); free(d); free(wro);
+    return rc;
+}
+
+static int job_device(pf_mp_plan_t *p, pf_ctx_t *ctx, job_t *J, fetch_t *f) {
+    if (f->rc) return f->rc;
+    const uint32_t n = J->w1 - J->w0;
+    int8_t *dec = (int8_t *)malloc(n ? n : 1);
+    uint64_t *cnt = (uint64_t *)calloc(n + 1, sizeof(uint64_t));
+    uint64_t *toff = (uint64_t *)calloc(n + 1, sizeof(uint64_t));
+    uint32_t *sel = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    entlist_t ent = {0};
+    uint32_t n_limit = 0;
+    int rc = (!dec || !cnt || !toff || !sel) ? PF_ERR_NOMEM : PF_OK;
+    for (uint32_t w = 0; w < n && !rc; w++) dec[w] = -1;
+    if (!rc && f->recs && n) {
+        const pf_aln_batch_t *A = &f->recs->aln;
+        /* windows over the device's per-window read limit stay undecided */
+        uint32_t ns = 0, big = 0;
+        for (uint32_t w = 0; w < n; w++) {
+            if (A->win_rec_off[w + 1] - A->win_rec_off[w] > PF_MAX_WIN_RECS) { big++; continue; }
+            sel[ns++] = w;
+        }
+        if (big == 0) {
+            rc = run_windows(p, ctx, J, f->recs, sel, ns, dec, &ent, cnt);
+        }
+        if (big || rc == PF_ERR_LIMIT) {
+            /* window by window; a window the device refuses stays -1 */
+            ent.n = 0; ent.nb = 0;
+            if (ent.off) ent.off[0] = 0;
+            memset(cnt, 0, (n + 1) * sizeof(uint64_t));
+            for (uint32_t w = 0; w < n; w++) dec[w] = -1;
+            rc = PF_OK;
+            for (uint32_t w = 0; w < n && !rc; w++) {
+                if (A->win_rec_off[w + 1] - A->win_rec_off[w] > PF_MAX_WIN_RECS) {
+                    fprintf(stderr, "[W::pomfret_amd] %s:%u-%u: %u records exceed the device limit of %u reads "
+                            "per window; left undecided\n", p->gaps->names[J->contig], A->win_start[w],
+                            A->win_end[w], A->win_rec_off[w + 1] - A->win_rec_off[w], PF_MAX_WIN_RECS);
+                    n_limit++;
+                    continue;
+                }
+                const uint32_t one = w;
+                rc = run_windows(p, ctx, J, f->recs, &one, 1, dec, &ent, cnt);
+                if (rc == PF_ERR_LIMIT) {
+                    fprintf(stderr, "[W::pomfret_amd] %s:%u-%u exceeds a device limit; left undecided\n",
+                            p->gaps->names[J->contig], A->win_start[w], A->win_end[w]);
+                    dec[w] = -1;
+                    cnt[w] = 0;
+                    n_limit++;
+                    rc = PF_OK;
+                }
+            }
+        }
+    }
+    if (!rc) {
+        toff[0] = 0;
+        for (uint32_t w = 0; w < n; w++) toff[w + 1] = toff[w] + cnt[w];
+        static const uint64_t zero = 0;
+        rc = job_store(J, n, dec, toff, ent.n, ent.off ? ent.off : &zero, ent.names, ent.hp, n_limit);
+    }
+    ent_free(&ent);
+    free(dec); free(cnt); free(toff); free(sel);
+    return rc;
+}
+
+int pf_mp_run_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
+    job_t *J = job_of(p, PF_JOB_WINDOWS, j);
+    if (!J || !ctx) return PF_ERR_ARG;
+    if (p->o.untagged && !p->raw_merged) return PF_ERR_ARG;
+    pf_bam_t *bam = NULL;
+    int rc = pf_bam_open(p->bam_path, NULL, &bam);
+    if (rc) return rc;
+    fetch_t f;
+    rc = job_fetch(p, bam, J, &f);
+    if (!rc) rc = job_device(p, ctx, J, &f);
+    if (f.recs) pf_bam_records_free(f.recs);
+    pf_bam_close(bam);
+    return rc;
+}
+
+/* ------------------------------------------------------------------ */
+/* finish: merge, blocks, outputs                                       */
+
+static int write_report(pf_mp_plan_t *p) {
+    char *fn = (char *)malloc(strlen(p->out_prefix) + 32);
+    if (!fn) return PF_ERR_NOMEM;
+    sprintf(fn, "%s.report.tsv", p->out_prefix);
+    FILE *fo = fopen(fn, "w");
+    free(fn);
+    if (!fo) return -1;
+    float n_switch = 0, n_fail = 0, n_correct = 0;    /* main_methreport's counters (4962-4965) */
+    int tot = 0;
+    for (uint32_t c = 0; c < p->n_contigs; c++) {
+        for (uint64_t w = p->win_off[c]; w < p->win_off[c + 1]; w++) {
+            const int start = (int)p->win_start[w], end = (int)p->win_end[w];
+            fprintf(fo, "%s\t%d\t%d\t", p->gaps->names[c], start, end);
+            const int d = p->decision[w];
+            if (d == 0) { n_correct++; fprintf(fo, "correct\n"); }
+            else if (d == 1) { n_switch++; fprintf(fo, "switch\n"); }
+            else { n_fail++; fprintf(fo, "fail\n"); }
+            tot++;
+            if (tot % 100 == 0)
+                fprintf(stdout, "Parsed N=%d regions, currently at %s:%d-%d, correct/(correct+switch)=%.2f%%, "
+                        "correct/N=%.2f%%\n", tot, p->gaps->names[c], start, end,
+                        n_correct / (n_correct + n_switch) * 100.0, n_correct / (float)tot * 100.0);
+        }
+    }
+    fprintf(stdout, "Total N=%d regions, correct/(correct+switch)=%.2f%%, correct/N=%.2f%%\n",
+            tot, n_correct / (n_correct + n_switch) * 100.0, n_correct / (float)tot * 100.0);
+    fprintf(stderr, "[M::%s] Total N=%d regions, correct/(correct+switch)=%.2f%%, correct/N=%.2f%%\n",
+            "main_methreport", tot, n_correct / (n_correct + n_switch) * 100.0, n_correct / (float)tot * 100.0);
+    fflush(stdout);
+    p->report_counts[0] = n_correct; p->report_counts[1] = n_switch; p->report_counts[2] = n_fail;
+    return fclose(fo) ? -1 : PF_OK;
+}
+
+static int write_methphase_outputs(pf_mp_plan_t *p) {
+    const size_t L = strlen(p->out_prefix) + 32;
+    char *fn = (char *)malloc(L);
+    if (!fn) return PF_ERR_NOMEM;
+    snprintf(fn, L, "%s.mp.gtf", p->out_prefix);
+    int rc = pf_write_gtf(p->gaps, p->blocks, fn);
+    if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] gtf written.\n");
+    if (!rc && p->o.write_tsv) {
+        snprintf(fn, L, "%s.mp.tsv", p->out_prefix);
+        rc = pf_write_tsv(p->gaps, p->blocks, fn);
+        if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] tsv written.\n");
+    }
+    /* rescue of dropped-interval sites (recover_variant_phase_in_dropped_intervals) + VCF */
+    const uint32_t C = p->n_contigs;
+    uint64_t *roff = (uint64_t *)calloc(C + 1, sizeof(uint64_t));
+    uint32_t *rpos = NULL;
+    uint8_t *rhap = NULL;
+    uint64_t rn = 0, rcap = 0;
+    pf_bam_t *bam = NULL;
+    pf_qname_tags_t tm, tr;
+    if (!rc && !roff) rc = PF_ERR_NOMEM;
+    if (!rc) rc = pf_tags_view(p->qname_hp, &tm);
+    if (!rc && p->o.untagged) rc = pf_tags_view(p->raw, &tr);
+    for (uint32_t c = 0; c < C && !rc; c++) {
+        const pf_gaps_t *g = p->gaps;
+        const uint64_t nd = g->drop_off[c + 1] - g->drop_off[c];
+        roff[c + 1] = rn;
+        if (!nd || p->tid[c] < 0) continue;
+        if (!bam && (rc = pf_bam_open(p->bam_path, NULL, &bam))) break;
+        pf_known_table_t *kt = NULL;
+        pf_rescue_map_t *m = NULL;
+        rc = pf_vcf_known_vars(p->vcf_path, g->names[c], &kt);
+        if (!rc) rc = pf_rescue_dropped(bam, g->names[c], (uint32_t)nd, g->drop_start + g->drop_off[c],
+                                        g->drop_end + g->drop_off[c], &kt->vars, &tm, p->o.untagged ? &tr : NULL, &m);
+        if (!rc && m->n) {
+            if (rn + m->n > rcap) {
+                while (rcap < rn + m->n) rcap = rcap ? 2 * rcap : 1024;
+                uint32_t *a = (uint32_t *)realloc(rpos, rcap * sizeof(uint32_t));
+                uint8_t *b = a ? (uint8_t *)realloc(rhap, rcap) : NULL;
+                if (a) rpos = a;
+                if (!a || !b) rc = PF_ERR_NOMEM;
+                else rhap = b;
+            }
+            if (!rc) {
+                memcpy(rpos + rn, m->pos, m->n * sizeof(uint32_t));
+                memcpy(rhap + rn, m->hap_of_ref, m->n);
+                rn += m->n;
+                roff[c + 1] = rn;
+            }
+        }
+        if (m) pf_rescue_map_free(m);
+        if (kt) pf_known_table_free(kt);
+    }
+    if (bam) pf_bam_close(bam);
+    if (!rc) {
+        pf_rescue_t res = {roff, rpos ? rpos : (const uint32_t *)roff, rhap ? rhap : (const uint8_t *)roff};
+        snprintf(fn, L, "%s.mp.vcf", p->out_prefix);
+        if (p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] writing vcf...\n");
+        rc = pf_write_vcf(p->vcf_path, p->gaps, p->blocks, &res, fn, NULL);
+        if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] vcf written.\n");
+    }
+    free(roff); free(rpos); free(rhap); free(fn);
+    return rc;
+}
+
+int pf_mp_finish(pf_mp_plan_t *p) {
+    if (!p) return PF_ERR_ARG;
+    if (p->finished) return PF_OK;
+    free(p->decision);
+    p->decision = (int8_t *)malloc(p->n_windows ? p->n_windows : 1);
+    if (!p->decision) return PF_ERR_NOMEM;
+    for (uint32_t w = 0; w < p->n_windows; w++) p->decision[w] = -1;
+    p->n_limit = 0;
+    /* jobs are runs of consecutive windows: visiting them by w0 visits the
+     * windows in (contig, window) order, the order in which the reference's
+     * per-contig tables fill (4396-4423) and then merge (4579-4595) */
+    uint32_t *by_w0 = (uint32_t *)malloc((p->n_jobs ? p->n_jobs : 1) * sizeof(uint32_t));
+    if (!by_w0) return PF_ERR_NOMEM;
+    for (uint32_t j = 0; j < p->n_jobs; j++) by_w0[j] = j;
+    for (uint32_t a = 1; a < p->n_jobs; a++) {            /* already sorted by construction */
+        uint32_t x = by_w0[a], b = a;
+        while (b > 0 && p->jobs[by_w0[b - 1]].w0 > p->jobs[x].w0) { by_w0[b] = by_w0[b - 1]; b--; }
+        by_w0[b] = x;
+    }
+    int rc = PF_OK;
+    for (uint32_t k = 0; k < p->n_jobs && !rc; k++) {
+        const job_t *J = &p->jobs[by_w0[k]];
+        if (!J->done) { rc = PF_ERR_ARG; break; }
+        p->n_limit += J->n_limit;
+        for (uint32_t w = J->w0; w < J->w1 && !rc; w++) {
+            const uint32_t i = w - J->w0;
+            p->decision[w] = J->dec[i];
+            if (J->dec[i] < 0 || p->o.mode == PF_MODE_REPORT) continue;
+            for (uint64_t e = J->tag_off[i]; e < J->tag_off[i + 1]; e++) {
+                const int r = tags_put(p->qname_hp, J->names + J->name_off[e],
+                                       (size_t)(J->name_off[e + 1] - J->name_off[e]), J->hp[e]);
+                if (r < 0) { rc = r; break; }
+            }
+        }
+    }
+    free(by_w0);
+    if (rc) return rc;
+    if (p->o.mode == PF_MODE_REPORT) {
+        if (p->out_prefix) rc = write_report(p);
+    } else {
+        rc = pf_phase_blocks(p->gaps, p->decision, &p->blocks);
+        if (!rc && p->out_prefix) rc = write_methphase_outputs(p);
+    }
+    if (!rc) p->finished = 1;
+    return rc;
+}
+
+int pf_mp_report_counts(const pf_mp_plan_t *p, double *counts3) {
+    if (!p || !counts3 || !p->finished) return PF_ERR_ARG;
+    memcpy(counts3, p->report_counts, sizeof p->report_counts);
+    return PF_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* in-process driver: one host thread per device                        */
+
+typedef struct {
+    pf_mp_plan_t *p;
+    pf_ctx_t *ctx;
+    int device;
+    int own_ctx;
+    int kind;
+    atomic_uint *next;
+    const uint32_t *todo;
+    uint32_t n_todo;
+    int rc;
+} dev_worker_t;
+
+typedef struct {
+    const pf_mp_plan_t *p;
+    pf_bam_t *bam;
+    const job_t *J;
+    fetch_t f;
+} prefetch_t;
+
+static void *prefetch_main(void *arg) {
+    prefetch_t *a = (prefetch_t *)arg;
+    job_fetch(a->p, a->bam, a->J, &a->f);
+    return NULL;
+}
+
+static void *dev_main(void *arg) {
+    dev_worker_t *W = (dev_worker_t *)arg;
+    pf_mp_plan_t *p = W->p;
+    int rc = PF_OK;
+    if (!W->ctx) {
+        rc = pf_ctx_create(W->device, &W->ctx);
+        W->own_ctx = 1;
+        if (rc) { W->rc = rc; return NULL; }
+    }
+    if (W->kind == PF_JOB_HAPTAG) {
+        for (;;) {
+            const uint32_t i = atomic_fetch_add(W->next, 1);
+            if (i >= W->n_todo || rc) break;
+            rc = pf_mp_run_haptag_job(p, W->ctx, W->todo[i]);
+        }
+        W->rc = rc;
+        return NULL;
+    }
+    /* window jobs: the fetch of the next job runs on a helper thread while
+     * this thread drives the device on the current one */
+    pf_bam_t *bam[2] = {NULL, NULL};
+    rc = pf_bam_open(p->bam_path, NULL, &bam[0]);
+    if (!rc) rc = pf_bam_open(p->bam_path, NULL, &bam[1]);
+    prefetch_t cur, nxt;
+    memset(&cur, 0, sizeof cur);
+    memset(&nxt, 0, sizeof nxt);
+    uint32_t i = rc ? UINT32_MAX : atomic_fetch_add(W->next, 1);
+    int have = 0, slot = 0;
+    if (i < W->n_todo) {
+        cur.p = p; cur.bam = bam[slot]; cur.J = &p->jobs[W->todo[i]];
+        job_fetch(p, cur.bam, cur.J, &cur.f);
+        have = 1;
+    }
+    while (have && !rc) {
+        pthread_t th;
+        int spawned = 0;
+        const uint32_t k = atomic_fetch_add(W->next, 1);
+        if (k < W->n_todo) {
+            nxt.p = p; nxt.bam = bam[slot ^ 1]; nxt.J = &p->jobs[W->todo[k]];
+            nxt.f.recs = NULL; nxt.f.rc = 0;
+            spawned = pthread_create(&th, NULL, prefetch_main, &nxt) == 0;
+            if (!spawned) job_fetch(p, nxt.bam, nxt.J, &nxt.f);
+        }
+        rc = job_device(p, W->ctx, (job_t *)cur.J, &cur.f);
+        if (cur.f.recs) pf_bam_records_free(cur.f.recs);
+        cur.f.recs = NULL;
+        if (spawned) pthread_join(th, NULL);
+        if (k < W->n_todo) { cur = nxt; slot ^= 1; }
+        else have = 0;
+    }
+    if (have && cur.f.recs) pf_bam_records_free(cur.f.recs);
+    if (bam[0]) pf_bam_close(bam[0]);
+    if (bam[1]) pf_bam_close(bam[1]);
+    W->rc = rc;
+    return NULL;
+}
+
+static int run_on_devices(pf_mp_plan_t *p, const pf_methphase_opts_t *o, int kind) {
+    const uint32_t n = kind == PF_JOB_HAPTAG ? p->n_ujobs : p->n_jobs;
+    const uint32_t *ord = kind == PF_JOB_HAPTAG ? p->uorder : p->order;
+    const job_t *J = kind == PF_JOB_HAPTAG ? p->ujobs : p->jobs;
+    uint32_t *todo = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    if (!todo) return PF_ERR_NOMEM;
+    uint32_t nt = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (o->world <= 1 || J[ord[i]].rank == o->rank) todo[nt++] = ord[i];
+    int nd = o->n_ctxs > 0 ? o->n_ctxs : (o->n_devices > 0 ? o->n_devices : pf_device_count());
+    if (nd <= 0) { free(todo); return PF_ERR_HIP; }
+    dev_worker_t *W = (dev_worker_t *)calloc(nd, sizeof(dev_worker_t));
+    pthread_t *th = (pthread_t *)calloc(nd, sizeof(pthread_t));
+    atomic_uint next;
+    atomic_init(&next, 0);
+    int rc = (!W || !th) ? PF_ERR_NOMEM : PF_OK;
+    for (int d = 0; d < nd && !rc; d++) {
+        W[d].p = p; W[d].kind = kind; W[d].next = &next; W[d].todo = todo; W[d].n_todo = nt;
+        W[d].ctx = o->n_ctxs > 0 ? o->ctxs[d] : NULL;
+        W[d].device = o->devices ? o->devices[d] : d;
+    }
+    if (!rc && nd == 1) {
+        dev_main(&W[0]);
+    } else if (!rc) {
+        for (int d = 0; d < nd; d++)
+            if (pthread_create(&th[d], NULL, dev_main, &W[d])) { W[d].rc = PF_ERR_INTERNAL; th[d] = 0; }
+        for (int d = 0; d < nd; d++) if (th[d]) pthread_join(th[d], NULL);
+    }
+    for (int d = 0; d < nd && W; d++) {
+        if (!rc && W[d].rc) rc = W[d].rc;
+        if (W[d].own_ctx && W[d].ctx) pf_ctx_destroy(W[d].ctx);
+    }
+    free(W); free(th); free(todo);
+    return rc;
+}
+
+int pf_mp_run_mine(pf_mp_plan_t *p, const pf_methphase_opts_t *run_opts, int kind) {
+    if (!p || !run_opts) return PF_ERR_ARG;
+    if (kind == PF_JOB_WINDOWS && p->o.untagged && !p->raw_merged) return PF_ERR_ARG;
+    return run_on_devices(p, run_opts, kind);
+}
+
+int pf_methphase_main(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
+    if (!o || !out) return PF_ERR_ARG;
+    *out = NULL;
+    if (o->world > 1) return PF_ERR_ARG;           /* multi-process runs use the pf_mp_* steps */
+    if (o->write_bam) return PF_ERR_UNSUPPORTED;
+    pf_mp_plan_t *p = NULL;
+    int rc = pf_mp_plan(o, &p);
+    if (!rc && o->untagged) {
+        rc = run_on_devices(p, o, PF_JOB_HAPTAG);
+        if (!rc) rc = pf_mp_merge_raw(p);
+    }
+    if (!rc) rc = run_on_devices(p, o, PF_JOB_WINDOWS);
+    if (!rc) rc = pf_mp_finish(p);
+    if (rc) { pf_mp_free(p); return rc; }
+    if (p->n_limit)
+        fprintf(stderr, "[W::pomfret_amd] %u windows left undecided for exceeding a device limit\n", p->n_limit);
+    *out = p;
+    return PF_OK;
+}

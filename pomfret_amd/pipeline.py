@@ -1,128 +1,440 @@
-"""`pomfret methphase` end to end with the GPU worker, host side in C:
+"""`pomfret methphase` / `pomfret report` end to end: a thin binding of the C
+pipeline driver (pomfret_amd/csrc/pf_pipeline.c, the pf_methphase_main /
+pf_mp_* entry points of include/pomfret_amd.h).  The host side is C:
 
-    f3  pf_vcf_gaps           phase-block gaps of the phased VCF
-                              (load_intervals_from_file + merge_close_intervals,
-                              blockjoin.c:4442-4523)
-    f1  pf_bam_fetch_windows  every gap's records, as load_reads_given_interval
-                              fetches them (1053-1076)
-    GPU pf_batch_upload_aln + pf_methphase_run per contig: K0 loader, K12, K3
-                              (the kt_for worker, 4340-4426)
-    f2  pf_phase_blocks, pf_write_gtf / _tsv / _vcf
-                              (lift_decisions ... output_modify_vcf, 4685-4717)
+    f3  pf_vcf_gaps                 phase-block gaps of the phased VCF
+                                    (load_intervals_from_file + merge_close_intervals,
+                                    blockjoin.c:4442-4523)
+    -u  pf_haptag_reads per contig  K4 pre-pass, qname first-wins per contig,
+                                    merged in contig order (1841-1898, 2069-2080)
+    f1  pf_bam_fetch_windows        each job's records (1053-1076), overlapped
+                                    with the previous job's kernels
+    GPU pf_batch_upload_aln + pf_methphase_run: K0 loader, K12, K3 (the kt_for
+                                    worker, 4340-4426)
+    a1  first-wins qname -> hp of joined windows, in (contig, window) order
+                                    (4408-4423, 4572-4595), a C table (pf_tags_t)
+    f2  pf_phase_blocks, pf_write_gtf / _tsv / _vcf + pf_rescue_dropped
+                                    (lift_decisions ... output_modify_vcf, 4685-4717)
 
-With untagged=True (`--bam-is-untagged`, -u) every contig's reads are first
-haplotagged on the GPU from the VCF's phased variants (pf_vcf_known_vars +
-pf_bam_fetch_contig_reads + pf_haptag_reads, the pre-pass of 1841-1898 with
-its first-wins qname table) and those tags replace the BAM's HP in the
-loader (1114-1122: a qname missing from the table is unphased).
-
-The first-wins qname -> hp table of joined windows (4408-4423, merged across
-contigs in contig order, 4572-4590) is returned for callers that write tags,
-and drives the VCF writer's rescue of sites in dropped intervals
-(recover_variant_phase_in_dropped_intervals, 2618-2694: pf_rescue_dropped
-over the BAM).
+`methphase_files` runs everything in this process (one host thread per GPU
+it drives).  `methphase_files_dist` is the one-process-per-GPU form: every
+rank builds the same plan, runs the jobs its static LPT shard owns, and the
+job results (per-window decisions + the joined windows' qname/tag lists)
+are gathered over torch.distributed to rank 0, which merges them in window
+order and writes the outputs -- the merged tables equal the single-process
+ones exactly.
 """
 from __future__ import annotations
 
-from typing import Dict, Optional
+import ctypes as C
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 
-from ._lib import Blocks, Context, Gaps
-from .abi import Config, LoadConfig
-from .bam import READBACK, BamFile, rescue_dropped, vcf_known_vars
+from ._lib import PomfretError, _blocks_contigs, _check, _gaps_contigs, _PfBlocks, _PfGaps, lib
+from .abi import Config, LoadConfig, PfCfg, PfLoadCfg
+
+MODE_METHPHASE, MODE_REPORT = 0, 1
+JOB_WINDOWS, JOB_HAPTAG = 0, 1
+
+
+class PfMethphaseOpts(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("bam_path", C.c_char_p), ("vcf_path", C.c_char_p),
+                ("out_prefix", C.c_char_p), ("cov_for_selection", C.c_int32), ("cov_for_runtime", C.c_int32),
+                ("n_cand", C.c_int32), ("cov", C.c_int32), ("k", C.c_int32), ("k_span", C.c_int32),
+                ("load", PfLoadCfg), ("untagged", C.c_int32), ("write_tsv", C.c_int32), ("write_bam", C.c_int32),
+                ("chunk_size", C.c_int32), ("chunk_stride", C.c_int32), ("threads", C.c_int32),
+                ("n_devices", C.c_int32), ("devices", C.c_void_p), ("ctxs", C.c_void_p), ("n_ctxs", C.c_int32),
+                ("rank", C.c_int32), ("world", C.c_int32), ("job_windows", C.c_uint32), ("verbose", C.c_int32)]
+
+
+class PfQnameTagsC(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("off", C.c_void_p), ("names", C.c_void_p), ("hp", C.c_void_p)]
+
+
+class PfMpJobInfo(C.Structure):
+    _fields_ = [("contig", C.c_uint32), ("contig_name", C.c_char_p), ("w0", C.c_uint32), ("w1", C.c_uint32),
+                ("rank", C.c_int32), ("lpt_pos", C.c_uint32), ("cost", C.c_double), ("done", C.c_int32),
+                ("cfg", PfCfg)]
+
+
+class PfMpJobResult(C.Structure):
+    _fields_ = [("n_windows", C.c_uint32), ("decision", C.c_void_p), ("tag_off", C.c_void_p),
+                ("tags", PfQnameTagsC), ("n_limit", C.c_uint32)]
+
+
+_bound = False
+
+
+def _bind():
+    global _bound
+    L = lib()
+    if _bound:
+        return L
+    vp, u32, i32 = C.c_void_p, C.c_uint32, C.c_int
+    L.pf_methphase_main.argtypes = [C.POINTER(PfMethphaseOpts), C.POINTER(vp)]
+    L.pf_mp_plan.argtypes = [C.POINTER(PfMethphaseOpts), C.POINTER(vp)]
+    L.pf_mp_free.argtypes = [vp]
+    L.pf_mp_n_jobs.argtypes = [vp, i32]
+    L.pf_mp_n_jobs.restype = u32
+    L.pf_mp_job_info.argtypes = [vp, i32, u32, C.POINTER(PfMpJobInfo)]
+    L.pf_mp_windows.argtypes = [vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp), C.POINTER(u32)]
+    L.pf_mp_run_mine.argtypes = [vp, C.POINTER(PfMethphaseOpts), i32]
+    L.pf_mp_run_job.argtypes = [vp, vp, u32]
+    L.pf_mp_run_haptag_job.argtypes = [vp, vp, u32]
+    L.pf_mp_merge_raw.argtypes = [vp]
+    L.pf_mp_get_job_result.argtypes = [vp, i32, u32, C.POINTER(PfMpJobResult)]
+    L.pf_mp_set_job_result.argtypes = [vp, i32, u32, C.POINTER(PfMpJobResult)]
+    L.pf_mp_finish.argtypes = [vp]
+    L.pf_mp_decisions.argtypes = [vp, C.POINTER(vp), C.POINTER(u32), C.POINTER(u32)]
+    L.pf_mp_gaps.argtypes = [vp]
+    L.pf_mp_gaps.restype = C.POINTER(_PfGaps)
+    L.pf_mp_blocks.argtypes = [vp]
+    L.pf_mp_blocks.restype = C.POINTER(_PfBlocks)
+    L.pf_mp_qname_hp.argtypes = [vp]
+    L.pf_mp_qname_hp.restype = vp
+    L.pf_mp_raw_hp.argtypes = [vp]
+    L.pf_mp_raw_hp.restype = vp
+    L.pf_mp_report_counts.argtypes = [vp, C.POINTER(C.c_double)]
+    L.pf_tags_new.restype = vp
+    L.pf_tags_free.argtypes = [vp]
+    L.pf_tags_size.argtypes = [vp]
+    L.pf_tags_size.restype = C.c_uint64
+    L.pf_tags_put_first.argtypes = [vp, u32, vp, vp, vp]
+    L.pf_tags_put_first.restype = C.c_int64
+    L.pf_tags_get.argtypes = [vp, u32, vp, vp, C.c_uint8, vp]
+    L.pf_tags_get.restype = C.c_int64
+    L.pf_tags_view.argtypes = [vp, C.POINTER(PfQnameTagsC)]
+    _bound = True
+    return L
+
+
+def _arr(ptr, n, dt) -> np.ndarray:
+    n = int(n)
+    if n == 0 or not ptr:
+        return np.zeros(0, dt)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), (n,)).copy()
+
+
+def _names_list(off: np.ndarray, names: np.ndarray) -> List[str]:
+    b = names.tobytes()
+    return [b[off[i]:off[i + 1]].decode("ascii", "replace") for i in range(len(off) - 1)]
+
+
+def _pack_names(names: List[str]):
+    enc = [q.encode() for q in names]
+    off = np.zeros(len(enc) + 1, np.uint64)
+    if enc:
+        off[1:] = np.cumsum([len(q) for q in enc])
+    buf = np.frombuffer(b"".join(enc) or b"\0", np.uint8).copy()
+    return off, buf
+
+
+def tags_dict(t) -> Dict[str, int]:
+    """A pf_tags_t as {qname: hp} in insertion order."""
+    L = _bind()
+    if not t:
+        return {}
+    v = PfQnameTagsC()
+    _check(L.pf_tags_view(t, C.byref(v)), "pf_tags_view")
+    off = _arr(v.off, v.n + 1, np.uint64)
+    names = _arr(v.names, off[-1] if v.n else 0, np.uint8)
+    hp = _arr(v.hp, v.n, np.uint8)
+    return dict(zip(_names_list(off, names), hp.tolist()))
+
+
+class Tags:
+    """Owned pf_tags_t (first-wins qname -> hp)."""
+
+    def __init__(self):
+        self.h = _bind().pf_tags_new()
+        if not self.h:
+            raise PomfretError("pf_tags_new")
+
+    def put_first(self, names: List[str], hp) -> int:
+        off, buf = _pack_names(names)
+        hp = np.ascontiguousarray(np.asarray(hp, np.uint8) if len(names) else np.zeros(1, np.uint8))
+        r = lib().pf_tags_put_first(self.h, len(names), off.ctypes.data, buf.ctypes.data, hp.ctypes.data)
+        if r < 0:
+            _check(int(r), "pf_tags_put_first")
+        return int(r)
+
+    def get(self, names: List[str], default: int = 254) -> np.ndarray:
+        off, buf = _pack_names(names)
+        out = np.zeros(max(len(names), 1), np.uint8)
+        r = lib().pf_tags_get(self.h, len(names), off.ctypes.data, buf.ctypes.data, default, out.ctypes.data)
+        if r < 0:
+            _check(int(r), "pf_tags_get")
+        return out[:len(names)]
+
+    def __len__(self):
+        return int(lib().pf_tags_size(self.h))
+
+    def to_dict(self) -> Dict[str, int]:
+        return tags_dict(self.h)
+
+    def close(self):
+        if self.h:
+            lib().pf_tags_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def make_opts(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],
+              lcfg: Optional[LoadConfig] = None, mode: int = MODE_METHPHASE, untagged: bool = False,
+              tsv: bool = False, threads: int = 8, n_devices: int = 0, ctxs=None, rank: int = 0, world: int = 1,
+              job_windows: int = 0, cov: int = 0, chunk_size: int = 50_000, chunk_stride: int = 1_000_000,
+              verbose: int = 0):
+    """pf_methphase_opts_t from Python values.  cfg None: per-contig
+    parameters from the BAM's coverage estimate (runs without -c)."""
+    lcfg = lcfg or LoadConfig()
+    o = PfMethphaseOpts()
+    o.mode = mode
+    o.bam_path = bam_path.encode()
+    o.vcf_path = vcf_path.encode()
+    o.out_prefix = out_prefix.encode() if out_prefix else None
+    if cfg is not None:
+        o.cov_for_selection, o.cov_for_runtime, o.n_cand = cfg.cov_for_selection, cfg.cov_for_runtime, cfg.n_cand
+        o.k, o.k_span = cfg.k, cfg.k_span
+    else:
+        o.cov_for_selection, o.cov_for_runtime, o.n_cand, o.k, o.k_span = -1, 0, 15, 3, 5000
+    o.cov = int(cov)
+    o.load = lcfg.to_c()
+    o.untagged = int(bool(untagged))
+    o.write_tsv = int(bool(tsv))
+    o.chunk_size, o.chunk_stride = int(chunk_size), int(chunk_stride)
+    o.threads = int(threads)
+    o.n_devices = int(n_devices)
+    keep = None
+    if ctxs:
+        keep = (C.c_void_p * len(ctxs))(*[c.handle for c in ctxs])
+        o.ctxs = C.cast(keep, C.c_void_p)
+        o.n_ctxs = len(ctxs)
+    o.rank, o.world = int(rank), int(world)
+    o.job_windows = int(job_windows)
+    o.verbose = int(verbose)
+    o._keep = keep
+    return o
+
+
+class Plan:
+    """A pf_mp_plan_t: the deterministic job list of one run and its results."""
+
+    def __init__(self, opts: PfMethphaseOpts, handle=None):
+        L = _bind()
+        self.opts = opts
+        if handle is None:
+            h = C.c_void_p()
+            _check(L.pf_mp_plan(C.byref(opts), C.byref(h)), "pf_mp_plan")
+            handle = h
+        self.h = handle
+
+    def n_jobs(self, kind: int = JOB_WINDOWS) -> int:
+        return int(lib().pf_mp_n_jobs(self.h, kind))
+
+    def job_info(self, kind: int, j: int) -> dict:
+        i = PfMpJobInfo()
+        _check(lib().pf_mp_job_info(self.h, kind, j, C.byref(i)), "pf_mp_job_info")
+        c = i.cfg
+        return dict(contig=int(i.contig), contig_name=i.contig_name.decode(), w0=int(i.w0), w1=int(i.w1),
+                    rank=int(i.rank), lpt_pos=int(i.lpt_pos), cost=float(i.cost), done=bool(i.done),
+                    cfg=Config(k=c.k, k_span=c.k_span, cov_for_selection=c.cov_for_selection,
+                               cov_for_runtime=c.cov_for_runtime, n_cand=c.n_cand))
+
+    def windows(self):
+        ws, we, co, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_uint32()
+        _check(lib().pf_mp_windows(self.h, C.byref(ws), C.byref(we), C.byref(co), C.byref(n)), "pf_mp_windows")
+        nc = int(lib().pf_mp_gaps(self.h).contents.n_contigs)
+        return _arr(ws, n.value, np.uint32), _arr(we, n.value, np.uint32), _arr(co, nc + 1, np.uint64)
+
+    def run_mine(self, kind: int, n_devices: int = 0, ctxs=None):
+        o = make_opts("", "", None, None, threads=self.opts.threads, n_devices=n_devices, ctxs=ctxs,
+                      rank=self.opts.rank, world=self.opts.world)
+        _check(lib().pf_mp_run_mine(self.h, C.byref(o), kind), "pf_mp_run_mine")
+
+    def merge_raw(self):
+        _check(lib().pf_mp_merge_raw(self.h), "pf_mp_merge_raw")
+
+    def get_result(self, kind: int, j: int) -> dict:
+        r = PfMpJobResult()
+        _check(lib().pf_mp_get_job_result(self.h, kind, j, C.byref(r)), "pf_mp_get_job_result")
+        n, t = int(r.n_windows), r.tags
+        off = _arr(t.off, t.n + 1, np.uint64)
+        return dict(decision=_arr(r.decision, n, np.int8), tag_off=_arr(r.tag_off, n + 1, np.uint64),
+                    off=off, names=_arr(t.names, off[-1] if t.n else 0, np.uint8), hp=_arr(t.hp, t.n, np.uint8),
+                    n_limit=int(r.n_limit))
+
+    def set_result(self, kind: int, j: int, res: dict):
+        dec = np.ascontiguousarray(res["decision"], np.int8)
+        n = dec.shape[0]
+        to = np.ascontiguousarray(res.get("tag_off", np.zeros(n + 1, np.uint64)), np.uint64)
+        off = np.ascontiguousarray(res["off"], np.uint64)
+        names = np.ascontiguousarray(res["names"] if len(res["names"]) else np.zeros(1, np.uint8), np.uint8)
+        hp = np.ascontiguousarray(res["hp"] if len(res["hp"]) else np.zeros(1, np.uint8), np.uint8)
+        decp = np.ascontiguousarray(dec if n else np.zeros(1, np.int8))
+        r = PfMpJobResult(n, decp.ctypes.data, to.ctypes.data,
+                          PfQnameTagsC(len(off) - 1, off.ctypes.data, names.ctypes.data, hp.ctypes.data),
+                          int(res.get("n_limit", 0)))
+        _check(lib().pf_mp_set_job_result(self.h, kind, j, C.byref(r)), "pf_mp_set_job_result")
+
+    def finish(self):
+        _check(lib().pf_mp_finish(self.h), "pf_mp_finish")
+
+    def decisions(self) -> np.ndarray:
+        d, n, nl = C.c_void_p(), C.c_uint32(), C.c_uint32()
+        _check(lib().pf_mp_decisions(self.h, C.byref(d), C.byref(n), C.byref(nl)), "pf_mp_decisions")
+        self.n_limit = int(nl.value)
+        return _arr(d, n.value, np.int8)
+
+    def qname_hp(self) -> Dict[str, int]:
+        return tags_dict(lib().pf_mp_qname_hp(self.h))
+
+    def raw_hp(self) -> Dict[str, int]:
+        return tags_dict(lib().pf_mp_raw_hp(self.h))
+
+    def contigs(self):
+        return _blocks_contigs(lib().pf_mp_blocks(self.h))
+
+    def gaps(self):
+        return _gaps_contigs(lib().pf_mp_gaps(self.h))
+
+    def report_counts(self):
+        c = (C.c_double * 3)()
+        _check(lib().pf_mp_report_counts(self.h, c), "pf_mp_report_counts")
+        return dict(correct=int(c[0]), switch=int(c[1]), fail=int(c[2]))
+
+    def close(self):
+        if self.h:
+            lib().pf_mp_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _result(plan: Plan, mode: int) -> Dict:
+    dec = plan.decisions()
+    if mode == MODE_REPORT:
+        return dict(decision=dec, counts=plan.report_counts(), n_limit=plan.n_limit)
+    return dict(decision=dec, contigs=plan.contigs(), qname_hp=plan.qname_hp(), raw_hp=plan.raw_hp(),
+                n_limit=plan.n_limit)
 
 
 def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],
-                    lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8,
-                    ctx: Optional[Context] = None, untagged: bool = False, tsv: bool = False) -> Dict:
-    """Run methphase over every gap of vcf_path with the reads of bam_path.
-    Writes out_prefix + .mp.gtf / .mp.vcf (and .mp.tsv with tsv=True, the
-    reference's --tsv) unless out_prefix is None.
-    cfg None: no -c, the per-contig parameters come from the BAM's coverage
-    estimate (estimate_read_coverage_dirtyfast + 4358-4390).
-    Returns dict(decision=int8[n_gaps], contigs=[...], qname_hp={qname: hp})."""
-    lcfg = lcfg or LoadConfig()
-    gaps = Gaps(vcf_path, READBACK)
-    own = ctx is None
-    ctx = ctx or Context(device)
-    decision = []
-    qname_hp: Dict[str, int] = {}
-    raw_hp: Dict[str, int] = {}
-    contigs = gaps.contigs()
+                    lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8, ctx=None,
+                    untagged: bool = False, tsv: bool = False, n_devices: int = 1, job_windows: int = 0) -> Dict:
+    """`pomfret methphase` over every gap of vcf_path with the reads of
+    bam_path, in this process (pf_methphase_main).  Writes out_prefix +
+    .mp.gtf / .mp.vcf (and .mp.tsv with tsv=True, the reference's
+    --output-tsv) unless out_prefix is None.  cfg None: no -c, per-contig
+    parameters from the coverage estimate (4358-4390).  ctx: drive that
+    context; else n_devices GPUs from `device` on (0: all visible).
+    Returns dict(decision=int8[n_gaps], contigs=[...], qname_hp={qname: hp},
+    raw_hp={qname: hp} (the -u table), n_limit)."""
+    L = _bind()
+    devs = None
+    if ctx is None and device and n_devices >= 1:
+        devs = (C.c_int32 * n_devices)(*range(device, device + n_devices))
+    o = make_opts(bam_path, vcf_path, out_prefix, cfg, lcfg, untagged=untagged, tsv=tsv, threads=threads,
+                  n_devices=0 if ctx is not None else n_devices, ctxs=[ctx] if ctx is not None else None,
+                  job_windows=job_windows)
+    if devs is not None:
+        o.devices = C.cast(devs, C.c_void_p)
+    h = C.c_void_p()
+    _check(L.pf_methphase_main(C.byref(o), C.byref(h)), "pf_methphase_main")
+    plan = Plan(o, handle=h)
     try:
-        with BamFile(bam_path) as bam:
-            est = bam.estimate_coverage() if cfg is None else None
-            if untagged:                         # the pre-pass tags every contig first (2069-2080)
-                for c in contigs:
-                    if bam.tid(c["name"]) >= 0:
-                        for q, h in _pre_haplotag(ctx, bam, vcf_path, c["name"]).items():
-                            raw_hp.setdefault(q, h)
-            for c in contigs:
-                g = c["gaps"]
-                if not g:
-                    continue
-                if bam.tid(c["name"]) < 0:
-                    decision.extend([-1] * len(g))
-                    continue
-                ws = np.array([a for a, _ in g], np.uint32)
-                we = np.array([b for _, b in g], np.uint32)
-                aln, qn, _ = bam.fetch_windows(c["name"], ws, we, readback=READBACK, threads=threads)
-                if untagged:
-                    aln.hp = np.array([raw_hp.get(q, 254) for q in qn], np.uint8)
-                ccfg = cfg if cfg is not None else Config.from_coverage(est[bam.tid(c["name"])], given=False)
-                db = ctx.upload_aln(ccfg, aln, lcfg)
-                try:
-                    out = db.run()
-                    rec_of_read = db.read_recs()
-                finally:
-                    db.free()
-                dec = np.asarray(out.decision, np.int8)
-                decision.extend(dec.tolist())
-                # reads -> windows: reads are the kept records in record order
-                wro = np.searchsorted(rec_of_read, aln.win_rec_off.astype(np.int64))
-                for w in range(len(g)):
-                    if dec[w] < 0:
-                        continue
-                    for i in range(wro[w], wro[w + 1]):
-                        q = qn[int(rec_of_read[i])]
-                        if q not in qname_hp:               # first wins (4414-4421)
-                            qname_hp[q] = int(out.read_hp[i])
-        blocks = Blocks(gaps, np.asarray(decision, np.int8))
-        if out_prefix is not None:
-            blocks.write_gtf(out_prefix + ".mp.gtf")
-            if tsv:
-                blocks.write_tsv(out_prefix + ".mp.tsv")
-            rescue = []
-            with BamFile(bam_path) as bam:
-                for c in contigs:
-                    if not c["dropped"] or bam.tid(c["name"]) < 0:
-                        rescue.append({})
-                        continue
-                    rescue.append(rescue_dropped(bam, c["name"], c["dropped"], vcf_known_vars(vcf_path, c["name"]),
-                                                 qname_hp, raw_hp if untagged else None))
-            blocks.write_vcf(vcf_path, out_prefix + ".mp.vcf", rescue=rescue)
-        res = dict(decision=np.asarray(decision, np.int8), contigs=blocks.contigs(), qname_hp=qname_hp)
-        blocks.close()
-        return res
+        return _result(plan, MODE_METHPHASE)
     finally:
-        gaps.close()
-        if own:
-            ctx.close()
+        plan.close()
 
 
-def _pre_haplotag(ctx: Context, bam: BamFile, vcf_path: str, contig: str) -> Dict[str, int]:
-    """pre_haplotagging_read_in_one_ref (1841-1898) on the GPU: qname -> hp,
-    first wins."""
-    known = vcf_known_vars(vcf_path, contig)
-    table: Dict[str, int] = {}
-    if len(known.pos) == 0:
-        return table
-    reads, qn, _ = bam.fetch_contig_reads(contig)
-    if len(qn) == 0:
-        return table
-    hp = ctx.haptag_reads(known, reads)
-    for q, h in zip(qn, hp.tolist()):
-        if q not in table:
-            table[q] = int(h)
-    return table
+def report_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cov: int = 0,
+                 chunk_size: int = 50_000, chunk_stride: int = 1_000_000, lcfg: Optional[LoadConfig] = None,
+                 untagged: bool = False, threads: int = 8, ctx=None, n_devices: int = 1, k: int = 3,
+                 k_span: int = 5000) -> Dict:
+    """`pomfret report` (main_methreport, 4901-5089): chunk windows inside the
+    phased blocks, one methphase decision each; writes
+    {out_prefix}.report.tsv and the running totals to stdout.  cov: -c
+    (0: the per-contig estimate).  Returns dict(decision, counts)."""
+    L = _bind()
+    o = make_opts(bam_path, vcf_path, out_prefix, Config(k=k, k_span=k_span), lcfg, mode=MODE_REPORT,
+                  untagged=untagged, threads=threads, n_devices=0 if ctx is not None else n_devices,
+                  ctxs=[ctx] if ctx is not None else None, cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride)
+    h = C.c_void_p()
+    _check(L.pf_methphase_main(C.byref(o), C.byref(h)), "pf_methphase_main")
+    plan = Plan(o, handle=h)
+    try:
+        return _result(plan, MODE_REPORT)
+    finally:
+        plan.close()
+
+
+def methphase_files_dist(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],
+                         lcfg: Optional[LoadConfig] = None, untagged: bool = False, tsv: bool = False,
+                         threads: int = 8, ctx=None, group=None, job_windows: int = 0, mode: int = MODE_METHPHASE,
+                         cov: int = 0, chunk_size: int = 50_000, chunk_stride: int = 1_000_000,
+                         runner: Optional[Callable] = None, writer: int = 0) -> Dict:
+    """One process per GPU (torch.distributed initialised; RCCL on GPUs,
+    gloo on CPU).  Every rank plans the same jobs and runs the ones its
+    static LPT shard owns on `ctx` (or its LOCAL_RANK device); -u tables are
+    all-gathered so every rank loads with the merged table; window-job
+    results are gathered to `writer`, which merges them in (contig, window)
+    order, writes the outputs and broadcasts the decisions.
+    `runner(plan, kind, j) -> result dict` replaces the device for a job
+    (the CPU tests plug the oracle in here)."""
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    o = make_opts(bam_path, vcf_path, out_prefix if rank == writer else None, cfg, lcfg, mode=mode,
+                  untagged=untagged, tsv=tsv, threads=threads, rank=rank, world=world, job_windows=job_windows,
+                  cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride)
+    plan = Plan(o)
+    try:
+        def run(kind):
+            mine = [j for j in range(plan.n_jobs(kind)) if plan.job_info(kind, j)["rank"] == rank]
+            if runner is not None:
+                for j in mine:
+                    plan.set_result(kind, j, runner(plan, kind, j))
+            elif mine:
+                if ctx is None:
+                    import os
+                    from ._lib import Context
+                    run.ctx = getattr(run, "ctx", None) or Context(int(os.environ.get("LOCAL_RANK", "0")))
+                    plan.run_mine(kind, ctxs=[run.ctx])
+                else:
+                    plan.run_mine(kind, ctxs=[ctx])
+            return {j: plan.get_result(kind, j) for j in mine}
+
+        if untagged:
+            got = [None] * world
+            dist.all_gather_object(got, run(JOB_HAPTAG), group=group)
+            for r, part in enumerate(got):
+                if r != rank:
+                    for j, res in part.items():
+                        plan.set_result(JOB_HAPTAG, j, res)
+            plan.merge_raw()
+        mine = run(JOB_WINDOWS)
+        got = [None] * world if rank == writer else None
+        dist.gather_object(mine, got, dst=writer, group=group)
+        out = [None]
+        if rank == writer:
+            for r, part in enumerate(got):
+                if r != rank:
+                    for j, res in part.items():
+                        plan.set_result(JOB_WINDOWS, j, res)
+            plan.finish()
+            out = [_result(plan, mode)]
+        dist.broadcast_object_list(out, src=writer, group=group)
+        return out[0]
+    finally:
+        if getattr(run, "ctx", None) is not None:
+            run.ctx.close()
+        plan.close()

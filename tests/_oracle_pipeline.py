@@ -87,3 +87,95 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
     vcf, counts = ep.vcf_bytes(vcf_path, contigs, blocks, rescue)
     return dict(decision=np.asarray(decision, np.int8), qname_hp=qname_hp, raw_hp=raw_hp,
                 gtf=ep.gtf_text(contigs, blocks), tsv=ep.tsv_text(contigs, blocks), vcf=vcf, counts=counts)
+
+
+def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4):
+    """runner(plan, kind, j) for pomfret_amd.pipeline.methphase_files_dist /
+    the Plan steps: a job's result computed by the oracle instead of the
+    device (CPU tests of the product's plan / shard / merge / write)."""
+    import oracle
+    from pomfret_amd import LoadConfig
+    from pomfret_amd.bam import BamFile, vcf_known_vars
+    from pomfret_amd.pipeline import JOB_HAPTAG
+
+    lcfg = lcfg or LoadConfig()
+
+    def pack(names):
+        enc = [q.encode() for q in names]
+        off = np.zeros(len(enc) + 1, np.uint64)
+        if enc:
+            off[1:] = np.cumsum([len(q) for q in enc])
+        return off, np.frombuffer(b"".join(enc), np.uint8).copy()
+
+    def run(plan, kind, j):
+        info = plan.job_info(kind, j)
+        with BamFile(bam_path) as bam:
+            if kind == JOB_HAPTAG:
+                kv = vcf_known_vars(vcf_path, info["contig_name"])
+                tab = {}
+                if len(kv.pos):
+                    reads, qn, _ = bam.fetch_contig_reads(info["contig_name"])
+                    if qn:
+                        for q, h in zip(qn, oracle.haptag_reads(kv, reads).tolist()):
+                            tab.setdefault(q, int(h))
+                off, names = pack(list(tab))
+                return dict(decision=np.zeros(0, np.int8), tag_off=np.zeros(1, np.uint64), off=off, names=names,
+                            hp=np.array(list(tab.values()), np.uint8))
+            ws, we, _ = plan.windows()
+            w0, w1 = info["w0"], info["w1"]
+            n = w1 - w0
+            if bam.tid(info["contig_name"]) < 0:
+                return dict(decision=np.full(n, -1, np.int8), tag_off=np.zeros(n + 1, np.uint64),
+                            off=np.zeros(1, np.uint64), names=np.zeros(0, np.uint8), hp=np.zeros(0, np.uint8))
+            aln, qn, _ = bam.fetch_windows(info["contig_name"], ws[w0:w1], we[w0:w1])
+        if plan.opts.untagged:
+            raw = plan.raw_hp()
+            aln.hp = np.array([raw.get(q, 254) for q in qn], np.uint8)
+        wb, rec_read = oracle.load_reads(lcfg, aln)
+        res = oracle.methphase(info["cfg"], wb, n_threads=n_threads)
+        recs = np.flatnonzero(rec_read != 0xFFFFFFFF)
+        ro = wb.win_read_off.astype(np.int64)
+        names, hp, cnt = [], [], []
+        for w in range(n):
+            k = 0
+            if res.decision[w] >= 0:
+                for i in range(ro[w], ro[w + 1]):
+                    names.append(qn[int(recs[i])])
+                    hp.append(int(res.read_hp[i]))
+                    k += 1
+            cnt.append(k)
+        off, nb = pack(names)
+        return dict(decision=res.decision.astype(np.int8), tag_off=np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64),
+                    off=off, names=nb, hp=np.array(hp, np.uint8))
+    return run
+
+
+def report_oracle(bam_path, vcf_path, cov, chunk_size, chunk_stride, lcfg=None, k=3, k_span=5000):
+    """main_methreport (blockjoin.c:4901-5089) on the oracle: chunk windows
+    of the raw gaps (restated loop, tests/test_windows.py), the per-contig
+    parameters cov/10+1, 2x, cov/4+1, one decision per window -> the
+    report.tsv text."""
+    import oracle
+    from pomfret_amd import Config, LoadConfig
+    from pomfret_amd.bam import BamFile
+    from test_windows import _report_windows_ref
+    lcfg = lcfg or LoadConfig()
+    rows = []
+    with BamFile(bam_path) as bam:
+        covs = bam.estimate_coverage() if cov <= 0 else None
+        for ci, c in enumerate(oracle.vcf_gaps(vcf_path)):
+            wins = _report_windows_ref(c["abs_start"], c["raw"], chunk_size, chunk_stride)
+            if not wins:
+                continue
+            cv = cov if cov > 0 else (covs[ci] if ci < len(covs) else 0)
+            sel = cv // 10 + 1
+            cfg = Config(k=k, k_span=k_span, cov_for_selection=sel, cov_for_runtime=2 * sel, n_cand=cv // 4 + 1)
+            if bam.tid(c["name"]) < 0:
+                dec = [-1] * len(wins)
+            else:
+                aln, _, _ = bam.fetch_windows(c["name"], [a for a, _ in wins], [b for _, b in wins])
+                wb, _ = oracle.load_reads(lcfg, aln)
+                dec = oracle.methphase(cfg, wb, n_threads=4).decision.tolist()
+            for (a, b), d in zip(wins, dec):
+                rows.append(f"{c['name']}\t{a}\t{b}\t" + ("correct" if d == 0 else "switch" if d == 1 else "fail") + "\n")
+    return "".join(rows)

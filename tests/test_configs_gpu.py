@@ -17,16 +17,19 @@ large or hand-made windows (VERDICT r01 "next round" 1 and 10):
     UINT32_MAX) on hand-worked windows.
 """
 import os
+import subprocess
 
 import numpy as np
 import pytest
 
-from tests._bamio import records_from_aln, write_bam, write_phased_vcf, write_u_vcf
-from tests._oracle_pipeline import methphase_files_oracle
+from tests import _fixtures as fx
+from tests._bamio import records_from_aln
+from tests._oracle_pipeline import methphase_files_oracle, report_oracle
 
 pytestmark = pytest.mark.gpu
 
-GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "example")
+GOLD = fx.GOLD
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _tile_aln(a, k):
@@ -97,23 +100,17 @@ def test_untagged_60x_end_to_end(oracle_lib, gpu_ctx, tmp_path):
     """configs[3] (`methphase -u` at 60x): het SNVs every ~1 kb outside the
     gaps with consistent CIGAR/MD/SEQ; the BAM carries no HP tags.  The K4
     pre-pass tags reads from the VCF, K0..K3 phase the gaps with those tags
-    (blockjoin.c:1114-1122), and every output equals the oracle pipeline."""
+    (blockjoin.c:1114-1122), and every output equals the oracle pipeline.
+    One window per job: the next job's fetch overlaps the current kernels."""
     from pomfret_amd import Config
     from pomfret_amd.pipeline import methphase_files
-    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
-    aln = make_aln_batch(AlnSpec(n_windows=3, coverage=60, seed=71, het_snv_rate=0.001, untag_frac=0.0),
-                         workers=3)
-    aln.hp[:] = 254                                   # untagged BAM
-    recs = records_from_aln(aln)
-    bam = str(tmp_path / "u.bam")
-    write_bam(bam, [("chrS", 400_000_000)], recs)
-    vcf = str(tmp_path / "u.vcf")
-    write_u_vcf(vcf, "chrS", aln)
+    aln, recs, bam, vcf = fx.untagged(tmp_path)
     cfg = Config.from_coverage(60, given=True)
     out = str(tmp_path / "out")
-    res = methphase_files(bam, vcf, out, cfg, ctx=gpu_ctx, untagged=True, tsv=True)
+    res = methphase_files(bam, vcf, out, cfg, ctx=gpu_ctx, untagged=True, tsv=True, job_windows=1)
     ref = methphase_files_oracle(bam, vcf, cfg, untagged=True, recs_by_contig={"chrS": recs})
     _compare_pipeline(res, ref, out)
+    assert res["raw_hp"] == ref["raw_hp"]
     assert (ref["decision"] >= 0).sum() >= 2
     joined = ref["decision"] >= 0
     assert np.array_equal(ref["decision"][joined], aln.meta["orient"][joined])
@@ -125,13 +122,7 @@ def test_tagged_pipeline_bytes(oracle_lib, gpu_ctx, tmp_path):
     bytes equal the oracle pipeline."""
     from pomfret_amd import Config
     from pomfret_amd.pipeline import methphase_files
-    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
-    aln = make_aln_batch(AlnSpec(n_windows=4, coverage=30, seed=22, len_scale=0.5), workers=4)
-    recs = records_from_aln(aln, hp_zero_every=11, de_absent_every=13)
-    bam = str(tmp_path / "t.bam")
-    write_bam(bam, [("chrS", 200_000_000)], recs)
-    vcf = str(tmp_path / "t.vcf")
-    write_phased_vcf(vcf, "chrS", list(zip(aln.win_start.tolist(), aln.win_end.tolist())))
+    aln, recs, bam, vcf = fx.tagged(tmp_path)
     cfg = Config.from_coverage(30, given=False)
     out = str(tmp_path / "out")
     res = methphase_files(bam, vcf, out, cfg, ctx=gpu_ctx, tsv=True)
@@ -148,21 +139,17 @@ def test_example_plumbing_c60(oracle_lib, gpu_ctx, tmp_path):
     .mp.gtf up to the two documented differences of the older build."""
     from pomfret_amd import Config
     from pomfret_amd.pipeline import methphase_files
-    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
-    vcf = os.path.join(GOLD, "variants.vcf.gz")
-    gaps = oracle_lib.vcf_gaps(vcf)
-    (s, e), = gaps[0]["gaps"]
-    aln = make_aln_batch(AlnSpec(n_windows=1, coverage=60, seed=6, windows_at=((s, e),), orient_at=(1,)),
-                         workers=1)
-    recs = records_from_aln(aln)
-    bam = str(tmp_path / "phased.bam")
-    write_bam(bam, [("chr6", 170_805_979)], recs)
+    aln, recs, bam, vcf, gaps = fx.example(tmp_path)
     cfg = Config.from_coverage(60, given=True)
     out = str(tmp_path / "out")
     res = methphase_files(bam, vcf, out, cfg, ctx=gpu_ctx, tsv=True)
     ref = methphase_files_oracle(bam, vcf, cfg, recs_by_contig={"chr6": recs})
     _compare_pipeline(res, ref, out)
     assert res["decision"].tolist() == [1]
+    _golden_check(out, gaps)
+
+
+def _golden_check(out, gaps):
     got = open(out + ".mp.vcf", "rb").read().split(b"\n")
     gold = open(os.path.join(GOLD, "output.mp.vcf"), "rb").read().split(b"\n")
     assert len(got) == len(gold)
@@ -170,6 +157,86 @@ def test_example_plumbing_c60(oracle_lib, gpu_ctx, tmp_path):
     assert len(diff) == 1 and int(got[diff[0]].split(b"\t")[1]) == gaps[0]["abs_end"]
     gtf = open(out + ".mp.gtf").read()
     assert gtf.replace("\t.\t+", ".\t+", 1) == open(os.path.join(GOLD, "output.mp.gtf")).read()
+
+
+def _cli(*args, timeout=300):
+    exe = os.path.join(ROOT, "pomfret_amd", "pomfret-amd")
+    return subprocess.run([exe, *args], capture_output=True, text=True, timeout=timeout)
+
+
+def test_cli_methphase_example(oracle_lib, tmp_path):
+    """The command-line drop-in: `pomfret-amd methphase -o out -c 60 --vcf
+    example/variants.vcf.gz phased.bam` (configs[0]) writes the oracle
+    pipeline's bytes."""
+    from pomfret_amd import Config
+    aln, recs, bam, vcf, gaps = fx.example(tmp_path)
+    out = str(tmp_path / "cli")
+    r = _cli("methphase", "-o", out, "-c", "60", "--vcf", vcf, "--output-tsv", "-t", "4", bam)
+    assert r.returncode == 0, r.stderr
+    ref = methphase_files_oracle(bam, vcf, Config.from_coverage(60, given=True), recs_by_contig={"chr6": recs})
+    assert open(out + ".mp.gtf").read() == ref["gtf"]
+    assert open(out + ".mp.tsv").read() == ref["tsv"]
+    assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+    _golden_check(out, gaps)
+
+
+def test_cli_untagged_no_c(oracle_lib, tmp_path):
+    """`pomfret-amd methphase -u` without -c: the K4 pre-pass, then the
+    per-contig parameters from the coverage estimate (4357-4374)."""
+    from pomfret_amd import Config
+    from pomfret_amd.bam import BamFile
+    aln, recs, bam, vcf = fx.untagged(tmp_path, n_windows=2, coverage=40)
+    out = str(tmp_path / "cli")
+    r = _cli("methphase", "-u", "-o", out, "--vcf", vcf, "--job-windows", "1", bam)
+    assert r.returncode == 0, r.stderr
+    with BamFile(bam) as b:
+        cfg = Config.from_coverage(b.estimate_coverage()[0], given=False)
+    ref = methphase_files_oracle(bam, vcf, cfg, untagged=True, recs_by_contig={"chrS": recs})
+    assert open(out + ".mp.gtf").read() == ref["gtf"]
+    assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+
+
+def test_report_gpu_matches_oracle(oracle_lib, gpu_ctx, tmp_path):
+    """`pomfret report` (a14, main_methreport 4901-5089) on the device:
+    chunk windows inside the phased blocks, report.tsv rows and totals equal
+    the oracle's; the CLI writes the same file."""
+    from pomfret_amd.pipeline import report_files
+    aln, recs, bam, vcf = fx.tagged(tmp_path, n_windows=3)
+    out = str(tmp_path / "rep")
+    res = report_files(bam, vcf, out, cov=30, chunk_size=10_000, chunk_stride=50_000, ctx=gpu_ctx)
+    text = open(out + ".report.tsv").read()
+    assert text == report_oracle(bam, vcf, 30, 10_000, 50_000)
+    assert sum(res["counts"].values()) == text.count("\n") > 0
+    r = _cli("report", "-o", str(tmp_path / "rep2"), "-c", "30", "--chunk-size", "10000", "--chunk-stride", "50000",
+             "--vcf", vcf, bam)
+    assert r.returncode == 0, r.stderr
+    assert open(str(tmp_path / "rep2") + ".report.tsv").read() == text
+    assert f"Total N={text.count(chr(10))} regions" in r.stdout
+
+
+def test_oversized_window_left_undecided(oracle_lib, gpu_ctx, tmp_path):
+    """A window with more records than the device's per-window limit (65,535)
+    is left undecided with a warning; the other windows of the run are
+    unaffected."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import methphase_files
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    from tests._bamio import Rec, write_bam, write_phased_vcf
+    aln = make_aln_batch(AlnSpec(n_windows=2, coverage=30, seed=22, len_scale=0.5), workers=2)
+    recs = records_from_aln(aln)
+    s1 = int(aln.win_start[1])
+    junk = [Rec(0, s1 + 1000 + (i % 20000), f"j{i}", cigar=[(20 << 4) | 0], seq=bytes([0x12] * 10), l_seq=20)
+            for i in range(66_000)]
+    allr = sorted(recs + junk, key=lambda r: r.pos)
+    bam = str(tmp_path / "big.bam")
+    write_bam(bam, [("chrS", 200_000_000)], allr)
+    vcf = str(tmp_path / "big.vcf")
+    write_phased_vcf(vcf, "chrS", list(zip(aln.win_start.tolist(), aln.win_end.tolist())))
+    cfg = Config.from_coverage(30, given=False)
+    res = methphase_files(bam, vcf, str(tmp_path / "o"), cfg, ctx=gpu_ctx)
+    ref = methphase_files_oracle(bam, vcf, cfg, recs_by_contig={"chrS": allr})
+    assert res["n_limit"] == 1 and res["decision"][1] == -1
+    assert res["decision"][0] == ref["decision"][0]
 
 
 def test_t8_counter_wrap_gpu(oracle_lib, gpu_ctx):

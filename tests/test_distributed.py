@@ -104,3 +104,60 @@ def test_two_rank_record_level_shards(tmp_path, oracle_lib):
     assert bytes(sub.mm[sub.mm_off[0]:sub.mm_off[1]]) == bytes(aln.mm[aln.mm_off[r0]:aln.mm_off[r0 + 1]])
     lq = int(aln.l_qseq[r0])
     assert bytes(sub.seq[:(lq + 1) // 2]) == bytes(aln.seq[aln.seq_off[r0]:aln.seq_off[r0] + (lq + 1) // 2])
+
+
+def _files_worker(rank, world, port, tmp, untagged):
+    """One rank of methphase_files_dist on gloo; the oracle computes this
+    rank's jobs (tests/_oracle_pipeline.oracle_job_runner)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import json
+        from pomfret_amd import Config
+        from pomfret_amd.pipeline import methphase_files_dist
+        from tests._oracle_pipeline import oracle_job_runner
+        bam, vcf = os.path.join(tmp, "in.bam"), os.path.join(tmp, "in.vcf")
+        cfg = Config.from_coverage(30, given=True)
+        res = methphase_files_dist(bam, vcf, os.path.join(tmp, "dist"), cfg, untagged=untagged, tsv=True,
+                                   job_windows=1, runner=oracle_job_runner(bam, vcf, n_threads=2))
+        with open(os.path.join(tmp, f"res{rank}.json"), "w") as f:
+            json.dump(dict(decision=res["decision"].tolist(), qname_hp=res["qname_hp"], raw_hp=res["raw_hp"]), f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("untagged", [False, True])
+def test_two_rank_pipeline_merges_like_one_process(tmp_path, oracle_lib, untagged):
+    """methphase_files_dist over 2 gloo ranks: each rank runs its LPT share
+    of the jobs (the -u tables all-gathered first), the writer merges the
+    joined windows' tags in (contig, window) order.  Decisions, the qname
+    table and the GTF/TSV/VCF bytes equal the single-process oracle pipeline
+    (blockjoin.c:4408-4423, 4579-4595)."""
+    import json
+    import shutil
+    from pomfret_amd import Config
+    from tests import _fixtures as fx
+    from tests._oracle_pipeline import methphase_files_oracle
+    if untagged:
+        aln, recs, bam, vcf = fx.untagged(tmp_path, n_windows=3, coverage=30, len_scale=0.5)
+    else:
+        aln, recs, bam, vcf = fx.tagged(tmp_path, n_windows=5, len_scale=0.4)
+    shutil.move(bam, tmp_path / "in.bam")
+    shutil.move(bam + ".bai", tmp_path / "in.bam.bai")
+    shutil.move(vcf, tmp_path / "in.vcf")
+    bam, vcf = str(tmp_path / "in.bam"), str(tmp_path / "in.vcf")
+    mp.spawn(_files_worker, args=(2, _free_port(), str(tmp_path), untagged), nprocs=2, join=True)
+    ref = methphase_files_oracle(bam, vcf, Config.from_coverage(30, given=True), untagged=untagged,
+                                 recs_by_contig={"chrS": recs})
+    for r in range(2):
+        got = json.load(open(tmp_path / f"res{r}.json"))
+        assert got["decision"] == ref["decision"].tolist()
+        assert got["qname_hp"] == ref["qname_hp"]
+        if untagged:
+            assert got["raw_hp"] == ref["raw_hp"]
+    out = str(tmp_path / "dist")
+    assert open(out + ".mp.gtf").read() == ref["gtf"]
+    assert open(out + ".mp.tsv").read() == ref["tsv"]
+    assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+    assert (ref["decision"] >= 0).any()
