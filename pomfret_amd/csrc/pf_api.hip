@@ -24,6 +24,7 @@
 __global__ void pf_k12_sites_methmers(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
+__global__ void pf_k3_wave(pf_dev_batch d);
 __global__ void pf_k3_fallback(pf_dev_batch d);
 __global__ void pf_k0_load(pf_load_dev d);
 __global__ void pf_k0_scan(pf_load_dev d);
@@ -40,7 +41,7 @@ __global__ void pf_selftest_wave(unsigned long long *bad);
 
 // kernel timing slots: "pf_k0_pack" is the scan + pack pair
 static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k0_pack", "pf_k12_sites_methmers", "pf_k2_methmers",
-                                        "pf_k3_greedy", "pf_k3_fallback"};
+                                        "pf_k3_wave", "pf_k3_fallback"};
 #define PF_GROWABLE (PF_ST_KEYS_OVF | PF_ST_BIG_OVF | PF_ST_SCR_OVF | PF_ST_STAGE_OVF | PF_ST_CALL_OVF | PF_ST_SITES_OVF)
 
 struct pf_ctx {
@@ -49,12 +50,14 @@ struct pf_ctx {
     hipEvent_t ev[PF_NKERN + 1];
     float last_ms[PF_NKERN];
     int have_times;
+    int k3_block;             /* last run's main greedy kernel: 1 the 256-thread build, 0 the one-wave build */
     float haptag_ms;          /* last pf_haptag_reads kernel time */
     int have_haptag;
     void *pin = nullptr;      /* pinned staging for large uploads (grown on demand) */
     size_t pin_cap = 0;
     uint32_t k3_lds_set = 0;  /* dynamic LDS limits set on the greedy kernels of this device */
     uint32_t k3_lds_fb_set = 0;
+    uint32_t k3w_lds_set = 0;
 };
 
 struct pf_dbatch {
@@ -515,7 +518,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     ALLOC(d.scr, d.scr_cap);
     ALLOC(d.stats, 16ull * W);
     ALLOC(d.prof, 80ull * W);
-    // greedy kernels' dynamic LDS.  40 KB (+ ~6 KB static) fits three
+    // greedy kernels' dynamic LDS.  40-48 KB (+ ~6 KB static) fits three
     // workgroups per CU, 72 KB two; a problem the main kernel cannot fit runs
     // in the fallback kernel after it.  Small windows (90 % of the windows
     // with <= 400 reads, ~30x) nearly all fit 40 KB, and the higher occupancy
@@ -528,8 +531,12 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
         std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
         if (rw[(W * 9) / 10] <= 400) lds_auto = 40960u;
+        else if (rw[(W * 9) / 10] <= 800) lds_auto = 49152u;    // 60x: three per CU, none deferred
     }
-    const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB");
+    const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB"), *ldw = getenv("PF_K3W_LDS");
+    // one-wave greedy kernel: ~25 KB leaves six problems per CU (a 60x
+    // window's compact image is ~18-23 KB); larger problems go to the fallback
+    d.lds_w = ldw ? (uint32_t)atoi(ldw) : 25600u;
     d.lds_bytes = lds ? (uint32_t)atoi(lds) : lds_auto;
     d.lds_fb = ldf ? (uint32_t)atoi(ldf) : lds ? d.lds_bytes : 73728u;
     if (d.lds_fb < d.lds_bytes) d.lds_fb = d.lds_bytes;
@@ -804,6 +811,12 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     HIPCHK(hipMemsetAsync(b->io, 0, PF_IO_HDR, st));
     if (b->W == 0) { HIPCHK(hipEventRecord(b->done[slot], st)); return PF_OK; }
     // the greedy kernels' dynamic LDS limits, raised per context when a batch needs more
+    if (d.lds_w > 65536u && d.lds_w > c->k3w_lds_set) {
+        if (hipFuncSetAttribute((const void *)pf_k3_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)d.lds_w) == hipSuccess)
+            c->k3w_lds_set = d.lds_w;
+        (void)hipGetLastError();
+    }
     if (d.lds_bytes > c->k3_lds_set || d.lds_fb > c->k3_lds_fb_set) {
         hipError_t e = hipFuncSetAttribute((const void *)pf_k3_greedy,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes);
@@ -851,7 +864,17 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][4], st));
     if (stages < 3) return PF_OK;
-    hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
+    // main greedy kernel: the 256-thread workgroup build; PF_K3_IMPL=wave runs
+    // the one-wavefront build (measured slower on MI355X at 30x-60x: one wave
+    // per problem leaves the greedy chain's latencies exposed)
+    {
+        const char *impl = getenv("PF_K3_IMPL");
+        c->k3_block = !(impl && strcmp(impl, "wave") == 0);
+    }
+    if (c->k3_block)
+        hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
+    else
+        hipLaunchKernelGGL(pf_k3_wave, dim3(2 * b->W), dim3(64), d.lds_w, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][5], st));
     // deferred problems (usually none): a grid-stride kernel over the main kernel's list
@@ -1110,7 +1133,7 @@ extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms
     int m = *n < tot ? *n : tot;
     for (int i = 0; i < m; i++) {
         if (i < PF_NKERN) {
-            if (names) names[i] = k_names[i];
+            if (names) names[i] = (i == 4 && ctx->k3_block) ? "pf_k3_greedy" : k_names[i];
             if (ms) ms[i] = ctx->have_times ? ctx->last_ms[i] : -1.0f;
         } else {
             if (names) names[i] = "pf_k4_haptag";

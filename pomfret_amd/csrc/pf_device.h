@@ -76,6 +76,7 @@ struct pf_dev_batch {
     unsigned long long *prof;          /* [W*2*8] diagnostic build only */
     uint32_t lds_bytes;                /* dynamic LDS of the main greedy kernel */
     uint32_t lds_fb;                   /* dynamic LDS of the fallback greedy kernel (>= lds_bytes) */
+    uint32_t lds_w;                    /* dynamic LDS of the one-wave greedy kernel */
     uint32_t k12_capw, k12_smax;       /* fused methmer phase limits (test overrides) */
     uint32_t k2_entcap;                /* fallback reads above this bound use HBM scratch */
     uint32_t k3_mode;                  /* test override: 0 exact pick, 1 always fold, 2 chunked record rows */

@@ -1138,13 +1138,14 @@ DEV uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
 // dictionary of methmer keys per site -> dense slot ids (replaces the per-site
 // key lists + linear search of insert_mmrs_to_counts / query_counts_of_mmrs)
+template <int NT = PF_K3_THREADS>
 DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uint32_t dir,
                  uint64_t *masks, uint32_t *base, uint32_t *sh_scan, K3Ctl &ctl) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t MW = (uint32_t)d.mw;
-    for (uint32_t j = tid; j < S * MW; j += PF_K3_THREADS) masks[j] = 0;
+    for (uint32_t j = tid; j < S * MW; j += NT) masks[j] = 0;
     __syncthreads();
-    for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
+    for (uint32_t i = wid; i < R; i += NT / 64) {
         const uint32_t g = 2 * (r0 + i) + dir;
         const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
         const uint32_t *kp = d.keys + d.mmr_off[g];
@@ -1157,13 +1158,13 @@ DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uin
     }
     __syncthreads();
     uint32_t carry = 0;
-    for (uint32_t p0 = 0; p0 < S; p0 += PF_K3_THREADS) {
+    for (uint32_t p0 = 0; p0 < S; p0 += NT) {
         const uint32_t p = p0 + tid;
         uint32_t c = 0;
         if (p < S)
             for (uint32_t m = 0; m < MW; m++) c += (uint32_t)__popcll(masks[(uint64_t)p * MW + m]);
         uint32_t tot;
-        const uint32_t ex = block_excl_scan<PF_K3_THREADS>(c, sh_scan, &tot);
+        const uint32_t ex = block_excl_scan<NT>(c, sh_scan, &tot);
         if (p < S) base[p] = carry + ex;
         carry += tot;
     }
@@ -1173,11 +1174,12 @@ DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uin
 
 // second half: rewrite every key in place into its slot id (destructive: a
 // problem is committed to a kernel before this)
+template <int NT = PF_K3_THREADS>
 DEV void k3_dict_rewrite(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uint32_t dir,
                          const uint64_t *masks, const uint32_t *base) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t MW = (uint32_t)d.mw;
-    for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
+    for (uint32_t i = wid; i < R; i += NT / 64) {
         const uint32_t g = 2 * (r0 + i) + dir;
         const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
         uint32_t *kp = d.keys + d.mmr_off[g];
@@ -2909,6 +2911,882 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_fallback(pf_dev_batch d) 
         k3_run<true>(d, d.k3_fb_list[i], smem, ctl, cd, sh_scan, d.lds_fb);
         __syncthreads();
     }
+}
+
+// ========================================================================
+// K3W: one wavefront per (window, direction) -- the main greedy kernel
+// ========================================================================
+// The greedy loop of haplotag_region1 (:4032-4071) is a serial chain of one
+// tagged read per iteration; its per-iteration work (n_cand candidates x
+// their in-range methmers, ~10^3 lookups at 60x) fits one wavefront.  One
+// wave per problem needs no workgroup barriers, no LDS reductions and no
+// redundant control across waves, and a compact LDS image lets 6-8 problems
+// share a CU, so the whole batch is resident at once.  LDS per problem:
+//   srec  16 B per site: (h0, h1, 1/h0, 1/h1) as floats, exact hap totals
+//         (they replace the u32 sum array: the range update reads h0 + h1)
+//   cnt   per slot, hap0 | hap1 packed: u8 pairs when no site is covered by
+//         more than 255 reads' methmers (no count can exceed that; checked
+//         per problem), else u16 pairs
+//   hp, flg 1 B per read, untag 1 bit per read
+// Slot lists stay in the HBM key arena (rewritten in place into slot ids by
+// the dictionary build); per-read methmer fields and the dir-1 scan order
+// are read from HBM when a read joins the candidate queue.
+#define K3W_NOFF 7
+#define K3W_LSMAX 512u            // longest methmer list the candidate cache holds (8 regs per lane)
+
+template <bool C8>
+DEV uint64_t k3w_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t nc, uint32_t ls, uint64_t off[K3W_NOFF]) {
+    const uint32_t nwords = (R + 63) >> 6;
+    off[0] = 0;                                                   // srec  16*S
+    off[1] = align16(16ull * S);                                  // cnt   ntot * (2 | 4)
+    off[2] = align16(off[1] + (C8 ? 2ull : 4ull) * ntot);         // cache nc * ls u16 slot ids
+    off[3] = align16(off[2] + 2ull * nc * ls);                    // hp    R
+    off[4] = align16(off[3] + R);                                 // flg   R
+    off[5] = align16(off[4] + R);                                 // untag nwords*8
+    off[6] = off[5] + 8ull * nwords;
+    return off[6];
+}
+
+struct K3WMem {
+    float4 *srec;
+    uint8_t *cnt;
+    uint16_t *cc;                // candidate slot-list cache: nc lists of ls u16 slot ids (0xFFFF: none)
+    uint32_t ls;
+    uint8_t *hp, *flg;
+    uint64_t *untag;
+    const uint32_t *kb;          // slot lists (HBM key arena, window base)
+    uint64_t kbase;
+};
+
+DEV uint32_t k3w_slot(const K3WMem &m, uint32_t i) {
+    const uint32_t v = m.cc[i];
+    return v == 0xFFFFu ? PF_NONE : v;
+}
+
+// one read's slot list (n entries at arena offset mo) into cache list cs
+DEV void k3w_cache_load(const K3WMem &m, uint32_t cs, uint32_t mo, uint32_t n, uint32_t lane) {
+    uint16_t *dst = m.cc + cs * m.ls;
+    for (uint32_t t = lane; t < n; t += 64) {
+        const uint32_t v = m.kb[mo + t];
+        dst[t] = v == PF_NONE ? (uint16_t)0xFFFFu : (uint16_t)v;
+    }
+}
+
+// count pair of slot s: (hap0, hap1)
+template <bool C8>
+DEV uint32_t k3w_cnt(const K3WMem &m, uint32_t s) {
+    if (C8) return reinterpret_cast<const uint16_t *>(m.cnt)[s];
+    return reinterpret_cast<const uint32_t *>(m.cnt)[s];
+}
+template <bool C8> DEV uint32_t k3w_c0(uint32_t c) { return C8 ? (c & 0xffu) : (c & 0xffffu); }
+template <bool C8> DEV uint32_t k3w_c1(uint32_t c) { return C8 ? (c >> 8) : (c >> 16); }
+
+// per-read methmer fields of window-local read rd, direction dir, from HBM
+DEV void k3w_read_fields(const pf_dev_batch &d, uint32_t r0, uint32_t rd, uint32_t dir, uint64_t kbase,
+                         uint32_t &n, uint32_t &st, uint32_t &mo) {
+    const uint64_t g = 2ull * (r0 + rd) + dir;
+    n = d.mmr_n[g];
+    st = d.mmr_start[g];
+    mo = (uint32_t)(d.mmr_off[g] - kbase);
+}
+
+// k3_qbuild with the per-read fields from HBM
+DEV uint32_t k3w_qbuild(const pf_dev_batch &d, const K3WMem &m, uint32_t r0, uint32_t nwords, int p, uint32_t dir,
+                        uint32_t lane, uint32_t *qbuf, uint32_t &q_pos, uint32_t &q_rd, uint32_t &q_n,
+                        uint32_t &q_st, uint32_t &q_mo, bool &more, int &cont) {
+    uint64_t bits = 0;
+    int wi, w0;
+    bool more_words;
+    if (dir == 0) {
+        const int q = p + 1;
+        if (q >= (int)(nwords * 64)) { more = false; return 0; }
+        w0 = q >> 6;
+        wi = w0 + (int)lane;
+        if (wi < (int)nwords) {
+            bits = m.untag[wi];
+            if (wi == w0) bits &= ~0ull << (q & 63);
+        }
+        more_words = w0 + 64 < (int)nwords;
+    } else {
+        const int q = p - 1;
+        if (q < 0) { more = false; return 0; }
+        w0 = q >> 6;
+        wi = w0 - (int)lane;
+        if (wi >= 0) {
+            bits = m.untag[wi];
+            if (wi == w0) {
+                const uint32_t b = (uint32_t)q & 63;
+                bits &= b == 63 ? ~0ull : ((1ull << (b + 1)) - 1ull);
+            }
+        }
+        more_words = w0 - 64 >= 0;
+    }
+    const uint32_t pc = (uint32_t)__popcll(bits);
+    const uint32_t incl = wave_incl_scan_dpp(pc);
+    const uint32_t tot = rdl(incl, 63);
+    uint32_t k = incl - pc;
+    while (bits != 0 && k < 64) {
+        const int b = dir == 0 ? __ffsll((unsigned long long)bits) - 1 : 63 - __clzll((long long)bits);
+        qbuf[k++] = (uint32_t)(wi * 64 + b);
+        bits &= ~(1ull << b);
+    }
+    wave_sync();
+    const uint32_t cnt = tot < 64 ? tot : 64;
+    if (lane < cnt) {
+        q_pos = qbuf[lane];
+        q_rd = dir ? d.rev_ord[r0 + q_pos] : q_pos;
+        k3w_read_fields(d, r0, q_rd, dir, m.kbase, q_n, q_st, q_mo);
+    }
+    if (tot > 64) cont = (int)qbuf[63];
+    else cont = dir == 0 ? (w0 + 64) * 64 - 1 : (w0 - 63) * 64;
+    more = tot > 64 || more_words;
+    wave_sync();
+    return cnt;
+}
+
+// update_available_methmer_range (:3669-3691) from the exact float totals
+DEV void k3w_range(const K3WMem &m, uint32_t S, int cov_rt, uint32_t lane, uint32_t &umin, uint32_t &umax) {
+    auto cov_ok = [&](int ii) -> bool {
+        const float4 r = m.srec[ii];
+        return (int)((uint32_t)r.x + (uint32_t)r.y) >= cov_rt;
+    };
+    const int m0 = (int)umin, M0 = (int)umax;
+    const bool left = lane < 32;
+    const int i = left ? m0 - (int)lane : M0 + (int)(lane - 32);
+    bool cvg = false;
+    if (left ? (m0 >= 0 && i >= 0) : (M0 >= 0 && i < (int)S)) cvg = cov_ok(i);
+    const uint64_t b = __ballot(cvg);
+    const uint32_t bl = (uint32_t)b, br = (uint32_t)(b >> 32);
+    int cl = bl == ~0u ? 32 : __ffs(~bl) - 1;
+    int cr = br == ~0u ? 32 : __ffs(~br) - 1;
+    if (cl == 32) {
+        for (;;) {
+            const int ii = m0 - cl - (int)lane;
+            const uint64_t b2 = __ballot(ii >= 0 && cov_ok(ii));
+            if (b2 == ~0ull) { cl += 64; continue; }
+            cl += __ffsll((unsigned long long)~b2) - 1;
+            break;
+        }
+    }
+    if (cr == 32) {
+        for (;;) {
+            const int ii = M0 + cr + (int)lane;
+            const uint64_t b2 = __ballot(ii < (int)S && cov_ok(ii));
+            if (b2 == ~0ull) { cr += 64; continue; }
+            cr += __ffsll((unsigned long long)~b2) - 1;
+            break;
+        }
+    }
+    if (m0 >= 0 && cl > 0) umin = (uint32_t)(m0 - cl + 1);
+    if (M0 >= 0 && cr > 0) umax = (uint32_t)(M0 + cr - 1);
+}
+
+// fp32 partial sums and push/positive counts of the lane's terms t =
+// tstart, tstart + step, ... < tend, eight terms' loads in flight.  Each
+// partial is a sequential fp32 sum of at most L terms (L = the candidate's
+// length), so it lies within gamma_{L-1} of its exact value; the partials
+// meet in fp64 exactly (fp32 values >= 2^-16 are multiples of 2^-39), and
+// k3w_pick_exact widens its intervals by that second gamma.
+template <bool C8>
+DEV uint32_t k3w_fill(const K3WMem &m, uint32_t f_lo, uint32_t f_kofs, uint32_t tstart, uint32_t tend,
+                      uint32_t step, float &e0, float &e1) {
+    uint32_t lcode = 0;
+    for (uint32_t tb = tstart; tb < tend; tb += 8 * step) {
+        uint32_t sl[8], cv[8];
+        float4 sr[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t t = tb + u * step;
+            const bool ok = t < tend;
+            sl[u] = k3w_slot(m, ok ? f_kofs + t : 0u);
+            sr[u] = m.srec[ok ? f_lo + t : 0u];
+            sl[u] = ok ? sl[u] : PF_NONE;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const bool ok = sl[u] != PF_NONE;
+            const uint32_t c = k3w_cnt<C8>(m, ok ? sl[u] : 0u);
+            cv[u] = ok ? c : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t a0 = k3w_c0<C8>(cv[u]), a1 = k3w_c1<C8>(cv[u]);
+            const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
+            const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
+            // pushed: key present (cv != 0) and hap total != 0 (:3505-3509);
+            // positive: cnt > 0 (:3619-3624); branch-free
+            const uint32_t hm = (sr[u].z != 0.f ? 1u : 0u) | (sr[u].w != 0.f ? 0x10000u : 0u);
+            const uint32_t pc = (a0 != 0u ? 1u : 0u) | (a1 != 0u ? 0x10000u : 0u);
+            lcode += pc + (cv[u] != 0u ? hm : 0u);
+            e0 += q0;
+            e1 += q1;
+        }
+    }
+    return lcode;
+}
+
+// the reference's sequential fp32 fold of one candidate (:3619-3636)
+template <bool C8>
+DEV void k3w_fold(const K3WMem &m, uint32_t lo, uint32_t kofs, uint32_t len, float &s0, float &s1) {
+    for (uint32_t t0 = 0; t0 < len; t0 += 8) {
+        uint32_t sl[8];
+        float4 sr[8];
+        float q0[8], q1[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t t = t0 + u;
+            const bool ok = t < len;
+            sl[u] = ok ? k3w_slot(m, kofs + t) : PF_NONE;
+            sr[u] = m.srec[ok ? lo + t : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const bool ok = sl[u] != PF_NONE;
+            const uint32_t c = ok ? k3w_cnt<C8>(m, sl[u]) : 0u;
+            q0[u] = div_u16_y((float)k3w_c0<C8>(c), sr[u].x, sr[u].z);
+            q1[u] = div_u16_y((float)k3w_c1<C8>(c), sr[u].y, sr[u].w);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            K3_FADD(s0, q0[u]);
+            K3_FADD(s1, q1[u]);
+        }
+    }
+}
+
+// insert_mmr_counts of one tagged read into hap tg (its sites are distinct)
+template <bool C8>
+DEV void k3w_insert(const K3WMem &m, uint32_t S, uint32_t n, uint32_t st, uint32_t mo, uint32_t tg, uint32_t lane) {
+    for (uint32_t tb = 0; tb < n; tb += 128) {
+        uint32_t sl[2], cc[2];
+        float4 sr[2];
+        bool ok[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const uint32_t t = tb + u * 64 + lane;
+            ok[u] = t < n && st + t < S;
+            sl[u] = k3w_slot(m, ok[u] ? mo + t : 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            ok[u] = ok[u] && sl[u] != PF_NONE;
+            cc[u] = k3w_cnt<C8>(m, ok[u] ? sl[u] : 0u);
+            sr[u] = m.srec[ok[u] ? st + tb + u * 64 + lane : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            if (ok[u]) {
+                const uint32_t site = st + tb + u * 64 + lane;
+                if (C8) reinterpret_cast<uint16_t *>(m.cnt)[sl[u]] = (uint16_t)(cc[u] + (tg ? 0x100u : 1u));
+                else reinterpret_cast<uint32_t *>(m.cnt)[sl[u]] = cc[u] + (tg ? 0x10000u : 1u);
+                const float h = (tg ? sr[u].y : sr[u].x) + 1.f;
+                float *f = reinterpret_cast<float *>(&m.srec[site]);
+                f[tg] = h;
+                f[2 + tg] = __builtin_amdgcn_rcpf(h);
+            }
+        }
+    }
+    wave_sync();
+}
+
+// per-problem set-up (k3_init for one wave): flags and tags, reference
+// reads seeding the counts (:3776-3810), the initial range, the T5 round
+// trip, the site records and the untagged bitmask
+template <bool C8>
+DEV void k3w_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
+                  uint32_t ntot, const K3WMem &m, uint32_t &umin, uint32_t &umax, K3Stats &stx, uint32_t &summ) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t s = d.win_start[w], e = d.win_end[w];
+    const uint32_t refbit = dir == 0 ? FLG_LEFT : FLG_RIGHT;
+    uint32_t *cw = reinterpret_cast<uint32_t *>(m.cnt);
+    const uint32_t cwords = C8 ? (ntot + 1) / 2 : ntot;
+    for (uint32_t j = lane; j < cwords; j += 64) cw[j] = 0;
+    for (uint32_t j = lane; j < S; j += 64) m.srec[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t sum_mmr = 0;
+    for (uint32_t i = lane; i < R; i += 64) {
+        const uint32_t r = r0 + i;
+        const uint32_t st = d.read_start[r], en = d.read_end[r];
+        uint32_t f = 0;
+        if (st <= s) {                                           // blockjoin.c:1127-1128
+            f |= FLG_LEFT;
+            if (en > s) f |= FLG_LEFT_STRICT;
+        } else if (en >= e) {                                    // blockjoin.c:1134-1135
+            f |= FLG_RIGHT;
+            if (st < e) f |= FLG_RIGHT_STRICT;
+        }
+        m.flg[i] = (uint8_t)f;
+        m.hp[i] = d.read_hp[r];
+        sum_mmr += d.mmr_n[2ull * r + dir];
+    }
+    {
+        const uint32_t *a = d.site_pos + d.win_site_off[w];
+        if (dir == 0) {
+            umin = 0;
+            umax = (uint32_t)ub_u32(a, 0, S, s);                 // #sites <= ref_start (:3994-3998)
+        } else {
+            umax = S - 1;
+            umin = (uint32_t)((int)ub_u32(a, 0, S, e) - 1);      // may wrap to UINT32_MAX (:3999-4003)
+        }
+        umin = uni(umin);
+        umax = uni(umax);
+    }
+    wave_sync();
+    // ---- reference reads seed the counts: eight reads' slot loads in flight
+    uint32_t ref_ins = 0;
+    for (uint32_t i0 = 0; i0 < R; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool isref = i < R && (m.flg[i] & refbit) && m.hp[i] <= 1;
+        uint64_t bal = __ballot(isref);
+        while (bal) {
+            uint32_t rd[8] = {0}, n[8] = {0}, st[8] = {0}, mo[8] = {0}, inc[8] = {0};
+            int k = 0;
+            for (; k < 8 && bal; k++) {
+                const uint32_t b = (uint32_t)__ffsll((unsigned long long)bal) - 1u;
+                bal &= bal - 1;
+                rd[k] = i0 + b;
+                k3w_read_fields(d, r0, rd[k], dir, m.kbase, n[k], st[k], mo[k]);
+                inc[k] = m.hp[rd[k]] ? 1u : 0u;
+                ref_ins += n[k];
+            }
+            uint32_t mx = 0;
+            for (int u = 0; u < k; u++) mx = n[u] > mx ? n[u] : mx;
+            for (uint32_t t0 = 0; t0 < mx; t0 += 64) {
+                uint32_t sl[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint32_t t = t0 + lane;
+                    const bool ok = t < n[u] && st[u] + t < S;
+                    sl[u] = ok ? m.kb[mo[u] + t] : PF_NONE;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    if (sl[u] != PF_NONE) {
+                        const uint32_t site = st[u] + t0 + lane;
+                        if (C8) atomicAdd(&cw[sl[u] >> 1], (inc[u] ? 0x100u : 1u) << ((sl[u] & 1u) * 16u));
+                        else atomicAdd(&cw[sl[u]], inc[u] ? 0x10000u : 1u);
+                        // exact hap totals as floats (ds_add_f32 of 1.0: integers < 2^24)
+                        atomicAdd(reinterpret_cast<float *>(&m.srec[site]) + inc[u], 1.f);
+                    }
+                }
+            }
+        }
+    }
+    wave_sync();
+    // reciprocals of the totals (0 for a zero total: its terms are never pushed)
+    for (uint32_t j = lane; j < S; j += 64) {
+        const float4 r = m.srec[j];
+        m.srec[j] = make_float4(r.x, r.y, r.x != 0.f ? __builtin_amdgcn_rcpf(r.x) : 0.f,
+                                r.y != 0.f ? __builtin_amdgcn_rcpf(r.y) : 0.f);
+    }
+    wave_sync();
+    summ = 0;
+#pragma unroll
+    for (int bb = 0; bb < 32; bb++) summ += (uint32_t)__popcll(__ballot((sum_mmr >> bb) & 1)) << bb;
+    stx.inserts = uni(ref_ins);                      // wave-uniform: the reads came from a ballot
+}
+
+// the T5 round trip and the untagged bitmask (aux: 4 B per read after the
+// layout)
+DEV void k3w_tags(const pf_dev_batch &d, uint32_t dir, uint32_t r0, uint32_t R, const K3WMem &m, uint32_t *aux) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nwords = (R + 63) >> 6;
+    const uint32_t refbit = dir == 0 ? FLG_LEFT : FLG_RIGHT;
+    for (uint32_t i = lane; i < R; i += 64) aux[i] = 0;
+    wave_sync();
+    // step 1.5 (:4010-4025): all reads unphased, ref reads restored through
+    // the (readID<<2)|hp round trip (hp >= 4 lands on readID|(hp>>2)); the
+    // last writer in reference order wins
+    for (uint32_t i = lane; i < R; i += 64)
+        if (m.flg[i] & refbit) {
+            const uint32_t t = i | ((uint32_t)m.hp[i] >> 2);
+            if (t < R) atomicMax(&aux[t], i + 1);
+        }
+    wave_sync();
+    for (uint32_t i = lane; i < R; i += 64) {
+        const uint32_t lw = aux[i];
+        m.hp[i] = lw ? (uint8_t)(d.read_hp[r0 + lw - 1] & 3) : (uint8_t)2;
+    }
+    wave_sync();
+    for (uint32_t j = 0; j < nwords; j++) {
+        const uint32_t p = j * 64 + lane;
+        bool u = false;
+        if (p < R) {
+            const uint32_t rd = dir ? d.rev_ord[r0 + p] : p;
+            const uint32_t h = m.hp[rd];
+            u = h != 0 && h != 1;
+        }
+        const uint64_t b = __ballot(u);
+        if (lane == 0) m.untag[j] = b;
+    }
+    wave_sync();
+}
+
+// 2x2 table on the opposite side's strict reads (:3940-3956), dir-0 tags, stats
+DEV void k3w_finish(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
+                    const K3WMem &m, uint32_t summ, const K3Stats &stx) {
+    const uint32_t lane = threadIdx.x & 63;
+    int tab0 = 0, tab1 = 0, tab2 = 0, tab3 = 0;
+    uint32_t nstrict = 0;
+    const uint32_t strict = dir == 0 ? FLG_RIGHT_STRICT : FLG_LEFT_STRICT;
+    for (uint32_t i = lane; i < R; i += 64) {
+        if (m.flg[i] & strict) {
+            nstrict++;
+            const uint32_t ref = d.read_hp[r0 + i], q = m.hp[i];
+            if (ref <= 1 && q <= 1) {
+                const uint32_t k = ref * 2 + q;
+                tab0 += k == 0; tab1 += k == 1; tab2 += k == 2; tab3 += k == 3;
+            }
+        }
+        if (dir == 0) d.hp_fwd[r0 + i] = m.hp[i];
+    }
+    uint32_t tsum[5] = {(uint32_t)tab0, (uint32_t)tab1, (uint32_t)tab2, (uint32_t)tab3, nstrict};
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        uint32_t tot = 0;
+        for (int bb = 0; bb < 16; bb++) tot += (uint32_t)__popcll(__ballot((tsum[k] >> bb) & 1)) << bb;
+        tsum[k] = tot;
+    }
+    if (lane < 4) d.table[((uint64_t)w * 2 + dir) * 4 + lane] = (int32_t)tsum[lane];
+    if (lane == 0) {
+        unsigned long long *sp = d.stats + ((uint64_t)w * 2 + dir) * PF_NSTAT;
+        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
+        sp[4] = summ; sp[5] = tsum[4]; sp[6] = R; sp[7] = S;
+    }
+}
+
+// pick from registers (k3_pick_exact with the per-candidate sums in lanes)
+DEV void k3w_pick_exact(double S0, double S1, uint32_t lane, uint32_t nc, uint32_t c_len, int l0, int l1,
+                        uint32_t &pick, uint32_t &cw, uint32_t &tg) {
+    const bool act = lane < nc;
+    if (!act) { S0 = 0.0; S1 = 0.0; }
+    // the reference's sequential sum within gamma_{L-1} of the exact sum, the
+    // per-lane fp32 partials within another gamma_{L-1} (k3w_fill): twice
+    // the single-sum margin, and 2^-8 of slack for the second-order terms
+    const double g = (double)(c_len > 1 ? c_len - 1 : 0) * (0x1p-23 * (1.0 + 0x1p-8));
+    const double E = g * (S0 + S1);
+    const double D = S0 > S1 ? S0 - S1 : S1 - S0;
+    const bool sgn = D > E;
+    const double dlo = sgn ? (D - E) * (1.0 - 0x1p-20) : 0.0;
+    const double dhi = (D + E) * (1.0 + 0x1p-20) + 0x1p-60;
+    const bool rel = l0 < 3 || l1 < 3;
+    const bool el = act && (!rel || dlo >= 3.0);
+    const bool un = !act || (rel && dhi < 3.0);
+    const uint64_t b_und = __ballot(!el && !un), b_el = __ballot(el);
+    const uint64_t b_sgn = __ballot(sgn), b_gt = __ballot(S0 > S1);
+    if (b_und) return;
+    if (b_el == 0) { pick = 2; return; }
+    const float flo = el ? (float)(dlo * (1.0 - 0x1p-20)) : 0.f;
+    const float fhi = (float)(dhi * (1.0 + 0x1p-20));
+    const uint32_t key = el ? __float_as_uint(flo) + 1u : 0u;
+    const uint32_t M = nc <= 16 ? (uint32_t)__builtin_amdgcn_readlane(
+                                      (int)dpp_max_step(dpp_max_step(dpp_max_step(dpp_max_step(key, 0), 1), 2), 3), 0)
+                                : wave_max_dpp(key);
+    const float mf = __uint_as_float(M - 1u);
+    const uint64_t b_hi = __ballot(el && fhi >= mf);
+    if (__popcll(b_hi) != 1) return;
+    const uint32_t cs = (uint32_t)__ffsll((unsigned long long)b_hi) - 1u;
+    if (!((b_sgn >> cs) & 1ull)) return;
+    pick = 1;
+    cw = cs;
+    tg = ((b_gt >> cs) & 1ull) ? 0u : 1u;
+}
+
+// per-wave fill scratch (static LDS): candidate fields and exact partial sums
+struct K3WFill {
+    uint4 cf[64];                // lo, kofs, first lane, length << 8 | lanes
+    double acc[128];             // hap 0 | hap 1 sums per candidate
+    uint32_t lcs[64];            // push/positive count pairs per candidate
+};
+
+template <bool C8>
+DEV void k3w_greedy(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
+                    uint32_t ntot, const K3WMem &m, uint32_t *qbuf, uint32_t *aux, K3WFill *fsc) {
+    const uint32_t lane = threadIdx.x & 63;
+    fsc->acc[lane] = 0.0;
+    fsc->acc[64 + lane] = 0.0;
+    fsc->lcs[lane] = 0u;
+    const int cov_rt = d.win_par[w * 4 + 1];
+    const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
+    const uint32_t nwords = (R + 63) >> 6;
+    K3Stats stx = {0, 0, 0, 0};
+#ifdef PF_K3_PROFILE
+    unsigned long long prof_acc[32] = {0};
+    unsigned long long prof_last = k3_stamp_now();
+#endif
+    uint32_t umin, umax, summ;
+    k3w_init<C8>(d, w, dir, r0, S, R, ntot, m, umin, umax, stx, summ);
+    k3w_tags(d, dir, r0, R, m, aux);
+    k3w_range(m, S, cov_rt, lane, umin, umax);
+    K3_STAMP(0);
+    int il = dir == 0 ? 0 : (int)R - 1;
+    uint32_t failed = 0;
+    uint32_t nc = 0;
+    uint32_t c_pos = 0, c_rd = 0, c_n = 0, c_st = 0, c_mo = 0, c_cs = 0;
+    uint32_t q_pos = 0, q_rd = 0, q_nn = 0, q_st = 0, q_mo = 0;
+    uint32_t q_cnt = 0, q_head = 0;
+    bool q_more = false;
+    int q_cont = 0;
+    uint32_t lsum = 0;
+    bool need_collect = true, have_win = false;
+    const bool force_fold = d.k3_mode == 1u;
+    uint32_t pfv[K3W_LSMAX / 64];                 // the queued read's slot list, loaded ahead
+    for (;;) {
+        if (have_win) k3w_range(m, S, cov_rt, lane, umin, umax);
+        // ---- candidate list: full collection from i_last (:4037-4051)
+        if (need_collect) {
+            bool done = false;
+            for (;;) {
+                if (dir == 0 ? il >= (int)R : il <= 0) { done = true; break; }
+                q_cnt = k3w_qbuild(d, m, r0, nwords, dir == 0 ? il - 1 : il + 1, dir, lane, qbuf,
+                                   q_pos, q_rd, q_nn, q_st, q_mo, q_more, q_cont);
+                const uint32_t take = q_cnt < NC ? q_cnt : NC;
+                c_pos = q_pos; c_rd = q_rd; c_n = q_nn; c_st = q_st; c_mo = q_mo;
+                q_head = take;
+                uint32_t found = take;
+                while (found < NC && q_more) {
+                    q_cnt = k3w_qbuild(d, m, r0, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
+                                       q_more, q_cont);
+                    q_head = 0;
+                    while (found < NC && q_head < q_cnt) {
+                        const uint32_t a0 = rdl(q_pos, q_head), a1 = rdl(q_rd, q_head), a2 = rdl(q_nn, q_head);
+                        const uint32_t a3 = rdl(q_st, q_head), a4 = rdl(q_mo, q_head);
+                        if (lane == found) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; }
+                        found++;
+                        q_head++;
+                    }
+                }
+                if (found == 0) {
+                    stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+                    if (++failed > 10) { done = true; break; }
+                    il += dir == 0 ? (int)NC : -(int)NC;
+                    continue;
+                }
+                nc = found;
+                break;
+            }
+            if (done) break;
+            need_collect = false;
+            // every candidate's slot list into cache list c
+            c_cs = lane;
+            for (uint32_t c = 0; c < nc; c++) k3w_cache_load(m, c, rdl(c_mo, c), rdl(c_n, c), lane);
+            wave_sync();
+        }
+        // ---- the next untagged read after the list, for this iteration's
+        // append; its slot list is loaded now and lands in the cache at the end
+        int qn = -1;
+        uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
+        if (nc == NC) {
+            if (q_head == q_cnt && q_more) {
+                q_cnt = k3w_qbuild(d, m, r0, nwords, q_cont, dir, lane, qbuf, q_pos, q_rd, q_nn, q_st, q_mo,
+                                   q_more, q_cont);
+                q_head = 0;
+            }
+            if (q_head < q_cnt) {
+                qn = (int)rdl(q_pos, q_head);
+                q_rd1 = rdl(q_rd, q_head); q_n1 = rdl(q_nn, q_head);
+                q_st1 = rdl(q_st, q_head); q_mo1 = rdl(q_mo, q_head);
+                q_head++;
+#pragma unroll
+                for (uint32_t u = 0; u < K3W_LSMAX / 64; u++) {
+                    const uint32_t t = u * 64 + lane;
+                    pfv[u] = t < q_n1 ? m.kb[q_mo1 + t] : PF_NONE;
+                }
+            }
+        }
+        // ---- lookup spans: sites in [min_i, max_i) (query_counts_of_mmrs, :3500-3501)
+        uint32_t c_len, c_lo, c_kofs;
+        {
+            const uint32_t lo = c_st > umin ? c_st : umin;
+            const uint32_t hi0 = c_st + c_n;
+            const uint32_t hi = hi0 < umax ? hi0 : umax;
+            c_len = lane < nc && hi > lo && umin != 0xFFFFFFFFu ? hi - lo : 0;
+            c_lo = lo;
+            c_kofs = c_cs * m.ls + (c_len ? lo - c_st : 0);
+        }
+        lsum += c_len;
+        if (nc >= NC) {
+            const uint32_t pl = rdl(c_pos, NC - 1);
+            stx.scanned += dir == 0 ? pl - (uint32_t)il + 1 : (uint32_t)il - pl + 1;
+        } else stx.scanned += dir == 0 ? (uint32_t)((int)R - il) : (uint32_t)(il + 1);
+        stx.iters++;
+        K3_STAMP(2);
+        // ---- term fill, balanced: candidate c gets g_c >= 1 lanes in
+        // proportion to its in-range methmers (sum <= 64), its lanes stride
+        // its terms; exact per-lane partial sums meet in LDS (fp64 sums are
+        // exact in any order)
+        uint32_t lcode;
+        double S0, S1;
+        {
+            const uint32_t incl = wave_incl_scan_dpp(c_len);
+            const uint32_t T = rdl(incl, 63);
+            const uint32_t g = lane < nc ? (T ? (uint32_t)(((uint64_t)c_len * (64u - nc)) / T) + 1u : 1u) : 0u;
+            const uint32_t gincl = wave_incl_scan_dpp(g);
+            if (lane < nc) fsc->cf[lane] = make_uint4(c_lo, c_kofs, gincl - g, (c_len << 8) | g);
+            wave_sync();
+            uint32_t c = 0;
+            for (uint32_t k = 0; k < nc; k++) c += rdl(gincl, k) <= lane ? 1u : 0u;
+            if (c < nc) {
+                const uint4 f = fsc->cf[c];
+                float x0 = 0.f, x1 = 0.f;
+                const uint32_t lc = k3w_fill<C8>(m, f.x, f.y, lane - f.z, f.w >> 8, f.w & 0xffu, x0, x1);
+                atomicAdd(&fsc->acc[c], (double)x0);
+                atomicAdd(&fsc->acc[64 + c], (double)x1);
+                atomicAdd(&fsc->lcs[c], lc);
+            }
+            wave_sync();
+            S0 = fsc->acc[lane];
+            S1 = fsc->acc[64 + lane];
+            lcode = fsc->lcs[lane];
+            fsc->acc[lane] = 0.0;
+            fsc->acc[64 + lane] = 0.0;
+            fsc->lcs[lane] = 0u;
+            wave_sync();
+        }
+        K3_STAMP(10);
+        // ---- pick: exact intervals, else the sequential fp32 fold
+        uint32_t pick = 0, cw = 0, tg = 0;
+        {
+            const int l0 = (int)(lcode & 0xffffu), l1 = (int)(lcode >> 16);
+            if (!force_fold) k3w_pick_exact(S0, S1, lane, nc, c_len, l0, l1, pick, cw, tg);
+            if (pick == 0) {
+                float s0 = 0.f, s1 = 0.f;
+                if (lane < nc) k3w_fold<C8>(m, c_lo, c_kofs, c_len, s0, s1);
+                const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
+                const bool elig = lane < nc && !(diff < 3.f && (l0 < 3 || l1 < 3));
+                const uint32_t hkey = elig ? __float_as_uint(diff) + 1u : 0u;
+                const uint32_t hmax = wave_max_dpp(hkey);
+                if (hmax == 0) pick = 2;
+                else {
+                    pick = 1;
+                    cw = 63u - (uint32_t)__clzll((long long)__ballot(hkey == hmax));
+                    tg = rdl(s0 > s1 ? 0u : 1u, cw);
+                }
+            }
+        }
+        K3_STAMP(19);
+        if (pick == 2) {
+            // nothing could be tagged (:4064-4069): move i_last, rescan
+            if (++failed > 10) break;
+            il += dir == 0 ? (int)NC : -(int)NC;
+            need_collect = true;
+            have_win = false;
+            continue;
+        }
+        // ---- the winner: tag, list minus the winner plus the queued read
+        const uint32_t rd = rdl(c_rd, cw), n = rdl(c_n, cw), st = rdl(c_st, cw), fs = rdl(c_cs, cw);
+        const uint32_t pw = rdl(c_pos, cw);
+        stx.inserts += n;
+        if (lane == 0) {
+            m.hp[rd] = (uint8_t)tg;
+            m.untag[pw >> 6] &= ~(1ull << (pw & 63));
+        }
+        failed = 0;
+        {
+            const int src = (int)lane + 1;
+            const uint32_t a0 = (uint32_t)__shfl((int)c_pos, src, 64), a1 = (uint32_t)__shfl((int)c_rd, src, 64);
+            const uint32_t a2 = (uint32_t)__shfl((int)c_n, src, 64), a3 = (uint32_t)__shfl((int)c_st, src, 64);
+            const uint32_t a4 = (uint32_t)__shfl((int)c_cs, src, 64);
+            if (lane >= cw) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_cs = a4; }
+        }
+        uint32_t ncn = nc - 1;
+        if (qn >= 0) {
+            if (lane == ncn) { c_pos = (uint32_t)qn; c_rd = q_rd1; c_n = q_n1; c_st = q_st1; c_cs = fs; }
+            ncn++;
+        }
+        nc = ncn;
+        if (nc == 0) need_collect = true;     // an empty batch: the reference's failure path (:4046-4051)
+        K3_STAMP(20);
+        k3w_insert<C8>(m, S, n, st, fs * m.ls, tg, lane);
+        K3_STAMP(21);
+        if (qn >= 0) {                        // the appended read takes the winner's cache list
+            uint16_t *dst = m.cc + fs * m.ls;
+#pragma unroll
+            for (uint32_t u = 0; u < K3W_LSMAX / 64; u++) {
+                const uint32_t t = u * 64 + lane;
+                if (t < q_n1) dst[t] = pfv[u] == PF_NONE ? (uint16_t)0xFFFFu : (uint16_t)pfv[u];
+            }
+            wave_sync();
+        }
+        have_win = true;
+        K3_STAMP(22);
+    }
+    {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int bb = 0; bb < 32; bb++) tot += (uint32_t)__popcll(__ballot((lsum >> bb) & 1)) << bb;
+        stx.lookups += tot;
+    }
+    k3w_finish(d, w, dir, r0, S, R, m, summ, stx);
+#ifdef PF_K3_PROFILE
+    if (lane == 0) {
+        unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 32;
+        for (int i = 0; i < 32; i++) pp[i] = prof_acc[i];
+    }
+#endif
+}
+
+// slot dictionary of one problem by one wave (k3_dict / k3_dict_rewrite with
+// eight reads' key loads in flight)
+DEV void k3w_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uint32_t dir, uint64_t *masks,
+                  uint32_t *base, uint32_t *sh_scan, K3Ctl &ctl, bool rewrite) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t MW = (uint32_t)d.mw;
+    if (!rewrite) {
+        for (uint32_t j = lane; j < S * MW; j += 64) masks[j] = 0;
+        wave_sync();
+    }
+    for (uint32_t i0 = 0; i0 < R; i0 += 8) {
+        uint32_t n[8], st[8];
+        uint32_t *kp[8];
+        uint32_t mx = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t i = i0 + u < R ? i0 + u : i0;
+            const uint64_t g = 2ull * (r0 + i) + dir;
+            n[u] = i0 + u < R ? d.mmr_n[g] : 0u;
+            st[u] = d.mmr_start[g];
+            kp[u] = d.keys + d.mmr_off[g];
+            mx = n[u] > mx ? n[u] : mx;
+        }
+        for (uint32_t t0 = 0; t0 < mx; t0 += 64) {
+            const uint32_t t = t0 + lane;
+            uint32_t key[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) key[u] = t < n[u] ? kp[u][t] : 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (t >= n[u]) continue;
+                const uint32_t site = st[u] + t;
+                const bool ok = site < S && key[u] < 64u * MW;
+                if (!rewrite) {
+                    if (ok) atomicOr((unsigned long long *)&masks[(uint64_t)site * MW + (key[u] >> 6)],
+                                     1ull << (key[u] & 63));
+                } else {
+                    uint32_t slot = PF_NONE;
+                    if (ok) {
+                        const uint64_t *row = masks + (uint64_t)site * MW;
+                        const uint32_t wi = key[u] >> 6, b = key[u] & 63;
+                        slot = base[site];
+                        for (uint32_t mm = 0; mm < wi; mm++) slot += (uint32_t)__popcll(row[mm]);
+                        slot += (uint32_t)__popcll(row[wi] & ((1ull << b) - 1ull));
+                    }
+                    kp[u][t] = slot;
+                }
+            }
+        }
+    }
+    wave_sync();
+    if (rewrite) return;
+    uint32_t carry = 0;
+    for (uint32_t p0 = 0; p0 < S; p0 += 64) {
+        const uint32_t p = p0 + lane;
+        uint32_t c = 0;
+        if (p < S)
+            for (uint32_t mm = 0; mm < MW; mm++) c += (uint32_t)__popcll(masks[(uint64_t)p * MW + mm]);
+        const uint32_t incl = wave_incl_scan_dpp(c);
+        if (p < S) base[p] = carry + incl - c;
+        carry += rdl(incl, 63);
+    }
+    if (lane == 0) ctl.ntot = carry;
+    wave_sync();
+}
+
+// LDS of the dictionary phase: masks, slot bases, and the per-site coverage
+// by methmer spans (S + 1 counters)
+DEV uint64_t k3w_p1_bytes(uint32_t S, uint32_t MW) {
+    return align16(8ull * S * MW) + align16(4ull * S) + 4ull * (S + 1);
+}
+
+DEV void k3w_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl, uint32_t *qbuf,
+                 uint32_t *sh_scan, K3WFill *fsc, const uint32_t lds) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t w = prob >> 1, dir = prob & 1;
+    const uint32_t S = d.win_S[w];
+    if (S == 0) {
+        if (lane < 4) d.table[((uint64_t)w * 2 + dir) * 4 + lane] = 0;
+        if (lane < PF_NSTAT) d.stats[((uint64_t)w * 2 + dir) * PF_NSTAT + lane] = 0;
+        return;
+    }
+    const uint32_t R = d.win_nreads[w];
+    const uint32_t r0 = d.win_read_off[w];
+    const uint32_t MW = (uint32_t)d.mw;
+    const uint64_t kbase = d.mmr_off[2ull * r0];
+    // the wave build: n_cand <= 64 (register candidate list), < 8192 sites
+    // (exact-interval pick), the dictionary in LDS, the exact or fold pick
+    if (d.win_par[w * 4 + 2] > 64 || S >= 8192u || d.k3_mode > 1u || k3w_p1_bytes(S, MW) > lds) {
+        k3_defer(d, prob);
+        return;
+    }
+    uint64_t *masks = reinterpret_cast<uint64_t *>(smem);
+    uint32_t *mbase = reinterpret_cast<uint32_t *>(smem + align16(8ull * S * MW));
+    uint32_t *cov = reinterpret_cast<uint32_t *>(smem + align16(8ull * S * MW) + align16(4ull * S));
+    k3w_dict(d, r0, R, S, dir, masks, mbase, sh_scan, ctl, false);
+    const uint32_t ntot = uni(ctl.ntot);
+    // deepest site coverage by methmer spans [st, st+n): it bounds every count
+    for (uint32_t j = lane; j <= S; j += 64) cov[j] = 0;
+    wave_sync();
+    for (uint32_t i = lane; i < R; i += 64) {
+        const uint64_t g = 2ull * (r0 + i) + dir;
+        const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
+        if (n && st < S) {
+            atomicAdd(&cov[st], 1u);
+            atomicAdd(&cov[st + n < S ? st + n : S], 0xFFFFFFFFu);
+        }
+    }
+    wave_sync();
+    uint32_t carry = 0, mx = 0;
+    for (uint32_t j0 = 0; j0 < S; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const uint32_t v = j < S ? cov[j] : 0u;
+        const uint32_t incl = wave_incl_scan_dpp(v) + carry;
+        carry = rdl(incl, 63);
+        const uint32_t c = j < S ? incl : 0u;
+        mx = c > mx ? c : mx;
+    }
+    mx = wave_max_dpp(mx);
+    const bool c8 = mx < 256u;
+    // longest methmer list of the direction: the candidate cache's stride
+    uint32_t mxl = 0;
+    for (uint32_t i = lane; i < R; i += 64) {
+        const uint32_t n = d.mmr_n[2ull * (r0 + i) + dir];
+        mxl = n > mxl ? n : mxl;
+    }
+    mxl = wave_max_dpp(mxl);
+    const uint32_t ls = (mxl + 7u) & ~7u;
+    const uint32_t NCw = (uint32_t)d.win_par[w * 4 + 2];
+    uint64_t off[K3W_NOFF];
+    const uint64_t need = c8 ? k3w_layout<true>(S, ntot, R, NCw, ls, off) : k3w_layout<false>(S, ntot, R, NCw, ls, off);
+    // the T5 scratch (4 B per read) goes after the layout when it fits there
+    const uint64_t need_aux = align16(need) + 4ull * R;
+    if (need_aux > lds || mxl > K3W_LSMAX || ntot >= 0xFFFFu) {
+        k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
+        return;
+    }
+    k3w_dict(d, r0, R, S, dir, masks, mbase, sh_scan, ctl, true);
+    K3WMem m;
+    m.srec = reinterpret_cast<float4 *>(smem + off[0]);
+    m.cnt = smem + off[1];
+    m.cc = reinterpret_cast<uint16_t *>(smem + off[2]);
+    m.ls = ls;
+    m.hp = smem + off[3];
+    m.flg = smem + off[4];
+    m.untag = reinterpret_cast<uint64_t *>(smem + off[5]);
+    m.kb = d.keys + kbase;
+    m.kbase = kbase;
+    uint32_t *aux2 = reinterpret_cast<uint32_t *>(smem + align16(need));
+    if (c8) k3w_greedy<true>(d, w, dir, r0, S, R, ntot, m, qbuf, aux2, fsc);
+    else k3w_greedy<false>(d, w, dir, r0, S, R, ntot, m, qbuf, aux2, fsc);
+}
+
+// Main greedy kernel: one wavefront per problem, heaviest first (k3_order);
+// problems it cannot take go to pf_k3_fallback.
+__global__ __launch_bounds__(64) void pf_k3_wave(pf_dev_batch d) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ K3Ctl ctl;
+    __shared__ uint32_t qbuf[64];
+    __shared__ uint32_t sh_scan[2];
+    __shared__ K3WFill fsc;
+    k3w_run(d, d.k3_order[blockIdx.x], smem, ctl, qbuf, sh_scan, &fsc, d.lds_w);
 }
 
 // ------------------------------------------------------------------------

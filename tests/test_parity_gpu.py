@@ -198,3 +198,20 @@ def test_pipelined_launch_finish(oracle_lib, gpu_ctx):
     _compare(ref, o2, "pipelined-2")
     _compare(ref, db.run(), "after")
     db.free()
+
+
+@pytest.mark.parametrize("env", [{"PF_K3_IMPL": "wave"}, {"PF_K3_IMPL": "wave", "PF_K3W_LDS": "6000"},
+                                 {"PF_K3_IMPL": "wave", "PF_K3W_LDS": "16384"}],
+                         ids=["wave_kernel", "wave_defers_most", "wave_small_lds"])
+def test_greedy_kernel_variants(oracle_lib, gpu_ctx, monkeypatch, env):
+    """The main greedy kernel is the 256-thread build; PF_K3_IMPL=wave runs
+    the one-wavefront build instead (fp32 lane partials, candidate slot-list
+    cache, u8 count pairs), and a small PF_K3W_LDS defers its problems to the
+    fallback kernel.  Every variant gives the oracle's bits."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for name, cfg, batch in [c for c in CASES if c[0] in ("synth30", "synth60", "gapmix", "oddtags", "report200")]:
+        ref = oracle_lib.methphase(cfg, batch, n_threads=8)
+        db = gpu_ctx.upload(cfg, batch)
+        _compare(ref, db.run(), f"{name}/{env}")
+        db.free()

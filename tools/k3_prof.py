@@ -16,18 +16,20 @@ names = ["init", "setup", "publish", "barrierB", "fold(chunked)", "pick fallback
          "barrierA", "fields", "fill_rows", "groupsum",
          "upkeep:collect", "upkeep:next read", "pick:lcode", "pick_exact",
          "tail:insert", "tail:hp/untag", "tail:shift", "tail:range update"]
-for cov in (30, 60):
+NW = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+COVS = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [30, 60]
+for cov in COVS:
     cfg = Config.from_coverage(cov, given=False)
-    b = make_batch(SynthSpec(n_windows=256, coverage=cov, seed=11))
+    b = make_batch(SynthSpec(n_windows=NW, coverage=cov, seed=11))
     ctx = Context(0)
     db = ctx.upload(cfg, b)
     db.run(); db.run()
     lib = L.lib()
     lib.pf_batch_prof.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
-    raw = np.zeros(256 * 80, np.uint64)
+    raw = np.zeros(NW * 80, np.uint64)
     lib.pf_batch_prof(db.handle, raw.ctypes.data, raw.size)
-    prof = raw[:256 * 64].reshape(256, 2, 32)
-    k12 = raw[256 * 64:].reshape(256, 16).astype(float)
+    prof = raw[:NW * 64].reshape(NW, 2, 32)
+    k12 = raw[NW * 64:].reshape(NW, 16).astype(float)
     st = db.stats()
     cnt = prof[:, :, 12:16].sum(axis=(0, 1)).astype(float)
     tot = np.concatenate([prof[:, :, :12], prof[:, :, 16:24]], axis=2).sum(axis=(0, 1)).astype(float)
@@ -47,7 +49,8 @@ for cov in (30, 60):
     print(f"  loop back-edge (tail end -> loop top, wave 0): {prof[:, :, 28].sum() / iters:.0f} cyc/iter")
     print(f"  per iter: failed picks {ev[0]/iters:.3f}  collects {ev[1]/iters:.3f}  "
           f"collect rebuilds {ev[2]/iters:.3f}  queue refills {ev[3]/iters:.3f}")
-    print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}")
+    print(f"  median problem cycles {np.median(per):.3g}, mean {per.mean():.3g}, max {per.max():.3g}, "
+          f"p90 {np.percentile(per, 90):.3g}")
     print(f"  per iter: lmax(chunked) {cnt[0]/iters:.1f}  nc(one-chunk) {cnt[1]/iters:.2f}  "
           f"picks needing the sequential fold {cnt[2]/iters*100:.2f}%")
     names12 = ["-", "T7+range", "sites", "revbuf", "dir arrays", "reservation", "methmers"]
