@@ -645,6 +645,8 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
     ld.hi = (uint8_t)lc->qual_hi;
     const char *fs = getenv("PF_K0_PATH");
     ld.force_seq = fs && strcmp(fs, "seq") == 0;
+    const char *kd = getenv("PF_K0_DIAG");
+    ld.diag = kd ? (uint32_t)atoi(kd) : 0u;
     int rc = 0;
 #define PUT(field, src, cnt) do { rc = dev_put(b, &field, src, cnt); if (rc) return fail(rc); } while (0)
 #define ALLOC(field, cnt) do { rc = dev_alloc(b, &field, cnt); if (rc) return fail(rc); } while (0)

@@ -60,6 +60,7 @@ struct pf_load_dev {
     uint32_t min_mapq, min_len;
     uint32_t lo, hi;                 /* uint8_t in the reference (799) */
     uint32_t force_seq;              /* test override: every record through the sequential path */
+    uint32_t diag;                   /* measurement only (PF_K0_DIAG): 1 = trigger placement reads no SEQ word */
     const uint32_t *order;           /* [n_recs] record of each wave slot: longest reads first */
     const uint32_t *rec_win;         /* [n_recs] window of each record */
     const uint32_t *win_rec_off;     /* [W+1] records of each window */

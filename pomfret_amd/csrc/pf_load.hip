@@ -440,7 +440,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                 uint32_t hw = 0;
                 if (k >= c0) { k -= c0; hw = 1; }
                 const uint32_t w = b * BW + i * RW + 2 * Lw + hw;
-                const uint64_t xw = nibswap(sw[w]);
+                const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(sw[w]);
                 const uint32_t bi = sel_nibble(zero_nibbles(xw ^ pat), k);
                 const uint32_t p = w * 16 + bi;
                 uint32_t key = 0xFFFFFFFFu;

@@ -58,6 +58,8 @@ def main():
     fetch, write, cal_f, cal_w = sys.argv[1:5]
     boundary = sys.argv[5] if len(sys.argv) > 5 else "records"
     from bench import WORKLOAD
+    # the bench's N=1 workload (strong scaling: every window on this GPU)
+    WORKLOAD = dict(WORKLOAD, windows_per_gpu=WORKLOAD["n_windows"])
     f = per_kernel(fetch, "FETCH_SIZE")
     w = per_kernel(write, "WRITE_SIZE")
     cf = per_kernel(cal_f, "FETCH_SIZE")
