@@ -504,6 +504,7 @@ int      pf_tags_view(const pf_tags_t *t, pf_qname_tags_t *out);
 #define PF_READBACK 50000          /* blockjoin.c READBACK, the fetch margin of 1053-1054 */
 #define PF_MODE_METHPHASE 0
 #define PF_MODE_REPORT    1
+#define PF_MODE_VARHAPTAG 2        /* pf_methphase_main only: out_prefix is the output BAM path */
 #define PF_JOB_WINDOWS 0           /* a run of consecutive windows of one contig */
 #define PF_JOB_HAPTAG  1           /* the -u pre-pass of one contig (1841-1898) */
 
@@ -522,7 +523,7 @@ typedef struct pf_methphase_opts {
     pf_load_cfg_t load;            /* -q, -L, --lo, --hi                                       */
     int32_t untagged;              /* -u, --bam-is-untagged                                    */
     int32_t write_tsv;             /* --output-tsv: {prefix}.mp.tsv                            */
-    int32_t write_bam;             /* --write-bam (PF_ERR_UNSUPPORTED in pf_methphase_main)    */
+    int32_t write_bam;             /* --write-bam: {prefix}.mp.bam + .bai (varhaptag: the BAM) */
     int32_t chunk_size, chunk_stride;  /* report: --chunk-size, --chunk-stride                 */
     int32_t threads;               /* host threads fetching one job's windows (-t)             */
     int32_t n_devices;             /* GPUs to drive from this process (0: all visible)         */
@@ -540,8 +541,9 @@ typedef struct pf_mp_plan pf_mp_plan_t;
 /* Whole run in this process: plan, (-u) pre-pass jobs on the devices, window
  * jobs on the devices (one host thread per GPU; the next job's BAM fetch
  * overlaps the current job's kernels), merge and outputs:
- * {prefix}.mp.gtf, .mp.vcf (and .mp.tsv), or {prefix}.report.tsv plus the
- * running totals on stdout.  On success *out holds the finished plan
+ * {prefix}.mp.gtf, .mp.vcf (and .mp.tsv, .mp.bam + .mp.bam.bai), or
+ * {prefix}.report.tsv plus the running totals on stdout, or (varhaptag) the
+ * -u pre-pass alone with {out}.varhaptag.tsv and the retagged {out} + .bai.  On success *out holds the finished plan
  * (decisions, tables, blocks) until pf_mp_free. */
 int  pf_methphase_main(const pf_methphase_opts_t *o, pf_mp_plan_t **out);
 
@@ -601,6 +603,35 @@ const pf_tags_t   *pf_mp_qname_hp(const pf_mp_plan_t *p);
 const pf_tags_t   *pf_mp_raw_hp(const pf_mp_plan_t *p);     /* NULL without -u */
 /* report: {correct, switch, fail} */
 int  pf_mp_report_counts(const pf_mp_plan_t *p, double *counts3);
+
+/* ------------------------------------------------------------------ */
+/* BAM output: --write-bam and varhaptag.                               */
+
+#define PF_RETAG_METHPHASE 0       /* output_modify_bam (blockjoin.c:3022-3103)   */
+#define PF_RETAG_VARHAPTAG 1       /* main_varhaptag (4737-4836)                  */
+
+/* Every record of bam_in, in file order (sam_itr_querys "."), with HP set
+ * to the new haplotag + 1 as bam_aux_update_int does it (an existing
+ * integer HP keeps its size when the value fits, else it grows in place; a
+ * missing HP is appended as the smallest integer type; a non-integer HP or
+ * corrupt aux data leaves the record unchanged), written to bam_out (NULL:
+ * none) with its BAI at bai_out (NULL: none; sam_index_build3 at 4723), and
+ * for varhaptag one TSV line per record to tsv_out (NULL: none):
+ * "#qname\thaptag_input\thaptag_new", then qname, HP-tag value, new + 1.
+ *   PF_RETAG_METHPHASE: the raw tag is raw's (the -u table; absent:
+ *     unphased) or the HP tag's (get_hp_from_aln); a qname in `methphased`
+ *     (st->qname2haptag) takes its tag, a raw 0/1 otherwise; either is
+ *     flipped when the phased interval the read starts in
+ *     (check_if_in_phased_intervals over g's merged gaps) needs it -- the
+ *     flip of blk's raw gap at the merged index - 1, carried over until the
+ *     next interval is entered, across contigs too (get_flip_status_by_idx).
+ *   PF_RETAG_VARHAPTAG: the new tag is raw's (absent: unphased).
+ * level: zlib level (htslib's "w" mode: -1, Z_DEFAULT_COMPRESSION).
+ * The iteration stops, as htslib's does, at a record whose CIGAR query
+ * length differs from l_qseq.  *n_records: records processed. */
+int  pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, const char *tsv_out, int mode,
+                  const pf_gaps_t *g, const pf_blocks_t *blk, const pf_tags_t *methphased, const pf_tags_t *raw,
+                  int level, uint64_t *n_records);
 
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
  * the observed table. */

@@ -1351,3 +1351,473 @@ int pf_bam_estimate_coverage(pf_bam_t *b, int32_t *covs, int32_t n) {
     free(z);
     return rc;
 }
+
+/* ------------------------------------------------------------------ */
+/* BAM writer: --write-bam (output_modify_bam, blockjoin.c:3022-3103, and
+ * the sam_index_build3 call at 4723) and varhaptag (main_varhaptag,
+ * 4737-4836).
+ *
+ * BGZF as htslib's bgzf_write writes it: 0xff00-byte blocks, raw deflate
+ * (zlib, window 15, memLevel 8, default strategy) at the given level (htslib's
+ * "w" mode: Z_DEFAULT_COMPRESSION), the header flushed into its own block(s)
+ * by bam_hdr_write, and bam_write1's bgzf_flush_try: a record that does not
+ * fit the current block starts a new one (only records larger than a block
+ * straddle blocks).  The index is built as hts_idx_push / hts_idx_finish
+ * build it while the file is written (chunks per bin, the 16 kb linear index
+ * with leading holes set to the first record's offset and later holes to the
+ * previous window's, the metadata pseudo-bin, the unplaced-read count); bins
+ * are written in ascending order and htslib's compress_binning (merging bins
+ * whose chunks span < 64 KiB of compressed file into their parent, in khash
+ * order) is not applied, so the index answers every query alike but is not
+ * byte-identical to htslib's -- parity unpinned (htslib is absent here).  The
+ * records themselves are copied byte for byte except the HP tag; a CG:B:I
+ * long-CIGAR record keeps its placeholder layout (htslib's bam_write1 would
+ * re-append the CG tag at the end of the aux data). */
+
+#define BGZF_BLK 0xff00
+static const uint8_t BGZF_EOF[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0,
+                                     0, 0, 0, 0, 0, 0, 0, 0};
+
+typedef struct {
+    FILE *f;
+    uint8_t ubuf[BGZF_BLK];
+    uint8_t cbuf[65536];
+    int n;
+    uint64_t caddr;              /* compressed address of the block being filled */
+    int level;
+    int err;
+} bgzfw_t;
+
+static int bgzfw_flush(bgzfw_t *w) {
+    if (w->err) return w->err;
+    if (w->n == 0) return 0;
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, w->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return w->err = PF_ERR_NOMEM;
+    zs.next_in = w->ubuf;
+    zs.avail_in = (uInt)w->n;
+    zs.next_out = w->cbuf + 18;
+    zs.avail_out = (uInt)(sizeof w->cbuf - 18 - 8);
+    const int rc = deflate(&zs, Z_FINISH);
+    const uint32_t clen = (uint32_t)zs.total_out;
+    deflateEnd(&zs);
+    if (rc != Z_STREAM_END) return w->err = PF_ERR_INTERNAL;
+    const uint32_t bsize = 18 + clen + 8;
+    uint8_t *h = w->cbuf;
+    const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0};
+    memcpy(h, hdr, 16);
+    h[16] = (uint8_t)((bsize - 1) & 0xff);
+    h[17] = (uint8_t)((bsize - 1) >> 8);
+    const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), w->ubuf, (uInt)w->n);
+    uint8_t *t = h + 18 + clen;
+    for (int i = 0; i < 4; i++) { t[i] = (uint8_t)(crc >> (8 * i)); t[4 + i] = (uint8_t)((uint32_t)w->n >> (8 * i)); }
+    if (fwrite(h, 1, bsize, w->f) != bsize) return w->err = -1;
+    w->caddr += bsize;
+    w->n = 0;
+    return 0;
+}
+
+static int bgzfw_write(bgzfw_t *w, const void *src, size_t n) {
+    const uint8_t *s = (const uint8_t *)src;
+    while (n && !w->err) {
+        size_t k = (size_t)(BGZF_BLK - w->n);
+        if (k > n) k = n;
+        memcpy(w->ubuf + w->n, s, k);
+        w->n += (int)k;
+        s += k;
+        n -= k;
+        if (w->n == BGZF_BLK) bgzfw_flush(w);
+    }
+    return w->err;
+}
+
+static uint64_t bgzfw_tell(const bgzfw_t *w) { return (w->caddr << 16) | (uint64_t)w->n; }
+
+/* hts_idx_push / hts_idx_finish for a BAI (min_shift 14, 5 levels) */
+typedef struct { uint32_t bin; uint64_t u, v; } ichunk_t;
+typedef struct {
+    ichunk_t *c; size_t n, m;
+    uint64_t *lin; size_t nl, ml;
+    int has_meta;
+    uint64_t off_beg, off_end, n_mapped, n_unmapped;
+} iref_t;
+typedef struct {
+    int32_t n_ref;
+    iref_t *r;
+    uint64_t n_no_coor;
+    int32_t last_tid, save_tid;
+    uint32_t last_bin, save_bin;
+    uint64_t save_off, last_off, off_beg;
+    uint64_t n_mapped, n_unmapped;
+    int finished;
+    int err;
+} bai_t;
+
+static uint32_t reg2bin14(int64_t beg, int64_t end) {
+    end--;
+    if (beg >> 14 == end >> 14) return (uint32_t)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (uint32_t)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (uint32_t)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (uint32_t)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (uint32_t)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+static void bai_chunk(bai_t *x, int32_t tid, uint32_t bin, uint64_t u, uint64_t v) {
+    if (x->err || tid < 0 || tid >= x->n_ref) return;
+    iref_t *r = &x->r[tid];
+    if (r->n == r->m) {
+        const size_t m = r->m ? 2 * r->m : 64;
+        ichunk_t *c = (ichunk_t *)realloc(r->c, m * sizeof(ichunk_t));
+        if (!c) { x->err = PF_ERR_NOMEM; return; }
+        r->c = c;
+        r->m = m;
+    }
+    r->c[r->n].bin = bin; r->c[r->n].u = u; r->c[r->n].v = v;
+    r->n++;
+}
+
+static void bai_meta(bai_t *x, int32_t tid, uint64_t beg, uint64_t end) {
+    if (tid < 0 || tid >= x->n_ref) return;
+    iref_t *r = &x->r[tid];
+    r->has_meta = 1;
+    r->off_beg = beg; r->off_end = end;
+    r->n_mapped = x->n_mapped; r->n_unmapped = x->n_unmapped;
+}
+
+static void bai_finish(bai_t *x, uint64_t final_off) {
+    if (x->finished) return;
+    if (x->save_tid >= 0) {
+        bai_chunk(x, x->save_tid, x->save_bin, x->save_off, final_off);
+        bai_meta(x, x->save_tid, x->off_beg, final_off);
+    }
+    x->finished = 1;
+}
+
+static void bai_push(bai_t *x, int32_t tid, int64_t beg, int64_t end, uint64_t offset, int mapped) {
+    if (tid < 0) x->n_no_coor++;
+    if (x->finished || x->err) return;
+    if (x->last_tid != tid || (x->last_tid >= 0 && tid < 0)) {
+        x->last_tid = tid;
+        x->last_bin = 0xffffffffu;
+    }
+    if (tid >= 0 && tid < x->n_ref && mapped) {          /* insert_to_l */
+        if (beg < 0) beg = 0;
+        if (end <= 0) end = 1;
+        iref_t *r = &x->r[tid];
+        const int64_t b = beg >> 14, e = (end - 1) >> 14;
+        if ((size_t)e + 1 > r->ml) {
+            size_t m = r->ml ? r->ml : 64;
+            while (m < (size_t)e + 1) m *= 2;
+            uint64_t *l = (uint64_t *)realloc(r->lin, m * sizeof(uint64_t));
+            if (!l) { x->err = PF_ERR_NOMEM; return; }
+            for (size_t i = r->ml; i < m; i++) l[i] = ~0ull;
+            r->lin = l;
+            r->ml = m;
+        }
+        for (int64_t i = b; i <= e; i++) if (r->lin[i] == ~0ull) r->lin[i] = x->last_off;
+        if (r->nl < (size_t)e + 1) r->nl = (size_t)e + 1;
+    }
+    const uint32_t bin = reg2bin14(beg, end);
+    if (x->last_bin != bin) {
+        if (x->save_bin != 0xffffffffu) bai_chunk(x, x->save_tid, x->save_bin, x->save_off, x->last_off);
+        if (x->last_bin == 0xffffffffu && x->save_bin != 0xffffffffu) {   /* change of contig */
+            bai_meta(x, x->save_tid, x->off_beg, x->last_off);
+            x->n_mapped = x->n_unmapped = 0;
+            x->off_beg = x->last_off;
+        }
+        x->save_off = x->last_off;
+        x->save_bin = x->last_bin = bin;
+        x->save_tid = tid;
+        if (tid < 0) { bai_finish(x, offset); return; }
+    }
+    if (mapped) x->n_mapped++;
+    else x->n_unmapped++;
+    x->last_off = offset;
+}
+
+static int cmp_ichunk(const void *a, const void *b) {
+    const ichunk_t *x = (const ichunk_t *)a, *y = (const ichunk_t *)b;
+    if (x->bin != y->bin) return x->bin < y->bin ? -1 : 1;
+    return x->u < y->u ? -1 : x->u > y->u;
+}
+
+static int bai_write(bai_t *x, const char *path) {
+    FILE *f = fopen(path, "wb");
+    if (!f) return -1;
+    int rc = 0;
+#define W(p, n) do { if (!rc && fwrite((p), 1, (n), f) != (size_t)(n)) rc = -1; } while (0)
+    W("BAI\1", 4);
+    int32_t nr = x->n_ref;
+    W(&nr, 4);
+    for (int32_t t = 0; t < x->n_ref; t++) {
+        iref_t *r = &x->r[t];
+        qsort(r->c, r->n, sizeof(ichunk_t), cmp_ichunk);
+        int32_t nb = 0;
+        for (size_t i = 0; i < r->n; i++) if (i == 0 || r->c[i].bin != r->c[i - 1].bin) nb++;
+        const int32_t nbt = nb + (r->has_meta ? 1 : 0);
+        W(&nbt, 4);
+        for (size_t i = 0; i < r->n;) {
+            size_t j = i;
+            while (j < r->n && r->c[j].bin == r->c[i].bin) j++;
+            const uint32_t bin = r->c[i].bin;
+            const int32_t nc = (int32_t)(j - i);
+            W(&bin, 4);
+            W(&nc, 4);
+            for (size_t k = i; k < j; k++) { W(&r->c[k].u, 8); W(&r->c[k].v, 8); }
+            i = j;
+        }
+        if (r->has_meta) {
+            const uint32_t mb = 37450;
+            const int32_t two = 2;
+            W(&mb, 4); W(&two, 4);
+            W(&r->off_beg, 8); W(&r->off_end, 8); W(&r->n_mapped, 8); W(&r->n_unmapped, 8);
+        }
+        /* update_loff: leading holes -> the contig's first record offset, others -> previous */
+        size_t l = 0;
+        const uint64_t offset0 = r->has_meta ? r->off_beg : 0;
+        for (; l < r->nl && r->lin[l] == ~0ull; l++) r->lin[l] = offset0;
+        for (; l < r->nl; l++) if (r->lin[l] == ~0ull) r->lin[l] = r->lin[l - 1];
+        const int32_t ni = (int32_t)r->nl;
+        W(&ni, 4);
+        for (size_t i = 0; i < r->nl; i++) W(&r->lin[i], 8);
+    }
+    W(&x->n_no_coor, 8);
+#undef W
+    if (fclose(f) && !rc) rc = -1;
+    return rc;
+}
+
+/* bam_aux_update_int(b, "HP", val) on a record's bytes: rewrite into out */
+static int hp_update(const uint8_t *d, uint32_t bs, const rec_t *r, int64_t val, vbuf_t *out) {
+    out->n = 0;
+    uint8_t type;
+    uint32_t sz;
+    if (val < INT16_MIN || val > UINT16_MAX) { type = val < 0 ? 'i' : 'I'; sz = 4; }
+    else if (val < INT8_MIN || val > UINT8_MAX) { type = val < 0 ? 's' : 'S'; sz = 2; }
+    else { type = val < 0 ? 'c' : 'C'; sz = 1; }
+    /* bam_aux_get: the first HP, or ENOENT at the end, or EINVAL on corrupt aux */
+    const uint8_t *p = r->aux, *hp = NULL;
+    int corrupt = 0;
+    while (p + 3 <= r->aux_end) {
+        const size_t s = aux_size(p, r->aux_end);
+        if (s == 0 || p + 3 + s > r->aux_end) { corrupt = 1; break; }
+        if (p[0] == 'H' && p[1] == 'P') { hp = p; break; }
+        p += 3 + s;
+    }
+    if (!hp && (corrupt || p != r->aux_end)) return vb_put(out, d, bs);      /* invalid aux: unchanged */
+    uint8_t v8[8];
+    for (int i = 0; i < 8; i++) v8[i] = (uint8_t)((uint64_t)val >> (8 * i));
+    if (!hp) {                                                   /* new tag at the end */
+        const uint8_t t3[3] = {'H', 'P', type};
+        int rc = vb_put(out, d, bs);
+        if (!rc) rc = vb_put(out, t3, 3);
+        if (!rc) rc = vb_put(out, v8, sz);
+        return rc;
+    }
+    uint32_t old_sz;
+    switch (hp[2]) {
+    case 'c': case 'C': old_sz = 1; break;
+    case 's': case 'S': old_sz = 2; break;
+    case 'i': case 'I': old_sz = 4; break;
+    default: return vb_put(out, d, bs);                          /* not an integer: unchanged */
+    }
+    if (old_sz >= sz) {                                          /* reuse the old space */
+        sz = old_sz;
+        type = (uint8_t)(val < 0 ? "\0cs\0i"[old_sz] : "\0CS\0I"[old_sz]);
+    }
+    const size_t at = (size_t)(hp - d);
+    int rc = vb_put(out, d, at + 2);
+    if (!rc) rc = vb_put(out, &type, 1);
+    if (!rc) rc = vb_put(out, v8, sz);
+    if (!rc) rc = vb_put(out, hp + 3 + old_sz, bs - (at + 3 + old_sz));
+    return rc;
+}
+
+int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, const char *tsv_out, int mode,
+                 const pf_gaps_t *g, const pf_blocks_t *blk, const pf_tags_t *methphased, const pf_tags_t *raw,
+                 int level, uint64_t *n_records) {
+    if (!bam_in || (!bam_out && !tsv_out) || (mode != PF_RETAG_METHPHASE && mode != PF_RETAG_VARHAPTAG))
+        return PF_ERR_ARG;
+    if (mode == PF_RETAG_METHPHASE && (!g || !blk || !methphased)) return PF_ERR_ARG;
+    if (mode == PF_RETAG_VARHAPTAG && !raw) return PF_ERR_ARG;
+    if (n_records) *n_records = 0;
+    bgzf_t *z = (bgzf_t *)malloc(sizeof(bgzf_t));
+    bgzfw_t *w = bam_out ? (bgzfw_t *)calloc(1, sizeof(bgzfw_t)) : NULL;
+    FILE *tsv = NULL;
+    bai_t X;
+    memset(&X, 0, sizeof X);
+    uint8_t *rec = NULL, *hdr = NULL;
+    size_t cap = 0;
+    vbuf_t ob = {0};
+    char **names = NULL;
+    int32_t *vcf_of_tid = NULL;
+    int32_t n_ref = 0;
+    int rc = (!z || (bam_out && !w)) ? PF_ERR_NOMEM : 0;
+    if (!rc) { rc = bgzf_open(z, bam_in); if (rc) { free(z); z = NULL; } }
+    if (!rc && w) {
+        w->f = fopen(bam_out, "wb");
+        w->level = level;
+        if (!w->f) rc = -1;
+    }
+    if (!rc && tsv_out) {
+        tsv = fopen(tsv_out, "w");
+        if (!tsv) rc = -1;
+        else fprintf(tsv, "#qname\thaptag_input\thaptag_new\n");
+    }
+    /* header: copied as read, then flushed into its own block (bam_hdr_write) */
+    if (!rc) {
+        uint8_t h8[8], w4[4];
+        if (bgzf_read(z, h8, 8) != 8 || memcmp(h8, "BAM\1", 4) != 0) rc = PF_ERR_ARG;
+        const uint32_t lt = rc ? 0 : rd32(h8 + 4);
+        if (!rc) { hdr = (uint8_t *)malloc(lt ? lt : 1); if (!hdr) rc = PF_ERR_NOMEM; }
+        if (!rc && bgzf_read(z, hdr, lt) != (int64_t)lt) rc = PF_ERR_ARG;
+        if (!rc && w) { bgzfw_write(w, h8, 8); bgzfw_write(w, hdr, lt); }
+        if (!rc && bgzf_read(z, w4, 4) != 4) rc = PF_ERR_ARG;
+        if (!rc) {
+            n_ref = (int32_t)rd32(w4);
+            if (n_ref < 0) rc = PF_ERR_ARG;
+            if (w) bgzfw_write(w, w4, 4);
+        }
+        if (!rc) {
+            names = (char **)calloc(n_ref ? (size_t)n_ref : 1, sizeof(char *));
+            vcf_of_tid = (int32_t *)malloc((n_ref ? (size_t)n_ref : 1) * sizeof(int32_t));
+            if (!names || !vcf_of_tid) rc = PF_ERR_NOMEM;
+        }
+        for (int32_t t = 0; t < n_ref && !rc; t++) {
+            if (bgzf_read(z, w4, 4) != 4) { rc = PF_ERR_ARG; break; }
+            const uint32_t ln = rd32(w4);
+            if (ln == 0 || ln > (1u << 20)) { rc = PF_ERR_ARG; break; }
+            names[t] = (char *)malloc(ln);
+            uint8_t l4[4];
+            if (!names[t]) { rc = PF_ERR_NOMEM; break; }
+            if (bgzf_read(z, names[t], ln) != (int64_t)ln || bgzf_read(z, l4, 4) != 4) { rc = PF_ERR_ARG; break; }
+            names[t][ln - 1] = 0;
+            if (w) { bgzfw_write(w, w4, 4); bgzfw_write(w, names[t], ln); bgzfw_write(w, l4, 4); }
+            vcf_of_tid[t] = -1;                          /* the contig's VCF index, by name */
+            if (g) for (uint32_t c = 0; c < g->n_contigs; c++) if (!strcmp(g->names[c], names[t])) { vcf_of_tid[t] = (int32_t)c; break; }
+        }
+        if (!rc && w) rc = bgzfw_flush(w);
+    }
+    if (!rc && w) {
+        X.n_ref = n_ref;
+        X.r = (iref_t *)calloc(n_ref ? (size_t)n_ref : 1, sizeof(iref_t));
+        if (!X.r) rc = PF_ERR_NOMEM;
+        X.last_tid = -1; X.save_tid = -1;
+        X.last_bin = X.save_bin = 0xffffffffu;
+        X.last_off = X.off_beg = bgzfw_tell(w);
+    }
+    /* output_modify_bam's cursor state (3038-3040, 3059-3064) */
+    int prev_unphased_idx = 1, need_flip = 0;
+    int32_t prev_tid = 0;
+    uint64_t nrec = 0;
+    while (!rc) {
+        uint8_t w4[4];
+        const int64_t gr = bgzf_read(z, w4, 4);
+        if (gr == 0) break;
+        if (gr != 4) { rc = PF_ERR_ARG; break; }
+        const uint32_t bs = rd32(w4);
+        if (bs < 32 || bs > (1u << 30)) { rc = PF_ERR_ARG; break; }
+        if (bs > cap) {
+            uint8_t *np = (uint8_t *)realloc(rec, bs);
+            if (!np) { rc = PF_ERR_NOMEM; break; }
+            rec = np;
+            cap = bs;
+        }
+        if (bgzf_read(z, rec, bs) != (int64_t)bs) { rc = PF_ERR_ARG; break; }
+        rec_t r;
+        if (rec_decode(rec, bs, &r)) { rc = PF_ERR_ARG; break; }
+        const uint8_t *cg = r.cigar;
+        uint32_t ncg = r.n_cigar;
+        if (ncg > 0 && r.tid >= 0 && r.pos >= 0 && (rd32(cg) & 15u) == 4u && (rd32(cg) >> 4) == r.l_qseq) {
+            const uint8_t *t = aux_find(r.aux, r.aux_end, "CG");
+            if (t && t[2] == 'B' && (t[3] == 'I' || t[3] == 'i')) {
+                const uint32_t nn = rd32(t + 4);
+                if (nn >= r.n_cigar && nn < (1u << 29)) { cg = t + 8; ncg = nn; }
+            }
+        }
+        uint64_t qlen = 0;
+        const uint64_t rlen = cigar_rlen(cg, ncg, &qlen);
+        if (ncg > 0 && r.l_qseq > 0 && !(r.flag & 4) && qlen != r.l_qseq) break;   /* sam_itr_next < 0 */
+        const size_t lq = r.l_qname > 0 ? r.l_qname - 1 : 0;
+        uint64_t qoff[2] = {0, (uint64_t)lq};
+        /* the raw tag: the -u table (absent -> unphased) or get_hp_from_aln (910-923) */
+        int hp_tag;
+        {
+            int64_t v = 0;
+            const uint8_t *t = aux_find(r.aux, r.aux_end, "HP");
+            hp_tag = (t && aux_int(t, &v) && v != 0) ? (int)(v - 1) : 254;
+            if (t && !aux_int(t, &v)) hp_tag = 254;      /* bam_aux2i of a non-integer: 0 */
+        }
+        int hp_raw = hp_tag;
+        if (raw) {
+            uint8_t h;
+            pf_tags_get(raw, 1, qoff, r.qname, 254, &h);
+            hp_raw = h;
+        }
+        int hp;
+        if (mode == PF_RETAG_VARHAPTAG) {
+            hp = hp_raw;                                 /* st->qname2haptag_raw, 4787-4795 */
+        } else {
+            if (r.tid != prev_tid) { prev_unphased_idx = 1; prev_tid = r.tid; }
+            /* check_if_in_phased_intervals (2406-2426) on the contig's merged gaps */
+            const int32_t c = (r.tid >= 0 && r.tid < n_ref) ? vcf_of_tid[r.tid] : -1;
+            int updated = 0;
+            if (c >= 0) {
+                const uint64_t go = g->gap_off[c], gn = g->gap_off[c + 1] - go;
+                for (uint64_t j = (uint64_t)prev_unphased_idx; j < gn; j++) {
+                    if ((int)r.pos >= (int)g->gap_end[go + j - 1] && (int)r.pos <= (int)g->gap_start[go + j]) {
+                        if ((int)j != prev_unphased_idx) { updated = 1; prev_unphased_idx = (int)j; }
+                        break;
+                    }
+                }
+            }
+            if (updated) {       /* get_flip_status_by_idx: flips_onraw indexed by the merged index - 1 */
+                const uint64_t fo = blk->dec_off[c], fn = blk->dec_off[c + 1] - fo;
+                const uint64_t k = (uint64_t)(prev_unphased_idx - 1);
+                need_flip = k < fn ? blk->flip[fo + k] : 0;
+            }
+            /* get_read_new_haplotag (2990-3020) */
+            uint8_t hm;
+            if (pf_tags_get(methphased, 1, qoff, r.qname, 0, &hm) > 0) {
+                hp = hm;
+                if (need_flip) hp ^= 1;
+            } else {
+                hp = hp_raw;
+                if ((hp == 0 || hp == 1) && need_flip) hp ^= 1;
+            }
+        }
+        if (tsv) fprintf(tsv, "%s\t%d\t%d\n", r.qname, hp_tag + 1, hp + 1);
+        if (w) {
+            rc = hp_update(rec, bs, &r, (int64_t)hp + 1, &ob);
+            if (rc) break;
+            uint8_t o4[4];
+            const uint32_t nb = (uint32_t)ob.n;
+            for (int i = 0; i < 4; i++) o4[i] = (uint8_t)(nb >> (8 * i));
+            if (w->n + 4 + nb > BGZF_BLK) bgzfw_flush(w);          /* bgzf_flush_try */
+            bgzfw_write(w, o4, 4);
+            bgzfw_write(w, ob.p, nb);
+            if (w->err) { rc = w->err; break; }
+            const int mapped = !(r.flag & 4);
+            const int64_t end = r.pos + ((mapped && rlen) ? (int64_t)rlen : 1);      /* bam_endpos */
+            bai_push(&X, r.tid, r.pos, end, bgzfw_tell(w), mapped);
+            if (X.err) { rc = X.err; break; }
+        }
+        nrec++;
+    }
+    if (!rc && w) {
+        rc = bgzfw_flush(w);
+        if (!rc) bai_finish(&X, bgzfw_tell(w));
+        if (!rc && fwrite(BGZF_EOF, 1, sizeof BGZF_EOF, w->f) != sizeof BGZF_EOF) rc = -1;
+    }
+    if (w) { if (w->f && fclose(w->f) && !rc) rc = -1; free(w); }
+    if (!rc && bam_out && bai_out) rc = bai_write(&X, bai_out);
+    if (tsv && fclose(tsv) && !rc) rc = -1;
+    for (int32_t t = 0; t < X.n_ref; t++) { free(X.r[t].c); free(X.r[t].lin); }
+    free(X.r);
+    if (names) for (int32_t t = 0; t < n_ref; t++) free(names[t]);
+    free(names); free(vcf_of_tid); free(rec); free(hdr); free(ob.p);
+    if (z) { bgzf_close(z); free(z); }
+    if (n_records) *n_records = nrec;
+    return rc;
+}

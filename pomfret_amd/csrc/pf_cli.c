@@ -4,14 +4,17 @@
  * blockjoin.c main_blockjoin 4643 / main_methreport 4901), running the
  * per-window hot path on the MI355X through libpomfret_amd.so.
  *
- *   pomfret-amd methphase -o out --vcf phased.vcf.gz [-c 60] [-u] [-t N] [--gpus G] reads.bam
+ *   pomfret-amd methphase -o out --vcf phased.vcf.gz [-c 60] [-u] [-t N] [--write-bam] [--gpus G] reads.bam
  *   pomfret-amd report    -o out --vcf phased.vcf.gz [-c C] [--chunk-size S --chunk-stride D] reads.bam
+ *   pomfret-amd varhaptag -o out.bam in.vcf in.bam
  *
- * Options and defaults follow the reference's cliopt_t (cli.c:47-75); the
- * -c arithmetic (cov/10, cov/4) and the order-dependent -n override are kept.
- * Added: --gpus G (GPUs driven by this process; default all visible) and
- * --job-windows W (windows per device job).  --gtf / --tsv phase-block
- * inputs and --write-bam are not implemented (an error, not a silent skip).
+ * Options and defaults follow the reference's cliopt_t (cli.c:47-75) and
+ * cliopt_haptag_t (cli.c:332-343); the -c arithmetic (cov/10, cov/4), the
+ * order-dependent -n override and varhaptag's --write-bam (which there turns
+ * the BAM output OFF, cli.c:416) are kept.  Added: --gpus G (GPUs driven by
+ * this process; default all visible) and --job-windows W (windows per device
+ * job).  --gtf / --tsv phase-block inputs are not implemented (an error, not
+ * a silent skip).
  */
 #include <getopt.h>
 #include <stdio.h>
@@ -34,6 +37,7 @@ static void help_main(void) {
     fprintf(stderr, "  methphase  Given aligned reads with methylation calls in bam\n");
     fprintf(stderr, "             and exiting phase blocks, try to use methylation to\n");
     fprintf(stderr, "             phase the unphased regions (on the GPU).\n");
+    fprintf(stderr, "  varhaptag  Haplotag reads from phased variants (on the GPU).\n");
     fprintf(stderr, "  report     Given aligned reads in bam and a phased vcf, sample\n");
     fprintf(stderr, "             intervals within phase blocks, pretend they are phase gaps\n");
     fprintf(stderr, "             and report whether meth-phasing would generate correct \n");
@@ -53,6 +57,7 @@ static void help_methphase(const char *prefix) {
                     "               with phased variants in vcf first (on the GPU).\n");
     fprintf(stderr, "  -t     [opt] Host threads fetching reads, per GPU. [1]\n");
     fprintf(stderr, "  --output-tsv [opt] Also write {prefix}.mp.tsv.\n");
+    fprintf(stderr, "  --write-bam  [opt] Also write {prefix}.mp.bam (+ .bai) with the new HP tags.\n");
     fprintf(stderr, "  --gpus [opt] GPUs to use. [all visible]\n");
 }
 
@@ -152,10 +157,55 @@ static int sancheck(cli_t *c) {                       /* sancheck_cliopt, cli.c:
         fprintf(stderr, "[E::pomfret-amd] --gtf / --tsv phase-block inputs are not implemented; use --vcf\n");
         return 1;
     }
-    if (c->out_bam) {
-        fprintf(stderr, "[E::pomfret-amd] --write-bam is not implemented\n");
+    return 0;
+}
+
+/* varhaptag: parse_cli_varhaptag (cli.c:386-446): -o out.bam, -t, -v,
+ * --write-bam (disables the BAM), positional in.vcf then in.bam */
+static int varhaptag(int argc, char **argv) {
+    const char *out = "pomfret_varhaptag", *vcf = NULL, *bam = NULL;
+    int threads = 1, verbose = 0, write_bam = 1, gpus = 0, o;
+    optind = 1;
+    while ((o = getopt_long(argc, argv, "ho:t:r:v", longopts, NULL)) >= 0) {
+        switch (o) {
+        case 'h': case O_HELP:
+            fprintf(stderr, "Usage: pomfret-amd varhaptag [-t threads] -o out.bam in.vcf in.bam 2>log\n");
+            return 1;
+        case 'o': out = optarg; break;
+        case 't': threads = atoi(optarg); break;
+        case 'v': verbose = 1; break;
+        case 'r': break;
+        case O_WBAM: write_bam = 0; break;
+        case O_GPUS: gpus = atoi(optarg); break;
+        default:
+            fprintf(stderr, "[E::parse_cli_varhaptag] unknown or incomplete option \"%s\"\n", argv[optind - 1]);
+            return 1;
+        }
+    }
+    for (int i = optind; i < argc; i++) {
+        if (!vcf) vcf = argv[i];
+        else if (!bam) bam = argv[i];
+        else { fprintf(stderr, "[E::parse_cli_varhaptag] too many positional arguments\n"); return 1; }
+    }
+    if (!vcf || !bam) { fprintf(stderr, "[E::sancheck_cliopt_varhaptag] need a vcf and a bam\n"); return 1; }
+    if (threads < 1) threads = 1;
+    pf_methphase_opts_t op;
+    memset(&op, 0, sizeof op);
+    op.mode = PF_MODE_VARHAPTAG;
+    op.bam_path = bam;
+    op.vcf_path = vcf;
+    op.out_prefix = out;
+    op.write_bam = write_bam;
+    op.threads = threads;
+    op.n_devices = gpus;
+    op.verbose = verbose;
+    pf_mp_plan_t *p = NULL;
+    const int rc = pf_methphase_main(&op, &p);
+    if (rc) {
+        fprintf(stderr, "[E::main] varhaptag failed: %s (%d)\n", pf_strerror(rc), rc);
         return 1;
     }
+    pf_mp_free(p);
     return 0;
 }
 
@@ -168,6 +218,7 @@ int main(int argc, char **argv) {
         help_main();
         return 1;
     }
+    if (!strcmp(argv[1], "varhaptag")) return varhaptag(argc - 1, argv + 1);
     const int report = !strcmp(argv[1], "report");
     if (!report && strcmp(argv[1], "methphase")) {
         fprintf(stderr, "[E::main] unknown subcommand: %s\n", argv[1]);
@@ -197,6 +248,7 @@ int main(int argc, char **argv) {
     o.load.qual_hi = c.hi;
     o.untagged = c.untagged;
     o.write_tsv = c.out_tsv;
+    o.write_bam = c.out_bam;
     o.chunk_size = c.chunk_size;
     o.chunk_stride = c.chunk_stride;
     o.threads = c.threads;

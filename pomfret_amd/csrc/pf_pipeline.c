@@ -503,7 +503,13 @@ const pf_tags_t *pf_mp_qname_hp(const pf_mp_plan_t *p) { return p ? p->qname_hp 
 const pf_tags_t *pf_mp_raw_hp(const pf_mp_plan_t *p) { return p && p->o.untagged ? p->raw : NULL; }
 
 int pf_mp_decisions(const pf_mp_plan_t *p, const int8_t **dec, uint32_t *n, uint32_t *n_limit) {
-    if (!p || !p->finished) return PF_ERR_ARG;
+    if (!p) return PF_ERR_ARG;
+    if (!p->finished) {                         /* varhaptag: no windows were run */
+        if (dec) *dec = NULL;
+        if (n) *n = 0;
+        if (n_limit) *n_limit = 0;
+        return PF_OK;
+    }
     if (dec) *dec = p->decision;
     if (n) *n = p->n_windows;
     if (n_limit) *n_limit = p->n_limit;
@@ -946,7 +952,35 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
         rc = pf_write_vcf(p->vcf_path, p->gaps, p->blocks, &res, fn, NULL);
         if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] vcf written.\n");
     }
+    if (!rc && p->o.write_bam) {                    /* output_modify_bam + sam_index_build3 (4719-4731) */
+        char *fb = (char *)malloc(L + 8);
+        if (!fb) rc = PF_ERR_NOMEM;
+        if (!rc) {
+            snprintf(fn, L, "%s.mp.bam", p->out_prefix);
+            snprintf(fb, L + 8, "%s.mp.bam.bai", p->out_prefix);
+            rc = pf_retag_bam(p->bam_path, fn, fb, NULL, PF_RETAG_METHPHASE, p->gaps, p->blocks, p->qname_hp,
+                              p->o.untagged ? p->raw : NULL, -1, NULL);
+            if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] bam written and indexed.\n");
+        }
+        free(fb);
+    }
     free(roff); free(rpos); free(rhap); free(fn);
+    return rc;
+}
+
+/* varhaptag (main_varhaptag, 4737-4836): the -u pre-pass on the devices,
+ * then {out}.varhaptag.tsv and, with write_bam, the retagged {out} + .bai */
+static int varhaptag_outputs(pf_mp_plan_t *p) {
+    const size_t L = strlen(p->out_prefix) + 32;
+    char *ft = (char *)malloc(L), *fb = (char *)malloc(L);
+    int rc = (!ft || !fb) ? PF_ERR_NOMEM : 0;
+    if (!rc) {
+        snprintf(ft, L, "%s.varhaptag.tsv", p->out_prefix);
+        snprintf(fb, L, "%s.bai", p->out_prefix);
+        rc = pf_retag_bam(p->bam_path, p->o.write_bam ? p->out_prefix : NULL, p->o.write_bam ? fb : NULL, ft,
+                          PF_RETAG_VARHAPTAG, NULL, NULL, NULL, p->raw, -1, NULL);
+    }
+    free(ft); free(fb);
     return rc;
 }
 
@@ -1134,7 +1168,21 @@ int pf_methphase_main(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     if (!o || !out) return PF_ERR_ARG;
     *out = NULL;
     if (o->world > 1) return PF_ERR_ARG;           /* multi-process runs use the pf_mp_* steps */
-    if (o->write_bam) return PF_ERR_UNSUPPORTED;
+    if (o->mode == PF_MODE_VARHAPTAG) {
+        if (!o->out_prefix) return PF_ERR_ARG;
+        pf_methphase_opts_t v = *o;
+        v.mode = PF_MODE_METHPHASE;
+        v.untagged = 1;
+        v.cov_for_selection = 1;                   /* no coverage estimate: no window runs */
+        pf_mp_plan_t *p = NULL;
+        int rc = pf_mp_plan(&v, &p);
+        if (!rc) rc = run_on_devices(p, &v, PF_JOB_HAPTAG);
+        if (!rc) rc = pf_mp_merge_raw(p);
+        if (!rc) rc = varhaptag_outputs(p);
+        if (rc) { pf_mp_free(p); return rc; }
+        *out = p;
+        return PF_OK;
+    }
     pf_mp_plan_t *p = NULL;
     int rc = pf_mp_plan(o, &p);
     if (!rc && o->untagged) {

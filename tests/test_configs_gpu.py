@@ -272,3 +272,38 @@ def test_t6_range_wrap_gpu(oracle_lib, gpu_ctx):
         assert np.array_equal(getattr(out, f), getattr(ref, f)), f
     assert out.dir_join[0, 1] == -1
     db.free()
+
+
+def test_cli_write_bam_and_varhaptag(oracle_lib, tmp_path):
+    """f4 on the device: `methphase -u --write-bam` writes {prefix}.mp.bam +
+    .bai whose HP tags follow output_modify_bam over the oracle pipeline's
+    tables (tests/test_bamw.py restates it), and `varhaptag -o out.bam vcf bam`
+    writes the K4 tags of the oracle's -u pre-pass (main_varhaptag)."""
+    from pomfret_amd import Config, _lib
+    from tests.test_bamw import _restate_methphase, aux_update_int, hp_tag_raw, parse_bam, qname
+    aln, recs, bam, vcf = fx.untagged(tmp_path, n_windows=2, coverage=30, len_scale=0.6)
+    out = str(tmp_path / "wb")
+    r = _cli("methphase", "-u", "-c", "30", "-o", out, "--vcf", vcf, "--write-bam", bam)
+    assert r.returncode == 0, r.stderr
+    ref = methphase_files_oracle(bam, vcf, Config.from_coverage(30, given=True), untagged=True,
+                                 recs_by_contig={"chrS": recs})
+    assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+    g = _lib.Gaps(vcf)
+    b = _lib.Blocks(g, ref["decision"])
+    _, bodies_in, _, _ = parse_bam(bam)
+    _, bodies_out, _, _ = parse_bam(out + ".mp.bam")
+    hp = _restate_methphase(bodies_in, [0] * len(bodies_in), g.contigs(), b.contigs(), ref["qname_hp"],
+                            ref["raw_hp"], tid_names=("chrS",))
+    assert len(bodies_out) == len(bodies_in)
+    for bi, bo, h in zip(bodies_in, bodies_out, hp):
+        assert bo == aux_update_int(bi, h + 1)
+    assert os.path.getsize(out + ".mp.bam.bai") > 0
+    vb = str(tmp_path / "vh.bam")
+    r = _cli("varhaptag", "-o", vb, vcf, bam)
+    assert r.returncode == 0, r.stderr
+    lines = open(vb + ".varhaptag.tsv").read().split("\n")[1:-1]
+    _, bodies_v, _, _ = parse_bam(vb)
+    for bi, bo, line in zip(bodies_in, bodies_v, lines):
+        h = ref["raw_hp"].get(qname(bi), 254)
+        assert line == f"{qname(bi)}\t{hp_tag_raw(bi) + 1}\t{h + 1}"
+        assert bo == aux_update_int(bi, h + 1)
