@@ -52,6 +52,7 @@ struct pf_ctx {
     int have_times;
     int k3_block;             /* last run's main greedy kernel: 1 the 256-thread build, 0 the one-wave build */
     float haptag_ms;          /* last pf_haptag_reads kernel time */
+    const char *haptag_name;  /* and the kernel that ran */
     int have_haptag;
     void *pin = nullptr;      /* pinned staging for large uploads (grown on demand) */
     size_t pin_cap = 0;
@@ -1127,7 +1128,9 @@ extern "C" int pf_batch_prof(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
     return PF_OK;
 }
 
-extern "C" void pf_ctx_set_haptag_ms(pf_ctx *c, float ms) { c->haptag_ms = ms; c->have_haptag = 1; }
+extern "C" void pf_ctx_set_haptag_ms(pf_ctx *c, float ms, const char *name) {
+    c->haptag_ms = ms; c->have_haptag = 1; c->haptag_name = name;
+}
 
 extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n) {
     if (!ctx || !n) return PF_ERR_ARG;
@@ -1138,7 +1141,7 @@ extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms
             if (names) names[i] = (i == 4 && ctx->k3_block) ? "pf_k3_greedy" : k_names[i];
             if (ms) ms[i] = ctx->have_times ? ctx->last_ms[i] : -1.0f;
         } else {
-            if (names) names[i] = "pf_k4_haptag";
+            if (names) names[i] = ctx->haptag_name;
             if (ms) ms[i] = ctx->haptag_ms;
         }
     }

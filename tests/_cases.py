@@ -182,3 +182,94 @@ def t6_range_wrap():
         h = i % 2
         reads.append((120_000 + 700 * i, 198_000, h, [(int(p), int(meth[k] ^ h)) for k, p in enumerate(sites)]))
     return _batch_from_reads(s, e, reads)
+
+
+# ---------------------------------------------------------------------------
+# -u pre-pass edge cases (reference blockjoin.c:1545-1840) for the wave kernel:
+# MD strings the serial machine treats specially, CIGARs with many ops, known
+# tables with same-position runs.
+def _rand_md(rng, n_tok):
+    """MD-like string: numbers (some with leading zeros / many digits),
+    mismatch letters (runs of 1-3), '^' runs of 1-150 letters, some holding a
+    second '^' (absorbed into the run, :1641-1652), and lowercase / N / U."""
+    letters = np.frombuffer(b"ACGTNUacgtnu", np.uint8)
+    out = []
+    kind = int(rng.integers(0, 3))          # first token: number, letter or '^'
+    for _ in range(n_tok):
+        if kind == 0:
+            v = int(rng.integers(0, 400)) if rng.random() < 0.9 else int(rng.integers(0, 10 ** 6))
+            s = str(v)
+            if rng.random() < 0.05:
+                s = "0" * int(rng.integers(1, 4)) + s
+            out.append(s)
+            kind = int(rng.integers(1, 3))
+        elif kind == 1:
+            n = int(rng.integers(1, 4))
+            out.append(bytes(letters[rng.integers(0, 12, n)]).decode())
+            kind = 0 if rng.random() < 0.8 else int(rng.integers(1, 3))
+        else:
+            n = int(rng.integers(1, 150)) if rng.random() < 0.2 else int(rng.integers(1, 4))
+            body = bytearray(letters[rng.integers(0, 12, n)])
+            if rng.random() < 0.1 and n > 1:
+                body[int(rng.integers(1, n))] = ord("^")
+            out.append("^" + body.decode())
+            kind = 0 if rng.random() < 0.9 else 1
+    return "".join(out)
+
+
+def u_quirks(seed=5, n_reads=300):
+    """make_u_batch reads with a third of the MD strings replaced by _rand_md,
+    a sixth of the CIGARs split into many short M/I/N/H/P ops (>64 ops), and
+    extra known entries making 2- and 3-long runs at one position."""
+    from pomfret_amd.abi import KnownVars, ReadAlnBatch
+    from pomfret_amd.synth_u import USpec, make_u_batch
+    known, reads, _ = make_u_batch(USpec(n_reads=n_reads, ref_len=200_000, mean_len=6000,
+                                         var_every=200, indel_frac=0.3, seed=seed))
+    rng = np.random.default_rng(seed)
+    # known: duplicate ~15% of the entries (one or two extra copies at the same
+    # position, alternating haptag and chars), keeping VCF order
+    kp, kl, ko, kh, kc, koff = [], [], [], [], [], [0]
+    for i in range(len(known.pos)):
+        reps = 1 + (int(rng.integers(1, 3)) if rng.random() < 0.15 else 0)
+        for c in range(reps):
+            kp.append(int(known.pos[i])); kl.append(int(known.len[i])); ko.append(int(known.op[i]))
+            kh.append(int(known.haptag[i]) ^ (c & 1))
+            ch = known.chars[known.char_off[i]:known.char_off[i + 1]].tolist()
+            if c:
+                ch = [(x + c) % 4 for x in ch]
+            kc += ch
+            koff.append(len(kc))
+    known = KnownVars(pos=np.array(kp), len=np.array(kl), op=np.array(ko), haptag=np.array(kh),
+                      char_off=np.array(koff), chars=np.array(kc, np.uint8))
+    cig, cig_off, md, md_off = [], [0], [], [0]
+    for r in range(reads.n_reads):
+        c = reads.cigar[reads.cigar_off[r]:reads.cigar_off[r + 1]].tolist()
+        m = bytes(reads.md[reads.md_off[r]:reads.md_off[r + 1]])
+        u = rng.random()
+        if u < 0.33:
+            m = _rand_md(rng, int(rng.integers(1, 400))).encode()
+        elif u < 0.5:
+            nc = []
+            for w in c:
+                op, ln = w & 0xf, w >> 4
+                if op == 0 and ln > 8:
+                    while ln > 0:
+                        k = min(ln, int(rng.integers(1, 6)))
+                        nc.append(k << 4 | 0)
+                        ln -= k
+                        x = rng.random()
+                        if x < 0.3:
+                            nc.append(int(rng.integers(1, 4)) << 4 | 1)
+                        elif x < 0.35:
+                            nc.append(int(rng.integers(1, 3)) << 4 | int(rng.choice([3, 5, 6])))
+                else:
+                    nc.append(w)
+            c = nc
+        cig += c
+        cig_off.append(len(cig))
+        md.append(np.frombuffer(m, np.uint8))
+        md_off.append(md_off[-1] + len(m))
+    reads = ReadAlnBatch(start=reads.start, end=reads.end, cigar_off=np.array(cig_off),
+                         cigar=np.array(cig, np.uint32), seq_off=reads.seq_off, seq_len=reads.seq_len,
+                         seq=reads.seq, md_off=np.array(md_off), md=np.concatenate(md))
+    return known, reads
