@@ -287,6 +287,18 @@ int  pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *known,
  * mismatches (0 expected). */
 int  pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches);
 
+/* Device BGZF inflate (the decompression of htslib's bgzf_read_block,
+ * bgzf.c, which load_reads_given_interval reaches through sam_itr_next at
+ * blockjoin.c:1076): every BGZF block of comp[0, comp_len) (whole blocks,
+ * concatenated as in a BAM file) is inflated on the device, one wavefront per
+ * block, and its CRC32 and ISIZE checked; the output (blocks back to back) is
+ * copied to out.  block_status[i] (when given, i < status_cap) receives block
+ * i's PF_INF_* code (pf_ingest.h; 0 = ok); kernel_ms the inflate kernel time.
+ * PF_ERR_ARG for a malformed block table, an undersized out, or any block
+ * that failed. */
+int  pf_bgzf_inflate(pf_ctx_t *ctx, const uint8_t *comp, uint64_t comp_len, uint8_t *out, uint64_t out_cap,
+                     uint64_t *out_len, uint32_t *block_status, uint32_t status_cap, float *kernel_ms);
+
 /* ------------------------------------------------------------------ */
 /* Window definition (host side).                                      */
 

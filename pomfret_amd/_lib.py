@@ -68,6 +68,8 @@ def lib():
         L.pf_batch_debug_calls.argtypes = [C.c_void_p] + [C.c_void_p] * 5 + [C.c_uint64]
         L.pf_batch_debug_calls.restype = C.c_int64
         L.pf_batch_load_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.pf_bgzf_inflate.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                      C.POINTER(C.c_uint64), C.c_void_p, C.c_uint32, C.POINTER(C.c_float)]
         if hasattr(L, "pf_haptag_reads"):
             L.pf_haptag_reads.argtypes = [C.c_void_p, C.POINTER(PfKnownVars),
                                           C.POINTER(PfReadAlnBatch), C.c_void_p]
@@ -295,6 +297,22 @@ class Context:
         """Record-level batch (pf_batch_upload_aln): K0 loads the reads on
         the device in every run."""
         return DeviceBatch(self, cfg, aln, lcfg=lcfg or LoadConfig())
+
+    def bgzf_inflate(self, comp: bytes, out_cap: int = None):
+        """Inflate every BGZF block of `comp` on the device (pf_bgzf_inflate).
+        Returns (output bytes, per-block status array, inflate kernel ms);
+        raises PomfretError when any block fails."""
+        comp = np.frombuffer(bytes(comp), np.uint8)
+        cap = out_cap if out_cap is not None else max(1, 65536 * (comp.size // 28 + 1))
+        out = np.empty(cap, np.uint8)
+        n = C.c_uint64()
+        st = np.zeros(comp.size // 26 + 1, np.uint32)
+        ms = C.c_float()
+        rc = lib().pf_bgzf_inflate(self.handle, comp.ctypes.data, comp.size, out.ctypes.data, cap, C.byref(n),
+                                   st.ctypes.data, st.size, C.byref(ms))
+        self.last_inflate_status = st
+        _check(rc, "pf_bgzf_inflate")
+        return out[:n.value].tobytes(), st, ms.value
 
     def kernel_times(self):
         names = (C.c_char_p * 8)()

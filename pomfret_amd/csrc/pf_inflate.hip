@@ -1,0 +1,566 @@
+// pf_inflate.hip -- BGZF blocks inflated on the device (SURVEY.md 8 f1 moved
+// to the GPU: host BGZF inflate bounds every run from files).
+//
+// A BAM file is a series of BGZF blocks, each an independent raw DEFLATE
+// stream (RFC 1951) of <= 64 KiB output with its CRC32 and size in the
+// footer.  htslib's bgzf_read_block inflates one block at a time and checks
+// the CRC; here every block of a fetch plan is inflated at once, one
+// wavefront per block, into a contiguous arena (block b's output at
+// out_off[b], the prefix sum of the ISIZE fields), so the BAM byte stream of a
+// run of consecutive blocks is contiguous in HBM.
+//
+// Decoder shape (wave64, gfx950):
+//  * the whole wave runs the DEFLATE state machine in lockstep on uniform
+//    values (bit buffer, output position) -- Huffman decoding is inherently
+//    serial within a block, the parallelism is across blocks (thousands of
+//    waves in flight);
+//  * the compressed input is held lane-distributed: lane k of `cur` holds
+//    dword k of the current 256-byte input window, `nxt` the next one,
+//    prefetched one window ahead; the bit reader takes dwords with readlane;
+//  * Huffman tables in LDS (per wave, ~3.9 KB): a 10-bit root table for
+//    literal/length codes and an 8-bit one for distances (symbol | length << 9,
+//    broadcast reads); codes longer than the root (rare) take a canonical
+//    walk over the per-length counts;
+//  * output is assembled lane-distributed in 256-byte chunks aligned to the
+//    arena (lane k holds bytes 4k..4k+3 of the chunk) and flushed with one
+//    coalesced store per chunk; a match only records its bytes' sources, and
+//    the chunk's flush loads every source in older output at once (after a
+//    workgroup-scope fence that makes the flushed chunks visible) and resolves
+//    in-chunk sources with ds_bpermute rounds;
+//  * measured (tests/test_inflate_gpu.py, BAM-like blocks): the decode is
+//    bound by scalar issue (one SALU instruction per 4 cycles per SIMD, ~45
+//    per symbol), about 12 GB/s of output on MI355X;
+//  * table construction is lane-parallel (counts by ballot, ranks by ballot
+//    prefix, root fill one symbol per lane).
+// A second kernel checks each block's CRC32 (reflected 0xEDB88320, zlib's
+// crc32) and ISIZE, as htslib does; any malformed stream, size or CRC
+// mismatch sets the block's status word and the host fails the fetch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "pf_ingest.h"
+
+#define DEV static __device__ __forceinline__
+#define INF_LROOT 10u
+#define INF_DROOT 8u
+#define INF_WAVES 4u
+
+DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+DEV uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
+DEV uint64_t uni64(uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); }
+DEV void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__constant__ uint16_t k_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
+                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t k_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t k_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193,
+                                     257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t k_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t k_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+struct InfLds {                         // one wave's tables
+    uint16_t lroot[1u << INF_LROOT];
+    uint16_t droot[1u << INF_DROOT];
+    uint16_t lsym[288];                 // symbols sorted by (length, value): canonical order
+    uint16_t dsym[32];
+    uint16_t cnt[2][16];                // codes per length (litlen, dist)
+    uint16_t off[2][16];                // first sorted index of each length
+    uint8_t lens[320];                  // code lengths: HLIT litlen then HDIST dist
+    uint16_t clroot[128];               // code-length code (max 7 bits: the root covers it)
+    uint16_t cnt_cl[16], off_cl[16];
+    uint16_t clsym[19];
+    uint32_t ring[128];                 // input windows (bit reader)
+};
+
+// --------------------------------------------------------------------------
+// bit reader over an LDS ring of two 256-byte input windows per wave: window
+// j sits in slot j & 1; entering window j waits for its load (issued when
+// window j-1 was entered) and issues window j+1's into the other slot with a
+// direct global->LDS load, so the wait is a full window after the issue.
+#define VMCNT0 0x0F70                   // s_waitcnt vmcnt(0) (gfx9 encoding, other counters at max)
+struct Bits {
+    uint64_t buf;
+    uint32_t cnt;
+    uint32_t rd;          // next dword (from the aligned base) to read
+    uint32_t lim;         // dwords that may be read (payload + slack)
+    uint32_t over;        // read past the payload
+    const uint32_t *src;  // aligned base
+    uint32_t *ring;       // 128 dwords of LDS
+};
+
+DEV void bits_issue(Bits &b, uint32_t j, uint32_t lane) {       // window j -> slot j & 1
+    uint32_t k = j * 64 + lane;
+    if (k >= b.lim) k = b.lim - 1;            // past the payload: any valid dword (never decoded)
+    __builtin_amdgcn_global_load_lds((const void *)(b.src + k),
+                                     (__attribute__((address_space(3))) void *)(b.ring + (j & 1u) * 64), 4, 0, 0);
+}
+
+DEV void bits_fill(Bits &b, uint32_t lane) {
+    b.cnt = uni(b.cnt);
+    b.buf = uni64(b.buf);
+    b.rd = uni(b.rd);
+    while (b.cnt <= 32) {
+        if ((b.rd & 63u) == 0) {
+            __builtin_amdgcn_s_waitcnt(VMCNT0);
+            wsync();
+            bits_issue(b, (b.rd >> 6) + 1, lane);
+        }
+        const uint32_t w = uni(b.ring[b.rd & 127u]);
+        b.buf |= (uint64_t)w << b.cnt;
+        b.cnt += 32;
+        b.rd++;
+        if (b.rd > b.lim) b.over = 1;
+    }
+}
+DEV uint32_t bits_get(Bits &b, uint32_t n) {       // n <= 32, after a fill covering it
+    const uint32_t v = (uint32_t)b.buf & (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u));
+    b.buf >>= n;
+    b.cnt -= n;
+    return v;
+}
+
+// --------------------------------------------------------------------------
+// table construction.  lens[0..n) -> per-length counts, sorted symbols and a
+// root table of `root` bits indexed by the bit-reversed code.  Returns 0 on
+// success, 1 for an over-subscribed set or an incomplete one (zlib's
+// inflate_table: incomplete only for a single length-1 code, never for the
+// code-length code; an empty set builds a table every lookup of which fails).
+DEV uint32_t build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint16_t *rt, uint16_t *sym,
+                         uint16_t *cnt, uint16_t *off, uint32_t lane, bool is_codes) {
+    // counts per length (uniform, 15 ballots per 64 symbols)
+    uint32_t c[16];
+#pragma unroll
+    for (uint32_t L = 0; L < 16; L++) c[L] = 0;
+    for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        const uint32_t l = s < n ? lens[s] : 0u;
+#pragma unroll
+        for (uint32_t L = 1; L < 16; L++) c[L] += (uint32_t)__popcll(__ballot(l == L));
+    }
+    uint32_t maxl = 0;
+    int32_t left = 1;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t L = 1; L < 16; L++) {
+        left <<= 1;
+        left -= (int32_t)c[L];
+        if (left < 0) bad = true;
+        if (c[L]) maxl = L;
+    }
+    if (bad) return 1;
+    if (maxl != 0 && left > 0 && (is_codes || maxl != 1)) return 1;
+    // offsets and first codes
+    uint32_t o[16], first[16];
+    o[0] = 0; o[1] = 0;
+    first[0] = 0;
+    uint32_t code = 0;
+#pragma unroll
+    for (uint32_t L = 1; L < 16; L++) {
+        code = (code + (L > 1 ? c[L - 1] : 0u)) << 1;
+        first[L] = code;
+        if (L > 1) o[L] = o[L - 1] + c[L - 1];
+    }
+    if (lane < 16) { cnt[lane] = 0; off[lane] = 0; }
+    wsync();
+#pragma unroll
+    for (uint32_t L = 1; L < 16; L++)
+        if (lane == L) { cnt[lane] = (uint16_t)c[L]; off[lane] = (uint16_t)o[L]; }
+    // clear the root table
+    const uint32_t rn = 1u << root;
+    for (uint32_t i = lane; i < rn; i += 64) rt[i] = 0;
+    wsync();
+    // ranks within each length, in symbol order: sorted symbols + root entries
+    uint32_t base[16];
+#pragma unroll
+    for (uint32_t L = 0; L < 16; L++) base[L] = 0;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint32_t s0 = 0; s0 < n; s0 += 64) {
+        const uint32_t s = s0 + lane;
+        const uint32_t l = s < n ? lens[s] : 0u;
+        uint32_t rank = 0, fc = 0, ol = 0;
+#pragma unroll
+        for (uint32_t L = 1; L < 16; L++) {
+            const uint64_t m = __ballot(l == L);
+            if (l == L) { rank = base[L] + (uint32_t)__popcll(m & lt); fc = first[L]; ol = o[L]; }
+            base[L] += (uint32_t)__popcll(m);
+        }
+        if (l) {
+            sym[ol + rank] = (uint16_t)s;
+            if (l <= root) {
+                const uint32_t cd = fc + rank;
+                const uint32_t rev = __builtin_bitreverse32(cd) >> (32 - l);
+                const uint16_t e = (uint16_t)(s | (l << 9));
+                for (uint32_t k = 0; k < (1u << (root - l)); k++) rt[rev | (k << l)] = e;
+            }
+        }
+    }
+    wsync();
+    return 0;
+}
+
+// canonical decode of a code longer than the root (or any code, from bit 0)
+DEV uint32_t slow_decode(uint64_t bits, const uint16_t *cnt, const uint16_t *off, const uint16_t *sym,
+                         uint32_t &len_out) {
+    uint32_t code = 0, first = 0, index = 0;
+    for (uint32_t L = 1; L < 16; L++) {
+        code |= (uint32_t)(bits >> (L - 1)) & 1u;
+        const uint32_t c = cnt[L];
+        if (code - first < c) {
+            len_out = L;
+            return sym[index + code - first];
+        }
+        index += c;
+        first += c;
+        first <<= 1;
+        code <<= 1;
+    }
+    len_out = 0;
+    return 0xFFFFu;
+}
+
+// --------------------------------------------------------------------------
+// output: 256-byte chunks aligned to the arena, lane k holds bytes 4k..4k+3.
+// A literal sets its byte; a match only records, per byte it covers, the
+// source offset (block-relative).  At the chunk's flush every byte sourced
+// from older output is loaded at once (one memory round trip per chunk, not
+// per match), then bytes sourced inside the chunk are resolved in rounds of
+// ds_bpermute (a source always precedes its byte, so every round resolves at
+// least the earliest pending byte), and the chunk is stored.
+struct Out {
+    uint8_t *arena;
+    uint64_t lo, hi;      // the block's output range [lo, hi)
+    uint64_t cb;          // current chunk's arena address
+    uint64_t a;           // next output address
+    uint32_t val;         // per lane: resolved bytes
+    uint32_t pend;        // per lane: bit i set while byte i waits for its source
+    uint32_t src[4];      // per lane: source offset (from lo) of pending byte i
+    uint32_t any;         // uniform: the chunk has pending bytes
+};
+
+DEV void out_flush(Out &o, uint32_t lane) {
+    if (o.any) {
+        // sources in flushed chunks: make their stores visible, load all at once
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        uint32_t add = 0, done = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint64_t s = o.lo + o.src[i];
+            if (((o.pend >> i) & 1u) && s < o.cb) {
+                add |= (uint32_t)o.arena[s] << (8 * i);
+                done |= 1u << i;
+            }
+        }
+        o.val |= add;
+        o.pend &= ~done;
+        while (__ballot(o.pend != 0)) {
+            const uint32_t v_all = o.val, r_all = ~o.pend & 0xFu;
+            uint32_t nv = o.val, np = o.pend;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const bool pi = (o.pend >> i) & 1u;
+                const uint32_t t = pi ? (uint32_t)(o.lo + o.src[i] - o.cb) : 4 * lane + i;
+                const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((t >> 2) << 2), (int)v_all);
+                const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((t >> 2) << 2), (int)r_all);
+                if (pi && ((r >> (t & 3u)) & 1u)) {
+                    nv |= ((w >> (8 * (t & 3u))) & 0xFFu) << (8 * i);
+                    np &= ~(1u << i);
+                }
+            }
+            o.val = nv;
+            o.pend = np;
+        }
+    }
+    const uint64_t addr = o.cb + 4ull * lane;
+    if (addr >= o.lo && addr + 4 <= o.hi && addr + 4 <= o.a) {
+        *reinterpret_cast<uint32_t *>(o.arena + addr) = o.val;
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint64_t q = addr + i;
+            if (q >= o.lo && q < o.hi && q < o.a) o.arena[q] = (uint8_t)(o.val >> (8 * i));
+        }
+    }
+    o.cb += 256;
+    o.val = 0;
+    o.pend = 0;
+    o.any = 0;
+}
+
+DEV void out_lit(Out &o, uint32_t v, uint32_t lane) {
+    const uint32_t rel = (uint32_t)(o.a - o.cb);
+    if (lane == (rel >> 2)) o.val |= v << (8 * (rel & 3u));
+    o.a++;
+    if (rel == 255) out_flush(o, lane);
+}
+
+// copy L bytes from distance D (D <= bytes already written, checked by the caller)
+DEV void out_match(Out &o, uint32_t L, uint32_t D, uint32_t lane) {
+    const uint64_t ms = o.a, me = o.a + L;
+    while (o.a < me) {
+        const uint64_t seg_end = me < o.cb + 256 ? me : o.cb + 256;
+        uint32_t setp = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint64_t q = o.cb + 4ull * lane + i;
+            if (q >= o.a && q < seg_end) {
+                const uint64_t s = D < L ? ms - D + (uint64_t)((uint32_t)(q - ms) % D) : q - D;
+                o.src[i] = (uint32_t)(s - o.lo);
+                setp |= 1u << i;
+            }
+        }
+        o.pend |= setp;
+        o.any = 1;
+        o.a = seg_end;
+        if (seg_end == o.cb + 256) out_flush(o, lane);
+    }
+}
+
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk,
+                                                            uint8_t *arena, uint32_t *status) {
+    __shared__ InfLds lds_all[INF_WAVES];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t bi = blockIdx.x * INF_WAVES + wv;
+    if (bi >= nblk) return;
+    InfLds &T = lds_all[wv];
+    const pf_bgzf_blk B = blk[bi];
+    const uint64_t in_off = B.in_off;
+    const uint32_t in_len = B.in_len, isize = B.isize;
+
+    Bits b;
+    b.src = reinterpret_cast<const uint32_t *>(in + (in_off & ~3ull));
+    b.lim = (uint32_t)(((in_off & 3u) + in_len + 3) >> 2) + 2;     // + slack: the reader peeks ahead
+    b.rd = 0;
+    b.over = 0;
+    b.ring = T.ring;
+    bits_issue(b, 0, lane);
+    b.buf = 0;
+    b.cnt = 0;
+    bits_fill(b, lane);
+    if ((in_off & 3u) != 0) bits_get(b, 8 * (uint32_t)(in_off & 3u));
+
+    Out o;
+    o.arena = arena;
+    o.lo = B.out_off;
+    o.hi = B.out_off + isize;
+    o.cb = B.out_off & ~255ull;
+    o.a = B.out_off;
+    o.val = 0;
+    o.pend = 0;
+    o.any = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) o.src[i] = 0;
+
+    uint32_t err = 0, final_blk = 0;
+    while (!final_blk && !err) {
+        err = uni(err);
+        final_blk = uni(final_blk);
+        bits_fill(b, lane);
+        final_blk = bits_get(b, 1);
+        const uint32_t type = bits_get(b, 2);
+        if (type == 0) {                                   // stored
+            bits_get(b, b.cnt & 7u);
+            bits_fill(b, lane);
+            const uint32_t len = bits_get(b, 16), nlen = bits_get(b, 16);
+            if ((len ^ 0xFFFFu) != nlen) { err = PF_INF_ESTORED; break; }
+            if (o.a + len > o.hi) { err = PF_INF_ESIZE; break; }
+            for (uint32_t i = 0; i < len; i++) {
+                bits_fill(b, lane);
+                out_lit(o, bits_get(b, 8), lane);
+            }
+            if (b.over) { err = PF_INF_EINPUT; break; }
+            continue;
+        }
+        if (type == 3) { err = PF_INF_ETYPE; break; }
+        uint32_t nlit = 288, ndist = 32;
+        if (type == 1) {                                   // fixed codes
+            for (uint32_t s = lane; s < 320; s += 64)
+                T.lens[s] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5);
+            wsync();
+        } else {                                           // dynamic: code lengths first
+            bits_fill(b, lane);
+            nlit = bits_get(b, 5) + 257;
+            ndist = bits_get(b, 5) + 1;
+            const uint32_t ncl = bits_get(b, 4) + 4;
+            if (nlit > 286 || ndist > 30) { err = PF_INF_ECODES; break; }
+            uint64_t clbits = 0;                           // up to 19 x 3 bits
+            bits_fill(b, lane);
+            const uint32_t n1 = ncl < 10 ? ncl : 10;
+            clbits = bits_get(b, 3 * n1);
+            if (ncl > 10) { bits_fill(b, lane); clbits |= (uint64_t)bits_get(b, 3 * (ncl - 10)) << 30; }
+            if (lane < 19) {
+                uint32_t l = 0;
+                for (uint32_t j = 0; j < ncl; j++)
+                    if (k_clord[j] == lane) l = (uint32_t)(clbits >> (3 * j)) & 7u;
+                T.lens[lane] = (uint8_t)l;
+            }
+            wsync();
+            if (build_table(T.lens, 19, 7, T.clroot, T.clsym, T.cnt_cl, T.off_cl, lane, true)) {
+                err = PF_INF_ECODES;
+                break;
+            }
+            // the litlen + dist code lengths (serial, uniform): litlen at
+            // lens[0..nlit), dist at lens[288..288+ndist), the rest 0
+            const uint32_t total = nlit + ndist;
+            uint32_t i = 0, prev = 0;
+            for (uint32_t q = lane; q < 320; q += 64) T.lens[q] = 0;
+            wsync();
+            while (i < total) {
+                bits_fill(b, lane);
+                const uint32_t e = uni(T.clroot[(uint32_t)b.buf & 127u]);
+                const uint32_t l = e >> 9, s = e & 511u;
+                if (l == 0) { err = PF_INF_ECODES; break; }
+                bits_get(b, l);
+                uint32_t rep = 1, val = s;
+                if (s == 16) {
+                    if (i == 0) { err = PF_INF_ECODES; break; }
+                    rep = 3 + bits_get(b, 2);
+                    val = prev;
+                } else if (s == 17) {
+                    rep = 3 + bits_get(b, 3);
+                    val = 0;
+                } else if (s == 18) {
+                    rep = 11 + bits_get(b, 7);
+                    val = 0;
+                }
+                if (i + rep > total) { err = PF_INF_ECODES; break; }
+                if (val)
+                    for (uint32_t j = lane; j < rep; j += 64) {
+                        const uint32_t q = i + j;
+                        T.lens[q < nlit ? q : 288 + q - nlit] = (uint8_t)val;
+                    }
+                i += rep;
+                prev = val;
+                if (b.over) { err = PF_INF_EINPUT; break; }
+            }
+            if (err) break;
+            wsync();
+            if (T.lens[256] == 0) { err = PF_INF_ECODES; break; }   // no end-of-block code
+        }
+        if (build_table(T.lens, nlit, INF_LROOT, T.lroot, T.lsym, T.cnt[0], T.off[0], lane, false) ||
+            build_table(T.lens + 288, ndist, INF_DROOT, T.droot, T.dsym, T.cnt[1], T.off[1], lane, false)) {
+            err = PF_INF_ECODES;
+            break;
+        }
+        // ---- the block's symbols
+        for (;;) {
+            o.a = uni64(o.a);
+            o.cb = uni64(o.cb);
+            o.any = uni(o.any);
+            b.over = uni(b.over);
+            bits_fill(b, lane);
+            uint32_t e = uni(T.lroot[(uint32_t)b.buf & ((1u << INF_LROOT) - 1u)]);
+            uint32_t l = e >> 9, s = e & 511u;
+            if (l == 0) {
+                s = slow_decode(b.buf, T.cnt[0], T.off[0], T.lsym, l);
+                s = uni(s);
+                l = uni(l);
+                if (l == 0) { err = PF_INF_ECODES; break; }
+            }
+            bits_get(b, l);
+            if (s < 256) {
+                if (o.a >= o.hi) { err = PF_INF_ESIZE; break; }
+                out_lit(o, s, lane);
+                continue;
+            }
+            if (s == 256) break;
+            const uint32_t li = s - 257;
+            if (li >= 29) { err = PF_INF_ECODES; break; }
+            const uint32_t L = k_lbase[li] + bits_get(b, k_lext[li]);
+            bits_fill(b, lane);
+            e = uni(T.droot[(uint32_t)b.buf & ((1u << INF_DROOT) - 1u)]);
+            l = e >> 9;
+            s = e & 511u;
+            if (l == 0) {
+                s = slow_decode(b.buf, T.cnt[1], T.off[1], T.dsym, l);
+                s = uni(s);
+                l = uni(l);
+                if (l == 0) { err = PF_INF_ECODES; break; }
+            }
+            bits_get(b, l);
+            if (s >= 30) { err = PF_INF_ECODES; break; }
+            const uint32_t D = k_dbase[s] + bits_get(b, k_dext[s]);
+            if ((uint64_t)D > o.a - o.lo) { err = PF_INF_EDIST; break; }
+            if (o.a + L > o.hi) { err = PF_INF_ESIZE; break; }
+            out_match(o, L, D, lane);
+            if (b.over) { err = PF_INF_EINPUT; break; }
+        }
+        if (b.over && !err) err = PF_INF_EINPUT;
+    }
+    if (!err && o.a != o.hi) err = PF_INF_ESIZE;
+    // the partial last chunk (bytes below o.a only)
+    if (o.a > o.cb) out_flush(o, lane);
+    if (lane == 0) status[bi] = err;
+}
+
+// --------------------------------------------------------------------------
+// CRC32 of each block's output: lane k takes bytes [k*S, (k+1)*S) of the
+// block front-padded to 64*S bytes with zeros (leading zeros leave a raw CRC
+// unchanged), raw CRCs combined with multiplications by x^(8n) mod P.
+DEV uint32_t gf_mul(uint32_t a, uint32_t b) {      // reflected, x^0 = 0x80000000 (zlib's multmodp)
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        p ^= (a & 0x80000000u) ? b : 0u;
+        a <<= 1;
+        b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+DEV uint32_t x8n(uint64_t n, const uint32_t *x2n) {  // x^(8n) mod P; x2n[k] = x^(2^k)
+    uint32_t p = 0x80000000u;
+    uint64_t e = n << 3;
+    for (uint32_t k = 0; e; k++, e >>= 1)
+        if (e & 1u) p = gf_mul(p, x2n[k & 31u]);
+    return p;
+}
+
+__global__ __launch_bounds__(256) void pf_bgzf_crc(const uint8_t *arena, const pf_bgzf_blk *blk, uint32_t nblk,
+                                                  uint32_t *status) {
+    __shared__ uint32_t tab[256];
+    __shared__ uint32_t x2n[32];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        tab[i] = c;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t p = 0x40000000u;                     // x^1
+        for (int k = 0; k < 32; k++) { x2n[k] = p; p = gf_mul(p, p); }
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t bi = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (bi >= nblk) return;
+    const pf_bgzf_blk B = blk[bi];
+    const uint32_t n = B.isize;
+    const uint32_t S = (n + 63) / 64;
+    const uint32_t pad = 64 * S - n;
+    const uint8_t *p = arena + B.out_off;
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < S; j++) {
+        const uint32_t v = lane * S + j;                 // virtual (padded) offset
+        const uint32_t byte = v >= pad ? p[v - pad] : 0u;
+        c = tab[(c ^ byte) & 0xFFu] ^ (c >> 8);
+    }
+    // lane k's contribution: raw_k * x^(8 S (63-k))
+    const uint32_t xs = x8n(S, x2n);
+    uint32_t m = 0x80000000u, base = xs;
+    uint32_t e = 63 - lane;
+    while (e) {
+        if (e & 1u) m = gf_mul(m, base);
+        base = gf_mul(base, base);
+        e >>= 1;
+    }
+    c = gf_mul(c, m);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
+    // crc32 = ~(raw ^ zeros(~0, n))
+    const uint32_t crc = ~(c ^ gf_mul(0xFFFFFFFFu, x8n(n, x2n)));
+    if (lane == 0 && crc != B.crc && status[bi] == 0) status[bi] = PF_INF_ECRC;
+}
