@@ -248,6 +248,13 @@ int64_t pf_batch_debug_calls(pf_dbatch_t *db, uint64_t *call_off, uint32_t *pos,
  * walked by the sequential path, records whose calls needed a sort, records
  * in implicit-canonical mode, records whose MM/ML could not be decoded,
  * emission chunks with a duplicate position.  n >= 8. */
+/* test hook: a record-level batch's record arrays copied back (sizes[5] =
+ * records, CIGAR ops, SEQ bytes (16-byte aligned slices), MM bytes, ML bytes;
+ * flag == NULL fills sizes only) */
+int  pf_batch_debug_recs(pf_dbatch_t *db, uint64_t *sizes, uint16_t *flag, uint8_t *mapq, uint32_t *pos,
+                         uint32_t *l_qseq, float *de, uint8_t *hp, uint64_t *cigar_off, uint32_t *cigar,
+                         uint64_t *seq_off, uint8_t *seq, uint64_t *mm_off, uint8_t *mm, uint64_t *ml_off,
+                         uint8_t *ml);
 int  pf_batch_load_counters(pf_dbatch_t *db, uint64_t *out, int n);
 
 /* One-shot convenience: upload + run + free on `device`. */
@@ -399,6 +406,12 @@ int32_t pf_bam_tid(const pf_bam_t *bam, const char *name);   /* -1 when absent *
 /* The index's per-reference metadata pseudo-bin: mapped / unmapped counts
  * (hts_idx_get_stat); PF_ERR_ARG when tid has none. */
 int  pf_bam_index_stats(const pf_bam_t *bam, int32_t tid, uint64_t *n_mapped, uint64_t *n_unmapped);
+const char *pf_bam_path(const pf_bam_t *bam);
+/* The BAI chunks [u, v) (virtual offsets) of region [beg, end) of tid, sorted
+ * by u, as hts_itr_query collects them (bins overlapping the region, chunks
+ * ending before the linear-index offset dropped).  Writes min(n, cap) pairs
+ * u, v to uv; returns n or a negative PF_ERR. */
+int64_t pf_bam_query_chunks(const pf_bam_t *bam, int32_t tid, int64_t beg, int64_t end, uint64_t *uv, uint64_t cap);
 
 /* The records of a set of windows of one contig, in window order and BAM
  * order inside a window, as pf_aln_batch_t (owned by this struct) plus the
@@ -425,6 +438,36 @@ typedef struct pf_bam_records {
 int  pf_bam_fetch_windows(pf_bam_t *bam, const char *chrom, uint32_t n_windows, const uint32_t *win_start,
                           const uint32_t *win_end, uint32_t readback, int n_threads, pf_bam_records_t **out);
 void pf_bam_records_free(pf_bam_records_t *recs);
+
+/* Device fetch: the same records as pf_bam_fetch_windows, but the host only
+ * plans the fetch from the BAI and reads the compressed bytes of the blocks
+ * the windows' index chunks touch; the device inflates them (pf_bgzf_inflate's
+ * kernels), walks the record chain, decodes every record (rec_decode,
+ * bam_tag2cigar, bam_endpos, the aux tags), runs each window's chunk walk
+ * (sam_itr_next, with the overlap rule pos + rlen > beg and the stops at
+ * another tid, pos >= end, a truncated record or EOF), and gathers the
+ * returned records into a record-level batch (pf_batch_upload_aln's layout)
+ * -- the record fields never cross PCIe.  Windows with more than
+ * max_win_recs records (0 = no limit) are left empty.  *out is the batch
+ * (pf_methphase_run etc.), *fetch the qnames and statistics (free with
+ * pf_bam_dev_fetch_free). */
+typedef struct pf_bam_dev_fetch {
+    uint32_t n_windows;
+    uint64_t n_recs;               /* records in the batch                               */
+    const uint32_t *win_rec_off;   /* [n_windows+1] the batch's records per window       */
+    const uint32_t *win_n_fetched; /* [n_windows] records the fetch returned (before the limit) */
+    const uint64_t *qname_off;     /* [n_recs+1] into qname                              */
+    const char *qname;
+    const int32_t *hp_tag;         /* [n_recs] raw HP value, INT32_MIN when absent       */
+    uint64_t n_truncated;          /* windows ended at a CIGAR/SEQ length mismatch       */
+    uint64_t comp_bytes, inflated_bytes, n_blocks, n_chain_recs;
+    double ms_read, ms_inflate, ms_chain, ms_decode, ms_select, ms_build, ms_total;
+    uint32_t attempts;             /* plans tried (a record past the planned blocks widens the plan) */
+} pf_bam_dev_fetch_t;
+int  pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lcfg, pf_bam_t *bam,
+                         const char *chrom, uint32_t n_windows, const uint32_t *win_start, const uint32_t *win_end,
+                         uint32_t readback, uint32_t max_win_recs, pf_dbatch_t **out, pf_bam_dev_fetch_t **fetch);
+void pf_bam_dev_fetch_free(pf_bam_dev_fetch_t *fetch);
 
 /* The -u pre-pass reads of one contig (pre_haplotagging_read_in_one_ref,
  * 1841-1898: sam_itr_querys over the whole contig, flags 4/256/2048

@@ -68,6 +68,7 @@ def lib():
         L.pf_batch_debug_calls.argtypes = [C.c_void_p] + [C.c_void_p] * 5 + [C.c_uint64]
         L.pf_batch_debug_calls.restype = C.c_int64
         L.pf_batch_load_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.pf_batch_debug_recs.argtypes = [C.c_void_p] * 16
         L.pf_bgzf_inflate.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                       C.POINTER(C.c_uint64), C.c_void_p, C.c_uint32, C.POINTER(C.c_float)]
         if hasattr(L, "pf_haptag_reads"):
@@ -354,6 +355,35 @@ class DeviceBatch:
         self.handle = h
         self.record_level = isinstance(batch, AlnBatch)
         ctx._batches.add(self)
+
+    @classmethod
+    def _wrap(cls, ctx: Context, handle, n_windows: int) -> "DeviceBatch":
+        """A record-level batch built by the library (e.g. the device fetch)."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        self.n_windows = n_windows
+        self.handle = handle
+        self.record_level = True
+        ctx._batches.add(self)
+        return self
+
+    def debug_recs(self) -> dict:
+        """The record arrays of a record-level batch (pf_batch_debug_recs)."""
+        sz = np.zeros(5, np.uint64)
+        _check(lib().pf_batch_debug_recs(self.handle, sz.ctypes.data, *([None] * 14)), "pf_batch_debug_recs")
+        n, nc, ns, nm, nl = (int(x) for x in sz)
+        d = dict(flag=np.zeros(n, np.uint16), mapq=np.zeros(n, np.uint8), pos=np.zeros(n, np.uint32),
+                 l_qseq=np.zeros(n, np.uint32), de=np.zeros(n, np.float32), hp=np.zeros(n, np.uint8),
+                 cigar_off=np.zeros(n + 1, np.uint64), cigar=np.zeros(max(nc, 1), np.uint32),
+                 seq_off=np.zeros(n + 1, np.uint64), seq=np.zeros(max(ns, 1), np.uint8),
+                 mm_off=np.zeros(n + 1, np.uint64), mm=np.zeros(max(nm, 1), np.uint8),
+                 ml_off=np.zeros(n + 1, np.uint64), ml=np.zeros(max(nl, 1), np.uint8))
+        keys = ["flag", "mapq", "pos", "l_qseq", "de", "hp", "cigar_off", "cigar", "seq_off", "seq", "mm_off", "mm",
+                "ml_off", "ml"]
+        _check(lib().pf_batch_debug_recs(self.handle, sz.ctypes.data, *[d[k].ctypes.data for k in keys]),
+               "pf_batch_debug_recs")
+        d["cigar"], d["seq"], d["mm"], d["ml"] = d["cigar"][:nc], d["seq"][:ns], d["mm"][:nm], d["ml"][:nl]
+        return d
 
     @property
     def n_reads(self) -> int:

@@ -50,6 +50,16 @@ class PfRescueMap(C.Structure):
 _bound = False
 
 
+class PfBamDevFetch(C.Structure):
+    _fields_ = [("n_windows", C.c_uint32), ("n_recs", C.c_uint64), ("win_rec_off", C.c_void_p),
+                ("win_n_fetched", C.c_void_p), ("qname_off", C.c_void_p), ("qname", C.c_void_p),
+                ("hp_tag", C.c_void_p), ("n_truncated", C.c_uint64), ("comp_bytes", C.c_uint64),
+                ("inflated_bytes", C.c_uint64), ("n_blocks", C.c_uint64), ("n_chain_recs", C.c_uint64),
+                ("ms_read", C.c_double), ("ms_inflate", C.c_double), ("ms_chain", C.c_double),
+                ("ms_decode", C.c_double), ("ms_select", C.c_double), ("ms_build", C.c_double),
+                ("ms_total", C.c_double), ("attempts", C.c_uint32)]
+
+
 def _bind():
     global _bound
     if _bound:
@@ -78,6 +88,12 @@ def _bind():
                                     C.POINTER(C.POINTER(PfRescueMap))]
     L.pf_rescue_map_free.argtypes = [C.POINTER(PfRescueMap)]
     L.pf_bam_estimate_coverage.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    L.pf_bam_query_chunks.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_uint64]
+    L.pf_bam_query_chunks.restype = C.c_int64
+    L.pf_batch_upload_bam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_uint32,
+                                      C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p),
+                                      C.POINTER(C.POINTER(PfBamDevFetch))]
+    L.pf_bam_dev_fetch_free.argtypes = [C.POINTER(PfBamDevFetch)]
     _bound = True
     return L
 
@@ -177,6 +193,50 @@ class BamFile:
         finally:
             L.pf_bam_records_free(out)
         return batch, qnames, info
+
+    def query_chunks(self, chrom: str, beg: int, end: int) -> np.ndarray:
+        """BAI chunks [u, v) of region [beg, end) (pf_bam_query_chunks), shape (n, 2)."""
+        L = _bind()
+        tid = self.tid(chrom)
+        n = int(L.pf_bam_query_chunks(self.handle, tid, int(beg), int(end), None, 0))
+        _check(min(n, 0), "pf_bam_query_chunks")
+        out = np.zeros(2 * max(n, 1), np.uint64)
+        L.pf_bam_query_chunks(self.handle, tid, int(beg), int(end), out.ctypes.data, n)
+        return out[:2 * n].reshape(n, 2)
+
+    def fetch_windows_device(self, ctx, cfg, chrom: str, starts: Sequence[int], ends: Sequence[int],
+                             lcfg=None, readback: int = READBACK, max_win_recs: int = 0):
+        """Device fetch (pf_batch_upload_bam): the windows' records inflated,
+        selected and gathered on the GPU into a record-level batch.  Returns
+        (DeviceBatch, qnames, info)."""
+        from ._lib import DeviceBatch
+        from .abi import LoadConfig
+        if self.path is None:
+            raise PomfretError("index-only BamFile cannot fetch")
+        L = _bind()
+        ws = np.ascontiguousarray(starts, np.uint32)
+        we = np.ascontiguousarray(ends, np.uint32)
+        c = cfg.to_c()
+        lc = (lcfg or LoadConfig()).to_c()
+        h = C.c_void_p()
+        f = C.POINTER(PfBamDevFetch)()
+        _check(L.pf_batch_upload_bam(ctx.handle, C.byref(c), C.byref(lc), self.handle, chrom.encode(), ws.size,
+                                     ws.ctypes.data, we.ctypes.data, int(readback), int(max_win_recs), C.byref(h),
+                                     C.byref(f)), "pf_batch_upload_bam")
+        try:
+            r = f.contents
+            n, W = int(r.n_recs), int(r.n_windows)
+            qo = _arr(r.qname_off, n + 1, np.uint64)
+            qb = _arr(r.qname, qo[-1] if n else 0, np.uint8).tobytes()
+            qnames = [qb[qo[i]:qo[i + 1]].decode("ascii", "replace") for i in range(n)]
+            info = {k: getattr(r, k) for k, _ in PfBamDevFetch._fields_
+                    if k not in ("win_rec_off", "win_n_fetched", "qname_off", "qname", "hp_tag")}
+            info["win_rec_off"] = _arr(r.win_rec_off, W + 1, np.uint32)
+            info["win_n_fetched"] = _arr(r.win_n_fetched, W, np.uint32)
+            info["hp_tag"] = _arr(r.hp_tag, n, np.int32)
+        finally:
+            L.pf_bam_dev_fetch_free(f)
+        return DeviceBatch._wrap(ctx, h, W), qnames, info
 
     def estimate_coverage(self) -> List[int]:
         """estimate_read_coverage_dirtyfast (blockjoin.c:951-1040): per contig."""

@@ -569,9 +569,14 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
 
 // ---------------------------------------------------------------------------
 // Record-level batches: raw BAM fields resident in HBM, K0 in front of K12.
-extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lc,
-                                   const pf_aln_batch_t *a, pf_dbatch_t **out) {
-    if (!ctx || !cfg || !lc || !a || !out) return PF_ERR_ARG;
+// aln_build sizes and allocates a batch from the records' lengths and small
+// fields (host arrays); `fill` places the large arrays (CIGAR, MM, ML and the
+// 16-byte aligned SEQ slices at seq_off) -- copied from host buffers by
+// pf_batch_upload_aln, gathered from the inflated BAM stream by the device
+// fetch (pf_ingest.hip).
+extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lc, const pf_aln_batch_t *a,
+                            const pf_aln_fill_t *fill, pf_dbatch_t **out) {
+    if (!ctx || !cfg || !lc || !a || !fill || !out) return PF_ERR_ARG;
     *out = nullptr;
     if (cfg->k < 1 || cfg->k_span < 0) return PF_ERR_ARG;
     if (cfg->k > 5) return PF_ERR_UNSUPPORTED;
@@ -579,36 +584,24 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
     if (W && (!a->win_start || !a->win_end || !a->win_rec_off)) return PF_ERR_ARG;
     if (W && (a->win_rec_off[0] != 0 || a->win_rec_off[W] != n)) return PF_ERR_ARG;
     if (!W && n) return PF_ERR_ARG;
-    if (n && (!a->flag || !a->mapq || !a->pos || !a->l_qseq || !a->de || !a->hp || !a->cigar_off || !a->cigar ||
-              !a->seq_off || !a->seq || !a->mm_off || !a->mm || !a->ml_off || !a->ml))
+    if (n && (!a->flag || !a->mapq || !a->pos || !a->l_qseq || !a->de || !a->hp || !a->cigar_off || !a->mm_off ||
+              !a->ml_off))
         return PF_ERR_ARG;
     for (uint32_t w = 0; w < W; w++)
         if (a->win_rec_off[w + 1] < a->win_rec_off[w]) return PF_ERR_ARG;
-    // record slices: monotone offsets, SEQ long enough for l_qseq (checked
-    // per record in parallel; the slice offsets are a prefix sum)
+    // slice sizes (prefix sums below): 16-byte aligned SEQ slices, HBM trigger
+    // slices for records whose bound exceeds K0's LDS list, trigger bounds
     std::vector<uint64_t> seq_off(n + 1), scr_off(n + 1), tbound(n);
     std::vector<int> prc(17, 0);
     par_for(n, [&](uint64_t lo, uint64_t hi) {
         int rc = 0;
         for (uint64_t r = lo; r < hi && !rc; r++) {
             if (a->cigar_off[r + 1] < a->cigar_off[r] || a->mm_off[r + 1] < a->mm_off[r] ||
-                a->ml_off[r + 1] < a->ml_off[r] || a->seq_off[r + 1] < a->seq_off[r]) { rc = PF_ERR_ARG; break; }
+                a->ml_off[r + 1] < a->ml_off[r]) { rc = PF_ERR_ARG; break; }
             const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
-            if (a->seq_off[r + 1] - a->seq_off[r] < sb) { rc = PF_ERR_ARG; break; }
-            // htslib refuses records whose CIGAR query length differs from l_qseq
-            // (bam_read1); K0's walk relies on it to stay inside SEQ
-            if (!(a->flag[r] & 4) && a->l_qseq[r] && a->cigar_off[r + 1] > a->cigar_off[r]) {
-                uint64_t ql = 0;
-                for (uint64_t c = a->cigar_off[r]; c < a->cigar_off[r + 1]; c++) {
-                    const uint32_t op = a->cigar[c] & 15u;
-                    if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += a->cigar[c] >> 4;
-                }
-                if (ql != a->l_qseq[r]) { rc = PF_ERR_ARG; break; }
-            }
             if (a->mm_off[r + 1] - a->mm_off[r] > 0xFFFFFFF0ull || a->ml_off[r + 1] - a->ml_off[r] > 0xFFFFFFF0ull)
                 rc = PF_ERR_LIMIT;
             if (a->l_qseq[r] >= (1u << 24)) rc = PF_ERR_LIMIT;   // K0 packs ranks into 24 bits
-            // this record's slice sizes, summed below
             seq_off[r] = (sb + PF_K0_SEQ_ALIGN + PF_K0_SEQ_ALIGN - 1) & ~(uint64_t)(PF_K0_SEQ_ALIGN - 1);
             // trigger lists that may exceed the per-wave LDS list get an HBM slice
             const uint64_t mln = a->ml_off[r + 1] - a->ml_off[r], mlen = a->mm_off[r + 1] - a->mm_off[r];
@@ -659,43 +652,15 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         float *pf; PUT(pf, a->de, n); ld.de = pf;
         uint64_t *p64; PUT(p64, a->cigar_off, n + 1); ld.cigar_off = p64;
         ALLOC(p32, a->cigar_off[n]); ld.cigar = p32;
-        if ((rc = pinned_put(ctx, p32, a->cigar, 4ull * a->cigar_off[n]))) return fail(rc);
         PUT(p64, a->mm_off, n + 1); ld.mm_off = p64;
         ALLOC(p8, a->mm_off[n] + 16); ld.mm = p8;            // padded: K0 stages the text with word loads
-        if (a->mm_off[n] && (rc = pinned_put(ctx, p8, a->mm, a->mm_off[n]))) return fail(rc);
         PUT(p64, a->ml_off, n + 1); ld.ml_off = p64;
         ALLOC(p8, a->ml_off[n]); ld.ml = p8;
-        if ((rc = pinned_put(ctx, p8, a->ml, a->ml_off[n]))) return fail(rc);
         PUT(p64, seq_off.data(), n + 1); ld.seq_off = p64;
         PUT(p64, scr_off.data(), n + 1); ld.scr_off = p64;
         ALLOC(p32, sc ? sc : 1); ld.scr = p32;
-        // SEQ repacked into 16-byte aligned, padded per-record slices, built
-        // piece by piece in the pinned buffer (no pageable copy of 1 GB)
         ALLOC(p8, so ? so : 1); ld.seq = p8;
-        rc = pinned_fill(ctx, p8, so, [&](uint8_t *buf, uint64_t lo, uint64_t hi) {
-            const uint64_t r0 = (uint64_t)(std::upper_bound(seq_off.begin(), seq_off.begin() + n + 1, lo) -
-                                           seq_off.begin()) - 1;
-            uint64_t r1 = r0;
-            while (r1 < n && seq_off[r1] < hi) r1++;
-            par_for(r1 - r0, [&](uint64_t a0, uint64_t a1) {
-                for (uint64_t r = r0 + a0; r < r0 + a1; r++) {
-                    const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
-                    const uint64_t x0 = std::max(seq_off[r], lo), x1 = std::min(seq_off[r + 1], hi);
-                    for (uint64_t x = x0; x < x1;) {               // data part, then the zero pad
-                        const uint64_t rel = x - seq_off[r];
-                        if (rel < sb) {
-                            const uint64_t k = std::min(sb - rel, x1 - x);
-                            memcpy(buf + (x - lo), a->seq + a->seq_off[r] + rel, k);
-                            x += k;
-                        } else {
-                            memset(buf + (x - lo), 0, x1 - x);
-                            x = x1;
-                        }
-                    }
-                }
-            });
-        });
-        if (rc) return fail(rc);
+        if ((rc = fill->fill(fill->user, ctx, &ld, seq_off.data(), so))) return fail(rc);
         // wave slots in decreasing read length: the long records start first
         // and the four waves of a workgroup finish together
         std::vector<uint32_t> ord(n);
@@ -790,6 +755,79 @@ extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
     return PF_OK;
 #undef PUT
 #undef ALLOC
+}
+
+// host arrays -> device: the large arrays through the context's pinned
+// staging, SEQ repacked into 16-byte aligned, zero-padded slices on the way
+struct HostFill {
+    const pf_aln_batch_t *a;
+};
+static int host_fill(void *user, pf_ctx_t *ctx, pf_load_dev *ld, const uint64_t *seq_off, uint64_t seq_bytes) {
+    const pf_aln_batch_t *a = static_cast<HostFill *>(user)->a;
+    const uint32_t n = a->n_recs;
+    int rc;
+    if ((rc = pinned_put(ctx, const_cast<uint32_t *>(ld->cigar), a->cigar, 4ull * a->cigar_off[n]))) return rc;
+    if (a->mm_off[n] && (rc = pinned_put(ctx, const_cast<uint8_t *>(ld->mm), a->mm, a->mm_off[n]))) return rc;
+    if ((rc = pinned_put(ctx, const_cast<uint8_t *>(ld->ml), a->ml, a->ml_off[n]))) return rc;
+    return pinned_fill(ctx, const_cast<uint8_t *>(ld->seq), seq_bytes, [&](uint8_t *buf, uint64_t lo, uint64_t hi) {
+        const uint64_t r0 = (uint64_t)(std::upper_bound(seq_off, seq_off + n + 1, lo) - seq_off) - 1;
+        uint64_t r1 = r0;
+        while (r1 < n && seq_off[r1] < hi) r1++;
+        par_for(r1 - r0, [&](uint64_t a0, uint64_t a1) {
+            for (uint64_t r = r0 + a0; r < r0 + a1; r++) {
+                const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
+                const uint64_t x0 = std::max(seq_off[r], lo), x1 = std::min(seq_off[r + 1], hi);
+                for (uint64_t x = x0; x < x1;) {               // data part, then the zero pad
+                    const uint64_t rel = x - seq_off[r];
+                    if (rel < sb) {
+                        const uint64_t k = std::min(sb - rel, x1 - x);
+                        memcpy(buf + (x - lo), a->seq + a->seq_off[r] + rel, k);
+                        x += k;
+                    } else {
+                        memset(buf + (x - lo), 0, x1 - x);
+                        x = x1;
+                    }
+                }
+            }
+        });
+    });
+}
+
+extern "C" int pf_batch_upload_aln(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lc,
+                                   const pf_aln_batch_t *a, pf_dbatch_t **out) {
+    if (!ctx || !cfg || !lc || !a || !out) return PF_ERR_ARG;
+    *out = nullptr;
+    const uint32_t n = a->n_recs;
+    if (n && (!a->cigar_off || !a->cigar || !a->seq_off || !a->seq || !a->mm_off || !a->mm || !a->ml_off ||
+              !a->ml || !a->l_qseq || !a->flag))
+        return PF_ERR_ARG;
+    // host-side checks of what the device fetch guarantees by construction:
+    // SEQ long enough for l_qseq, CIGAR query length equal to l_qseq
+    std::vector<int> prc(1, 0);
+    par_for(n, [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t r = lo; r < hi; r++) {
+            if (a->cigar_off[r + 1] < a->cigar_off[r] || a->seq_off[r + 1] < a->seq_off[r]) break;
+            const uint64_t sb = ((uint64_t)a->l_qseq[r] + 1) / 2;
+            bool bad = a->seq_off[r + 1] - a->seq_off[r] < sb;
+            // htslib refuses records whose CIGAR query length differs from l_qseq
+            // (bam_read1); K0's walk relies on it to stay inside SEQ
+            if (!bad && !(a->flag[r] & 4) && a->l_qseq[r] && a->cigar_off[r + 1] > a->cigar_off[r]) {
+                uint64_t ql = 0;
+                for (uint64_t c = a->cigar_off[r]; c < a->cigar_off[r + 1]; c++) {
+                    const uint32_t op = a->cigar[c] & 15u;
+                    if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += a->cigar[c] >> 4;
+                }
+                bad = ql != a->l_qseq[r];
+            }
+            if (bad) { __atomic_store_n(&prc[0], 1, __ATOMIC_RELAXED); break; }
+        }
+    });
+    for (uint32_t r = 0; r < n && !prc[0]; r++)
+        if (a->cigar_off[r + 1] < a->cigar_off[r] || a->seq_off[r + 1] < a->seq_off[r]) prc[0] = 1;
+    if (prc[0]) return PF_ERR_ARG;
+    HostFill hf{a};
+    pf_aln_fill_t f{host_fill, &hf};
+    return pf_aln_build(ctx, cfg, lc, a, &f, out);
 }
 
 extern "C" int pf_batch_read_recs(const pf_dbatch_t *b, uint32_t *rec_of_read, uint32_t n) {
@@ -1166,6 +1204,46 @@ extern "C" int64_t pf_batch_debug_calls(pf_dbatch_t *b, uint64_t *call_off, uint
         HIPCHK(hipMemcpy(last, b->d.read_last, 4ull * b->R, hipMemcpyDeviceToHost));
     }
     return (int64_t)b->N;
+}
+
+extern "C" int pf_batch_debug_recs(pf_dbatch_t *b, uint64_t *sizes, uint16_t *flag, uint8_t *mapq, uint32_t *pos,
+                                   uint32_t *l_qseq, float *de, uint8_t *hp, uint64_t *cigar_off, uint32_t *cigar,
+                                   uint64_t *seq_off, uint8_t *seq, uint64_t *mm_off, uint8_t *mm, uint64_t *ml_off,
+                                   uint8_t *ml) {
+    if (!b || !sizes || !b->has_aln) return PF_ERR_ARG;
+    const pf_load_dev &ld = b->ld;
+    const uint64_t n = ld.n_recs;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    uint64_t last[4] = {0, 0, 0, 0};
+    if (n) {
+        HIPCHK(hipMemcpy(&last[0], ld.cigar_off + n, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&last[1], ld.seq_off + n, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&last[2], ld.mm_off + n, 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(&last[3], ld.ml_off + n, 8, hipMemcpyDeviceToHost));
+    }
+    sizes[0] = n;
+    for (int i = 0; i < 4; i++) sizes[1 + i] = last[i];
+    if (!flag) return PF_OK;
+    if (!mapq || !pos || !l_qseq || !de || !hp || !cigar_off || !cigar || !seq_off || !seq || !mm_off || !mm ||
+        !ml_off || !ml)
+        return PF_ERR_ARG;
+    if (!n) return PF_OK;
+    HIPCHK(hipMemcpy(flag, ld.flag, 2 * n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(mapq, ld.mapq, n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pos, ld.pos, 4 * n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(l_qseq, ld.l_qseq, 4 * n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(de, ld.de, 4 * n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hp, ld.hp, n, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cigar_off, ld.cigar_off, 8 * (n + 1), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(seq_off, ld.seq_off, 8 * (n + 1), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(mm_off, ld.mm_off, 8 * (n + 1), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ml_off, ld.ml_off, 8 * (n + 1), hipMemcpyDeviceToHost));
+    if (last[0]) HIPCHK(hipMemcpy(cigar, ld.cigar, 4 * last[0], hipMemcpyDeviceToHost));
+    if (last[1]) HIPCHK(hipMemcpy(seq, ld.seq, last[1], hipMemcpyDeviceToHost));
+    if (last[2]) HIPCHK(hipMemcpy(mm, ld.mm, last[2], hipMemcpyDeviceToHost));
+    if (last[3]) HIPCHK(hipMemcpy(ml, ld.ml, last[3], hipMemcpyDeviceToHost));
+    return PF_OK;
 }
 
 extern "C" int pf_batch_load_counters(pf_dbatch_t *b, uint64_t *out, int n) {

@@ -370,6 +370,8 @@ void pf_bam_close(pf_bam_t *b) {
     free(b);
 }
 
+const char *pf_bam_path(const pf_bam_t *b) { return b ? b->path : NULL; }
+
 int32_t pf_bam_n_targets(const pf_bam_t *b) { return b ? (b->path ? b->n_ref : b->n_ref_idx) : 0; }
 const char *pf_bam_target_name(const pf_bam_t *b, int32_t tid) {
     return b && b->names && tid >= 0 && tid < b->n_ref ? b->names[tid] : NULL;
@@ -673,8 +675,10 @@ static int cmp_chunk(const void *a, const void *b) {
     return x < y ? -1 : x > y;
 }
 
-static int fetch_region(fetcher_t *F, int64_t beg, int64_t end, recbuf_t *rb) {
-    const ref_idx_t *ri = &F->b->idx[F->tid];
+/* the index chunks of region [beg, end) of tid, sorted by start offset
+ * (hts_itr_query's chunk list before it walks them) */
+static int64_t region_chunks(const pf_bam_t *b, int32_t tid, int64_t beg, int64_t end, chunk_t **buf, size_t *cap) {
+    const ref_idx_t *ri = &b->idx[tid];
     if (end <= beg) return 0;
     /* the bins reg2bins(beg, end) lists are exactly the index bins whose
      * interval overlaps [beg, end): level l bin k covers
@@ -696,18 +700,34 @@ static int fetch_region(fetcher_t *F, int64_t beg, int64_t end, recbuf_t *rb) {
         if (!(lo < end && hi > beg)) continue;
         for (uint32_t c = 0; c < bb->n; c++) {
             if (bb->c[c].v <= min_off) continue;
-            if (nc == F->chunk_cap) {
-                const size_t cap = F->chunk_cap ? 2 * F->chunk_cap : 64;
-                chunk_t *np = (chunk_t *)realloc(F->chunks, cap * sizeof(chunk_t));
+            if (nc == *cap) {
+                const size_t ncap = *cap ? 2 * *cap : 64;
+                chunk_t *np = (chunk_t *)realloc(*buf, ncap * sizeof(chunk_t));
                 if (!np) return PF_ERR_NOMEM;
-                F->chunks = np;
-                F->chunk_cap = cap;
+                *buf = np;
+                *cap = ncap;
             }
-            F->chunks[nc++] = bb->c[c];
+            (*buf)[nc++] = bb->c[c];
         }
     }
-    if (!nc) return 0;
-    qsort(F->chunks, nc, sizeof(chunk_t), cmp_chunk);
+    if (nc) qsort(*buf, nc, sizeof(chunk_t), cmp_chunk);
+    return (int64_t)nc;
+}
+
+int64_t pf_bam_query_chunks(const pf_bam_t *b, int32_t tid, int64_t beg, int64_t end, uint64_t *uv, uint64_t cap) {
+    if (!b || tid < 0 || tid >= b->n_ref_idx || (cap && !uv)) return PF_ERR_ARG;
+    chunk_t *buf = NULL;
+    size_t bcap = 0;
+    const int64_t n = region_chunks(b, tid, beg, end, &buf, &bcap);
+    for (int64_t i = 0; i < n && (uint64_t)i < cap; i++) { uv[2 * i] = buf[i].u; uv[2 * i + 1] = buf[i].v; }
+    free(buf);
+    return n;
+}
+
+static int fetch_region(fetcher_t *F, int64_t beg, int64_t end, recbuf_t *rb) {
+    const int64_t nci = region_chunks(F->b, F->tid, beg, end, &F->chunks, &F->chunk_cap);
+    if (nci <= 0) return (int)nci;
+    const size_t nc = (size_t)nci;
     uint64_t done = 0;                          /* records before this offset were read */
     for (size_t c = 0; c < nc; c++) {
         uint64_t at = F->chunks[c].u > done ? F->chunks[c].u : done;

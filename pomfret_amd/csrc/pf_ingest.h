@@ -27,3 +27,63 @@ typedef struct pf_bgzf_blk {
 __global__ void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena,
                            uint32_t *status);
 __global__ void pf_bgzf_crc(const uint8_t *arena, const pf_bgzf_blk *blk, uint32_t nblk, uint32_t *status);
+
+// ---- device fetch (pf_ingest.hip): runs of blocks, windows, chunks, records
+typedef struct pf_run_dev {
+    uint64_t a0, a1;          // the run's inflated bytes [a0, a1) in the arena
+    uint64_t chain_start;     // first record start the chain walks from (min chunk start)
+    uint64_t stop_pos;        // chain output: position after its last whole record
+    uint32_t to_eof;          // the run ends at the file's end
+    uint32_t rec0, n_rec;     // chain output: its records [rec0, rec0 + n_rec) of the record arrays
+    uint32_t stop;            // chain output: PF_CHAIN_*
+} pf_run_dev;
+#define PF_CHAIN_END 0u        // stop_pos == a1
+#define PF_CHAIN_CUT 1u        // a record (or its size field) runs past a1
+#define PF_CHAIN_CORRUPT 2u    // block_size < 32 or > 2^30 at stop_pos
+
+typedef struct pf_chunk_dev {
+    uint64_t u, v;            // arena positions of the chunk's virtual offsets
+    uint32_t run, pad;
+} pf_chunk_dev;
+
+typedef struct pf_win_dev {
+    int64_t beg, end;         // region [beg, end)
+    uint32_t c0, c1;          // its chunks
+    int32_t tid;
+    uint32_t skip;            // write pass: window emptied (over the record limit)
+    uint64_t out;             // write pass: first slot of its record list
+} pf_win_dev;
+
+// window status of the select pass
+#define PF_WIN_OK 0u
+#define PF_WIN_MORE 1u         // needs blocks past its run's end (host widens the plan)
+#define PF_WIN_ERR 2u          // corrupt record / index offset inside a record / truncated file
+#define PF_WIN_TRUNC 3u        // ended at a record whose CIGAR and SEQ lengths differ (counted, not an error)
+
+// decoded records (SoA, indexed like the chain)
+typedef struct pf_recs_dev {
+    uint64_t *pos;            // arena position of the block_size field
+    uint64_t *cig, *seq, *qn, *mm, *ml;     // arena positions
+    uint32_t *bs, *l_qseq, *ncig, *rlen, *qn_len, *mm_len, *ml_len, *md_len;
+    int32_t *tid, *rpos, *hp_tag;
+    float *de;
+    uint16_t *flag;
+    uint8_t *mapq, *hp, *st;  // st: bit 0 corrupt, bit 1 truncated (CIGAR/SEQ length mismatch), bit 2 MD:Z present
+    uint64_t *md;
+} pf_recs_dev;
+#define PF_REC_CORRUPT 1u
+#define PF_REC_TRUNC 2u
+#define PF_REC_MD 4u
+
+__global__ void pf_chain(const uint8_t *arena, pf_run_dev *runs, uint32_t n_runs, uint64_t *rec_pos);
+__global__ void pf_recdec(const uint8_t *arena, uint32_t n_recs, pf_recs_dev R);
+__global__ void pf_select(const pf_win_dev *wins, uint32_t n_wins, const pf_chunk_dev *chunks, const pf_run_dev *runs,
+                          pf_recs_dev R, uint32_t write, uint32_t *win_n, uint32_t *win_st, uint32_t *out);
+__global__ void pf_gather_small(const uint32_t *sel, uint64_t n, pf_recs_dev R, uint16_t *flag, uint8_t *mapq,
+                                uint32_t *pos, uint32_t *l_qseq, float *de, uint8_t *hp, int32_t *hp_tag,
+                                uint32_t *ncig, uint32_t *mm_len, uint32_t *ml_len, uint32_t *qn_len,
+                                uint32_t *md_len, uint32_t *rlen, uint8_t *st);
+__global__ void pf_gather_big(const uint8_t *arena, const uint32_t *sel, uint64_t n, pf_recs_dev R,
+                              const uint64_t *cig_off, uint32_t *cig, const uint64_t *seq_off, uint8_t *seq,
+                              const uint64_t *mm_off, uint8_t *mm, const uint64_t *ml_off, uint8_t *ml,
+                              const uint64_t *qn_off, uint8_t *qn, const uint64_t *md_off, uint8_t *md);

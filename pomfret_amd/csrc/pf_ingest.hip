@@ -118,3 +118,494 @@ out:
     (void)hipFree(d_st);
     return rc;
 }
+
+// ===========================================================================
+// Device fetch: the windows' records from the BAM file through the device
+// (inflate, chain, decode, select, gather) into a record-level batch.
+#include <algorithm>
+#include <chrono>
+#include <thread>
+#include <errno.h>
+#include <fcntl.h>
+#include <unistd.h>
+#include <sys/stat.h>
+#include "pf_load.h"
+
+namespace {
+
+struct DevBuf {                                  // device allocations freed together
+    std::vector<void *> p;
+    ~DevBuf() { for (void *x : p) (void)hipFree(x); }
+    template <typename T> T *alloc(size_t n) {
+        void *x = nullptr;
+        if (hipMalloc(&x, n ? n * sizeof(T) : 1) != hipSuccess) return nullptr;
+        p.push_back(x);
+        return static_cast<T *>(x);
+    }
+};
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// one merged byte range of the file and the blocks scanned in it
+struct Range {
+    uint64_t f0, f1;          // requested [f0, f1) file bytes
+    uint64_t buf0;            // its bytes in the compressed upload buffer
+    uint64_t end_addr;        // file address after its last whole block
+    uint32_t b0, b1;          // its blocks
+    bool to_eof;
+};
+
+struct Plan {
+    std::vector<pf_bgzf_blk> blk;
+    std::vector<uint64_t> caddr;            // file address of each block
+    std::vector<Range> runs;
+    std::vector<uint8_t> comp;              // compressed bytes of every run, back to back
+    uint64_t arena = 0;                     // inflated bytes
+};
+
+// the gathered small fields, host side
+struct Small {
+    std::vector<uint16_t> flag;
+    std::vector<uint8_t> mapq, hp, st;
+    std::vector<uint32_t> pos, l_qseq, ncig, mm_len, ml_len, qn_len, md_len, rlen;
+    std::vector<float> de;
+    std::vector<int32_t> hp_tag;
+    void resize(size_t n) {
+        flag.resize(n); mapq.resize(n); hp.resize(n); st.resize(n); pos.resize(n); l_qseq.resize(n);
+        ncig.resize(n); mm_len.resize(n); ml_len.resize(n); qn_len.resize(n); md_len.resize(n); rlen.resize(n);
+        de.resize(n); hp_tag.resize(n);
+    }
+};
+
+int read_range(int fd, uint64_t off, uint64_t n, uint8_t *dst) {
+    uint64_t got = 0;
+    while (got < n) {
+        const ssize_t k = pread(fd, dst + got, (size_t)std::min<uint64_t>(n - got, 1ull << 30), (off_t)(off + got));
+        if (k < 0) { if (errno == EINTR) continue; return -1; }
+        if (k == 0) break;
+        got += (uint64_t)k;
+    }
+    return got == n ? 0 : -1;
+}
+
+}  // namespace
+
+struct pf_bam_dev_fetch_own {
+    pf_bam_dev_fetch_t pub;
+    std::vector<uint32_t> win_rec_off, win_n, win_status;
+    std::vector<uint64_t> qn_off, md_off;
+    std::vector<char> qn, md;
+    Small s;
+};
+
+extern "C" void pf_bam_dev_fetch_free(pf_bam_dev_fetch_t *f) { delete reinterpret_cast<pf_bam_dev_fetch_own *>(f); }
+
+// device fill of a record-level batch: gather the large arrays from the arena
+struct DevFill {
+    const uint8_t *arena;
+    const uint32_t *sel;
+    uint64_t n;
+    pf_recs_dev R;
+    const uint64_t *d_cig_off, *d_mm_off, *d_ml_off;
+    hipStream_t st;
+};
+static int dev_fill(void *user, pf_ctx *ctx, pf_load_dev *ld, const uint64_t *seq_off, uint64_t seq_bytes) {
+    (void)ctx; (void)seq_bytes;
+    DevFill *f = static_cast<DevFill *>(user);
+    if (!f->n) return PF_OK;
+    // the batch's seq_off is on the device already (ld->seq_off)
+    hipLaunchKernelGGL(pf_gather_big, dim3((unsigned)((f->n + 3) / 4)), dim3(256), 0, f->st, f->arena, f->sel, f->n,
+                       f->R, ld->cigar_off, const_cast<uint32_t *>(ld->cigar), ld->seq_off,
+                       const_cast<uint8_t *>(ld->seq), ld->mm_off, const_cast<uint8_t *>(ld->mm), ld->ml_off,
+                       const_cast<uint8_t *>(ld->ml), nullptr, nullptr, nullptr, nullptr);
+    (void)seq_off;
+    if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
+    return hipStreamSynchronize(f->st) == hipSuccess ? PF_OK : PF_ERR_HIP;
+}
+
+extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lc, pf_bam_t *bam,
+                                   const char *chrom, uint32_t W, const uint32_t *ws, const uint32_t *we,
+                                   uint32_t readback, uint32_t max_win_recs, pf_dbatch_t **out,
+                                   pf_bam_dev_fetch_t **fetch_out) {
+    if (!ctx || !cfg || !lc || !bam || !chrom || !out || !fetch_out || (W && (!ws || !we))) return PF_ERR_ARG;
+    *out = nullptr;
+    *fetch_out = nullptr;
+    const char *path = pf_bam_path(bam);
+    const int32_t tid = pf_bam_tid(bam, chrom);
+    if (!path || tid < 0) return PF_ERR_ARG;
+    const double t_start = now_ms();
+    // ---- chunk lists (the BAI query of every window)
+    std::vector<int64_t> beg(W), end(W);
+    std::vector<uint64_t> uv;
+    std::vector<uint32_t> wc(W + 1, 0);
+    for (uint32_t w = 0; w < W; w++) {
+        const int64_t s = (int32_t)ws[w], e = (int32_t)we[w], rb = (int32_t)readback;
+        const int64_t b1 = s - rb > 0 ? s - rb : 0;
+        beg[w] = b1 > 0 ? b1 - 1 : 0;
+        end[w] = e + rb;
+        const int64_t n = pf_bam_query_chunks(bam, tid, beg[w], end[w], nullptr, 0);
+        if (n < 0) return (int)n;
+        const size_t o = uv.size();
+        uv.resize(o + 2 * (size_t)n);
+        if (n && pf_bam_query_chunks(bam, tid, beg[w], end[w], uv.data() + o, (uint64_t)n) != n) return PF_ERR_INTERNAL;
+        wc[w + 1] = wc[w] + (uint32_t)n;
+    }
+    const uint32_t NC = wc[W];
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) return -1;
+    struct stat stt;
+    if (fstat(fd, &stt) != 0) { close(fd); return -1; }
+    const uint64_t fsize = (uint64_t)stt.st_size;
+    hipStream_t st = pf_ctx_stream((const pf_ctx *)ctx);
+    if (hipSetDevice(pf_ctx_device((const pf_ctx *)ctx)) != hipSuccess) { close(fd); return PF_ERR_HIP; }
+    pf_bam_dev_fetch_own *F = new pf_bam_dev_fetch_own();
+    memset(&F->pub, 0, sizeof F->pub);
+    int rc = PF_OK;
+    uint64_t ext = 4ull << 16;            // bytes read past a chunk's last block (records spanning blocks)
+    for (int attempt = 0; attempt < 8; attempt++) {
+        DevBuf D;
+        Plan P;
+        double t0 = now_ms();
+        // ---- byte ranges: [u >> 16, (v >> 16) + ext) per chunk, merged
+        std::vector<std::pair<uint64_t, uint64_t>> rq;
+        rq.reserve(NC);
+        for (uint32_t c = 0; c < NC; c++) {
+            const uint64_t a0 = uv[2 * c] >> 16, a1 = std::min(fsize, (uv[2 * c + 1] >> 16) + ext);
+            if (a0 < fsize) rq.push_back({a0, std::max(a1, a0 + 1)});
+        }
+        std::sort(rq.begin(), rq.end());
+        for (auto &x : rq) {
+            if (!P.runs.empty() && x.first <= P.runs.back().f1) P.runs.back().f1 = std::max(P.runs.back().f1, x.second);
+            else P.runs.push_back(Range{x.first, x.second, 0, 0, 0, 0, false});
+        }
+        uint64_t tot = 0;
+        for (auto &R : P.runs) { R.buf0 = tot; tot += R.f1 - R.f0; }
+        P.comp.resize(tot + 512);
+        // parallel reads of the ranges
+        {
+            std::vector<int> rr(P.runs.size(), 0);
+            const size_t nt = std::min<size_t>(16, P.runs.size() ? P.runs.size() : 1);
+            std::vector<std::thread> th;
+            for (size_t t = 0; t < nt; t++)
+                th.emplace_back([&, t]() {
+                    for (size_t i = t; i < P.runs.size(); i += nt)
+                        rr[i] = read_range(fd, P.runs[i].f0, P.runs[i].f1 - P.runs[i].f0, P.comp.data() + P.runs[i].buf0);
+                });
+            for (auto &t : th) t.join();
+            for (int x : rr) if (x) rc = -1;
+            memset(P.comp.data() + tot, 0, 512);
+        }
+        if (rc) break;
+        const double t_read = now_ms() - t0;
+        // ---- blocks of each range (whole blocks only)
+        for (uint32_t ri = 0; ri < P.runs.size() && !rc; ri++) {
+            Range &R = P.runs[ri];
+            R.b0 = (uint32_t)P.blk.size();
+            uint64_t o = 0;
+            const uint64_t len = R.f1 - R.f0;
+            const uint8_t *c = P.comp.data() + R.buf0;
+            while (o + 18 <= len) {
+                const uint8_t *h = c + o;
+                if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { rc = PF_ERR_ARG; break; }
+                const uint32_t xlen = rd16(h + 10);
+                if (o + 12 + xlen > len) break;
+                uint32_t bsize = 0;
+                for (uint32_t x = 0; x + 4 <= xlen;) {
+                    const uint8_t *sf = h + 12 + x;
+                    const uint32_t slen = rd16(sf + 2);
+                    if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = rd16(sf + 4) + 1;
+                    x += 4 + slen;
+                }
+                if (bsize < 12 + xlen + 8 || bsize > 65536) { rc = PF_ERR_ARG; break; }
+                if (o + bsize > len) break;
+                pf_bgzf_blk b;
+                b.in_off = R.buf0 + o + 12 + xlen;
+                b.in_len = bsize - 12 - xlen - 8;
+                b.crc = rd32(h + bsize - 8);
+                b.isize = rd32(h + bsize - 4);
+                if (b.isize > 65536) { rc = PF_ERR_ARG; break; }
+                b.out_off = P.arena;
+                b.run = ri;
+                P.arena += b.isize;
+                P.blk.push_back(b);
+                P.caddr.push_back(R.f0 + o);
+                o += bsize;
+            }
+            R.b1 = (uint32_t)P.blk.size();
+            R.end_addr = R.f0 + o;
+            R.to_eof = R.end_addr >= fsize;
+        }
+        if (rc) break;
+        const uint32_t NB = (uint32_t)P.blk.size(), NR = (uint32_t)P.runs.size();
+        // ---- chunks -> arena positions; chain starts per run
+        auto find_blk = [&](uint64_t addr) -> int64_t {
+            const auto it = std::lower_bound(P.caddr.begin(), P.caddr.end(), addr);
+            return (it != P.caddr.end() && *it == addr) ? (int64_t)(it - P.caddr.begin()) : -1;
+        };
+        std::vector<pf_chunk_dev> ch(NC);
+        std::vector<pf_run_dev> rd(NR);
+        for (uint32_t ri = 0; ri < NR; ri++) {
+            const Range &R = P.runs[ri];
+            rd[ri].a0 = R.b0 < R.b1 ? P.blk[R.b0].out_off : P.arena;
+            rd[ri].a1 = R.b0 < R.b1 ? P.blk[R.b1 - 1].out_off + P.blk[R.b1 - 1].isize : rd[ri].a0;
+            rd[ri].chain_start = UINT64_MAX;
+            rd[ri].to_eof = R.to_eof ? 1u : 0u;
+            rd[ri].stop_pos = 0;
+            rd[ri].rec0 = rd[ri].n_rec = rd[ri].stop = 0;
+        }
+        bool more = false;
+        for (uint32_t c = 0; c < NC && !rc; c++) {
+            const uint64_t u = uv[2 * c], v = uv[2 * c + 1];
+            const int64_t bu = find_blk(u >> 16);
+            if (bu < 0 || (u & 0xFFFF) > P.blk[bu].isize) {
+                if ((u >> 16) >= fsize) { ch[c].u = ch[c].v = 0; ch[c].run = 0; continue; }
+                rc = PF_ERR_ARG;
+                break;
+            }
+            const uint32_t ri = P.blk[bu].run;
+            ch[c].u = P.blk[bu].out_off + (u & 0xFFFF);
+            ch[c].run = ri;
+            const int64_t bv = find_blk(v >> 16);
+            if (bv >= 0 && P.blk[bv].run == ri && (v & 0xFFFF) <= P.blk[bv].isize) ch[c].v = P.blk[bv].out_off + (v & 0xFFFF);
+            else if ((v >> 16) == P.runs[ri].end_addr && (v & 0xFFFF) == 0) ch[c].v = rd[ri].a1;
+            else if ((v >> 16) >= P.runs[ri].end_addr && !P.runs[ri].to_eof) { more = true; ch[c].v = rd[ri].a1; }
+            else ch[c].v = rd[ri].a1;                                   // past EOF: read to the end
+            if (ch[c].u < ch[c].v) rd[ri].chain_start = std::min(rd[ri].chain_start, ch[c].u);
+        }
+        if (rc) break;
+        if (more) { ext *= 4; continue; }
+        for (auto &R : rd) if (R.chain_start == UINT64_MAX) R.chain_start = R.a1;
+        std::vector<pf_win_dev> wd(W);
+        for (uint32_t w = 0; w < W; w++) {
+            wd[w].beg = beg[w]; wd[w].end = end[w]; wd[w].c0 = wc[w]; wd[w].c1 = wc[w + 1];
+            wd[w].tid = tid; wd[w].skip = 0; wd[w].out = 0;
+        }
+        // ---- upload + inflate
+        t0 = now_ms();
+        uint8_t *d_comp = D.alloc<uint8_t>(P.comp.size());
+        pf_bgzf_blk *d_blk = D.alloc<pf_bgzf_blk>(NB);
+        uint8_t *d_arena = D.alloc<uint8_t>(P.arena + 512);
+        uint32_t *d_bst = D.alloc<uint32_t>(NB);
+        pf_run_dev *d_run = D.alloc<pf_run_dev>(NR);
+        pf_chunk_dev *d_ch = D.alloc<pf_chunk_dev>(NC);
+        pf_win_dev *d_win = D.alloc<pf_win_dev>(W);
+        uint32_t *d_wn = D.alloc<uint32_t>(2ull * W);
+        if (!d_comp || !d_blk || !d_arena || !d_bst || !d_run || !d_ch || !d_win || !d_wn) { rc = PF_ERR_NOMEM; break; }
+        hipEvent_t ev[8];
+        for (auto &e : ev) if (hipEventCreate(&e) != hipSuccess) rc = PF_ERR_HIP;
+        if (rc) break;
+        auto evdone = [&]() { for (auto &e : ev) (void)hipEventDestroy(e); };
+        bool ok = hipMemcpyAsync(d_comp, P.comp.data(), P.comp.size(), hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_blk, P.blk.data(), sizeof(pf_bgzf_blk) * NB, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemsetAsync(d_bst, 0, 4ull * NB, st) == hipSuccess &&
+                  hipMemsetAsync(d_arena + P.arena, 0, 512, st) == hipSuccess &&
+                  hipMemcpyAsync(d_run, rd.data(), sizeof(pf_run_dev) * NR, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_ch, ch.data(), sizeof(pf_chunk_dev) * NC, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_win, wd.data(), sizeof(pf_win_dev) * W, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipEventRecord(ev[0], st) == hipSuccess;
+        if (ok) ok = pf_inflate_launch(st, d_comp, d_blk, NB, d_arena, d_bst, ev[0], ev[1]) == PF_OK &&
+                     hipEventRecord(ev[2], st) == hipSuccess;
+        // ---- chain: count, offsets, write
+        if (ok && NR) {
+            hipLaunchKernelGGL(pf_chain, dim3((NR + 63) / 64), dim3(64), 0, st, d_arena, d_run, NR, (uint64_t *)nullptr);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        std::vector<uint32_t> bst(NB);
+        ok = ok && hipMemcpyAsync(bst.data(), d_bst, 4ull * NB, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(rd.data(), d_run, sizeof(pf_run_dev) * NR, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+        if (!ok) { evdone(); rc = PF_ERR_HIP; break; }
+        for (uint32_t i = 0; i < NB; i++)
+            if (bst[i]) {
+                fprintf(stderr, "[E::pomfret_amd] BGZF block at file offset %llu: device inflate status %u\n",
+                        (unsigned long long)P.caddr[i], bst[i]);
+                rc = PF_ERR_ARG;
+                break;
+            }
+        if (rc) { evdone(); break; }
+        uint64_t NRec = 0;
+        for (auto &R : rd) { R.rec0 = (uint32_t)NRec; NRec += R.n_rec; }
+        if (NRec >= (1ull << 32)) { evdone(); rc = PF_ERR_LIMIT; break; }
+        pf_recs_dev Rv;
+        Rv.pos = D.alloc<uint64_t>(NRec); Rv.cig = D.alloc<uint64_t>(NRec); Rv.seq = D.alloc<uint64_t>(NRec);
+        Rv.qn = D.alloc<uint64_t>(NRec); Rv.mm = D.alloc<uint64_t>(NRec); Rv.ml = D.alloc<uint64_t>(NRec);
+        Rv.md = D.alloc<uint64_t>(NRec);
+        Rv.bs = D.alloc<uint32_t>(NRec); Rv.l_qseq = D.alloc<uint32_t>(NRec); Rv.ncig = D.alloc<uint32_t>(NRec);
+        Rv.rlen = D.alloc<uint32_t>(NRec); Rv.qn_len = D.alloc<uint32_t>(NRec); Rv.mm_len = D.alloc<uint32_t>(NRec);
+        Rv.ml_len = D.alloc<uint32_t>(NRec); Rv.md_len = D.alloc<uint32_t>(NRec);
+        Rv.tid = D.alloc<int32_t>(NRec); Rv.rpos = D.alloc<int32_t>(NRec); Rv.hp_tag = D.alloc<int32_t>(NRec);
+        Rv.de = D.alloc<float>(NRec); Rv.flag = D.alloc<uint16_t>(NRec);
+        Rv.mapq = D.alloc<uint8_t>(NRec); Rv.hp = D.alloc<uint8_t>(NRec); Rv.st = D.alloc<uint8_t>(NRec);
+        if (!Rv.pos || !Rv.st || !Rv.hp || !Rv.mapq || !Rv.flag || !Rv.de || !Rv.hp_tag || !Rv.rpos || !Rv.tid ||
+            !Rv.md_len || !Rv.ml_len || !Rv.mm_len || !Rv.qn_len || !Rv.rlen || !Rv.ncig || !Rv.l_qseq || !Rv.bs ||
+            !Rv.md || !Rv.ml || !Rv.mm || !Rv.qn || !Rv.seq || !Rv.cig) { evdone(); rc = PF_ERR_NOMEM; break; }
+        ok = hipMemcpyAsync(d_run, rd.data(), sizeof(pf_run_dev) * NR, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipEventRecord(ev[3], st) == hipSuccess;
+        if (ok && NR) {
+            hipLaunchKernelGGL(pf_chain, dim3((NR + 63) / 64), dim3(64), 0, st, d_arena, d_run, NR, Rv.pos);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        if (ok && NRec) {
+            hipLaunchKernelGGL(pf_recdec, dim3((unsigned)((NRec + 3) / 4)), dim3(256), 0, st, d_arena, (uint32_t)NRec, Rv);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        ok = ok && hipEventRecord(ev[4], st) == hipSuccess;
+        if (ok && W) {
+            hipLaunchKernelGGL(pf_select, dim3((W + 3) / 4), dim3(256), 0, st, d_win, W, d_ch, d_run, Rv, 0u, d_wn,
+                               d_wn + W, (uint32_t *)nullptr);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        std::vector<uint32_t> wn(2ull * W);
+        ok = ok && hipMemcpyAsync(wn.data(), d_wn, 8ull * W, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+        if (!ok) { evdone(); rc = PF_ERR_HIP; break; }
+        bool need_more = false;
+        uint64_t n_trunc = 0;
+        for (uint32_t w = 0; w < W; w++) {
+            if (wn[W + w] == PF_WIN_MORE) need_more = true;
+            else if (wn[W + w] == PF_WIN_ERR) rc = PF_ERR_ARG;
+            else if (wn[W + w] == PF_WIN_TRUNC) n_trunc++;
+        }
+        if (rc) { evdone(); break; }
+        if (need_more) { evdone(); ext *= 4; continue; }
+        // ---- record lists: windows over the limit are emptied
+        F->win_n.assign(wn.begin(), wn.begin() + W);
+        F->win_status.assign(wn.begin() + W, wn.end());
+        F->win_rec_off.assign(W + 1, 0);
+        for (uint32_t w = 0; w < W; w++) {
+            const bool skip = max_win_recs && wn[w] > max_win_recs;
+            wd[w].skip = skip ? 1u : 0u;
+            wd[w].out = F->win_rec_off[w];
+            F->win_rec_off[w + 1] = F->win_rec_off[w] + (skip ? 0u : wn[w]);
+        }
+        const uint64_t NS = F->win_rec_off[W];
+        if (NS >= (1ull << 32)) { evdone(); rc = PF_ERR_LIMIT; break; }
+        uint32_t *d_sel = D.alloc<uint32_t>(NS);
+        if (!d_sel) { evdone(); rc = PF_ERR_NOMEM; break; }
+        ok = hipMemcpyAsync(d_win, wd.data(), sizeof(pf_win_dev) * W, hipMemcpyHostToDevice, st) == hipSuccess;
+        if (ok && W) {
+            hipLaunchKernelGGL(pf_select, dim3((W + 3) / 4), dim3(256), 0, st, d_win, W, d_ch, d_run, Rv, 1u, d_wn,
+                               d_wn + W, d_sel);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        // ---- small fields of the selected records -> host
+        Small &S = F->s;
+        S.resize(NS);
+        uint16_t *g_flag = D.alloc<uint16_t>(NS);
+        uint8_t *g_mapq = D.alloc<uint8_t>(NS), *g_hp = D.alloc<uint8_t>(NS), *g_st = D.alloc<uint8_t>(NS);
+        uint32_t *g32 = D.alloc<uint32_t>(8 * NS);
+        float *g_de = D.alloc<float>(NS);
+        int32_t *g_hpt = D.alloc<int32_t>(NS);
+        if (!g_flag || !g_mapq || !g_hp || !g_st || !g32 || !g_de || !g_hpt) { evdone(); rc = PF_ERR_NOMEM; break; }
+        if (ok && NS) {
+            hipLaunchKernelGGL(pf_gather_small, dim3((unsigned)((NS + 255) / 256)), dim3(256), 0, st, d_sel, NS, Rv,
+                               g_flag, g_mapq, g32, g32 + NS, g_de, g_hp, g_hpt, g32 + 2 * NS, g32 + 3 * NS,
+                               g32 + 4 * NS, g32 + 5 * NS, g32 + 6 * NS, g32 + 7 * NS, g_st);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        ok = ok && hipEventRecord(ev[5], st) == hipSuccess;
+        std::vector<uint32_t> h32(8 * NS);
+        ok = ok && hipMemcpyAsync(S.flag.data(), g_flag, 2 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(S.mapq.data(), g_mapq, NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(S.hp.data(), g_hp, NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(S.st.data(), g_st, NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(h32.data(), g32, 32 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(S.de.data(), g_de, 4 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(S.hp_tag.data(), g_hpt, 4 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+        if (!ok) { evdone(); rc = PF_ERR_HIP; break; }
+        memcpy(S.pos.data(), h32.data(), 4 * NS);
+        memcpy(S.l_qseq.data(), h32.data() + NS, 4 * NS);
+        memcpy(S.ncig.data(), h32.data() + 2 * NS, 4 * NS);
+        memcpy(S.mm_len.data(), h32.data() + 3 * NS, 4 * NS);
+        memcpy(S.ml_len.data(), h32.data() + 4 * NS, 4 * NS);
+        memcpy(S.qn_len.data(), h32.data() + 5 * NS, 4 * NS);
+        memcpy(S.md_len.data(), h32.data() + 6 * NS, 4 * NS);
+        memcpy(S.rlen.data(), h32.data() + 7 * NS, 4 * NS);
+        // ---- qnames (and MD) -> host
+        F->qn_off.assign(NS + 1, 0);
+        F->md_off.assign(NS + 1, 0);
+        for (uint64_t i = 0; i < NS; i++) {
+            F->qn_off[i + 1] = F->qn_off[i] + S.qn_len[i];
+            F->md_off[i + 1] = F->md_off[i] + S.md_len[i];
+        }
+        F->qn.resize(F->qn_off[NS] + 1);
+        uint64_t *d_qo = D.alloc<uint64_t>(NS + 1);
+        uint8_t *d_qn = D.alloc<uint8_t>(F->qn_off[NS] + 1);
+        if (!d_qo || !d_qn) { evdone(); rc = PF_ERR_NOMEM; break; }
+        ok = hipMemcpyAsync(d_qo, F->qn_off.data(), 8 * (NS + 1), hipMemcpyHostToDevice, st) == hipSuccess;
+        if (ok && NS) {
+            hipLaunchKernelGGL(pf_gather_big, dim3((unsigned)((NS + 3) / 4)), dim3(256), 0, st, d_arena, d_sel, NS, Rv,
+                               (const uint64_t *)nullptr, (uint32_t *)nullptr, (const uint64_t *)nullptr,
+                               (uint8_t *)nullptr, (const uint64_t *)nullptr, (uint8_t *)nullptr,
+                               (const uint64_t *)nullptr, (uint8_t *)nullptr, d_qo, d_qn, (const uint64_t *)nullptr,
+                               (uint8_t *)nullptr);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        ok = ok && hipMemcpyAsync(F->qn.data(), d_qn, F->qn_off[NS], hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+        if (!ok) { evdone(); rc = PF_ERR_HIP; break; }
+        // ---- the record-level batch: sizes on the host, large arrays gathered on the device
+        std::vector<uint64_t> cig_off(NS + 1, 0), mm_off(NS + 1, 0), ml_off(NS + 1, 0);
+        for (uint64_t i = 0; i < NS; i++) {
+            cig_off[i + 1] = cig_off[i] + S.ncig[i];
+            mm_off[i + 1] = mm_off[i] + S.mm_len[i];
+            ml_off[i + 1] = ml_off[i] + S.ml_len[i];
+        }
+        pf_aln_batch_t a;
+        memset(&a, 0, sizeof a);
+        a.n_windows = W;
+        a.n_recs = (uint32_t)NS;
+        a.win_start = ws; a.win_end = we; a.win_rec_off = F->win_rec_off.data();
+        a.flag = S.flag.data(); a.mapq = S.mapq.data(); a.pos = S.pos.data(); a.l_qseq = S.l_qseq.data();
+        a.de = S.de.data(); a.hp = S.hp.data();
+        a.cigar_off = cig_off.data(); a.mm_off = mm_off.data(); a.ml_off = ml_off.data();
+        DevFill df{d_arena, d_sel, NS, Rv, nullptr, nullptr, nullptr, st};
+        pf_aln_fill_t fl{dev_fill, &df};
+        ok = hipEventRecord(ev[6], st) == hipSuccess;
+        rc = ok ? pf_aln_build(ctx, cfg, lc, &a, &fl, out) : PF_ERR_HIP;
+        ok = hipEventRecord(ev[7], st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+        float ms_inf = 0, ms_chain = 0, ms_dec = 0, ms_sel = 0, ms_build = 0;
+        if (ok) {
+            (void)hipEventElapsedTime(&ms_inf, ev[0], ev[1]);
+            (void)hipEventElapsedTime(&ms_chain, ev[2], ev[3]);
+            (void)hipEventElapsedTime(&ms_dec, ev[3], ev[4]);
+            (void)hipEventElapsedTime(&ms_sel, ev[4], ev[5]);
+            (void)hipEventElapsedTime(&ms_build, ev[6], ev[7]);
+        }
+        evdone();
+        if (rc) break;
+        pf_bam_dev_fetch_t &pub = F->pub;
+        pub.n_windows = W;
+        pub.n_recs = NS;
+        pub.win_rec_off = F->win_rec_off.data();
+        pub.win_n_fetched = F->win_n.data();
+        pub.qname_off = F->qn_off.data();
+        pub.qname = F->qn.data();
+        pub.hp_tag = F->s.hp_tag.data();
+        pub.n_truncated = n_trunc;
+        pub.comp_bytes = tot;
+        pub.inflated_bytes = P.arena;
+        pub.n_blocks = NB;
+        pub.n_chain_recs = NRec;
+        pub.ms_read = t_read;
+        pub.ms_inflate = ms_inf;
+        pub.ms_chain = ms_chain;
+        pub.ms_decode = ms_dec;
+        pub.ms_select = ms_sel;
+        pub.ms_build = ms_build;
+        pub.ms_total = now_ms() - t_start;
+        pub.attempts = (uint32_t)attempt + 1;
+        break;
+    }
+    close(fd);
+    if (rc || !*out) {
+        if (*out) { pf_batch_free(*out); *out = nullptr; }
+        delete F;
+        return rc ? rc : PF_ERR_INTERNAL;
+    }
+    *fetch_out = &F->pub;
+    return PF_OK;
+}

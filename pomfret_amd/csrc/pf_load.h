@@ -108,4 +108,23 @@ struct pf_load_dev {
     uint8_t *call_cat;
 };
 
+#ifdef __cplusplus
+/* placement of a record-level batch's large arrays (pf_aln_build, pf_api.hip):
+ * fill() writes ld->cigar / mm / ml (sized by the batch's offsets) and the
+ * SEQ slices (seq_off[r], 16-byte aligned, zero padded; seq_bytes total) */
+struct pf_ctx;
+struct pf_dbatch;
+typedef struct pf_aln_fill {
+    int (*fill)(void *user, struct pf_ctx *ctx, pf_load_dev *ld, const uint64_t *seq_off, uint64_t seq_bytes);
+    void *user;
+} pf_aln_fill_t;
+struct pf_cfg;
+struct pf_load_cfg;
+struct pf_aln_batch;
+/* a record-level batch from the records' lengths and small fields (host
+ * arrays of a; its cigar / seq / mm / ml pointers are not read) */
+extern "C" int pf_aln_build(struct pf_ctx *ctx, const struct pf_cfg *cfg, const struct pf_load_cfg *lc,
+                            const struct pf_aln_batch *a, const pf_aln_fill_t *fill, struct pf_dbatch **out);
+#endif
+
 #endif

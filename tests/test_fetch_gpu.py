@@ -1,0 +1,128 @@
+"""f1 on the device: pf_batch_upload_bam (BGZF inflate, record chain, record
+decode, window chunk walk and gather on the GPU) against the host reader
+pf_bam_fetch_windows on the same BAM -- the batch's record arrays, qnames and
+raw HP values bit for bit, then the methphase decisions.  BAMs are written by
+the test-side writer (tests/_bamio.py, htslib's block and index rules)."""
+import struct
+
+import numpy as np
+import pytest
+
+from tests import _bamio
+from tests._fixtures import tagged
+
+pytestmark = pytest.mark.gpu
+
+
+def _compare(host, hqn, hinfo, db, dqn, dinfo):
+    assert np.array_equal(dinfo["win_rec_off"], host.win_rec_off)
+    d = db.debug_recs()
+    for k in ("flag", "mapq", "pos", "l_qseq", "hp", "cigar_off", "cigar", "mm_off", "mm", "ml_off", "ml"):
+        assert np.array_equal(d[k], getattr(host, k)), k
+    assert np.array_equal(d["de"].view(np.uint32), host.de.view(np.uint32))
+    so = d["seq_off"]
+    for i in range(host.n_recs):
+        nb = (int(host.l_qseq[i]) + 1) // 2
+        a = host.seq[host.seq_off[i]:host.seq_off[i] + nb]
+        b = d["seq"][so[i]:so[i] + nb]
+        assert np.array_equal(a, b), i
+        assert not d["seq"][so[i] + nb:so[i + 1]].any()
+    assert dqn == hqn
+    assert np.array_equal(dinfo["hp_tag"], hinfo["hp_tag"])
+    assert dinfo["n_truncated"] == hinfo["n_truncated"]
+
+
+def _both(ctx, bam, chrom, ws, we, cfg, lcfg, **kw):
+    from pomfret_amd.bam import BamFile
+    with BamFile(bam) as b:
+        host, hqn, hinfo = b.fetch_windows(chrom, ws, we, threads=4)
+        db, dqn, dinfo = b.fetch_windows_device(ctx, cfg, chrom, ws, we, lcfg, **kw)
+    return host, hqn, hinfo, db, dqn, dinfo
+
+
+def test_device_fetch_tagged(gpu_ctx, tmp_path):
+    from pomfret_amd import Config, LoadConfig
+    aln, recs, bam, vcf = tagged(tmp_path, n_windows=4, coverage=30)
+    cfg, lcfg = Config.from_coverage(30, given=False), LoadConfig()
+    # the gap windows, plus windows shifted into their neighbours' readback
+    ws = np.concatenate([aln.win_start, aln.win_start + 40_000, [0, 190_000_000]]).astype(np.uint32)
+    we = np.concatenate([aln.win_end, aln.win_end + 40_000, [10, 190_000_010]]).astype(np.uint32)
+    host, hqn, hinfo, db, dqn, dinfo = _both(gpu_ctx, bam, "chrS", ws, we, cfg, lcfg)
+    assert host.n_recs > 0 and dinfo["n_blocks"] > 0
+    _compare(host, hqn, hinfo, db, dqn, dinfo)
+    out = db.run()
+    ref = gpu_ctx.upload_aln(cfg, host, lcfg).run()
+    for f in ("decision", "dir_table", "win_n_reads", "read_hp"):
+        assert np.array_equal(getattr(out, f), getattr(ref, f)), f
+    print(f"\n[fetch] {host.n_recs} records, {dinfo['n_blocks']} blocks, {dinfo['comp_bytes'] / 1e6:.1f} MB -> "
+          f"{dinfo['inflated_bytes'] / 1e6:.1f} MB; inflate {dinfo['ms_inflate']:.3f} ms, chain "
+          f"{dinfo['ms_chain']:.3f}, decode {dinfo['ms_decode']:.3f}, select+small {dinfo['ms_select']:.3f}, "
+          f"build {dinfo['ms_build']:.3f}, total {dinfo['ms_total']:.1f} ms")
+
+
+def _odd_records(tmp_path):
+    """Records exercising the decoder: Mm/Ml tags, an ML of another type, a
+    malformed tag ending the aux walk, a CG:B:I long CIGAR, a record of
+    ~600 KB (spans many blocks: the plan must widen), a CIGAR/SEQ length
+    mismatch (the fetch of its window ends there), HP:i:0 / missing de."""
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    aln = make_aln_batch(AlnSpec(n_windows=3, coverage=20, seed=9, len_scale=0.3), workers=1)
+    recs = _bamio.records_from_aln(aln, hp_zero_every=7, de_absent_every=5)
+    w1 = int(aln.win_rec_off[1])
+    rng = np.random.default_rng(2)
+
+    def ren(r, a, b):
+        r.aux = r.aux.replace(a, b, 1)
+
+    ren(recs[3], b"MMZ", b"MmZ")
+    ren(recs[3], b"MLBC", b"MlBC")
+    i = recs[5].aux.find(b"MLBC")                               # ML:B:S -- not B:C, the read gets no calls
+    assert i >= 0
+    cnt = struct.unpack_from("<I", recs[5].aux, i + 4)[0]
+    recs[5].aux = recs[5].aux[:i] + b"MLBS" + struct.pack("<I", cnt) + bytes(2 * cnt) + recs[5].aux[i + 8 + cnt:]
+    recs[7].aux = b"XXq\x01" + recs[7].aux                     # unknown type: the walk stops
+    r = recs[9]                                                 # CG:B:I long CIGAR
+    real = list(r.cigar)
+    rl = _bamio.ref_len(real)
+    r.cigar = [(r.l_seq << 4) | 4, (rl << 4) | 3]
+    r.aux = r.aux + _bamio.aux_BI("CG", real)
+    big = recs[11]                                              # ~600 KB record
+    n = 400_000
+    s = rng.integers(1, 16, n, dtype=np.uint8)
+    big.l_seq = n
+    big.seq = bytes((s[0::2] << 4) | s[1::2])
+    big.cigar = [(n << 4) | 0]
+    big.aux = _bamio.aux_i("HP", 1)
+    bad = recs[w1 + 4]                                          # query length != l_seq
+    bad.cigar = list(bad.cigar) + [(3 << 4) | 1]
+    bam = str(tmp_path / "odd.bam")
+    _bamio.write_bam(bam, [("chrS", 200_000_000)], recs)
+    return aln, bam
+
+
+def test_device_fetch_odd_records(gpu_ctx, tmp_path):
+    from pomfret_amd import Config, LoadConfig
+    aln, bam = _odd_records(tmp_path)
+    cfg, lcfg = Config.from_coverage(20, given=False), LoadConfig()
+    host, hqn, hinfo, db, dqn, dinfo = _both(gpu_ctx, bam, "chrS", aln.win_start, aln.win_end, cfg, lcfg)
+    assert hinfo["n_truncated"] >= 1
+    _compare(host, hqn, hinfo, db, dqn, dinfo)
+    out = db.run()
+    ref = gpu_ctx.upload_aln(cfg, host, lcfg).run()
+    assert np.array_equal(out.decision, ref.decision)
+    assert np.array_equal(out.read_hp, ref.read_hp)
+
+
+def test_device_fetch_record_limit(gpu_ctx, tmp_path):
+    from pomfret_amd import Config, LoadConfig
+    from pomfret_amd.bam import BamFile
+    aln, recs, bam, vcf = tagged(tmp_path, n_windows=3, coverage=30, seed=4)
+    cfg = Config.from_coverage(30, given=False)
+    with BamFile(bam) as b:
+        host, _, _ = b.fetch_windows("chrS", aln.win_start, aln.win_end)
+        per = np.diff(host.win_rec_off.astype(np.int64))
+        lim = int(np.sort(per)[1])                           # the largest window is over the limit
+        db, qn, info = b.fetch_windows_device(gpu_ctx, cfg, "chrS", aln.win_start, aln.win_end, max_win_recs=lim)
+    got = np.diff(info["win_rec_off"].astype(np.int64))
+    assert np.array_equal(info["win_n_fetched"], per)
+    assert np.array_equal(got, np.where(per > lim, 0, per))
