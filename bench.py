@@ -158,6 +158,82 @@ def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 2
     return n_reads * reps / dt, dt, reps
 
 
+def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu: bool = True):
+    """End to end from files (never `value`): the first n_windows windows of
+    the workload written as a BAM + BAI (QUAL strings included, zlib level 6,
+    tests/_bamio.py's writer), then per path the wall time from the BAM file to
+    decisions on the host:
+      device_fetch: BAI plan + compressed blocks read on the host, inflate /
+                    record chain / window fetch / gather / K0..K3 on the GPU
+                    (pf_batch_upload_bam + pf_methphase_run);
+      host_fetch:   the host reader inflates and decodes (pf_bam_fetch_windows,
+                    `threads` threads), upload_aln, K0..K3;
+      cpu_port:     the host reader + the oracle's record-level path on
+                    `threads` threads (the reference's structure: htslib decode
+                    + the kt_for worker)."""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import _bamio
+    from pomfret_amd.bam import BamFile
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    t = time.perf_counter()
+    aln = make_aln_batch(AlnSpec(n_windows=n_windows, coverage=wl["coverage"], gap=wl["gap"], seed=1000),
+                         workers=threads)
+    recs = _bamio.records_from_aln(aln, qual=True)
+    path = os.path.join(workdir, f"pf_e2e_{os.getpid()}.bam")
+    _bamio.write_bam(path, [("chrS", 2_000_000_000)], recs, workers=threads, level=6)
+    del recs
+    gen_s = time.perf_counter() - t
+    ws, we = aln.win_start, aln.win_end
+    res = {"windows": n_windows, "records": int(aln.n_recs), "bam_bytes": os.path.getsize(path),
+           "threads": threads, "gen_s": round(gen_s, 1)}
+    try:
+        with BamFile(path) as b:
+            dev = None
+            for rep in range(2):                        # the second (warm) pass is reported
+                t0 = time.perf_counter()
+                db, qn, info = b.fetch_windows_device(ctx, cfg, "chrS", ws, we, lcfg)
+                t1 = time.perf_counter()
+                out = db.run()
+                t2 = time.perf_counter()
+                reads = int(out.win_n_reads.sum())
+                dec_dev = out.decision.copy()
+                db.free()
+                dev = {"reads_per_s": round(reads / (t2 - t0), 1), "ms": round((t2 - t0) * 1e3, 1),
+                       "fetch_ms": round((t1 - t0) * 1e3, 1), "run_ms": round((t2 - t1) * 1e3, 1),
+                       "inflate_ms": round(info["ms_inflate"], 2), "read_ms": round(info["ms_read"], 1),
+                       "chain_ms": round(info["ms_chain"], 2), "decode_ms": round(info["ms_decode"], 2),
+                       "select_ms": round(info["ms_select"], 2), "build_ms": round(info["ms_build"], 1),
+                       "compressed_bytes": int(info["comp_bytes"]), "inflated_bytes": int(info["inflated_bytes"]),
+                       "inflate_GBps": round(info["inflated_bytes"] / max(info["ms_inflate"], 1e-6) / 1e6, 2)}
+            res["reads"] = reads
+            res["device_fetch"] = dev
+            t0 = time.perf_counter()
+            got, qn_h, _ = b.fetch_windows("chrS", ws, we, threads=threads)
+            t1 = time.perf_counter()
+            db = ctx.upload_aln(cfg, got, lcfg)
+            out = db.run()
+            t2 = time.perf_counter()
+            db.free()
+            res["host_fetch"] = {"reads_per_s": round(reads / (t2 - t0), 1), "ms": round((t2 - t0) * 1e3, 1),
+                                 "fetch_ms": round((t1 - t0) * 1e3, 1), "upload_run_ms": round((t2 - t1) * 1e3, 1)}
+            res["decisions_match"] = bool(np.array_equal(out.decision, dec_dev))
+            if cpu:
+                import oracle
+                t3 = time.perf_counter()
+                ref = oracle.methphase_aln(cfg, lcfg, got, n_threads=threads)
+                t4 = time.perf_counter()
+                res["cpu_port"] = {"reads_per_s": round(reads / ((t1 - t0) + (t4 - t3)), 1),
+                                   "ms": round(((t1 - t0) + (t4 - t3)) * 1e3, 1),
+                                   "what": f"host fetch ({threads} threads) + oracle record-level worker "
+                                           f"({threads} threads)"}
+                res["decisions_match"] = res["decisions_match"] and bool(np.array_equal(ref.decision, dec_dev))
+    finally:
+        os.unlink(path)
+        if os.path.exists(path + ".bai"):
+            os.unlink(path + ".bai")
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,6 +246,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-legs", action="store_true", help="skip the calls-level and PCIe-inclusive legs")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--e2e-windows", type=int, default=64,
+                    help="windows of the end-to-end (BAM file -> decisions) leg; 0 skips it")
     ap.add_argument("--calls-level", action="store_true",
                     help="time the calls-level boundary (reads + 5mC calls resident, no K0)")
     args = ap.parse_args()
@@ -371,6 +449,13 @@ def main():
                                   "efficiency": round(eff, 3) if eff else None},
                "t32_linear_estimate": round(v_cpu * 32 / threads, 1)}
 
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_legs and args.e2e_windows > 0:
+        threads = args.cpu_threads or min(CPU_SHARE, len(os.sched_getaffinity(0)))
+        e2e = e2e_leg(ctx, cfg, lcfg, wl, min(args.e2e_windows, wl["n_windows"]), threads,
+                      os.environ.get("TMPDIR", "/tmp"), cpu=not args.no_cpu)
+        log(f"[bench] e2e: {json.dumps(e2e)}")
+
     par = f"windows dealt over dp{world}" + (" (weak: per-rank batches)" if args.weak else " (strong: one job)")
     res = {
         "metric": "aligned reads/sec (methphase kernel)",
@@ -409,6 +494,7 @@ def main():
         # 16-thread port scaled linearly to 32 threads (an upper bound for it)
         "vs_cpu_t32_estimate": round(value / cpu["t32_linear_estimate"], 2) if cpu else None,
         "pcie_inclusive": pcie,
+        "e2e": e2e,
         "calls_level": calls_leg,
         "decisions": {"cis": int((out.decision == 0).sum()), "trans": int((out.decision == 1).sum()),
                       "none": int((out.decision < 0).sum())},

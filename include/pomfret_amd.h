@@ -464,6 +464,9 @@ typedef struct pf_bam_dev_fetch {
     double ms_read, ms_inflate, ms_chain, ms_decode, ms_select, ms_build, ms_total;
     uint32_t attempts;             /* plans tried (a record past the planned blocks widens the plan) */
 } pf_bam_dev_fetch_t;
+/* replace a record-level batch's per-record HP values (the -u table's tags,
+ * blockjoin.c:1114-1122); n must equal its record count */
+int  pf_batch_set_hp(pf_dbatch_t *db, const uint8_t *hp, uint32_t n);
 int  pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lcfg, pf_bam_t *bam,
                          const char *chrom, uint32_t n_windows, const uint32_t *win_start, const uint32_t *win_end,
                          uint32_t readback, uint32_t max_win_recs, pf_dbatch_t **out, pf_bam_dev_fetch_t **fetch);
@@ -589,6 +592,8 @@ typedef struct pf_methphase_opts {
                                       LPT partition gives `rank` (world <= 1: all of them)      */
     uint32_t job_windows;          /* max windows per job (0: 1024)                            */
     int32_t verbose;               /* < 0: no progress messages                                */
+    int32_t host_fetch;            /* 1: records fetched and decoded on the host (pf_bam_fetch_windows
+                                      + pf_batch_upload_aln); 0: the device fetch (pf_batch_upload_bam) */
 } pf_methphase_opts_t;
 
 typedef struct pf_mp_plan pf_mp_plan_t;

@@ -1206,6 +1206,15 @@ extern "C" int64_t pf_batch_debug_calls(pf_dbatch_t *b, uint64_t *call_off, uint
     return (int64_t)b->N;
 }
 
+extern "C" int pf_batch_set_hp(pf_dbatch_t *b, const uint8_t *hp, uint32_t n) {
+    if (!b || !b->has_aln || n != b->ld.n_recs || (n && !hp)) return PF_ERR_ARG;
+    if (!n) return PF_OK;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    HIPCHK(hipMemcpy(const_cast<uint8_t *>(b->ld.hp), hp, n, hipMemcpyHostToDevice));
+    return PF_OK;
+}
+
 extern "C" int pf_batch_debug_recs(pf_dbatch_t *b, uint64_t *sizes, uint16_t *flag, uint8_t *mapq, uint32_t *pos,
                                    uint32_t *l_qseq, float *de, uint8_t *hp, uint64_t *cigar_off, uint32_t *cigar,
                                    uint64_t *seq_off, uint8_t *seq, uint64_t *mm_off, uint8_t *mm, uint64_t *ml_off,

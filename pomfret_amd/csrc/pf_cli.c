@@ -12,7 +12,8 @@
  * cliopt_haptag_t (cli.c:332-343); the -c arithmetic (cov/10, cov/4), the
  * order-dependent -n override and varhaptag's --write-bam (which there turns
  * the BAM output OFF, cli.c:416) are kept.  Added: --gpus G (GPUs driven by
- * this process; default all visible) and --job-windows W (windows per device
+ * this process; default all visible), --host-fetch (records inflated and
+ * decoded on the host instead of the device fetch) and --job-windows W (windows per device
  * job).  --gtf / --tsv phase-block inputs are not implemented (an error, not
  * a silent skip).
  */
@@ -59,10 +60,11 @@ static void help_methphase(const char *prefix) {
     fprintf(stderr, "  --output-tsv [opt] Also write {prefix}.mp.tsv.\n");
     fprintf(stderr, "  --write-bam  [opt] Also write {prefix}.mp.bam (+ .bai) with the new HP tags.\n");
     fprintf(stderr, "  --gpus [opt] GPUs to use. [all visible]\n");
+    fprintf(stderr, "  --host-fetch [opt] Inflate and decode BAM records on the host instead of the GPU.\n");
 }
 
 enum { O_LO = 301, O_HI, O_GTF = 304, O_VCF = 306, O_MAPQ, O_TSV, O_WBAM, O_OTSV, O_BAMT, O_UNTAG, O_WIT,
-       O_CSIZE, O_CSTRIDE, O_HELP = 400, O_DBG, O_GPUS = 500, O_JOBW };
+       O_CSIZE, O_CSTRIDE, O_HELP = 400, O_DBG, O_GPUS = 500, O_JOBW, O_HFETCH };
 
 static const struct option longopts[] = {
     {"lo", required_argument, 0, O_LO},          {"hi", required_argument, 0, O_HI},
@@ -74,11 +76,12 @@ static const struct option longopts[] = {
     {"chunk-size", required_argument, 0, O_CSIZE}, {"chunk-stride", required_argument, 0, O_CSTRIDE},
     {"help", no_argument, 0, O_HELP},            {"dbg", no_argument, 0, O_DBG},
     {"gpus", required_argument, 0, O_GPUS},      {"job-windows", required_argument, 0, O_JOBW},
+    {"host-fetch", no_argument, 0, O_HFETCH},
     {0, 0, 0, 0}};
 
 typedef struct {
     int help, threads, lo, hi, readlen, mapq, k, k_span, cov, cov_sel, n_cand, untagged, out_tsv, out_bam;
-    int chunk_size, chunk_stride, gpus, job_windows, verbose;
+    int chunk_size, chunk_stride, gpus, job_windows, verbose, host_fetch;
     char *prefix, *vcf, *gtf, *tsv, *bam;
 } cli_t;
 
@@ -116,6 +119,7 @@ static int parse(int argc, char **argv, cli_t *c) {
         case O_DBG: break;
         case O_GPUS: c->gpus = atoi(optarg); break;
         case O_JOBW: c->job_windows = atoi(optarg); break;
+        case O_HFETCH: c->host_fetch = 1; break;
         default:
             fprintf(stderr, "[E::parse_cli] unknown or incomplete option \"%s\"\n", argv[optind - 1]);
             return 1;
@@ -254,6 +258,7 @@ int main(int argc, char **argv) {
     o.threads = c.threads;
     o.n_devices = c.gpus;
     o.job_windows = c.job_windows > 0 ? (uint32_t)c.job_windows : 0;
+    o.host_fetch = c.host_fetch;
     o.verbose = c.verbose;
     pf_mp_plan_t *p = NULL;
     const int rc = pf_methphase_main(&o, &p);

@@ -449,10 +449,6 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
         }
         // ---- the block's symbols
         for (;;) {
-            o.a = uni64(o.a);
-            o.cb = uni64(o.cb);
-            o.any = uni(o.any);
-            b.over = uni(b.over);
             bits_fill(b, lane);
             uint32_t e = uni(T.lroot[(uint32_t)b.buf & ((1u << INF_LROOT) - 1u)]);
             uint32_t l = e >> 9, s = e & 511u;

@@ -840,6 +840,104 @@ static int job_device(pf_mp_plan_t *p, pf_ctx_t *ctx, job_t *J, fetch_t *f) {
     return rc;
 }
 
+/* one job through the device fetch (pf_batch_upload_bam): the host plans the
+ * fetch from the BAI and reads compressed blocks, the device inflates,
+ * selects and gathers the windows' records; a window over the record limit
+ * stays undecided (as job_device), a batch the device refuses for another
+ * limit goes through the host path window by window */
+static int job_device_fetch(pf_mp_plan_t *p, pf_ctx_t *ctx, pf_bam_t *bam, job_t *J) {
+    const uint32_t n = J->w1 - J->w0;
+    if (p->tid[J->contig] < 0 || !n) {
+        fetch_t f = {NULL, PF_OK};
+        return job_device(p, ctx, J, &f);
+    }
+    const pf_cfg_t *cf = &p->cfg[J->contig];
+    pf_load_cfg_t lc = p->o.load;
+    pf_dbatch_t *db = NULL;
+    pf_bam_dev_fetch_t *F = NULL;
+    int rc = pf_batch_upload_bam(ctx, cf, &lc, bam, p->gaps->names[J->contig], n, p->win_start + J->w0,
+                                 p->win_end + J->w0, PF_READBACK, PF_MAX_WIN_RECS, &db, &F);
+    if (rc == PF_ERR_LIMIT) {                   /* per window on the host path */
+        fetch_t f;
+        rc = job_fetch(p, bam, J, &f);
+        if (!rc) rc = job_device(p, ctx, J, &f);
+        if (f.recs) pf_bam_records_free(f.recs);
+        return rc;
+    }
+    if (rc) return rc;
+    const uint64_t NR = F->n_recs;
+    int8_t *dec = (int8_t *)malloc(n);
+    uint64_t *cnt = (uint64_t *)calloc(n + 1, sizeof(uint64_t));
+    uint32_t *rec_of = (uint32_t *)malloc((NR ? NR : 1) * sizeof(uint32_t));
+    uint8_t *rhp = (uint8_t *)malloc(NR ? NR : 1);
+    uint8_t *hp = NULL;
+    entlist_t ent = {0};
+    uint32_t n_limit = 0;
+    if (!dec || !cnt || !rec_of || !rhp) rc = PF_ERR_NOMEM;
+    for (uint32_t w = 0; w < n && !rc; w++) {
+        dec[w] = -1;
+        if (F->win_n_fetched[w] > PF_MAX_WIN_RECS) {
+            fprintf(stderr, "[W::pomfret_amd] %s:%u-%u: %u records exceed the device limit of %u reads per window; "
+                    "left undecided\n", p->gaps->names[J->contig], p->win_start[J->w0 + w], p->win_end[J->w0 + w],
+                    F->win_n_fetched[w], PF_MAX_WIN_RECS);
+            n_limit++;
+        }
+    }
+    if (!rc && p->o.untagged && NR) {           /* the -u table replaces HP (1114-1122) */
+        hp = (uint8_t *)malloc(NR);
+        if (!hp) rc = PF_ERR_NOMEM;
+        if (!rc) {
+            const int64_t g = pf_tags_get(p->raw, (uint32_t)NR, F->qname_off, F->qname, 254, hp);
+            if (g < 0) rc = (int)g;
+        }
+        if (!rc) rc = pf_batch_set_hp(db, hp, (uint32_t)NR);
+    }
+    if (!rc) {
+        pf_window_out_t o;
+        memset(&o, 0, sizeof o);
+        o.decision = dec;
+        o.read_hp = rhp;
+        rc = pf_methphase_run(ctx, db, &o);
+    }
+    uint32_t R_ = 0;
+    if (!rc) {
+        R_ = pf_batch_n_reads(db);
+        if (R_ > NR) rc = PF_ERR_INTERNAL;
+    }
+    if (!rc && R_) rc = pf_batch_read_recs(db, rec_of, (uint32_t)(NR ? NR : 1));
+    if (!rc) {
+        uint32_t i = 0;
+        for (uint32_t w = 0; w < n && !rc; w++) {
+            if (F->win_n_fetched[w] > PF_MAX_WIN_RECS) dec[w] = -1;
+            const uint32_t rend = F->win_rec_off[w + 1];
+            const uint64_t e0 = ent.n;
+            for (; i < R_ && rec_of[i] < rend; i++) {
+                if (dec[w] < 0 || p->o.mode == PF_MODE_REPORT) continue;
+                const uint32_t rec = rec_of[i];
+                rc = ent_push(&ent, F->qname + F->qname_off[rec], (size_t)(F->qname_off[rec + 1] - F->qname_off[rec]),
+                              rhp[i]);
+                if (rc) break;
+            }
+            cnt[w] = ent.n - e0;
+        }
+    }
+    if (!rc) {
+        uint64_t *toff = (uint64_t *)calloc(n + 1, sizeof(uint64_t));
+        if (!toff) rc = PF_ERR_NOMEM;
+        if (!rc) {
+            for (uint32_t w = 0; w < n; w++) toff[w + 1] = toff[w] + cnt[w];
+            static const uint64_t zero = 0;
+            rc = job_store(J, n, dec, toff, ent.n, ent.off ? ent.off : &zero, ent.names, ent.hp, n_limit);
+        }
+        free(toff);
+    }
+    ent_free(&ent);
+    pf_batch_free(db);
+    pf_bam_dev_fetch_free(F);
+    free(dec); free(cnt); free(rec_of); free(rhp); free(hp);
+    return rc;
+}
+
 int pf_mp_run_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
     job_t *J = job_of(p, PF_JOB_WINDOWS, j);
     if (!J || !ctx) return PF_ERR_ARG;
@@ -847,6 +945,11 @@ int pf_mp_run_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
     pf_bam_t *bam = NULL;
     int rc = pf_bam_open(p->bam_path, NULL, &bam);
     if (rc) return rc;
+    if (!p->o.host_fetch) {
+        rc = job_device_fetch(p, ctx, bam, J);
+        pf_bam_close(bam);
+        return rc;
+    }
     fetch_t f;
     rc = job_fetch(p, bam, J, &f);
     if (!rc) rc = job_device(p, ctx, J, &f);
@@ -1088,6 +1191,17 @@ static void *dev_main(void *arg) {
     pf_bam_t *bam[2] = {NULL, NULL};
     rc = pf_bam_open(p->bam_path, NULL, &bam[0]);
     if (!rc) rc = pf_bam_open(p->bam_path, NULL, &bam[1]);
+    if (!rc && !p->o.host_fetch) {              /* device fetch: host planning + reads, the rest on the GPU */
+        for (;;) {
+            const uint32_t k = atomic_fetch_add(W->next, 1);
+            if (k >= W->n_todo || rc) break;
+            rc = job_device_fetch(p, W->ctx, bam[0], &p->jobs[W->todo[k]]);
+        }
+        pf_bam_close(bam[0]);
+        pf_bam_close(bam[1]);
+        W->rc = rc;
+        return NULL;
+    }
     prefetch_t cur, nxt;
     memset(&cur, 0, sizeof cur);
     memset(&nxt, 0, sizeof nxt);

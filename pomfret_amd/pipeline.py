@@ -45,7 +45,8 @@ class PfMethphaseOpts(C.Structure):
                 ("load", PfLoadCfg), ("untagged", C.c_int32), ("write_tsv", C.c_int32), ("write_bam", C.c_int32),
                 ("chunk_size", C.c_int32), ("chunk_stride", C.c_int32), ("threads", C.c_int32),
                 ("n_devices", C.c_int32), ("devices", C.c_void_p), ("ctxs", C.c_void_p), ("n_ctxs", C.c_int32),
-                ("rank", C.c_int32), ("world", C.c_int32), ("job_windows", C.c_uint32), ("verbose", C.c_int32)]
+                ("rank", C.c_int32), ("world", C.c_int32), ("job_windows", C.c_uint32), ("verbose", C.c_int32),
+                ("host_fetch", C.c_int32)]
 
 
 class PfQnameTagsC(C.Structure):
@@ -189,7 +190,7 @@ def make_opts(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Opti
               lcfg: Optional[LoadConfig] = None, mode: int = MODE_METHPHASE, untagged: bool = False,
               tsv: bool = False, threads: int = 8, n_devices: int = 0, ctxs=None, rank: int = 0, world: int = 1,
               job_windows: int = 0, cov: int = 0, chunk_size: int = 50_000, chunk_stride: int = 1_000_000,
-              verbose: int = 0):
+              verbose: int = 0, host_fetch: bool = False):
     """pf_methphase_opts_t from Python values.  cfg None: per-contig
     parameters from the BAM's coverage estimate (runs without -c)."""
     lcfg = lcfg or LoadConfig()
@@ -218,6 +219,7 @@ def make_opts(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Opti
     o.rank, o.world = int(rank), int(world)
     o.job_windows = int(job_windows)
     o.verbose = int(verbose)
+    o.host_fetch = int(bool(host_fetch))
     o._keep = keep
     return o
 
@@ -330,7 +332,8 @@ def _result(plan: Plan, mode: int) -> Dict:
 
 def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],
                     lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8, ctx=None,
-                    untagged: bool = False, tsv: bool = False, n_devices: int = 1, job_windows: int = 0) -> Dict:
+                    untagged: bool = False, tsv: bool = False, n_devices: int = 1, job_windows: int = 0,
+                    host_fetch: bool = False) -> Dict:
     """`pomfret methphase` over every gap of vcf_path with the reads of
     bam_path, in this process (pf_methphase_main).  Writes out_prefix +
     .mp.gtf / .mp.vcf (and .mp.tsv with tsv=True, the reference's
@@ -345,7 +348,7 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
         devs = (C.c_int32 * n_devices)(*range(device, device + n_devices))
     o = make_opts(bam_path, vcf_path, out_prefix, cfg, lcfg, untagged=untagged, tsv=tsv, threads=threads,
                   n_devices=0 if ctx is not None else n_devices, ctxs=[ctx] if ctx is not None else None,
-                  job_windows=job_windows)
+                  job_windows=job_windows, host_fetch=host_fetch)
     if devs is not None:
         o.devices = C.cast(devs, C.c_void_p)
     h = C.c_void_p()
@@ -360,7 +363,7 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
 def report_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cov: int = 0,
                  chunk_size: int = 50_000, chunk_stride: int = 1_000_000, lcfg: Optional[LoadConfig] = None,
                  untagged: bool = False, threads: int = 8, ctx=None, n_devices: int = 1, k: int = 3,
-                 k_span: int = 5000) -> Dict:
+                 k_span: int = 5000, host_fetch: bool = False) -> Dict:
     """`pomfret report` (main_methreport, 4901-5089): chunk windows inside the
     phased blocks, one methphase decision each; writes
     {out_prefix}.report.tsv and the running totals to stdout.  cov: -c
@@ -368,7 +371,8 @@ def report_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cov: i
     L = _bind()
     o = make_opts(bam_path, vcf_path, out_prefix, Config(k=k, k_span=k_span), lcfg, mode=MODE_REPORT,
                   untagged=untagged, threads=threads, n_devices=0 if ctx is not None else n_devices,
-                  ctxs=[ctx] if ctx is not None else None, cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride)
+                  ctxs=[ctx] if ctx is not None else None, cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride,
+                  host_fetch=host_fetch)
     h = C.c_void_p()
     _check(L.pf_methphase_main(C.byref(o), C.byref(h)), "pf_methphase_main")
     plan = Plan(o, handle=h)
@@ -382,7 +386,7 @@ def methphase_files_dist(bam_path: str, vcf_path: str, out_prefix: Optional[str]
                          lcfg: Optional[LoadConfig] = None, untagged: bool = False, tsv: bool = False,
                          threads: int = 8, ctx=None, group=None, job_windows: int = 0, mode: int = MODE_METHPHASE,
                          cov: int = 0, chunk_size: int = 50_000, chunk_stride: int = 1_000_000,
-                         runner: Optional[Callable] = None, writer: int = 0) -> Dict:
+                         runner: Optional[Callable] = None, writer: int = 0, host_fetch: bool = False) -> Dict:
     """One process per GPU (torch.distributed initialised; RCCL on GPUs,
     gloo on CPU).  Every rank plans the same jobs and runs the ones its
     static LPT shard owns on `ctx` (or its LOCAL_RANK device); -u tables are
@@ -395,7 +399,7 @@ def methphase_files_dist(bam_path: str, vcf_path: str, out_prefix: Optional[str]
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     o = make_opts(bam_path, vcf_path, out_prefix if rank == writer else None, cfg, lcfg, mode=mode,
                   untagged=untagged, tsv=tsv, threads=threads, rank=rank, world=world, job_windows=job_windows,
-                  cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride)
+                  cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride, host_fetch=host_fetch)
     plan = Plan(o)
     try:
         def run(kind):

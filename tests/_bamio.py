@@ -52,6 +52,7 @@ class Rec:
     l_seq: int = 0
     aux: bytes = b""
     bin_override: Optional[int] = None
+    qual: Optional[bytes] = None                      # None: absent (0xFF)
 
 
 def aux_Z(tag: str, s: str) -> bytes:
@@ -86,7 +87,8 @@ def encode_record(r: Rec) -> bytes:
     b = r.bin_override if r.bin_override is not None else (reg2bin(r.pos, end) if r.pos >= 0 else 4680)
     body = struct.pack("<iiBBHHHiiii", r.tid, r.pos, len(qn), r.mapq, b, len(r.cigar), r.flag, r.l_seq,
                        -1, -1, 0)
-    body += qn + struct.pack(f"<{len(r.cigar)}I", *r.cigar) + bytes(r.seq) + b"\xff" * r.l_seq + r.aux
+    ql = r.qual if r.qual is not None else b"\xff" * r.l_seq
+    body += qn + struct.pack(f"<{len(r.cigar)}I", *r.cigar) + bytes(r.seq) + ql + r.aux
     return struct.pack("<i", len(body)) + body
 
 
@@ -129,10 +131,65 @@ class _Bgzf:
         return bytes(self.out) + EOF_BLOCK
 
 
-def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, text: str = "@HD\tVN:1.6\tSO:coordinate\n"):
+def _deflate_block(args):
+    data, level = args
+    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    z = c.compress(data) + c.flush()
+    bsize = 18 + len(z) + 8
+    hdr = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize - 1)
+    return hdr + z + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data))
+
+
+class _BgzfPar:
+    """The same block boundaries as _Bgzf, blocks compressed at close() in a
+    process pool; tell() returns a token (raw block index << 16 | offset) that
+    translate() turns into the virtual offset once block addresses are known."""
+
+    def __init__(self, level: int, workers: int):
+        self.level, self.workers = level, workers
+        self.blocks = []
+        self.buf = bytearray()
+        self.addr = None
+
+    def tell(self) -> int:
+        return (len(self.blocks) << 16) | len(self.buf)
+
+    def _flush(self):
+        if self.buf:
+            self.blocks.append(bytes(self.buf))
+            self.buf = bytearray()
+
+    def write(self, data: bytes):
+        i = 0
+        while i < len(data):
+            k = min(BLOCK - len(self.buf), len(data) - i)
+            self.buf += data[i:i + k]
+            i += k
+            if len(self.buf) == BLOCK:
+                self._flush()
+
+    def flush(self):
+        self._flush()
+
+    def close(self) -> bytes:
+        self._flush()
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(self.workers) as pool:
+            comp = pool.map(_deflate_block, [(b, self.level) for b in self.blocks], chunksize=16)
+        self.addr = np.concatenate([[0], np.cumsum([len(c) for c in comp])]).astype(np.int64)
+        return b"".join(comp) + EOF_BLOCK
+
+    def translate(self, tok: int) -> int:
+        return (int(self.addr[tok >> 16]) << 16) | (tok & 0xFFFF)
+
+
+def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, text: str = "@HD\tVN:1.6\tSO:coordinate\n",
+              workers: int = 0, level: int = 6):
     """refs: [(name, length)]; recs sorted by (tid, pos) with unplaced reads
-    (tid -1) last.  Writes path and path + '.bai' (or bai_path)."""
-    z = _Bgzf()
+    (tid -1) last.  Writes path and path + '.bai' (or bai_path).  workers > 1
+    compresses the blocks in a process pool (same bytes as the serial writer
+    at the same level)."""
+    z = _BgzfPar(level, workers) if workers > 1 else _Bgzf()
     hdr = b"BAM\1" + struct.pack("<i", len(text)) + text.encode() + struct.pack("<i", len(refs))
     for name, ln in refs:
         nb = name.encode() + b"\0"
@@ -172,6 +229,12 @@ def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, 
         else:
             m[2] += 1
     data = z.close()
+    if workers > 1:                            # tokens -> virtual offsets
+        tr = z.translate
+        bins = [{b: [[tr(u), tr(v)] for u, v in ch] for b, ch in d.items()} for d in bins]
+        lin = [{w: tr(u) for w, u in d.items()} for d in lin]
+        meta = [[tr(m[0]) if m[0] is not None else None, tr(m[1]) if m[1] is not None else None, m[2], m[3]]
+                for m in meta]
     with open(path, "wb") as f:
         f.write(data)
     idx = bytearray(b"BAI\1" + struct.pack("<i", nref))
@@ -197,11 +260,20 @@ def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, 
         f.write(bytes(idx))
 
 
-def records_from_aln(aln, tid: int = 0, prefix: str = "r", hp_zero_every: int = 0, de_absent_every: int = 0):
+def records_from_aln(aln, tid: int = 0, prefix: str = "r", hp_zero_every: int = 0, de_absent_every: int = 0,
+                     qual: bool = False, seed: int = 0):
     """One Rec per record of an AlnBatch (tests/_aln_cases / synth_aln), with
     MM:Z, ML:B:C, MD:Z (when the generator made one), HP:i (absent for 254; HP:i:0 every hp_zero_every-th
-    unphased record) and de:f (absent when < 0)."""
+    unphased record) and de:f (absent when < 0).  qual=True gives every record
+    a QUAL string (slices of a pool of Phred values ~ N(20, 6), nanopore-like
+    entropy) instead of the absent 0xFF run, so BGZF sizes and inflate work
+    are those of a real BAM."""
     out = []
+    pool = None
+    if qual:
+        rng = np.random.default_rng(seed)
+        pool = rng.normal(20, 6, 1 << 24).clip(2, 50).astype(np.uint8).tobytes()
+        starts = rng.integers(0, (1 << 24) - 1, aln.n_recs)
     for i in range(aln.n_recs):
         cig = [int(x) for x in aln.cigar[aln.cigar_off[i]:aln.cigar_off[i + 1]]]
         lq = int(aln.l_qseq[i])
@@ -225,8 +297,12 @@ def records_from_aln(aln, tid: int = 0, prefix: str = "r", hp_zero_every: int = 
             aux += aux_BC("ML", ml)
         if "md" in aln.meta:
             aux += aux_Z("MD", aln.meta["md"][i])
+        q = None
+        if pool is not None:
+            o = int(starts[i]) % max(1, (1 << 24) - lq)
+            q = pool[o:o + lq]
         out.append(Rec(tid=tid, pos=int(aln.pos[i]), qname=f"{prefix}{i}", flag=int(aln.flag[i]),
-                       mapq=int(aln.mapq[i]), cigar=cig, seq=seq, l_seq=lq, aux=aux))
+                       mapq=int(aln.mapq[i]), cigar=cig, seq=seq, l_seq=lq, aux=aux, qual=q))
     return out
 
 

@@ -126,3 +126,34 @@ def test_device_fetch_record_limit(gpu_ctx, tmp_path):
     got = np.diff(info["win_rec_off"].astype(np.int64))
     assert np.array_equal(info["win_n_fetched"], per)
     assert np.array_equal(got, np.where(per > lim, 0, per))
+
+
+@pytest.mark.parametrize("mode", ["tagged", "untagged", "report"])
+def test_pipeline_device_vs_host_fetch(gpu_ctx, tmp_path, mode):
+    """The C driver with the device fetch (default) and with --host-fetch:
+    identical decisions, first-wins tag tables and output bytes."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import methphase_files, report_files
+    from tests._fixtures import untagged
+    if mode == "untagged":
+        aln, recs, bam, vcf = untagged(tmp_path, n_windows=3, coverage=60)
+        cfg = Config.from_coverage(60, given=False)
+    else:
+        aln, recs, bam, vcf = tagged(tmp_path, n_windows=4, coverage=30, seed=31)
+        cfg = Config.from_coverage(30, given=False)
+    outs = {}
+    for hf in (False, True):
+        pre = str(tmp_path / f"o{int(hf)}")
+        if mode == "report":
+            outs[hf] = (report_files(bam, vcf, pre, cov=30, chunk_size=20_000, chunk_stride=200_000,
+                                     ctx=gpu_ctx, host_fetch=hf), pre)
+        else:
+            outs[hf] = (methphase_files(bam, vcf, pre, cfg, ctx=gpu_ctx, untagged=mode == "untagged", tsv=True,
+                                        host_fetch=hf), pre)
+    (rd, pd), (rh, ph) = outs[False], outs[True]
+    assert np.array_equal(rd["decision"], rh["decision"])
+    exts = [".report.tsv"] if mode == "report" else [".mp.gtf", ".mp.vcf", ".mp.tsv"]
+    if mode != "report":
+        assert rd["qname_hp"] == rh["qname_hp"]
+    for e in exts:
+        assert open(pd + e, "rb").read() == open(ph + e, "rb").read(), e
