@@ -53,12 +53,6 @@ DEV void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-__constant__ uint16_t k_lbase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
-                                     35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t k_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t k_dbase[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193,
-                                     257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t k_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t k_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 struct InfLds {                         // one wave's tables
@@ -467,7 +461,11 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
             if (s == 256) break;
             const uint32_t li = s - 257;
             if (li >= 29) { err = PF_INF_ECODES; break; }
-            const uint32_t L = k_lbase[li] + bits_get(b, k_lext[li]);
+            // length base / extra bits (RFC 1951 3.2.5) by arithmetic: a table
+            // lookup would be a memory load on the decode chain
+            const uint32_t lx = li < 8 ? 0u : li == 28 ? 0u : (li - 4) >> 2;
+            const uint32_t lb = li < 8 ? 3 + li : li == 28 ? 258u : ((4 + (li & 3u)) << lx) + 3;
+            const uint32_t L = lb + bits_get(b, lx);
             bits_fill(b, lane);
             e = uni(T.droot[(uint32_t)b.buf & ((1u << INF_DROOT) - 1u)]);
             l = e >> 9;
@@ -480,7 +478,9 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
             }
             bits_get(b, l);
             if (s >= 30) { err = PF_INF_ECODES; break; }
-            const uint32_t D = k_dbase[s] + bits_get(b, k_dext[s]);
+            const uint32_t dx = s < 4 ? 0u : (s - 2) >> 1;
+            const uint32_t db = s < 4 ? 1 + s : ((2 + (s & 1u)) << dx) + 1;
+            const uint32_t D = db + bits_get(b, dx);
             if ((uint64_t)D > o.a - o.lo) { err = PF_INF_EDIST; break; }
             if (o.a + L > o.hi) { err = PF_INF_ESIZE; break; }
             out_match(o, L, D, lane);

@@ -372,7 +372,6 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
     constexpr uint32_t ROWS = 8, RW = 128, BW = ROWS * RW;
     const uint64_t pat = (rev ? (uint64_t)NT_G : (uint64_t)NT_C) * 0x1111111111111111ull;
     const uint4 *sq4 = reinterpret_cast<const uint4 *>(seq);
-    const uint64_t *sw = reinterpret_cast<const uint64_t *>(seq);
     const uint32_t nwords = (len + 15) / 16;
     const uint32_t nblk = (nwords + BW - 1) / BW;
     const uint32_t nd = t.nd;
@@ -424,30 +423,75 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
         wsync();
         for (uint32_t j0 = ti; j0 < tend; j0 += 64) {
             const uint32_t j = j0 + lane;
-            if (j < tend) {
-                const uint32_t e = TB[slot(j)];
+            const bool act = j < tend;
+            uint32_t e = 0, i = 8, Lw = 0, hw = 0, k = 0;
+            if (act) {
+                e = TB[slot(j)];
                 const uint32_t rr = (e & 0xFFFFFFu) - carry;
                 const uint32_t f = rev ? btot - 1 - rr : rr;    // forward rank inside the block
-                uint32_t i = 0;
+                i = 0;
 #pragma unroll
                 for (uint32_t q = 1; q < ROWS; q++) i += pref[q] <= f ? 1u : 0u;
                 const uint16_t *sbi = L.u.s.sb + i * 64;
                 uint32_t lo = 0, n = 64;                        // last pair with base <= f
                 while (n > 0) { const uint32_t h = n >> 1; if (sbi[lo + h] <= f) { lo += h + 1; n -= h + 1; } else n = h; }
-                const uint32_t Lw = lo - 1;
-                uint32_t k = f - sbi[Lw];
+                Lw = lo - 1;
+                k = f - sbi[Lw];
                 const uint32_t c0 = L.u.s.sc[i * 64 + Lw];
-                uint32_t hw = 0;
                 if (k >= c0) { k -= c0; hw = 1; }
+            }
+            // The trigger's word and its neighbour word (the context base at a
+            // word edge) come from the registers of the lane that loaded them
+            // (ds_bpermute), not from a second read of SEQ: lane Lw of row i
+            // holds words 2Lw (x, y) and 2Lw+1 (z, w).
+            uint32_t x0 = 0, x1 = 0, n0 = 0, n1 = 0;
+            bool edge = false;
+#pragma unroll
+            for (uint32_t q = 0; q < ROWS; q++) {
+                const bool mine = i == q;
+                if (!__ballot(mine)) continue;
+                const int sl = (int)((mine ? Lw : lane) << 2);
+                const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].x);
+                const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].y);
+                const uint32_t a2 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].z);
+                const uint32_t a3 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].w);
+                // neighbour pair: forward reads need the next word, reverse the previous one
+                const uint32_t nl = rev ? (Lw > 0 ? Lw - 1 : 0u) : (Lw < 63 ? Lw + 1 : 63u);
+                const int snl = (int)((mine ? nl : lane) << 2);
+                const uint32_t b0 = (uint32_t)__builtin_amdgcn_ds_bpermute(snl, (int)(rev ? v[q].z : v[q].x));
+                const uint32_t b1 = (uint32_t)__builtin_amdgcn_ds_bpermute(snl, (int)(rev ? v[q].w : v[q].y));
+                // across a row boundary: the next row's first word / the previous row's last word
+                uint32_t r0 = 0, r1 = 0;
+                bool redge = true;
+                if (!rev && q + 1 < ROWS) { r0 = rdl(v[q + 1 < ROWS ? q + 1 : q].x, 0); r1 = rdl(v[q + 1 < ROWS ? q + 1 : q].y, 0); redge = false; }
+                if (rev && q > 0) { r0 = rdl(v[q > 0 ? q - 1 : q].z, 63); r1 = rdl(v[q > 0 ? q - 1 : q].w, 63); redge = false; }
+                if (mine) {
+                    x0 = hw ? a2 : a0;
+                    x1 = hw ? a3 : a1;
+                    if (!rev) {
+                        if (!hw) { n0 = a2; n1 = a3; }
+                        else if (Lw < 63) { n0 = b0; n1 = b1; }
+                        else { n0 = r0; n1 = r1; edge = redge; }
+                    } else {
+                        if (hw) { n0 = a0; n1 = a1; }
+                        else if (Lw > 0) { n0 = b0; n1 = b1; }
+                        else { n0 = r0; n1 = r1; edge = redge; }
+                    }
+                }
+            }
+            if (act) {
                 const uint32_t w = b * BW + i * RW + 2 * Lw + hw;
-                const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(sw[w]);
+                const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(((uint64_t)x1 << 32) | x0);
+                const uint64_t xn = nibswap(((uint64_t)n1 << 32) | n0);
                 const uint32_t bi = sel_nibble(zero_nibbles(xw ^ pat), k);
                 const uint32_t p = w * 16 + bi;
                 uint32_t key = 0xFFFFFFFFu;
                 if (p > 0 && p < len - 1) {
                     bool ctx;
-                    if (!rev) ctx = (bi < 15 ? (uint32_t)(xw >> (4 * (bi + 1))) & 15u : nib(seq, p + 1)) == NT_G;
-                    else ctx = (bi > 0 ? (uint32_t)(xw >> (4 * (bi - 1))) & 15u : nib(seq, p - 1)) == NT_C;
+                    if (!rev) ctx = (bi < 15 ? (uint32_t)(xw >> (4 * (bi + 1))) & 15u
+                                             : edge ? nib(seq, p + 1) : (uint32_t)xn & 15u) == NT_G;
+                    else ctx = (bi > 0 ? (uint32_t)(xw >> (4 * (bi - 1))) & 15u
+                                       : edge ? nib(seq, p - 1) : (uint32_t)(xn >> 60) & 15u) == NT_C;
                     if (ctx) {
                         const uint32_t q = e >> 24;
                         key = (p << 2) | (q < d.lo ? 1u : q >= d.hi ? 0u : 2u);

@@ -14,8 +14,9 @@ from pomfret_amd import Config, Context, LoadConfig  # noqa: E402
 from pomfret_amd.synth_aln import AlnSpec, make_aln_batch  # noqa: E402
 
 nw = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-aln = make_aln_batch(AlnSpec(n_windows=nw, coverage=30, seed=1000))
-cfg = Config.from_coverage(30, given=False)
+cov = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+aln = make_aln_batch(AlnSpec(n_windows=nw, coverage=cov, seed=1000))
+cfg = Config.from_coverage(cov, given=False)
 ctx = Context(0)
 db = ctx.upload_aln(cfg, aln, LoadConfig())
 lib = L.lib()
