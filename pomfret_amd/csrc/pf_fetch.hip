@@ -52,8 +52,8 @@ DEV uint32_t ld16u(const uint8_t *a, uint64_t p) { return ld32u(a, p) & 0xFFFFu;
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void pf_chain(const uint8_t *arena, pf_run_dev *runs, uint32_t n_runs,
                                                uint64_t *rec_pos) {
-    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= n_runs) return;
+    const uint32_t i = blockIdx.x;            // one wave per run, lane 0 walks (a dependent chain)
+    if (threadIdx.x != 0 || i >= n_runs) return;
     pf_run_dev R = runs[i];
     uint64_t p = R.chain_start;
     uint32_t n = 0, stop = PF_CHAIN_END;

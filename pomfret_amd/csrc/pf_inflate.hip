@@ -32,8 +32,9 @@
 //    per symbol), about 12 GB/s of output on MI355X;
 //  * table construction is lane-parallel (counts by ballot, ranks by ballot
 //    prefix, root fill one symbol per lane).
-// A second kernel checks each block's CRC32 (reflected 0xEDB88320, zlib's
-// crc32) and ISIZE, as htslib does; any malformed stream, size or CRC
+// Each block's CRC32 (reflected 0xEDB88320, zlib's crc32) is folded in at
+// every chunk flush (VALU work beside the scalar decode) and checked with the
+// ISIZE against the footer, as htslib does; any malformed stream, size or CRC
 // mismatch sets the block's status word and the host fails the fetch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -223,6 +224,28 @@ DEV uint32_t slow_decode(uint64_t bits, const uint16_t *cnt, const uint16_t *off
 // per match), then bytes sourced inside the chunk are resolved in rounds of
 // ds_bpermute (a source always precedes its byte, so every round resolves at
 // least the earliest pending byte), and the chunk is stored.
+// CRC32 (reflected 0xEDB88320, zlib's crc32) in raw form (init 0, no final
+// xor): raw(A || B) = raw(A) * x^(8|B|) ^ raw(B) in GF(2)[x] mod P, and
+// leading zero bytes leave a raw CRC unchanged.  crc32(M) = ~(raw(M) ^
+// ~0 * x^(8|M|)).
+DEV uint32_t gf_mul(uint32_t a, uint32_t b) {      // reflected, x^0 = 0x80000000 (zlib's multmodp)
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        p ^= (a & 0x80000000u) ? b : 0u;
+        a <<= 1;
+        b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+DEV uint32_t x8n(uint64_t n, const uint32_t *x2n) {  // x^(8n) mod P; x2n[k] = x^(2^k)
+    uint32_t p = 0x80000000u;
+    uint64_t e = n << 3;
+    for (uint32_t k = 0; e; k++, e >>= 1)
+        if (e & 1u) p = gf_mul(p, x2n[k & 31u]);
+    return p;
+}
+
 struct Out {
     uint8_t *arena;
     uint64_t lo, hi;      // the block's output range [lo, hi)
@@ -232,7 +255,31 @@ struct Out {
     uint32_t pend;        // per lane: bit i set while byte i waits for its source
     uint32_t src[4];      // per lane: source offset (from lo) of pending byte i
     uint32_t any;         // uniform: the chunk has pending bytes
+    uint32_t crc;         // uniform: raw CRC of the flushed chunks
+    uint32_t ck;          // per lane: x^(8 * (252 - 4 lane)), its word's weight in a full chunk
+    const uint32_t *tab;  // CRC table (LDS)
+    const uint32_t *x2n;  // x^(2^k) (LDS)
 };
+
+// fold a chunk's resolved bytes into the block CRC: m = bytes of the chunk
+// that belong to the block's stream (256, or the last chunk's length); bytes
+// before the block's start are zero (leading zeros)
+DEV void out_crc(Out &o, uint32_t lane, uint32_t m) {
+    const uint32_t nv = m > 4 * lane ? (m - 4 * lane < 4 ? m - 4 * lane : 4u) : 0u;   // this lane's bytes
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++)
+        if (i < nv) c = o.tab[(c ^ (o.val >> (8 * i))) & 0xFFu] ^ (c >> 8);
+    uint32_t wgt = o.ck;
+    if (m != 256) {                                     // weight of this lane's bytes: x^(8 (m - 4 lane - nv))
+        const uint32_t e = nv ? m - 4 * lane - nv : 0u;
+        wgt = x8n(e, o.x2n);
+    }
+    c = nv ? gf_mul(c, wgt) : 0u;
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) c ^= (uint32_t)__shfl_xor((int)c, s, 64);
+    o.crc = gf_mul(o.crc, m == 256 ? o.x2n[11] : x8n(m, o.x2n)) ^ uni(c);
+}
 
 DEV void out_flush(Out &o, uint32_t lane) {
     if (o.any) {
@@ -268,6 +315,7 @@ DEV void out_flush(Out &o, uint32_t lane) {
             o.pend = np;
         }
     }
+    out_crc(o, lane, o.a >= o.cb + 256 ? 256u : (uint32_t)(o.a - o.cb));
     const uint64_t addr = o.cb + 4ull * lane;
     if (addr >= o.lo && addr + 4 <= o.hi && addr + 4 <= o.a) {
         *reinterpret_cast<uint32_t *>(o.arena + addr) = o.val;
@@ -317,6 +365,17 @@ DEV void out_match(Out &o, uint32_t L, uint32_t D, uint32_t lane) {
 __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk,
                                                             uint8_t *arena, uint32_t *status) {
     __shared__ InfLds lds_all[INF_WAVES];
+    __shared__ uint32_t crc_tab[256], crc_x2n[32];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        crc_tab[i] = c;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t p = 0x40000000u;                     // x^1
+        for (int k = 0; k < 32; k++) { crc_x2n[k] = p; p = gf_mul(p, p); }
+    }
+    __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t bi = blockIdx.x * INF_WAVES + wv;
@@ -349,6 +408,10 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
     o.any = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 4; i++) o.src[i] = 0;
+    o.crc = 0;
+    o.tab = crc_tab;
+    o.x2n = crc_x2n;
+    o.ck = x8n(252 - 4 * lane, crc_x2n);
 
     uint32_t err = 0, final_blk = 0;
     while (!final_blk && !err) {
@@ -491,72 +554,7 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
     if (!err && o.a != o.hi) err = PF_INF_ESIZE;
     // the partial last chunk (bytes below o.a only)
     if (o.a > o.cb) out_flush(o, lane);
+    // CRC32 of the output against the footer (bgzf_uncompress's check)
+    if (!err && ~(o.crc ^ gf_mul(0xFFFFFFFFu, x8n(isize, crc_x2n))) != B.crc) err = PF_INF_ECRC;
     if (lane == 0) status[bi] = err;
-}
-
-// --------------------------------------------------------------------------
-// CRC32 of each block's output: lane k takes bytes [k*S, (k+1)*S) of the
-// block front-padded to 64*S bytes with zeros (leading zeros leave a raw CRC
-// unchanged), raw CRCs combined with multiplications by x^(8n) mod P.
-DEV uint32_t gf_mul(uint32_t a, uint32_t b) {      // reflected, x^0 = 0x80000000 (zlib's multmodp)
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 0; i < 32; i++) {
-        p ^= (a & 0x80000000u) ? b : 0u;
-        a <<= 1;
-        b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
-    }
-    return p;
-}
-DEV uint32_t x8n(uint64_t n, const uint32_t *x2n) {  // x^(8n) mod P; x2n[k] = x^(2^k)
-    uint32_t p = 0x80000000u;
-    uint64_t e = n << 3;
-    for (uint32_t k = 0; e; k++, e >>= 1)
-        if (e & 1u) p = gf_mul(p, x2n[k & 31u]);
-    return p;
-}
-
-__global__ __launch_bounds__(256) void pf_bgzf_crc(const uint8_t *arena, const pf_bgzf_blk *blk, uint32_t nblk,
-                                                  uint32_t *status) {
-    __shared__ uint32_t tab[256];
-    __shared__ uint32_t x2n[32];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-        uint32_t c = i;
-        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
-        tab[i] = c;
-    }
-    if (threadIdx.x == 0) {
-        uint32_t p = 0x40000000u;                     // x^1
-        for (int k = 0; k < 32; k++) { x2n[k] = p; p = gf_mul(p, p); }
-    }
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t bi = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (bi >= nblk) return;
-    const pf_bgzf_blk B = blk[bi];
-    const uint32_t n = B.isize;
-    const uint32_t S = (n + 63) / 64;
-    const uint32_t pad = 64 * S - n;
-    const uint8_t *p = arena + B.out_off;
-    uint32_t c = 0;
-    for (uint32_t j = 0; j < S; j++) {
-        const uint32_t v = lane * S + j;                 // virtual (padded) offset
-        const uint32_t byte = v >= pad ? p[v - pad] : 0u;
-        c = tab[(c ^ byte) & 0xFFu] ^ (c >> 8);
-    }
-    // lane k's contribution: raw_k * x^(8 S (63-k))
-    const uint32_t xs = x8n(S, x2n);
-    uint32_t m = 0x80000000u, base = xs;
-    uint32_t e = 63 - lane;
-    while (e) {
-        if (e & 1u) m = gf_mul(m, base);
-        base = gf_mul(base, base);
-        e >>= 1;
-    }
-    c = gf_mul(c, m);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o, 64);
-    // crc32 = ~(raw ^ zeros(~0, n))
-    const uint32_t crc = ~(c ^ gf_mul(0xFFFFFFFFu, x8n(n, x2n)));
-    if (lane == 0 && crc != B.crc && status[bi] == 0) status[bi] = PF_INF_ECRC;
 }

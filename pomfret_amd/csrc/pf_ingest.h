@@ -26,7 +26,6 @@ typedef struct pf_bgzf_blk {
 
 __global__ void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena,
                            uint32_t *status);
-__global__ void pf_bgzf_crc(const uint8_t *arena, const pf_bgzf_blk *blk, uint32_t nblk, uint32_t *status);
 
 // ---- device fetch (pf_ingest.hip): runs of blocks, windows, chunks, records
 typedef struct pf_run_dev {

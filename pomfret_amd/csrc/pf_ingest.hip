@@ -66,8 +66,6 @@ int pf_inflate_launch(hipStream_t st, const uint8_t *d_in, const pf_bgzf_blk *d_
     hipLaunchKernelGGL(pf_inflate, dim3((nblk + 3) / 4), dim3(256), 0, st, d_in, d_blk, nblk, d_arena, d_status);
     if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
     if (e1 && hipEventRecord(e1, st) != hipSuccess) return PF_ERR_HIP;
-    hipLaunchKernelGGL(pf_bgzf_crc, dim3((nblk + 3) / 4), dim3(256), 0, st, d_arena, d_blk, nblk, d_status);
-    if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
     return PF_OK;
 }
 
@@ -123,7 +121,9 @@ out:
 // Device fetch: the windows' records from the BAM file through the device
 // (inflate, chain, decode, select, gather) into a record-level batch.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <mutex>
 #include <thread>
 #include <errno.h>
 #include <fcntl.h>
@@ -133,9 +133,13 @@ out:
 
 namespace {
 
-struct DevBuf {                                  // device allocations freed together
+struct DevBuf {                                  // device allocations freed together, after the stream drains
     std::vector<void *> p;
-    ~DevBuf() { for (void *x : p) (void)hipFree(x); }
+    hipStream_t st = nullptr;
+    ~DevBuf() {
+        if (st) (void)hipStreamSynchronize(st);
+        for (void *x : p) (void)hipFree(x);
+    }
     template <typename T> T *alloc(size_t n) {
         void *x = nullptr;
         if (hipMalloc(&x, n ? n * sizeof(T) : 1) != hipSuccess) return nullptr;
@@ -161,9 +165,30 @@ struct Plan {
     std::vector<pf_bgzf_blk> blk;
     std::vector<uint64_t> caddr;            // file address of each block
     std::vector<Range> runs;
-    std::vector<uint8_t> comp;              // compressed bytes of every run, back to back
+    uint8_t *comp = nullptr;                // compressed bytes of every run, back to back (pinned)
+    uint64_t comp_n = 0;
     uint64_t arena = 0;                     // inflated bytes
 };
+
+// one pinned staging buffer per device for the compressed bytes (grown on
+// demand, reused by every fetch on that device: pinning costs about as much
+// as the copy it enables)
+std::mutex g_pin_mu;
+std::vector<std::pair<uint8_t *, size_t>> g_pin;
+uint8_t *pinned(int dev, size_t n) {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    if ((size_t)dev >= g_pin.size()) g_pin.resize(dev + 1, {nullptr, 0});
+    auto &e = g_pin[dev];
+    if (e.second < n) {
+        if (e.first) (void)hipHostFree(e.first);
+        e = {nullptr, 0};
+        void *p = nullptr;
+        const size_t cap = n + n / 4;
+        if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        e = {static_cast<uint8_t *>(p), cap};
+    }
+    return e.first;
+}
 
 // the gathered small fields, host side
 struct Small {
@@ -266,6 +291,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
     uint64_t ext = 4ull << 16;            // bytes read past a chunk's last block (records spanning blocks)
     for (int attempt = 0; attempt < 8; attempt++) {
         DevBuf D;
+        D.st = st;
         Plan P;
         double t0 = now_ms();
         // ---- byte ranges: [u >> 16, (v >> 16) + ext) per chunk, merged
@@ -282,20 +308,47 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         }
         uint64_t tot = 0;
         for (auto &R : P.runs) { R.buf0 = tot; tot += R.f1 - R.f0; }
-        P.comp.resize(tot + 512);
-        // parallel reads of the ranges
+        P.comp_n = tot + 512;
+        P.comp = pinned(pf_ctx_device((const pf_ctx *)ctx), P.comp_n);
+        uint8_t *d_comp = D.alloc<uint8_t>(P.comp_n);
+        if (!P.comp || !d_comp) { rc = PF_ERR_NOMEM; break; }
+        // parallel reads into the pinned buffer in segments of <= 64 MiB, each
+        // segment's H2D copy overlapping the reads of the next (pieces of
+        // <= 4 MiB on 16 threads)
         {
-            std::vector<int> rr(P.runs.size(), 0);
-            const size_t nt = std::min<size_t>(16, P.runs.size() ? P.runs.size() : 1);
-            std::vector<std::thread> th;
-            for (size_t t = 0; t < nt; t++)
-                th.emplace_back([&, t]() {
-                    for (size_t i = t; i < P.runs.size(); i += nt)
-                        rr[i] = read_range(fd, P.runs[i].f0, P.runs[i].f1 - P.runs[i].f0, P.comp.data() + P.runs[i].buf0);
-                });
-            for (auto &t : th) t.join();
-            for (int x : rr) if (x) rc = -1;
-            memset(P.comp.data() + tot, 0, 512);
+            constexpr uint64_t SEG = 64ull << 20, PIECE = 4ull << 20;
+            std::vector<std::pair<uint64_t, uint64_t>> pieces;     // (run, offset in run)
+            for (uint32_t ri = 0; ri < P.runs.size(); ri++)
+                for (uint64_t o = 0; o < P.runs[ri].f1 - P.runs[ri].f0; o += PIECE) pieces.push_back({ri, o});
+            std::atomic<int> bad{0};
+            size_t pi = 0;
+            uint64_t copied = 0;
+            while (pi < pieces.size() && !bad.load()) {
+                size_t pe = pi;
+                const uint64_t seg0 = P.runs[pieces[pi].first].buf0 + pieces[pi].second;
+                while (pe < pieces.size() && P.runs[pieces[pe].first].buf0 + pieces[pe].second < seg0 + SEG) pe++;
+                std::atomic<size_t> next{pi};
+                std::vector<std::thread> th;
+                const size_t nt = std::min<size_t>(16, pe - pi);
+                for (size_t t = 0; t < nt; t++)
+                    th.emplace_back([&]() {
+                        for (size_t k; (k = next.fetch_add(1)) < pe;) {
+                            const Range &R = P.runs[pieces[k].first];
+                            const uint64_t o = pieces[k].second, n = std::min(PIECE, R.f1 - R.f0 - o);
+                            if (read_range(fd, R.f0 + o, n, P.comp + R.buf0 + o)) bad.store(1);
+                        }
+                    });
+                for (auto &t : th) t.join();
+                const uint64_t seg1 = pe < pieces.size() ? P.runs[pieces[pe].first].buf0 + pieces[pe].second : tot;
+                if (hipMemcpyAsync(d_comp + copied, P.comp + copied, seg1 - copied, hipMemcpyHostToDevice, st) !=
+                    hipSuccess) bad.store(2);
+                copied = seg1;
+                pi = pe;
+            }
+            memset(P.comp + tot, 0, 512);
+            if (!bad.load() && hipMemcpyAsync(d_comp + tot, P.comp + tot, 512, hipMemcpyHostToDevice, st) != hipSuccess)
+                bad.store(2);
+            if (bad.load()) rc = bad.load() == 1 ? -1 : PF_ERR_HIP;
         }
         if (rc) break;
         const double t_read = now_ms() - t0;
@@ -305,7 +358,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
             R.b0 = (uint32_t)P.blk.size();
             uint64_t o = 0;
             const uint64_t len = R.f1 - R.f0;
-            const uint8_t *c = P.comp.data() + R.buf0;
+            const uint8_t *c = P.comp + R.buf0;
             while (o + 18 <= len) {
                 const uint8_t *h = c + o;
                 if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { rc = PF_ERR_ARG; break; }
@@ -384,7 +437,6 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         }
         // ---- upload + inflate
         t0 = now_ms();
-        uint8_t *d_comp = D.alloc<uint8_t>(P.comp.size());
         pf_bgzf_blk *d_blk = D.alloc<pf_bgzf_blk>(NB);
         uint8_t *d_arena = D.alloc<uint8_t>(P.arena + 512);
         uint32_t *d_bst = D.alloc<uint32_t>(NB);
@@ -392,13 +444,12 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         pf_chunk_dev *d_ch = D.alloc<pf_chunk_dev>(NC);
         pf_win_dev *d_win = D.alloc<pf_win_dev>(W);
         uint32_t *d_wn = D.alloc<uint32_t>(2ull * W);
-        if (!d_comp || !d_blk || !d_arena || !d_bst || !d_run || !d_ch || !d_win || !d_wn) { rc = PF_ERR_NOMEM; break; }
+        if (!d_blk || !d_arena || !d_bst || !d_run || !d_ch || !d_win || !d_wn) { rc = PF_ERR_NOMEM; break; }
         hipEvent_t ev[8];
         for (auto &e : ev) if (hipEventCreate(&e) != hipSuccess) rc = PF_ERR_HIP;
         if (rc) break;
         auto evdone = [&]() { for (auto &e : ev) (void)hipEventDestroy(e); };
-        bool ok = hipMemcpyAsync(d_comp, P.comp.data(), P.comp.size(), hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipMemcpyAsync(d_blk, P.blk.data(), sizeof(pf_bgzf_blk) * NB, hipMemcpyHostToDevice, st) == hipSuccess &&
+        bool ok = hipMemcpyAsync(d_blk, P.blk.data(), sizeof(pf_bgzf_blk) * NB, hipMemcpyHostToDevice, st) == hipSuccess &&
                   hipMemsetAsync(d_bst, 0, 4ull * NB, st) == hipSuccess &&
                   hipMemsetAsync(d_arena + P.arena, 0, 512, st) == hipSuccess &&
                   hipMemcpyAsync(d_run, rd.data(), sizeof(pf_run_dev) * NR, hipMemcpyHostToDevice, st) == hipSuccess &&
@@ -409,7 +460,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
                      hipEventRecord(ev[2], st) == hipSuccess;
         // ---- chain: count, offsets, write
         if (ok && NR) {
-            hipLaunchKernelGGL(pf_chain, dim3((NR + 63) / 64), dim3(64), 0, st, d_arena, d_run, NR, (uint64_t *)nullptr);
+            hipLaunchKernelGGL(pf_chain, dim3(NR), dim3(64), 0, st, d_arena, d_run, NR, (uint64_t *)nullptr);
             ok = hipGetLastError() == hipSuccess;
         }
         std::vector<uint32_t> bst(NB);
@@ -444,7 +495,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         ok = hipMemcpyAsync(d_run, rd.data(), sizeof(pf_run_dev) * NR, hipMemcpyHostToDevice, st) == hipSuccess &&
              hipEventRecord(ev[3], st) == hipSuccess;
         if (ok && NR) {
-            hipLaunchKernelGGL(pf_chain, dim3((NR + 63) / 64), dim3(64), 0, st, d_arena, d_run, NR, Rv.pos);
+            hipLaunchKernelGGL(pf_chain, dim3(NR), dim3(64), 0, st, d_arena, d_run, NR, Rv.pos);
             ok = hipGetLastError() == hipSuccess;
         }
         if (ok && NRec) {
