@@ -20,11 +20,14 @@ from .abi import WindowBatch
 
 
 def window_costs(batch: WindowBatch) -> np.ndarray:
+    """LPT cost of each window, reads x calls: the greedy
+    chain has about R iterations, each over terms proportional to the
+    window's calls."""
     ro = batch.win_read_off.astype(np.int64)
     co = batch.read_call_off.astype(np.int64)
     reads = np.diff(ro)
     calls = co[ro[1:]] - co[ro[:-1]]
-    return reads.astype(np.float64) * np.maximum(calls, 1).astype(np.float64) / np.maximum(reads, 1)
+    return reads.astype(np.float64) * np.maximum(calls, 1).astype(np.float64)
 
 
 def lpt_partition(costs: np.ndarray, n_parts: int):
