@@ -50,26 +50,33 @@ DEV uint32_t ld32u(const uint8_t *a, uint64_t p) {
 DEV uint32_t ld16u(const uint8_t *a, uint64_t p) { return ld32u(a, p) & 0xFFFFu; }
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void pf_chain(const uint8_t *arena, pf_run_dev *runs, uint32_t n_runs,
+// The record chain, split at the chunk starts the index already knows to be
+// record boundaries: one lane per segment walks block_size hops from its
+// start; a segment other than its run's last must land exactly on the next
+// start (else the chain is treated as corrupt there).  Count pass (rec_pos
+// null): n, stop, stop_pos per segment; write pass: positions from rec0.
+__global__ __launch_bounds__(64) void pf_chain(const uint8_t *arena, pf_seg_dev *segs, uint32_t n_segs,
                                                uint64_t *rec_pos) {
-    const uint32_t i = blockIdx.x;            // one wave per run, lane 0 walks (a dependent chain)
-    if (threadIdx.x != 0 || i >= n_runs) return;
-    pf_run_dev R = runs[i];
-    uint64_t p = R.chain_start;
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n_segs) return;
+    const pf_seg_dev S = segs[i];
+    if (rec_pos && !S.live) return;
+    uint64_t p = S.s;
     uint32_t n = 0, stop = PF_CHAIN_END;
-    while (p < R.a1) {
-        if (p + 4 > R.a1) { stop = PF_CHAIN_CUT; break; }
+    while (p < S.e) {
+        if (p + 4 > S.a1) { stop = PF_CHAIN_CUT; break; }
         const uint32_t bs = ld32u(arena, p);
         if (bs < 32 || bs > (1u << 30)) { stop = PF_CHAIN_CORRUPT; break; }
-        if (p + 4 + bs > R.a1) { stop = PF_CHAIN_CUT; break; }
-        if (rec_pos) rec_pos[R.rec0 + n] = p;
+        if (p + 4 + bs > S.a1) { stop = PF_CHAIN_CUT; break; }
+        if (rec_pos) rec_pos[S.rec0 + n] = p;
         n++;
         p += 4 + (uint64_t)bs;
     }
+    if (!S.last && stop == PF_CHAIN_END && p != S.e) stop = PF_CHAIN_CORRUPT;   // overshot a known boundary
     if (!rec_pos) {
-        runs[i].n_rec = n;
-        runs[i].stop = stop;
-        runs[i].stop_pos = p;
+        segs[i].n = n;
+        segs[i].stop = stop;
+        segs[i].stop_pos = p;
     }
 }
 

@@ -40,6 +40,15 @@ typedef struct pf_run_dev {
 #define PF_CHAIN_CUT 1u        // a record (or its size field) runs past a1
 #define PF_CHAIN_CORRUPT 2u    // block_size < 32 or > 2^30 at stop_pos
 
+typedef struct pf_seg_dev {       // a piece of a run's record chain between known record starts
+    uint64_t s, e;            // walk from s until e (the next known start, or the run's end a1)
+    uint64_t a1;              // the run's end
+    uint64_t stop_pos;        // count pass: position after its last whole record
+    uint32_t run, last;       // its run; the run's last segment
+    uint32_t n, stop;         // count pass: records, PF_CHAIN_*
+    uint32_t rec0, live;      // write pass: first record index; 0 = past a corrupt segment
+} pf_seg_dev;
+
 typedef struct pf_chunk_dev {
     uint64_t u, v;            // arena positions of the chunk's virtual offsets
     uint32_t run, pad;
@@ -74,7 +83,7 @@ typedef struct pf_recs_dev {
 #define PF_REC_TRUNC 2u
 #define PF_REC_MD 4u
 
-__global__ void pf_chain(const uint8_t *arena, pf_run_dev *runs, uint32_t n_runs, uint64_t *rec_pos);
+__global__ void pf_chain(const uint8_t *arena, pf_seg_dev *segs, uint32_t n_segs, uint64_t *rec_pos);
 __global__ void pf_recdec(const uint8_t *arena, uint32_t n_recs, pf_recs_dev R);
 __global__ void pf_select(const pf_win_dev *wins, uint32_t n_wins, const pf_chunk_dev *chunks, const pf_run_dev *runs,
                           pf_recs_dev R, uint32_t write, uint32_t *win_n, uint32_t *win_st, uint32_t *out);

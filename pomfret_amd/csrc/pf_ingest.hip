@@ -430,6 +430,32 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         if (rc) break;
         if (more) { ext *= 4; continue; }
         for (auto &R : rd) if (R.chain_start == UINT64_MAX) R.chain_start = R.a1;
+        // chain segments: each run's chain cut at the chunk starts (record
+        // boundaries by the index's construction), walked in parallel
+        std::vector<pf_seg_dev> sg;
+        {
+            std::vector<std::vector<uint64_t>> starts(NR);
+            for (uint32_t c = 0; c < NC; c++)
+                if (ch[c].u < ch[c].v) starts[ch[c].run].push_back(ch[c].u);
+            for (uint32_t ri = 0; ri < NR; ri++) {
+                auto &v = starts[ri];
+                v.push_back(rd[ri].chain_start);
+                std::sort(v.begin(), v.end());
+                v.erase(std::unique(v.begin(), v.end()), v.end());
+                for (size_t k = 0; k < v.size(); k++) {
+                    pf_seg_dev g;
+                    memset(&g, 0, sizeof g);
+                    g.s = v[k];
+                    g.last = k + 1 == v.size();
+                    g.e = g.last ? rd[ri].a1 : v[k + 1];
+                    g.a1 = rd[ri].a1;
+                    g.run = ri;
+                    g.live = 1;
+                    sg.push_back(g);
+                }
+            }
+        }
+        const uint32_t NS_ = (uint32_t)sg.size();
         std::vector<pf_win_dev> wd(W);
         for (uint32_t w = 0; w < W; w++) {
             wd[w].beg = beg[w]; wd[w].end = end[w]; wd[w].c0 = wc[w]; wd[w].c1 = wc[w + 1];
@@ -441,10 +467,11 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         uint8_t *d_arena = D.alloc<uint8_t>(P.arena + 512);
         uint32_t *d_bst = D.alloc<uint32_t>(NB);
         pf_run_dev *d_run = D.alloc<pf_run_dev>(NR);
+        pf_seg_dev *d_sg = D.alloc<pf_seg_dev>(NS_);
         pf_chunk_dev *d_ch = D.alloc<pf_chunk_dev>(NC);
         pf_win_dev *d_win = D.alloc<pf_win_dev>(W);
         uint32_t *d_wn = D.alloc<uint32_t>(2ull * W);
-        if (!d_blk || !d_arena || !d_bst || !d_run || !d_ch || !d_win || !d_wn) { rc = PF_ERR_NOMEM; break; }
+        if (!d_blk || !d_arena || !d_bst || !d_run || !d_sg || !d_ch || !d_win || !d_wn) { rc = PF_ERR_NOMEM; break; }
         hipEvent_t ev[8];
         for (auto &e : ev) if (hipEventCreate(&e) != hipSuccess) rc = PF_ERR_HIP;
         if (rc) break;
@@ -452,20 +479,20 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         bool ok = hipMemcpyAsync(d_blk, P.blk.data(), sizeof(pf_bgzf_blk) * NB, hipMemcpyHostToDevice, st) == hipSuccess &&
                   hipMemsetAsync(d_bst, 0, 4ull * NB, st) == hipSuccess &&
                   hipMemsetAsync(d_arena + P.arena, 0, 512, st) == hipSuccess &&
-                  hipMemcpyAsync(d_run, rd.data(), sizeof(pf_run_dev) * NR, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_sg, sg.data(), sizeof(pf_seg_dev) * NS_, hipMemcpyHostToDevice, st) == hipSuccess &&
                   hipMemcpyAsync(d_ch, ch.data(), sizeof(pf_chunk_dev) * NC, hipMemcpyHostToDevice, st) == hipSuccess &&
                   hipMemcpyAsync(d_win, wd.data(), sizeof(pf_win_dev) * W, hipMemcpyHostToDevice, st) == hipSuccess &&
                   hipEventRecord(ev[0], st) == hipSuccess;
         if (ok) ok = pf_inflate_launch(st, d_comp, d_blk, NB, d_arena, d_bst, ev[0], ev[1]) == PF_OK &&
                      hipEventRecord(ev[2], st) == hipSuccess;
         // ---- chain: count, offsets, write
-        if (ok && NR) {
-            hipLaunchKernelGGL(pf_chain, dim3(NR), dim3(64), 0, st, d_arena, d_run, NR, (uint64_t *)nullptr);
+        if (ok && NS_) {
+            hipLaunchKernelGGL(pf_chain, dim3((NS_ + 63) / 64), dim3(64), 0, st, d_arena, d_sg, NS_, (uint64_t *)nullptr);
             ok = hipGetLastError() == hipSuccess;
         }
         std::vector<uint32_t> bst(NB);
         ok = ok && hipMemcpyAsync(bst.data(), d_bst, 4ull * NB, hipMemcpyDeviceToHost, st) == hipSuccess &&
-             hipMemcpyAsync(rd.data(), d_run, sizeof(pf_run_dev) * NR, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(sg.data(), d_sg, sizeof(pf_seg_dev) * NS_, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipStreamSynchronize(st) == hipSuccess;
         if (!ok) { evdone(); rc = PF_ERR_HIP; break; }
         for (uint32_t i = 0; i < NB; i++)
@@ -476,26 +503,57 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
                 break;
             }
         if (rc) { evdone(); break; }
+        // per run: its segments in order; a segment that stopped early ends the
+        // run's chain there (the later segments' records are not reachable by
+        // a serial walk either)
         uint64_t NRec = 0;
-        for (auto &R : rd) { R.rec0 = (uint32_t)NRec; NRec += R.n_rec; }
+        for (uint32_t k = 0; k < NS_;) {
+            const uint32_t ri = sg[k].run;
+            pf_run_dev &R = rd[ri];
+            R.rec0 = (uint32_t)NRec;
+            R.n_rec = 0;
+            bool dead = false;
+            for (; k < NS_ && sg[k].run == ri; k++) {
+                pf_seg_dev &g = sg[k];
+                g.live = dead ? 0u : 1u;
+                if (dead) continue;
+                g.rec0 = (uint32_t)(NRec + R.n_rec);
+                R.n_rec += g.n;
+                if (g.last || g.stop != PF_CHAIN_END) {
+                    R.stop = g.stop;
+                    R.stop_pos = g.stop_pos;
+                    dead = !g.last;
+                }
+            }
+            NRec += R.n_rec;
+        }
+        for (uint32_t ri = 0; ri < NR; ri++)              // runs without segments (no chunk of theirs reads records)
+            if (rd[ri].chain_start >= rd[ri].a1) { rd[ri].n_rec = 0; rd[ri].stop = PF_CHAIN_END; rd[ri].stop_pos = rd[ri].a1; }
         if (NRec >= (1ull << 32)) { evdone(); rc = PF_ERR_LIMIT; break; }
+        // the record arrays, one allocation
         pf_recs_dev Rv;
-        Rv.pos = D.alloc<uint64_t>(NRec); Rv.cig = D.alloc<uint64_t>(NRec); Rv.seq = D.alloc<uint64_t>(NRec);
-        Rv.qn = D.alloc<uint64_t>(NRec); Rv.mm = D.alloc<uint64_t>(NRec); Rv.ml = D.alloc<uint64_t>(NRec);
-        Rv.md = D.alloc<uint64_t>(NRec);
-        Rv.bs = D.alloc<uint32_t>(NRec); Rv.l_qseq = D.alloc<uint32_t>(NRec); Rv.ncig = D.alloc<uint32_t>(NRec);
-        Rv.rlen = D.alloc<uint32_t>(NRec); Rv.qn_len = D.alloc<uint32_t>(NRec); Rv.mm_len = D.alloc<uint32_t>(NRec);
-        Rv.ml_len = D.alloc<uint32_t>(NRec); Rv.md_len = D.alloc<uint32_t>(NRec);
-        Rv.tid = D.alloc<int32_t>(NRec); Rv.rpos = D.alloc<int32_t>(NRec); Rv.hp_tag = D.alloc<int32_t>(NRec);
-        Rv.de = D.alloc<float>(NRec); Rv.flag = D.alloc<uint16_t>(NRec);
-        Rv.mapq = D.alloc<uint8_t>(NRec); Rv.hp = D.alloc<uint8_t>(NRec); Rv.st = D.alloc<uint8_t>(NRec);
-        if (!Rv.pos || !Rv.st || !Rv.hp || !Rv.mapq || !Rv.flag || !Rv.de || !Rv.hp_tag || !Rv.rpos || !Rv.tid ||
-            !Rv.md_len || !Rv.ml_len || !Rv.mm_len || !Rv.qn_len || !Rv.rlen || !Rv.ncig || !Rv.l_qseq || !Rv.bs ||
-            !Rv.md || !Rv.ml || !Rv.mm || !Rv.qn || !Rv.seq || !Rv.cig) { evdone(); rc = PF_ERR_NOMEM; break; }
+        {
+            const uint64_t n = NRec ? NRec : 1, a8 = (8 * n + 255) & ~255ull, a4 = (4 * n + 255) & ~255ull,
+                           a2 = (2 * n + 255) & ~255ull, a1 = (n + 255) & ~255ull;
+            uint8_t *m = D.alloc<uint8_t>(8 * a8 + 12 * a4 + a2 + 3 * a1);
+            if (!m) { evdone(); rc = PF_ERR_NOMEM; break; }
+            auto take = [&](uint64_t bytes) { uint8_t *r = m; m += bytes; return r; };
+            Rv.pos = (uint64_t *)take(a8); Rv.cig = (uint64_t *)take(a8); Rv.seq = (uint64_t *)take(a8);
+            Rv.qn = (uint64_t *)take(a8); Rv.mm = (uint64_t *)take(a8); Rv.ml = (uint64_t *)take(a8);
+            Rv.md = (uint64_t *)take(a8); take(a8);
+            Rv.bs = (uint32_t *)take(a4); Rv.l_qseq = (uint32_t *)take(a4); Rv.ncig = (uint32_t *)take(a4);
+            Rv.rlen = (uint32_t *)take(a4); Rv.qn_len = (uint32_t *)take(a4); Rv.mm_len = (uint32_t *)take(a4);
+            Rv.ml_len = (uint32_t *)take(a4); Rv.md_len = (uint32_t *)take(a4);
+            Rv.tid = (int32_t *)take(a4); Rv.rpos = (int32_t *)take(a4); Rv.hp_tag = (int32_t *)take(a4);
+            Rv.de = (float *)take(a4);
+            Rv.flag = (uint16_t *)take(a2);
+            Rv.mapq = take(a1); Rv.hp = take(a1); Rv.st = take(a1);
+        }
         ok = hipMemcpyAsync(d_run, rd.data(), sizeof(pf_run_dev) * NR, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(d_sg, sg.data(), sizeof(pf_seg_dev) * NS_, hipMemcpyHostToDevice, st) == hipSuccess &&
              hipEventRecord(ev[3], st) == hipSuccess;
-        if (ok && NR) {
-            hipLaunchKernelGGL(pf_chain, dim3(NR), dim3(64), 0, st, d_arena, d_run, NR, Rv.pos);
+        if (ok && NS_) {
+            hipLaunchKernelGGL(pf_chain, dim3((NS_ + 63) / 64), dim3(64), 0, st, d_arena, d_sg, NS_, Rv.pos);
             ok = hipGetLastError() == hipSuccess;
         }
         if (ok && NRec) {

@@ -32,5 +32,5 @@ with BamFile(path) as b:
         db, qn, info = b.fetch_windows_device(ctx, cfg, "chrS", aln.win_start, aln.win_end, LoadConfig())
         out = db.run()
         db.free()
-        print(f"{(time.perf_counter() - t) * 1e3:.1f} ms, {int(out.win_n_reads.sum())} reads, "
-              f"inflate {info['ms_inflate']:.1f} ms, read {info['ms_read']:.1f} ms", flush=True)
+        ms = {k: round(v, 2) for k, v in info.items() if k.startswith("ms_")}
+        print(f"{(time.perf_counter() - t) * 1e3:.1f} ms, {int(out.win_n_reads.sum())} reads, {ms}", flush=True)
