@@ -463,6 +463,7 @@ typedef struct pf_bam_dev_fetch {
     uint64_t comp_bytes, inflated_bytes, n_blocks, n_chain_recs;
     double ms_read, ms_inflate, ms_chain, ms_decode, ms_select, ms_build, ms_total;
     uint32_t attempts;             /* plans tried (a record past the planned blocks widens the plan) */
+    const uint8_t *read_hp;        /* pf_haptag_bam: [n_recs] each read's tag (NULL otherwise)  */
 } pf_bam_dev_fetch_t;
 /* replace a record-level batch's per-record HP values (the -u table's tags,
  * blockjoin.c:1114-1122); n must equal its record count */
@@ -471,6 +472,13 @@ int  pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t
                          const char *chrom, uint32_t n_windows, const uint32_t *win_start, const uint32_t *win_end,
                          uint32_t readback, uint32_t max_win_recs, pf_dbatch_t **out, pf_bam_dev_fetch_t **fetch);
 void pf_bam_dev_fetch_free(pf_bam_dev_fetch_t *fetch);
+/* The -u pre-pass with the device fetch: the reads pf_bam_fetch_contig_reads
+ * returns (the whole contig, primary mapped, MD:Z required: PF_ERR_ARG
+ * otherwise) inflated, selected and gathered on the device and haptagged there
+ * by K4 against `known` (pf_haptag_reads' semantics).  *fetch holds n_recs
+ * reads in BAM order: read_hp, qnames. */
+int  pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, const char *chrom,
+                   pf_bam_dev_fetch_t **fetch);
 
 /* The -u pre-pass reads of one contig (pre_haplotagging_read_in_one_ref,
  * 1841-1898: sam_itr_querys over the whole contig, flags 4/256/2048

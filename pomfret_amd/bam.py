@@ -57,7 +57,7 @@ class PfBamDevFetch(C.Structure):
                 ("inflated_bytes", C.c_uint64), ("n_blocks", C.c_uint64), ("n_chain_recs", C.c_uint64),
                 ("ms_read", C.c_double), ("ms_inflate", C.c_double), ("ms_chain", C.c_double),
                 ("ms_decode", C.c_double), ("ms_select", C.c_double), ("ms_build", C.c_double),
-                ("ms_total", C.c_double), ("attempts", C.c_uint32)]
+                ("ms_total", C.c_double), ("attempts", C.c_uint32), ("read_hp", C.c_void_p)]
 
 
 def _bind():
@@ -94,6 +94,8 @@ def _bind():
                                       C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_void_p),
                                       C.POINTER(C.POINTER(PfBamDevFetch))]
     L.pf_bam_dev_fetch_free.argtypes = [C.POINTER(PfBamDevFetch)]
+    L.pf_haptag_bam.argtypes = [C.c_void_p, C.POINTER(PfKnownVars), C.c_void_p, C.c_char_p,
+                                C.POINTER(C.POINTER(PfBamDevFetch))]
     _bound = True
     return L
 
@@ -230,13 +232,35 @@ class BamFile:
             qb = _arr(r.qname, qo[-1] if n else 0, np.uint8).tobytes()
             qnames = [qb[qo[i]:qo[i + 1]].decode("ascii", "replace") for i in range(n)]
             info = {k: getattr(r, k) for k, _ in PfBamDevFetch._fields_
-                    if k not in ("win_rec_off", "win_n_fetched", "qname_off", "qname", "hp_tag")}
+                    if k not in ("win_rec_off", "win_n_fetched", "qname_off", "qname", "hp_tag", "read_hp")}
             info["win_rec_off"] = _arr(r.win_rec_off, W + 1, np.uint32)
             info["win_n_fetched"] = _arr(r.win_n_fetched, W, np.uint32)
             info["hp_tag"] = _arr(r.hp_tag, n, np.int32)
         finally:
             L.pf_bam_dev_fetch_free(f)
         return DeviceBatch._wrap(ctx, h, W), qnames, info
+
+    def haptag_device(self, ctx, chrom: str, known) -> Tuple[np.ndarray, List[str], dict]:
+        """The -u pre-pass of one contig through the device fetch
+        (pf_haptag_bam): (tag per read, qnames, info), reads in BAM order."""
+        if self.path is None:
+            raise PomfretError("index-only BamFile cannot fetch")
+        L = _bind()
+        kc = known.to_c()
+        f = C.POINTER(PfBamDevFetch)()
+        _check(L.pf_haptag_bam(ctx.handle, C.byref(kc), self.handle, chrom.encode(), C.byref(f)), "pf_haptag_bam")
+        try:
+            r = f.contents
+            n = int(r.n_recs)
+            qo = _arr(r.qname_off, n + 1, np.uint64)
+            qb = _arr(r.qname, qo[-1] if n else 0, np.uint8).tobytes()
+            qnames = [qb[qo[i]:qo[i + 1]].decode("ascii", "replace") for i in range(n)]
+            hp = _arr(r.read_hp, n, np.uint8)
+            info = {k: getattr(r, k) for k, _ in PfBamDevFetch._fields_ if k.startswith("ms_") or k in
+                    ("n_truncated", "comp_bytes", "inflated_bytes", "n_blocks", "n_chain_recs", "attempts")}
+        finally:
+            L.pf_bam_dev_fetch_free(f)
+        return hp, qnames, info
 
     def estimate_coverage(self) -> List[int]:
         """estimate_read_coverage_dirtyfast (blockjoin.c:951-1040): per contig."""

@@ -207,12 +207,16 @@ __global__ __launch_bounds__(256) void pf_recdec(const uint8_t *arena, uint32_t 
     }
     // CIGAR query and reference lengths (lane-parallel)
     uint64_t rl = 0, ql = 0;
+    uint32_t nins = 0;
     if (!(st & PF_REC_CORRUPT)) {
         for (uint32_t c = lane; c < ncig; c += 64) {
             const uint32_t v = ld32u(a, cig + 4ull * c), op = v & 15u, ln = v >> 4;
             if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += ln;
             if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += ln;
+            nins += op == 1 ? 1u : 0u;
         }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) nins += (uint32_t)__shfl_xor((int)nins, o, 64);
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             rl += (uint64_t)__shfl_xor((long long)rl, o, 64);
@@ -253,6 +257,7 @@ __global__ __launch_bounds__(256) void pf_recdec(const uint8_t *arena, uint32_t 
         R.mapq[r] = (uint8_t)mapq;
         R.l_qseq[r] = (uint32_t)lseq;
         R.ncig[r] = ncig;
+        R.nins[r] = nins;
         R.cig[r] = cig;
         R.seq[r] = seq;
         R.qn[r] = d + 32;
@@ -309,7 +314,10 @@ __global__ __launch_bounds__(256) void pf_select(const pf_win_dev *wins, uint32_
             const bool halt = in && ((rst & (PF_REC_CORRUPT | PF_REC_TRUNC)) || tid != W.tid || (int64_t)rp >= W.end);
             const uint64_t mh = __ballot(halt), mi = __ballot(in);
             const uint32_t fh = mh ? (uint32_t)__ffsll((long long)mh) - 1 : 64u;
-            const bool take = in && lane < fh && (int64_t)rp + (int64_t)(in ? R.rlen[k] : 0) > W.beg;
+            // -u reads (pre_haplotagging_read_in_one_ref, 1869-1871): primary mapped only
+            const bool take = in && lane < fh && (int64_t)rp + (int64_t)(in ? R.rlen[k] : 0) > W.beg &&
+                              (!W.reads || !(R.flag[k] & (4u | 256u | 2048u)));
+            if (W.reads && __ballot(take && !(rst & PF_REC_MD))) { status = PF_WIN_ERR; stop = true; break; }
             const uint64_t mt = __ballot(take);
             if (write && take) out[W.out + cnt + (uint32_t)__popcll(mt & lanemask_lt(lane))] = k;
             cnt += (uint32_t)__popcll(mt);
@@ -359,7 +367,7 @@ __global__ __launch_bounds__(256) void pf_gather_small(const uint32_t *sel, uint
                                                        uint8_t *mapq, uint32_t *pos, uint32_t *l_qseq, float *de,
                                                        uint8_t *hp, int32_t *hp_tag, uint32_t *ncig, uint32_t *mm_len,
                                                        uint32_t *ml_len, uint32_t *qn_len, uint32_t *md_len,
-                                                       uint32_t *rlen, uint8_t *st) {
+                                                       uint32_t *rlen, uint8_t *st, uint32_t *nins) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = sel[i];
@@ -377,6 +385,7 @@ __global__ __launch_bounds__(256) void pf_gather_small(const uint32_t *sel, uint
     md_len[i] = R.md_len[k];
     rlen[i] = R.rlen[k];
     st[i] = R.st[k];
+    nins[i] = R.nins[k];
 }
 
 // byte copy (any alignment), one wave
@@ -404,7 +413,7 @@ __global__ __launch_bounds__(256) void pf_gather_big(const uint8_t *arena, const
     if (seq) {
         const uint64_t sb = ((uint64_t)R.l_qseq[k] + 1) / 2, s0 = seq_off[i], s1 = seq_off[i + 1];
         uint8_t *dst = seq + s0;
-        const uint64_t nw = sb / 4;
+        const uint64_t nw = (s0 & 3u) ? 0 : sb / 4;          // unaligned slices (the -u reads): bytes
         wcopy32(reinterpret_cast<uint32_t *>(dst), arena, R.seq[k], nw, lane);
         for (uint64_t j = 4 * nw + lane; j < s1 - s0; j += 64) dst[j] = j < sb ? arena[R.seq[k] + j] : 0;
     }

@@ -23,6 +23,7 @@
 // reads of a contig; the host resolves it once (O(reads + variants)) and hands
 // every read its slice bounds.
 #include <hip/hip_runtime.h>
+#include "pf_ingest.h"
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -561,11 +562,14 @@ static hipError_t put(std::vector<void *> &al, T **dst, const T *src, size_t n) 
     return e;
 }
 
-extern "C" int pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *K, const pf_read_aln_batch_t *Rb,
-                               uint8_t *hp_out) {
-    if (!ctx || !K || !Rb || !hp_out) return PF_ERR_ARG;
-    const uint32_t N = Rb->n_reads, V = K->n;
+// K4 over reads whose arrays may already be on the device: per read the host
+// needs start, end, the number of CIGAR insertions, the CIGAR length and the
+// MD length (the cursor chain and the scratch slices); dv supplies the reads'
+// device arrays (cigar_off .. md) or is null (copied from Rb's host arrays).
+int pf_haptag_core(pf_ctx_t *ctx, const pf_known_vars_t *K, uint32_t N, const pf_k4_reads_host &h,
+                   const pf_read_aln_batch_t *Rb, const pf_k4_reads_dev *dv, uint8_t *hp_out) {
     if (N == 0) return PF_OK;
+    const uint32_t V = K->n;
     if (V == 0) { memset(hp_out, HAPTAG_UNPHASED, N); return PF_OK; }
     int rc = PF_OK;
     bool thread_impl = false;
@@ -581,16 +585,13 @@ extern "C" int pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *K, const pf
         uint64_t acc = 0;
         for (uint32_t r = 0; r < N; r++) {
             uint32_t i = prev;
-            while (i < V && K->pos[i] < Rb->start[r]) i++;
+            while (i < V && K->pos[i] < h.start[r]) i++;
             prev = i == 0 ? 0 : i - 1;
             uint32_t j = i;
-            while (j < V && K->pos[j] < Rb->end[r]) j++;
+            while (j < V && K->pos[j] < h.end[r]) j++;
             il[r] = i; je[r] = j;
-            uint32_t n_ins = 0;
-            for (uint64_t c = Rb->cigar_off[r]; c < Rb->cigar_off[r + 1]; c++) n_ins += (Rb->cigar[c] & 0xf) == 1;
-            const uint64_t mdl = Rb->md_off[r + 1] - Rb->md_off[r];
-            const uint64_t ncig = Rb->cigar_off[r + 1] - Rb->cigar_off[r];
-            const uint64_t vcap = n_ins + mdl + 1;
+            const uint64_t mdl = h.md_len[r], ncig = h.ncig[r];
+            const uint64_t vcap = h.n_ins[r] + mdl + 1;
             // u32 units: per-thread kernel keys (nk + vcap u64) + RVar (16 B each);
             // wave kernel I lists (5 ncig + 1), MD events (4 mdl), sorted knowns (2 nk)
             const uint64_t need_t = 2 * ((j - i) + vcap + 2 * vcap);
@@ -603,7 +604,6 @@ extern "C" int pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *K, const pf
     {
         const int dev = pf_ctx_device(ctx);
         hipStream_t st = pf_ctx_stream(ctx);
-        const uint64_t ncig = Rb->cigar_off[N], nseq = Rb->seq_off[N], nmd = Rb->md_off[N];
         HCHK(hipSetDevice(dev));
         d.n_reads = N; d.n_known = V;
         HCHK(put(al, (uint32_t **)&d.kpos, K->pos, V));
@@ -612,15 +612,21 @@ extern "C" int pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *K, const pf
         HCHK(put(al, (uint8_t **)&d.khap, K->haptag, V));
         HCHK(put(al, (uint64_t **)&d.kchar_off, K->char_off, V + 1));
         HCHK(put(al, (uint8_t **)&d.kchars, K->chars, K->char_off[V]));
-        HCHK(put(al, (uint32_t **)&d.start, Rb->start, N));
-        HCHK(put(al, (uint32_t **)&d.end, Rb->end, N));
-        HCHK(put(al, (uint64_t **)&d.cigar_off, Rb->cigar_off, N + 1));
-        HCHK(put(al, (uint32_t **)&d.cigar, Rb->cigar, ncig));
-        HCHK(put(al, (uint64_t **)&d.seq_off, Rb->seq_off, N + 1));
-        HCHK(put(al, (uint32_t **)&d.seq_len, Rb->seq_len, N));
-        HCHK(put(al, (uint8_t **)&d.seq, Rb->seq, nseq));
-        HCHK(put(al, (uint64_t **)&d.md_off, Rb->md_off, N + 1));
-        HCHK(put(al, (uint8_t **)&d.md, (const uint8_t *)Rb->md, nmd));
+        if (dv) {
+            d.start = dv->start; d.end = dv->end; d.cigar_off = dv->cigar_off; d.cigar = dv->cigar;
+            d.seq_off = dv->seq_off; d.seq_len = dv->seq_len; d.seq = dv->seq; d.md_off = dv->md_off; d.md = dv->md;
+        } else {
+            const uint64_t ncig = Rb->cigar_off[N], nseq = Rb->seq_off[N], nmd = Rb->md_off[N];
+            HCHK(put(al, (uint32_t **)&d.start, Rb->start, N));
+            HCHK(put(al, (uint32_t **)&d.end, Rb->end, N));
+            HCHK(put(al, (uint64_t **)&d.cigar_off, Rb->cigar_off, N + 1));
+            HCHK(put(al, (uint32_t **)&d.cigar, Rb->cigar, ncig));
+            HCHK(put(al, (uint64_t **)&d.seq_off, Rb->seq_off, N + 1));
+            HCHK(put(al, (uint32_t **)&d.seq_len, Rb->seq_len, N));
+            HCHK(put(al, (uint8_t **)&d.seq, Rb->seq, nseq));
+            HCHK(put(al, (uint64_t **)&d.md_off, Rb->md_off, N + 1));
+            HCHK(put(al, (uint8_t **)&d.md, (const uint8_t *)Rb->md, nmd));
+        }
         HCHK(put(al, (uint32_t **)&d.i_left, il.data(), N));
         HCHK(put(al, (uint32_t **)&d.j_end, je.data(), N));
         HCHK(put(al, (uint64_t **)&d.scr_off, so.data(), N + 1));
@@ -665,4 +671,21 @@ done:
     if (e1) (void)hipEventDestroy(e1);
     for (void *p : al) (void)hipFree(p);
     return rc;
+}
+
+extern "C" int pf_haptag_reads(pf_ctx_t *ctx, const pf_known_vars_t *K, const pf_read_aln_batch_t *Rb,
+                               uint8_t *hp_out) {
+    if (!ctx || !K || !Rb || !hp_out) return PF_ERR_ARG;
+    const uint32_t N = Rb->n_reads;
+    if (N == 0) return PF_OK;
+    std::vector<uint32_t> nins(N), ncig(N), mdl(N);
+    for (uint32_t r = 0; r < N; r++) {
+        uint32_t n = 0;
+        for (uint64_t c = Rb->cigar_off[r]; c < Rb->cigar_off[r + 1]; c++) n += (Rb->cigar[c] & 0xf) == 1;
+        nins[r] = n;
+        ncig[r] = (uint32_t)(Rb->cigar_off[r + 1] - Rb->cigar_off[r]);
+        mdl[r] = (uint32_t)(Rb->md_off[r + 1] - Rb->md_off[r]);
+    }
+    pf_k4_reads_host h{Rb->start, Rb->end, nins.data(), ncig.data(), mdl.data()};
+    return pf_haptag_core(ctx, K, N, h, Rb, nullptr, hp_out);
 }

@@ -58,7 +58,8 @@ typedef struct pf_win_dev {
     int64_t beg, end;         // region [beg, end)
     uint32_t c0, c1;          // its chunks
     int32_t tid;
-    uint32_t skip;            // write pass: window emptied (over the record limit)
+    uint16_t skip;            // write pass: window emptied (over the record limit)
+    uint16_t reads;           // the -u pre-pass fetch: primary mapped records only, MD:Z required
     uint64_t out;             // write pass: first slot of its record list
 } pf_win_dev;
 
@@ -72,7 +73,7 @@ typedef struct pf_win_dev {
 typedef struct pf_recs_dev {
     uint64_t *pos;            // arena position of the block_size field
     uint64_t *cig, *seq, *qn, *mm, *ml;     // arena positions
-    uint32_t *bs, *l_qseq, *ncig, *rlen, *qn_len, *mm_len, *ml_len, *md_len;
+    uint32_t *bs, *l_qseq, *ncig, *rlen, *qn_len, *mm_len, *ml_len, *md_len, *nins;
     int32_t *tid, *rpos, *hp_tag;
     float *de;
     uint16_t *flag;
@@ -90,8 +91,31 @@ __global__ void pf_select(const pf_win_dev *wins, uint32_t n_wins, const pf_chun
 __global__ void pf_gather_small(const uint32_t *sel, uint64_t n, pf_recs_dev R, uint16_t *flag, uint8_t *mapq,
                                 uint32_t *pos, uint32_t *l_qseq, float *de, uint8_t *hp, int32_t *hp_tag,
                                 uint32_t *ncig, uint32_t *mm_len, uint32_t *ml_len, uint32_t *qn_len,
-                                uint32_t *md_len, uint32_t *rlen, uint8_t *st);
+                                uint32_t *md_len, uint32_t *rlen, uint8_t *st, uint32_t *nins);
 __global__ void pf_gather_big(const uint8_t *arena, const uint32_t *sel, uint64_t n, pf_recs_dev R,
                               const uint64_t *cig_off, uint32_t *cig, const uint64_t *seq_off, uint8_t *seq,
                               const uint64_t *mm_off, uint8_t *mm, const uint64_t *ml_off, uint8_t *ml,
                               const uint64_t *qn_off, uint8_t *qn, const uint64_t *md_off, uint8_t *md);
+
+// -u reads for K4 (pf_haptag.hip): per-read host fields the cursor chain and
+// scratch sizing need, and the reads' device arrays
+typedef struct pf_k4_reads_host {
+    const uint32_t *start, *end, *n_ins, *ncig, *md_len;
+} pf_k4_reads_host;
+typedef struct pf_k4_reads_dev {
+    const uint32_t *start, *end;
+    const uint64_t *cigar_off;
+    const uint32_t *cigar;
+    const uint64_t *seq_off;
+    const uint32_t *seq_len;
+    const uint8_t *seq;
+    const uint64_t *md_off;
+    const uint8_t *md;
+} pf_k4_reads_dev;
+#ifdef __cplusplus
+struct pf_ctx;
+struct pf_known_vars;
+struct pf_read_aln_batch;
+int pf_haptag_core(struct pf_ctx *ctx, const struct pf_known_vars *K, uint32_t N, const pf_k4_reads_host &h,
+                   const struct pf_read_aln_batch *Rb, const pf_k4_reads_dev *dv, uint8_t *hp_out);
+#endif

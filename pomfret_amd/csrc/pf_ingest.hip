@@ -194,12 +194,13 @@ uint8_t *pinned(int dev, size_t n) {
 struct Small {
     std::vector<uint16_t> flag;
     std::vector<uint8_t> mapq, hp, st;
-    std::vector<uint32_t> pos, l_qseq, ncig, mm_len, ml_len, qn_len, md_len, rlen;
+    std::vector<uint32_t> pos, l_qseq, ncig, mm_len, ml_len, qn_len, md_len, rlen, nins;
     std::vector<float> de;
     std::vector<int32_t> hp_tag;
     void resize(size_t n) {
         flag.resize(n); mapq.resize(n); hp.resize(n); st.resize(n); pos.resize(n); l_qseq.resize(n);
         ncig.resize(n); mm_len.resize(n); ml_len.resize(n); qn_len.resize(n); md_len.resize(n); rlen.resize(n);
+        nins.resize(n);
         de.resize(n); hp_tag.resize(n);
     }
 };
@@ -219,6 +220,7 @@ int read_range(int fd, uint64_t off, uint64_t n, uint8_t *dst) {
 
 struct pf_bam_dev_fetch_own {
     pf_bam_dev_fetch_t pub;
+    std::vector<uint8_t> read_hp;
     std::vector<uint32_t> win_rec_off, win_n, win_status;
     std::vector<uint64_t> qn_off, md_off;
     std::vector<char> qn, md;
@@ -250,26 +252,32 @@ static int dev_fill(void *user, pf_ctx *ctx, pf_load_dev *ld, const uint64_t *se
     return hipStreamSynchronize(f->st) == hipSuccess ? PF_OK : PF_ERR_HIP;
 }
 
-extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lc, pf_bam_t *bam,
-                                   const char *chrom, uint32_t W, const uint32_t *ws, const uint32_t *we,
-                                   uint32_t readback, uint32_t max_win_recs, pf_dbatch_t **out,
-                                   pf_bam_dev_fetch_t **fetch_out) {
-    if (!ctx || !cfg || !lc || !bam || !chrom || !out || !fetch_out || (W && (!ws || !we))) return PF_ERR_ARG;
-    *out = nullptr;
-    *fetch_out = nullptr;
+// what the device fetch hands its sink: the arena, the selected records
+// (indices into the decoded record arrays, window by window) and their small
+// fields on the host; device memory stays valid until the sink returns
+struct FetchOut {
+    const uint8_t *arena;
+    const uint32_t *sel;
+    uint64_t n;
+    pf_recs_dev R;
+    const Small *S;
+    hipStream_t st;
+    DevBuf *D;
+};
+
+// The device fetch of W regions [beg, end) of tid (reads: the -u pre-pass
+// records); F receives window counts, qnames and statistics; sink builds what
+// the caller needs from the gathered records.
+template <typename Sink>
+static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, const int64_t *beg, const int64_t *end,
+                     uint32_t reads, uint32_t max_win_recs, pf_bam_dev_fetch_own *F, Sink &&sink) {
     const char *path = pf_bam_path(bam);
-    const int32_t tid = pf_bam_tid(bam, chrom);
     if (!path || tid < 0) return PF_ERR_ARG;
     const double t_start = now_ms();
     // ---- chunk lists (the BAI query of every window)
-    std::vector<int64_t> beg(W), end(W);
     std::vector<uint64_t> uv;
     std::vector<uint32_t> wc(W + 1, 0);
     for (uint32_t w = 0; w < W; w++) {
-        const int64_t s = (int32_t)ws[w], e = (int32_t)we[w], rb = (int32_t)readback;
-        const int64_t b1 = s - rb > 0 ? s - rb : 0;
-        beg[w] = b1 > 0 ? b1 - 1 : 0;
-        end[w] = e + rb;
         const int64_t n = pf_bam_query_chunks(bam, tid, beg[w], end[w], nullptr, 0);
         if (n < 0) return (int)n;
         const size_t o = uv.size();
@@ -285,7 +293,6 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
     const uint64_t fsize = (uint64_t)stt.st_size;
     hipStream_t st = pf_ctx_stream((const pf_ctx *)ctx);
     if (hipSetDevice(pf_ctx_device((const pf_ctx *)ctx)) != hipSuccess) { close(fd); return PF_ERR_HIP; }
-    pf_bam_dev_fetch_own *F = new pf_bam_dev_fetch_own();
     memset(&F->pub, 0, sizeof F->pub);
     int rc = PF_OK;
     uint64_t ext = 4ull << 16;            // bytes read past a chunk's last block (records spanning blocks)
@@ -459,7 +466,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         std::vector<pf_win_dev> wd(W);
         for (uint32_t w = 0; w < W; w++) {
             wd[w].beg = beg[w]; wd[w].end = end[w]; wd[w].c0 = wc[w]; wd[w].c1 = wc[w + 1];
-            wd[w].tid = tid; wd[w].skip = 0; wd[w].out = 0;
+            wd[w].tid = tid; wd[w].skip = 0; wd[w].reads = (uint16_t)reads; wd[w].out = 0;
         }
         // ---- upload + inflate
         t0 = now_ms();
@@ -535,7 +542,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         {
             const uint64_t n = NRec ? NRec : 1, a8 = (8 * n + 255) & ~255ull, a4 = (4 * n + 255) & ~255ull,
                            a2 = (2 * n + 255) & ~255ull, a1 = (n + 255) & ~255ull;
-            uint8_t *m = D.alloc<uint8_t>(8 * a8 + 12 * a4 + a2 + 3 * a1);
+            uint8_t *m = D.alloc<uint8_t>(8 * a8 + 13 * a4 + a2 + 3 * a1);
             if (!m) { evdone(); rc = PF_ERR_NOMEM; break; }
             auto take = [&](uint64_t bytes) { uint8_t *r = m; m += bytes; return r; };
             Rv.pos = (uint64_t *)take(a8); Rv.cig = (uint64_t *)take(a8); Rv.seq = (uint64_t *)take(a8);
@@ -543,7 +550,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
             Rv.md = (uint64_t *)take(a8); take(a8);
             Rv.bs = (uint32_t *)take(a4); Rv.l_qseq = (uint32_t *)take(a4); Rv.ncig = (uint32_t *)take(a4);
             Rv.rlen = (uint32_t *)take(a4); Rv.qn_len = (uint32_t *)take(a4); Rv.mm_len = (uint32_t *)take(a4);
-            Rv.ml_len = (uint32_t *)take(a4); Rv.md_len = (uint32_t *)take(a4);
+            Rv.ml_len = (uint32_t *)take(a4); Rv.md_len = (uint32_t *)take(a4); Rv.nins = (uint32_t *)take(a4);
             Rv.tid = (int32_t *)take(a4); Rv.rpos = (int32_t *)take(a4); Rv.hp_tag = (int32_t *)take(a4);
             Rv.de = (float *)take(a4);
             Rv.flag = (uint16_t *)take(a2);
@@ -604,23 +611,23 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         S.resize(NS);
         uint16_t *g_flag = D.alloc<uint16_t>(NS);
         uint8_t *g_mapq = D.alloc<uint8_t>(NS), *g_hp = D.alloc<uint8_t>(NS), *g_st = D.alloc<uint8_t>(NS);
-        uint32_t *g32 = D.alloc<uint32_t>(8 * NS);
+        uint32_t *g32 = D.alloc<uint32_t>(9 * NS);
         float *g_de = D.alloc<float>(NS);
         int32_t *g_hpt = D.alloc<int32_t>(NS);
         if (!g_flag || !g_mapq || !g_hp || !g_st || !g32 || !g_de || !g_hpt) { evdone(); rc = PF_ERR_NOMEM; break; }
         if (ok && NS) {
             hipLaunchKernelGGL(pf_gather_small, dim3((unsigned)((NS + 255) / 256)), dim3(256), 0, st, d_sel, NS, Rv,
                                g_flag, g_mapq, g32, g32 + NS, g_de, g_hp, g_hpt, g32 + 2 * NS, g32 + 3 * NS,
-                               g32 + 4 * NS, g32 + 5 * NS, g32 + 6 * NS, g32 + 7 * NS, g_st);
+                               g32 + 4 * NS, g32 + 5 * NS, g32 + 6 * NS, g32 + 7 * NS, g_st, g32 + 8 * NS);
             ok = hipGetLastError() == hipSuccess;
         }
         ok = ok && hipEventRecord(ev[5], st) == hipSuccess;
-        std::vector<uint32_t> h32(8 * NS);
+        std::vector<uint32_t> h32(9 * NS);
         ok = ok && hipMemcpyAsync(S.flag.data(), g_flag, 2 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipMemcpyAsync(S.mapq.data(), g_mapq, NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipMemcpyAsync(S.hp.data(), g_hp, NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipMemcpyAsync(S.st.data(), g_st, NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
-             hipMemcpyAsync(h32.data(), g32, 32 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipMemcpyAsync(h32.data(), g32, 36 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipMemcpyAsync(S.de.data(), g_de, 4 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipMemcpyAsync(S.hp_tag.data(), g_hpt, 4 * NS, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipStreamSynchronize(st) == hipSuccess;
@@ -633,6 +640,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         memcpy(S.qn_len.data(), h32.data() + 5 * NS, 4 * NS);
         memcpy(S.md_len.data(), h32.data() + 6 * NS, 4 * NS);
         memcpy(S.rlen.data(), h32.data() + 7 * NS, 4 * NS);
+        memcpy(S.nins.data(), h32.data() + 8 * NS, 4 * NS);
         // ---- qnames (and MD) -> host
         F->qn_off.assign(NS + 1, 0);
         F->md_off.assign(NS + 1, 0);
@@ -656,25 +664,12 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         ok = ok && hipMemcpyAsync(F->qn.data(), d_qn, F->qn_off[NS], hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipStreamSynchronize(st) == hipSuccess;
         if (!ok) { evdone(); rc = PF_ERR_HIP; break; }
-        // ---- the record-level batch: sizes on the host, large arrays gathered on the device
-        std::vector<uint64_t> cig_off(NS + 1, 0), mm_off(NS + 1, 0), ml_off(NS + 1, 0);
-        for (uint64_t i = 0; i < NS; i++) {
-            cig_off[i + 1] = cig_off[i] + S.ncig[i];
-            mm_off[i + 1] = mm_off[i] + S.mm_len[i];
-            ml_off[i + 1] = ml_off[i] + S.ml_len[i];
-        }
-        pf_aln_batch_t a;
-        memset(&a, 0, sizeof a);
-        a.n_windows = W;
-        a.n_recs = (uint32_t)NS;
-        a.win_start = ws; a.win_end = we; a.win_rec_off = F->win_rec_off.data();
-        a.flag = S.flag.data(); a.mapq = S.mapq.data(); a.pos = S.pos.data(); a.l_qseq = S.l_qseq.data();
-        a.de = S.de.data(); a.hp = S.hp.data();
-        a.cigar_off = cig_off.data(); a.mm_off = mm_off.data(); a.ml_off = ml_off.data();
-        DevFill df{d_arena, d_sel, NS, Rv, nullptr, nullptr, nullptr, st};
-        pf_aln_fill_t fl{dev_fill, &df};
+        // ---- the caller's product of the gathered records
         ok = hipEventRecord(ev[6], st) == hipSuccess;
-        rc = ok ? pf_aln_build(ctx, cfg, lc, &a, &fl, out) : PF_ERR_HIP;
+        {
+            FetchOut fo{d_arena, d_sel, NS, Rv, &S, st, &D};
+            rc = ok ? sink(fo) : PF_ERR_HIP;
+        }
         ok = hipEventRecord(ev[7], st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
         float ms_inf = 0, ms_chain = 0, ms_dec = 0, ms_sel = 0, ms_build = 0;
         if (ok) {
@@ -710,11 +705,107 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
         break;
     }
     close(fd);
+    return rc;
+}
+
+extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cfg_t *lc, pf_bam_t *bam,
+                                   const char *chrom, uint32_t W, const uint32_t *ws, const uint32_t *we,
+                                   uint32_t readback, uint32_t max_win_recs, pf_dbatch_t **out,
+                                   pf_bam_dev_fetch_t **fetch_out) {
+    if (!ctx || !cfg || !lc || !bam || !chrom || !out || !fetch_out || (W && (!ws || !we))) return PF_ERR_ARG;
+    *out = nullptr;
+    *fetch_out = nullptr;
+    // the region string load_reads_given_interval builds (1053-1054):
+    // chrom:max(s-rb,0)-(e+rb), htslib's 0-based [max(b-1, 0), E)
+    std::vector<int64_t> beg(W), end(W);
+    for (uint32_t w = 0; w < W; w++) {
+        const int64_t s = (int32_t)ws[w], e = (int32_t)we[w], rb = (int32_t)readback;
+        const int64_t b1 = s - rb > 0 ? s - rb : 0;
+        beg[w] = b1 > 0 ? b1 - 1 : 0;
+        end[w] = e + rb;
+    }
+    pf_bam_dev_fetch_own *F = new pf_bam_dev_fetch_own();
+    int rc = dev_fetch(ctx, bam, pf_bam_tid(bam, chrom), W, beg.data(), end.data(), 0u, max_win_recs, F,
+                       [&](FetchOut &fo) -> int {
+        // the record-level batch: sizes on the host, large arrays gathered on the device
+        const Small &S = *fo.S;
+        const uint64_t NS = fo.n;
+        std::vector<uint64_t> cig_off(NS + 1, 0), mm_off(NS + 1, 0), ml_off(NS + 1, 0);
+        for (uint64_t i = 0; i < NS; i++) {
+            cig_off[i + 1] = cig_off[i] + S.ncig[i];
+            mm_off[i + 1] = mm_off[i] + S.mm_len[i];
+            ml_off[i + 1] = ml_off[i] + S.ml_len[i];
+        }
+        pf_aln_batch_t a;
+        memset(&a, 0, sizeof a);
+        a.n_windows = W;
+        a.n_recs = (uint32_t)NS;
+        a.win_start = ws; a.win_end = we; a.win_rec_off = F->win_rec_off.data();
+        a.flag = S.flag.data(); a.mapq = S.mapq.data(); a.pos = S.pos.data(); a.l_qseq = S.l_qseq.data();
+        a.de = S.de.data(); a.hp = S.hp.data();
+        a.cigar_off = cig_off.data(); a.mm_off = mm_off.data(); a.ml_off = ml_off.data();
+        DevFill df{fo.arena, fo.sel, NS, fo.R, nullptr, nullptr, nullptr, fo.st};
+        pf_aln_fill_t fl{dev_fill, &df};
+        return pf_aln_build(ctx, cfg, lc, &a, &fl, out);
+    });
     if (rc || !*out) {
         if (*out) { pf_batch_free(*out); *out = nullptr; }
         delete F;
         return rc ? rc : PF_ERR_INTERNAL;
     }
+    *fetch_out = &F->pub;
+    return PF_OK;
+}
+
+extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
+                             pf_bam_dev_fetch_t **fetch_out) {
+    if (!ctx || !K || !bam || !chrom || !fetch_out) return PF_ERR_ARG;
+    *fetch_out = nullptr;
+    // sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX)
+    const int64_t beg = 0, end = INT64_MAX;
+    pf_bam_dev_fetch_own *F = new pf_bam_dev_fetch_own();
+    int rc = dev_fetch(ctx, bam, pf_bam_tid(bam, chrom), 1, &beg, &end, 1u, 0u, F, [&](FetchOut &fo) -> int {
+        const Small &S = *fo.S;
+        const uint64_t N = fo.n;
+        if (N >= (1ull << 32)) return PF_ERR_LIMIT;
+        F->read_hp.assign(N, 0);
+        if (!N) return PF_OK;
+        std::vector<uint32_t> start(N), endp(N);
+        std::vector<uint64_t> co(N + 1, 0), so(N + 1, 0), mo(N + 1, 0);
+        for (uint64_t i = 0; i < N; i++) {
+            start[i] = S.pos[i];
+            endp[i] = (uint32_t)((int64_t)(int32_t)S.pos[i] + (int64_t)S.rlen[i]);   // bam_endpos
+            co[i + 1] = co[i] + S.ncig[i];
+            so[i + 1] = so[i] + (S.l_qseq[i] + 1ull) / 2;
+            mo[i + 1] = mo[i] + S.md_len[i];
+        }
+        DevBuf &D = *fo.D;
+        uint32_t *d_start = D.alloc<uint32_t>(N), *d_end = D.alloc<uint32_t>(N), *d_len = D.alloc<uint32_t>(N);
+        uint64_t *d_co = D.alloc<uint64_t>(N + 1), *d_so = D.alloc<uint64_t>(N + 1), *d_mo = D.alloc<uint64_t>(N + 1);
+        uint32_t *d_cig = D.alloc<uint32_t>(co[N]);
+        uint8_t *d_seq = D.alloc<uint8_t>(so[N] + 16), *d_md = D.alloc<uint8_t>(mo[N] + 16);
+        if (!d_start || !d_end || !d_len || !d_co || !d_so || !d_mo || !d_cig || !d_seq || !d_md) return PF_ERR_NOMEM;
+        hipStream_t st = fo.st;
+        bool ok = hipMemcpyAsync(d_start, start.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_end, endp.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_len, S.l_qseq.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_co, co.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_so, so.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
+                  hipMemcpyAsync(d_mo, mo.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(pf_gather_big, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, fo.arena, fo.sel, N, fo.R,
+                               (const uint64_t *)d_co, d_cig, (const uint64_t *)d_so, d_seq, (const uint64_t *)nullptr,
+                               (uint8_t *)nullptr, (const uint64_t *)nullptr, (uint8_t *)nullptr,
+                               (const uint64_t *)nullptr, (uint8_t *)nullptr, (const uint64_t *)d_mo, d_md);
+            ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+        }
+        if (!ok) return PF_ERR_HIP;
+        pf_k4_reads_host h{start.data(), endp.data(), S.nins.data(), S.ncig.data(), S.md_len.data()};
+        pf_k4_reads_dev dv{d_start, d_end, d_co, d_cig, d_so, d_len, d_seq, d_mo, d_md};
+        return pf_haptag_core(ctx, K, (uint32_t)N, h, nullptr, &dv, F->read_hp.data());
+    });
+    if (rc) { delete F; return rc; }
+    F->pub.read_hp = F->read_hp.data();
     *fetch_out = &F->pub;
     return PF_OK;
 }

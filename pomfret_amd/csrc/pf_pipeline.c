@@ -627,7 +627,23 @@ int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
     pf_tags_t *seen = NULL;
     int rc = pf_vcf_known_vars(p->vcf_path, contig, &kt);
     if (!rc && kt->vars.n) rc = pf_bam_open(p->bam_path, NULL, &bam);
-    if (!rc && kt->vars.n) rc = pf_bam_fetch_contig_reads(bam, contig, &rd);
+    if (!rc && kt->vars.n && !p->o.host_fetch) {
+        /* device fetch + K4 on the device (pf_haptag_bam) */
+        pf_bam_dev_fetch_t *F = NULL;
+        rc = pf_haptag_bam(ctx, &kt->vars, bam, contig, &F);
+        if (!rc && F->n_recs) {
+            seen = pf_tags_new();
+            if (!seen) rc = PF_ERR_NOMEM;
+            for (uint64_t r = 0; r < F->n_recs && !rc; r++) {
+                const char *nm = F->qname + F->qname_off[r];
+                const size_t l = (size_t)(F->qname_off[r + 1] - F->qname_off[r]);
+                const int ins = tags_put(seen, nm, l, F->read_hp[r]);
+                if (ins < 0) rc = ins;
+                else if (ins) rc = ent_push(&e, nm, l, F->read_hp[r]);
+            }
+        }
+        pf_bam_dev_fetch_free(F);
+    } else if (!rc && kt->vars.n) rc = pf_bam_fetch_contig_reads(bam, contig, &rd);
     if (!rc && rd && rd->reads.n_reads) {
         hp = (uint8_t *)malloc(rd->reads.n_reads);
         seen = pf_tags_new();

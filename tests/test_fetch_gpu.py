@@ -157,3 +157,38 @@ def test_pipeline_device_vs_host_fetch(gpu_ctx, tmp_path, mode):
         assert rd["qname_hp"] == rh["qname_hp"]
     for e in exts:
         assert open(pd + e, "rb").read() == open(ph + e, "rb").read(), e
+
+
+def test_haptag_bam_vs_host(gpu_ctx, tmp_path):
+    """-u pre-pass through the device fetch (pf_haptag_bam) against the host
+    reader + K4 (pf_bam_fetch_contig_reads + pf_haptag_reads): the same reads
+    (qnames, BAM order, secondary/unmapped skipped) and tags."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_bam import _u_bam
+    from pomfret_amd.bam import BamFile, vcf_known_vars
+    from pomfret_amd.synth_u import USpec
+    known, reads, order, bam, vcf = _u_bam(tmp_path, USpec(n_reads=600, ref_len=400_000))
+    kv = vcf_known_vars(vcf, "chrU")
+    with BamFile(bam) as b:
+        got, qn, _ = b.fetch_contig_reads("chrU")
+        hp_d, qn_d, info = b.haptag_device(gpu_ctx, "chrU", kv)
+    assert qn_d == qn
+    assert np.array_equal(hp_d, gpu_ctx.haptag_reads(kv, got))
+
+
+@pytest.mark.parametrize("cov", [60])
+def test_untagged_pipeline_device_prepass(gpu_ctx, tmp_path, cov):
+    """The driver's -u run with the device pre-pass and device fetch equals the
+    host-fetch run (decisions, the raw -u table, outputs)."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import methphase_files
+    from tests._fixtures import untagged
+    aln, recs, bam, vcf = untagged(tmp_path, n_windows=2, coverage=cov, seed=5)
+    cfg = Config.from_coverage(cov, given=False)
+    r = {hf: methphase_files(bam, vcf, str(tmp_path / f"u{int(hf)}"), cfg, ctx=gpu_ctx, untagged=True, host_fetch=hf)
+         for hf in (False, True)}
+    assert np.array_equal(r[False]["decision"], r[True]["decision"])
+    assert r[False]["raw_hp"] == r[True]["raw_hp"]
+    assert r[False]["qname_hp"] == r[True]["qname_hp"]
