@@ -17,8 +17,11 @@ pytestmark = pytest.mark.gpu
 def _compare(host, hqn, hinfo, db, dqn, dinfo):
     assert np.array_equal(dinfo["win_rec_off"], host.win_rec_off)
     d = db.debug_recs()
-    for k in ("flag", "mapq", "pos", "l_qseq", "hp", "cigar_off", "cigar", "mm_off", "mm", "ml_off", "ml"):
+    for k in ("flag", "mapq", "pos", "l_qseq", "hp", "cigar_off", "mm_off", "ml_off"):
         assert np.array_equal(d[k], getattr(host, k)), k
+    for k in ("cigar", "mm", "ml"):                    # the arrays' used parts (an empty batch keeps a pad element)
+        n = int(getattr(host, k + "_off")[-1])
+        assert np.array_equal(d[k], getattr(host, k)[:n]), k
     assert np.array_equal(d["de"].view(np.uint32), host.de.view(np.uint32))
     so = d["seq_off"]
     for i in range(host.n_recs):
@@ -192,3 +195,38 @@ def test_untagged_pipeline_device_prepass(gpu_ctx, tmp_path, cov):
     assert np.array_equal(r[False]["decision"], r[True]["decision"])
     assert r[False]["raw_hp"] == r[True]["raw_hp"]
     assert r[False]["qname_hp"] == r[True]["qname_hp"]
+
+
+def test_device_fetch_contigs_and_eof(gpu_ctx, tmp_path):
+    """Two contigs and unplaced reads at the end of the file: fetches that
+    stop at a record of the next tid, windows reaching past the last record of
+    a contig, the last contig's fetch running into the unplaced tail (tid -1)
+    and into EOF, and an empty contig -- device fetch against the host reader."""
+    from pomfret_amd import Config, LoadConfig
+    from pomfret_amd.bam import BamFile
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    a1 = make_aln_batch(AlnSpec(n_windows=2, coverage=20, seed=41, len_scale=0.3), workers=1)
+    a2 = make_aln_batch(AlnSpec(n_windows=2, coverage=20, seed=42, len_scale=0.3), workers=1)
+    r1 = _bamio.records_from_aln(a1, tid=0, prefix="a")
+    r2 = _bamio.records_from_aln(a2, tid=2, prefix="b")
+    un = _bamio.records_from_aln(a2, tid=-1, prefix="u")[:25]
+    for r in un:                                         # unplaced: no position, unmapped
+        r.pos, r.flag, r.cigar = -1, 4, []
+    bam = str(tmp_path / "multi.bam")
+    _bamio.write_bam(bam, [("c1", 200_000_000), ("c_empty", 1_000_000), ("c3", 200_000_000)], r1 + r2 + un)
+    cfg, lcfg = Config.from_coverage(20, given=False), LoadConfig()
+    ends1 = int(max(r.pos for r in r1)) + 200_000
+    cases = [("c1", np.concatenate([a1.win_start, [ends1, 0]]), np.concatenate([a1.win_end, [ends1 + 10, 5_000_000]])),
+             ("c3", np.concatenate([a2.win_start, [int(max(r.pos for r in r2)) + 30_000]]),
+              np.concatenate([a2.win_end, [199_000_000]])),
+             ("c_empty", np.array([1000], np.uint32), np.array([2000], np.uint32))]
+    for chrom, ws, we in cases:
+        ws = np.asarray(ws, np.uint32)
+        we = np.asarray(we, np.uint32)
+        with BamFile(bam) as b:
+            host, hqn, hinfo = b.fetch_windows(chrom, ws, we, threads=2)
+            db, dqn, dinfo = b.fetch_windows_device(gpu_ctx, cfg, chrom, ws, we, lcfg)
+        _compare(host, hqn, hinfo, db, dqn, dinfo)
+        if host.n_recs:
+            assert np.array_equal(db.run().decision, gpu_ctx.upload_aln(cfg, host, lcfg).run().decision)
+        db.free()
