@@ -237,42 +237,14 @@ static void par_for(uint64_t n, F f) {
     for (auto &x : th) x.join();
 }
 
-// large host -> device copies go through the context's pinned buffer
-// (parallel memcpy in, one DMA out) in 256 MiB pieces
-static int pinned_put(pf_ctx *c, void *dst, const void *src, size_t bytes) {
-    const size_t piece = (size_t)256 << 20;
-    if (bytes < ((size_t)4 << 20)) {
-        HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-        return PF_OK;
-    }
-    const size_t want = std::min(bytes, piece);
-    if (c->pin_cap < want) {
-        if (c->pin) (void)hipHostFree(c->pin);
-        c->pin = nullptr;
-        c->pin_cap = 0;
-        if (hipHostMalloc(&c->pin, want, hipHostMallocDefault) != hipSuccess) {
-            c->pin = nullptr;
-            HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
-            return PF_OK;
-        }
-        c->pin_cap = want;
-    }
-    for (size_t o = 0; o < bytes; o += c->pin_cap) {
-        const size_t k = std::min(c->pin_cap, bytes - o);
-        uint8_t *pin = (uint8_t *)c->pin;
-        const uint8_t *s8 = (const uint8_t *)src + o;
-        par_for(k, [&](uint64_t lo, uint64_t hi) { memcpy(pin + lo, s8 + lo, hi - lo); });
-        HIPCHK(hipMemcpy((uint8_t *)dst + o, pin, k, hipMemcpyHostToDevice));
-    }
-    return PF_OK;
-}
-
-// like pinned_put, but the pieces are produced by fill(buf, lo, hi) in the
-// pinned buffer itself
+// large host -> device copies go through the context's pinned buffer, two
+// 256 MiB halves: fill(buf, lo, hi) writes piece k into one half (parallel
+// memcpy or the SEQ repack) while the previous piece's DMA runs from the
+// other half (async on the context's stream, one event per half)
 template <typename F>
-static int pinned_fill(pf_ctx *c, void *dst, size_t bytes, F fill) {
-    const size_t piece = (size_t)256 << 20;
-    const size_t want = std::max<size_t>(std::min(bytes, piece), 1);
+static int pinned_stream(pf_ctx *c, void *dst, size_t bytes, F fill) {
+    const size_t half = (size_t)256 << 20;
+    const size_t want = 2 * half;
     if (c->pin_cap < want) {
         if (c->pin) (void)hipHostFree(c->pin);
         c->pin = nullptr;
@@ -280,12 +252,40 @@ static int pinned_fill(pf_ctx *c, void *dst, size_t bytes, F fill) {
         if (hipHostMalloc(&c->pin, want, hipHostMallocDefault) != hipSuccess) { c->pin = nullptr; return PF_ERR_NOMEM; }
         c->pin_cap = want;
     }
-    for (size_t o = 0; o < bytes; o += c->pin_cap) {
-        const size_t k = std::min(c->pin_cap, bytes - o);
-        fill((uint8_t *)c->pin, (uint64_t)o, (uint64_t)(o + k));
-        HIPCHK(hipMemcpy((uint8_t *)dst + o, c->pin, k, hipMemcpyHostToDevice));
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int rc = PF_OK;
+    for (int i = 0; i < 2 && !rc; i++)
+        if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) rc = PF_ERR_HIP;
+    bool used[2] = {false, false};
+    for (size_t o = 0, k = 0; o < bytes && !rc; o += half, k++) {
+        const int h = (int)(k & 1);
+        uint8_t *buf = (uint8_t *)c->pin + h * half;
+        if (used[h] && hipEventSynchronize(ev[h]) != hipSuccess) { rc = PF_ERR_HIP; break; }
+        const size_t n = std::min(half, bytes - o);
+        fill(buf, (uint64_t)o, (uint64_t)(o + n));
+        if (hipMemcpyAsync((uint8_t *)dst + o, buf, n, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipEventRecord(ev[h], c->stream) != hipSuccess) { rc = PF_ERR_HIP; break; }
+        used[h] = true;
     }
-    return PF_OK;
+    if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) rc = PF_ERR_HIP;
+    for (auto e : ev) if (e) (void)hipEventDestroy(e);
+    return rc;
+}
+
+static int pinned_put(pf_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (bytes < ((size_t)4 << 20)) {
+        HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+        return PF_OK;
+    }
+    const uint8_t *s8 = (const uint8_t *)src;
+    return pinned_stream(c, dst, bytes, [&](uint8_t *buf, uint64_t lo, uint64_t hi) {
+        par_for(hi - lo, [&](uint64_t a, uint64_t b) { memcpy(buf + a, s8 + lo + a, b - a); });
+    });
+}
+
+template <typename F>
+static int pinned_fill(pf_ctx *c, void *dst, size_t bytes, F fill) {
+    return pinned_stream(c, dst, bytes, fill);
 }
 
 static void free_arena(pf_dbatch *b, void *p) {
