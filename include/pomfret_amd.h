@@ -407,6 +407,9 @@ int32_t pf_bam_tid(const pf_bam_t *bam, const char *name);   /* -1 when absent *
  * (hts_idx_get_stat); PF_ERR_ARG when tid has none. */
 int  pf_bam_index_stats(const pf_bam_t *bam, int32_t tid, uint64_t *n_mapped, uint64_t *n_unmapped);
 const char *pf_bam_path(const pf_bam_t *bam);
+/* The index's count of unplaced records (the optional n_no_coor after the
+ * references); -1 when the index does not have one. */
+int64_t pf_bam_n_no_coor(const pf_bam_t *bam);
 /* The BAI chunks [u, v) (virtual offsets) of region [beg, end) of tid, sorted
  * by u, as hts_itr_query collects them (bins overlapping the region, chunks
  * ending before the linear-index offset dropped).  Writes min(n, cap) pairs
@@ -498,6 +501,13 @@ void pf_bam_reads_free(pf_bam_reads_t *reads);
  * (estimate_read_coverage_dirtyfast, 951-1040): covs[tid] for
  * tid < pf_bam_n_targets (n >= that).  A full sequential pass over the BAM. */
 int  pf_bam_estimate_coverage(pf_bam_t *bam, int32_t *covs, int32_t n);
+/* The same estimate with the BAM's records inflated, chained and decoded on
+ * ctx's device (the device fetch, pieces of <= piece_bytes compressed bytes
+ * per call; 0 = 4 GiB), contig by contig through the index; identical covs
+ * for a coordinate-sorted, indexed BAM (the only kind the pipeline opens).
+ * Falls back to pf_bam_estimate_coverage when the index has no unplaced-read
+ * count (the last contig's estimate depends on it). */
+int  pf_bam_estimate_coverage_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_t *covs, int32_t n, uint64_t piece_bytes);
 
 /* qname -> tag table across the boundary (first entry of a qname wins). */
 typedef struct pf_qname_tags {

@@ -88,6 +88,9 @@ def _bind():
                                     C.POINTER(C.POINTER(PfRescueMap))]
     L.pf_rescue_map_free.argtypes = [C.POINTER(PfRescueMap)]
     L.pf_bam_estimate_coverage.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    L.pf_bam_estimate_coverage_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64]
+    L.pf_bam_n_no_coor.argtypes = [C.c_void_p]
+    L.pf_bam_n_no_coor.restype = C.c_int64
     L.pf_bam_query_chunks.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_uint64]
     L.pf_bam_query_chunks.restype = C.c_int64
     L.pf_batch_upload_bam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_char_p, C.c_uint32,
@@ -268,6 +271,21 @@ class BamFile:
         cov = np.zeros(max(self.n_targets, 1), np.int32)
         _check(L.pf_bam_estimate_coverage(self.handle, cov.ctypes.data, cov.size), "pf_bam_estimate_coverage")
         return cov[:self.n_targets].tolist()
+
+    def estimate_coverage_device(self, ctx, piece_bytes: int = 0) -> List[int]:
+        """The same estimate with the pass over the BAM on ctx's device
+        (pf_bam_estimate_coverage_dev); piece_bytes bounds the compressed bytes
+        of one fetch (0: 4 GiB)."""
+        L = _bind()
+        cov = np.zeros(max(self.n_targets, 1), np.int32)
+        _check(L.pf_bam_estimate_coverage_dev(ctx.handle, self.handle, cov.ctypes.data, cov.size, piece_bytes),
+               "pf_bam_estimate_coverage_dev")
+        return cov[:self.n_targets].tolist()
+
+    @property
+    def n_unplaced(self) -> int:
+        """The index's count of unplaced records (-1: not recorded)."""
+        return int(_bind().pf_bam_n_no_coor(self.handle))
 
     def fetch_contig_reads(self, chrom: str) -> Tuple[ReadAlnBatch, List[str], dict]:
         """The -u pre-pass reads of one contig (pf_bam_fetch_contig_reads):

@@ -191,6 +191,7 @@ struct pf_bam {
     uint64_t data_off;           /* virtual offset of the first record */
     int32_t n_ref_idx;
     ref_idx_t *idx;
+    int64_t n_no_coor;           /* the index's count of unplaced records; -1 when it has none */
 };
 
 static int cmp_bin(const void *a, const void *b) {
@@ -275,6 +276,7 @@ static int load_bai(pf_bam_t *b, const char *path) {
         for (uint32_t i = 0; i < ni; i++) ri->intv[i] = rd64(d + o + 8ull * i);
         o += 8ull * ni;
     }
+    b->n_no_coor = o + 8 <= n ? (int64_t)(rd64(d + o) & 0x7FFFFFFFFFFFFFFFull) : -1;
     rc = PF_OK;
 out:
     free(d);
@@ -371,6 +373,7 @@ void pf_bam_close(pf_bam_t *b) {
 }
 
 const char *pf_bam_path(const pf_bam_t *b) { return b ? b->path : NULL; }
+int64_t pf_bam_n_no_coor(const pf_bam_t *b) { return b ? b->n_no_coor : -1; }
 
 int32_t pf_bam_n_targets(const pf_bam_t *b) { return b ? (b->path ? b->n_ref : b->n_ref_idx) : 0; }
 const char *pf_bam_target_name(const pf_bam_t *b, int32_t tid) {

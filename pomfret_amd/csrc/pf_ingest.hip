@@ -809,3 +809,68 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
     *fetch_out = &F->pub;
     return PF_OK;
 }
+
+// estimate_read_coverage_dirtyfast (blockjoin.c:951-1040) through the device
+// fetch: the serial pass's records are, for a coordinate-sorted BAM, each
+// contig's records in index order followed by the unplaced tail, so the pass
+// is restated per contig -- whole-contig fetches (split into position pieces
+// of bounded compressed size; a record counts in the piece its start falls
+// in), the filters and 5 kb bins on the host from the gathered small fields.
+// Its sequential quirks carry over: a truncated record ends the whole pass
+// (its contig keeps the bins counted so far, later contigs 0), and unplaced
+// reads at the end leave the last contig with reads at 0 (refID -1 when the
+// loop ends).  Contigs without records stay 0.
+extern "C" int pf_bam_estimate_coverage_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_t *covs, int32_t n,
+                                            uint64_t piece_bytes) {
+    if (!ctx || !bam || !covs) return PF_ERR_ARG;
+    const int32_t nr = pf_bam_n_targets(bam);
+    if (n < nr) return PF_ERR_ARG;
+    const int64_t n_unplaced = pf_bam_n_no_coor(bam);
+    if (n_unplaced < 0) return pf_bam_estimate_coverage(bam, covs, n);
+    if (!piece_bytes) piece_bytes = 4ull << 30;
+    for (int32_t i = 0; i < n; i++) covs[i] = 0;
+    constexpr uint32_t MOD = 5000;
+    int32_t last = -1;
+    bool stopped = false;
+    std::vector<uint64_t> bins, uv;
+    for (int32_t t = 0; t < nr && !stopped; t++) {
+        const int64_t nc = pf_bam_query_chunks(bam, t, 0, INT64_MAX, nullptr, 0);
+        if (nc < 0) return (int)nc;
+        if (nc == 0) continue;
+        uv.resize(2 * (size_t)nc);
+        if (pf_bam_query_chunks(bam, t, 0, INT64_MAX, uv.data(), (uint64_t)nc) != nc) return PF_ERR_INTERNAL;
+        uint64_t c0 = UINT64_MAX, c1 = 0;
+        for (int64_t c = 0; c < nc; c++) { c0 = std::min(c0, uv[2 * c] >> 16); c1 = std::max(c1, uv[2 * c + 1] >> 16); }
+        last = t;
+        const uint32_t len = pf_bam_target_len(bam, t);
+        const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>(len ? len : 1, (c1 - c0 + piece_bytes - 1) / piece_bytes));
+        const int64_t step = (int64_t)((len + K - 1) / K);
+        bins.assign(len / MOD, 0);
+        for (uint64_t k = 0; k < K && !stopped; k++) {
+            const int64_t beg = (int64_t)k * step, end = k + 1 == K ? INT64_MAX : (int64_t)(k + 1) * step;
+            pf_bam_dev_fetch_own F;
+            const int rc = dev_fetch(ctx, bam, t, 1, &beg, &end, 0u, 0u, &F, [&](FetchOut &fo) -> int {
+                const Small &S = *fo.S;
+                for (uint64_t i = 0; i < fo.n; i++) {
+                    const int32_t pos = (int32_t)S.pos[i];
+                    if (k && pos < beg) continue;                   // counted in an earlier piece
+                    if ((S.flag[i] & (4u | 256u | 2048u)) || S.mapq[i] < 5 || S.l_qseq[i] < 15000) continue;
+                    if ((double)S.de[i] > 0.1) continue;
+                    const uint32_t st = (uint32_t)pos, en = (uint32_t)(pos + (int32_t)S.rlen[i]);   // bam_endpos
+                    for (int64_t x = (int32_t)st; x < (int64_t)en; x += MOD) {
+                        const uint64_t b = (uint64_t)x / MOD;
+                        if (x >= 0 && b < bins.size()) bins[b]++;
+                    }
+                }
+                return PF_OK;
+            });
+            if (rc) return rc;
+            if (F.win_status[0] == PF_WIN_TRUNC) stopped = true;
+        }
+        uint64_t tot = 0;
+        for (uint64_t b : bins) tot += b;
+        covs[t] = bins.empty() ? 0 : (int32_t)(tot / bins.size());
+    }
+    if (!stopped && n_unplaced > 0 && last >= 0) covs[last] = 0;
+    return PF_OK;
+}

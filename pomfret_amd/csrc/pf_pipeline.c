@@ -7,7 +7,8 @@
  *     load_intervals_from_file + merge_close_intervals      -> pf_vcf_gaps
  *     (-u) pre_haplotagging_read_in_one_ref per contig (1841-1898),
  *          qname first-wins per contig, merged in contig order     -> K4 jobs
- *     estimate_read_coverage_dirtyfast when -c is absent (4547)     -> pf_bam_estimate_coverage
+ *     estimate_read_coverage_dirtyfast when -c is absent (4547)     -> pf_bam_estimate_coverage_dev
+ *                                                   (pf_bam_estimate_coverage with --host-fetch / no device)
  *     kt_for(blockjoin_one_chrom_callback) over contigs (4560):
  *       per-contig parameters and clamps (4357-4390), one
  *       haplotag_region_given_bam per merged gap, and for a joined gap
@@ -325,7 +326,17 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     if (need_est) {
         covs = (int32_t *)calloc(nt > 0 ? nt : 1, sizeof(int32_t));
         if (!covs) rc = PF_ERR_NOMEM;
-        if (!rc) rc = pf_bam_estimate_coverage(bam, covs, nt > 0 ? nt : 1);
+        if (!rc && !o->host_fetch && (o->n_ctxs > 0 || pf_device_count() > 0)) {
+            /* the pass over the whole BAM on the device (the first context or
+             * device of the run); runs without a device scan on the host */
+            pf_ctx_t *ec = o->n_ctxs > 0 ? o->ctxs[0] : NULL;
+            int own = 0;
+            if (!ec) { rc = pf_ctx_create(o->devices ? o->devices[0] : 0, &ec); own = !rc; }
+            if (!rc) rc = pf_bam_estimate_coverage_dev(ec, bam, covs, nt > 0 ? nt : 1, 0);
+            if (own) pf_ctx_destroy(ec);
+        } else if (!rc) {
+            rc = pf_bam_estimate_coverage(bam, covs, nt > 0 ? nt : 1);
+        }
     }
     /* windows: merged gaps (methphase) or report chunks of the raw gaps */
     uint64_t nw = 0, cap = 0;

@@ -484,6 +484,7 @@ def test_estimate_coverage(tmp_path):
     write_bam(p1, [("a", lens[0]), ("b", lens[1]), ("c", lens[2])], seqfix)
     with BamFile(p1) as b:
         got = b.estimate_coverage()
+        assert b.n_unplaced == 0
     assert got == _py_cov(seqfix, lens) and got[0] > 0
     # an unplaced read at the end reassigns refID: the last contig keeps 0
     un = Rec(-1, -1, "unplaced", flag=4, cigar=[], seq=bytes(50), l_seq=100)
@@ -491,4 +492,5 @@ def test_estimate_coverage(tmp_path):
     write_bam(p2, [("a", lens[0]), ("b", lens[1]), ("c", lens[2])], seqfix + [un])
     with BamFile(p2) as b:
         got2 = b.estimate_coverage()
+        assert b.n_unplaced == 1
     assert got2[:2] == got[:2] and got[2] > 0 and got2[2] == 0

@@ -230,3 +230,51 @@ def test_device_fetch_contigs_and_eof(gpu_ctx, tmp_path):
         if host.n_recs:
             assert np.array_equal(db.run().decision, gpu_ctx.upload_aln(cfg, host, lcfg).run().decision)
         db.free()
+
+
+def _cov_records(rng, lens, n_per, trunc_at=None):
+    from tests._bamio import Rec, aux_f
+    recs = []
+    for tid, n in enumerate(n_per):
+        for _ in range(n):
+            L = int(rng.integers(5_000, 40_000))
+            p = int(rng.integers(0, max(1, lens[tid] - 1000)))
+            flag = int(rng.choice([0, 0, 0, 16, 256, 2048]))
+            aux = aux_f("de", float(rng.choice([0.01, 0.05, 0.2]))) if rng.random() < 0.7 else b""
+            recs.append(Rec(tid, p, f"t{tid}_{len(recs)}", flag=flag, mapq=int(rng.integers(0, 60)),
+                            cigar=[(L << 4) | 0], seq=rng.integers(0, 256, (L + 1) // 2, np.uint8).tobytes(),
+                            l_seq=L, aux=aux))
+    recs.sort(key=lambda r: (r.tid, r.pos))
+    if trunc_at is not None:                          # CIGAR and SEQ lengths differ: the pass stops there
+        r = recs[trunc_at]
+        r.flag = 0
+        r.cigar = [((r.l_seq - 7) << 4) | 0]
+    return recs
+
+
+@pytest.mark.parametrize("piece", [0, 256 << 10])
+def test_estimate_coverage_device(gpu_ctx, tmp_path, piece):
+    """pf_bam_estimate_coverage_dev against the serial host pass: plain,
+    an unplaced tail (the last contig keeps 0), an empty contig, a truncated
+    record mid-file (later contigs 0), and pieces of 256 KiB compressed (a
+    record counts in the piece its start falls in)."""
+    from tests._bamio import Rec
+    from pomfret_amd.bam import BamFile
+    rng = np.random.default_rng(21)
+    lens = [300_000, 1_000_000, 123_456, 60_000]
+    refs = [("a", lens[0]), ("empty", lens[1]), ("b", lens[2]), ("c", lens[3])]
+    base = _cov_records(rng, lens, [150, 0, 150, 60])
+    un = [Rec(-1, -1, f"u{i}", flag=4, cigar=[], seq=bytes(50), l_seq=100) for i in range(3)]
+    n_a = sum(r.tid == 0 for r in base)
+    cases = {"plain": base, "unplaced": base + un,
+             "trunc": _cov_records(np.random.default_rng(21), lens, [150, 0, 150, 60], trunc_at=n_a + 40) + un}
+    for name, recs in cases.items():
+        path = str(tmp_path / f"{name}.bam")
+        _bamio.write_bam(path, refs, recs)
+        with BamFile(path) as b:
+            host = b.estimate_coverage()
+            dev = b.estimate_coverage_device(gpu_ctx, piece)
+            assert b.n_unplaced == (3 if name != "plain" else 0)
+        assert dev == host, name
+        assert host[0] > 0 and host[1] == 0
+        assert (host[3] > 0) == (name == "plain")
