@@ -219,12 +219,12 @@ def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu:
             res["decisions_match"] = bool(np.array_equal(out.decision, dec_dev))
             # the pass over the whole BAM that runs without -c pay first
             # (estimate_read_coverage_dirtyfast): device fetch vs the serial host pass
-            t0 = time.perf_counter()
+            c0 = time.perf_counter()
             cov_d = b.estimate_coverage_device(ctx)
-            t1 = time.perf_counter()
+            c1 = time.perf_counter()
             cov_h = b.estimate_coverage()
-            t2 = time.perf_counter()
-            res["coverage_estimate"] = {"device_ms": round((t1 - t0) * 1e3, 1), "host_ms": round((t2 - t1) * 1e3, 1),
+            c2 = time.perf_counter()
+            res["coverage_estimate"] = {"device_ms": round((c1 - c0) * 1e3, 1), "host_ms": round((c2 - c1) * 1e3, 1),
                                         "match": cov_d == cov_h, "cov": int(cov_d[0])}
             if cpu:
                 import oracle
