@@ -1036,6 +1036,7 @@ extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_
         if (b->W) {
             for (int i = 0; i < PF_NKERN; i++)
                 (void)hipEventElapsedTime(&c->last_ms[i], b->ev[slot][i], b->ev[slot][i + 1]);
+            (void)hipGetLastError();               // a failed timing query must not fail a later launch check
             c->have_times = 1;
         }
         const uint32_t stt = b->W ? v.status[0] : 0;

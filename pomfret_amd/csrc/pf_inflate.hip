@@ -17,19 +17,22 @@
 //  * the compressed input is held lane-distributed: lane k of `cur` holds
 //    dword k of the current 256-byte input window, `nxt` the next one,
 //    prefetched one window ahead; the bit reader takes dwords with readlane;
-//  * Huffman tables in LDS (per wave, ~3.9 KB): a 10-bit root table for
+//  * Huffman tables in LDS (per wave, ~4 KB): a 10-bit root table for
 //    literal/length codes and an 8-bit one for distances (symbol | length << 9,
-//    broadcast reads); codes longer than the root (rare) take a canonical
-//    walk over the per-length counts;
+//    broadcast reads); a code longer than the root (rare) is found by all
+//    code lengths tested at once, one per lane (the canonical walk's answer);
+//    literal-pair root entries were tried and measured slower (few pairs fit
+//    10 bits on BAM content, and the larger table costs a wave of occupancy);
+//  * measured by SQ counters (tools/ubench/inflate_ab, BAM-like blocks): per
+//    output byte ~35 SALU + ~25 VALU instructions and ~0.9 LDS reads, scalar
+//    issue at ~2/3 of one SALU per CU-cycle;
 //  * output is assembled lane-distributed in 256-byte chunks aligned to the
 //    arena (lane k holds bytes 4k..4k+3 of the chunk) and flushed with one
 //    coalesced store per chunk; a match only records its bytes' sources, and
 //    the chunk's flush loads every source in older output at once (after a
 //    workgroup-scope fence that makes the flushed chunks visible) and resolves
 //    in-chunk sources with ds_bpermute rounds;
-//  * measured (tests/test_inflate_gpu.py, BAM-like blocks): the decode is
-//    bound by scalar issue (one SALU instruction per 4 cycles per SIMD, ~45
-//    per symbol), about 12 GB/s of output on MI355X;
+//    11.5-13.6 GB/s of output on MI355X (8k-32k blocks);
 //  * table construction is lane-parallel (counts by ballot, ranks by ballot
 //    prefix, root fill one symbol per lane).
 // Each block's CRC32 (reflected 0xEDB88320, zlib's crc32) is folded in at
@@ -58,15 +61,20 @@ __constant__ uint8_t k_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12,
 
 struct InfLds {                         // one wave's tables
     uint16_t lroot[1u << INF_LROOT];
-    uint16_t droot[1u << INF_DROOT];
+    union {
+        uint16_t droot[1u << INF_DROOT];
+        struct {                        // the code-length code: done with before droot is built
+            uint16_t clroot[128];       // (max 7 bits: the root covers it)
+            uint16_t cnt_cl[16], off_cl[16], fst_cl[16];
+            uint16_t clsym[19];
+        } cl;
+    };
     uint16_t lsym[288];                 // symbols sorted by (length, value): canonical order
     uint16_t dsym[32];
     uint16_t cnt[2][16];                // codes per length (litlen, dist)
     uint16_t off[2][16];                // first sorted index of each length
+    uint16_t fst[2][16];                // first canonical code of each length
     uint8_t lens[320];                  // code lengths: HLIT litlen then HDIST dist
-    uint16_t clroot[128];               // code-length code (max 7 bits: the root covers it)
-    uint16_t cnt_cl[16], off_cl[16];
-    uint16_t clsym[19];
     uint32_t ring[128];                 // input windows (bit reader)
 };
 
@@ -123,8 +131,9 @@ DEV uint32_t bits_get(Bits &b, uint32_t n) {       // n <= 32, after a fill cove
 // success, 1 for an over-subscribed set or an incomplete one (zlib's
 // inflate_table: incomplete only for a single length-1 code, never for the
 // code-length code; an empty set builds a table every lookup of which fails).
-DEV uint32_t build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint16_t *rt, uint16_t *sym,
-                         uint16_t *cnt, uint16_t *off, uint32_t lane, bool is_codes) {
+template <typename E>
+DEV uint32_t build_table(const uint8_t *lens, uint32_t n, uint32_t root, E *rt, uint16_t *sym,
+                         uint16_t *cnt, uint16_t *off, uint16_t *fst, uint32_t lane, bool is_codes) {
     // counts per length (uniform, 15 ballots per 64 symbols)
     uint32_t c[16];
 #pragma unroll
@@ -158,11 +167,11 @@ DEV uint32_t build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint16_
         first[L] = code;
         if (L > 1) o[L] = o[L - 1] + c[L - 1];
     }
-    if (lane < 16) { cnt[lane] = 0; off[lane] = 0; }
+    if (lane < 16) { cnt[lane] = 0; off[lane] = 0; fst[lane] = 0; }
     wsync();
 #pragma unroll
     for (uint32_t L = 1; L < 16; L++)
-        if (lane == L) { cnt[lane] = (uint16_t)c[L]; off[lane] = (uint16_t)o[L]; }
+        if (lane == L) { cnt[lane] = (uint16_t)c[L]; off[lane] = (uint16_t)o[L]; fst[lane] = (uint16_t)first[L]; }
     // clear the root table
     const uint32_t rn = 1u << root;
     for (uint32_t i = lane; i < rn; i += 64) rt[i] = 0;
@@ -187,7 +196,7 @@ DEV uint32_t build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint16_
             if (l <= root) {
                 const uint32_t cd = fc + rank;
                 const uint32_t rev = __builtin_bitreverse32(cd) >> (32 - l);
-                const uint16_t e = (uint16_t)(s | (l << 9));
+                const E e = (E)(s | (l << 9));
                 for (uint32_t k = 0; k < (1u << (root - l)); k++) rt[rev | (k << l)] = e;
             }
         }
@@ -196,24 +205,20 @@ DEV uint32_t build_table(const uint8_t *lens, uint32_t n, uint32_t root, uint16_
     return 0;
 }
 
-// canonical decode of a code longer than the root (or any code, from bit 0)
-DEV uint32_t slow_decode(uint64_t bits, const uint16_t *cnt, const uint16_t *off, const uint16_t *sym,
-                         uint32_t &len_out) {
-    uint32_t code = 0, first = 0, index = 0;
-    for (uint32_t L = 1; L < 16; L++) {
-        code |= (uint32_t)(bits >> (L - 1)) & 1u;
-        const uint32_t c = cnt[L];
-        if (code - first < c) {
-            len_out = L;
-            return sym[index + code - first];
-        }
-        index += c;
-        first += c;
-        first <<= 1;
-        code <<= 1;
-    }
-    len_out = 0;
-    return 0xFFFFu;
+// canonical decode of a code longer than the root (or any code, from bit 0):
+// lane L tests whether the next L bits, read as a code, fall in length L's
+// range [fst[L], fst[L] + cnt[L]); the shortest such length is the code's
+// (the serial canonical walk's answer, all lengths at once)
+DEV uint32_t slow_decode(uint64_t bits, const uint16_t *cnt, const uint16_t *off, const uint16_t *fst,
+                         const uint16_t *sym, uint32_t lane, uint32_t &len_out) {
+    const uint32_t L = lane & 15u;
+    const uint32_t c = cnt[L], f = fst[L], o = off[L];
+    const uint32_t code = L ? __builtin_bitreverse32((uint32_t)bits) >> (32 - L) : 0u;
+    const uint64_t m = __ballot(lane >= 1 && lane < 16 && code - f < c);
+    if (!m) { len_out = 0; return 0xFFFFu; }
+    const uint32_t Ls = (uint32_t)__builtin_ctzll(m);
+    len_out = Ls;
+    return sym[rdl(o + code - f, Ls)];
 }
 
 // --------------------------------------------------------------------------
@@ -457,7 +462,7 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
                 T.lens[lane] = (uint8_t)l;
             }
             wsync();
-            if (build_table(T.lens, 19, 7, T.clroot, T.clsym, T.cnt_cl, T.off_cl, lane, true)) {
+            if (build_table(T.lens, 19, 7, T.cl.clroot, T.cl.clsym, T.cl.cnt_cl, T.cl.off_cl, T.cl.fst_cl, lane, true)) {
                 err = PF_INF_ECODES;
                 break;
             }
@@ -469,7 +474,7 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
             wsync();
             while (i < total) {
                 bits_fill(b, lane);
-                const uint32_t e = uni(T.clroot[(uint32_t)b.buf & 127u]);
+                const uint32_t e = uni(T.cl.clroot[(uint32_t)b.buf & 127u]);   // (no pairs in this table)
                 const uint32_t l = e >> 9, s = e & 511u;
                 if (l == 0) { err = PF_INF_ECODES; break; }
                 bits_get(b, l);
@@ -499,8 +504,8 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
             wsync();
             if (T.lens[256] == 0) { err = PF_INF_ECODES; break; }   // no end-of-block code
         }
-        if (build_table(T.lens, nlit, INF_LROOT, T.lroot, T.lsym, T.cnt[0], T.off[0], lane, false) ||
-            build_table(T.lens + 288, ndist, INF_DROOT, T.droot, T.dsym, T.cnt[1], T.off[1], lane, false)) {
+        if (build_table(T.lens, nlit, INF_LROOT, T.lroot, T.lsym, T.cnt[0], T.off[0], T.fst[0], lane, false) ||
+            build_table(T.lens + 288, ndist, INF_DROOT, T.droot, T.dsym, T.cnt[1], T.off[1], T.fst[1], lane, false)) {
             err = PF_INF_ECODES;
             break;
         }
@@ -510,7 +515,7 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
             uint32_t e = uni(T.lroot[(uint32_t)b.buf & ((1u << INF_LROOT) - 1u)]);
             uint32_t l = e >> 9, s = e & 511u;
             if (l == 0) {
-                s = slow_decode(b.buf, T.cnt[0], T.off[0], T.lsym, l);
+                s = slow_decode(b.buf, T.cnt[0], T.off[0], T.fst[0], T.lsym, lane, l);
                 s = uni(s);
                 l = uni(l);
                 if (l == 0) { err = PF_INF_ECODES; break; }
@@ -534,7 +539,7 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
             l = e >> 9;
             s = e & 511u;
             if (l == 0) {
-                s = slow_decode(b.buf, T.cnt[1], T.off[1], T.dsym, l);
+                s = slow_decode(b.buf, T.cnt[1], T.off[1], T.fst[1], T.dsym, lane, l);
                 s = uni(s);
                 l = uni(l);
                 if (l == 0) { err = PF_INF_ECODES; break; }

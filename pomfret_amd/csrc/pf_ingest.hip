@@ -61,8 +61,8 @@ int64_t pf_bgzf_scan(const uint8_t *comp, uint64_t len, uint64_t out_base, uint3
 // status copied back; returns PF_OK or PF_ERR_ARG naming the first bad block.
 int pf_inflate_launch(hipStream_t st, const uint8_t *d_in, const pf_bgzf_blk *d_blk, uint32_t nblk, uint8_t *d_arena,
                       uint32_t *d_status, hipEvent_t e0, hipEvent_t e1) {
-    if (!nblk) return PF_OK;
     if (e0 && hipEventRecord(e0, st) != hipSuccess) return PF_ERR_HIP;
+    if (!nblk) return e1 && hipEventRecord(e1, st) != hipSuccess ? PF_ERR_HIP : PF_OK;   // (the pair stays timeable)
     hipLaunchKernelGGL(pf_inflate, dim3((nblk + 3) / 4), dim3(256), 0, st, d_in, d_blk, nblk, d_arena, d_status);
     if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
     if (e1 && hipEventRecord(e1, st) != hipSuccess) return PF_ERR_HIP;
@@ -294,6 +294,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
     hipStream_t st = pf_ctx_stream((const pf_ctx *)ctx);
     if (hipSetDevice(pf_ctx_device((const pf_ctx *)ctx)) != hipSuccess) { close(fd); return PF_ERR_HIP; }
     memset(&F->pub, 0, sizeof F->pub);
+    (void)hipGetLastError();             // launches below are checked with hipGetLastError: no stale error
     int rc = PF_OK;
     uint64_t ext = 4ull << 16;            // bytes read past a chunk's last block (records spanning blocks)
     for (int attempt = 0; attempt < 8; attempt++) {
@@ -678,6 +679,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             (void)hipEventElapsedTime(&ms_dec, ev[3], ev[4]);
             (void)hipEventElapsedTime(&ms_sel, ev[4], ev[5]);
             (void)hipEventElapsedTime(&ms_build, ev[6], ev[7]);
+            (void)hipGetLastError();
         }
         evdone();
         if (rc) break;
