@@ -251,14 +251,14 @@ DEV uint32_t x8n(uint64_t n, const uint32_t *x2n) {  // x^(8n) mod P; x2n[k] = x
     return p;
 }
 
-struct Out {
-    uint8_t *arena;
-    uint64_t lo, hi;      // the block's output range [lo, hi)
-    uint64_t cb;          // current chunk's arena address
-    uint64_t a;           // next output address
+struct Out {               // positions are 32-bit, relative to base (scalar registers are scarce)
+    uint8_t *base;        // the arena's 256-byte chunk holding the block's first byte
+    uint32_t lo, hi;      // the block's output range [lo, hi), lo < 256
+    uint32_t cb;          // current chunk
+    uint32_t a;           // next output position
     uint32_t val;         // per lane: resolved bytes
     uint32_t pend;        // per lane: bit i set while byte i waits for its source
-    uint32_t src[4];      // per lane: source offset (from lo) of pending byte i
+    uint32_t src[4];      // per lane: source position of pending byte i
     uint32_t any;         // uniform: the chunk has pending bytes
     uint32_t crc;         // uniform: raw CRC of the flushed chunks
     uint32_t ck;          // per lane: x^(8 * (252 - 4 lane)), its word's weight in a full chunk
@@ -294,9 +294,9 @@ DEV void out_flush(Out &o, uint32_t lane) {
         uint32_t add = 0, done = 0;
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++) {
-            const uint64_t s = o.lo + o.src[i];
+            const uint32_t s = o.src[i];
             if (((o.pend >> i) & 1u) && s < o.cb) {
-                add |= (uint32_t)o.arena[s] << (8 * i);
+                add |= (uint32_t)o.base[s] << (8 * i);
                 done |= 1u << i;
             }
         }
@@ -308,7 +308,7 @@ DEV void out_flush(Out &o, uint32_t lane) {
 #pragma unroll
             for (uint32_t i = 0; i < 4; i++) {
                 const bool pi = (o.pend >> i) & 1u;
-                const uint32_t t = pi ? (uint32_t)(o.lo + o.src[i] - o.cb) : 4 * lane + i;
+                const uint32_t t = pi ? o.src[i] - o.cb : 4 * lane + i;
                 const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((t >> 2) << 2), (int)v_all);
                 const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((t >> 2) << 2), (int)r_all);
                 if (pi && ((r >> (t & 3u)) & 1u)) {
@@ -320,15 +320,15 @@ DEV void out_flush(Out &o, uint32_t lane) {
             o.pend = np;
         }
     }
-    out_crc(o, lane, o.a >= o.cb + 256 ? 256u : (uint32_t)(o.a - o.cb));
-    const uint64_t addr = o.cb + 4ull * lane;
+    out_crc(o, lane, o.a >= o.cb + 256 ? 256u : o.a - o.cb);
+    const uint32_t addr = o.cb + 4 * lane;
     if (addr >= o.lo && addr + 4 <= o.hi && addr + 4 <= o.a) {
-        *reinterpret_cast<uint32_t *>(o.arena + addr) = o.val;
+        *reinterpret_cast<uint32_t *>(o.base + addr) = o.val;
     } else {
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++) {
-            const uint64_t q = addr + i;
-            if (q >= o.lo && q < o.hi && q < o.a) o.arena[q] = (uint8_t)(o.val >> (8 * i));
+            const uint32_t q = addr + i;
+            if (q >= o.lo && q < o.hi && q < o.a) o.base[q] = (uint8_t)(o.val >> (8 * i));
         }
     }
     o.cb += 256;
@@ -338,7 +338,7 @@ DEV void out_flush(Out &o, uint32_t lane) {
 }
 
 DEV void out_lit(Out &o, uint32_t v, uint32_t lane) {
-    const uint32_t rel = (uint32_t)(o.a - o.cb);
+    const uint32_t rel = o.a - o.cb;
     if (lane == (rel >> 2)) o.val |= v << (8 * (rel & 3u));
     o.a++;
     if (rel == 255) out_flush(o, lane);
@@ -346,16 +346,16 @@ DEV void out_lit(Out &o, uint32_t v, uint32_t lane) {
 
 // copy L bytes from distance D (D <= bytes already written, checked by the caller)
 DEV void out_match(Out &o, uint32_t L, uint32_t D, uint32_t lane) {
-    const uint64_t ms = o.a, me = o.a + L;
+    const uint32_t ms = o.a, me = o.a + L;
     while (o.a < me) {
-        const uint64_t seg_end = me < o.cb + 256 ? me : o.cb + 256;
+        const uint32_t seg_end = me < o.cb + 256 ? me : o.cb + 256;
         uint32_t setp = 0;
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++) {
-            const uint64_t q = o.cb + 4ull * lane + i;
+            const uint32_t q = o.cb + 4 * lane + i;
             if (q >= o.a && q < seg_end) {
-                const uint64_t s = D < L ? ms - D + (uint64_t)((uint32_t)(q - ms) % D) : q - D;
-                o.src[i] = (uint32_t)(s - o.lo);
+                const uint32_t s = D < L ? ms - D + (q - ms) % D : q - D;
+                o.src[i] = s;
                 setp |= 1u << i;
             }
         }
@@ -403,11 +403,11 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
     if ((in_off & 3u) != 0) bits_get(b, 8 * (uint32_t)(in_off & 3u));
 
     Out o;
-    o.arena = arena;
-    o.lo = B.out_off;
-    o.hi = B.out_off + isize;
-    o.cb = B.out_off & ~255ull;
-    o.a = B.out_off;
+    o.base = arena + (B.out_off & ~255ull);
+    o.lo = (uint32_t)(B.out_off & 255u);
+    o.hi = o.lo + isize;
+    o.cb = 0;
+    o.a = o.lo;
     o.val = 0;
     o.pend = 0;
     o.any = 0;
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
             const uint32_t dx = s < 4 ? 0u : (s - 2) >> 1;
             const uint32_t db = s < 4 ? 1 + s : ((2 + (s & 1u)) << dx) + 1;
             const uint32_t D = db + bits_get(b, dx);
-            if ((uint64_t)D > o.a - o.lo) { err = PF_INF_EDIST; break; }
+            if (D > o.a - o.lo) { err = PF_INF_EDIST; break; }
             if (o.a + L > o.hi) { err = PF_INF_ESIZE; break; }
             out_match(o, L, D, lane);
             if (b.over) { err = PF_INF_EINPUT; break; }

@@ -10,10 +10,14 @@
 #include <vector>
 #include "../../pomfret_amd/csrc/pf_ingest.h"
 
-namespace v0 {
+namespace v0 {                          // A: _inf_a.hip (a saved earlier version) when present
 #undef INF_AB
 #define INF_AB 0
+#if __has_include("_inf_a.hip")
+#include "_inf_a.hip"
+#else
 #include "../../pomfret_amd/csrc/pf_inflate.hip"
+#endif
 }
 namespace v1 {
 #undef INF_AB
