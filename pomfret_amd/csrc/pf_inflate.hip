@@ -47,6 +47,9 @@
 #define INF_LROOT 10u
 #define INF_DROOT 8u
 #define INF_WAVES 4u
+#ifndef INF_SPEC
+#define INF_SPEC 1                      // literal runs decoded from every bit offset at once
+#endif
 
 DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 DEV uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
@@ -350,13 +353,23 @@ DEV void out_match(Out &o, uint32_t L, uint32_t D, uint32_t lane) {
     while (o.a < me) {
         const uint32_t seg_end = me < o.cb + 256 ? me : o.cb + 256;
         uint32_t setp = 0;
+        if (D < L) {                                     // overlapping copy: the source repeats with period D
 #pragma unroll
-        for (uint32_t i = 0; i < 4; i++) {
-            const uint32_t q = o.cb + 4 * lane + i;
-            if (q >= o.a && q < seg_end) {
-                const uint32_t s = D < L ? ms - D + (q - ms) % D : q - D;
-                o.src[i] = s;
-                setp |= 1u << i;
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t q = o.cb + 4 * lane + i;
+                if (q >= o.a && q < seg_end) {
+                    o.src[i] = ms - D + (q - ms) % D;
+                    setp |= 1u << i;
+                }
+            }
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++) {
+                const uint32_t q = o.cb + 4 * lane + i;
+                if (q >= o.a && q < seg_end) {
+                    o.src[i] = q - D;
+                    setp |= 1u << i;
+                }
             }
         }
         o.pend |= setp;
@@ -512,6 +525,31 @@ __global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, 
         // ---- the block's symbols
         for (;;) {
             bits_fill(b, lane);
+#if INF_SPEC
+            // a run of literals: lane k looks up the root entry at bit offset
+            // k of the buffered bits (a literal whose code lies inside them
+            // is kept), then the run follows offsets 0, l0, l0 + l1, ... with
+            // one readlane per literal; the first symbol that is not such a
+            // literal goes to the general step below.  (Taking matches into
+            // the run as well measured slower: 14.1 vs 14.35 GB/s.)
+            {
+                const uint32_t ek = T.lroot[(uint32_t)(b.buf >> lane) & ((1u << INF_LROOT) - 1u)];
+                const uint32_t lk = ek >> 9, sk = ek & 511u;
+                const uint32_t lit = (lk != 0 && sk < 256 && lane + lk <= b.cnt) ? (sk | (lk << 8)) : 0u;
+                uint32_t off = 0;
+                while (off < 64) {
+                    const uint32_t x = rdl(lit, off);
+                    if (!x || o.a >= o.hi) break;        // (a full output is flagged by the general step)
+                    out_lit(o, x & 255u, lane);
+                    off += x >> 8;
+                }
+                if (off) {
+                    b.buf = off >= 64 ? 0ull : b.buf >> off;
+                    b.cnt -= off;
+                    bits_fill(b, lane);
+                }
+            }
+#endif
             uint32_t e = uni(T.lroot[(uint32_t)b.buf & ((1u << INF_LROOT) - 1u)]);
             uint32_t l = e >> 9, s = e & 511u;
             if (l == 0) {

@@ -1,6 +1,7 @@
 """Test data for inflate_ab: BGZF blocks of BAM-like content (4-bit SEQ +
 quality strings) written to argv[1]; two mixes: QUAL-heavy (one 10 kb read
-segment per block) and SEQ-heavy."""
+segment per block) and SEQ-heavy.  argv[2] = "huff": Huffman-only streams
+(no matches), to separate the literal path from the match path."""
 import sys
 import zlib
 import struct
@@ -8,7 +9,8 @@ import numpy as np
 
 
 def bgzf_block(data: bytes, level: int = 6) -> bytes:
-    c = zlib.compressobj(level, zlib.DEFLATED, -15)
+    strat = zlib.Z_HUFFMAN_ONLY if len(sys.argv) > 2 and sys.argv[2] == "huff" else zlib.Z_DEFAULT_STRATEGY
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strat)
     z = c.compress(data) + c.flush()
     bsize = 18 + len(z) + 8
     hdr = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize - 1)
