@@ -380,7 +380,10 @@ DEV void out_match(Out &o, uint32_t L, uint32_t D, uint32_t lane) {
 }
 
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk,
+#ifndef INF_WPE
+#define INF_WPE 8                       // waves per SIMD the register allocation aims at
+#endif
+__global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(INF_WPE, INF_WPE))) void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk,
                                                             uint8_t *arena, uint32_t *status) {
     __shared__ InfLds lds_all[INF_WAVES];
     __shared__ uint32_t crc_tab[256], crc_x2n[32];
