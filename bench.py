@@ -226,6 +226,31 @@ def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu:
             c2 = time.perf_counter()
             res["coverage_estimate"] = {"device_ms": round((c1 - c0) * 1e3, 1), "host_ms": round((c2 - c1) * 1e3, 1),
                                         "match": cov_d == cov_h, "cov": int(cov_d[0])}
+            # the whole driver, file to .mp.vcf/.mp.gtf (pf_methphase_main: VCF
+            # gaps, plan, jobs, first-wins tables, writers), device fetch vs
+            # --host-fetch, with the run's parameters given (the coverage
+            # estimate a run without -c adds is timed above)
+            from pomfret_amd.pipeline import methphase_files
+            vcf = path[:-4] + ".vcf"
+            _bamio.write_phased_vcf(vcf, "chrS", list(zip(ws.tolist(), we.tolist())), chrom_len=2_000_000_000)
+            drv = {}
+            for hf in (False, True):
+                pre = path[:-4] + f".drv{int(hf)}"
+                d0 = time.perf_counter()
+                r = methphase_files(path, vcf, pre, cfg, lcfg, ctx=ctx, threads=threads, host_fetch=hf)
+                d1 = time.perf_counter()
+                outs = [open(pre + e, "rb").read() for e in (".mp.vcf", ".mp.gtf")]
+                for e in (".mp.vcf", ".mp.gtf"):
+                    os.unlink(pre + e)
+                drv[hf] = (d1 - d0, r["decision"], outs)
+            res["driver"] = {"device_fetch_ms": round(drv[False][0] * 1e3, 1),
+                             "device_fetch_reads_per_s": round(reads / drv[False][0], 1),
+                             "host_fetch_ms": round(drv[True][0] * 1e3, 1),
+                             "host_fetch_reads_per_s": round(reads / drv[True][0], 1),
+                             "outputs_identical": drv[False][2] == drv[True][2],
+                             "decisions_match": bool(np.array_equal(drv[False][1], dec_dev)),
+                             "what": "methphase_files: BAM + phased VCF -> .mp.vcf/.mp.gtf, parameters given"}
+            os.unlink(vcf)
             if cpu:
                 import oracle
                 t3 = time.perf_counter()
