@@ -342,7 +342,8 @@ DEV void out_flush(Out &o, uint32_t lane) {
 
 DEV void out_lit(Out &o, uint32_t v, uint32_t lane) {
     const uint32_t rel = o.a - o.cb;
-    if (lane == (rel >> 2)) o.val |= v << (8 * (rel & 3u));
+    const uint32_t add = v << (8 * (rel & 3u));
+    o.val |= lane == (rel >> 2) ? add : 0u;              // a select, not an exec-mask branch
     o.a++;
     if (rel == 255) out_flush(o, lane);
 }
@@ -353,23 +354,22 @@ DEV void out_match(Out &o, uint32_t L, uint32_t D, uint32_t lane) {
     while (o.a < me) {
         const uint32_t seg_end = me < o.cb + 256 ? me : o.cb + 256;
         uint32_t setp = 0;
+        // (selects, not exec-mask branches: the scalar unit is the bottleneck)
         if (D < L) {                                     // overlapping copy: the source repeats with period D
 #pragma unroll
             for (uint32_t i = 0; i < 4; i++) {
                 const uint32_t q = o.cb + 4 * lane + i;
-                if (q >= o.a && q < seg_end) {
-                    o.src[i] = ms - D + (q - ms) % D;
-                    setp |= 1u << i;
-                }
+                const bool in = q >= o.a && q < seg_end;
+                o.src[i] = in ? ms - D + (q - ms) % D : o.src[i];
+                setp |= in ? 1u << i : 0u;
             }
         } else {
 #pragma unroll
             for (uint32_t i = 0; i < 4; i++) {
                 const uint32_t q = o.cb + 4 * lane + i;
-                if (q >= o.a && q < seg_end) {
-                    o.src[i] = q - D;
-                    setp |= 1u << i;
-                }
+                const bool in = q >= o.a && q < seg_end;
+                o.src[i] = in ? q - D : o.src[i];
+                setp |= in ? 1u << i : 0u;
             }
         }
         o.pend |= setp;
@@ -540,11 +540,20 @@ __global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(
                 const uint32_t lk = ek >> 9, sk = ek & 511u;
                 const uint32_t lit = (lk != 0 && sk < 256 && lane + lk <= b.cnt) ? (sk | (lk << 8)) : 0u;
                 uint32_t off = 0;
-                while (off < 64) {
-                    const uint32_t x = rdl(lit, off);
-                    if (!x || o.a >= o.hi) break;        // (a full output is flagged by the general step)
-                    out_lit(o, x & 255u, lane);
-                    off += x >> 8;
+                if (o.hi - o.a >= 64) {                  // room for any run (<= 64 literals)
+                    while (off < 64) {
+                        const uint32_t x = rdl(lit, off);
+                        if (!x) break;
+                        out_lit(o, x & 255u, lane);
+                        off += x >> 8;
+                    }
+                } else {
+                    while (off < 64) {
+                        const uint32_t x = rdl(lit, off);
+                        if (!x || o.a >= o.hi) break;    // (a full output is flagged by the general step)
+                        out_lit(o, x & 255u, lane);
+                        off += x >> 8;
+                    }
                 }
                 if (off) {
                     b.buf = off >= 64 ? 0ull : b.buf >> off;
