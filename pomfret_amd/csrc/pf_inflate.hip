@@ -121,6 +121,12 @@ DEV void bits_fill(Bits &b, uint32_t lane) {
         if (b.rd > b.lim) b.over = 1;
     }
 }
+DEV uint32_t bits_take(Bits &b, uint32_t n) {      // n < 32, after a fill covering it
+    const uint32_t v = (uint32_t)b.buf & ((1u << n) - 1u);
+    b.buf >>= n;
+    b.cnt -= n;
+    return v;
+}
 DEV uint32_t bits_get(Bits &b, uint32_t n) {       // n <= 32, after a fill covering it
     const uint32_t v = (uint32_t)b.buf & (n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1u));
     b.buf >>= n;
@@ -581,9 +587,13 @@ __global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(
             if (li >= 29) { err = PF_INF_ECODES; break; }
             // length base / extra bits (RFC 1951 3.2.5) by arithmetic: a table
             // lookup would be a memory load on the decode chain
-            const uint32_t lx = li < 8 ? 0u : li == 28 ? 0u : (li - 4) >> 2;
-            const uint32_t lb = li < 8 ? 3 + li : li == 28 ? 258u : ((4 + (li & 3u)) << lx) + 3;
-            const uint32_t L = lb + bits_get(b, lx);
+            uint32_t L;
+            if (li < 8) L = 3 + li;                      // no extra bits (the short matches of BAM content)
+            else if (li == 28) L = 258;
+            else {
+                const uint32_t lx = (li - 4) >> 2;
+                L = ((4 + (li & 3u)) << lx) + 3 + bits_take(b, lx);
+            }
             bits_fill(b, lane);
             e = uni(T.droot[(uint32_t)b.buf & ((1u << INF_DROOT) - 1u)]);
             l = e >> 9;
@@ -596,9 +606,12 @@ __global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(
             }
             bits_get(b, l);
             if (s >= 30) { err = PF_INF_ECODES; break; }
-            const uint32_t dx = s < 4 ? 0u : (s - 2) >> 1;
-            const uint32_t db = s < 4 ? 1 + s : ((2 + (s & 1u)) << dx) + 1;
-            const uint32_t D = db + bits_get(b, dx);
+            uint32_t D;
+            if (s < 4) D = 1 + s;
+            else {
+                const uint32_t dx = (s - 2) >> 1;
+                D = ((2 + (s & 1u)) << dx) + 1 + bits_take(b, dx);
+            }
             if (D > o.a - o.lo) { err = PF_INF_EDIST; break; }
             if (o.a + L > o.hi) { err = PF_INF_ESIZE; break; }
             out_match(o, L, D, lane);
