@@ -22,6 +22,8 @@ namespace v0 {                          // A: _inf_a.hip (a saved earlier versio
 namespace v1 {
 #undef INF_AB
 #define INF_AB 1
+#undef INF_SPECM
+#define INF_SPECM 1
 #include "../../pomfret_amd/csrc/pf_inflate.hip"
 }
 
