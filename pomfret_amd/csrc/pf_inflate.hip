@@ -23,9 +23,12 @@
 //    code lengths tested at once, one per lane (the canonical walk's answer);
 //    literal-pair root entries were tried and measured slower (few pairs fit
 //    10 bits on BAM content, and the larger table costs a wave of occupancy);
+//  * runs of literals and short matches are decoded speculatively: lane k
+//    pre-decodes the symbol (and a match's distance) starting at bit offset k
+//    of the buffered bits and the run follows the stream with readlanes;
 //  * measured by SQ counters (tools/ubench/inflate_ab, BAM-like blocks): per
-//    output byte ~35 SALU + ~25 VALU instructions and ~0.9 LDS reads, scalar
-//    issue at ~2/3 of one SALU per CU-cycle;
+//    output byte 23 SALU + 21 VALU instructions and 0.5 LDS reads (35 + 25 +
+//    0.9 before the speculative runs), the decode bound by scalar issue;
 //  * output is assembled lane-distributed in 256-byte chunks aligned to the
 //    arena (lane k holds bytes 4k..4k+3 of the chunk) and flushed with one
 //    coalesced store per chunk; a match only records its bytes' sources, and
