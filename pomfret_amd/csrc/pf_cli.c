@@ -60,7 +60,7 @@ static void help_methphase(const char *prefix) {
     fprintf(stderr, "  --output-tsv [opt] Also write {prefix}.mp.tsv.\n");
     fprintf(stderr, "  --write-bam  [opt] Also write {prefix}.mp.bam (+ .bai) with the new HP tags.\n");
     fprintf(stderr, "  --gpus [opt] GPUs to use. [all visible]\n");
-    fprintf(stderr, "  --host-fetch [opt] Inflate and decode BAM records on the host instead of the GPU.\n");
+    fprintf(stderr, "  --host-fetch [opt] Inflate and decode BAM records (and the coverage pass) on the host instead of the GPU.\n");
 }
 
 enum { O_LO = 301, O_HI, O_GTF = 304, O_VCF = 306, O_MAPQ, O_TSV, O_WBAM, O_OTSV, O_BAMT, O_UNTAG, O_WIT,
