@@ -56,6 +56,8 @@ struct pf_ctx {
     int have_haptag;
     void *pin = nullptr;      /* pinned staging for large uploads (grown on demand) */
     size_t pin_cap = 0;
+    void *stage = nullptr;    /* pinned staging of the device fetch's compressed bytes */
+    size_t stage_cap = 0;
     uint32_t k3_lds_set = 0;  /* dynamic LDS limits set on the greedy kernels of this device */
     uint32_t k3_lds_fb_set = 0;
     uint32_t k3w_lds_set = 0;
@@ -197,6 +199,32 @@ extern "C" int pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches) {
 extern "C" int pf_ctx_device(const pf_ctx *c) { return c->device; }
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c) { return c->stream; }
 
+// the context's pinned staging buffer for the device fetch's compressed bytes
+// (pf_ingest.hip), grown on demand; the caller owns the context's stream
+extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n) {
+    if (c->stage_cap < n) {
+        if (c->stage) { (void)hipStreamSynchronize(c->stream); (void)hipHostFree(c->stage); }
+        c->stage = nullptr;
+        c->stage_cap = 0;
+        void *p = nullptr;
+        const size_t cap = n + n / 4;
+        if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        c->stage = p;
+        c->stage_cap = cap;
+    }
+    return static_cast<uint8_t *>(c->stage);
+}
+
+// release the staging buffer when it grew past `keep` bytes
+extern "C" void pf_ctx_stage_trim(pf_ctx *c, size_t keep) {
+    if (c->stage && c->stage_cap > keep) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipHostFree(c->stage);
+        c->stage = nullptr;
+        c->stage_cap = 0;
+    }
+}
+
 extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
@@ -204,6 +232,7 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
     if (c->pin) (void)hipHostFree(c->pin);
+    if (c->stage) (void)hipHostFree(c->stage);
     delete c;
 }
 
@@ -873,7 +902,6 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
             c->k3_lds_fb_set = d.lds_fb;
         }
     }
-    (void)hipGetLastError();
     HIPCHK(hipEventRecord(b->ev[slot][0], st));
     if (b->has_aln) {
         // K0: filters + 5mC extraction of every record into staging slices

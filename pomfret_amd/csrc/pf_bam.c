@@ -1393,7 +1393,8 @@ int pf_bam_estimate_coverage(pf_bam_t *b, int32_t *covs, int32_t n) {
  * whose chunks span < 64 KiB of compressed file into their parent, in khash
  * order) is not applied, so the index answers every query alike but is not
  * byte-identical to htslib's -- parity unpinned (htslib is absent here).  The
- * records themselves are copied byte for byte except the HP tag; a CG:B:I
+ * records themselves are copied byte for byte except the HP tag and the bin
+ * field, which bam_read1 recomputes from the CIGAR; a CG:B:I
  * long-CIGAR record keeps its placeholder layout (htslib's bam_write1 would
  * re-append the CG tag at the end of the aux data). */
 
@@ -1814,6 +1815,12 @@ int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, c
         if (w) {
             rc = hp_update(rec, bs, &r, (int64_t)hp + 1, &ob);
             if (rc) break;
+            if (ncg > 0) {       /* bam_read1 recomputes bin from the CIGAR (hts_reg2bin(pos, pos + rlen, 14, 5)) */
+                const int64_t rl = ((r.flag & 4) || rlen == 0) ? 1 : (int64_t)rlen;
+                const uint32_t bin = reg2bin14(r.pos, r.pos + rl);
+                ob.p[10] = (uint8_t)bin;
+                ob.p[11] = (uint8_t)(bin >> 8);
+            }
             uint8_t o4[4];
             const uint32_t nb = (uint32_t)ob.n;
             for (int i = 0; i < 4; i++) o4[i] = (uint8_t)(nb >> (8 * i));

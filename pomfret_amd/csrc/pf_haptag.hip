@@ -567,7 +567,7 @@ static hipError_t put(std::vector<void *> &al, T **dst, const T *src, size_t n) 
 // MD length (the cursor chain and the scratch slices); dv supplies the reads'
 // device arrays (cigar_off .. md) or is null (copied from Rb's host arrays).
 int pf_haptag_core(pf_ctx_t *ctx, const pf_known_vars_t *K, uint32_t N, const pf_k4_reads_host &h,
-                   const pf_read_aln_batch_t *Rb, const pf_k4_reads_dev *dv, uint8_t *hp_out) {
+                   const pf_read_aln_batch_t *Rb, const pf_k4_reads_dev *dv, uint8_t *hp_out, uint32_t *prev_left) {
     if (N == 0) return PF_OK;
     const uint32_t V = K->n;
     if (V == 0) { memset(hp_out, HAPTAG_UNPHASED, N); return PF_OK; }
@@ -581,7 +581,7 @@ int pf_haptag_core(pf_ctx_t *ctx, const pf_known_vars_t *K, uint32_t N, const pf
     std::vector<uint32_t> il(N), je(N);
     std::vector<uint64_t> so(N + 1);
     {
-        uint32_t prev = 0;
+        uint32_t prev = prev_left ? *prev_left : 0;
         uint64_t acc = 0;
         for (uint32_t r = 0; r < N; r++) {
             uint32_t i = prev;
@@ -600,6 +600,7 @@ int pf_haptag_core(pf_ctx_t *ctx, const pf_known_vars_t *K, uint32_t N, const pf
             acc += (std::max(need_t, need_w) + 1) & ~1ull;
         }
         so[N] = acc;
+        if (prev_left) *prev_left = prev;
     }
     {
         const int dev = pf_ctx_device(ctx);
@@ -658,6 +659,8 @@ int pf_haptag_core(pf_ctx_t *ctx, const pf_known_vars_t *K, uint32_t N, const pf
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
             pf_ctx_set_haptag_ms(ctx, ms, thread_impl ? "pf_k4_thread" : "pf_k4_haptag");
+        else
+            (void)hipGetLastError();       // a failed timing query must not fail a later launch check
         if (d.prof) {
             unsigned long long pr[8];
             HCHK(hipMemcpy(pr, d.prof, sizeof(pr), hipMemcpyDeviceToHost));

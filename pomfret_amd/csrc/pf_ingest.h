@@ -116,6 +116,10 @@ typedef struct pf_k4_reads_dev {
 struct pf_ctx;
 struct pf_known_vars;
 struct pf_read_aln_batch;
+// prev_left: the reference's prev_i_left cursor (blockjoin.c:1716-1720) going
+// in and coming out, so that a contig haptagged in pieces chains like one
+// call (null: starts at 0)
 int pf_haptag_core(struct pf_ctx *ctx, const struct pf_known_vars *K, uint32_t N, const pf_k4_reads_host &h,
-                   const struct pf_read_aln_batch *Rb, const pf_k4_reads_dev *dv, uint8_t *hp_out);
+                   const struct pf_read_aln_batch *Rb, const pf_k4_reads_dev *dv, uint8_t *hp_out,
+                   uint32_t *prev_left = nullptr);
 #endif

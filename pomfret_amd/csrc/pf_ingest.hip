@@ -11,6 +11,8 @@
 struct pf_ctx;
 extern "C" int pf_ctx_device(const pf_ctx *c);
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c);
+extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n);
+extern "C" void pf_ctx_stage_trim(pf_ctx *c, size_t keep);
 
 #define ICHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "[E::pomfret_amd] %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
@@ -170,25 +172,10 @@ struct Plan {
     uint64_t arena = 0;                     // inflated bytes
 };
 
-// one pinned staging buffer per device for the compressed bytes (grown on
-// demand, reused by every fetch on that device: pinning costs about as much
-// as the copy it enables)
-std::mutex g_pin_mu;
-std::vector<std::pair<uint8_t *, size_t>> g_pin;
-uint8_t *pinned(int dev, size_t n) {
-    std::lock_guard<std::mutex> g(g_pin_mu);
-    if ((size_t)dev >= g_pin.size()) g_pin.resize(dev + 1, {nullptr, 0});
-    auto &e = g_pin[dev];
-    if (e.second < n) {
-        if (e.first) (void)hipHostFree(e.first);
-        e = {nullptr, 0};
-        void *p = nullptr;
-        const size_t cap = n + n / 4;
-        if (hipHostMalloc(&p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
-        e = {static_cast<uint8_t *>(p), cap};
-    }
-    return e.first;
-}
+// The compressed bytes are staged in the context's pinned buffer (grown on
+// demand and reused by every fetch of that context: pinning costs about as
+// much as the copy it enables).  One fetch runs on a context at a time, so
+// the buffer needs no lock; two contexts never share one.
 
 // the gathered small fields, host side
 struct Small {
@@ -294,8 +281,8 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
     hipStream_t st = pf_ctx_stream((const pf_ctx *)ctx);
     if (hipSetDevice(pf_ctx_device((const pf_ctx *)ctx)) != hipSuccess) { close(fd); return PF_ERR_HIP; }
     memset(&F->pub, 0, sizeof F->pub);
-    (void)hipGetLastError();             // launches below are checked with hipGetLastError: no stale error
     int rc = PF_OK;
+    bool done = false;                    // an attempt covered every window and ran the sink
     uint64_t ext = 4ull << 16;            // bytes read past a chunk's last block (records spanning blocks)
     for (int attempt = 0; attempt < 8; attempt++) {
         DevBuf D;
@@ -317,7 +304,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         uint64_t tot = 0;
         for (auto &R : P.runs) { R.buf0 = tot; tot += R.f1 - R.f0; }
         P.comp_n = tot + 512;
-        P.comp = pinned(pf_ctx_device((const pf_ctx *)ctx), P.comp_n);
+        P.comp = pf_ctx_stage((pf_ctx *)ctx, P.comp_n);
         uint8_t *d_comp = D.alloc<uint8_t>(P.comp_n);
         if (!P.comp || !d_comp) { rc = PF_ERR_NOMEM; break; }
         // parallel reads into the pinned buffer in segments of <= 64 MiB, each
@@ -704,9 +691,15 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         pub.ms_build = ms_build;
         pub.ms_total = now_ms() - t_start;
         pub.attempts = (uint32_t)attempt + 1;
+        done = true;
         break;
     }
     close(fd);
+    pf_ctx_stage_trim((pf_ctx *)ctx, 8ull << 30);   // an outsized fetch does not stay pinned
+    if (!rc && !done) {
+        fprintf(stderr, "[E::pomfret_amd] device fetch: records still run past the planned blocks after 8 plans\n");
+        rc = PF_ERR_LIMIT;
+    }
     return rc;
 }
 
@@ -759,55 +752,127 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
     return PF_OK;
 }
 
+// Position pieces of one contig for whole-contig device fetches, each of
+// about piece_bytes of compressed BAM (the contig's index chunks span
+// [c0, c1) of the file): K pieces of equal reference length; a record belongs
+// to the piece its start falls in.  piece_bytes 0: PF_FETCH_PIECE_BYTES or
+// 4 GiB (tests force several pieces on small files with the variable).
+static uint64_t contig_pieces(pf_bam_t *bam, int32_t tid, uint64_t piece_bytes, int64_t *step) {
+    if (!piece_bytes)
+        if (const char *e = getenv("PF_FETCH_PIECE_BYTES")) piece_bytes = strtoull(e, nullptr, 10);
+    if (!piece_bytes) piece_bytes = 4ull << 30;
+    const int64_t nc = pf_bam_query_chunks(bam, tid, 0, INT64_MAX, nullptr, 0);
+    std::vector<uint64_t> uv(2 * (size_t)std::max<int64_t>(nc, 0));
+    uint64_t c0 = UINT64_MAX, c1 = 0;
+    if (nc > 0 && pf_bam_query_chunks(bam, tid, 0, INT64_MAX, uv.data(), (uint64_t)nc) == nc)
+        for (int64_t c = 0; c < nc; c++) { c0 = std::min(c0, uv[2 * c] >> 16); c1 = std::max(c1, uv[2 * c + 1] >> 16); }
+    const uint32_t len = pf_bam_target_len(bam, tid);
+    const uint64_t K = c1 > c0 ? std::max<uint64_t>(1, std::min<uint64_t>(len ? len : 1, (c1 - c0 + piece_bytes - 1) /
+                                                                                           piece_bytes)) : 1;
+    *step = (int64_t)((len + K - 1) / K);
+    return K;
+}
+
 extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
                              pf_bam_dev_fetch_t **fetch_out) {
     if (!ctx || !K || !bam || !chrom || !fetch_out) return PF_ERR_ARG;
     *fetch_out = nullptr;
-    // sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX)
-    const int64_t beg = 0, end = INT64_MAX;
+    // sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX),
+    // fetched in position pieces of bounded size whose reads are concatenated
+    // in BAM order (a read is taken in the piece its start falls in: the
+    // coordinate-sorted records of an earlier start form a prefix of a
+    // piece's overlap list); the K4 cursor chain runs on across pieces
+    const int32_t tid = pf_bam_tid(bam, chrom);
+    if (tid < 0) return PF_ERR_ARG;
+    int64_t step = 0;
+    const uint64_t NP = contig_pieces(bam, tid, 0, &step);
     pf_bam_dev_fetch_own *F = new pf_bam_dev_fetch_own();
-    int rc = dev_fetch(ctx, bam, pf_bam_tid(bam, chrom), 1, &beg, &end, 1u, 0u, F, [&](FetchOut &fo) -> int {
-        const Small &S = *fo.S;
-        const uint64_t N = fo.n;
-        if (N >= (1ull << 32)) return PF_ERR_LIMIT;
-        F->read_hp.assign(N, 0);
-        if (!N) return PF_OK;
-        std::vector<uint32_t> start(N), endp(N);
-        std::vector<uint64_t> co(N + 1, 0), so(N + 1, 0), mo(N + 1, 0);
-        for (uint64_t i = 0; i < N; i++) {
-            start[i] = S.pos[i];
-            endp[i] = (uint32_t)((int64_t)(int32_t)S.pos[i] + (int64_t)S.rlen[i]);   // bam_endpos
-            co[i + 1] = co[i] + S.ncig[i];
-            so[i + 1] = so[i] + (S.l_qseq[i] + 1ull) / 2;
-            mo[i + 1] = mo[i] + S.md_len[i];
+    F->qn_off.assign(1, 0);
+    uint32_t prev_left = 0;
+    double ms[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t comp = 0, infl = 0, nblk = 0, nchain = 0;
+    uint32_t attempts = 0;
+    int rc = PF_OK;
+    for (uint64_t k = 0; k < NP && !rc; k++) {
+        const int64_t beg = (int64_t)k * step, end = k + 1 == NP ? INT64_MAX : (int64_t)(k + 1) * step;
+        pf_bam_dev_fetch_own P;
+        rc = dev_fetch(ctx, bam, tid, 1, &beg, &end, 1u, 0u, &P, [&](FetchOut &fo) -> int {
+            const Small &S = *fo.S;
+            uint64_t m = 0;                                   // reads counted in an earlier piece
+            if (k) while (m < fo.n && (int32_t)S.pos[m] < beg) m++;
+            const uint64_t N = fo.n - m;
+            if (F->read_hp.size() + N >= (1ull << 32)) return PF_ERR_LIMIT;
+            const size_t h0 = F->read_hp.size();
+            F->read_hp.resize(h0 + N, 0);
+            if (!N) return PF_OK;
+            std::vector<uint32_t> start(N), endp(N), nins(N), ncig(N), mdl(N), lq(N);
+            std::vector<uint64_t> co(N + 1, 0), so(N + 1, 0), mo(N + 1, 0);
+            for (uint64_t i = 0; i < N; i++) {
+                const uint64_t r = m + i;
+                start[i] = S.pos[r];
+                endp[i] = (uint32_t)((int64_t)(int32_t)S.pos[r] + (int64_t)S.rlen[r]);   // bam_endpos
+                nins[i] = S.nins[r]; ncig[i] = S.ncig[r]; mdl[i] = S.md_len[r]; lq[i] = S.l_qseq[r];
+                co[i + 1] = co[i] + S.ncig[r];
+                so[i + 1] = so[i] + (S.l_qseq[r] + 1ull) / 2;
+                mo[i + 1] = mo[i] + S.md_len[r];
+            }
+            DevBuf &D = *fo.D;
+            uint32_t *d_start = D.alloc<uint32_t>(N), *d_end = D.alloc<uint32_t>(N), *d_len = D.alloc<uint32_t>(N);
+            uint64_t *d_co = D.alloc<uint64_t>(N + 1), *d_so = D.alloc<uint64_t>(N + 1), *d_mo = D.alloc<uint64_t>(N + 1);
+            uint32_t *d_cig = D.alloc<uint32_t>(co[N]);
+            uint8_t *d_seq = D.alloc<uint8_t>(so[N] + 16), *d_md = D.alloc<uint8_t>(mo[N] + 16);
+            if (!d_start || !d_end || !d_len || !d_co || !d_so || !d_mo || !d_cig || !d_seq || !d_md) return PF_ERR_NOMEM;
+            hipStream_t st = fo.st;
+            bool ok = hipMemcpyAsync(d_start, start.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
+                      hipMemcpyAsync(d_end, endp.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
+                      hipMemcpyAsync(d_len, lq.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
+                      hipMemcpyAsync(d_co, co.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
+                      hipMemcpyAsync(d_so, so.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
+                      hipMemcpyAsync(d_mo, mo.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess;
+            if (ok) {
+                hipLaunchKernelGGL(pf_gather_big, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, fo.arena, fo.sel + m,
+                                   N, fo.R, (const uint64_t *)d_co, d_cig, (const uint64_t *)d_so, d_seq,
+                                   (const uint64_t *)nullptr, (uint8_t *)nullptr, (const uint64_t *)nullptr,
+                                   (uint8_t *)nullptr, (const uint64_t *)nullptr, (uint8_t *)nullptr,
+                                   (const uint64_t *)d_mo, d_md);
+                ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+            }
+            if (!ok) return PF_ERR_HIP;
+            pf_k4_reads_host h{start.data(), endp.data(), nins.data(), ncig.data(), mdl.data()};
+            pf_k4_reads_dev dv{d_start, d_end, d_co, d_cig, d_so, d_len, d_seq, d_mo, d_md};
+            return pf_haptag_core(ctx, K, (uint32_t)N, h, nullptr, &dv, F->read_hp.data() + h0, &prev_left);
+        });
+        if (rc) break;
+        // this piece's reads' qnames (after the prefix of earlier starts)
+        const uint64_t n = P.pub.n_recs, got = F->read_hp.size() - (F->qn_off.size() - 1), m = n - got;
+        for (uint64_t i = m; i < n; i++) {
+            F->qn.insert(F->qn.end(), P.qn.begin() + P.qn_off[i], P.qn.begin() + P.qn_off[i + 1]);
+            F->qn_off.push_back(F->qn.size());
         }
-        DevBuf &D = *fo.D;
-        uint32_t *d_start = D.alloc<uint32_t>(N), *d_end = D.alloc<uint32_t>(N), *d_len = D.alloc<uint32_t>(N);
-        uint64_t *d_co = D.alloc<uint64_t>(N + 1), *d_so = D.alloc<uint64_t>(N + 1), *d_mo = D.alloc<uint64_t>(N + 1);
-        uint32_t *d_cig = D.alloc<uint32_t>(co[N]);
-        uint8_t *d_seq = D.alloc<uint8_t>(so[N] + 16), *d_md = D.alloc<uint8_t>(mo[N] + 16);
-        if (!d_start || !d_end || !d_len || !d_co || !d_so || !d_mo || !d_cig || !d_seq || !d_md) return PF_ERR_NOMEM;
-        hipStream_t st = fo.st;
-        bool ok = hipMemcpyAsync(d_start, start.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipMemcpyAsync(d_end, endp.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipMemcpyAsync(d_len, S.l_qseq.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipMemcpyAsync(d_co, co.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipMemcpyAsync(d_so, so.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipMemcpyAsync(d_mo, mo.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess;
-        if (ok) {
-            hipLaunchKernelGGL(pf_gather_big, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, fo.arena, fo.sel, N, fo.R,
-                               (const uint64_t *)d_co, d_cig, (const uint64_t *)d_so, d_seq, (const uint64_t *)nullptr,
-                               (uint8_t *)nullptr, (const uint64_t *)nullptr, (uint8_t *)nullptr,
-                               (const uint64_t *)nullptr, (uint8_t *)nullptr, (const uint64_t *)d_mo, d_md);
-            ok = hipGetLastError() == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
-        }
-        if (!ok) return PF_ERR_HIP;
-        pf_k4_reads_host h{start.data(), endp.data(), S.nins.data(), S.ncig.data(), S.md_len.data()};
-        pf_k4_reads_dev dv{d_start, d_end, d_co, d_cig, d_so, d_len, d_seq, d_mo, d_md};
-        return pf_haptag_core(ctx, K, (uint32_t)N, h, nullptr, &dv, F->read_hp.data());
-    });
+        comp += P.pub.comp_bytes; infl += P.pub.inflated_bytes; nblk += P.pub.n_blocks; nchain += P.pub.n_chain_recs;
+        ms[0] += P.pub.ms_read; ms[1] += P.pub.ms_inflate; ms[2] += P.pub.ms_chain; ms[3] += P.pub.ms_decode;
+        ms[4] += P.pub.ms_select; ms[5] += P.pub.ms_build; ms[6] += P.pub.ms_total;
+        attempts += P.pub.attempts;
+        if (P.win_status[0] == PF_WIN_TRUNC) { F->pub.n_truncated = 1; break; }   // sam_itr_next < 0 ends the loop
+    }
     if (rc) { delete F; return rc; }
-    F->pub.read_hp = F->read_hp.data();
+    const uint64_t N = F->read_hp.size();
+    F->qn.push_back(0);
+    F->win_rec_off = {0, (uint32_t)N};
+    F->win_n = {(uint32_t)N};
+    pf_bam_dev_fetch_t &pub = F->pub;
+    pub.n_windows = 1;
+    pub.n_recs = N;
+    pub.win_rec_off = F->win_rec_off.data();
+    pub.win_n_fetched = F->win_n.data();
+    pub.qname_off = F->qn_off.data();
+    pub.qname = F->qn.data();
+    pub.hp_tag = nullptr;
+    pub.comp_bytes = comp; pub.inflated_bytes = infl; pub.n_blocks = nblk; pub.n_chain_recs = nchain;
+    pub.ms_read = ms[0]; pub.ms_inflate = ms[1]; pub.ms_chain = ms[2]; pub.ms_decode = ms[3];
+    pub.ms_select = ms[4]; pub.ms_build = ms[5]; pub.ms_total = ms[6];
+    pub.attempts = attempts;
+    pub.read_hp = F->read_hp.data();
     *fetch_out = &F->pub;
     return PF_OK;
 }
@@ -829,24 +894,19 @@ extern "C" int pf_bam_estimate_coverage_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_
     if (n < nr) return PF_ERR_ARG;
     const int64_t n_unplaced = pf_bam_n_no_coor(bam);
     if (n_unplaced < 0) return pf_bam_estimate_coverage(bam, covs, n);
-    if (!piece_bytes) piece_bytes = 4ull << 30;
     for (int32_t i = 0; i < n; i++) covs[i] = 0;
     constexpr uint32_t MOD = 5000;
     int32_t last = -1;
     bool stopped = false;
-    std::vector<uint64_t> bins, uv;
+    std::vector<uint64_t> bins;
     for (int32_t t = 0; t < nr && !stopped; t++) {
         const int64_t nc = pf_bam_query_chunks(bam, t, 0, INT64_MAX, nullptr, 0);
         if (nc < 0) return (int)nc;
         if (nc == 0) continue;
-        uv.resize(2 * (size_t)nc);
-        if (pf_bam_query_chunks(bam, t, 0, INT64_MAX, uv.data(), (uint64_t)nc) != nc) return PF_ERR_INTERNAL;
-        uint64_t c0 = UINT64_MAX, c1 = 0;
-        for (int64_t c = 0; c < nc; c++) { c0 = std::min(c0, uv[2 * c] >> 16); c1 = std::max(c1, uv[2 * c + 1] >> 16); }
         last = t;
         const uint32_t len = pf_bam_target_len(bam, t);
-        const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>(len ? len : 1, (c1 - c0 + piece_bytes - 1) / piece_bytes));
-        const int64_t step = (int64_t)((len + K - 1) / K);
+        int64_t step = 0;
+        const uint64_t K = contig_pieces(bam, t, piece_bytes, &step);
         bins.assign(len / MOD, 0);
         for (uint64_t k = 0; k < K && !stopped; k++) {
             const int64_t beg = (int64_t)k * step, end = k + 1 == K ? INT64_MAX : (int64_t)(k + 1) * step;

@@ -333,21 +333,25 @@ def _result(plan: Plan, mode: int) -> Dict:
 def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],
                     lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8, ctx=None,
                     untagged: bool = False, tsv: bool = False, n_devices: int = 1, job_windows: int = 0,
-                    host_fetch: bool = False) -> Dict:
+                    host_fetch: bool = False, ctxs=None) -> Dict:
     """`pomfret methphase` over every gap of vcf_path with the reads of
     bam_path, in this process (pf_methphase_main).  Writes out_prefix +
     .mp.gtf / .mp.vcf (and .mp.tsv with tsv=True, the reference's
     --output-tsv) unless out_prefix is None.  cfg None: no -c, per-contig
     parameters from the coverage estimate (4358-4390).  ctx: drive that
-    context; else n_devices GPUs from `device` on (0: all visible).
+    context; ctxs: drive those contexts, one host thread each, over one job
+    queue (two contexts of one device exercise the multi-GPU dispatcher);
+    else n_devices GPUs from `device` on (0: all visible).
     Returns dict(decision=int8[n_gaps], contigs=[...], qname_hp={qname: hp},
     raw_hp={qname: hp} (the -u table), n_limit)."""
     L = _bind()
     devs = None
-    if ctx is None and device and n_devices >= 1:
+    if ctx is not None:
+        ctxs = [ctx]
+    if not ctxs and device and n_devices >= 1:
         devs = (C.c_int32 * n_devices)(*range(device, device + n_devices))
     o = make_opts(bam_path, vcf_path, out_prefix, cfg, lcfg, untagged=untagged, tsv=tsv, threads=threads,
-                  n_devices=0 if ctx is not None else n_devices, ctxs=[ctx] if ctx is not None else None,
+                  n_devices=0 if ctxs else n_devices, ctxs=ctxs or None,
                   job_windows=job_windows, host_fetch=host_fetch)
     if devs is not None:
         o.devices = C.cast(devs, C.c_void_p)
@@ -363,15 +367,17 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
 def report_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cov: int = 0,
                  chunk_size: int = 50_000, chunk_stride: int = 1_000_000, lcfg: Optional[LoadConfig] = None,
                  untagged: bool = False, threads: int = 8, ctx=None, n_devices: int = 1, k: int = 3,
-                 k_span: int = 5000, host_fetch: bool = False) -> Dict:
+                 k_span: int = 5000, host_fetch: bool = False, ctxs=None) -> Dict:
     """`pomfret report` (main_methreport, 4901-5089): chunk windows inside the
     phased blocks, one methphase decision each; writes
     {out_prefix}.report.tsv and the running totals to stdout.  cov: -c
     (0: the per-contig estimate).  Returns dict(decision, counts)."""
     L = _bind()
+    if ctx is not None:
+        ctxs = [ctx]
     o = make_opts(bam_path, vcf_path, out_prefix, Config(k=k, k_span=k_span), lcfg, mode=MODE_REPORT,
-                  untagged=untagged, threads=threads, n_devices=0 if ctx is not None else n_devices,
-                  ctxs=[ctx] if ctx is not None else None, cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride,
+                  untagged=untagged, threads=threads, n_devices=0 if ctxs else n_devices,
+                  ctxs=ctxs or None, cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride,
                   host_fetch=host_fetch)
     h = C.c_void_p()
     _check(L.pf_methphase_main(C.byref(o), C.byref(h)), "pf_methphase_main")

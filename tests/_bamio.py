@@ -316,6 +316,37 @@ def expected_fetch(recs: List[Rec], tid: int, s: int, e: int, readback: int) -> 
             if r.tid == tid and r.pos < end and endpos(r.pos, r.cigar, r.flag) > beg]
 
 
+def _vcf_header(contigs):
+    return ["##fileformat=VCFv4.2"] + [f"##contig=<ID={c},length={n}>" for c, n in contigs] + [
+        '##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype">',
+        '##FORMAT=<ID=PS,Number=1,Type=Integer,Description="Phase set">',
+        "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1"]
+
+
+def phased_vcf_lines(chrom: str, windows):
+    """Body lines of write_phased_vcf for one contig."""
+    lines = []
+    first = max(1, windows[0][0] - 1000)
+    ps = first
+    pts = [(first, ps)]
+    for s, e in windows:
+        pts.append((s, ps))
+        ps = e
+        pts.append((e, ps))
+    pts.append((windows[-1][1] + 1000, ps))
+    for k, (pos, p) in enumerate(pts):
+        gt = "0|1" if k % 2 == 0 else "1|0"
+        lines.append(f"{chrom}\t{pos}\t.\tA\tG\t50\tPASS\t.\tGT:PS\t{gt}:{p}")
+    return lines
+
+
+def write_vcf_multi(path: str, contigs, bodies):
+    """A multi-contig VCF: header with `contigs` [(name, length)], then the
+    body lines of each contig in the order given."""
+    with open(path, "w") as f:
+        f.write("\n".join(_vcf_header(contigs) + [ln for b in bodies for ln in b]) + "\n")
+
+
 def write_phased_vcf(path: str, chrom: str, windows, chrom_len: int = 100_000_000):
     """A one-sample phased VCF whose phase-block gaps are exactly `windows`
     [(s, e), ...] (sorted, far apart): block k ends with a variant at POS s_k
@@ -352,6 +383,14 @@ def write_u_vcf(path: str, chrom: str, aln, chrom_len: int = 400_000_000):
              '##FORMAT=<ID=GT,Number=1,Type=String,Description="Genotype">',
              '##FORMAT=<ID=PS,Number=1,Type=Integer,Description="Phase set">',
              "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1"]
+    lines += u_vcf_lines(chrom, aln)
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+def u_vcf_lines(chrom: str, aln):
+    """Body lines of write_u_vcf for one contig."""
+    lines = []
     ps = None
     for w in range(aln.n_windows):
         sv = aln.meta["snv"][w]
@@ -368,5 +407,4 @@ def write_u_vcf(path: str, chrom: str, aln, chrom_len: int = 400_000_000):
                     ps = e
             gt = "0|1" if hb == 1 else "1|0"
             lines.append(f"{chrom}\t{pos}\t.\t{'ACGT'[r]}\t{'ACGT'[a]}\t50\tPASS\t.\tGT:PS\t{gt}:{ps}")
-    with open(path, "w") as f:
-        f.write("\n".join(lines) + "\n")
+    return lines

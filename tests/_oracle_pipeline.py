@@ -25,10 +25,11 @@ if HERE not in sys.path:
 def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, recs_by_contig=None,
                            n_threads=8):
     """-> dict(decision, qname_hp, raw_hp, gtf, tsv, vcf, counts).  recs_by_contig
-    ({contig: [Rec]} as written) feeds the rescue restatement."""
+    ({contig: [Rec]} as written) feeds the rescue restatement.  cfg None: no
+    -c, every contig's parameters from its coverage estimate."""
     import oracle
     from oracle import epilogue as ep
-    from pomfret_amd import LoadConfig
+    from pomfret_amd import Config, LoadConfig
     from pomfret_amd.bam import BamFile, vcf_known_vars
     from test_bam import _py_rescue
 
@@ -36,6 +37,14 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
     contigs = oracle.vcf_gaps(vcf_path)
     decision, qname_hp, raw_hp = [], {}, {}
     with BamFile(bam_path) as bam:
+        covs = bam.estimate_coverage() if cfg is None else None
+
+        def contig_cfg(name):
+            # no -c: the contig's own estimate, looked up by name (4358-4390)
+            if cfg is not None:
+                return cfg
+            return Config.from_coverage(int(covs[bam.tid(name)]), given=False)
+
         if untagged:
             for c in contigs:
                 if bam.tid(c["name"]) < 0:
@@ -65,7 +74,7 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
             if untagged:
                 aln.hp = np.array([raw_hp.get(q, 254) for q in qn], np.uint8)
             wb, rec_read = oracle.load_reads(lcfg, aln)
-            res = oracle.methphase(cfg, wb, n_threads=n_threads)
+            res = oracle.methphase(contig_cfg(c["name"]), wb, n_threads=n_threads)
             recs_of_read = np.flatnonzero(rec_read != 0xFFFFFFFF)
             dec = res.decision.astype(np.int8)
             decision += dec.tolist()

@@ -161,3 +161,48 @@ def test_two_rank_pipeline_merges_like_one_process(tmp_path, oracle_lib, untagge
     assert open(out + ".mp.tsv").read() == ref["tsv"]
     assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
     assert (ref["decision"] >= 0).any()
+
+
+def _mc_worker(rank, world, port, tmp, untagged):
+    """One rank of methphase_files_dist over the multi-contig fixture, no -c
+    (per-contig parameters from the host coverage estimate), oracle runner."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import json
+        from pomfret_amd.pipeline import methphase_files_dist
+        from tests._oracle_pipeline import oracle_job_runner
+        bam, vcf = os.path.join(tmp, "m.bam"), os.path.join(tmp, "m.vcf")
+        res = methphase_files_dist(bam, vcf, os.path.join(tmp, "dist"), None, untagged=untagged, tsv=True,
+                                   job_windows=2, runner=oracle_job_runner(bam, vcf, n_threads=2))
+        with open(os.path.join(tmp, f"res{rank}.json"), "w") as f:
+            json.dump(dict(decision=res["decision"].tolist(), qname_hp=list(res["qname_hp"].items()),
+                           raw_hp=res["raw_hp"]), f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("untagged", [False, True])
+def test_two_rank_multicontig(tmp_path, oracle_lib, untagged):
+    """Four BAM contigs, three in the VCF (one without reads, header order
+    different from the VCF's), qnames shared across contigs, no -c: the two
+    ranks' jobs merged on the writer equal the single-process oracle pipeline
+    -- per-contig parameters (4358-4390), contig-order first-wins merge
+    (4579-4595), the shared -u raw table (1880), PS 0 on later contigs."""
+    import json
+    from tests import _fixtures as fx
+    from tests._oracle_pipeline import methphase_files_oracle
+    bam, vcf, recs_by, _ = fx.multi_contig(tmp_path, untagged=untagged)
+    mp.spawn(_mc_worker, args=(2, _free_port(), str(tmp_path), untagged), nprocs=2, join=True)
+    ref = methphase_files_oracle(bam, vcf, None, untagged=untagged, recs_by_contig=recs_by)
+    for r in range(2):
+        got = json.load(open(tmp_path / f"res{r}.json"))
+        assert got["decision"] == ref["decision"].tolist()
+        assert [tuple(x) for x in got["qname_hp"]] == list(ref["qname_hp"].items())
+        assert got["raw_hp"] == ref["raw_hp"]
+    out = str(tmp_path / "dist")
+    assert open(out + ".mp.gtf").read() == ref["gtf"]
+    assert open(out + ".mp.tsv").read() == ref["tsv"]
+    assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+    assert (ref["decision"] >= 0).sum() >= 3

@@ -1,0 +1,173 @@
+"""Whole-genome-shaped runs on the device (VERDICT r02 "next round" 1 and 6a):
+the multi-contig fixture of tests/_fixtures.multi_contig through the product
+driver, against the oracle pipeline (tests/_oracle_pipeline.py):
+
+  * methphase with and without -c, pre-haplotagged and -u: decisions, the
+    merged first-wins qname table, the -u raw table, GTF/TSV/VCF bytes;
+  * the cross-contig behaviour the reference has: per-contig parameters from
+    the coverage estimate looked up by name (blockjoin.c:4358-4390, 4537-4539),
+    the per-contig first-wins tables merged in contig order (4579-4595), the
+    -u raw table shared by every contig (1880), prev_group_ID never reset so
+    later contigs get abs_start 0 -> PS 0 and a skipped first GTF block
+    (1406-1410, 2743);
+  * `report` with the per-contig estimate read by VCF contig index
+    (covs[i_ref], 5046) and with -c;
+  * two contexts of one device (the multi-GPU work queue, pf_pipeline.c
+    run_on_devices) byte-identical to one.
+"""
+import numpy as np
+import pytest
+
+from tests import _fixtures as fx
+from tests._oracle_pipeline import methphase_files_oracle, report_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mc_tagged(tmp_path_factory):
+    return fx.multi_contig(tmp_path_factory.mktemp("mct"), untagged=False)
+
+
+@pytest.fixture(scope="module")
+def mc_untagged(tmp_path_factory):
+    return fx.multi_contig(tmp_path_factory.mktemp("mcu"), untagged=True)
+
+
+def _outputs(prefix):
+    return (open(prefix + ".mp.gtf").read(), open(prefix + ".mp.tsv").read(), open(prefix + ".mp.vcf", "rb").read())
+
+
+def _check_quirks(ref, recs_by):
+    """The fixture really exercises the cross-contig paths."""
+    gtf = [ln.split("\t") for ln in ref["gtf"].splitlines()]
+    # later contigs: abs_start 0, so their first block (start 0) is skipped
+    for name in ("chrB", "chrC"):
+        assert all(f[3] != "0" for f in gtf if f[0] == name)
+    assert any(f[0] == "chrA" for f in gtf)
+    vcf = ref["vcf"].split(b"\n")
+    assert any(ln.startswith(b"chrC\t") and ln.endswith(b":0") for ln in vcf)       # PS 0
+    # a qname joined on both chrA and chrC: the table keeps chrA's (contig order)
+    dec = ref["decision"]
+    assert (dec >= 0).sum() >= 3 and (dec < 0).sum() >= 2
+    names_c = {r.qname for r in recs_by["chrC"]}
+    names_a = {r.qname for r in recs_by["chrA"]}
+    assert names_a & names_c & set(ref["qname_hp"])
+
+
+@pytest.mark.parametrize("given", [True, False], ids=["c30", "estimate"])
+@pytest.mark.parametrize("untagged", [False, True], ids=["tagged", "u"])
+def test_multicontig_methphase(oracle_lib, gpu_ctx, tmp_path, mc_tagged, mc_untagged, untagged, given):
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import methphase_files
+    bam, vcf, recs_by, _ = mc_untagged if untagged else mc_tagged
+    cfg = Config.from_coverage(30, given=True) if given else None
+    out = str(tmp_path / "o")
+    res = methphase_files(bam, vcf, out, cfg, ctx=gpu_ctx, untagged=untagged, tsv=True, job_windows=2)
+    ref = methphase_files_oracle(bam, vcf, cfg, untagged=untagged, recs_by_contig=recs_by)
+    assert np.array_equal(res["decision"], ref["decision"])
+    assert res["qname_hp"] == ref["qname_hp"]
+    assert list(res["qname_hp"]) == list(ref["qname_hp"])          # insertion (merge) order too
+    assert res["raw_hp"] == ref["raw_hp"]
+    gtf, tsv, vcf_b = _outputs(out)
+    assert gtf == ref["gtf"] and tsv == ref["tsv"] and vcf_b == ref["vcf"]
+    _check_quirks(ref, recs_by)
+    if untagged:
+        assert len(ref["raw_hp"]) > 0
+
+
+def test_multicontig_plan_parameters(oracle_lib, gpu_ctx, mc_tagged):
+    """No -c: each contig's job parameters come from the device coverage
+    estimate of that contig, looked up by name (the header order differs from
+    the VCF's), est/10+1, 2x, est/4+1 with the clamps (4358-4390)."""
+    from pomfret_amd import Config
+    from pomfret_amd.bam import BamFile
+    from pomfret_amd.pipeline import JOB_WINDOWS, Plan, make_opts
+    bam, vcf, _, _ = mc_tagged
+    with BamFile(bam) as b:
+        covs = b.estimate_coverage()
+        tids = {n: b.tid(n) for n in fx.MULTI_VCF_ORDER}
+    assert len(set(covs)) >= 3
+    plan = Plan(make_opts(bam, vcf, None, None, ctxs=[gpu_ctx], job_windows=2))
+    try:
+        seen = set()
+        for j in range(plan.n_jobs(JOB_WINDOWS)):
+            info = plan.job_info(JOB_WINDOWS, j)
+            want = Config.from_coverage(int(covs[tids[info["contig_name"]]]), given=False)
+            got = info["cfg"]
+            assert (got.cov_for_selection, got.cov_for_runtime, got.n_cand) == \
+                (want.cov_for_selection, want.cov_for_runtime, want.n_cand), info["contig_name"]
+            seen.add(info["contig_name"])
+        assert seen == set(fx.MULTI_VCF_ORDER)
+        assert plan.n_jobs(JOB_WINDOWS) >= 4
+    finally:
+        plan.close()
+
+
+@pytest.mark.parametrize("cov", [0, 30], ids=["estimate", "c30"])
+def test_multicontig_report(oracle_lib, gpu_ctx, tmp_path, mc_tagged, cov):
+    """`report` over every contig: the estimate is read by VCF contig index
+    (covs[i_ref], 5046, so chrA gets chrD's), chunk windows from abs_start 0
+    on the later contigs; rows and totals equal the oracle's."""
+    from pomfret_amd.pipeline import report_files
+    bam, vcf, _, _ = mc_tagged
+    out = str(tmp_path / "rep")
+    res = report_files(bam, vcf, out, cov=cov, chunk_size=10_000, chunk_stride=25_000, ctx=gpu_ctx)
+    text = open(out + ".report.tsv").read()
+    assert text == report_oracle(bam, vcf, cov, 10_000, 25_000)
+    assert sum(res["counts"].values()) == text.count("\n")
+    assert {ln.split("\t")[0] for ln in text.splitlines()} == set(fx.MULTI_VCF_ORDER)
+
+
+@pytest.mark.parametrize("untagged", [False, True], ids=["tagged", "u"])
+def test_two_contexts_one_device(gpu_ctx, tmp_path, mc_tagged, mc_untagged, untagged):
+    """Two contexts on device 0 drive the in-process multi-GPU path: one host
+    thread per context claiming jobs from one queue (and -u jobs), per-context
+    staging buffers.  Outputs are byte-identical to the one-context run."""
+    from pomfret_amd import Config, Context
+    from pomfret_amd.pipeline import methphase_files
+    bam, vcf, _, _ = mc_untagged if untagged else mc_tagged
+    cfg = Config.from_coverage(30, given=True)
+    one = methphase_files(bam, vcf, str(tmp_path / "one"), cfg, ctx=gpu_ctx, untagged=untagged, tsv=True,
+                          job_windows=1)
+    ctxs = [Context(0), Context(0)]
+    try:
+        two = methphase_files(bam, vcf, str(tmp_path / "two"), cfg, ctxs=ctxs, untagged=untagged, tsv=True,
+                              job_windows=1)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert np.array_equal(one["decision"], two["decision"])
+    assert list(one["qname_hp"].items()) == list(two["qname_hp"].items())
+    assert one["raw_hp"] == two["raw_hp"]
+    assert _outputs(str(tmp_path / "one")) == _outputs(str(tmp_path / "two"))
+
+
+def test_untagged_prepass_in_pieces(oracle_lib, gpu_ctx, tmp_path, mc_untagged, monkeypatch):
+    """The -u pre-pass fetches each contig in position pieces of bounded
+    compressed size (a 60x chromosome is tens of GB); forced to
+    64 KiB pieces here, the reads are taken once each, in BAM order, with the
+    K4 cursor chain carried across pieces: the raw table and every output
+    equal the oracle pipeline's."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import methphase_files
+    bam, vcf, recs_by, _ = mc_untagged
+    monkeypatch.setenv("PF_FETCH_PIECE_BYTES", str(64 << 10))
+    cfg = Config.from_coverage(30, given=True)
+    out = str(tmp_path / "p")
+    res = methphase_files(bam, vcf, out, cfg, ctx=gpu_ctx, untagged=True, tsv=True, job_windows=2)
+    ref = methphase_files_oracle(bam, vcf, cfg, untagged=True, recs_by_contig=recs_by)
+    assert res["raw_hp"] == ref["raw_hp"] and len(ref["raw_hp"]) > 0
+    assert np.array_equal(res["decision"], ref["decision"])
+    assert _outputs(out) == (ref["gtf"], ref["tsv"], ref["vcf"])
+    # one contig directly: the same reads, tags and order as a one-piece fetch
+    from pomfret_amd.bam import BamFile, vcf_known_vars
+    kv = vcf_known_vars(vcf, "chrC")
+    with BamFile(bam) as b:
+        hp_p, qn_p, info_p = b.haptag_device(gpu_ctx, "chrC", kv)
+        monkeypatch.delenv("PF_FETCH_PIECE_BYTES")
+        hp_1, qn_1, info_1 = b.haptag_device(gpu_ctx, "chrC", kv)
+    assert qn_p == qn_1 and np.array_equal(hp_p, hp_1)
+    assert info_p["attempts"] > info_1["attempts"]                 # several pieces ran
+    prim = [r for r in recs_by["chrC"] if not (r.flag & (4 | 256 | 2048))]
+    assert qn_1 == [r.qname for r in prim]
