@@ -268,6 +268,121 @@ def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu:
     return res
 
 
+def k4_bytes(known, reads) -> int:
+    """SURVEY.md 8d's -u bytes: per read 4 n_cigar + (l_MD + 1) + n_X +
+    n_I_bases + 16 V_known_in_span + 1."""
+    cig = np.asarray(reads.cigar, np.uint32)
+    kp = np.asarray(known.pos, np.int64)
+    v_span = int((np.searchsorted(kp, np.asarray(reads.end, np.int64))
+                  - np.searchsorted(kp, np.asarray(reads.start, np.int64))).sum())
+    md = np.asarray(reads.md, np.uint8)
+    n_x = int(np.isin(md, np.frombuffer(b"ACGT", np.uint8)).sum())
+    ins = int((cig[(cig & 15) == 1] >> 4).sum())
+    return int(4 * cig.shape[0] + md.shape[0] + reads.n_reads + n_x + ins + 16 * v_span + reads.n_reads)
+
+
+def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bool = True):
+    """BASELINE configs[3]'s shape from files (never `value`): `pomfret
+    methphase -u` without -c on a whole-genome-shaped 60x BAM (tests/_genome:
+    4 contigs, reads uniform over each contig, ~1,000 phase-block gaps of
+    5-40 kb between 50-100 kb blocks, 5 % short blocks merged away, het SNVs
+    1/kb with MD:Z, no HP, QUAL strings, zlib level 6), timed file to
+    .mp.vcf/.mp.gtf:
+      cli:      the pomfret-amd binary as a user runs it (process start, HIP
+                init, the device coverage pass, the device -u pre-pass over
+                every primary read, the window jobs, the writers);
+      driver:   the same driver in this process on a warm context;
+      cpu_port: the product's planner / writers with the host reader, the
+                serial host coverage pass and the oracle computing every job
+                (tests/_oracle_pipeline.methphase_files_port, `threads`
+                threads);
+    outputs compared byte for byte.  Also the K4 kernel on the largest
+    contig's reads (HIP events, SURVEY 8d's -u bytes)."""
+    import subprocess
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    import _genome
+    from pomfret_amd.bam import BamFile, vcf_known_vars
+    from pomfret_amd.pipeline import methphase_files
+    spec = _genome.GenomeSpec()
+    spec.contigs = tuple((n, int(L * scale)) for n, L in spec.contigs)
+    prefix = os.path.join(workdir, f"pf_e2eu_{os.getpid()}")
+    t = time.perf_counter()
+    g = _genome.write_genome(prefix, spec, workers=threads)
+    res = {"contigs": len(spec.contigs), "genome_bp": int(sum(L for _, L in spec.contigs)),
+           "coverage": spec.coverage, "records": g["n_records"],
+           "bam_bytes": g["bam_bytes"], "known_snvs": g["n_snvs"], "threads": threads,
+           "gen_s": round(time.perf_counter() - t, 1)}
+    log(f"[bench] e2e_u: generated {res['records']} records, {res['bam_bytes'] / 1e9:.2f} GB in {res['gen_s']}s")
+    outs = {}
+
+    def take(pre):
+        o = [open(pre + e, "rb").read() for e in (".mp.vcf", ".mp.gtf")]
+        for e in (".mp.vcf", ".mp.gtf"):
+            os.unlink(pre + e)
+        return o
+
+    try:
+        cli = os.path.join(HERE, "pomfret_amd", "pomfret-amd")
+        cmd = [cli, "methphase", "-u", "-t", str(threads), "-o", prefix + ".cli", "--vcf", g["vcf"], g["bam"]]
+        t0 = time.perf_counter()
+        p = subprocess.run(cmd, capture_output=True, text=True)
+        t1 = time.perf_counter()
+        if p.returncode != 0:
+            raise RuntimeError(f"pomfret-amd failed ({p.returncode}): {p.stderr[-2000:]}")
+        outs["cli"] = take(prefix + ".cli")
+        log(f"[bench] e2e_u: cli {t1 - t0:.2f}s")
+        t0d = time.perf_counter()
+        r = methphase_files(g["bam"], g["vcf"], prefix + ".drv", None, lcfg, ctx=ctx, untagged=True, threads=threads)
+        t1d = time.perf_counter()
+        outs["driver"] = take(prefix + ".drv")
+        dec = r["decision"]
+        res["windows"] = int(dec.shape[0])
+        res["decisions"] = {"cis": int((dec == 0).sum()), "trans": int((dec == 1).sum()),
+                            "none": int((dec < 0).sum())}
+        res["raw_tags"] = len(r["raw_hp"])
+        log(f"[bench] e2e_u: driver {t1d - t0d:.2f}s, {res['windows']} windows")
+        res["cli"] = {"s": round(t1 - t0, 2), "records_per_s": round(res["records"] / (t1 - t0), 1),
+                      "what": " ".join(["pomfret-amd", "methphase", "-u", "-t", str(threads), "-o", "P",
+                                        "--vcf", "V", "B"])}
+        res["driver"] = {"s": round(t1d - t0d, 2), "records_per_s": round(res["records"] / (t1d - t0d), 1),
+                         "what": "methphase_files in this process, warm context"}
+        # K4 on the largest contig (the -u pre-pass's kernel, warm)
+        name = max(spec.contigs, key=lambda c: c[1])[0]
+        kv = vcf_known_vars(g["vcf"], name)
+        with BamFile(g["bam"]) as b:
+            b.haptag_device(ctx, name, kv)
+            t0k = time.perf_counter()
+            hp, qn, info = b.haptag_device(ctx, name, kv)
+            t1k = time.perf_counter()
+            kt = ctx.kernel_times()
+            kname = next((k for k in kt if k.startswith("pf_k4")), None)
+            reads, _, _ = b.fetch_contig_reads(name)
+        kms = kt.get(kname, float("nan"))
+        ab = k4_bytes(kv, reads)
+        res["k4"] = {"kernel": kname, "contig": name, "reads": int(reads.n_reads), "known": int(len(kv.pos)),
+                     "ms": round(kms, 4), "reads_per_s": round(reads.n_reads / (kms * 1e-3), 1),
+                     "algo_bytes": ab, "GBps": round(ab / (kms * 1e-3) / 1e9, 2),
+                     "prepass_ms": round((t1k - t0k) * 1e3, 1), "inflate_ms": round(info["ms_inflate"], 2),
+                     "inflated_bytes": int(info["inflated_bytes"])}
+        log(f"[bench] e2e_u: k4 {json.dumps(res['k4'])}")
+        if cpu:
+            from _oracle_pipeline import methphase_files_port
+            rp, ph = methphase_files_port(g["bam"], g["vcf"], prefix + ".port", None, lcfg, untagged=True,
+                                          threads=threads)
+            outs["cpu_port"] = take(prefix + ".port")
+            res["cpu_port"] = {"s": round(ph["total_s"], 2), "records_per_s": round(res["records"] / ph["total_s"], 1),
+                               "phases_s": {k: round(v, 2) for k, v in ph.items() if k != "total_s"},
+                               "what": f"host reader + serial host coverage pass + oracle jobs, {threads} threads"}
+            res["vs_cpu_port"] = round(ph["total_s"] / (t1 - t0), 2)
+        res["outputs_identical"] = all(o == outs["cli"] for o in outs.values())
+        res["compared"] = sorted(outs)
+    finally:
+        for f in (g["bam"], g["bam"] + ".bai", g["vcf"]):
+            if os.path.exists(f):
+                os.unlink(f)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -282,6 +397,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e-windows", type=int, default=64,
                     help="windows of the end-to-end (BAM file -> decisions) leg; 0 skips it")
+    ap.add_argument("--e2e-u-scale", type=float, default=1.0,
+                    help="genome scale of the configs[3]-shaped -u leg (1.0: 96 Mb, ~1,000 windows); 0 skips it")
     ap.add_argument("--calls-level", action="store_true",
                     help="time the calls-level boundary (reads + 5mC calls resident, no K0)")
     args = ap.parse_args()
@@ -490,6 +607,16 @@ def main():
                       os.environ.get("TMPDIR", "/tmp"), cpu=not args.no_cpu)
         log(f"[bench] e2e: {json.dumps(e2e)}")
 
+    e2e_u = None
+    if rank == 0 and world == 1 and not args.no_legs and args.e2e_u_scale > 0:
+        threads = args.cpu_threads or min(CPU_SHARE, len(os.sched_getaffinity(0)))
+        e2e_u = e2e_u_leg(ctx, lcfg, threads, os.environ.get("TMPDIR", "/tmp"), scale=args.e2e_u_scale,
+                          cpu=not args.no_cpu)
+        log(f"[bench] e2e_u: {json.dumps(e2e_u)}")
+        if e2e_u.get("k4"):
+            kernels[e2e_u["k4"]["kernel"]] = {"ms": e2e_u["k4"]["ms"], "algo_bytes": e2e_u["k4"]["algo_bytes"],
+                                              "GBps": e2e_u["k4"]["GBps"], "leg": "e2e_u (largest contig)"}
+
     par = f"windows dealt over dp{world}" + (" (weak: per-rank batches)" if args.weak else " (strong: one job)")
     res = {
         "metric": "aligned reads/sec (methphase kernel)",
@@ -529,6 +656,7 @@ def main():
         "vs_cpu_t32_estimate": round(value / cpu["t32_linear_estimate"], 2) if cpu else None,
         "pcie_inclusive": pcie,
         "e2e": e2e,
+        "e2e_u": e2e_u,
         "calls_level": calls_leg,
         "decisions": {"cis": int((out.decision == 0).sum()), "trans": int((out.decision == 1).sum()),
                       "none": int((out.decision < 0).sum())},

@@ -135,7 +135,24 @@ def make_aln_window(spec: AlnSpec, w: int):
     hp[only_right] = truth[only_right] ^ orient
     hp[rng.random(n) < spec.untag_frac] = HAPTAG_UNPHASED
     strand = (rng.random(n) < 0.5).astype(np.int64)
-    rs0 = starts - span_lo                                  # ref-relative read start
+    out, flag, mapq, de = _build_reads(spec, rng, ref, starts - span_lo, lens, truth, strand,
+                                       site_of, site_p, site_asm, site_hap, snv)
+    res = dict(s=s, e=e, orient=orient, pos=starts, flag=flag, mapq=mapq, de=de, hp=hp, recs=out)
+    if snv is not None:
+        res["snv"] = dict(pos=snv["pos"] + span_lo, ref=snv["ref"], alt=snv["alt"], h_alt=snv["h_alt"])
+    return res
+
+
+
+def _build_reads(spec: AlnSpec, rng, ref: np.ndarray, rs0: np.ndarray, lens: np.ndarray, truth: np.ndarray,
+                 strand: np.ndarray, site_of: np.ndarray, site_p: np.ndarray, site_asm: np.ndarray,
+                 site_hap: np.ndarray, snv):
+    """BAM records of reads at ref-relative starts rs0 with reference spans
+    lens: CIGAR with indel events and soft clips, 4-bit SEQ (the reference,
+    the read's het SNV alleles, substitutions), MD:Z when snv is given, and
+    the MM/ML pair of the read's CpG calls; then flag / MAPQ / de with the
+    filter failures.  -> (records, flag, mapq, de)."""
+    n = rs0.shape[0]
 
     # indel events, non-overlapping, strictly inside each read
     n_ev = rng.poisson(spec.indel_rate * lens)
@@ -293,11 +310,7 @@ def make_aln_window(spec: AlnSpec, w: int):
         mapq[bad[kind == 2]] = 5
         de[bad[kind == 3]] = 0.2
         flag[bad[kind == 4]] |= np.uint16(4)
-    res = dict(s=s, e=e, orient=orient, pos=starts, flag=flag, mapq=mapq, de=de, hp=hp, recs=out)
-    if snv is not None:
-        res["snv"] = dict(pos=snv["pos"] + span_lo, ref=snv["ref"], alt=snv["alt"], h_alt=snv["h_alt"])
-    return res
-
+    return out, flag, mapq, de
 
 def _plant_snvs(spec: AlnSpec, w: int, ref: np.ndarray, cpg: np.ndarray, span_lo: int, s: int, e: int):
     """Het SNVs for the -u path (a separate stream: the records of a spec
@@ -332,27 +345,36 @@ _ACGT = "ACGT"
 
 def _md_string(core: np.ndarray, ref: np.ndarray, rs0: int, ops: np.ndarray, lens: np.ndarray) -> str:
     """SAM MD:Z of an alignment whose query (without the leading clip) is
-    `core` against `ref` from ref index rs0, ops M/I/D only."""
-    parts, run, q, rc = [], 0, 0, int(rs0)
-    for op, ln in zip(ops.tolist(), lens.tolist()):
-        if op == 0:
-            mis = np.flatnonzero(core[q:q + ln] != ref[rc:rc + ln])
-            last = 0
-            for m in mis.tolist():
-                parts.append(str(run + m - last))
-                parts.append(_ACGT[int(ref[rc + m])])
-                run, last = 0, m + 1
-            run += ln - last
-            q += ln
-            rc += ln
-        elif op == 1:
-            q += ln
-        elif op == 2:
-            parts.append(str(run))
-            parts.append("^" + "".join(_ACGT[int(b)] for b in ref[rc:rc + ln]))
-            run = 0
-            rc += ln
-    parts.append(str(run))
+    `core` against `ref` from ref index rs0, ops M/I/D only: the matched
+    reference bases between consecutive events (a mismatching M base, a
+    deletion), each event as its reference base or ^ + the deleted bases."""
+    ops = np.asarray(ops, np.int64)
+    lens = np.asarray(lens, np.int64)
+    qlen = np.where(ops == 2, 0, lens)
+    rlen = np.where(ops == 1, 0, lens)
+    q0 = np.concatenate([[0], np.cumsum(qlen)[:-1]])
+    r0 = int(rs0) + np.concatenate([[0], np.cumsum(rlen)[:-1]])
+    m = ops == 0
+    ml = lens[m]
+    base = np.concatenate([[0], np.cumsum(ml)[:-1]])
+    step = np.arange(int(ml.sum()), dtype=np.int64)
+    qi = np.repeat(q0[m] - base, ml) + step
+    ri = np.repeat(r0[m] - base, ml) + step
+    mpos = ri[core[qi] != ref[ri]]
+    d = ops == 2
+    epos = np.concatenate([mpos, r0[d]])
+    elen = np.concatenate([np.zeros(mpos.shape[0], np.int64), lens[d]])
+    o = np.argsort(epos, kind="stable")
+    parts, cur = [], int(rs0)
+    for p, ln in zip(epos[o].tolist(), elen[o].tolist()):
+        parts.append(str(p - cur))
+        if ln == 0:
+            parts.append(_ACGT[int(ref[p])])
+            cur = p + 1
+        else:
+            parts.append("^" + "".join(_ACGT[int(b)] for b in ref[p:p + ln]))
+            cur = p + ln
+    parts.append(str(int(rs0) + int(rlen.sum()) - cur))
     return "".join(parts)
 
 

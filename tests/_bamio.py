@@ -183,60 +183,46 @@ class _BgzfPar:
         return (int(self.addr[tok >> 16]) << 16) | (tok & 0xFFFF)
 
 
-def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, text: str = "@HD\tVN:1.6\tSO:coordinate\n",
-              workers: int = 0, level: int = 6):
-    """refs: [(name, length)]; recs sorted by (tid, pos) with unplaced reads
-    (tid -1) last.  Writes path and path + '.bai' (or bai_path).  workers > 1
-    compresses the blocks in a process pool (same bytes as the serial writer
-    at the same level)."""
-    z = _BgzfPar(level, workers) if workers > 1 else _Bgzf()
+def bam_header(refs, text: str = "@HD\tVN:1.6\tSO:coordinate\n") -> bytes:
     hdr = b"BAM\1" + struct.pack("<i", len(text)) + text.encode() + struct.pack("<i", len(refs))
     for name, ln in refs:
         nb = name.encode() + b"\0"
         hdr += struct.pack("<i", len(nb)) + nb + struct.pack("<i", ln)
-    z.write(hdr)
-    z.flush()                                  # bam_hdr_write flushes the header block
-    nref = len(refs)
+    return hdr
+
+
+def bai_bytes(nref: int, entries) -> bytes:
+    """The BAI of records given in file order as (tid, pos, end, flag, u, v)
+    (virtual offsets of each record's start and end; tid < 0: unplaced), the
+    way htslib's indexer builds it: bins with contiguous chunks merged, the
+    16 kb linear index with gaps filled by the previous offset, the metadata
+    pseudo-bin, n_no_coor."""
     bins = [dict() for _ in range(nref)]       # bin -> [[u, v], ...]
     lin = [dict() for _ in range(nref)]
     meta = [[None, None, 0, 0] for _ in range(nref)]
     last_bin = [None] * nref
     n_no_coor = 0
-    for r in recs:
-        u = z.tell()
-        z.write(encode_record(r))
-        v = z.tell()
-        if r.tid < 0:
+    for t, pos, end, flag, u, v in entries:
+        if t < 0:
             n_no_coor += 1
             continue
-        t = r.tid
-        end = endpos(r.pos, r.cigar, r.flag)
-        b = reg2bin(r.pos, end)
+        b = reg2bin(pos, end)
         ch = bins[t].setdefault(b, [])
         if last_bin[t] == b and ch and ch[-1][1] == u:
             ch[-1][1] = v                      # contiguous records of one bin: one chunk
         else:
             ch.append([u, v])
         last_bin[t] = b
-        for wdw in range(r.pos >> 14, ((end - 1) >> 14) + 1):
+        for wdw in range(pos >> 14, ((end - 1) >> 14) + 1):
             lin[t].setdefault(wdw, u)
         m = meta[t]
         if m[0] is None:
             m[0] = u
         m[1] = v
-        if r.flag & 4:
+        if flag & 4:
             m[3] += 1
         else:
             m[2] += 1
-    data = z.close()
-    if workers > 1:                            # tokens -> virtual offsets
-        tr = z.translate
-        bins = [{b: [[tr(u), tr(v)] for u, v in ch] for b, ch in d.items()} for d in bins]
-        lin = [{w: tr(u) for w, u in d.items()} for d in lin]
-        meta = [[tr(m[0]) if m[0] is not None else None, tr(m[1]) if m[1] is not None else None, m[2], m[3]]
-                for m in meta]
-    with open(path, "wb") as f:
-        f.write(data)
     idx = bytearray(b"BAI\1" + struct.pack("<i", nref))
     for t in range(nref):
         bl = sorted(bins[t].items())
@@ -256,8 +242,33 @@ def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, 
             idx += struct.pack("<Q", val)
             prev = val
     idx += struct.pack("<Q", n_no_coor)
+    return bytes(idx)
+
+
+def write_bam(path: str, refs, recs: List[Rec], bai_path: Optional[str] = None, text: str = "@HD\tVN:1.6\tSO:coordinate\n",
+              workers: int = 0, level: int = 6):
+    """refs: [(name, length)]; recs sorted by (tid, pos) with unplaced reads
+    (tid -1) last.  Writes path and path + '.bai' (or bai_path).  workers > 1
+    compresses the blocks in a process pool (same bytes as the serial writer
+    at the same level)."""
+    z = _BgzfPar(level, workers) if workers > 1 else _Bgzf()
+    z.write(bam_header(refs, text))
+    z.flush()                                  # bam_hdr_write flushes the header block
+    entries = []
+    for r in recs:
+        u = z.tell()
+        z.write(encode_record(r))
+        v = z.tell()
+        end = endpos(r.pos, r.cigar, r.flag) if r.tid >= 0 else 0
+        entries.append((r.tid, r.pos, end, r.flag, u, v))
+    data = z.close()
+    if workers > 1:                            # tokens -> virtual offsets
+        tr = z.translate
+        entries = [(t, p, e, f, tr(u), tr(v)) for t, p, e, f, u, v in entries]
+    with open(path, "wb") as f:
+        f.write(data)
     with open(bai_path or path + ".bai", "wb") as f:
-        f.write(bytes(idx))
+        f.write(bai_bytes(len(refs), entries))
 
 
 def records_from_aln(aln, tid: int = 0, prefix: str = "r", hp_zero_every: int = 0, de_absent_every: int = 0,

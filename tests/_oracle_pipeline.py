@@ -98,10 +98,11 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
                 gtf=ep.gtf_text(contigs, blocks), tsv=ep.tsv_text(contigs, blocks), vcf=vcf, counts=counts)
 
 
-def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4):
+def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4, fetch_threads=1):
     """runner(plan, kind, j) for pomfret_amd.pipeline.methphase_files_dist /
     the Plan steps: a job's result computed by the oracle instead of the
-    device (CPU tests of the product's plan / shard / merge / write)."""
+    device (CPU tests of the product's plan / shard / merge / write).
+    fetch_threads: host reader threads per window job."""
     import oracle
     from pomfret_amd import LoadConfig
     from pomfret_amd.bam import BamFile, vcf_known_vars
@@ -136,7 +137,7 @@ def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4):
             if bam.tid(info["contig_name"]) < 0:
                 return dict(decision=np.full(n, -1, np.int8), tag_off=np.zeros(n + 1, np.uint64),
                             off=np.zeros(1, np.uint64), names=np.zeros(0, np.uint8), hp=np.zeros(0, np.uint8))
-            aln, qn, _ = bam.fetch_windows(info["contig_name"], ws[w0:w1], we[w0:w1])
+            aln, qn, _ = bam.fetch_windows(info["contig_name"], ws[w0:w1], we[w0:w1], threads=fetch_threads)
         if plan.opts.untagged:
             raw = plan.raw_hp()
             aln.hp = np.array([raw.get(q, 254) for q in qn], np.uint8)
@@ -157,6 +158,49 @@ def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4):
         return dict(decision=res.decision.astype(np.int8), tag_off=np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint64),
                     off=off, names=nb, hp=np.array(hp, np.uint8))
     return run
+
+
+def methphase_files_port(bam_path, vcf_path, out_prefix, cfg, lcfg=None, untagged=False, threads=16,
+                         tsv=False, job_windows=0):
+    """The CPU port of the whole `pomfret methphase` driver -- the bench's CPU
+    side of the file-to-output legs, and a CPU check of the product's
+    planner / merge / writers.  The product's C plan and writers run with
+    --host-fetch semantics (the serial host coverage pass of
+    estimate_read_coverage_dirtyfast when cfg is None, blockjoin.c:951-1040;
+    the host BAM reader), and every job is computed by the oracle: the -u
+    pre-pass one contig per thread (the reference runs it serially while
+    loading the VCF, 2069-2080), then the window jobs in order, each fetched
+    with `threads` reader threads and run on `threads` oracle threads over
+    windows (the reference's kt_for runs contigs, 4560).  Writes the same
+    outputs as methphase_files.  -> (result dict, seconds per phase)."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+    from pomfret_amd.pipeline import JOB_HAPTAG, JOB_WINDOWS, MODE_METHPHASE, Plan, _result, make_opts
+
+    t0 = time.perf_counter()
+    o = make_opts(bam_path, vcf_path, out_prefix, cfg, lcfg, untagged=untagged, tsv=tsv, threads=threads,
+                  job_windows=job_windows, host_fetch=True)
+    plan = Plan(o)
+    t1 = time.perf_counter()
+    run = oracle_job_runner(bam_path, vcf_path, lcfg, n_threads=threads, fetch_threads=threads)
+    try:
+        if untagged:
+            nj = plan.n_jobs(JOB_HAPTAG)
+            with ThreadPoolExecutor(max(1, min(threads, nj))) as ex:
+                res = list(ex.map(lambda j: run(plan, JOB_HAPTAG, j), range(nj)))
+            for j, r in enumerate(res):
+                plan.set_result(JOB_HAPTAG, j, r)
+            plan.merge_raw()
+        t2 = time.perf_counter()
+        for j in range(plan.n_jobs(JOB_WINDOWS)):
+            plan.set_result(JOB_WINDOWS, j, run(plan, JOB_WINDOWS, j))
+        t3 = time.perf_counter()
+        plan.finish()
+        out = _result(plan, MODE_METHPHASE)
+        t4 = time.perf_counter()
+    finally:
+        plan.close()
+    return out, dict(plan_s=t1 - t0, haptag_s=t2 - t1, windows_s=t3 - t2, finish_s=t4 - t3, total_s=t4 - t0)
 
 
 def report_oracle(bam_path, vcf_path, cov, chunk_size, chunk_stride, lcfg=None, k=3, k_span=5000):

@@ -353,7 +353,7 @@ def _py_rescue(recs, known_pos, dropped, meth, raw=None):
         if not poss:
             continue
         pb = [(p << 33) for p in poss]
-        for j in expected_fetch(recs, 0, start, end - 0, 0):
+        for j in expected_fetch(recs, recs[0].tid if recs else 0, start, end - 0, 0):
             r = recs[j]
             hm = meth.get(r.qname)
             if hm is None:

@@ -13,7 +13,11 @@ driver, against the oracle pipeline (tests/_oracle_pipeline.py):
   * `report` with the per-contig estimate read by VCF contig index
     (covs[i_ref], 5046) and with -c;
   * two contexts of one device (the multi-GPU work queue, pf_pipeline.c
-    run_on_devices) byte-identical to one.
+    run_on_devices) byte-identical to one;
+  * BASELINE configs[3]'s shape at small scale (tests/_genome): -u without -c
+    on a genome whose windows share reads, with merged gaps whose dropped
+    intervals go through the rescue, against the oracle pipeline and against
+    the CPU port of the driver (the bench's e2e_u comparison).
 """
 import numpy as np
 import pytest
@@ -171,3 +175,36 @@ def test_untagged_prepass_in_pieces(oracle_lib, gpu_ctx, tmp_path, mc_untagged, 
     assert info_p["attempts"] > info_1["attempts"]                 # several pieces ran
     prim = [r for r in recs_by["chrC"] if not (r.flag & (4 | 256 | 2048))]
     assert qn_1 == [r.qname for r in prim]
+
+
+@pytest.fixture(scope="module")
+def genome_small(tmp_path_factory):
+    from tests import _genome
+    d = tmp_path_factory.mktemp("gen")
+    return _genome.write_genome(str(d / "g"), _genome.small_spec(), workers=4, keep_recs=True)
+
+
+@pytest.mark.parametrize("job_windows", [0, 3], ids=["default_jobs", "jobs3"])
+def test_genome_untagged_estimate(oracle_lib, gpu_ctx, tmp_path, genome_small, job_windows):
+    """`methphase -u` without -c on a 4-contig genome (reads uniform over
+    each contig, adjacent windows sharing reads, short blocks merged away):
+    decisions, the -u raw table, the merged first-wins table and the
+    GTF/TSV/VCF bytes (dropped-interval rescue included) equal the oracle
+    pipeline's; the CPU port of the driver writes the same bytes."""
+    from pomfret_amd.pipeline import methphase_files
+    from tests._oracle_pipeline import methphase_files_port
+    g = genome_small
+    out = str(tmp_path / "o")
+    res = methphase_files(g["bam"], g["vcf"], out, None, ctx=gpu_ctx, untagged=True, tsv=True,
+                          job_windows=job_windows)
+    ref = methphase_files_oracle(g["bam"], g["vcf"], None, untagged=True, recs_by_contig=g["recs_by_contig"])
+    assert np.array_equal(res["decision"], ref["decision"])
+    assert res["raw_hp"] == ref["raw_hp"] and len(ref["raw_hp"]) > 1000
+    assert list(res["qname_hp"].items()) == list(ref["qname_hp"].items())
+    assert _outputs(out) == (ref["gtf"], ref["tsv"], ref["vcf"])
+    dec = ref["decision"]
+    assert (dec >= 0).sum() >= 5 and len(dec) >= 15
+    assert ref["counts"][1] > 0                                  # rescued dropped-interval variants
+    port, _ = methphase_files_port(g["bam"], g["vcf"], str(tmp_path / "p"), None, untagged=True, threads=4,
+                                   tsv=True)
+    assert _outputs(str(tmp_path / "p")) == _outputs(out)

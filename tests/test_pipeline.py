@@ -129,3 +129,23 @@ def test_cli_parses_and_fails_loudly_without_a_device(tmp_path):
                        capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 1 and "failed" in r.stderr
     assert not os.path.exists(str(tmp_path / "o") + ".mp.gtf")
+
+
+def test_genome_port_matches_oracle(oracle_lib, tmp_path):
+    """BASELINE configs[3]'s shape at small scale (tests/_genome: 4 contigs,
+    windows sharing reads, merged gaps): the CPU port of the driver (the
+    bench's e2e_u CPU side: the product's plan / merge / writers, the serial
+    host coverage pass, oracle jobs on a thread pool) equals the oracle
+    pipeline, dropped-interval rescue included."""
+    from tests import _genome
+    from tests._oracle_pipeline import methphase_files_port
+    g = _genome.write_genome(str(tmp_path / "g"), _genome.small_spec(seed=9), workers=4, keep_recs=True)
+    out = str(tmp_path / "p")
+    res, ph = methphase_files_port(g["bam"], g["vcf"], out, None, untagged=True, threads=4, tsv=True)
+    ref = methphase_files_oracle(g["bam"], g["vcf"], None, untagged=True, recs_by_contig=g["recs_by_contig"])
+    assert np.array_equal(res["decision"], ref["decision"]) and (ref["decision"] >= 0).sum() >= 5
+    assert res["raw_hp"] == ref["raw_hp"] and list(res["qname_hp"].items()) == list(ref["qname_hp"].items())
+    assert open(out + ".mp.gtf").read() == ref["gtf"]
+    assert open(out + ".mp.tsv").read() == ref["tsv"]
+    assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+    assert ref["counts"][1] > 0 and set(ph) >= {"plan_s", "haptag_s", "windows_s", "total_s"}
