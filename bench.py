@@ -345,7 +345,7 @@ def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bo
                       "what": " ".join(["pomfret-amd", "methphase", "-u", "-t", str(threads), "-o", "P",
                                         "--vcf", "V", "B"])}
         res["driver"] = {"s": round(t1d - t0d, 2), "records_per_s": round(res["records"] / (t1d - t0d), 1),
-                         "what": "methphase_files in this process, warm context"}
+                         "phases": r["stats"], "what": "methphase_files in this process, warm context"}
         # K4 on the largest contig (the -u pre-pass's kernel, warm)
         name = max(spec.contigs, key=lambda c: c[1])[0]
         kv = vcf_known_vars(g["vcf"], name)

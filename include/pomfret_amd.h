@@ -537,6 +537,17 @@ typedef struct pf_rescue_map {
 int  pf_rescue_dropped(pf_bam_t *bam, const char *chrom, uint32_t n_drop, const uint32_t *drop_start,
                        const uint32_t *drop_end, const pf_known_vars_t *known, const pf_qname_tags_t *methphased,
                        const pf_qname_tags_t *raw, pf_rescue_map_t **out);
+/* the same with the intervals spread over `threads` host threads (each with
+ * its own file handle); the result is the serial pass's */
+int  pf_rescue_dropped_mt(pf_bam_t *bam, const char *chrom, uint32_t n_drop, const uint32_t *drop_start,
+                          const uint32_t *drop_end, const pf_known_vars_t *known, const pf_qname_tags_t *methphased,
+                          const pf_qname_tags_t *raw, int threads, pf_rescue_map_t **out);
+/* several contigs at once (the qname tables built once, every (contig,
+ * interval) one work item); out[c] per contig, each the serial pass's */
+int  pf_rescue_dropped_multi(pf_bam_t *bam, uint32_t n_contigs, const char *const *chroms, const uint32_t *n_drop,
+                             const uint32_t *const *drop_start, const uint32_t *const *drop_end,
+                             const pf_known_vars_t *const *known, const pf_qname_tags_t *methphased,
+                             const pf_qname_tags_t *raw, int threads, pf_rescue_map_t **out);
 void pf_rescue_map_free(pf_rescue_map_t *map);
 
 /* -u known variants of one contig: insert_variant_from_vcf_line (1432-1543)
@@ -681,6 +692,21 @@ const pf_tags_t   *pf_mp_qname_hp(const pf_mp_plan_t *p);
 const pf_tags_t   *pf_mp_raw_hp(const pf_mp_plan_t *p);     /* NULL without -u */
 /* report: {correct, switch, fail} */
 int  pf_mp_report_counts(const pf_mp_plan_t *p, double *counts3);
+/* measurement hook: wall seconds per phase of the run and the device-fetch
+ * sums (pf_bam_dev_fetch_t's ms_* and byte counts) of its jobs; index 0 =
+ * window jobs, 1 = -u pre-pass jobs */
+typedef struct pf_mp_stats {
+    double s_plan;              /* VCF gaps, coverage estimate, job plan      */
+    double s_estimate;          /* the coverage pass (inside s_plan)          */
+    double s_haptag;            /* -u pre-pass jobs + the merge of their tables */
+    double s_windows;           /* window jobs                                 */
+    double s_finish;            /* first-wins merge, phase blocks, writers    */
+    double fetch_ms[2][7];      /* read, inflate, chain, decode, select, build, total */
+    uint64_t comp_bytes[2], inflated_bytes[2];
+    double run_ms[2];           /* pf_methphase_run / K4 wall, summed over jobs */
+    uint64_t n_fetch[2];        /* device fetches */
+} pf_mp_stats_t;
+int  pf_mp_stats(const pf_mp_plan_t *p, pf_mp_stats_t *s);
 
 /* ------------------------------------------------------------------ */
 /* BAM output: --write-bam and varhaptag.                               */

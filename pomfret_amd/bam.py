@@ -86,6 +86,9 @@ def _bind():
     L.pf_rescue_dropped.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                     C.POINTER(PfKnownVars), C.POINTER(PfQnameTags), C.POINTER(PfQnameTags),
                                     C.POINTER(C.POINTER(PfRescueMap))]
+    L.pf_rescue_dropped_mt.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                       C.POINTER(PfKnownVars), C.POINTER(PfQnameTags), C.POINTER(PfQnameTags),
+                                       C.c_int, C.POINTER(C.POINTER(PfRescueMap))]
     L.pf_rescue_map_free.argtypes = [C.POINTER(PfRescueMap)]
     L.pf_bam_estimate_coverage.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     L.pf_bam_estimate_coverage_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64]
@@ -347,9 +350,10 @@ def _qname_tags(table: Dict[str, int]):
 
 
 def rescue_dropped(bam: BamFile, contig: str, dropped, known: KnownVars, methphased: Dict[str, int],
-                   raw: Optional[Dict[str, int]] = None) -> Dict[int, int]:
-    """pf_rescue_dropped: {0-based pos: hap_of_ref} of one contig's dropped
-    intervals [(s, e), ...] for the VCF writer (Blocks.write_vcf rescue)."""
+                   raw: Optional[Dict[str, int]] = None, threads: int = 1) -> Dict[int, int]:
+    """pf_rescue_dropped(_mt): {0-based pos: hap_of_ref} of one contig's
+    dropped intervals [(s, e), ...] for the VCF writer (Blocks.write_vcf
+    rescue); threads > 1 spreads the intervals over host threads."""
     L = _bind()
     ds = np.ascontiguousarray([a for a, _ in dropped] or [0], np.uint32)
     de = np.ascontiguousarray([b for _, b in dropped] or [0], np.uint32)
@@ -357,9 +361,9 @@ def rescue_dropped(bam: BamFile, contig: str, dropped, known: KnownVars, methpha
     tr, kr = _qname_tags(raw) if raw is not None else (None, None)
     kc = known.to_c()
     out = C.POINTER(PfRescueMap)()
-    _check(L.pf_rescue_dropped(bam.handle, contig.encode(), len(dropped), ds.ctypes.data, de.ctypes.data,
-                               C.byref(kc), C.byref(tm), C.byref(tr) if tr is not None else None, C.byref(out)),
-           "pf_rescue_dropped")
+    _check(L.pf_rescue_dropped_mt(bam.handle, contig.encode(), len(dropped), ds.ctypes.data, de.ctypes.data,
+                                  C.byref(kc), C.byref(tm), C.byref(tr) if tr is not None else None, int(threads),
+                                  C.byref(out)), "pf_rescue_dropped_mt")
     try:
         m = out.contents
         n = int(m.n)

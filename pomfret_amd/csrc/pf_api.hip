@@ -58,6 +58,8 @@ struct pf_ctx {
     size_t pin_cap = 0;
     void *stage = nullptr;    /* pinned staging of the device fetch's compressed bytes */
     size_t stage_cap = 0;
+    void *dws = nullptr;      /* device workspace of the inflate's first pass (tokens, tables) */
+    size_t dws_cap = 0;
     uint32_t k3_lds_set = 0;  /* dynamic LDS limits set on the greedy kernels of this device */
     uint32_t k3_lds_fb_set = 0;
     uint32_t k3w_lds_set = 0;
@@ -215,6 +217,22 @@ extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n) {
     return static_cast<uint8_t *>(c->stage);
 }
 
+// the context's device workspace of at least n bytes (grown on demand, kept:
+// one fetch runs on a context at a time)
+extern "C" uint8_t *pf_ctx_devws(pf_ctx *c, size_t n) {
+    if (c->dws_cap < n) {
+        if (c->dws) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->dws); }
+        c->dws = nullptr;
+        c->dws_cap = 0;
+        void *p = nullptr;
+        const size_t cap = n + n / 8;
+        if (hipMalloc(&p, cap) != hipSuccess) return nullptr;
+        c->dws = p;
+        c->dws_cap = cap;
+    }
+    return static_cast<uint8_t *>(c->dws);
+}
+
 // release the staging buffer when it grew past `keep` bytes
 extern "C" void pf_ctx_stage_trim(pf_ctx *c, size_t keep) {
     if (c->stage && c->stage_cap > keep) {
@@ -233,6 +251,7 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     (void)hipStreamDestroy(c->stream);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
+    if (c->dws) (void)hipFree(c->dws);
     delete c;
 }
 

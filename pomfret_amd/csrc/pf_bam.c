@@ -25,6 +25,7 @@
  * bam_tag2cigar does.
  */
 #include <pthread.h>
+#include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -1165,115 +1166,247 @@ void pf_rescue_map_free(pf_rescue_map_t *m) {
     free(o);
 }
 
+/* the rescue's dropped intervals of one contig: its known positions per
+ * interval (pushed before the reads' variants, 2653-2663) and, per interval,
+ * (rp << 8 | hap) in vote order */
+typedef struct {
+    int32_t tid;
+    uint32_t n_drop;
+    const uint32_t *drop_start, *drop_end;
+    uint64_t *kpos_off;               /* [n_drop + 1] into kpos */
+    u64v_t kpos;                      /* known positions as pos << 33 */
+    u64v_t *per;                      /* [n_drop] */
+} rescue_ctg_t;
+
+typedef struct {
+    const pf_bam_t *b;
+    const qtab_t *qm, *qr;
+    rescue_ctg_t *ctg;
+    const uint64_t *item_off;         /* [n_ctg + 1]: intervals of the contigs before */
+    uint32_t n_ctg;
+    uint64_t n_items;
+    atomic_uint_fast64_t *next;
+    int rc;
+} rescue_job_t;
+
+static int rescue_one(rescue_job_t *J, fetcher_t *F, const rescue_ctg_t *R, uint32_t k, u64v_t *pb) {
+    const uint32_t start = R->drop_start[k] - 1u, end = R->drop_end[k] + 1u;
+    pb->n = 0;
+    int rc = 0;
+    for (uint64_t i = R->kpos_off[k]; i < R->kpos_off[k + 1] && !rc; i++) rc = u64_push(pb, R->kpos.a[i]);
+    if (rc) return rc;
+    /* "%s:%d-%d" of (start, end): htslib's 0-based [start-1, end) */
+    const int64_t b1 = (int32_t)start, e1 = (int32_t)end;
+    const int64_t beg = b1 > 0 ? b1 - 1 : 0;
+    recbuf_t rb;
+    memset(&rb, 0, sizeof rb);
+    if (R->tid >= 0 && R->tid < J->b->n_ref_idx) {
+        F->tid = R->tid;
+        rc = fetch_region(F, beg, e1, &rb);
+    }
+    {                                                              /* closing offsets */
+        const uint64_t vq = rb.f[F_QN].n, vc = rb.f[F_CIG].n / 4, vm = rb.f[F_MM].n;
+        if (!rc) rc = vb_put(&rb.f[F_QNOFF], &vq, 8);
+        if (!rc) rc = vb_put(&rb.f[F_CIGOFF], &vc, 8);
+        if (!rc) rc = vb_put(&rb.f[F_MMOFF], &vm, 8);
+    }
+    const size_t nk = pb->n;
+    for (uint64_t r = 0; r < rb.n_recs && !rc; r++) {
+        const uint64_t *qo = (const uint64_t *)rb.f[F_QNOFF].p;
+        const char *qn = (const char *)rb.f[F_QN].p + qo[r];
+        const size_t ql = (size_t)(qo[r + 1] - qo[r]);
+        const int hm = qtab_get(J->qm, qn, ql);
+        if (hm < 0) continue;
+        int hr;
+        if (J->qr) { hr = qtab_get(J->qr, qn, ql); if (hr < 0) continue; }
+        else hr = ((const uint8_t *)rb.f[F_HP].p)[r];
+        if (hr == 254) continue;
+        if (!((const uint16_t *)rb.f[F_FLAG].p)[r]) { rc = PF_ERR_ARG; break; }   /* assert(tagd), 1596 */
+        const uint64_t *co = (const uint64_t *)rb.f[F_CIGOFF].p, *mo = (const uint64_t *)rb.f[F_MMOFF].p;
+        rc = read_var_positions(((const uint32_t *)rb.f[F_POS].p)[r],
+                                (const uint32_t *)rb.f[F_CIG].p + co[r], (uint32_t)(co[r + 1] - co[r]),
+                                (const char *)rb.f[F_MM].p + mo[r], (size_t)(mo[r + 1] - mo[r]),
+                                (uint32_t)hm & 0xFFu, pb);
+    }
+    rb_free(&rb);
+    if (rc || nk == 0) return rc;                                  /* pb.n == 0: goto done */
+    qsort(pb->a, pb->n, 8, cmp_u64);
+    /* for (i = 0; i < pb.n-1;): a known position sorted last is never visited */
+    u64v_t *o = &R->per[k];
+    for (size_t i = 0; i + 1 < pb->n && !rc;) {
+        if (pb->a[i] & (1ull << 32)) { i++; continue; }
+        const uint32_t rp = (uint32_t)(pb->a[i] >> 33);
+        uint32_t c[2] = {0, 0};
+        size_t j;
+        for (j = i + 1; j < pb->n; j++) {
+            if (!(pb->a[j] & (1ull << 32))) break;
+            if ((uint32_t)(pb->a[j] >> 33) != rp) break;
+            const uint32_t h = (uint32_t)pb->a[j] & 0xFFu;
+            if (h < 2) c[h]++;
+        }
+        const uint32_t hap = c[0] > c[1] ? 1u : c[1] > c[0] ? 0u : 254u;
+        rc = u64_push(o, ((uint64_t)rp << 8) | hap);
+        i = j;
+    }
+    return rc;
+}
+
+static void *rescue_main(void *arg) {
+    rescue_job_t *J = (rescue_job_t *)arg;
+    fetcher_t F;
+    memset(&F, 0, sizeof F);
+    F.b = J->b;
+    F.reads_mode = 2;
+    u64v_t pb = {0};
+    int rc = 0, open = 0;
+    for (;;) {
+        const uint64_t it = atomic_fetch_add(J->next, 1);
+        if (it >= J->n_items || rc) break;
+        uint32_t c = 0;
+        while (J->item_off[c + 1] <= it) c++;
+        const rescue_ctg_t *R = &J->ctg[c];
+        if (!open && R->tid >= 0 && R->tid < J->b->n_ref_idx) {
+            if ((rc = bgzf_open(&F.z, J->b->path))) break;
+            open = 1;
+        }
+        rc = rescue_one(J, &F, R, (uint32_t)(it - J->item_off[c]), &pb);
+    }
+    if (open) bgzf_close(&F.z);
+    free(F.rec);
+    free(F.chunks);
+    free(pb.a);
+    J->rc = rc;
+    return NULL;
+}
+
+/* recover_variant_phase_in_dropped_intervals (2475-2694) for several contigs
+ * at once: the qname tables are built once, every (contig, interval) is a
+ * work item taken by `threads` host threads (each with its own file handle),
+ * and each contig's results are then taken in interval order, so the last
+ * write per position is the serial pass's */
+int pf_rescue_dropped_multi(pf_bam_t *b, uint32_t n_ctg, const char *const *chroms, const uint32_t *n_drop,
+                            const uint32_t *const *drop_start, const uint32_t *const *drop_end,
+                            const pf_known_vars_t *const *known, const pf_qname_tags_t *methphased,
+                            const pf_qname_tags_t *raw, int threads, pf_rescue_map_t **out) {
+    if (!b || !b->path || !methphased || !out || (n_ctg && (!chroms || !n_drop || !drop_start || !drop_end || !known)))
+        return PF_ERR_ARG;
+    for (uint32_t c = 0; c < n_ctg; c++) {
+        out[c] = NULL;
+        if (!chroms[c] || !known[c] || (n_drop[c] && (!drop_start[c] || !drop_end[c]))) return PF_ERR_ARG;
+    }
+    qtab_t qm = {0}, qr = {0};
+    rescue_ctg_t *R = (rescue_ctg_t *)calloc(n_ctg ? n_ctg : 1, sizeof(rescue_ctg_t));
+    uint64_t *item_off = (uint64_t *)calloc((size_t)n_ctg + 1, sizeof(uint64_t));
+    int rc = (!R || !item_off) ? PF_ERR_NOMEM : 0;
+    if (!rc) rc = qtab_build(&qm, methphased);
+    if (!rc && raw) rc = qtab_build(&qr, raw);
+    for (uint32_t c = 0; c < n_ctg && !rc; c++) {
+        rescue_ctg_t *r = &R[c];
+        r->tid = pf_bam_tid(b, chroms[c]);
+        r->n_drop = n_drop[c];
+        r->drop_start = drop_start[c];
+        r->drop_end = drop_end[c];
+        r->kpos_off = (uint64_t *)calloc((size_t)r->n_drop + 1, sizeof(uint64_t));
+        r->per = (u64v_t *)calloc(r->n_drop ? r->n_drop : 1, sizeof(u64v_t));
+        if (!r->kpos_off || !r->per) { rc = PF_ERR_NOMEM; break; }
+        /* the known-position cursor runs across a contig's intervals in order (2653-2663) */
+        const pf_known_vars_t *kv = known[c];
+        uint32_t prev_i = 0;
+        for (uint32_t k = 0; k < r->n_drop && !rc; k++) {
+            const uint32_t start = r->drop_start[k] - 1u, end = r->drop_end[k] + 1u;
+            for (uint32_t i = prev_i; i < kv->n; i++) {
+                const uint32_t p = kv->pos[i];
+                if (p >= start && p < end && (rc = u64_push(&r->kpos, (uint64_t)p << 33))) break;
+                if (p >= end) { prev_i = i; break; }
+            }
+            r->kpos_off[k + 1] = r->kpos.n;
+        }
+        item_off[c + 1] = item_off[c] + r->n_drop;
+    }
+    const uint64_t n_items = n_ctg ? item_off[n_ctg] : 0;
+    if (!rc && n_items) {
+        int nt = threads > 0 ? threads : 1;
+        if ((uint64_t)nt > n_items) nt = (int)n_items;
+        atomic_uint_fast64_t next;
+        atomic_init(&next, 0);
+        rescue_job_t *J = (rescue_job_t *)calloc((size_t)nt, sizeof(rescue_job_t));
+        pthread_t *th = (pthread_t *)calloc((size_t)nt, sizeof(pthread_t));
+        char *made = (char *)calloc((size_t)nt, 1);
+        if (!J || !th || !made) rc = PF_ERR_NOMEM;
+        for (int t = 0; t < nt && !rc; t++)
+            J[t] = (rescue_job_t){b, &qm, raw ? &qr : NULL, R, item_off, n_ctg, n_items, &next, 0};
+        if (!rc) {
+            for (int t = 1; t < nt; t++) made[t] = pthread_create(&th[t], NULL, rescue_main, &J[t]) == 0;
+            rescue_main(&J[0]);
+            for (int t = 1; t < nt; t++) {
+                if (made[t]) pthread_join(th[t], NULL);
+                else rescue_main(&J[t]);
+            }
+            for (int t = 0; t < nt && !rc; t++) rc = J[t].rc;
+        }
+        free(J); free(th); free(made);
+    }
+    for (uint32_t c = 0; c < n_ctg && !rc; c++) {
+        /* in interval order: pos << 40 | sequence << 8 | hap; the sort keeps
+         * the last write per position (the hash's) */
+        const rescue_ctg_t *r = &R[c];
+        u64v_t res = {0};
+        uint64_t seq = 0;
+        for (uint32_t k = 0; k < r->n_drop && !rc; k++)
+            for (size_t i = 0; i < r->per[k].n && !rc; i++)
+                rc = u64_push(&res, ((r->per[k].a[i] >> 8) << 40) | (seq++ << 8) | (r->per[k].a[i] & 0xFFu));
+        struct pf_rescue_own *o = NULL;
+        if (!rc) {
+            qsort(res.a, res.n, 8, cmp_u64);
+            o = (struct pf_rescue_own *)calloc(1, sizeof *o);
+            if (o) { o->pos = (uint32_t *)malloc((res.n ? res.n : 1) * 4); o->hap = (uint8_t *)malloc(res.n ? res.n : 1); }
+            if (!o || !o->pos || !o->hap) rc = PF_ERR_NOMEM;
+            else {
+                uint32_t n = 0;
+                for (size_t i = 0; i < res.n; i++) {
+                    const uint32_t p = (uint32_t)(res.a[i] >> 40);
+                    if (i + 1 < res.n && (uint32_t)(res.a[i + 1] >> 40) == p) continue;
+                    o->pos[n] = p;
+                    o->hap[n] = (uint8_t)(res.a[i] & 0xFFu);
+                    n++;
+                }
+                o->pub.n = n;
+                o->pub.pos = o->pos;
+                o->pub.hap_of_ref = o->hap;
+                out[c] = &o->pub;
+            }
+        }
+        if (rc && o) pf_rescue_map_free(&o->pub);
+        free(res.a);
+    }
+    for (uint32_t c = 0; R && c < n_ctg; c++) {
+        for (uint32_t k = 0; R[c].per && k < R[c].n_drop; k++) free(R[c].per[k].a);
+        free(R[c].per);
+        free(R[c].kpos_off);
+        free(R[c].kpos.a);
+    }
+    free(R);
+    free(item_off);
+    free(qm.key_off);
+    free(qr.key_off);
+    if (rc)
+        for (uint32_t c = 0; c < n_ctg; c++) { pf_rescue_map_free(out[c]); out[c] = NULL; }
+    return rc;
+}
+
+int pf_rescue_dropped_mt(pf_bam_t *b, const char *chrom, uint32_t n_drop, const uint32_t *drop_start,
+                         const uint32_t *drop_end, const pf_known_vars_t *known, const pf_qname_tags_t *methphased,
+                         const pf_qname_tags_t *raw, int threads, pf_rescue_map_t **out) {
+    if (!b || !chrom || !known || !methphased || !out || (n_drop && (!drop_start || !drop_end)) || !b->path)
+        return PF_ERR_ARG;
+    return pf_rescue_dropped_multi(b, 1, &chrom, &n_drop, &drop_start, &drop_end, &known, methphased, raw, threads,
+                                   out);
+}
+
 int pf_rescue_dropped(pf_bam_t *b, const char *chrom, uint32_t n_drop, const uint32_t *drop_start,
                       const uint32_t *drop_end, const pf_known_vars_t *known, const pf_qname_tags_t *methphased,
                       const pf_qname_tags_t *raw, pf_rescue_map_t **out) {
-    if (!b || !chrom || !known || !methphased || !out || (n_drop && (!drop_start || !drop_end)) || !b->path)
-        return PF_ERR_ARG;
-    *out = NULL;
-    const int32_t tid = pf_bam_tid(b, chrom);
-    qtab_t qm = {0}, qr = {0};
-    u64v_t pb = {0}, res = {0};
-    fetcher_t F;
-    memset(&F, 0, sizeof F);
-    F.b = b;
-    F.tid = tid;
-    F.reads_mode = 2;
-    int rc = qtab_build(&qm, methphased);
-    if (!rc && raw) rc = qtab_build(&qr, raw);
-    if (!rc && tid >= 0 && tid < b->n_ref_idx) rc = bgzf_open(&F.z, b->path);
-    uint32_t prev_i = 0;
-    uint64_t seq = 0;
-    for (uint32_t k = 0; k < n_drop && !rc; k++) {
-        const uint32_t start = drop_start[k] - 1u, end = drop_end[k] + 1u;
-        pb.n = 0;
-        for (uint32_t i = prev_i; i < known->n; i++) {          /* 2653-2663 */
-            const uint32_t p = known->pos[i];
-            if (p >= start && p < end && (rc = u64_push(&pb, (uint64_t)p << 33))) break;
-            if (p >= end) { prev_i = i; break; }
-        }
-        if (rc) break;
-        /* "%s:%d-%d" of (start, end): htslib's 0-based [start-1, end) */
-        const int64_t b1 = (int32_t)start, e1 = (int32_t)end;
-        const int64_t beg = b1 > 0 ? b1 - 1 : 0;
-        recbuf_t rb;
-        memset(&rb, 0, sizeof rb);
-        if (tid >= 0 && tid < b->n_ref_idx) rc = fetch_region(&F, beg, e1, &rb);
-        {                                                              /* closing offsets */
-            const uint64_t vq = rb.f[F_QN].n, vc = rb.f[F_CIG].n / 4, vm = rb.f[F_MM].n;
-            if (!rc) rc = vb_put(&rb.f[F_QNOFF], &vq, 8);
-            if (!rc) rc = vb_put(&rb.f[F_CIGOFF], &vc, 8);
-            if (!rc) rc = vb_put(&rb.f[F_MMOFF], &vm, 8);
-        }
-        const size_t nk = pb.n;
-        for (uint64_t r = 0; r < rb.n_recs && !rc; r++) {
-            const uint64_t *qo = (const uint64_t *)rb.f[F_QNOFF].p;
-            const char *qn = (const char *)rb.f[F_QN].p + qo[r];
-            const size_t ql = (size_t)(qo[r + 1] - qo[r]);
-            const int hm = qtab_get(&qm, qn, ql);
-            if (hm < 0) continue;
-            int hr;
-            if (raw) { hr = qtab_get(&qr, qn, ql); if (hr < 0) continue; }
-            else hr = ((const uint8_t *)rb.f[F_HP].p)[r];
-            if (hr == 254) continue;
-            if (!((const uint16_t *)rb.f[F_FLAG].p)[r]) { rc = PF_ERR_ARG; break; }   /* assert(tagd), 1596 */
-            const uint64_t *co = (const uint64_t *)rb.f[F_CIGOFF].p, *mo = (const uint64_t *)rb.f[F_MMOFF].p;
-            rc = read_var_positions(((const uint32_t *)rb.f[F_POS].p)[r],
-                                    (const uint32_t *)rb.f[F_CIG].p + co[r], (uint32_t)(co[r + 1] - co[r]),
-                                    (const char *)rb.f[F_MM].p + mo[r], (size_t)(mo[r + 1] - mo[r]),
-                                    (uint32_t)hm & 0xFFu, &pb);
-        }
-        rb_free(&rb);
-        if (rc || nk == 0) continue;                                   /* pb.n == 0: goto done */
-        qsort(pb.a, pb.n, 8, cmp_u64);
-        /* for (i = 0; i < pb.n-1;): a known position sorted last is never visited */
-        for (size_t i = 0; i + 1 < pb.n && !rc;) {
-            if (pb.a[i] & (1ull << 32)) { i++; continue; }
-            const uint32_t rp = (uint32_t)(pb.a[i] >> 33);
-            uint32_t c[2] = {0, 0};
-            size_t j;
-            for (j = i + 1; j < pb.n; j++) {
-                if (!(pb.a[j] & (1ull << 32))) break;
-                if ((uint32_t)(pb.a[j] >> 33) != rp) break;
-                const uint32_t h = (uint32_t)pb.a[j] & 0xFFu;
-                if (h < 2) c[h]++;
-            }
-            const uint32_t hap = c[0] > c[1] ? 1u : c[1] > c[0] ? 0u : 254u;
-            rc = u64_push(&res, ((uint64_t)rp << 40) | (seq++ << 8) | hap);
-            i = j;
-        }
-    }
-    bgzf_close(&F.z);
-    free(F.rec);
-    free(F.chunks);
-    free(qm.key_off);
-    free(qr.key_off);
-    free(pb.a);
-    struct pf_rescue_own *o = NULL;
-    if (!rc) {
-        /* the hash keeps the last write per position */
-        qsort(res.a, res.n, 8, cmp_u64);
-        o = (struct pf_rescue_own *)calloc(1, sizeof *o);
-        if (o) { o->pos = (uint32_t *)malloc((res.n ? res.n : 1) * 4); o->hap = (uint8_t *)malloc(res.n ? res.n : 1); }
-        if (!o || !o->pos || !o->hap) rc = PF_ERR_NOMEM;
-        else {
-            uint32_t n = 0;
-            for (size_t i = 0; i < res.n; i++) {
-                const uint32_t p = (uint32_t)(res.a[i] >> 40);
-                if (i + 1 < res.n && (uint32_t)(res.a[i + 1] >> 40) == p) continue;
-                o->pos[n] = p;
-                o->hap[n] = (uint8_t)(res.a[i] & 0xFFu);
-                n++;
-            }
-            o->pub.n = n;
-            o->pub.pos = o->pos;
-            o->pub.hap_of_ref = o->hap;
-        }
-    }
-    free(res.a);
-    if (rc) { pf_rescue_map_free(o ? &o->pub : NULL); return rc; }
-    *out = &o->pub;
-    return PF_OK;
+    return pf_rescue_dropped_mt(b, chrom, n_drop, drop_start, drop_end, known, methphased, raw, 1, out);
 }
 
 /* ------------------------------------------------------------------ */

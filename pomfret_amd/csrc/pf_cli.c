@@ -273,6 +273,13 @@ int main(int argc, char **argv) {
     for (uint32_t i = 0; i < n; i++) joined += dec[i] >= 0;
     fprintf(stderr, "[M::main] %u of %u windows joined; %u read tags; done, used %.1fs\n", joined, n,
             (unsigned)pf_tags_size(pf_mp_qname_hp(p)), now_s() - T);
+    if (c.verbose) {
+        pf_mp_stats_t st;
+        if (pf_mp_stats(p, &st) == PF_OK)
+            fprintf(stderr, "[M::main] phases: plan %.3fs (coverage pass %.3fs), -u pre-pass %.3fs, windows %.3fs, "
+                    "writers %.3fs; device inflate %.1f ms (-u) + %.1f ms (windows)\n", st.s_plan, st.s_estimate,
+                    st.s_haptag, st.s_windows, st.s_finish, st.fetch_ms[1][1], st.fetch_ms[0][1]);
+    }
     pf_mp_free(p);
     return 0;
 }

@@ -395,8 +395,8 @@ DEV void out_match(Out &o, uint32_t L, uint32_t D, uint32_t lane) {
 #ifndef INF_WPE
 #define INF_WPE 8                       // waves per SIMD the register allocation aims at
 #endif
-__global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(INF_WPE, INF_WPE))) void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk,
-                                                            uint8_t *arena, uint32_t *status) {
+template <bool FALLBACK_ONLY>
+DEV void inflate_blocks(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena, uint32_t *status) {
     __shared__ InfLds lds_all[INF_WAVES];
     __shared__ uint32_t crc_tab[256], crc_x2n[32];
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
@@ -413,6 +413,7 @@ __global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t bi = blockIdx.x * INF_WAVES + wv;
     if (bi >= nblk) return;
+    if (FALLBACK_ONLY && uni(status[bi]) != PF_INF_FALLBACK) return;
     InfLds &T = lds_all[wv];
     const pf_bgzf_blk B = blk[bi];
     const uint64_t in_off = B.in_off;
@@ -667,4 +668,14 @@ __global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(
     // CRC32 of the output against the footer (bgzf_uncompress's check)
     if (!err && ~(o.crc ^ gf_mul(0xFFFFFFFFu, x8n(isize, crc_x2n))) != B.crc) err = PF_INF_ECRC;
     if (lane == 0) status[bi] = err;
+}
+
+__global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(INF_WPE, INF_WPE))) void pf_inflate(
+    const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena, uint32_t *status) {
+    inflate_blocks<false>(in, blk, nblk, arena, status);
+}
+
+__global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(INF_WPE, INF_WPE))) void pf_inflate_fallback(
+    const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena, uint32_t *status) {
+    inflate_blocks<true>(in, blk, nblk, arena, status);
 }

@@ -46,6 +46,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/pomfret_amd.h"
 
@@ -228,7 +229,39 @@ struct pf_mp_plan {
     int finished;
     uint32_t n_limit;
     double report_counts[3];   /* correct, switch, fail */
+    pf_mp_stats_t st;          /* measurement hook (pf_mp_stats) */
+    pthread_mutex_t st_mu;
 };
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+/* add a device fetch's timings to the run's stats (kind 0 windows, 1 -u) */
+static void st_fetch(pf_mp_plan_t *p, int kind, const pf_bam_dev_fetch_t *F, double run_ms) {
+    pthread_mutex_lock(&p->st_mu);
+    pf_mp_stats_t *s = &p->st;
+    if (F) {
+        const double m[7] = {F->ms_read, F->ms_inflate, F->ms_chain, F->ms_decode, F->ms_select, F->ms_build,
+                             F->ms_total};
+        for (int i = 0; i < 7; i++) s->fetch_ms[kind][i] += m[i];
+        s->comp_bytes[kind] += F->comp_bytes;
+        s->inflated_bytes[kind] += F->inflated_bytes;
+        s->n_fetch[kind]++;
+    }
+    s->run_ms[kind] += run_ms;
+    pthread_mutex_unlock(&p->st_mu);
+}
+
+int pf_mp_stats(const pf_mp_plan_t *p, pf_mp_stats_t *s) {
+    if (!p || !s) return PF_ERR_ARG;
+    pthread_mutex_lock((pthread_mutex_t *)&p->st_mu);
+    *s = p->st;
+    pthread_mutex_unlock((pthread_mutex_t *)&p->st_mu);
+    return PF_OK;
+}
 
 static char *dupstr(const char *s) {
     if (!s) return NULL;
@@ -257,6 +290,7 @@ void pf_mp_free(pf_mp_plan_t *p) {
     if (p->blocks) pf_blocks_free(p->blocks);
     if (p->gaps) pf_gaps_free(p->gaps);
     free(p->bam_path); free(p->vcf_path); free(p->out_prefix);
+    pthread_mutex_destroy(&p->st_mu);
     free(p);
 }
 
@@ -296,8 +330,10 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     if (o->mode != PF_MODE_METHPHASE && o->mode != PF_MODE_REPORT) return PF_ERR_ARG;
     if (o->mode == PF_MODE_REPORT && (o->chunk_size <= 0 || o->chunk_stride <= 0)) return PF_ERR_ARG;
     *out = NULL;
+    const double t_plan0 = now_s();
     pf_mp_plan_t *p = (pf_mp_plan_t *)calloc(1, sizeof *p);
     if (!p) return PF_ERR_NOMEM;
+    pthread_mutex_init(&p->st_mu, NULL);
     p->o = *o;
     p->bam_path = dupstr(o->bam_path);
     p->vcf_path = dupstr(o->vcf_path);
@@ -323,6 +359,7 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     const int32_t nt = pf_bam_n_targets(bam);
     int32_t *covs = NULL;
     const int need_est = o->mode == PF_MODE_METHPHASE ? o->cov_for_selection <= 0 : o->cov <= 0;
+    const double t_est0 = now_s();
     if (need_est) {
         covs = (int32_t *)calloc(nt > 0 ? nt : 1, sizeof(int32_t));
         if (!covs) rc = PF_ERR_NOMEM;
@@ -338,6 +375,7 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
             rc = pf_bam_estimate_coverage(bam, covs, nt > 0 ? nt : 1);
         }
     }
+    p->st.s_estimate = now_s() - t_est0;
     /* windows: merged gaps (methphase) or report chunks of the raw gaps */
     uint64_t nw = 0, cap = 0;
     for (uint32_t c = 0; c < C && !rc; c++) {
@@ -464,6 +502,7 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     if (rc) { pf_mp_free(p); return rc; }
     mp_log(p, "[M::pf_mp_plan] %s: %ld windows in %ld jobs", o->mode == PF_MODE_REPORT ? "report" : "methphase",
            (long)p->n_windows, (long)p->n_jobs);
+    p->st.s_plan = now_s() - t_plan0;
     *out = p;
     return PF_OK;
 }
@@ -641,7 +680,9 @@ int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
     if (!rc && kt->vars.n && !p->o.host_fetch) {
         /* device fetch + K4 on the device (pf_haptag_bam) */
         pf_bam_dev_fetch_t *F = NULL;
+        const double t0 = now_s();
         rc = pf_haptag_bam(ctx, &kt->vars, bam, contig, &F);
+        if (!rc) st_fetch(p, 1, F, (now_s() - t0) * 1e3 - F->ms_total);
         if (!rc && F->n_recs) {
             seen = pf_tags_new();
             if (!seen) rc = PF_ERR_NOMEM;
@@ -685,6 +726,7 @@ int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
 int pf_mp_merge_raw(pf_mp_plan_t *p) {
     if (!p) return PF_ERR_ARG;
     if (!p->o.untagged) { p->raw_merged = 1; return PF_OK; }
+    const double t0 = now_s();
     /* contig order, first wins across contigs (the -u table is one hash
      * filled contig by contig, 2069-2080) */
     uint32_t *by_contig = (uint32_t *)malloc((p->n_contigs ? p->n_contigs : 1) * sizeof(uint32_t));
@@ -704,6 +746,7 @@ int pf_mp_merge_raw(pf_mp_plan_t *p) {
     }
     free(by_contig);
     if (!rc) p->raw_merged = 1;
+    p->st.s_haptag += now_s() - t0;
     return rc;
 }
 
@@ -884,6 +927,7 @@ static int job_device_fetch(pf_mp_plan_t *p, pf_ctx_t *ctx, pf_bam_t *bam, job_t
     pf_bam_dev_fetch_t *F = NULL;
     int rc = pf_batch_upload_bam(ctx, cf, &lc, bam, p->gaps->names[J->contig], n, p->win_start + J->w0,
                                  p->win_end + J->w0, PF_READBACK, PF_MAX_WIN_RECS, &db, &F);
+    if (!rc) st_fetch(p, 0, F, 0.0);
     if (rc == PF_ERR_LIMIT) {                   /* per window on the host path */
         fetch_t f;
         rc = job_fetch(p, bam, J, &f);
@@ -924,7 +968,9 @@ static int job_device_fetch(pf_mp_plan_t *p, pf_ctx_t *ctx, pf_bam_t *bam, job_t
         memset(&o, 0, sizeof o);
         o.decision = dec;
         o.read_hp = rhp;
+        const double t0 = now_s();
         rc = pf_methphase_run(ctx, db, &o);
+        st_fetch(p, 0, NULL, (now_s() - t0) * 1e3);
     }
     uint32_t R_ = 0;
     if (!rc) {
@@ -1044,36 +1090,55 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
     if (!rc && !roff) rc = PF_ERR_NOMEM;
     if (!rc) rc = pf_tags_view(p->qname_hp, &tm);
     if (!rc && p->o.untagged) rc = pf_tags_view(p->raw, &tr);
+    /* every contig with dropped intervals at once: one work queue of
+     * (contig, interval) items on the run's host threads */
+    const pf_gaps_t *g = p->gaps;
+    uint32_t nr = 0;
+    const char **rn_names = (const char **)calloc(C ? C : 1, sizeof(char *));
+    uint32_t *rn_nd = (uint32_t *)calloc(C ? C : 1, sizeof(uint32_t)), *rn_c = (uint32_t *)calloc(C ? C : 1, 4);
+    const uint32_t **rn_ds = (const uint32_t **)calloc(C ? C : 1, sizeof(uint32_t *));
+    const uint32_t **rn_de = (const uint32_t **)calloc(C ? C : 1, sizeof(uint32_t *));
+    pf_known_table_t **kts = (pf_known_table_t **)calloc(C ? C : 1, sizeof(pf_known_table_t *));
+    const pf_known_vars_t **kvs = (const pf_known_vars_t **)calloc(C ? C : 1, sizeof(pf_known_vars_t *));
+    pf_rescue_map_t **maps = (pf_rescue_map_t **)calloc(C ? C : 1, sizeof(pf_rescue_map_t *));
+    if (!rc && (!rn_names || !rn_nd || !rn_c || !rn_ds || !rn_de || !kts || !kvs || !maps)) rc = PF_ERR_NOMEM;
     for (uint32_t c = 0; c < C && !rc; c++) {
-        const pf_gaps_t *g = p->gaps;
         const uint64_t nd = g->drop_off[c + 1] - g->drop_off[c];
-        roff[c + 1] = rn;
         if (!nd || p->tid[c] < 0) continue;
-        if (!bam && (rc = pf_bam_open(p->bam_path, NULL, &bam))) break;
-        pf_known_table_t *kt = NULL;
-        pf_rescue_map_t *m = NULL;
-        rc = pf_vcf_known_vars(p->vcf_path, g->names[c], &kt);
-        if (!rc) rc = pf_rescue_dropped(bam, g->names[c], (uint32_t)nd, g->drop_start + g->drop_off[c],
-                                        g->drop_end + g->drop_off[c], &kt->vars, &tm, p->o.untagged ? &tr : NULL, &m);
-        if (!rc && m->n) {
-            if (rn + m->n > rcap) {
-                while (rcap < rn + m->n) rcap = rcap ? 2 * rcap : 1024;
-                uint32_t *a = (uint32_t *)realloc(rpos, rcap * sizeof(uint32_t));
-                uint8_t *b = a ? (uint8_t *)realloc(rhap, rcap) : NULL;
-                if (a) rpos = a;
-                if (!a || !b) rc = PF_ERR_NOMEM;
-                else rhap = b;
-            }
-            if (!rc) {
-                memcpy(rpos + rn, m->pos, m->n * sizeof(uint32_t));
-                memcpy(rhap + rn, m->hap_of_ref, m->n);
-                rn += m->n;
-                roff[c + 1] = rn;
-            }
-        }
-        if (m) pf_rescue_map_free(m);
-        if (kt) pf_known_table_free(kt);
+        rc = pf_vcf_known_vars(p->vcf_path, g->names[c], &kts[nr]);
+        if (rc) break;
+        rn_names[nr] = g->names[c]; rn_nd[nr] = (uint32_t)nd; rn_c[nr] = c;
+        rn_ds[nr] = g->drop_start + g->drop_off[c]; rn_de[nr] = g->drop_end + g->drop_off[c];
+        kvs[nr] = &kts[nr]->vars;
+        nr++;
     }
+    if (!rc && nr) rc = pf_bam_open(p->bam_path, NULL, &bam);
+    if (!rc && nr)
+        rc = pf_rescue_dropped_multi(bam, nr, rn_names, rn_nd, rn_ds, rn_de, kvs, &tm, p->o.untagged ? &tr : NULL,
+                                     p->o.threads > 0 ? p->o.threads : 1, maps);
+    for (uint32_t c = 0, i = 0; c < C && !rc; c++) {
+        roff[c + 1] = rn;
+        if (i >= nr || rn_c[i] != c) continue;
+        const pf_rescue_map_t *m = maps[i++];
+        if (!m->n) continue;
+        if (rn + m->n > rcap) {
+            while (rcap < rn + m->n) rcap = rcap ? 2 * rcap : 1024;
+            uint32_t *a = (uint32_t *)realloc(rpos, rcap * sizeof(uint32_t));
+            uint8_t *b = a ? (uint8_t *)realloc(rhap, rcap) : NULL;
+            if (a) rpos = a;
+            if (!a || !b) { rc = PF_ERR_NOMEM; break; }
+            rhap = b;
+        }
+        memcpy(rpos + rn, m->pos, m->n * sizeof(uint32_t));
+        memcpy(rhap + rn, m->hap_of_ref, m->n);
+        rn += m->n;
+        roff[c + 1] = rn;
+    }
+    for (uint32_t i = 0; i < nr; i++) {
+        if (maps && maps[i]) pf_rescue_map_free(maps[i]);
+        if (kts && kts[i]) pf_known_table_free(kts[i]);
+    }
+    free(rn_names); free(rn_nd); free(rn_c); free(rn_ds); free(rn_de); free(kts); free(kvs); free(maps);
     if (bam) pf_bam_close(bam);
     if (!rc) {
         pf_rescue_t res = {roff, rpos ? rpos : (const uint32_t *)roff, rhap ? rhap : (const uint8_t *)roff};
@@ -1117,6 +1182,7 @@ static int varhaptag_outputs(pf_mp_plan_t *p) {
 int pf_mp_finish(pf_mp_plan_t *p) {
     if (!p) return PF_ERR_ARG;
     if (p->finished) return PF_OK;
+    const double t0 = now_s();
     free(p->decision);
     p->decision = (int8_t *)malloc(p->n_windows ? p->n_windows : 1);
     if (!p->decision) return PF_ERR_NOMEM;
@@ -1158,6 +1224,7 @@ int pf_mp_finish(pf_mp_plan_t *p) {
         if (!rc && p->out_prefix) rc = write_methphase_outputs(p);
     }
     if (!rc) p->finished = 1;
+    p->st.s_finish += now_s() - t0;
     return rc;
 }
 
@@ -1263,7 +1330,15 @@ static void *dev_main(void *arg) {
     return NULL;
 }
 
+static int run_on_devices_(pf_mp_plan_t *p, const pf_methphase_opts_t *o, int kind);
 static int run_on_devices(pf_mp_plan_t *p, const pf_methphase_opts_t *o, int kind) {
+    const double t0 = now_s();
+    const int rc = run_on_devices_(p, o, kind);
+    *(kind == PF_JOB_HAPTAG ? &p->st.s_haptag : &p->st.s_windows) += now_s() - t0;
+    return rc;
+}
+
+static int run_on_devices_(pf_mp_plan_t *p, const pf_methphase_opts_t *o, int kind) {
     const uint32_t n = kind == PF_JOB_HAPTAG ? p->n_ujobs : p->n_jobs;
     const uint32_t *ord = kind == PF_JOB_HAPTAG ? p->uorder : p->order;
     const job_t *J = kind == PF_JOB_HAPTAG ? p->ujobs : p->jobs;
@@ -1305,10 +1380,34 @@ int pf_mp_run_mine(pf_mp_plan_t *p, const pf_methphase_opts_t *run_opts, int kin
     return run_on_devices(p, run_opts, kind);
 }
 
+static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out);
+
+/* one set of contexts for the whole run (coverage pass, -u pre-pass, window
+ * jobs): a context's streams, pinned staging and kernels are set up once, not
+ * once per phase */
 int pf_methphase_main(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     if (!o || !out) return PF_ERR_ARG;
     *out = NULL;
     if (o->world > 1) return PF_ERR_ARG;           /* multi-process runs use the pf_mp_* steps */
+    const int nd = o->n_ctxs > 0 ? 0 : (o->n_devices > 0 ? o->n_devices : pf_device_count());
+    if (nd <= 0) return methphase_main_(o, out);
+    pf_ctx_t **ctxs = (pf_ctx_t **)calloc((size_t)nd, sizeof(pf_ctx_t *));
+    if (!ctxs) return PF_ERR_NOMEM;
+    int rc = PF_OK;
+    for (int d = 0; d < nd && !rc; d++) rc = pf_ctx_create(o->devices ? o->devices[d] : d, &ctxs[d]);
+    if (!rc) {
+        pf_methphase_opts_t oo = *o;
+        oo.ctxs = ctxs;
+        oo.n_ctxs = nd;
+        rc = methphase_main_(&oo, out);
+        if (*out) { (*out)->o.ctxs = NULL; (*out)->o.n_ctxs = 0; }
+    }
+    for (int d = 0; d < nd; d++) if (ctxs[d]) pf_ctx_destroy(ctxs[d]);
+    free(ctxs);
+    return rc;
+}
+
+static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     if (o->mode == PF_MODE_VARHAPTAG) {
         if (!o->out_prefix) return PF_ERR_ARG;
         pf_methphase_opts_t v = *o;

@@ -59,6 +59,13 @@ class PfMpJobInfo(C.Structure):
                 ("cfg", PfCfg)]
 
 
+class PfMpStats(C.Structure):
+    _fields_ = [("s_plan", C.c_double), ("s_estimate", C.c_double), ("s_haptag", C.c_double),
+                ("s_windows", C.c_double), ("s_finish", C.c_double), ("fetch_ms", (C.c_double * 7) * 2),
+                ("comp_bytes", C.c_uint64 * 2), ("inflated_bytes", C.c_uint64 * 2), ("run_ms", C.c_double * 2),
+                ("n_fetch", C.c_uint64 * 2)]
+
+
 class PfMpJobResult(C.Structure):
     _fields_ = [("n_windows", C.c_uint32), ("decision", C.c_void_p), ("tag_off", C.c_void_p),
                 ("tags", PfQnameTagsC), ("n_limit", C.c_uint32)]
@@ -97,6 +104,7 @@ def _bind():
     L.pf_mp_raw_hp.argtypes = [vp]
     L.pf_mp_raw_hp.restype = vp
     L.pf_mp_report_counts.argtypes = [vp, C.POINTER(C.c_double)]
+    L.pf_mp_stats.argtypes = [vp, C.POINTER(PfMpStats)]
     L.pf_tags_new.restype = vp
     L.pf_tags_free.argtypes = [vp]
     L.pf_tags_size.argtypes = [vp]
@@ -310,6 +318,19 @@ class Plan:
         _check(lib().pf_mp_report_counts(self.h, c), "pf_mp_report_counts")
         return dict(correct=int(c[0]), switch=int(c[1]), fail=int(c[2]))
 
+    def stats(self) -> Dict:
+        """Wall seconds per phase and the device-fetch sums of the run
+        (pf_mp_stats; a measurement hook)."""
+        st = PfMpStats()
+        _check(lib().pf_mp_stats(self.h, C.byref(st)), "pf_mp_stats")
+        names = ("read", "inflate", "chain", "decode", "select", "build", "total")
+        out = {k: round(getattr(st, k), 4) for k in ("s_plan", "s_estimate", "s_haptag", "s_windows", "s_finish")}
+        for i, kind in enumerate(("windows", "haptag")):
+            out[kind] = dict({f"{n}_ms": round(st.fetch_ms[i][j], 2) for j, n in enumerate(names)},
+                             comp_bytes=int(st.comp_bytes[i]), inflated_bytes=int(st.inflated_bytes[i]),
+                             run_ms=round(st.run_ms[i], 2), n_fetch=int(st.n_fetch[i]))
+        return out
+
     def close(self):
         if self.h:
             lib().pf_mp_free(self.h)
@@ -327,7 +348,7 @@ def _result(plan: Plan, mode: int) -> Dict:
     if mode == MODE_REPORT:
         return dict(decision=dec, counts=plan.report_counts(), n_limit=plan.n_limit)
     return dict(decision=dec, contigs=plan.contigs(), qname_hp=plan.qname_hp(), raw_hp=plan.raw_hp(),
-                n_limit=plan.n_limit)
+                n_limit=plan.n_limit, stats=plan.stats())
 
 
 def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],

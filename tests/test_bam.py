@@ -428,6 +428,17 @@ def test_rescue_dropped_matches_restatement(tmp_path):
     exp = _py_rescue(recs, kpos, dropped, meth)
     assert got == exp and len(got) > 5 and any(v != 254 for v in got.values())
     assert got_raw == _py_rescue(recs, kpos, dropped, meth, raw)
+    # threads: the intervals spread over host threads give the serial result,
+    # also with intervals that overlap (the last write per position wins and
+    # the known-position cursor runs across the intervals in order)
+    dropped2 = [(1200, 4000), (3000, 5200), (6000, 9000), (8800, 12500), (12000, 18000)]
+    with BamFile(p) as b:
+        for th in (2, 3, 8):
+            assert rescue_dropped(b, "c", dropped, kn, meth, threads=th) == got
+            assert rescue_dropped(b, "c", dropped, kn, meth, raw, threads=th) == got_raw
+        one = rescue_dropped(b, "c", dropped2, kn, meth)
+        assert rescue_dropped(b, "c", dropped2, kn, meth, threads=4) == one
+    assert one == _py_rescue(recs, kpos, dropped2, meth)
 
 
 def _py_cov(recs, lens):
