@@ -482,6 +482,14 @@ void pf_bam_dev_fetch_free(pf_bam_dev_fetch_t *fetch);
  * reads in BAM order: read_hp, qnames. */
 int  pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, const char *chrom,
                    pf_bam_dev_fetch_t **fetch);
+/* the same with the contig's coverage estimate (estimate_read_coverage_dirtyfast,
+ * 951-1040) from the same whole-contig fetch: every record is selected, the
+ * primary mapped ones are haplotagged; *truncated is set when a truncated
+ * record ended the pass (the serial estimate stops there).  Used by the driver
+ * for `methphase -u` without -c: one pass over each contig instead of two. */
+int  pf_haptag_bam_cov(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, const char *chrom,
+                       pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *truncated);
+
 
 /* The -u pre-pass reads of one contig (pre_haplotagging_read_in_one_ref,
  * 1841-1898: sam_itr_querys over the whole contig, flags 4/256/2048
@@ -508,6 +516,9 @@ int  pf_bam_estimate_coverage(pf_bam_t *bam, int32_t *covs, int32_t n);
  * Falls back to pf_bam_estimate_coverage when the index has no unplaced-read
  * count (the last contig's estimate depends on it). */
 int  pf_bam_estimate_coverage_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_t *covs, int32_t n, uint64_t piece_bytes);
+/* one contig of that pass (0 without records; *truncated: the pass would stop here) */
+int  pf_bam_estimate_contig_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, int32_t *cov, int32_t *truncated);
+
 
 /* qname -> tag table across the boundary (first entry of a qname wins). */
 typedef struct pf_qname_tags {

@@ -399,6 +399,12 @@ template <bool FALLBACK_ONLY>
 DEV void inflate_blocks(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena, uint32_t *status) {
     __shared__ InfLds lds_all[INF_WAVES];
     __shared__ uint32_t crc_tab[256], crc_x2n[32];
+    if (FALLBACK_ONLY) {                            // (uniform per workgroup: skip the setup when nothing is flagged)
+        const uint32_t b0 = blockIdx.x * INF_WAVES;
+        bool any = false;
+        for (uint32_t k = 0; k < INF_WAVES && b0 + k < nblk; k++) any |= status[b0 + k] == PF_INF_FALLBACK;
+        if (!any) return;
+    }
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;

@@ -320,11 +320,23 @@ __global__ __launch_bounds__(64) void pf_inflate_tok(const uint8_t *in, const pf
     };
 
     uint32_t it = 0;
+#ifdef SI_PROF
+    uint64_t p_ref = 0, p_hdr = 0, p_dec = 0, p_n = 0, p_t0 = __builtin_amdgcn_s_memtime(), pa = 0, pb = 0, pc = 0;
+#define SI_TS(x) x = __builtin_amdgcn_s_memtime()
+#else
+#define SI_TS(x)
+#endif
     while (__ballot(state != ST_DONE)) {
+        SI_TS(pa);
         if (++it == SI_RP) {
             it = 0;
             lb_refill(b, ring, state != ST_DONE);
         }
+        SI_TS(pb);
+#ifdef SI_PROF
+        p_ref += pb - pa;
+        p_n++;
+#endif
         if (state == ST_DONE) continue;
         if (b.rd > b.end) { err = PF_INF_EINPUT; state = ST_DONE; continue; }
         if (state == ST_HDR) {
@@ -409,6 +421,10 @@ __global__ __launch_bounds__(64) void pf_inflate_tok(const uint8_t *in, const pf
             continue;
         }
         // ---- one symbol (or one stored byte) per lane
+        SI_TS(pc);
+#ifdef SI_PROF
+        p_hdr += pc - pb;
+#endif
         lb_fill(b, ring, lane);
         uint32_t s, L = 0, D = 0;
         if (state == ST_STORED) {
@@ -450,6 +466,9 @@ __global__ __launch_bounds__(64) void pf_inflate_tok(const uint8_t *in, const pf
                 state = bfinal ? ST_DONE : ST_HDR;
             }
         }
+#ifdef SI_PROF
+        p_dec += __builtin_amdgcn_s_memtime() - pc;
+#endif
         if (s < 256) {                                     // a literal (or a stored byte)
             if (out + ln >= isize) { err = PF_INF_ESIZE; state = ST_DONE; continue; }
             lacc |= s << (8 * ln);
@@ -474,6 +493,11 @@ __global__ __launch_bounds__(64) void pf_inflate_tok(const uint8_t *in, const pf
             }
         }
     }
+#ifdef SI_PROF
+    const uint64_t p_tot = __builtin_amdgcn_s_memtime() - p_t0;
+    if (lane == 0 && bi < nblk) { mt[17] = (uint32_t)p_n; mt[18] = (uint32_t)(p_tot >> 4); mt[19] = (uint32_t)(p_ref >> 4); }
+    if (lane == 1 && bi < nblk) { mt[17] = (uint32_t)(p_hdr >> 4); mt[18] = (uint32_t)(p_dec >> 4); mt[19] = 0; }
+#endif
     if (bi >= nblk) return;
     if (!err && ln) { emit(lacc | (ln << 24), out, ln); out += ln; }
     if (!err && out != isize) err = PF_INF_ESIZE;
@@ -541,7 +565,16 @@ __global__ __launch_bounds__(LZ_T) void pf_inflate_lz(const pf_bgzf_blk *blk, ui
     }
     const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
 
+#ifdef SI_PROF
+    uint64_t q_tok = 0, q_own = 0, q_val = 0, q_jmp = 0, q_rounds = 0, qa = 0, q0 = __builtin_amdgcn_s_memtime();
+#define SQ_T(acc) { const uint64_t qn = __builtin_amdgcn_s_memtime(); acc += qn - qa; qa = qn; }
+#else
+#define SQ_T(acc)
+#endif
     for (uint32_t c0 = 0; c0 < isize; c0 += SI_CH) {
+#ifdef SI_PROF
+        qa = __builtin_amdgcn_s_memtime();
+#endif
         const uint32_t k = c0 >> 12;
         const uint32_t cl = isize - c0 < SI_CH ? isize - c0 : SI_CH;
         const uint32_t e0 = mt[1 + k];
@@ -577,6 +610,7 @@ __global__ __launch_bounds__(LZ_T) void pf_inflate_lz(const pf_bgzf_blk *blk, ui
             st += (v & 0x80000000u) ? (int32_t)((v >> 16) & 255u) + 3 : (int32_t)((v >> 24) & 3u);
         }
         __syncthreads();
+        SQ_T(q_tok);
         // each byte's token: the running max of the marks, per thread then across the block
         const uint32_t x0 = t * LZ_PER;
         uint32_t o[LZ_PER];
@@ -599,6 +633,7 @@ __global__ __launch_bounds__(LZ_T) void pf_inflate_lz(const pf_bgzf_blk *blk, ui
         uint32_t carry = (uint32_t)__shfl_up((int)smx, 1, 64);
         if (lane == 0) carry = 0;
         for (uint32_t w = 0; w < wv; w++) carry = wsum[w] > carry ? wsum[w] : carry;
+        SQ_T(q_own);
         // values, or the source of a byte copied from this chunk
         uint32_t pend = 0;
 #pragma unroll
@@ -626,8 +661,12 @@ __global__ __launch_bounds__(LZ_T) void pf_inflate_lz(const pf_bgzf_blk *blk, ui
                 pend |= 1u << j;
             }
         }
+        SQ_T(q_val);
         // sources inside the chunk: pointer jumping
         while (__syncthreads_or(pend != 0)) {
+#ifdef SI_PROF
+            q_rounds++;
+#endif
             uint32_t got = 0, nv[LZ_PER], ns[LZ_PER];
 #pragma unroll
             for (uint32_t j = 0; j < LZ_PER; j++) {
@@ -648,6 +687,18 @@ __global__ __launch_bounds__(LZ_T) void pf_inflate_lz(const pf_bgzf_blk *blk, ui
             pend &= ~got;
         }
     }
+#ifdef SI_PROF
+    {
+        const uint64_t qn = __builtin_amdgcn_s_memtime();
+        q_jmp += 0;
+        if (t == 0 && (bi & 63u) >= 2) {            // per block (x16 clocks): chunks total, tokens + owners, values | rounds
+            uint32_t *pm = const_cast<uint32_t *>(mt);
+            pm[17] = (uint32_t)((qn - q0) >> 4);
+            pm[18] = (uint32_t)((q_tok + q_own) >> 4);
+            pm[19] = (uint32_t)((q_val >> 4) & 0xFFFFFFu) | ((uint32_t)(q_rounds < 255 ? q_rounds : 255) << 24);
+        }
+    }
+#endif
     __syncthreads();
     // CRC32 of the image: 256 slices of 256 bytes combined
     {

@@ -807,8 +807,29 @@ static uint64_t contig_pieces(pf_bam_t *bam, int32_t tid, uint64_t piece_bytes, 
     return K;
 }
 
-extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
-                             pf_bam_dev_fetch_t **fetch_out) {
+// the coverage estimate's per-record rule (estimate_read_coverage_dirtyfast,
+// 951-1040): a record passing flag 4/256/2048, mapq >= 5, l_qseq >= 15000
+// and de <= 0.1 adds 1 to the 5 kb bins of start, start + 5000, ... < bam_endpos
+static void cov_add(std::vector<uint64_t> &bins, const Small &S, uint64_t i) {
+    constexpr uint32_t MOD = 5000;
+    if ((S.flag[i] & (4u | 256u | 2048u)) || S.mapq[i] < 5 || S.l_qseq[i] < 15000) return;
+    if ((double)S.de[i] > 0.1) return;
+    const int32_t pos = (int32_t)S.pos[i];
+    const uint32_t st = (uint32_t)pos, en = (uint32_t)(pos + (int32_t)S.rlen[i]);   // bam_endpos
+    for (int64_t x = (int32_t)st; x < (int64_t)en; x += MOD) {
+        const uint64_t b = (uint64_t)x / MOD;
+        if (x >= 0 && b < bins.size()) bins[b]++;
+    }
+}
+
+// The -u pre-pass of one contig (pf_haptag_bam) and, with cov != nullptr,
+// the contig's coverage estimate from the same whole-contig fetch: every
+// record of the contig is selected (the estimate's pass), the primary mapped
+// ones go to K4 (the -u pass's records, which must carry MD).  *trunc is set
+// when a truncated record ended the fetch (the estimate's serial pass stops
+// there).
+static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
+                           pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *trunc) {
     if (!ctx || !K || !bam || !chrom || !fetch_out) return PF_ERR_ARG;
     *fetch_out = nullptr;
     // sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX),
@@ -820,6 +841,9 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
     if (tid < 0) return PF_ERR_ARG;
     int64_t step = 0;
     const uint64_t NP = contig_pieces(bam, tid, 0, &step);
+    const bool with_cov = cov != nullptr;
+    std::vector<uint64_t> bins;
+    if (with_cov) bins.assign(pf_bam_target_len(bam, tid) / 5000, 0);
     pf_bam_dev_fetch_own *F = new pf_bam_dev_fetch_own();
     F->qn_off.assign(1, 0);
     uint32_t prev_left = 0;
@@ -830,11 +854,20 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
     for (uint64_t k = 0; k < NP && !rc; k++) {
         const int64_t beg = (int64_t)k * step, end = k + 1 == NP ? INT64_MAX : (int64_t)(k + 1) * step;
         pf_bam_dev_fetch_own P;
-        rc = dev_fetch(ctx, bam, tid, 1, &beg, &end, 1u, 0u, &P, [&](FetchOut &fo) -> int {
+        std::vector<uint32_t> take;                           // this piece's -u reads: selection positions
+        rc = dev_fetch(ctx, bam, tid, 1, &beg, &end, with_cov ? 0u : 1u, 0u, &P, [&](FetchOut &fo) -> int {
             const Small &S = *fo.S;
-            uint64_t m = 0;                                   // reads counted in an earlier piece
+            uint64_t m = 0;                                   // records counted in an earlier piece
             if (k) while (m < fo.n && (int32_t)S.pos[m] < beg) m++;
-            const uint64_t N = fo.n - m;
+            for (uint64_t i = m; i < fo.n; i++) {
+                if (with_cov) {
+                    cov_add(bins, S, i);
+                    if (S.flag[i] & (4u | 256u | 2048u)) continue;              // primary mapped only (1869-1871)
+                    if (!(S.st[i] & PF_REC_MD)) return PF_ERR_ARG;              // the reference asserts MD
+                }
+                take.push_back((uint32_t)i);
+            }
+            const uint64_t N = take.size();
             if (F->read_hp.size() + N >= (1ull << 32)) return PF_ERR_LIMIT;
             const size_t h0 = F->read_hp.size();
             F->read_hp.resize(h0 + N, 0);
@@ -842,7 +875,7 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
             std::vector<uint32_t> start(N), endp(N), nins(N), ncig(N), mdl(N), lq(N);
             std::vector<uint64_t> co(N + 1, 0), so(N + 1, 0), mo(N + 1, 0);
             for (uint64_t i = 0; i < N; i++) {
-                const uint64_t r = m + i;
+                const uint64_t r = take[i];
                 start[i] = S.pos[r];
                 endp[i] = (uint32_t)((int64_t)(int32_t)S.pos[r] + (int64_t)S.rlen[r]);   // bam_endpos
                 nins[i] = S.nins[r]; ncig[i] = S.ncig[r]; mdl[i] = S.md_len[r]; lq[i] = S.l_qseq[r];
@@ -851,12 +884,23 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
                 mo[i + 1] = mo[i] + S.md_len[r];
             }
             DevBuf &D = *fo.D;
+            hipStream_t st = fo.st;
+            const uint32_t *d_take = fo.sel + m;               // contiguous unless the estimate's records are mixed in
+            if (with_cov) {
+                std::vector<uint32_t> sel(fo.n), ts(N);
+                uint32_t *d_ts = D.alloc<uint32_t>(N);
+                if (!d_ts) return PF_ERR_NOMEM;
+                if (hipMemcpyAsync(sel.data(), fo.sel, 4 * fo.n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess) return PF_ERR_HIP;
+                for (uint64_t i = 0; i < N; i++) ts[i] = sel[take[i]];
+                if (hipMemcpyAsync(d_ts, ts.data(), 4 * N, hipMemcpyHostToDevice, st) != hipSuccess) return PF_ERR_HIP;
+                d_take = d_ts;
+            }
             uint32_t *d_start = D.alloc<uint32_t>(N), *d_end = D.alloc<uint32_t>(N), *d_len = D.alloc<uint32_t>(N);
             uint64_t *d_co = D.alloc<uint64_t>(N + 1), *d_so = D.alloc<uint64_t>(N + 1), *d_mo = D.alloc<uint64_t>(N + 1);
             uint32_t *d_cig = D.alloc<uint32_t>(co[N]);
             uint8_t *d_seq = D.alloc<uint8_t>(so[N] + 16), *d_md = D.alloc<uint8_t>(mo[N] + 16);
             if (!d_start || !d_end || !d_len || !d_co || !d_so || !d_mo || !d_cig || !d_seq || !d_md) return PF_ERR_NOMEM;
-            hipStream_t st = fo.st;
             bool ok = hipMemcpyAsync(d_start, start.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
                       hipMemcpyAsync(d_end, endp.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
                       hipMemcpyAsync(d_len, lq.data(), 4 * N, hipMemcpyHostToDevice, st) == hipSuccess &&
@@ -864,7 +908,7 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
                       hipMemcpyAsync(d_so, so.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess &&
                       hipMemcpyAsync(d_mo, mo.data(), 8 * (N + 1), hipMemcpyHostToDevice, st) == hipSuccess;
             if (ok) {
-                hipLaunchKernelGGL(pf_gather_big, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, fo.arena, fo.sel + m,
+                hipLaunchKernelGGL(pf_gather_big, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, fo.arena, d_take,
                                    N, fo.R, (const uint64_t *)d_co, d_cig, (const uint64_t *)d_so, d_seq,
                                    (const uint64_t *)nullptr, (uint8_t *)nullptr, (const uint64_t *)nullptr,
                                    (uint8_t *)nullptr, (const uint64_t *)nullptr, (uint8_t *)nullptr,
@@ -877,9 +921,8 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
             return pf_haptag_core(ctx, K, (uint32_t)N, h, nullptr, &dv, F->read_hp.data() + h0, &prev_left);
         });
         if (rc) break;
-        // this piece's reads' qnames (after the prefix of earlier starts)
-        const uint64_t n = P.pub.n_recs, got = F->read_hp.size() - (F->qn_off.size() - 1), m = n - got;
-        for (uint64_t i = m; i < n; i++) {
+        // this piece's reads' qnames
+        for (const uint32_t i : take) {
             F->qn.insert(F->qn.end(), P.qn.begin() + P.qn_off[i], P.qn.begin() + P.qn_off[i + 1]);
             F->qn_off.push_back(F->qn.size());
         }
@@ -890,6 +933,12 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
         if (P.win_status[0] == PF_WIN_TRUNC) { F->pub.n_truncated = 1; break; }   // sam_itr_next < 0 ends the loop
     }
     if (rc) { delete F; return rc; }
+    if (with_cov) {
+        uint64_t tot = 0;
+        for (uint64_t b : bins) tot += b;
+        *cov = bins.empty() ? 0 : (int32_t)(tot / bins.size());
+        if (trunc) *trunc = F->pub.n_truncated ? 1 : 0;
+    }
     const uint64_t N = F->read_hp.size();
     F->qn.push_back(0);
     F->win_rec_off = {0, (uint32_t)N};
@@ -911,6 +960,17 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
     return PF_OK;
 }
 
+extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
+                             pf_bam_dev_fetch_t **fetch_out) {
+    return haptag_bam_impl(ctx, K, bam, chrom, fetch_out, nullptr, nullptr);
+}
+
+extern "C" int pf_haptag_bam_cov(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
+                                 pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *truncated) {
+    if (!cov || !truncated) return PF_ERR_ARG;
+    return haptag_bam_impl(ctx, K, bam, chrom, fetch_out, cov, truncated);
+}
+
 // estimate_read_coverage_dirtyfast (blockjoin.c:951-1040) through the device
 // fetch: the serial pass's records are, for a coordinate-sorted BAM, each
 // contig's records in index order followed by the unplaced tail, so the pass
@@ -921,6 +981,48 @@ extern "C" int pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *
 // (its contig keeps the bins counted so far, later contigs 0), and unplaced
 // reads at the end leave the last contig with reads at 0 (refID -1 when the
 // loop ends).  Contigs without records stay 0.
+// one contig of the device pass: *cov its estimate (0 without records),
+// *stopped set by a truncated record (the serial pass ends there)
+static int est_contig(pf_ctx_t *ctx, pf_bam_t *bam, int32_t t, uint64_t piece_bytes, int32_t *cov, bool *stopped,
+                      bool *has_chunks) {
+    *cov = 0;
+    *stopped = false;
+    const int64_t nc = pf_bam_query_chunks(bam, t, 0, INT64_MAX, nullptr, 0);
+    if (nc < 0) return (int)nc;
+    *has_chunks = nc > 0;
+    if (nc == 0) return PF_OK;
+    const uint32_t len = pf_bam_target_len(bam, t);
+    int64_t step = 0;
+    const uint64_t K = contig_pieces(bam, t, piece_bytes, &step);
+    std::vector<uint64_t> bins(len / 5000, 0);
+    for (uint64_t k = 0; k < K && !*stopped; k++) {
+        const int64_t beg = (int64_t)k * step, end = k + 1 == K ? INT64_MAX : (int64_t)(k + 1) * step;
+        pf_bam_dev_fetch_own F;
+        const int rc = dev_fetch(ctx, bam, t, 1, &beg, &end, 0u, 0u, &F, [&](FetchOut &fo) -> int {
+            const Small &S = *fo.S;
+            for (uint64_t i = 0; i < fo.n; i++) {
+                if (k && (int32_t)S.pos[i] < beg) continue;                 // counted in an earlier piece
+                cov_add(bins, S, i);
+            }
+            return PF_OK;
+        });
+        if (rc) return rc;
+        if (F.win_status[0] == PF_WIN_TRUNC) *stopped = true;
+    }
+    uint64_t tot = 0;
+    for (uint64_t b : bins) tot += b;
+    *cov = bins.empty() ? 0 : (int32_t)(tot / bins.size());
+    return PF_OK;
+}
+
+extern "C" int pf_bam_estimate_contig_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, int32_t *cov, int32_t *truncated) {
+    if (!ctx || !bam || !cov || !truncated || tid < 0 || tid >= pf_bam_n_targets(bam)) return PF_ERR_ARG;
+    bool stopped = false, has = false;
+    const int rc = est_contig(ctx, bam, tid, 0, cov, &stopped, &has);
+    *truncated = stopped ? 1 : 0;
+    return rc;
+}
+
 extern "C" int pf_bam_estimate_coverage_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_t *covs, int32_t n,
                                             uint64_t piece_bytes) {
     if (!ctx || !bam || !covs) return PF_ERR_ARG;
@@ -929,43 +1031,13 @@ extern "C" int pf_bam_estimate_coverage_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_
     const int64_t n_unplaced = pf_bam_n_no_coor(bam);
     if (n_unplaced < 0) return pf_bam_estimate_coverage(bam, covs, n);
     for (int32_t i = 0; i < n; i++) covs[i] = 0;
-    constexpr uint32_t MOD = 5000;
     int32_t last = -1;
     bool stopped = false;
-    std::vector<uint64_t> bins;
     for (int32_t t = 0; t < nr && !stopped; t++) {
-        const int64_t nc = pf_bam_query_chunks(bam, t, 0, INT64_MAX, nullptr, 0);
-        if (nc < 0) return (int)nc;
-        if (nc == 0) continue;
-        last = t;
-        const uint32_t len = pf_bam_target_len(bam, t);
-        int64_t step = 0;
-        const uint64_t K = contig_pieces(bam, t, piece_bytes, &step);
-        bins.assign(len / MOD, 0);
-        for (uint64_t k = 0; k < K && !stopped; k++) {
-            const int64_t beg = (int64_t)k * step, end = k + 1 == K ? INT64_MAX : (int64_t)(k + 1) * step;
-            pf_bam_dev_fetch_own F;
-            const int rc = dev_fetch(ctx, bam, t, 1, &beg, &end, 0u, 0u, &F, [&](FetchOut &fo) -> int {
-                const Small &S = *fo.S;
-                for (uint64_t i = 0; i < fo.n; i++) {
-                    const int32_t pos = (int32_t)S.pos[i];
-                    if (k && pos < beg) continue;                   // counted in an earlier piece
-                    if ((S.flag[i] & (4u | 256u | 2048u)) || S.mapq[i] < 5 || S.l_qseq[i] < 15000) continue;
-                    if ((double)S.de[i] > 0.1) continue;
-                    const uint32_t st = (uint32_t)pos, en = (uint32_t)(pos + (int32_t)S.rlen[i]);   // bam_endpos
-                    for (int64_t x = (int32_t)st; x < (int64_t)en; x += MOD) {
-                        const uint64_t b = (uint64_t)x / MOD;
-                        if (x >= 0 && b < bins.size()) bins[b]++;
-                    }
-                }
-                return PF_OK;
-            });
-            if (rc) return rc;
-            if (F.win_status[0] == PF_WIN_TRUNC) stopped = true;
-        }
-        uint64_t tot = 0;
-        for (uint64_t b : bins) tot += b;
-        covs[t] = bins.empty() ? 0 : (int32_t)(tot / bins.size());
+        bool has = false;
+        const int rc = est_contig(ctx, bam, t, piece_bytes, &covs[t], &stopped, &has);
+        if (rc) return rc;
+        if (has) last = t;
     }
     if (!stopped && n_unplaced > 0 && last >= 0) covs[last] = 0;
     return PF_OK;

@@ -231,6 +231,11 @@ struct pf_mp_plan {
     double report_counts[3];   /* correct, switch, fail */
     pf_mp_stats_t st;          /* measurement hook (pf_mp_stats) */
     pthread_mutex_t st_mu;
+    /* -u without -c, one process: the coverage estimate comes from the -u
+     * pre-pass's whole-contig fetches (pf_haptag_bam_cov), per VCF contig */
+    int est_deferred;
+    int32_t *ucov, *utrunc;
+    uint8_t *uhave;
 };
 
 static double now_s(void) {
@@ -290,6 +295,7 @@ void pf_mp_free(pf_mp_plan_t *p) {
     if (p->blocks) pf_blocks_free(p->blocks);
     if (p->gaps) pf_gaps_free(p->gaps);
     free(p->bam_path); free(p->vcf_path); free(p->out_prefix);
+    free(p->ucov); free(p->utrunc); free(p->uhave);
     pthread_mutex_destroy(&p->st_mu);
     free(p);
 }
@@ -325,7 +331,26 @@ static void mp_log(const pf_mp_plan_t *p, const char *fmt, const char *a, long x
     if (p->o.verbose) { fprintf(stderr, fmt, a, x, y); fputc('\n', stderr); }
 }
 
-int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
+/* the methphase parameters of contig c from its coverage estimate (or -c) */
+static void methphase_cfg(pf_cfg_t *cf, const pf_methphase_opts_t *o, int cov_est) {
+    int sel = o->cov_for_selection, nc = o->n_cand, rt = o->cov_for_runtime;
+    if (sel <= 0) {                                   /* 4357-4374 */
+        sel = cov_est / 10 + 1;
+        rt = 2 * sel;
+        nc = cov_est / 4 + 1;
+    } else if (rt <= 0) {
+        rt = 2 * sel;                                  /* config.cov_for_runtime, 4655 */
+    }
+    if (sel <= 0) sel = 1;                             /* clamps, 4381-4390 */
+    if (nc <= 1) nc = 2;
+    cf->cov_for_selection = sel; cf->cov_for_runtime = rt; cf->n_cand = nc;
+}
+
+static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_est);
+
+int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) { return mp_plan(o, out, 0); }
+
+static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_est) {
     if (!o || !out || !o->bam_path || !o->vcf_path) return PF_ERR_ARG;
     if (o->mode != PF_MODE_METHPHASE && o->mode != PF_MODE_REPORT) return PF_ERR_ARG;
     if (o->mode == PF_MODE_REPORT && (o->chunk_size <= 0 || o->chunk_stride <= 0)) return PF_ERR_ARG;
@@ -351,7 +376,10 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     p->tid = (int32_t *)calloc(C ? C : 1, sizeof(int32_t));
     p->cfg = (pf_cfg_t *)calloc(C ? C : 1, sizeof(pf_cfg_t));
     p->win_off = (uint64_t *)calloc(C + 1, sizeof(uint64_t));
-    if (!p->tid || !p->cfg || !p->win_off) { pf_mp_free(p); return PF_ERR_NOMEM; }
+    p->ucov = (int32_t *)calloc(C ? C : 1, sizeof(int32_t));
+    p->utrunc = (int32_t *)calloc(C ? C : 1, sizeof(int32_t));
+    p->uhave = (uint8_t *)calloc(C ? C : 1, 1);
+    if (!p->tid || !p->cfg || !p->win_off || !p->ucov || !p->utrunc || !p->uhave) { pf_mp_free(p); return PF_ERR_NOMEM; }
 
     pf_bam_t *bam = NULL;
     rc = pf_bam_open(o->bam_path, NULL, &bam);
@@ -360,10 +388,14 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     int32_t *covs = NULL;
     const int need_est = o->mode == PF_MODE_METHPHASE ? o->cov_for_selection <= 0 : o->cov <= 0;
     const double t_est0 = now_s();
+    p->est_deferred = need_est && defer_est && o->mode == PF_MODE_METHPHASE && o->untagged && !o->host_fetch &&
+                      o->n_ctxs > 0;
     if (need_est) {
         covs = (int32_t *)calloc(nt > 0 ? nt : 1, sizeof(int32_t));
         if (!covs) rc = PF_ERR_NOMEM;
-        if (!rc && !o->host_fetch && (o->n_ctxs > 0 || pf_device_count() > 0)) {
+        if (!rc && p->est_deferred) {
+            /* estimated from the -u pre-pass's fetches (finish_deferred_estimate) */
+        } else if (!rc && !o->host_fetch && (o->n_ctxs > 0 || pf_device_count() > 0)) {
             /* the pass over the whole BAM on the device (the first context or
              * device of the run); runs without a device scan on the host */
             pf_ctx_t *ec = o->n_ctxs > 0 ? o->ctxs[0] : NULL;
@@ -385,18 +417,7 @@ int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
         cf->k_span = o->k_span > 0 ? o->k_span : 5000;
         cf->hard_cov = 15;
         if (o->mode == PF_MODE_METHPHASE) {
-            int sel = o->cov_for_selection, nc = o->n_cand, rt = o->cov_for_runtime;
-            if (sel <= 0) {                                   /* 4357-4374 */
-                const int cov = (p->tid[c] >= 0 && p->tid[c] < nt) ? covs[p->tid[c]] : 0;
-                sel = cov / 10 + 1;
-                rt = 2 * sel;
-                nc = cov / 4 + 1;
-            } else if (rt <= 0) {
-                rt = 2 * sel;                                  /* config.cov_for_runtime, 4655 */
-            }
-            if (sel <= 0) sel = 1;                             /* clamps, 4381-4390 */
-            if (nc <= 1) nc = 2;
-            cf->cov_for_selection = sel; cf->cov_for_runtime = rt; cf->n_cand = nc;
+            methphase_cfg(cf, o, need_est && (p->tid[c] >= 0 && p->tid[c] < nt) ? covs[p->tid[c]] : 0);
         } else {                                               /* 5045-5051: no clamps */
             /* covs is indexed by the VCF contig index here, as the reference
              * does (covs[i_ref], 5046); out of range reads as 0 */
@@ -681,7 +702,12 @@ int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
         /* device fetch + K4 on the device (pf_haptag_bam) */
         pf_bam_dev_fetch_t *F = NULL;
         const double t0 = now_s();
-        rc = pf_haptag_bam(ctx, &kt->vars, bam, contig, &F);
+        if (p->est_deferred) {                  /* the contig's coverage estimate from the same fetch */
+            rc = pf_haptag_bam_cov(ctx, &kt->vars, bam, contig, &F, &p->ucov[J->contig], &p->utrunc[J->contig]);
+            if (!rc) p->uhave[J->contig] = 1;
+        } else {
+            rc = pf_haptag_bam(ctx, &kt->vars, bam, contig, &F);
+        }
         if (!rc) st_fetch(p, 1, F, (now_s() - t0) * 1e3 - F->ms_total);
         if (!rc && F->n_recs) {
             seen = pf_tags_new();
@@ -1234,6 +1260,61 @@ int pf_mp_report_counts(const pf_mp_plan_t *p, double *counts3) {
     return PF_OK;
 }
 
+/* The deferred coverage estimate (-u without -c, one process): the serial
+ * pass's per-contig values from the -u pre-pass's fetches, the contigs the
+ * pre-pass did not fetch (no variants) estimated on their own when a needed
+ * contig comes after them, and the pass's quirks kept (a truncated record
+ * zeroes every later contig; unplaced reads at the end zero the last contig
+ * with reads; an index without n_no_coor: the serial host pass); then each
+ * contig's parameters (4357-4390). */
+static int finish_deferred_estimate(pf_mp_plan_t *p, pf_ctx_t *ctx) {
+    if (!p->est_deferred) return PF_OK;
+    const double t0 = now_s();
+    pf_bam_t *bam = NULL;
+    int rc = pf_bam_open(p->bam_path, NULL, &bam);
+    if (rc) return rc;
+    const int32_t nt = pf_bam_n_targets(bam);
+    int32_t *covs = (int32_t *)calloc(nt > 0 ? nt : 1, sizeof(int32_t));
+    int32_t *trunc = (int32_t *)calloc(nt > 0 ? nt : 1, sizeof(int32_t));
+    uint8_t *have = (uint8_t *)calloc(nt > 0 ? nt : 1, 1);
+    if (!covs || !trunc || !have) rc = PF_ERR_NOMEM;
+    int32_t maxneed = -1;
+    for (uint32_t c = 0; c < p->n_contigs && !rc; c++) {
+        const int32_t t = p->tid[c];
+        if (t < 0 || t >= nt) continue;
+        if (p->uhave[c]) { covs[t] = p->ucov[c]; trunc[t] = p->utrunc[c]; have[t] = 1; }
+        if (p->win_off[c + 1] > p->win_off[c] && t > maxneed) maxneed = t;
+    }
+    const int64_t n_unplaced = rc ? 0 : pf_bam_n_no_coor(bam);
+    if (!rc && n_unplaced < 0) {
+        rc = pf_bam_estimate_coverage(bam, covs, nt > 0 ? nt : 1);        /* as pf_bam_estimate_coverage_dev does */
+    } else if (!rc) {
+        int32_t last = -1;
+        int stopped = 0;
+        for (int32_t t = 0; t < nt && !rc; t++) {
+            if (stopped) { covs[t] = 0; continue; }
+            const int64_t nc = pf_bam_query_chunks(bam, t, 0, INT64_MAX, NULL, 0);
+            if (nc < 0) { rc = (int)nc; break; }
+            if (nc == 0) { covs[t] = 0; continue; }
+            last = t;
+            if (!have[t]) {
+                if (t > maxneed) continue;                 /* neither used nor ahead of a contig that is */
+                rc = pf_bam_estimate_contig_dev(ctx, bam, t, &covs[t], &trunc[t]);
+            }
+            if (trunc[t]) stopped = 1;
+        }
+        if (!rc && !stopped && n_unplaced > 0 && last >= 0) covs[last] = 0;
+    }
+    for (uint32_t c = 0; c < p->n_contigs && !rc; c++) {
+        const int32_t t = p->tid[c];
+        methphase_cfg(&p->cfg[c], &p->o, (t >= 0 && t < nt) ? covs[t] : 0);
+    }
+    free(covs); free(trunc); free(have);
+    pf_bam_close(bam);
+    p->st.s_estimate += now_s() - t0;
+    return rc;
+}
+
 /* ------------------------------------------------------------------ */
 /* in-process driver: one host thread per device                        */
 
@@ -1424,11 +1505,12 @@ static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
         return PF_OK;
     }
     pf_mp_plan_t *p = NULL;
-    int rc = pf_mp_plan(o, &p);
+    int rc = mp_plan(o, &p, 1);
     if (!rc && o->untagged) {
         rc = run_on_devices(p, o, PF_JOB_HAPTAG);
         if (!rc) rc = pf_mp_merge_raw(p);
     }
+    if (!rc && p->est_deferred) rc = finish_deferred_estimate(p, o->ctxs[0]);
     if (!rc) rc = run_on_devices(p, o, PF_JOB_WINDOWS);
     if (!rc) rc = pf_mp_finish(p);
     if (rc) { pf_mp_free(p); return rc; }
