@@ -66,6 +66,8 @@ class AlnSpec:
     het_snv_rate: float = 0.0  # > 0: het SNVs outside the gap, alt on one truth haplotype, and MD:Z per record
     windows_at: tuple = ()     # explicit (s, e) per window index instead of the strided layout
     orient_at: tuple = ()      # explicit cis (0) / trans (1) per window index
+    skip_frac: float = 0.0     # windows whose left-block reads lost their HP tags (skipped by 1161-1163)
+    nosite_frac: float = 0.0   # windows without allele- or unmethylated sites (no site qualifies, 4266)
 
 
 def _qual_from_cat(rng, cat):
@@ -109,6 +111,12 @@ def make_aln_window(spec: AlnSpec, w: int):
     site_p = np.where(cls < 0.7, 0.95, 0.05)
     site_asm = cls >= 0.9
     site_hap = rng.integers(0, 2, cpg.shape[0])
+    # window kinds of real runs (a separate stream: other windows are unchanged)
+    kind_u = np.random.default_rng([spec.seed, w, 79]).random()
+    skip_window = kind_u < spec.skip_frac
+    if spec.skip_frac <= kind_u < spec.skip_frac + spec.nosite_frac:
+        site_p[:] = 0.95
+        site_asm[:] = False
     site_of = np.full(L, -1, np.int64)
     site_of[cpg] = np.arange(cpg.shape[0])
     snv = _plant_snvs(spec, w, ref, cpg, span_lo, s, e) if spec.het_snv_rate > 0 else None
@@ -134,6 +142,8 @@ def make_aln_window(spec: AlnSpec, w: int):
     only_right = (~tl) & (ends > e)
     hp[only_right] = truth[only_right] ^ orient
     hp[rng.random(n) < spec.untag_frac] = HAPTAG_UNPHASED
+    if skip_window:
+        hp[tl & (np.arange(n) % 4 != 0)] = HAPTAG_UNPHASED
     strand = (rng.random(n) < 0.5).astype(np.int64)
     out, flag, mapq, de = _build_reads(spec, rng, ref, starts - span_lo, lens, truth, strand,
                                        site_of, site_p, site_asm, site_hap, snv)

@@ -36,7 +36,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
-from _bamio import (BLOCK, EOF_BLOCK, Rec, _deflate_block, aux_BC, aux_f, aux_Z, bai_bytes,  # noqa: E402
+from _bamio import (BLOCK, EOF_BLOCK, Rec, _deflate_block, aux_BC, aux_f, aux_i, aux_Z, bai_bytes,  # noqa: E402
                     bam_header, encode_record, endpos)
 
 A_, C_, G_ = 0, 1, 2
@@ -57,6 +57,7 @@ class GenomeSpec:
     qual: bool = True
     level: int = 6
     chunk_reads: int = 1000
+    hp_tags: bool = False         # HP:i from the phase of the block a read starts in (pre-haplotagged BAM)
 
     def read_spec(self):
         from pomfret_amd.synth_aln import AlnSpec
@@ -153,6 +154,13 @@ def _chunk_job(args):
     out, flag, mapq, de = _build_reads(rs, rng, g["ref"], g["starts"][sl], g["lens"][sl], g["truth"][sl],
                                        g["strand"][sl], g["site_of"], g["site_p"], g["site_asm"], g["site_hap"],
                                        g["snv"])
+    hp_of = None
+    if spec.hp_tags:                                    # the VCF's hap index of the read's block: truth ^ orient
+        st_ = g["starts"][sl]
+        blk = np.searchsorted(g["blocks"][:, 0], st_, side="right") - 1
+        inb = (blk >= 0) & (st_ < g["blocks"][np.maximum(blk, 0), 1])
+        hp_of = np.where(inb, g["truth"][sl] ^ g["orient"][np.maximum(blk, 0)], 254)
+        hp_of[np.random.default_rng([spec.seed, ci, 6, k]).random(r1 - r0) < 0.1] = 254
     qpool = None
     if spec.qual:
         qpool = np.random.default_rng([spec.seed, ci, 4, k]).normal(20, 6, 1 << 21).clip(2, 50) \
@@ -170,6 +178,8 @@ def _chunk_job(args):
             aux += aux_BC("ML", r["ml"])
         if "md" in r:
             aux += aux_Z("MD", r["md"])
+        if spec.hp_tags and hp_of is not None and hp_of[i] != 254:
+            aux += aux_i("HP", int(hp_of[i]) + 1)
         lq = int(r["l_qseq"])
         q = None
         if qpool is not None:
@@ -280,3 +290,15 @@ def small_spec(seed: int = 7) -> GenomeSpec:
                       chunk_reads=400,
                       aln=AlnSpec(het_snv_rate=0.001, untag_frac=0.0, mean_len=15_000, sd_len=7_500,
                                   min_len=7_500, max_len=75_000))
+
+
+def report_spec(seed: int = 11) -> GenomeSpec:
+    """BASELINE configs[4]'s shape at test scale: a 200x pileup over one
+    contig with pre-haplotagged reads, phase blocks of 40-90 kb (the report's
+    chunk windows sample inside them) and half-length reads."""
+    from pomfret_amd.synth_aln import AlnSpec
+    return GenomeSpec(contigs=(("chr1", 560_000),), coverage=200, block_min=40_000, block_max=90_000,
+                      short_block_frac=0.0, gap_min=5_000, gap_max=30_000, lead=60_000, seed=seed, qual=False,
+                      level=1, chunk_reads=500, hp_tags=True,
+                      aln=AlnSpec(het_snv_rate=0.001, untag_frac=0.0, mean_len=15_000, sd_len=7_500,
+                                  min_len=7_500, max_len=60_000))

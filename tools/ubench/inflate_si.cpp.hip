@@ -15,6 +15,24 @@
 namespace w {
 #include "../../pomfret_amd/csrc/pf_inflate.hip"
 }
+namespace vp {
+#define SI_PROF 1
+#define SI_LR 8u
+#define SI_DR 7u
+#define SI_LCAP 96u
+#define SI_DCAP 32u
+#define SI_RS 8u
+#define SI_RP 4u
+#include "../../pomfret_amd/csrc/pf_inflate_simt.hip"
+#undef SI_LR
+#undef SI_DR
+#undef SI_LCAP
+#undef SI_DCAP
+#undef SI_RS
+#undef SI_RP
+#undef SI_PROF
+#undef SI_TS
+}
 namespace v1 {
 #define SI_LR 9u
 #define SI_DR 7u
@@ -118,10 +136,10 @@ int main(int argc, char **argv) {
                          uint32_t *);
     typedef void (*lzk)(const pf_bgzf_blk *, uint32_t, uint64_t, const uint32_t *, const uint32_t *, uint8_t *,
                         uint32_t *);
-    const int NV = 4;
-    tokk tk[NV] = {nullptr, v1::pf_inflate_tok, v2::pf_inflate_tok, v3::pf_inflate_tok};
-    lzk lz[NV] = {nullptr, v1::pf_inflate_lz, v2::pf_inflate_lz, v3::pf_inflate_lz};
-    const char *name[NV] = {"wave", "9/7 c128 r16", "8/7 c128 r16", "8/7 c96 r8"};
+    const int NV = 5;
+    tokk tk[NV] = {nullptr, v1::pf_inflate_tok, v2::pf_inflate_tok, v3::pf_inflate_tok, vp::pf_inflate_tok};
+    lzk lz[NV] = {nullptr, v1::pf_inflate_lz, v2::pf_inflate_lz, v3::pf_inflate_lz, vp::pf_inflate_lz};
+    const char *name[NV] = {"wave", "9/7 c128 r16", "8/7 c128 r16", "8/7 c96 r8", "prof 8/7 c96"};
     for (int rep = 0; rep < 2; rep++)
         for (int v = 0; v < NV; v++) {
             CK(hipMemset(d_st, 0, 4ull * nb));
@@ -154,6 +172,28 @@ int main(int argc, char **argv) {
             printf("%-13s blocks %u out %.0f MB: pass1 %.3f ms pass2 %.3f ms total %.3f ms = %.2f GB/s  bad %u %s\n",
                    name[v], nb, out / 1e6, ms1, ms2, ms1 + ms2, out / ((ms1 + ms2) * 1e6), bad,
                    same ? "identical" : "DIFFER");
+            if (v == NV - 1) {                  // s_memtime sections per wave (x16 clocks), averaged
+                std::vector<uint32_t> mh((size_t)nb * PF_SI_META);
+                CK(hipMemcpy(mh.data(), meta, 4ull * PF_SI_META * nb, hipMemcpyDeviceToHost));
+                double sn = 0, st = 0, sr = 0, sh = 0, sd = 0;
+                uint32_t nw = 0;
+                for (uint32_t b = 0; b + 1 < nb; b += 64, nw++) {
+                    const uint32_t *m0 = &mh[(size_t)b * PF_SI_META], *m1 = &mh[(size_t)(b + 1) * PF_SI_META];
+                    sn += m0[17]; st += 16.0 * m0[18]; sr += 16.0 * m0[19]; sh += 16.0 * m1[17]; sd += 16.0 * m1[18];
+                }
+                printf("  pass1 per wave: iterations %.0f, clocks total %.3g = %.0f per iteration: refill %.0f, header %.0f, "
+                       "decode %.0f, emit/rest %.0f\n", sn / nw, st / nw, st / sn, sr / sn, sh / sn, sd / sn,
+                       (st - sr - sh - sd) / sn);
+                double lt = 0, lo = 0, lv = 0, lr = 0;
+                uint32_t nl = 0;
+                for (uint32_t b = 0; b < nb; b++) {
+                    if ((b & 63u) < 2) continue;
+                    const uint32_t *m = &mh[(size_t)b * PF_SI_META];
+                    lt += 16.0 * m[17]; lo += 16.0 * m[18]; lv += 16.0 * (m[19] & 0xFFFFFFu); lr += m[19] >> 24; nl++;
+                }
+                printf("  pass2 per block: clocks %.0f: tokens+owners %.0f, values %.0f, jumps %.0f; rounds %.1f\n",
+                       lt / nl, lo / nl, lv / nl, (lt - lo - lv) / nl, lr / nl);
+            }
         }
     return 0;
 }
