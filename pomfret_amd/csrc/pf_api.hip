@@ -258,7 +258,9 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
 template <typename T>
 static int dev_alloc(pf_dbatch *b, T **p, size_t n) {
     void *q = nullptr;
-    size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    // 64 B of slack: kernels may read a whole 16-B group past an array's end
+    // (K12's dense pass loads call positions four at a time)
+    size_t bytes = std::max<size_t>(n, 1) * sizeof(T) + 64;
     if (hipMalloc(&q, bytes) != hipSuccess) return PF_ERR_NOMEM;
     b->allocs.push_back(q);
     *p = static_cast<T *>(q);
@@ -524,6 +526,12 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             return (a & 1) > (c & 1);
         });
         PUT(p, ord.data(), ord.size()); d.k3_order = p;
+        std::vector<uint32_t> word(W);
+        for (uint32_t i = 0; i < W; i++) word[i] = i;
+        std::stable_sort(word.begin(), word.end(), [&](uint32_t a, uint32_t c) {
+            return in->win_read_off[a + 1] - in->win_read_off[a] > in->win_read_off[c + 1] - in->win_read_off[c];
+        });
+        PUT(p, word.data(), word.size()); d.k12_order = p;
     }
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
     ALLOC(d.k3_fb_list, std::max<uint32_t>(2 * W, 1));
@@ -594,6 +602,8 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     const char *kc = getenv("PF_K12_CAP"), *ks = getenv("PF_K12_SMAX");
     d.k12_capw = kc ? std::min<uint32_t>((uint32_t)atoi(kc), PF_K12_CAPW) : PF_K12_CAPW;
     d.k12_smax = ks ? std::min<uint32_t>((uint32_t)atoi(ks), PF_K12_SMAX) : PF_K12_SMAX;
+    const char *kd = getenv("PF_K12_DENSE");
+    d.k12_dense = kd && atoi(kd) ? 1u : 0u;
     const char *ke = getenv("PF_K2_ENTCAP");
     d.k2_entcap = ke ? std::min<uint32_t>((uint32_t)atoi(ke), PF_K2_ENT_CAP) : PF_K2_ENT_CAP;
     // PF_K3_PATH=fold|rows drives every greedy pick through the sequential

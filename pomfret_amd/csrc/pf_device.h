@@ -56,6 +56,7 @@ struct pf_dev_batch {
     /* per-window results of K1 */
     uint32_t *win_S, *win_nreads;
     const uint32_t *k3_order;          /* [2W] greedy problems (w<<1|dir), heaviest first */
+    const uint32_t *k12_order;         /* [W] windows for K12's workgroups, heaviest first */
     uint32_t *k3_fb_list, *k3_fb_ctr;  /* problems the main greedy kernel defers to pf_k3_fallback */
     uint32_t *site_pos, *st1_pos, *site_q1;
     uint8_t *len0, *len1;
@@ -78,6 +79,7 @@ struct pf_dev_batch {
     uint32_t lds_fb;                   /* dynamic LDS of the fallback greedy kernel (>= lds_bytes) */
     uint32_t lds_w;                    /* dynamic LDS of the one-wave greedy kernel */
     uint32_t k12_capw, k12_smax;       /* fused methmer phase limits (test overrides) */
+    uint32_t k12_dense;                /* 1: every window takes K12's dense (HBM) site path (tests) */
     uint32_t k2_entcap;                /* fallback reads above this bound use HBM scratch */
     uint32_t k3_mode;                  /* test override: 0 exact pick, 1 always fold, 2 chunked record rows */
 };

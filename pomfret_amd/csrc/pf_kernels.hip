@@ -52,7 +52,7 @@ DEV unsigned long long k3_stamp_now() {
     prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
 #define K3_COUNT(i, v) do { prof_acc[i] += (v); } while (0)
 #define K12_STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = k3_stamp_now(); \
-    d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + (i)] = t_ - k12_t0; k12_t0 = t_; } } while (0)
+    d.prof[64ull * d.W + (uint64_t)w * 16 + (i)] = t_ - k12_t0; k12_t0 = t_; } } while (0)
 #define K2_STAMP(i) do { if (k2acc) { const unsigned long long t_ = k3_stamp_now(); \
     k2acc[i] += t_ - k2acc[9]; k2acc[9] = t_; } } while (0)
 #else
@@ -639,7 +639,9 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     __shared__ uint32_t sh_tbase[PF_K1_THREADS];
     __shared__ unsigned long long sh_base[2];
     constexpr uint32_t NT = PF_K1_THREADS, NW = NT / 64;
-    const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    // windows heaviest first (k12_order): the big windows of a gap mix start
+    // in the first wave of workgroups instead of forming the kernel's tail
+    const uint32_t w = d.k12_order[blockIdx.x], tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
 #ifdef PF_K3_PROFILE
     unsigned long long k12_t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -692,7 +694,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     constexpr uint32_t HN = 8192, HMAX = 6144, BW = 8192;
     uint32_t *hkeys = tile, *hcnt = tile + HN;
     uint64_t *bmap = reinterpret_cast<uint64_t *>(tile + 2 * HN);
-    const bool range_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64;
+    const bool range_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64 && !d.k12_dense;
     bool hash_ok = false;
     // the window's calls are one contiguous run: flat passes, four
     // independent (cat, pos) loads in flight per thread
@@ -727,6 +729,15 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
             }
             __syncthreads();
         }
+        // more repeated positions than the hash may hold: the dense path,
+        // without pass B (an overflowing table leaves every later key probing
+        // a full table, the whole workgroup contending on the reservation
+        // counter: 5-7 M cycles on a 500 kb gap)
+        uint32_t rep = 0, rep_tot = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < BW / NT; j++) rep += (uint32_t)__popcll(bmap[tid * (BW / NT) + j]);
+        block_excl_scan<NT>(rep, sh_scan, &rep_tot);
+        if (rep_tot <= HMAX) {
         for (uint32_t j = tid; j < HN; j += NT) { hkeys[j] = PF_NONE; hcnt[j] = 0; }
         if (tid == 0) { sh_misc[5] = 0; sh_misc[6] = 0; }
         __syncthreads();
@@ -767,6 +778,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
             for (uint32_t j = tid; j < BW; j += NT) bmap[j] = 0;
             __syncthreads();
         }
+        }
     }
     if (hash_ok) {
         for (uint32_t j = tid; j < HN; j += NT) {
@@ -803,50 +815,142 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
         if (tid == 0) sh_misc[4] = total;
         __syncthreads();
     }
-    // ---- general path: dense per-position counts, tile by tile, in position order
-    for (uint64_t base = pmin; !hash_ok && base <= pmax; base += PF_K1_TILE) {
-        const uint64_t top = base + PF_K1_TILE;
-        for (uint32_t j = tid; j < PF_K1_TILE; j += NT) tile[j] = 0;
+    // ---- general path (a position range beyond the bitmaps, or more repeated
+    // positions than the hash holds: the big windows of a gap mix).  The
+    // window's calls are bucketed by 16 K-position chunk into an HBM scratch
+    // list of u16 (offset in chunk | meth/unmeth bit), then each chunk is
+    // counted with LDS atomics in the tile and scanned in position order.
+    // Two flat passes over the calls (histogram, scatter; the chunk counters
+    // are wave-aggregated) and one per chunk over its own calls.  Round 2
+    // counted 32 K-position LDS tiles each over every read of the window (two
+    // binary searches per read and tile); device-scope atomics on an HBM
+    // counter array were tried this round: ~15 cycles per call at L2, 6-9 M
+    // cycles on a 500 kb gap -- both ~10x this.
+    if (!hash_ok) {
+        constexpr uint32_t CHB = 14, CH = 1u << CHB, MAXCH = 8191;
+        static_assert(CH + 2 * (MAXCH + 1) <= PF_K1_TILE, "chunk counters + chunk offsets fit the tile");
+        uint32_t *ccnt = tile, *coff = tile + CH, *cfill = coff + MAXCH + 1;
+        const uint64_t ncall = C1 - C0;
+        const uint64_t need = (2ull * ncall + 15) & ~15ull;
+        if (tid == 0) {
+            const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)need);
+            sh_base[0] = o;
+            if (o + need > d.scr_cap) atomicOr(d.status, PF_ST_SCR_OVF);
+        }
         __syncthreads();
-        for (uint32_t i = wid; i < R; i += NW) {
-            const uint32_t r = r0 + i;
-            const uint64_t c0 = d.read_call_off[r], c1 = d.read_call_off[r + 1];
-            if (c1 == c0) continue;
-            if ((uint64_t)d.call_pos[c1 - 1] < base || (uint64_t)d.call_pos[c0] >= top) continue;
-            const uint64_t lo = lb_u32(d.call_pos, c0, c1, (uint32_t)base);
-            const uint64_t hi = top > 0xFFFFFFFFull ? c1 : lb_u32(d.call_pos, lo, c1, (uint32_t)top);
-            for (uint64_t c = lo + lane; c < hi; c += 64) {
-                const uint32_t cat = d.call_cat[c];
-                if (cat < 2) atomicAdd(&tile[d.call_pos[c] - (uint32_t)base], cat == 0 ? 1u : 0x10000u);
+        const uint64_t so = sh_base[0];
+#ifdef PF_K3_PROFILE
+        const unsigned long long dz0 = k3_stamp_now();
+#endif
+        if (so + need > d.scr_cap) {
+            // the scratch arena is full (status set; the host grows it and
+            // re-runs): no sites, and K3 skips the window
+            if (tid == 0) sh_misc[4] = 0;
+            __syncthreads();
+        } else {
+            uint16_t *sc = reinterpret_cast<uint16_t *>(d.scr + so);
+            const uint32_t span = pmax - pmin + 1;
+            // one wave-aggregated LDS add per distinct chunk among the lanes
+            // (a wave's 64 consecutive calls are mostly one read's, 1-2 chunks)
+            auto chunk_add = [&](bool act, uint32_t ch, uint32_t *ctr, bool ret) -> uint32_t {
+                uint32_t mine = 0;
+                uint64_t todo = __ballot(act);
+                while (todo) {
+                    const uint32_t l0 = (uint32_t)__ffsll((long long)todo) - 1;
+                    const uint32_t lc = rdl(ch, l0);
+                    const uint64_t m = __ballot(act && ch == lc);
+                    uint32_t base = 0;
+                    if (lane == l0) {
+                        if (ret) base = atomicAdd(&ctr[lc], (uint32_t)__popcll(m));
+                        else atomicAdd(&ctr[lc], (uint32_t)__popcll(m));
+                    }
+                    base = rdl(base, l0);
+                    if (act && ch == lc) mine = base + (uint32_t)__popcll(m & lanemask_lt(lane));
+                    todo &= ~m;
+                }
+                return mine;
+            };
+            const uint64_t cend = C0 + (ncall + NT - 1) / NT * NT;   // whole waves in every pass
+            for (uint64_t sup = 0; sup < span; sup += (uint64_t)MAXCH << CHB) {
+                const uint32_t nch = (uint32_t)min<uint64_t>((span - sup + CH - 1) >> CHB, MAXCH);
+                const uint64_t slim = min<uint64_t>((uint64_t)nch << CHB, span - sup);
+                for (uint32_t j = tid; j <= nch; j += NT) { coff[j] = 0; cfill[j] = 0; }
+                __syncthreads();
+                // A: calls per chunk
+                for (uint64_t c = C0 + tid; c < cend; c += NT) {
+                    const bool in = c < C1;
+                    const uint32_t cat = in ? d.call_cat[c] : 2u;
+                    const uint64_t rel = in ? (uint64_t)(d.call_pos[c] - pmin) - sup : ~0ull;
+                    const bool act = cat < 2 && rel < slim;
+                    chunk_add(act, act ? (uint32_t)(rel >> CHB) : 0u, coff, false);
+                }
+                __syncthreads();
+                // chunk offsets (exclusive scan, 8 chunks per thread)
+                {
+                    uint32_t v[8], t = 0;
+#pragma unroll
+                    for (uint32_t u = 0; u < 8; u++) { const uint32_t j = tid * 8 + u; v[u] = j < nch ? coff[j] : 0u; t += v[u]; }
+                    uint32_t tot;
+                    uint32_t ex = block_excl_scan<NT>(t, sh_scan, &tot);
+#pragma unroll
+                    for (uint32_t u = 0; u < 8; u++) { const uint32_t j = tid * 8 + u; if (j < nch) coff[j] = ex; ex += v[u]; }
+                    if (tid == 0) coff[nch] = tot;
+                }
+                __syncthreads();
+                // C: scatter the calls into their chunks' lists
+                for (uint64_t c = C0 + tid; c < cend; c += NT) {
+                    const bool in = c < C1;
+                    const uint32_t cat = in ? d.call_cat[c] : 2u;
+                    const uint64_t rel = in ? (uint64_t)(d.call_pos[c] - pmin) - sup : ~0ull;
+                    const bool act = cat < 2 && rel < slim;
+                    const uint32_t ch = act ? (uint32_t)(rel >> CHB) : 0u;
+                    const uint32_t slot = chunk_add(act, ch, cfill, true);
+                    if (act) sc[coff[ch] + slot] = (uint16_t)(((uint32_t)rel & (CH - 1)) | (cat << 15));
+                }
+                __threadfence();                         // the lists are read back through L2 (L1 invalidated)
+                __syncthreads();
+                // D: each chunk counted in LDS, scanned in position order
+                for (uint32_t ch = 0; ch < nch; ch++) {
+                    const uint32_t l0 = coff[ch], l1 = coff[ch + 1];
+                    if (l1 == l0) continue;                  // uniform: no calls, no site
+                    for (uint32_t j = tid; j < CH / 4; j += NT) reinterpret_cast<uint4 *>(ccnt)[j] = make_uint4(0, 0, 0, 0);
+                    __syncthreads();
+                    for (uint32_t t = l0 + tid; t < l1; t += NT) {
+                        const uint32_t v = sc[t];
+                        atomicAdd(&ccnt[v & (CH - 1)], (v >> 15) ? 0x10000u : 1u);
+                    }
+                    __syncthreads();
+                    uint32_t qmask = 0;
+                    constexpr uint32_t PER = CH / NT;        // 16 positions per thread
+#pragma unroll
+                    for (uint32_t jj = 0; jj < PER; jj++) {
+                        const uint32_t j = (jj + tid) & (PER - 1);   // rotated: conflict-free banks
+                        const uint32_t v = ccnt[tid * PER + j];
+                        // counts are uint16 holding count<<4 in the reference: count mod 4096 (blockjoin.c:3236)
+                        if ((int)(v & 4095u) >= cov && (int)((v >> 16) & 4095u) >= cov) qmask |= 1u << j;
+                    }
+                    uint32_t total;
+                    const uint32_t excl = block_excl_scan<NT>((uint32_t)__popc(qmask), sh_scan, &total);
+                    const uint32_t srun = sh_misc[4];
+                    uint32_t m = qmask, rank = srun + excl;
+                    const uint32_t pb = pmin + (uint32_t)sup + (ch << CHB) + tid * PER;
+                    while (m) {
+                        const uint32_t j = __ffs(m) - 1;
+                        m &= m - 1;
+                        if (rank < scap) d.site_pos[sb + rank] = pb + j;
+                        else atomicOr(d.status, PF_ST_SITE_OVF);
+                        rank++;
+                    }
+                    __syncthreads();
+                    if (tid == 0) sh_misc[4] = srun + total;
+                    __syncthreads();
+                }
+                __syncthreads();
             }
         }
-        __syncthreads();
-        // each thread owns 32 consecutive positions, visited in a rotated order
-        // (bank = (j + tid) mod 32: conflict-free)
-        uint32_t qmask = 0;
-#pragma unroll 8
-        for (uint32_t jj = 0; jj < 32; jj++) {
-            const uint32_t j = (jj + tid) & 31;
-            const uint32_t v = tile[tid * 32 + j];
-            // counts are uint16 holding count<<4 in the reference: count mod 4096 (blockjoin.c:3236)
-            if ((int)(v & 4095u) >= cov && (int)((v >> 16) & 4095u) >= cov) qmask |= 1u << j;
-        }
-        uint32_t total;
-        const uint32_t excl = block_excl_scan<NT>((uint32_t)__popc(qmask), sh_scan, &total);
-        const uint32_t srun = sh_misc[4];
-        {
-            uint32_t m = qmask, rank = srun + excl;
-            while (m) {
-                const uint32_t j = __ffs(m) - 1;
-                m &= m - 1;
-                if (rank < scap) d.site_pos[sb + rank] = (uint32_t)base + tid * 32 + j;
-                else atomicOr(d.status, PF_ST_SITE_OVF);
-                rank++;
-            }
-        }
-        __syncthreads();
-        if (tid == 0) sh_misc[4] = srun + total;
-        __syncthreads();
+#ifdef PF_K3_PROFILE
+        if (tid == 0) d.prof[64ull * d.W + (uint64_t)w * 16] = k3_stamp_now() - dz0;   // the dense path
+#endif
     }
     K12_STAMP(2);
     uint32_t S = sh_misc[4];
@@ -1100,9 +1204,9 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
         k2_flush(d, kst, pend_off, pend_n, lane);
 #ifdef PF_K3_PROFILE
         if (tid == 0) {
-            for (int j = 0; j < 7; j++) d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 8 + j] = k2a[j];
-            d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 7] = k2a[7];
-            d.prof[64ull * d.W + (uint64_t)blockIdx.x * 16 + 15] = k2a[8];
+            for (int j = 0; j < 7; j++) d.prof[64ull * d.W + (uint64_t)w * 16 + 8 + j] = k2a[j];
+            d.prof[64ull * d.W + (uint64_t)w * 16 + 7] = k2a[7];
+            d.prof[64ull * d.W + (uint64_t)w * 16 + 15] = k2a[8];
         }
 #endif
     } else {

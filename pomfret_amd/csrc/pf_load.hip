@@ -201,59 +201,97 @@ DEV uint32_t swar_dec(uint64_t y, uint32_t n) {      // bytes 0..n-1 of y (n in 
     return (uint32_t)(((z & 0x0000FFFF0000FFFFull) * 42949672960001ull) >> 32);
 }
 
+// One pass over the text with the next row in flight: every ';' of a row
+// closes an entry (its comma count is a difference of the row's comma scan),
+// and the next entry's header is parsed right away from the row registers
+// (readlane; a header past the next row -- never in real data -- reads
+// memory).  Round 2 rescanned from each entry's start and read every header
+// byte from memory: one dependent round trip per row and per header byte.
+struct K0Hdr { uint32_t base, strand, nc, h; int mi; };
+
 DEV bool k0_mm_entries(const uint32_t *gw, const uint8_t *mm, uint32_t mis, uint32_t mlen, uint32_t mln,
                        uint32_t lane, K0Tgt &t) {
-    uint32_t i = 0;
-    uint64_t ml_cur = 0;
-    bool found = false;
     t.nd = 0;
-    while (i < mlen) {
-        uint32_t e = mlen, commas = 0;
-        for (uint32_t k0 = (mis + i) >> 2; 4 * k0 < mis + mlen; k0 += 64) {
-            const uint32_t k = k0 + lane;
-            const int32_t b = (int32_t)(4 * k) - (int32_t)mis;
-            const uint32_t w = 4 * k < mis + mlen ? gw[k] : 0u;
-            const uint32_t vm = bytes_in(b, i, mlen);
-            const uint32_t sm = bytes_eq(w, ';') & vm, cm = bytes_eq(w, ',') & vm;
-            const uint64_t bs = __ballot(sm != 0);
-            if (bs) {
-                const uint32_t l0 = (uint32_t)__ffsll((long long)bs) - 1;
-                const uint32_t sb = (uint32_t)__builtin_ctz(rdl(sm, l0)) >> 3;   // byte of the first ';'
-                e = 4 * (k0 + l0) - mis + sb;
-                const uint32_t cm2 = lane < l0 ? cm : lane == l0 ? cm & ((1u << (8 * sb)) - 1u) : 0u;
-                commas += wsum_small((uint32_t)__builtin_popcount(cm2));
-                break;
-            }
-            commas += wsum_small((uint32_t)__builtin_popcount(cm));
-        }
-        e = uni(e);
-        commas = uni(commas);
-        if (e - i < 3) return false;
-        const uint32_t base = mm[i], strand = mm[i + 1];
-        if (strand != '+' && strand != '-') return false;
+    if (mlen == 0) return true;
+    const uint32_t wend = mis + mlen;
+    const uint32_t kmaxw = (wend - 1) / 4 + 1;       // the padded text holds this word
+    auto ld = [&](uint32_t k) { return gw[min(k, kmaxw)]; };
+    uint32_t k0 = 0;
+    // rows in flight four deep (a 2 KB text -- dorado's h + m entries of a
+    // 30 kb read -- costs one memory round trip, not eight)
+    uint32_t w = ld(lane), pw = ld(64 + lane), pw2 = ld(128 + lane), pw3 = ld(192 + lane);
+    auto byte_at = [&](uint32_t x) -> uint32_t {      // text byte x < mlen (uniform x)
+        const uint32_t kx = (mis + x) >> 2, sh = 8 * ((mis + x) & 3u);
+        if (kx - k0 < 64) return (rdl(w, kx - k0) >> sh) & 0xFFu;
+        if (kx - k0 < 128) return (rdl(pw, kx - k0 - 64) >> sh) & 0xFFu;
+        return mm[x];
+    };
+    K0Hdr H;
+    auto header = [&](uint32_t i) {                   // base, strand, codes, '.'/'?' (the entry's ';' stops every loop)
+        H.base = byte_at(i);
+        H.strand = i + 1 < mlen ? byte_at(i + 1) : 0u;
         uint32_t h = i + 2, nc = 0;
         int mi = -1;
-        if (is_digit(mm[h])) {
-            while (h < e && is_digit(mm[h])) h++;
+        uint32_t c = h < mlen ? byte_at(h) : 0u;
+        if (is_digit(c)) {
+            while (h < mlen && is_digit(byte_at(h))) h++;
             nc = 1;
         } else {
-            while (h < e && is_alpha(mm[h])) {
-                if (mm[h] == 'm' && mi < 0) mi = (int)nc;
+            while (h < mlen && is_alpha(c = byte_at(h))) {
+                if (c == 'm' && mi < 0) mi = (int)nc;
                 nc++;
                 h++;
             }
         }
-        if (nc == 0) return false;
-        if (base == ',') commas--;                    // count the skip list's commas only
-        if (h < e && (mm[h] == '.' || mm[h] == '?')) h++;
-        if (!found && base == 'C' && strand == '+' && mi >= 0 && commas > 0) {
+        if (h < mlen && ((c = byte_at(h)) == '.' || c == '?')) h++;
+        H.h = h; H.nc = nc; H.mi = mi;
+    };
+    uint64_t ml_cur = 0;
+    bool found = false;
+    // entry [i, e) with `commas` commas
+    auto close = [&](uint32_t i, uint32_t e, uint32_t commas) -> bool {
+        if (e - i < 3) return false;
+        if (H.strand != '+' && H.strand != '-') return false;
+        if (H.nc == 0) return false;
+        if (H.base == ',') commas--;                  // count the skip list's commas only
+        if (!found && H.base == 'C' && H.strand == '+' && H.mi >= 0 && commas > 0) {
             found = true;
-            if (mln && ml_cur + (uint64_t)commas * nc > mln) return false;
-            t.nd = commas; t.nc = nc; t.mi = (uint32_t)mi; t.th = h; t.te = e; t.ml = ml_cur;
+            if (mln && ml_cur + (uint64_t)commas * H.nc > mln) return false;
+            t.nd = commas; t.nc = H.nc; t.mi = (uint32_t)H.mi; t.th = H.h; t.te = e; t.ml = ml_cur;
         }
-        ml_cur += (uint64_t)commas * nc;
-        i = e + 1;
+        ml_cur += (uint64_t)commas * H.nc;
+        return true;
+    };
+    uint32_t i = 0, ci = 0, cg = 0;                   // entry start, commas before it, before the row
+    header(0);
+    for (;;) {
+        const int32_t b = (int32_t)(4 * (k0 + lane)) - (int32_t)mis;
+        const uint32_t vm = bytes_in(b, 0, mlen);
+        const uint32_t sm = bytes_eq(w, ';') & vm, cm = bytes_eq(w, ',') & vm;
+        const uint32_t ncl = (uint32_t)__builtin_popcount(cm);
+        const uint32_t cin = wscan(ncl, lane);
+        for (uint64_t bs = __ballot(sm != 0); bs; bs &= bs - 1) {
+            const uint32_t l0 = (uint32_t)__ffsll((long long)bs) - 1;
+            const uint32_t sml = rdl(sm, l0), cml = rdl(cm, l0), cb0 = cg + rdl(cin, l0) - rdl(ncl, l0);
+            for (uint32_t m = sml; m; m &= m - 1) {
+                const uint32_t sb = (uint32_t)__builtin_ctz(m) >> 3;
+                const uint32_t e = 4 * (k0 + l0) - mis + sb;
+                const uint32_t ce = cb0 + (uint32_t)__builtin_popcount(cml & ((1u << (8 * sb)) - 1u));
+                if (!close(i, e, ce - ci)) return false;
+                i = e + 1;
+                ci = ce;
+                if (i < mlen) header(i);
+            }
+        }
+        cg += rdl(cin, 63);
+        if (4 * (k0 + 64) >= wend) break;
+        k0 += 64;
+        w = pw;
+        pw = pw2;
+        pw2 = pw3;
+        pw3 = ld(k0 + 192 + lane);
     }
+    if (i < mlen && !close(i, mlen, cg - ci)) return false;   // an entry without its ';'
     if (mln && ml_cur > mln) return false;
     return true;
 }
@@ -880,9 +918,18 @@ DEV void k0_chunk_implicit(const pf_load_dev &d, K0W &L, uint32_t nv, uint32_t c
 
 // Wave-parallel walk (phase 3).  Returns false when the CIGAR reaches a
 // fatal operation.
+// bam_endpos rides along: each lane sums the reference-consuming lengths of
+// the operations it loads (M/D/N/=/X), every tile of the CIGAR, including the
+// tiles past the last trigger (round 2 re-read the whole CIGAR afterwards).
+DEV uint32_t k0_refc(uint32_t c) {
+    const uint32_t op = c & 15u;
+    return (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) ? c >> 4 : 0u;
+}
+
 template <int MODE, typename TP>
 DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t ncig, uint32_t qs, bool rev, TP TB,
-                 uint32_t nT, const uint8_t *seq, uint32_t len, bool implicit, uint32_t lane, K0Out &o) {
+                 uint32_t nT, const uint8_t *seq, uint32_t len, bool implicit, uint32_t lane, K0Out &o,
+                 uint32_t &racc) {
     const uint32_t cgoffset = rev ? 0xFFFFFFFFu : 0u;
     uint32_t a_cur = 0, off_cur = 0, j = 0, tc = 0, i_ref = qs;
     if ((cig[0] & 15u) == 4u) {                       // prologue (629-652)
@@ -900,6 +947,7 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
         const uint32_t g = j + lane;
         const uint32_t c = cn;
         if (j + 64 < ncig) cn = j + 64 + lane < ncig ? cig[j + 64 + lane] : 4u;
+        racc += k0_refc(c);                           // past the end: 4u (S), nothing
         const uint32_t op = c & 15u, ln = c >> 4;
         const uint64_t stop = __ballot(op == 3u || op == 4u);     // past the end acts as a stop
         const uint64_t bad = __ballot(op > 4u && g < ncig);
@@ -951,17 +999,22 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
         j += 64;
     }
     // fatal operations past the last consumed trigger are still reached
-    // by the reference's loop (it walks every op up to N/S)
-    while (j < ncig && !trunc) {
+    // by the reference's loop (it walks every op up to N/S); the end position
+    // counts every operation (the tile at j is already in flight in cn)
+    bool first = true;
+    for (; j < ncig; j += 64) {
         const uint32_t g = j + lane;
-        const uint32_t op = g < ncig ? cig[g] & 15u : 4u;
+        const uint32_t c = first ? cn : g < ncig ? cig[g] : 4u;
+        first = false;
+        racc += k0_refc(c);
+        if (trunc) continue;
+        const uint32_t op = c & 15u;
         const uint64_t stop = __ballot(op == 3u || op == 4u);
         const uint64_t bad = __ballot(op > 4u && g < ncig);
         const uint32_t fs = stop ? (uint32_t)__ffsll((long long)stop) - 1 : 64u;
         const uint32_t fb = bad ? (uint32_t)__ffsll((long long)bad) - 1 : 64u;
         if (fb < fs) return false;
         trunc = fs < 64;
-        j += 64;
     }
     return true;
 }
@@ -980,7 +1033,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
 
     K0Tgt t;
     bool okmm;
-    uint32_t nT = 0;
+    uint32_t nT = 0, mlq0 = 0xFFFFFFFFu, mlq1 = 0xFFFFFFFFu;
     bool implicit = false;
     K0_T0;
     // PF_K0_DIAG=4/2/3 (measurement only, results invalid): stop after the
@@ -993,6 +1046,18 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
         okmm = k0_mm_entries(gw, mmg, mis, mlen, mln, lane, t);
         if (okmm && t.nd > cap) okmm = false;       // only a malformed tag lists more calls than its size allows
         if (okmm && t.nd) {
+            // the first 512 ML values (8 per lane, packed) are loaded before
+            // the rank pass and arrive while it runs
+            if (mln) {
+                uint32_t q[8];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t j = min(lane + 64u * u, t.nd - 1);   // in the entry's ML slice (checked)
+                    q[u] = ml[t.ml + (uint64_t)j * t.nc + t.mi];
+                }
+                mlq0 = q[0] | (q[1] << 8) | (q[2] << 16) | (q[3] << 24);
+                mlq1 = q[4] | (q[5] << 8) | (q[6] << 16) | (q[7] << 24);
+            }
             k0_dw_table(L.u.mg.mV, lane);
             wsync();
             okmm = k0_mm_ranks(gw, mmg, mis, t, rev, TB, L.u.mg.mV, lane);
@@ -1001,9 +1066,10 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     wsync();
     bool past = false;
     if (okmm && t.nd) {                               // the C+m entry's ML values ride in the ranks' top byte
-#pragma unroll 4
-        for (uint32_t j = lane; j < t.nd; j += 64) {
-            const uint32_t q = mln ? ml[t.ml + (uint64_t)j * t.nc + t.mi] : 255u;
+        uint32_t u = 0;
+        for (uint32_t j = lane; j < t.nd; j += 64, u++) {
+            const uint32_t q = !mln ? 255u : u < 8 ? ((u < 4 ? mlq0 : mlq1) >> (8 * (u & 3))) & 0xFFu
+                                                   : (uint32_t)ml[t.ml + (uint64_t)j * t.nc + t.mi];
             const uint32_t sj = rev ? t.nd - 1 - j : j;
             const uint32_t rk = TB[sj];
             past |= rk >= (1u << 24);                 // l_qseq < 2^24: such a rank is past the read's C's
@@ -1051,7 +1117,8 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
 
     const uint32_t qs = d.pos[r];
     const bool stale = (cig[0] & 15u) == 4u && (TB[nT - 1] >> 2) <= (cig[0] >> 4);
-    bool fatal = false;
+    bool fatal = false, walked = false;
+    uint32_t racc = 0;                                // this lane's share of bam_endpos (the wave walk)
     if (stale || d.force_seq) {
         if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_SEQPATH], 1ull);
         K0Out s = o;
@@ -1060,7 +1127,8 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
         k0_bcast(o, s);
         fatal = uni(f ? 1u : 0u) != 0;
     } else {
-        fatal = !k0_walk<1>(d, L, cig, ncig, qs, rev, TB, nT, seq, len, implicit, lane, o);
+        fatal = !k0_walk<1>(d, L, cig, ncig, qs, rev, TB, nT, seq, len, implicit, lane, o, racc);
+        walked = true;
     }
     K0_STAMP(2);
     if (fatal) {
@@ -1087,12 +1155,11 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
             }
         }
     }
-    // bam_endpos: reference-consuming operations of the whole CIGAR
-    uint32_t rlen = 0;
-    for (uint32_t c = lane; c < ncig; c += 64) {
-        const uint32_t op = cig[c] & 15u;
-        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rlen += cig[c] >> 4;
-    }
+    // bam_endpos: reference-consuming operations of the whole CIGAR (summed
+    // by the wave walk; the lane-0 walk's records sum them here)
+    uint32_t rlen = racc;
+    if (!walked)
+        for (uint32_t c = lane; c < ncig; c += 64) rlen += k0_refc(cig[c]);
     rlen = wscan(rlen, lane);
     if (lane == 63) {
         d.rec_start[r] = qs;

@@ -131,3 +131,77 @@ def aln_cases():
         ("aln_dense_cpg", synth_aln(2, 30, 44, cpg_rate=0.12, len_scale=0.5)),
         ("aln60", synth_aln(2, 60, 45)),
     ]
+
+
+def mm_fuzz_batch(seed=17, n=160):
+    """Records whose MM/ML texts stress K0's tag parser: several entries
+    (h / ChEBI / m / combined codes, '.'/'?' or neither, a missing final ';'),
+    texts of 1-6 KB (entries and headers across the parser's 256-byte rows),
+    leading zeros, 8-9 digit counts (the SWAR fallback), bytes after the last
+    count, and malformed lists (an empty count, a stray byte before the last
+    comma, a trailing comma, ML too short).  Every record is CpG-rich so most
+    are kept; expected calls come from the oracle."""
+    rng = np.random.default_rng(seed)
+    recs = []
+    for i in range(n):
+        L = int(rng.integers(300, 9000))
+        # CpG-rich: a third of the positions start a CG
+        b = rng.choice(list("ACGT"), L)
+        cg = rng.random(L - 1) < 0.08
+        b[:-1][cg] = "C"
+        b[1:][cg] = "G"
+        seq = "".join(b)
+        rev = bool(rng.random() < 0.5)
+        tgt = "G" if rev else "C"
+        n_t = seq.count(tgt)
+        # skip list over the read's target bases (original orientation)
+        keep = np.flatnonzero(rng.random(n_t) < rng.uniform(0.05, 0.9))
+        d = np.diff(np.concatenate([[-1], keep])) - 1
+        skips = [str(x) for x in d.tolist()]
+        kind = rng.integers(0, 12)
+        if kind == 0 and skips:
+            skips[0] = "0" * int(rng.integers(1, 4)) + skips[0]              # leading zeros
+        if kind == 1 and skips:
+            skips[-1] = str(int(rng.integers(10_000_000, 999_999_999)))     # 8-9 digits (past the read)
+        if kind == 2 and len(skips) > 1:
+            skips[int(rng.integers(0, len(skips)))] = str(int(rng.integers(10_000_000, 99_999_999)))
+        lst = ",".join(skips)
+        tail = ""
+        if kind == 3:
+            tail = "x7"                                                      # bytes after the last count
+        if kind == 4 and len(skips) > 2:
+            j = lst.index(",", 1)
+            lst = lst[:j] + "x" + lst[j:]                                    # stray byte before a comma
+        if kind == 5 and len(skips) > 2:
+            j = lst.index(",", 1)
+            lst = lst[:j] + "," + lst[j:]                                    # an empty count
+        if kind == 6:
+            tail = ","                                                       # trailing comma
+        nd = len(skips)
+        pre, ml = "", []
+        hdr = "C+m" + ["?", ".", ""][int(rng.integers(0, 3))]
+        ncm = 1
+        lay = int(rng.integers(0, 4))
+        if lay == 1:                                                         # h entry first (dorado)
+            hl = ",".join(str(x) for x in rng.integers(0, 5, int(rng.integers(1, 900))))
+            pre = f"C+h?,{hl};"
+            ml += rng.integers(0, 256, hl.count(",") + 1).tolist()
+        elif lay == 2:                                                       # ChEBI code first
+            cl = ",".join(str(x) for x in rng.integers(0, 30, int(rng.integers(1, 300))))
+            pre = f"C+76792?,{cl};"
+            ml += rng.integers(0, 256, cl.count(",") + 1).tolist()
+        elif lay == 3:                                                       # combined codes
+            hdr = "C+hm?"
+            ncm = 2
+        end = "" if rng.random() < 0.1 else ";"
+        post = "" if rng.random() < 0.7 else "A+a?,1,2;"
+        mm = f"{pre}{hdr},{lst}{tail}{end}" + (post if end else "")
+        ml += rng.integers(0, 256, nd * ncm).tolist()
+        if kind == 7 and ml:
+            ml = ml[:-1]                                                     # ML too short
+        if kind == 8:
+            ml = []                                                          # no ML: 255 everywhere
+        if post and end:
+            ml += [1, 2]
+        recs.append(dict(seq=seq, cigar=f"{L}M", mm=mm, ml=ml, pos=10_000 + 20_000 * i, flag=16 if rev else 0))
+    return records_batch([(0, 10_000 + 20_000 * n, recs)])

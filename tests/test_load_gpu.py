@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from tests._aln_cases import HANDMADE, LOAD_CFG_SMALL, aln_cases, handmade_batch, records_batch
+from tests._aln_cases import HANDMADE, LOAD_CFG_SMALL, aln_cases, handmade_batch, mm_fuzz_batch, records_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -124,4 +124,16 @@ def test_scratch_trigger_lists(oracle_lib, gpu_ctx):
     big = np.diff(aln.ml_off.astype(np.int64)) > 2048
     assert big.any()
     db, _ = _check_calls(oracle_lib, gpu_ctx, Config.from_coverage(30, given=False), LoadConfig(), aln, "dense")
+    db.free()
+
+
+@pytest.mark.parametrize("seed", [17, 18, 19])
+def test_mm_parser_fuzz(oracle_lib, gpu_ctx, seed):
+    """MM/ML texts of 1-6 KB with every layout and malformation of
+    mm_fuzz_batch: K0's calls equal the oracle's record for record (kept or
+    dropped, positions, categories)."""
+    from pomfret_amd import Config
+    aln = mm_fuzz_batch(seed)
+    db, b = _check_calls(oracle_lib, gpu_ctx, Config(), LOAD_CFG_SMALL, aln, f"mm-fuzz{seed}")
+    assert 0 < db.n_reads < aln.n_recs
     db.free()

@@ -147,6 +147,39 @@ def test_greedy_pick_paths(oracle_lib, gpu_ctx, monkeypatch, path):
         db.free()
 
 
+@pytest.mark.parametrize("name,cfg,batch", CASES, ids=[c[0] for c in CASES])
+def test_dense_site_path(oracle_lib, gpu_ctx, monkeypatch, name, cfg, batch):
+    """K12's dense site path (HBM counters over the window's position range,
+    taken by windows whose range exceeds the LDS bitmaps or whose repeated
+    positions overflow the LDS hash: the big windows of a gap mix), forced on
+    every window of every case: identical results."""
+    monkeypatch.setenv("PF_K12_DENSE", "1")
+    ref = oracle_lib.methphase(cfg, batch, n_threads=8)
+    db = gpu_ctx.upload(cfg, batch)
+    out = db.run()
+    _compare(ref, out, name + "/dense")
+    db.free()
+
+
+def test_wide_windows_parity(oracle_lib, gpu_ctx):
+    """Windows whose call positions span more than 2^19 (the LDS bitmap
+    range): 400-500 kb gaps at 20x take the dense path without any override."""
+    from pomfret_amd import Config
+    from pomfret_amd.synth import SynthSpec, make_batch
+    cfg = Config.from_coverage(20, given=False)
+    b = make_batch(SynthSpec(n_windows=3, coverage=20, seed=41, gap=450_000))
+    span = [int(b.call_pos[b.read_call_off[b.win_read_off[w]]:b.read_call_off[b.win_read_off[w + 1]]].max()
+                - b.call_pos[b.read_call_off[b.win_read_off[w]]:b.read_call_off[b.win_read_off[w + 1]]].min())
+            for w in range(b.n_windows)]
+    assert min(span) >= 1 << 19, span
+    ref = oracle_lib.methphase(cfg, b, n_threads=8)
+    db = gpu_ctx.upload(cfg, b)
+    out = db.run()
+    _compare(ref, out, "wide")
+    assert (out.win_n_sites > 0).all()
+    db.free()
+
+
 @pytest.mark.parametrize("env", [{"PF_K12_CAP": "0"}, {"PF_K12_SMAX": "0"},
                                  {"PF_K12_CAP": "0", "PF_K2_ENTCAP": "0"}, {"PF_K12_CAP": "40"}],
                          ids=["all_reads_fallback", "no_lds_sites", "fallback_hbm_scratch", "mixed"])

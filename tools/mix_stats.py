@@ -59,6 +59,7 @@ if prof:
     p3 = raw[:W * 64].reshape(W, 2, 32)
     k3c = (p3[:, :, :12].sum(axis=2) + p3[:, :, 16:24].sum(axis=2)).astype(float)
     k12p = raw[W * 64:].reshape(W, 16)[:, 1:7].astype(float)
+    dz = raw[W * 64:].reshape(W, 16)[:, 0].astype(float)   # dense path: zero + atomics
     k12 = k12p.sum(axis=1)
     print("K12 cycles per window: p50 %.3g p90 %.3g max %.3g   K3 cycles per problem: p50 %.3g p90 %.3g max %.3g"
           % (np.median(k12), np.percentile(k12, 90), k12.max(), np.median(k3c), np.percentile(k3c, 90), k3c.max()))
@@ -70,6 +71,8 @@ if prof:
     big = gap >= 150e3
     print("K12 phases, cycles: mean small (<150 kb) | mean big | heaviest window")
     hw = int(np.argmax(k12))
+    print(f"  dense-path windows {(dz > 0).sum()}: zero+atomics cycles mean {dz[dz > 0].mean() if (dz > 0).any() else 0:.3g}, "
+          f"heaviest {dz[hw]:.3g}")
     for j in range(6):
         print(f"    {names12[j]:12s} {k12p[~big, j].mean():10.0f} | {k12p[big, j].mean():10.0f} | {k12p[hw, j]:10.0f}")
     # cycles vs gap: the tail's shape
