@@ -26,6 +26,7 @@ __global__ void pf_k2_methmers(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
 __global__ void pf_k3_wave(pf_dev_batch d);
 __global__ void pf_k3_fallback(pf_dev_batch d);
+__global__ void pf_k3_heavy(pf_dev_batch d);
 __global__ void pf_k0_load(pf_load_dev d);
 __global__ void pf_k0_scan(pf_load_dev d);
 __global__ void pf_k0_pack(pf_load_dev d);
@@ -47,9 +48,11 @@ static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k0_pack", "pf_k12_site
 struct pf_ctx {
     int device;
     hipStream_t stream;
+    hipStream_t stream2;      /* the heavy greedy problems, beside the main greedy kernel */
     hipEvent_t ev[PF_NKERN + 1];
     float last_ms[PF_NKERN];
     int have_times;
+    float heavy_ms;           /* last run's pf_k3_heavy time (-1: not launched) */
     int k3_block;             /* last run's main greedy kernel: 1 the 256-thread build, 0 the one-wave build */
     float haptag_ms;          /* last pf_haptag_reads kernel time */
     const char *haptag_name;  /* and the kernel that ran */
@@ -83,6 +86,9 @@ struct pf_dbatch {
     uint64_t io_bytes = 0;
     hipEvent_t ev[PF_SLOTS][PF_NKERN + 1];   // kernel boundaries per slot
     hipEvent_t done[PF_SLOTS];               // slot's D2H complete
+    hipEvent_t hev[PF_SLOTS][2];             // pf_k3_heavy's boundaries on the context's second stream
+    uint32_t n_heavy = 0;                    // k3_order's first n_heavy problems run in pf_k3_heavy
+    bool heavy_launched[PF_SLOTS] = {false, false};
     int have_ev = 0;
     uint64_t n_launch = 0, n_finish = 0;
     uint64_t site_total;
@@ -171,6 +177,8 @@ extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
     pf_ctx *c = new pf_ctx();
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    c->heavy_ms = -1.0f;
     for (int i = 0; i <= PF_NKERN; i++) HIPCHK(hipEventCreate(&c->ev[i]));
     c->have_times = 0;
     c->have_haptag = 0;
@@ -249,6 +257,7 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     (void)hipStreamSynchronize(c->stream);
     for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->stream2);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->dws) (void)hipFree(c->dws);
@@ -353,6 +362,7 @@ extern "C" void pf_batch_free(pf_dbatch_t *b) {
         for (int i = 0; i < PF_SLOTS; i++) {
             for (int k = 0; k <= PF_NKERN; k++) (void)hipEventDestroy(b->ev[i][k]);
             (void)hipEventDestroy(b->done[i]);
+            for (int k = 0; k < 2; k++) (void)hipEventDestroy(b->hev[i][k]);
         }
     delete b;
 }
@@ -532,6 +542,24 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             return in->win_read_off[a + 1] - in->win_read_off[a] > in->win_read_off[c + 1] - in->win_read_off[c];
         });
         PUT(p, word.data(), word.size()); d.k12_order = p;
+        // Heavy problems: windows with at least twice the median reads (and
+        // >= 600).  They lead k3_order, and run in pf_k3_heavy on the
+        // context's second stream beside the main greedy kernel, starting at
+        // once with the fallback's LDS budget instead of being deferred to the
+        // fallback kernel after it (the serial tail of a gap mix: ~200 problems
+        // of 1,000-1,400 reads, ~5 ms each).  PF_K3_HEAVY=n forces the n
+        // heaviest problems (tests; 0 disables the split).
+        if (W) {
+            std::vector<uint32_t> rw(W);
+            for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
+            std::nth_element(rw.begin(), rw.begin() + W / 2, rw.end());
+            const uint32_t thr = std::max<uint32_t>(600u, 2u * rw[W / 2]);
+            uint32_t nh = 0;
+            while (nh < 2 * W && in->win_read_off[(ord[nh] >> 1) + 1] - in->win_read_off[ord[nh] >> 1] >= thr) nh++;
+            const char *hv = getenv("PF_K3_HEAVY");
+            if (hv) nh = std::min<uint32_t>((uint32_t)atoi(hv), 2 * W);
+            b->n_heavy = nh;
+        }
     }
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
     ALLOC(d.k3_fb_list, std::max<uint32_t>(2 * W, 1));
@@ -616,6 +644,8 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         for (int k = 0; k <= PF_NKERN; k++)
             if (hipEventCreate(&b->ev[i][k]) != hipSuccess) return fail(PF_ERR_HIP);
         if (hipEventCreate(&b->done[i]) != hipSuccess) return fail(PF_ERR_HIP);
+        for (int k = 0; k < 2; k++)
+            if (hipEventCreate(&b->hev[i][k]) != hipSuccess) return fail(PF_ERR_HIP);
     }
     b->have_ev = 1;
     *out = b;
@@ -922,6 +952,9 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         if (e == hipSuccess)
             e = hipFuncSetAttribute((const void *)pf_k3_fallback, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)d.lds_fb);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)pf_k3_heavy, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)d.lds_fb);
         if (e != hipSuccess) {
             fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u / %u B dynamic LDS): %s\n", d.lds_bytes,
                     d.lds_fb, hipGetErrorString(e));
@@ -969,9 +1002,21 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         const char *impl = getenv("PF_K3_IMPL");
         c->k3_block = !(impl && strcmp(impl, "wave") == 0);
     }
-    if (c->k3_block)
-        hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W), dim3(PF_K3_THREADS), d.lds_bytes, st, d);
-    else
+    const uint32_t nh = c->k3_block ? b->n_heavy : 0u;
+    if (nh) {
+        // the heavy problems on the second stream, from the same point (K2 done)
+        HIPCHK(hipStreamWaitEvent(c->stream2, b->ev[slot][4], 0));
+        HIPCHK(hipEventRecord(b->hev[slot][0], c->stream2));
+        hipLaunchKernelGGL(pf_k3_heavy, dim3(nh), dim3(PF_K3_THREADS), d.lds_fb, c->stream2, d);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(b->hev[slot][1], c->stream2));
+    }
+    if (c->k3_block) {
+        pf_dev_batch dl = d;
+        dl.k3_order = d.k3_order + nh;
+        if (2 * b->W > nh)
+            hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W - nh), dim3(PF_K3_THREADS), d.lds_bytes, st, dl);
+    } else
         hipLaunchKernelGGL(pf_k3_wave, dim3(2 * b->W), dim3(64), d.lds_w, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][5], st));
@@ -980,6 +1025,8 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
                        st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][6], st));
+    if (nh) HIPCHK(hipStreamWaitEvent(st, b->hev[slot][1], 0));   // join: the heavy problems are done
+    b->heavy_launched[slot] = nh != 0;
     HIPCHK(hipMemcpyAsync(b->h_io[slot], b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(b->done[slot], st));
     return PF_OK;
@@ -1093,6 +1140,8 @@ extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_
         if (b->W) {
             for (int i = 0; i < PF_NKERN; i++)
                 (void)hipEventElapsedTime(&c->last_ms[i], b->ev[slot][i], b->ev[slot][i + 1]);
+            c->heavy_ms = -1.0f;
+            if (b->heavy_launched[slot]) (void)hipEventElapsedTime(&c->heavy_ms, b->hev[slot][0], b->hev[slot][1]);
             (void)hipGetLastError();               // a failed timing query must not fail a later launch check
             c->have_times = 1;
         }
@@ -1230,12 +1279,16 @@ extern "C" void pf_ctx_set_haptag_ms(pf_ctx *c, float ms, const char *name) {
 
 extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n) {
     if (!ctx || !n) return PF_ERR_ARG;
-    const int tot = PF_NKERN + (ctx->have_haptag ? 1 : 0);
+    const int hv = ctx->heavy_ms >= 0.0f ? 1 : 0;
+    const int tot = PF_NKERN + hv + (ctx->have_haptag ? 1 : 0);
     int m = *n < tot ? *n : tot;
     for (int i = 0; i < m; i++) {
         if (i < PF_NKERN) {
             if (names) names[i] = (i == 4 && ctx->k3_block) ? "pf_k3_greedy" : k_names[i];
             if (ms) ms[i] = ctx->have_times ? ctx->last_ms[i] : -1.0f;
+        } else if (i == PF_NKERN && hv) {
+            if (names) names[i] = "pf_k3_heavy";
+            if (ms) ms[i] = ctx->heavy_ms;
         } else {
             if (names) names[i] = ctx->haptag_name;
             if (ms) ms[i] = ctx->haptag_ms;

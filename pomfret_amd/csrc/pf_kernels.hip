@@ -3003,6 +3003,16 @@ __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     k3_run<false>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes);
 }
 
+// The heavy problems (k3_order's first n, pf_api.hip): the fallback's build
+// and LDS budget, launched on a second stream beside the main kernel.
+__global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_heavy(pf_dev_batch d) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ K3Ctl ctl;
+    __shared__ K3Cand cd;
+    __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
+    k3_run<true>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_fb);
+}
+
 // Problems the main kernel deferred (dictionary or tables beyond the LDS
 // budget, n_cand > 64, >= 8192 sites, test overrides): all variants.
 __global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_fallback(pf_dev_batch d) {

@@ -161,6 +161,22 @@ def test_dense_site_path(oracle_lib, gpu_ctx, monkeypatch, name, cfg, batch):
     db.free()
 
 
+@pytest.mark.parametrize("name,cfg,batch", CASES, ids=[c[0] for c in CASES])
+def test_heavy_problem_split(oracle_lib, gpu_ctx, monkeypatch, name, cfg, batch):
+    """The heaviest greedy problems in pf_k3_heavy on the context's second
+    stream, beside the main kernel (PF_K3_HEAVY forces the 3 heaviest): the
+    same results, and the heavy kernel reports its time."""
+    monkeypatch.setenv("PF_K3_HEAVY", "3")
+    ref = oracle_lib.methphase(cfg, batch, n_threads=8)
+    db = gpu_ctx.upload(cfg, batch)
+    out = db.run()
+    _compare(ref, out, name + "/heavy")
+    assert "pf_k3_heavy" in gpu_ctx.kernel_times()
+    out2 = db.run()                                  # pipelined slots reuse the events
+    _compare(ref, out2, name + "/heavy-rerun")
+    db.free()
+
+
 def test_wide_windows_parity(oracle_lib, gpu_ctx):
     """Windows whose call positions span more than 2^19 (the LDS bitmap
     range): 400-500 kb gaps at 20x take the dense path without any override."""
