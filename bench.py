@@ -55,7 +55,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algo_bytes(batch, stats, n_sites):
+def algo_bytes(batch, stats, n_sites, heavy=()):
     """Algorithmic bytes per launch of each kernel.
 
     K12 sites + methmers (fused; the K2 kernel only takes fallback reads,
@@ -77,9 +77,16 @@ def algo_bytes(batch, stats, n_sites):
     k1 = 5 * N + 9 * S
     k2 = 2 * 5 * N + 8 * mmr          # calls read per direction + sites read / methmers written
     k3 = 12 * lookups + 8 * inserts + scanned + 2 * strict
+    # the problems pf_k3_heavy runs (pf_batch_heavy) are credited to it
+    hv = np.zeros(stats.shape[:2], bool)
+    for p in heavy:
+        hv[int(p) >> 1, int(p) & 1] = True
+    st_h = stats[hv]
+    k3h = int(12 * st_h[:, 0].sum() + 8 * st_h[:, 1].sum() + st_h[:, 3].sum() + 2 * st_h[:, 5].sum()) if len(st_h) else 0
     # fallback kernels (pf_k2_methmers, pf_k3_fallback) take the rare oversize reads
     # and problems, none on this workload: credited 0 B
-    return {"pf_k12_sites_methmers": k1 + k2, "pf_k2_methmers": 0, "pf_k3_greedy": k3, "pf_k3_fallback": 0}
+    return {"pf_k12_sites_methmers": k1 + k2, "pf_k2_methmers": 0, "pf_k3_greedy": k3 - k3h, "pf_k3_heavy": k3h,
+            "pf_k3_fallback": 0}
 
 
 def k0_bytes(aln, read_recs, n_calls):
@@ -535,7 +542,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     stats = db.stats()
     kmean = {k: v / args.steps for k, v in kern_acc.items()}
-    ab = algo_bytes(batch, stats, out.win_n_sites)
+    ab = algo_bytes(batch, stats, out.win_n_sites, db.heavy_problems())
     if record_level:
         ab["pf_k0_load"] = k0_bytes(aln, rr, batch.n_calls)
         ab["pf_k0_pack"] = pack_bytes(aln.n_recs, batch.n_reads, batch.n_calls)

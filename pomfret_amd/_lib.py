@@ -55,6 +55,7 @@ def lib():
         L.pf_last_kernel_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p),
                                            C.POINTER(C.c_float), C.POINTER(C.c_int)]
         L.pf_batch_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.pf_batch_heavy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
         L.pf_batch_debug_sites.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_uint32]
         L.pf_batch_debug_methmers.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
@@ -459,6 +460,14 @@ class DeviceBatch:
         out = np.zeros((max(self.n_windows, 1), 2, 8), np.uint64)
         _check(lib().pf_batch_stats(self.handle, out.ctypes.data, out.size), "pf_batch_stats")
         return out[:self.n_windows]
+
+    def heavy_problems(self) -> np.ndarray:
+        """Greedy problems (w<<1 | dir) run in pf_k3_heavy (see pf_batch_heavy)."""
+        n = lib().pf_batch_heavy(self.handle, None, 0)
+        out = np.zeros(max(n, 1), np.uint32)
+        if n:
+            lib().pf_batch_heavy(self.handle, out.ctypes.data, n)
+        return out[:n]
 
     def debug_sites(self, w: int, direction: int, cap: int = 1 << 22):
         real = np.zeros(cap, np.uint32)

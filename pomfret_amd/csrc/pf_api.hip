@@ -88,6 +88,7 @@ struct pf_dbatch {
     hipEvent_t done[PF_SLOTS];               // slot's D2H complete
     hipEvent_t hev[PF_SLOTS][2];             // pf_k3_heavy's boundaries on the context's second stream
     uint32_t n_heavy = 0;                    // k3_order's first n_heavy problems run in pf_k3_heavy
+    std::vector<uint32_t> h_heavy;           // and those problems
     bool heavy_launched[PF_SLOTS] = {false, false};
     int have_ev = 0;
     uint64_t n_launch = 0, n_finish = 0;
@@ -559,6 +560,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             const char *hv = getenv("PF_K3_HEAVY");
             if (hv) nh = std::min<uint32_t>((uint32_t)atoi(hv), 2 * W);
             b->n_heavy = nh;
+            b->h_heavy.assign(ord.begin(), ord.begin() + nh);
         }
     }
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
@@ -1015,7 +1017,7 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         pf_dev_batch dl = d;
         dl.k3_order = d.k3_order + nh;
         if (2 * b->W > nh)
-            hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W - nh), dim3(PF_K3_THREADS), d.lds_bytes, st, dl);
+            hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W - nh), dim3(PF_K3S_THREADS), d.lds_bytes, st, dl);
     } else
         hipLaunchKernelGGL(pf_k3_wave, dim3(2 * b->W), dim3(64), d.lds_w, st, d);
     HIPCHK(hipGetLastError());
@@ -1263,6 +1265,12 @@ extern "C" int pf_batch_stats(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
     if (b->W) HIPCHK(hipMemcpy(out, b->d.stats, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return PF_OK;
+}
+
+extern "C" int pf_batch_heavy(const pf_dbatch_t *b, uint32_t *probs, uint32_t cap) {
+    if (!b) return PF_ERR_ARG;
+    for (uint32_t i = 0; i < b->n_heavy && i < cap && probs; i++) probs[i] = b->h_heavy[i];
+    return (int)b->n_heavy;
 }
 
 extern "C" int pf_batch_prof(pf_dbatch_t *b, uint64_t *out, uint64_t n) {

@@ -1662,22 +1662,22 @@ DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
 // insert_mmr_counts of one tagged read (hap tg) by the whole workgroup: its
 // sites are distinct, so a plain read-modify-write per site; only hap tg's
 // divisor entry changes (its total becomes >= 1, so no zero case)
-template <bool SLDS>
+template <bool SLDS, int NT = PF_K3_THREADS>
 DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint32_t mo, uint32_t tg) {
     const uint32_t inc = tg ? 0x10000u : 1u, sh = tg ? 16u : 0u;
     float *srf = reinterpret_cast<float *>(m.srec) + tg;   // (h_tg, -, 1/h_tg, -) of site 0
-    for (uint32_t tb = 0; tb < n; tb += 2 * PF_K3_THREADS) {
+    for (uint32_t tb = 0; tb < n; tb += 2 * NT) {
         uint32_t sl[2], cc[2], sv[2];
         bool ok[2];
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const uint32_t t = tb + u * PF_K3_THREADS + threadIdx.x;
+            const uint32_t t = tb + u * NT + threadIdx.x;
             ok[u] = t < n && st + t < S;
             sl[u] = k3_slot_raw<SLDS>(m, ok[u] ? mo + t : 0u);
         }
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const uint32_t t = tb + u * PF_K3_THREADS + threadIdx.x;
+            const uint32_t t = tb + u * NT + threadIdx.x;
             ok[u] = ok[u] && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
             cc[u] = m.cnt[ok[u] ? sl[u] : 0u];
             sv[u] = m.sum[ok[u] ? st + t : 0u];
@@ -1686,7 +1686,7 @@ DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             if (ok[u]) {
-                const uint32_t site = st + tb + u * PF_K3_THREADS + threadIdx.x;
+                const uint32_t site = st + tb + u * NT + threadIdx.x;
                 const uint32_t s2 = sv[u] + inc;
                 const float f = (float)((s2 >> sh) & 0xffffu);
                 m.cnt[sl[u]] = cc[u] + inc;
@@ -1828,7 +1828,7 @@ DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t 
 // state, slot-list offsets (and the u16 LDS copy), reference reads seeding the
 // counts (insert_ref_reads_methmer_counts, :3776-3810), the initial range,
 // the T5 round trip and the untagged bitmask.
-template <bool SLDS>
+template <bool SLDS, int NT = PF_K3_THREADS>
 DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
                  const K3Mem &m, K3Ctl &ctl, uint32_t *sh_scan, K3Stats &stx) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
@@ -1841,9 +1841,9 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
     const uint32_t *kb = d.keys + kbase;
     uint32_t sum_mmr = 0, mx_mmr = 0;
     // ---- init tables and per-read state
-    for (uint32_t j = tid; j < ntot; j += PF_K3_THREADS) m.cnt[j] = 0;
-    for (uint32_t j = tid; j < S; j += PF_K3_THREADS) m.sum[j] = 0;
-    for (uint32_t i = tid; i < R; i += PF_K3_THREADS) {
+    for (uint32_t j = tid; j < ntot; j += NT) m.cnt[j] = 0;
+    for (uint32_t j = tid; j < S; j += NT) m.sum[j] = 0;
+    for (uint32_t i = tid; i < R; i += NT) {
         const uint32_t r = r0 + i;
         const uint32_t st = d.read_start[r], en = d.read_end[r];
         uint32_t f = 0;
@@ -1882,16 +1882,16 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
     // slot-list offsets: LDS copy (prefix sum of mn) or the HBM arena
     if (SLDS) {
         uint32_t carry = 0;
-        for (uint32_t i0 = 0; i0 < R; i0 += PF_K3_THREADS) {
+        for (uint32_t i0 = 0; i0 < R; i0 += NT) {
             const uint32_t i = i0 + tid;
             const uint32_t v = i < R ? m.mn[i] : 0;
             uint32_t tot;
-            const uint32_t ex = block_excl_scan<PF_K3_THREADS>(v, sh_scan, &tot);
+            const uint32_t ex = block_excl_scan<NT>(v, sh_scan, &tot);
             if (i < R) m.mo[i] = carry + ex;
             carry += tot;
         }
         __syncthreads();
-        for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
+        for (uint32_t i = wid; i < R; i += (NT / 64)) {
             const uint32_t g = 2 * (r0 + i) + dir;
             const uint32_t *src = kb + (d.mmr_off[g] - kbase);
             uint16_t *dst = m.sl16 + m.mo[i];
@@ -1902,14 +1902,14 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
             }
         }
     } else {
-        for (uint32_t i = tid; i < R; i += PF_K3_THREADS)
+        for (uint32_t i = tid; i < R; i += NT)
             m.mo[i] = (uint32_t)(d.mmr_off[2ull * (r0 + i) + dir] - kbase);
     }
     __syncthreads();
     // ---- reference reads seed the counts (insert_ref_reads_methmer_counts, :3776-3810)
     const uint32_t refbit = dir == 0 ? FLG_LEFT : FLG_RIGHT;
     uint32_t ref_ins = 0;
-    for (uint32_t i = wid; i < R; i += PF_K3_WAVES) {
+    for (uint32_t i = wid; i < R; i += (NT / 64)) {
         const uint32_t hp = m.hp[i];
         if (!(m.flg[i] & refbit) || hp > 1) continue;
         const uint32_t n = m.mn[i], st = m.mst[i], mo = m.mo[i];
@@ -1928,25 +1928,25 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
     if (sum_mmr) atomicAdd(&ctl.summ, sum_mmr);
     if (mx_mmr) atomicMax(&ctl.mxlen, mx_mmr);
     __syncthreads();
-    for (uint32_t j = tid; j < S; j += PF_K3_THREADS) m.srec[j] = site_rec(m.sum[j]);
+    for (uint32_t j = tid; j < S; j += NT) m.srec[j] = site_rec(m.sum[j]);
     if (wid == 0) k3_range_update(m.sum, S, cov_rt, ctl, lane);
     // ---- step 1.5 (:4010-4025): all reads unphased, ref reads restored through
     // the (readID<<2)|hp round trip (hp >= 4 lands on readID|(hp>>2)); the last
     // writer in reference order wins.
-    for (uint32_t i = tid; i < R; i += PF_K3_THREADS) {
+    for (uint32_t i = tid; i < R; i += NT) {
         if (m.flg[i] & refbit) {
             const uint32_t t = i | ((uint32_t)m.hp[i] >> 2);
             if (t < R) atomicMax(&m.aux[t], i + 1);
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < R; i += PF_K3_THREADS) {
+    for (uint32_t i = tid; i < R; i += NT) {
         const uint32_t lw = m.aux[i];
         m.hp[i] = lw ? (uint8_t)(d.read_hp[r0 + lw - 1] & 3) : (uint8_t)2;
     }
     __syncthreads();
     // untagged bitmask in scan order (dir 0: read order, dir 1: revbuf order)
-    for (uint32_t j = wid; j < nwords; j += PF_K3_WAVES) {
+    for (uint32_t j = wid; j < nwords; j += (NT / 64)) {
         const uint32_t p = j * 64 + lane;
         bool u = false;
         if (p < R) {
@@ -2039,9 +2039,9 @@ DEV void k3_range_regs(const K3Mem &m, uint32_t S, int cov_rt, uint32_t lane, ui
 // redundantly -- identical register copies of the candidate list, the queue
 // and the range -- so nothing is published between waves; two barriers per
 // iteration: after the term fill (B) and after the winner's insert (X).
-template <bool SLDS>
+template <bool SLDS, int NT = PF_K3_THREADS>
 DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
-                        const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan) {
+                        const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan, uint32_t *qb) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
     const int cov_rt = d.win_par[w * 4 + 1];
     const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
@@ -2051,7 +2051,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     unsigned long long prof_acc[32] = {0};
     unsigned long long prof_last = k3_stamp_now();
 #endif
-    k3_init<SLDS>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
+    k3_init<SLDS, NT>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
     K3_STAMP(0);
     int il = uni_i(ctl.i_last);
     uint32_t failed = 0;
@@ -2062,14 +2062,14 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     uint32_t q_cnt = 0, q_head = 0;
     bool q_more = false;
     int q_cont = 0;
-    uint32_t *qbuf = cd.read + 64 * wid;                 // per-wave queue scratch
+    uint32_t *qbuf = qb + 64 * wid;                      // per-wave queue scratch
     uint32_t lsum = 0;
     bool need_collect = true, have_win = false;
     // per-candidate totals, double-buffered by iteration parity: exact fp64
     // hap sums [2][128] and push/positive count pairs [2][64]
     double *accd = reinterpret_cast<double *>(cd.key);
     uint32_t *lcp = cd.pos;
-    accd[tid] = 0.0;
+    if (tid < 256) accd[tid] = 0.0;
     if (tid < 128) lcp[tid] = 0u;
     uint32_t par = 0;
     __syncthreads();
@@ -2152,7 +2152,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             const uint32_t lgn = 31 - __clz(ncp);
             const uint32_t G = 64u >> lgn;
             const uint32_t fc = lane & (ncp - 1), fj = lane >> lgn;
-            const uint32_t J = wid * G + fj, GS = PF_K3_WAVES * G;
+            const uint32_t J = wid * G + fj, GS = (NT / 64) * G;
             const uint32_t f_lo = (uint32_t)__shfl((int)c_lo, (int)fc, 64);
             const uint32_t f_len = (uint32_t)__shfl((int)c_len, (int)fc, 64);
             const uint32_t f_kofs = (uint32_t)__shfl((int)c_kofs, (int)fc, 64);
@@ -2238,7 +2238,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // ---- insert_mmr_counts of the winner, the whole workgroup (after every
         // wave's fold, if the pick needed one, has read the tables)
         if (folded) __syncthreads();
-        k3_insert_all<SLDS>(m, S, n, st, mo, tg);
+        k3_insert_all<SLDS, NT>(m, S, n, st, mo, tg);
         have_win = true;
         K3_STAMP(21);
         __syncthreads();                                           // (X)
@@ -2869,9 +2869,12 @@ DEV void k3_defer(const pf_dev_batch &d, uint32_t prob) {
 // false is the main kernel's slim build: slot dictionary and lists in LDS,
 // n_cand <= 64 (register candidate list), < 8192 sites (exact-interval pick
 // only); anything else is deferred to the FULL build.
-template <bool FULL>
+template <bool FULL, int NT = PF_K3_THREADS>
 DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan,
-                const uint32_t lds) {
+                const uint32_t lds, uint32_t *qb = nullptr) {
+    // qb: per-wave queue scratch of the slim loop, 64 entries per wave; the
+    // kernels that pass none (fallback, heavy: 256 threads) use cd.read
+    static_assert(NT <= PF_MAX_NCAND || NT == PF_K3S_THREADS, "cd.read holds 64 entries per wave");
     const uint32_t tid = threadIdx.x;
     const uint32_t w = prob >> 1, dir = prob & 1;
     const uint32_t S = d.win_S[w];
@@ -2918,13 +2921,13 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
         masks = reinterpret_cast<uint64_t *>(g);
         mbase = reinterpret_cast<uint32_t *>(g + align16(8ull * S * MW));
     }
-    k3_dict(d, r0, R, S, dir, masks, mbase, sh_scan, ctl);
+    k3_dict<NT>(d, r0, R, S, dir, masks, mbase, sh_scan, ctl);
     const uint32_t ntot = uni(ctl.ntot);
     // sum of methmers over the window's reads (slot-list size)
     uint32_t summ = 0;
-    for (uint32_t i = tid; i < R; i += PF_K3_THREADS) summ += d.mmr_n[2ull * (r0 + i) + dir];
+    for (uint32_t i = tid; i < R; i += NT) summ += d.mmr_n[2ull * (r0 + i) + dir];
     uint32_t summ_tot;
-    block_excl_scan<PF_K3_THREADS>(summ, sh_scan, &summ_tot);
+    block_excl_scan<NT>(summ, sh_scan, &summ_tot);
 
     // ---- P2: greedy.  Prefer everything in LDS (u16 slot lists), then LDS
     // tables with slot lists read from the HBM arena, then all in HBM.  The
@@ -2940,18 +2943,18 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
         k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
         return;
     }
-    k3_dict_rewrite(d, r0, R, S, dir, masks, mbase);
+    k3_dict_rewrite<NT>(d, r0, R, S, dir, masks, mbase);
     const uint32_t *kb = d.keys + kbase;
     if (slim_fit) {
         K3Mem m;
         if (slots_ok && slim_s <= lds) {
             (void)k3_layout(S, ntot, R, dir, summ_tot, true, 0, off);
             k3_mem(smem, off, 0, true, kb, m);
-            k3_greedy_slim<true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+            k3_greedy_slim<true, NT>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qb ? qb : cd.read);
         } else {
             (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off);
             k3_mem(smem, off, 0, false, kb, m);
-            k3_greedy_slim<false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
+            k3_greedy_slim<false, NT>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qb ? qb : cd.read);
         }
         return;
     }
@@ -2995,12 +2998,16 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
 }
 
 // Main greedy kernel: every problem, heaviest first (k3_order); the slim build.
-__global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_greedy(pf_dev_batch d) {
+// 512 threads (round 3; 256 before): the greedy loop's control runs
+// redundantly in every wave, so more waves shorten only the parallel parts
+// of an iteration (the term fill, the winner's insert) -- its latency chain.
+__global__ __launch_bounds__(PF_K3S_THREADS) __attribute__((amdgpu_waves_per_eu(6))) void pf_k3_greedy(pf_dev_batch d) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ K3Ctl ctl;
     __shared__ K3Cand cd;
-    __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
-    k3_run<false>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes);
+    __shared__ uint32_t sh_scan[PF_K3S_THREADS / 64 + 1];
+    __shared__ uint32_t qb[PF_K3S_THREADS];              // per-wave queue scratch
+    k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes, qb);
 }
 
 // The heavy problems (k3_order's first n, pf_api.hip): the fallback's build
