@@ -23,7 +23,7 @@
 #define PF_K2_ENT_CAP 1024        /* per-wave LDS entry buffer; larger reads use HBM scratch */
 #define PF_K3_THREADS 256
 #define PF_K3_WAVES (PF_K3_THREADS / PF_WAVE)
-#define PF_K3S_THREADS 512         /* the main (slim) greedy kernel */
+#define PF_K3S_THREADS 256         /* the main (slim) greedy kernel (512 measured: DESIGN.md 8) */
 #define PF_MAX_NCAND 256
 #define PF_K12_CAPW 512           /* per-wave site-entry buffer of the fused methmer phase */
 #define PF_K12_WB 8               /* bytes per wave-buffer entry: chars, crank, u16 irank, u32 staged key */

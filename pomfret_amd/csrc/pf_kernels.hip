@@ -2998,16 +2998,25 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
 }
 
 // Main greedy kernel: every problem, heaviest first (k3_order); the slim build.
-// 512 threads (round 3; 256 before): the greedy loop's control runs
-// redundantly in every wave, so more waves shorten only the parallel parts
-// of an iteration (the term fill, the winner's insert) -- its latency chain.
-__global__ __launch_bounds__(PF_K3S_THREADS) __attribute__((amdgpu_waves_per_eu(6))) void pf_k3_greedy(pf_dev_batch d) {
+// PF_K3S_THREADS threads per problem.  The greedy loop's control runs
+// redundantly in every wave, so more waves shorten only the parallel parts of
+// an iteration (the term fill, the winner's insert); 512 threads were measured
+// in round 3 (50 kb batch 5.25 -> 4.96 ms, gap mix 7.3 -> 10.3 ms: register-
+// limited to two problems per CU; with 6 waves per SIMD forced, spills, 5.48 /
+// 11.2 ms) and 256 kept.
+__global__ __launch_bounds__(PF_K3S_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ K3Ctl ctl;
     __shared__ K3Cand cd;
     __shared__ uint32_t sh_scan[PF_K3S_THREADS / 64 + 1];
-    __shared__ uint32_t qb[PF_K3S_THREADS];              // per-wave queue scratch
-    k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes, qb);
+    if constexpr (PF_K3S_THREADS > PF_MAX_NCAND) {
+        __shared__ uint32_t qb[PF_K3S_THREADS];          // per-wave queue scratch beyond cd.read
+        k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes, qb);
+    } else {
+        // no extra static LDS: two 72 KB problems plus their static LDS fill a
+        // CU's 160 KB exactly (1 KB more halves the main kernel's occupancy)
+        k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes);
+    }
 }
 
 // The heavy problems (k3_order's first n, pf_api.hip): the fallback's build
