@@ -870,19 +870,27 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
                 }
                 return mine;
             };
-            const uint64_t cend = C0 + (ncall + NT - 1) / NT * NT;   // whole waves in every pass
+            const uint64_t cend4 = C0 + (ncall + 4 * NT - 1) / (4 * NT) * (4 * NT);   // whole waves in every pass
             for (uint64_t sup = 0; sup < span; sup += (uint64_t)MAXCH << CHB) {
                 const uint32_t nch = (uint32_t)min<uint64_t>((span - sup + CH - 1) >> CHB, MAXCH);
                 const uint64_t slim = min<uint64_t>((uint64_t)nch << CHB, span - sup);
                 for (uint32_t j = tid; j <= nch; j += NT) { coff[j] = 0; cfill[j] = 0; }
                 __syncthreads();
-                // A: calls per chunk
-                for (uint64_t c = C0 + tid; c < cend; c += NT) {
-                    const bool in = c < C1;
-                    const uint32_t cat = in ? d.call_cat[c] : 2u;
-                    const uint64_t rel = in ? (uint64_t)(d.call_pos[c] - pmin) - sup : ~0ull;
-                    const bool act = cat < 2 && rel < slim;
-                    chunk_add(act, act ? (uint32_t)(rel >> CHB) : 0u, coff, false);
+                // A: calls per chunk (four calls per thread per step, loads first)
+                for (uint64_t c0 = C0 + tid; c0 < cend4; c0 += 4ull * NT) {
+                    uint32_t cat4[4], pos4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint64_t c = c0 + (uint64_t)u * NT;
+                        cat4[u] = c < C1 ? d.call_cat[c] : 2u;
+                        pos4[u] = c < C1 ? d.call_pos[c] : pmin;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint64_t rel = (uint64_t)(pos4[u] - pmin) - sup;
+                        const bool act = cat4[u] < 2 && rel < slim;
+                        chunk_add(act, act ? (uint32_t)(rel >> CHB) : 0u, coff, false);
+                    }
                 }
                 __syncthreads();
                 // chunk offsets (exclusive scan, 8 chunks per thread)
@@ -898,14 +906,22 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
                 }
                 __syncthreads();
                 // C: scatter the calls into their chunks' lists
-                for (uint64_t c = C0 + tid; c < cend; c += NT) {
-                    const bool in = c < C1;
-                    const uint32_t cat = in ? d.call_cat[c] : 2u;
-                    const uint64_t rel = in ? (uint64_t)(d.call_pos[c] - pmin) - sup : ~0ull;
-                    const bool act = cat < 2 && rel < slim;
-                    const uint32_t ch = act ? (uint32_t)(rel >> CHB) : 0u;
-                    const uint32_t slot = chunk_add(act, ch, cfill, true);
-                    if (act) sc[coff[ch] + slot] = (uint16_t)(((uint32_t)rel & (CH - 1)) | (cat << 15));
+                for (uint64_t c0 = C0 + tid; c0 < cend4; c0 += 4ull * NT) {
+                    uint32_t cat4[4], pos4[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint64_t c = c0 + (uint64_t)u * NT;
+                        cat4[u] = c < C1 ? d.call_cat[c] : 2u;
+                        pos4[u] = c < C1 ? d.call_pos[c] : pmin;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint64_t rel = (uint64_t)(pos4[u] - pmin) - sup;
+                        const bool act = cat4[u] < 2 && rel < slim;
+                        const uint32_t ch = act ? (uint32_t)(rel >> CHB) : 0u;
+                        const uint32_t slot = chunk_add(act, ch, cfill, true);
+                        if (act) sc[coff[ch] + slot] = (uint16_t)(((uint32_t)rel & (CH - 1)) | (cat4[u] << 15));
+                    }
                 }
                 __threadfence();                         // the lists are read back through L2 (L1 invalidated)
                 __syncthreads();
@@ -915,9 +931,13 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
                     if (l1 == l0) continue;                  // uniform: no calls, no site
                     for (uint32_t j = tid; j < CH / 4; j += NT) reinterpret_cast<uint4 *>(ccnt)[j] = make_uint4(0, 0, 0, 0);
                     __syncthreads();
-                    for (uint32_t t = l0 + tid; t < l1; t += NT) {
-                        const uint32_t v = sc[t];
-                        atomicAdd(&ccnt[v & (CH - 1)], (v >> 15) ? 0x10000u : 1u);
+                    for (uint32_t t0 = l0 + tid; t0 < l1; t0 += 4 * NT) {   // four list loads in flight
+                        uint32_t v4[4];
+#pragma unroll
+                        for (int u = 0; u < 4; u++) v4[u] = t0 + u * NT < l1 ? sc[t0 + u * NT] : 0xFFFFFFFFu;
+#pragma unroll
+                        for (int u = 0; u < 4; u++)
+                            if (v4[u] != 0xFFFFFFFFu) atomicAdd(&ccnt[v4[u] & (CH - 1)], (v4[u] >> 15) ? 0x10000u : 1u);
                     }
                     __syncthreads();
                     uint32_t qmask = 0;
