@@ -554,7 +554,9 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             std::vector<uint32_t> rw(W);
             for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
             std::nth_element(rw.begin(), rw.begin() + W / 2, rw.end());
-            const uint32_t thr = std::max<uint32_t>(600u, 2u * rw[W / 2]);
+            const char *hx = getenv("PF_K3_HEAVY_X");       // tuning: the multiple of the median
+            const double x = hx ? atof(hx) : 2.0;
+            const uint32_t thr = std::max<uint32_t>(hx ? 1u : 600u, (uint32_t)(x * rw[W / 2]));
             uint32_t nh = 0;
             while (nh < 2 * W && in->win_read_off[(ord[nh] >> 1) + 1] - in->win_read_off[ord[nh] >> 1] >= thr) nh++;
             const char *hv = getenv("PF_K3_HEAVY");
@@ -618,7 +620,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
         std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
         if (rw[(W * 9) / 10] <= 400) lds_auto = 40960u;
-        else if (rw[(W * 9) / 10] <= 800) lds_auto = 49152u;    // 60x: three per CU, none deferred
+        else if (rw[(W * 9) / 10] <= 800) lds_auto = 45056u;    // 60x: three per CU (u8 count pairs, round 3)
     }
     const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB"), *ldw = getenv("PF_K3W_LDS");
     // one-wave greedy kernel: ~25 KB leaves six problems per CU (a 60x

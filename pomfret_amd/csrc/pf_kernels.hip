@@ -1242,7 +1242,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
 struct K3Ctl {
     uint32_t S, R, ntot, nc, L, done, failed, inserted, winner, tag;
     int32_t i_last;
-    uint32_t min_i, max_i, fail, summ, nstrict, mxlen;
+    uint32_t min_i, max_i, fail, summ, nstrict, mxlen, cmax;
     uint32_t ins_n, ins_st, ins_mo, ins_tg;   // register variant: winner whose insert is pending
     unsigned long long scr;
     int32_t tab[4];
@@ -1340,11 +1340,11 @@ struct K3Mem {
 // P2 byte layout.  Returns the bytes needed with `rcw` records per wave;
 // slots (u16) are included only when with_slots.
 DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint32_t summ,
-                       bool with_slots, uint32_t rcw, uint64_t off[K3_NOFF]) {
+                       bool with_slots, uint32_t rcw, uint64_t off[K3_NOFF], bool c8 = false) {
     const uint32_t nwords = (R + 63) >> 6;
     off[0] = 0;                                        // sum   S*4
     off[1] = align16(off[0] + 4ull * S);               // cnt   ntot*4
-    off[2] = align16(off[1] + 4ull * ntot);            // hp    R
+    off[2] = align16(off[1] + (c8 ? 2ull : 4ull) * ntot);   // hp    R (cnt: u8 pairs when c8)
     off[3] = align16(off[2] + R);                      // flg   R
     off[4] = align16(off[3] + R);                      // ord   R*4 (dir 1)
     off[5] = align16(off[4] + (dir ? 4ull * R : 0));   // untag nwords*8
@@ -1636,6 +1636,16 @@ DEV uint32_t k3_slot(const K3Mem &m, uint32_t off) {
 // Fill of one lane's record-row entries t = tstart, tstart+step, ... < tpad
 // (entries t >= tend are written as zero); returns the lane's push/positive
 // count pair.  Four rounds of loads in flight.
+// a slot's (hap0, hap1) counts as hap0 | hap1 << 16: u16 pairs (C8 = false)
+// or, when no site is covered by more than 255 reads' methmers (so no count
+// can exceed 255), u8 pairs -- half the table, more problems per CU
+template <bool C8>
+DEV uint32_t k3_cnt_get(const K3Mem &m, uint32_t sl) {
+    if (!C8) return m.cnt[sl];
+    const uint32_t c = reinterpret_cast<const uint16_t *>(m.cnt)[sl];
+    return (c & 0xffu) | ((c >> 8) << 16);
+}
+
 template <bool SLDS>
 DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32_t tstart, uint32_t tend,
                           uint32_t tpad, uint32_t step, float2 *row, double &e0, double &e1) {
@@ -1682,7 +1692,7 @@ DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
 // insert_mmr_counts of one tagged read (hap tg) by the whole workgroup: its
 // sites are distinct, so a plain read-modify-write per site; only hap tg's
 // divisor entry changes (its total becomes >= 1, so no zero case)
-template <bool SLDS, int NT = PF_K3_THREADS>
+template <bool SLDS, int NT = PF_K3_THREADS, bool C8 = false>
 DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint32_t mo, uint32_t tg) {
     const uint32_t inc = tg ? 0x10000u : 1u, sh = tg ? 16u : 0u;
     float *srf = reinterpret_cast<float *>(m.srec) + tg;   // (h_tg, -, 1/h_tg, -) of site 0
@@ -1699,7 +1709,7 @@ DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint
         for (int u = 0; u < 2; u++) {
             const uint32_t t = tb + u * NT + threadIdx.x;
             ok[u] = ok[u] && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
-            cc[u] = m.cnt[ok[u] ? sl[u] : 0u];
+            cc[u] = C8 ? (uint32_t)reinterpret_cast<const uint16_t *>(m.cnt)[ok[u] ? sl[u] : 0u] : m.cnt[ok[u] ? sl[u] : 0u];
             sv[u] = m.sum[ok[u] ? st + t : 0u];
         }
         asm volatile("" ::: "memory");              // every load issued before the first store
@@ -1709,7 +1719,8 @@ DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint
                 const uint32_t site = st + tb + u * NT + threadIdx.x;
                 const uint32_t s2 = sv[u] + inc;
                 const float f = (float)((s2 >> sh) & 0xffffu);
-                m.cnt[sl[u]] = cc[u] + inc;
+                if (C8) reinterpret_cast<uint16_t *>(m.cnt)[sl[u]] = (uint16_t)(cc[u] + (tg ? 0x100u : 1u));
+                else m.cnt[sl[u]] = cc[u] + inc;
                 m.sum[site] = s2;
                 srf[4 * site] = f;
                 srf[4 * site + 2] = __builtin_amdgcn_rcpf(f);
@@ -1722,7 +1733,7 @@ DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint
 // tstart+step, ... < tend, accumulated into the exact fp64 sums (no record
 // rows: the sequential fold, needed for 0.05-0.5 % of picks, recomputes its
 // terms with k3_fold_direct).  Returns the push/positive count pair.
-template <bool SLDS>
+template <bool SLDS, bool C8 = false>
 DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32_t tstart, uint32_t tend,
                           uint32_t step, double &e0, double &e1) {
     uint32_t lcode = 0;
@@ -1740,7 +1751,7 @@ DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
         for (int u = 0; u < 4; u++) {
             const uint32_t t = tb + u * step;
             const bool ok = t < tend && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
-            const uint32_t c = m.cnt[ok ? sl[u] : 0u];
+            const uint32_t c = k3_cnt_get<C8>(m, ok ? sl[u] : 0u);
             cv[u] = ok ? c : 0u;
         }
 #pragma unroll
@@ -1767,7 +1778,7 @@ DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
 // The reference's sequential float sums (blockjoin.c:3619-3636) of one
 // candidate, terms recomputed from the tables in methmer order (the rare
 // picks the exact intervals cannot decide).
-template <bool SLDS>
+template <bool SLDS, bool C8 = false>
 DEV void k3_fold_direct(const K3Mem &m, uint32_t lo, uint32_t kofs, uint32_t len, float &s0, float &s1) {
     for (uint32_t t0 = 0; t0 < len; t0 += 8) {
         uint32_t sl[8];
@@ -1783,7 +1794,7 @@ DEV void k3_fold_direct(const K3Mem &m, uint32_t lo, uint32_t kofs, uint32_t len
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const bool ok = t0 + u < len && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
-            const uint32_t c = ok ? m.cnt[ok ? sl[u] : 0u] : 0u;
+            const uint32_t c = ok ? k3_cnt_get<C8>(m, sl[u]) : 0u;
             q0[u] = div_u16_y((float)(c & 0xffffu), sr[u].x, sr[u].z);
             q1[u] = div_u16_y((float)(c >> 16), sr[u].y, sr[u].w);
         }
@@ -1848,7 +1859,7 @@ DEV void k3_pick_exact(const double *accd, uint32_t lane, uint32_t nc, uint32_t 
 // state, slot-list offsets (and the u16 LDS copy), reference reads seeding the
 // counts (insert_ref_reads_methmer_counts, :3776-3810), the initial range,
 // the T5 round trip and the untagged bitmask.
-template <bool SLDS, int NT = PF_K3_THREADS>
+template <bool SLDS, int NT = PF_K3_THREADS, bool C8 = false>
 DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
                  const K3Mem &m, K3Ctl &ctl, uint32_t *sh_scan, K3Stats &stx) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
@@ -1861,7 +1872,7 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
     const uint32_t *kb = d.keys + kbase;
     uint32_t sum_mmr = 0, mx_mmr = 0;
     // ---- init tables and per-read state
-    for (uint32_t j = tid; j < ntot; j += NT) m.cnt[j] = 0;
+    for (uint32_t j = tid; j < (C8 ? (ntot + 1) / 2 : ntot); j += NT) m.cnt[j] = 0;
     for (uint32_t j = tid; j < S; j += NT) m.sum[j] = 0;
     for (uint32_t i = tid; i < R; i += NT) {
         const uint32_t r = r0 + i;
@@ -1939,7 +1950,8 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
             const uint32_t site = st + t;
             const uint32_t slot = k3_slot<SLDS>(m, mo + t);
             if (site < S && slot != PF_NONE) {
-                atomicAdd(&m.cnt[slot], inc);
+                if (C8) atomicAdd(&m.cnt[slot >> 1], (hp ? 0x100u : 1u) << ((slot & 1u) * 16u));
+                else atomicAdd(&m.cnt[slot], inc);
                 atomicAdd(&m.sum[site], inc);
             }
         }
@@ -2059,7 +2071,7 @@ DEV void k3_range_regs(const K3Mem &m, uint32_t S, int cov_rt, uint32_t lane, ui
 // redundantly -- identical register copies of the candidate list, the queue
 // and the range -- so nothing is published between waves; two barriers per
 // iteration: after the term fill (B) and after the winner's insert (X).
-template <bool SLDS, int NT = PF_K3_THREADS>
+template <bool SLDS, int NT = PF_K3_THREADS, bool C8 = false>
 DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
                         const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan, uint32_t *qb) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
@@ -2071,7 +2083,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     unsigned long long prof_acc[32] = {0};
     unsigned long long prof_last = k3_stamp_now();
 #endif
-    k3_init<SLDS, NT>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
+    k3_init<SLDS, NT, C8>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
     K3_STAMP(0);
     int il = uni_i(ctl.i_last);
     uint32_t failed = 0;
@@ -2177,7 +2189,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             const uint32_t f_len = (uint32_t)__shfl((int)c_len, (int)fc, 64);
             const uint32_t f_kofs = (uint32_t)__shfl((int)c_kofs, (int)fc, 64);
             double x0 = 0.0, x1 = 0.0;
-            const uint32_t lcode = k3_fill_sums<SLDS>(m, f_lo, f_kofs, J, f_len, GS, x0, x1);
+            const uint32_t lcode = k3_fill_sums<SLDS, C8>(m, f_lo, f_kofs, J, f_len, GS, x0, x1);
             if (fc < nc) {
                 atomicAdd(&lcp[par * 64 + fc], lcode);
                 atomicAdd(&accd[par * 128 + fc], x0);
@@ -2207,7 +2219,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             if (pick == 0) {
                 folded = true;
                 float s0 = 0.f, s1 = 0.f;
-                if (lane < nc) k3_fold_direct<SLDS>(m, c_lo, c_kofs, c_len, s0, s1);
+                if (lane < nc) k3_fold_direct<SLDS, C8>(m, c_lo, c_kofs, c_len, s0, s1);
                 const float diff = s0 > s1 ? s0 - s1 : s1 - s0;
                 const bool elig = lane < nc && !(diff < 3.f && (l0 < 3 || l1 < 3));
                 const uint32_t hkey = elig ? __float_as_uint(diff) + 1u : 0u;
@@ -2258,7 +2270,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // ---- insert_mmr_counts of the winner, the whole workgroup (after every
         // wave's fold, if the pick needed one, has read the tables)
         if (folded) __syncthreads();
-        k3_insert_all<SLDS, NT>(m, S, n, st, mo, tg);
+        k3_insert_all<SLDS, NT, C8>(m, S, n, st, mo, tg);
         have_win = true;
         K3_STAMP(21);
         __syncthreads();                                           // (X)
@@ -2956,8 +2968,37 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     // takes the rest.
     uint64_t off[K3_NOFF];
     const bool slots_ok = ntot < 0xFFFFu;
-    const uint64_t slim_s = k3_layout(S, ntot, R, dir, summ_tot, true, 0, off);
-    const uint64_t slim_n = k3_layout(S, ntot, R, dir, summ_tot, false, 0, off);
+    // u8 count pairs when no site is covered by more than 255 reads' methmer
+    // spans [st, st+n) (every count is bounded by that coverage): the deepest
+    // coverage from a difference array in the LDS left after the dictionary
+    bool c8 = false;
+    if (slim_ok && (!FULL || p1_lds) && need1 + align16(4ull * (S + 1)) <= lds) {
+        uint32_t *cov = reinterpret_cast<uint32_t *>(smem + need1);
+        for (uint32_t j = tid; j <= S; j += NT) cov[j] = 0;
+        if (tid == 0) ctl.cmax = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < R; i += NT) {
+            const uint64_t g = 2ull * (r0 + i) + dir;
+            const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
+            if (n && st < S) {
+                atomicAdd(&cov[st], 1u);
+                atomicAdd(&cov[st + n < S ? st + n : S], 0xFFFFFFFFu);
+            }
+        }
+        __syncthreads();
+        const uint32_t per = (S + NT) / NT;                 // S + 1 entries, contiguous per thread
+        const uint32_t j0 = tid * per, j1 = min(j0 + per, S + 1);
+        uint32_t part = 0;
+        for (uint32_t j = j0; j < j1; j++) part += cov[j];
+        uint32_t tot;
+        uint32_t run = block_excl_scan<NT>(part, sh_scan, &tot), mx = 0;
+        for (uint32_t j = j0; j < j1; j++) { run += cov[j]; mx = run > mx ? run : mx; }
+        if (mx) atomicMax(&ctl.cmax, mx);
+        __syncthreads();
+        c8 = uni(ctl.cmax) < 256u;
+    }
+    const uint64_t slim_s = k3_layout(S, ntot, R, dir, summ_tot, true, 0, off, c8);
+    const uint64_t slim_n = k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8);
     const bool slim_fit = slim_ok && ((slots_ok && slim_s <= lds) || slim_n <= lds);
     if (!FULL && !slim_fit) {
         k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
@@ -2967,14 +3008,17 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     const uint32_t *kb = d.keys + kbase;
     if (slim_fit) {
         K3Mem m;
+        uint32_t *qq = qb ? qb : cd.read;
         if (slots_ok && slim_s <= lds) {
-            (void)k3_layout(S, ntot, R, dir, summ_tot, true, 0, off);
+            (void)k3_layout(S, ntot, R, dir, summ_tot, true, 0, off, c8);
             k3_mem(smem, off, 0, true, kb, m);
-            k3_greedy_slim<true, NT>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qb ? qb : cd.read);
+            if (c8) k3_greedy_slim<true, NT, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
+            else k3_greedy_slim<true, NT, false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
         } else {
-            (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off);
+            (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8);
             k3_mem(smem, off, 0, false, kb, m);
-            k3_greedy_slim<false, NT>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qb ? qb : cd.read);
+            if (c8) k3_greedy_slim<false, NT, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
+            else k3_greedy_slim<false, NT, false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
         }
         return;
     }
