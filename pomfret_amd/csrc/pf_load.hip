@@ -1020,7 +1020,8 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
 }
 
 template <typename TP>
-DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, uint32_t cap) {
+DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, uint32_t cap, const K0Tgt &t,
+                   bool okm) {
     const uint32_t len = d.l_qseq[r];
     const bool rev = (d.flag[r] & 16u) != 0;
     const uint8_t *mmg = d.mm + d.mm_off[r];
@@ -1031,19 +1032,13 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     const uint32_t *cig = d.cigar + d.cigar_off[r];
     const uint32_t ncig = (uint32_t)(d.cigar_off[r + 1] - d.cigar_off[r]);
 
-    K0Tgt t;
-    bool okmm;
+    bool okmm = okm;
     uint32_t nT = 0, mlq0 = 0xFFFFFFFFu, mlq1 = 0xFFFFFFFFu;
     bool implicit = false;
     K0_T0;
-    // PF_K0_DIAG=4/2/3 (measurement only, results invalid): stop after the
-    // filters / the MM phase / the SEQ pass, so that phase costs are kernel-time
-    // differences (the s_memtime build's counter atomics distort them)
-    if (d.diag == 4u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
     {
         const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
         const uint32_t *gw = reinterpret_cast<const uint32_t *>(mmg - mis);
-        okmm = k0_mm_entries(gw, mmg, mis, mlen, mln, lane, t);
         if (okmm && t.nd > cap) okmm = false;       // only a malformed tag lists more calls than its size allows
         if (okmm && t.nd) {
             // the first 512 ML values (8 per lane, packed) are loaded before
@@ -1191,9 +1186,26 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_e
         if (lane == 0) d.rec_n[r] = PF_NONE;
         return;
     }
+    // PF_K0_DIAG=4/2/3 (measurement only, results invalid): stop after the
+    // filters / the MM phase / the SEQ pass, so that phase costs are kernel-time
+    // differences (the s_memtime build's counter atomics distort them)
+    if (d.diag == 4u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
+    // The tag's entries first: the C+m entry's skip count decides where the
+    // trigger list lives -- the wave's LDS list when it fits (640), else the
+    // record's HBM slice, which the upload sizes from the ML length (an upper
+    // bound: dorado's h + m entries make it twice the m list, so round 2 sent
+    // ~45 % of 60x records to HBM, with every rank, key and binary search of
+    // their trigger lists an L2 round trip).
+    const uint8_t *mmg = d.mm + d.mm_off[r];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
+    K0Tgt t;
+    const bool okm = k0_mm_entries(reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis,
+                                   (uint32_t)(d.mm_off[r + 1] - d.mm_off[r]),
+                                   (uint32_t)(d.ml_off[r + 1] - d.ml_off[r]), lane, t);
     const uint64_t s0 = d.scr_off[r], s1 = d.scr_off[r + 1];
-    if (s1 == s0) k0_record(d, L, r, lane, L.T, (uint32_t)PF_K0_TCAP);
-    else k0_record(d, L, r, lane, d.scr + s0, (uint32_t)(s1 - s0));
+    if (s1 == s0 || !okm || uni(t.nd) <= (uint32_t)PF_K0_TCAP)
+        k0_record(d, L, r, lane, L.T, (uint32_t)PF_K0_TCAP, t, okm);
+    else k0_record(d, L, r, lane, d.scr + s0, (uint32_t)(s1 - s0), t, okm);
 }
 
 // ---------------------------------------------------------------------------
