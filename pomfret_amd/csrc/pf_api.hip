@@ -48,7 +48,8 @@ static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k0_pack", "pf_k12_site
 struct pf_ctx {
     int device;
     hipStream_t stream;
-    hipStream_t stream2;      /* the heavy greedy problems, beside the main greedy kernel */
+    hipStream_t stream2;      /* the heavy greedy problems, beside the main greedy kernel; the fetch's copies */
+    hipStream_t stream3;      /* the fetch's second inflate stream */
     hipEvent_t ev[PF_NKERN + 1];
     float last_ms[PF_NKERN];
     int have_times;
@@ -179,6 +180,7 @@ extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking));
     c->heavy_ms = -1.0f;
     for (int i = 0; i <= PF_NKERN; i++) HIPCHK(hipEventCreate(&c->ev[i]));
     c->have_times = 0;
@@ -209,12 +211,18 @@ extern "C" int pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches) {
 
 extern "C" int pf_ctx_device(const pf_ctx *c) { return c->device; }
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c) { return c->stream; }
+extern "C" hipStream_t pf_ctx_stream2(const pf_ctx *c) { return c->stream2; }
+extern "C" hipStream_t pf_ctx_stream3(const pf_ctx *c) { return c->stream3; }
 
 // the context's pinned staging buffer for the device fetch's compressed bytes
 // (pf_ingest.hip), grown on demand; the caller owns the context's stream
 extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n) {
     if (c->stage_cap < n) {
-        if (c->stage) { (void)hipStreamSynchronize(c->stream); (void)hipHostFree(c->stage); }
+        if (c->stage) {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->stream2);
+            (void)hipHostFree(c->stage);
+        }
         c->stage = nullptr;
         c->stage_cap = 0;
         void *p = nullptr;
@@ -246,6 +254,7 @@ extern "C" uint8_t *pf_ctx_devws(pf_ctx *c, size_t n) {
 extern "C" void pf_ctx_stage_trim(pf_ctx *c, size_t keep) {
     if (c->stage && c->stage_cap > keep) {
         (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(c->stream2);
         (void)hipHostFree(c->stage);
         c->stage = nullptr;
         c->stage_cap = 0;
@@ -259,6 +268,7 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->stream2);
+    (void)hipStreamDestroy(c->stream3);
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
     if (c->dws) (void)hipFree(c->dws);

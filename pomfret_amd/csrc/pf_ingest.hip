@@ -11,6 +11,8 @@
 struct pf_ctx;
 extern "C" int pf_ctx_device(const pf_ctx *c);
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c);
+extern "C" hipStream_t pf_ctx_stream2(const pf_ctx *c);
+extern "C" hipStream_t pf_ctx_stream3(const pf_ctx *c);
 extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n);
 extern "C" void pf_ctx_stage_trim(pf_ctx *c, size_t keep);
 
@@ -169,10 +171,12 @@ out:
 
 namespace {
 
-struct DevBuf {                                  // device allocations freed together, after the stream drains
+struct DevBuf {                                  // device allocations freed together, after the streams drain
     std::vector<void *> p;
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr, st2 = nullptr, st3 = nullptr;
     ~DevBuf() {
+        if (st2) (void)hipStreamSynchronize(st2);
+        if (st3) (void)hipStreamSynchronize(st3);
         if (st) (void)hipStreamSynchronize(st);
         for (void *x : p) (void)hipFree(x);
     }
@@ -195,6 +199,7 @@ struct Range {
     uint64_t end_addr;        // file address after its last whole block
     uint32_t b0, b1;          // its blocks
     bool to_eof;
+    uint64_t scan = 0;        // bytes of the run scanned into blocks so far
 };
 
 struct Plan {
@@ -333,17 +338,137 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         std::sort(rq.begin(), rq.end());
         for (auto &x : rq) {
             if (!P.runs.empty() && x.first <= P.runs.back().f1) P.runs.back().f1 = std::max(P.runs.back().f1, x.second);
-            else P.runs.push_back(Range{x.first, x.second, 0, 0, 0, 0, false});
+            else P.runs.push_back(Range{x.first, x.second, 0, 0, 0, 0, false, 0});
         }
         uint64_t tot = 0;
         for (auto &R : P.runs) { R.buf0 = tot; tot += R.f1 - R.f0; }
+        // The pinned buffer holds the runs' bytes, then a two-half ring of
+        // block descriptors on their way to the device.
+        constexpr uint32_t RING = 16384;                                   // descriptors per half
+        // A launch waits for MINB blocks, and launches alternate between two
+        // streams so that one's tail overlaps the next (a wave decodes a block
+        // at a few MB/s: the rate comes from blocks in flight, about one per
+        // wave slot of the chip).
+        constexpr uint32_t MINB = 4096;
+        const uint64_t ring_at = (tot + 512 + 255) & ~255ull;
         P.comp_n = tot + 512;
-        P.comp = pf_ctx_stage((pf_ctx *)ctx, P.comp_n);
+        P.comp = pf_ctx_stage((pf_ctx *)ctx, ring_at + 2ull * RING * sizeof(pf_bgzf_blk));
         uint8_t *d_comp = D.alloc<uint8_t>(P.comp_n);
         if (!P.comp || !d_comp) { rc = PF_ERR_NOMEM; break; }
-        // parallel reads into the pinned buffer in segments of <= 64 MiB, each
-        // segment's H2D copy overlapping the reads of the next (pieces of
-        // <= 4 MiB on 16 threads)
+        pf_bgzf_blk *ring = reinterpret_cast<pf_bgzf_blk *>(P.comp + ring_at);
+        // The inflated arena is sized from the compressed bytes (BAM inflates
+        // 1.5-3x); blocks past it wait for an exact arena after the reads.
+        const uint64_t acap = 4 * tot + (1ull << 20);
+        uint8_t *d_arena = D.alloc<uint8_t>(acap + 512);
+        if (!d_arena) { rc = PF_ERR_NOMEM; break; }
+        hipStream_t cs = pf_ctx_stream2((const pf_ctx *)ctx), s3 = pf_ctx_stream3((const pf_ctx *)ctx);
+        D.st2 = cs;
+        D.st3 = s3;
+        hipEvent_t ev[8], ecp, eh[2];
+        bool used[2] = {false, false};
+        int nev = 0;
+        for (auto &e : ev) if (hipEventCreateWithFlags(&e, 0) == hipSuccess) nev++;
+        const bool ev_ok = nev == 8 && hipEventCreateWithFlags(&ecp, hipEventDisableTiming) == hipSuccess &&
+                           hipEventCreateWithFlags(&eh[0], hipEventDisableTiming) == hipSuccess &&
+                           hipEventCreateWithFlags(&eh[1], hipEventDisableTiming) == hipSuccess;
+        if (!ev_ok) { rc = PF_ERR_HIP; break; }
+        struct EvGuard {
+            hipEvent_t *ev, *ecp, *eh;
+            ~EvGuard() {
+                for (int i = 0; i < 8; i++) (void)hipEventDestroy(ev[i]);
+                (void)hipEventDestroy(*ecp); (void)hipEventDestroy(eh[0]); (void)hipEventDestroy(eh[1]);
+            }
+        } evg{ev, &ecp, eh};
+        // per batch of blocks: its device descriptors and status words
+        struct Batch { uint32_t b0, n; pf_bgzf_blk *d_blk; uint32_t *d_st; };
+        std::vector<Batch> batches;
+        uint32_t nb_sent = 0;                 // blocks whose inflate is enqueued
+        uint32_t cur = 0;                     // first run not completely scanned
+        bool spill = false;                   // the arena estimate was short
+        // Scan the runs' blocks up to buffer offset `front` (whole blocks only;
+        // a run is complete once its last whole block is scanned).
+        auto scan_to = [&](uint64_t front) -> int {
+            for (; cur < P.runs.size(); cur++) {
+                Range &R = P.runs[cur];
+                if (R.buf0 > front) return PF_OK;
+                if (R.scan == 0) R.b0 = (uint32_t)P.blk.size();
+                const uint64_t len = R.f1 - R.f0, avail = std::min(len, front - R.buf0);
+                const uint8_t *c = P.comp + R.buf0;
+                uint64_t o = R.scan;
+                bool end = false;
+                for (;;) {
+                    if (o + 18 > len) { end = true; break; }
+                    if (o + 18 > avail) break;
+                    const uint8_t *h = c + o;
+                    if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return PF_ERR_ARG;
+                    const uint32_t xlen = rd16(h + 10);
+                    if (o + 12 + xlen > len) { end = true; break; }
+                    if (o + 12 + xlen > avail) break;
+                    uint32_t bsize = 0;
+                    for (uint32_t x = 0; x + 4 <= xlen;) {
+                        const uint8_t *sf = h + 12 + x;
+                        const uint32_t slen = rd16(sf + 2);
+                        if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = rd16(sf + 4) + 1;
+                        x += 4 + slen;
+                    }
+                    if (bsize < 12 + xlen + 8 || bsize > 65536) return PF_ERR_ARG;
+                    if (o + bsize > len) { end = true; break; }
+                    if (o + bsize > avail) break;
+                    pf_bgzf_blk b;
+                    b.in_off = R.buf0 + o + 12 + xlen;
+                    b.in_len = bsize - 12 - xlen - 8;
+                    b.crc = rd32(h + bsize - 8);
+                    b.isize = rd32(h + bsize - 4);
+                    if (b.isize > 65536) return PF_ERR_ARG;
+                    b.out_off = P.arena;
+                    b.run = cur;
+                    P.arena += b.isize;
+                    P.blk.push_back(b);
+                    P.caddr.push_back(R.f0 + o);
+                    o += bsize;
+                }
+                R.scan = o;
+                if (!end) return PF_OK;
+                R.b1 = (uint32_t)P.blk.size();
+                R.end_addr = R.f0 + o;
+                R.to_eof = R.end_addr >= fsize;
+            }
+            return PF_OK;
+        };
+        // Enqueue the inflate of the scanned blocks not yet sent (at least
+        // MINB of them unless `last`), into `arena`:
+        // descriptors through the pinned ring on the copy stream, the kernel
+        // on the main stream behind the copies.
+        auto send = [&](uint8_t *arena, bool last) -> int {
+            if (!last && P.blk.size() - nb_sent < MINB) return PF_OK;
+            while (nb_sent < P.blk.size()) {
+                const uint32_t n = std::min<uint32_t>(RING, (uint32_t)P.blk.size() - nb_sent);
+                const int h = (int)(batches.size() & 1);
+                if (used[h] && hipEventSynchronize(eh[h]) != hipSuccess) return PF_ERR_HIP;
+                pf_bgzf_blk *hb = ring + (size_t)h * RING;
+                memcpy(hb, P.blk.data() + nb_sent, sizeof(pf_bgzf_blk) * n);
+                Batch B{nb_sent, n, D.alloc<pf_bgzf_blk>(n), D.alloc<uint32_t>(n)};
+                if (!B.d_blk || !B.d_st) return PF_ERR_NOMEM;
+                if (hipMemcpyAsync(B.d_blk, hb, sizeof(pf_bgzf_blk) * n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+                    hipEventRecord(eh[h], cs) != hipSuccess || hipEventRecord(ecp, cs) != hipSuccess)
+                    return PF_ERR_HIP;
+                const hipStream_t ks = (batches.size() & 1) ? s3 : st;
+                if (batches.empty() && hipEventRecord(ev[0], cs) != hipSuccess) return PF_ERR_HIP;
+                if (hipStreamWaitEvent(ks, ecp, 0) != hipSuccess || hipMemsetAsync(B.d_st, 0, 4ull * n, ks) != hipSuccess)
+                    return PF_ERR_HIP;
+                used[h] = true;
+                const int r = pf_inflate_launch((pf_ctx *)ctx, ks, d_comp, B.d_blk, P.blk.data() + nb_sent, n, arena,
+                                                B.d_st, nullptr, nullptr);
+                if (r) return r;
+                batches.push_back(B);
+                nb_sent += n;
+            }
+            return PF_OK;
+        };
+        // Parallel reads into the pinned buffer in segments of <= 64 MiB
+        // (pieces of <= 4 MiB on 16 threads); each segment's H2D copy runs on
+        // the copy stream and its whole blocks are inflated on the main stream
+        // while the next segment is read.
         {
             constexpr uint64_t SEG = 64ull << 20, PIECE = 4ull << 20;
             std::vector<std::pair<uint64_t, uint64_t>> pieces;     // (run, offset in run)
@@ -352,7 +477,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             std::atomic<int> bad{0};
             size_t pi = 0;
             uint64_t copied = 0;
-            while (pi < pieces.size() && !bad.load()) {
+            while (pi < pieces.size() && !bad.load() && !rc) {
                 size_t pe = pi;
                 const uint64_t seg0 = P.runs[pieces[pi].first].buf0 + pieces[pi].second;
                 while (pe < pieces.size() && P.runs[pieces[pe].first].buf0 + pieces[pe].second < seg0 + SEG) pe++;
@@ -368,58 +493,47 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
                         }
                     });
                 for (auto &t : th) t.join();
+                if (bad.load()) break;
                 const uint64_t seg1 = pe < pieces.size() ? P.runs[pieces[pe].first].buf0 + pieces[pe].second : tot;
-                if (hipMemcpyAsync(d_comp + copied, P.comp + copied, seg1 - copied, hipMemcpyHostToDevice, st) !=
-                    hipSuccess) bad.store(2);
-                copied = seg1;
+                if (pe == pieces.size()) memset(P.comp + tot, 0, 512);
+                const uint64_t cend = pe == pieces.size() ? tot + 512 : seg1;
+                if (hipMemcpyAsync(d_comp + copied, P.comp + copied, cend - copied, hipMemcpyHostToDevice, cs) !=
+                    hipSuccess) { bad.store(2); break; }
+                copied = cend;
                 pi = pe;
+                rc = scan_to(seg1);
+                if (!rc && !spill) {
+                    if (P.arena > acap) spill = true;
+                    else rc = send(d_arena, false);
+                }
             }
-            memset(P.comp + tot, 0, 512);
-            if (!bad.load() && hipMemcpyAsync(d_comp + tot, P.comp + tot, 512, hipMemcpyHostToDevice, st) != hipSuccess)
-                bad.store(2);
-            if (bad.load()) rc = bad.load() == 1 ? -1 : PF_ERR_HIP;
+            if (!rc && bad.load()) rc = bad.load() == 1 ? -1 : PF_ERR_HIP;
+            if (!rc && pieces.empty()) {
+                memset(P.comp + tot, 0, 512);
+                if (hipMemcpyAsync(d_comp, P.comp, 512, hipMemcpyHostToDevice, cs) != hipSuccess) rc = PF_ERR_HIP;
+            }
         }
+        if (!rc) rc = scan_to(tot);
+        if (!rc && spill) {
+            // the exact arena: what was inflated moves over, the rest follows
+            uint8_t *a2 = D.alloc<uint8_t>(P.arena + 512);
+            if (!a2) rc = PF_ERR_NOMEM;
+            const uint64_t done = nb_sent ? P.blk[nb_sent - 1].out_off + P.blk[nb_sent - 1].isize : 0;
+            if (!rc && (hipEventRecord(ecp, s3) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess))
+                rc = PF_ERR_HIP;
+            if (!rc && done && hipMemcpyAsync(a2, d_arena, done, hipMemcpyDeviceToDevice, st) != hipSuccess) rc = PF_ERR_HIP;
+            if (!rc && (hipEventRecord(ecp, st) != hipSuccess || hipStreamWaitEvent(s3, ecp, 0) != hipSuccess))
+                rc = PF_ERR_HIP;
+            d_arena = a2;
+        }
+        if (!rc) rc = send(d_arena, true);
+        if (!rc && batches.empty() && hipEventRecord(ev[0], st) != hipSuccess) rc = PF_ERR_HIP;
+        if (!rc && (hipEventRecord(ecp, cs) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess ||
+                    hipEventRecord(ecp, s3) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess ||
+                    hipEventRecord(ev[1], st) != hipSuccess))
+            rc = PF_ERR_HIP;
         if (rc) break;
         const double t_read = now_ms() - t0;
-        // ---- blocks of each range (whole blocks only)
-        for (uint32_t ri = 0; ri < P.runs.size() && !rc; ri++) {
-            Range &R = P.runs[ri];
-            R.b0 = (uint32_t)P.blk.size();
-            uint64_t o = 0;
-            const uint64_t len = R.f1 - R.f0;
-            const uint8_t *c = P.comp + R.buf0;
-            while (o + 18 <= len) {
-                const uint8_t *h = c + o;
-                if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) { rc = PF_ERR_ARG; break; }
-                const uint32_t xlen = rd16(h + 10);
-                if (o + 12 + xlen > len) break;
-                uint32_t bsize = 0;
-                for (uint32_t x = 0; x + 4 <= xlen;) {
-                    const uint8_t *sf = h + 12 + x;
-                    const uint32_t slen = rd16(sf + 2);
-                    if (sf[0] == 'B' && sf[1] == 'C' && slen == 2) bsize = rd16(sf + 4) + 1;
-                    x += 4 + slen;
-                }
-                if (bsize < 12 + xlen + 8 || bsize > 65536) { rc = PF_ERR_ARG; break; }
-                if (o + bsize > len) break;
-                pf_bgzf_blk b;
-                b.in_off = R.buf0 + o + 12 + xlen;
-                b.in_len = bsize - 12 - xlen - 8;
-                b.crc = rd32(h + bsize - 8);
-                b.isize = rd32(h + bsize - 4);
-                if (b.isize > 65536) { rc = PF_ERR_ARG; break; }
-                b.out_off = P.arena;
-                b.run = ri;
-                P.arena += b.isize;
-                P.blk.push_back(b);
-                P.caddr.push_back(R.f0 + o);
-                o += bsize;
-            }
-            R.b1 = (uint32_t)P.blk.size();
-            R.end_addr = R.f0 + o;
-            R.to_eof = R.end_addr >= fsize;
-        }
-        if (rc) break;
         const uint32_t NB = (uint32_t)P.blk.size(), NR = (uint32_t)P.runs.size();
         // ---- chunks -> arena positions; chain starts per run
         auto find_blk = [&](uint64_t addr) -> int64_t {
@@ -490,38 +604,29 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             wd[w].beg = beg[w]; wd[w].end = end[w]; wd[w].c0 = wc[w]; wd[w].c1 = wc[w + 1];
             wd[w].tid = tid; wd[w].skip = 0; wd[w].reads = (uint16_t)reads; wd[w].out = 0;
         }
-        // ---- upload + inflate
+        // ---- tables of the later stages (the inflate is enqueued already)
         t0 = now_ms();
-        pf_bgzf_blk *d_blk = D.alloc<pf_bgzf_blk>(NB);
-        uint8_t *d_arena = D.alloc<uint8_t>(P.arena + 512);
-        uint32_t *d_bst = D.alloc<uint32_t>(NB);
         pf_run_dev *d_run = D.alloc<pf_run_dev>(NR);
         pf_seg_dev *d_sg = D.alloc<pf_seg_dev>(NS_);
         pf_chunk_dev *d_ch = D.alloc<pf_chunk_dev>(NC);
         pf_win_dev *d_win = D.alloc<pf_win_dev>(W);
         uint32_t *d_wn = D.alloc<uint32_t>(2ull * W);
-        if (!d_blk || !d_arena || !d_bst || !d_run || !d_sg || !d_ch || !d_win || !d_wn) { rc = PF_ERR_NOMEM; break; }
-        hipEvent_t ev[8];
-        for (auto &e : ev) if (hipEventCreate(&e) != hipSuccess) rc = PF_ERR_HIP;
-        if (rc) break;
-        auto evdone = [&]() { for (auto &e : ev) (void)hipEventDestroy(e); };
-        bool ok = hipMemcpyAsync(d_blk, P.blk.data(), sizeof(pf_bgzf_blk) * NB, hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipMemsetAsync(d_bst, 0, 4ull * NB, st) == hipSuccess &&
-                  hipMemsetAsync(d_arena + P.arena, 0, 512, st) == hipSuccess &&
+        if (!d_run || !d_sg || !d_ch || !d_win || !d_wn) { rc = PF_ERR_NOMEM; break; }
+        auto evdone = [&]() {};
+        bool ok = hipMemsetAsync(d_arena + P.arena, 0, 512, st) == hipSuccess &&
                   hipMemcpyAsync(d_sg, sg.data(), sizeof(pf_seg_dev) * NS_, hipMemcpyHostToDevice, st) == hipSuccess &&
                   hipMemcpyAsync(d_ch, ch.data(), sizeof(pf_chunk_dev) * NC, hipMemcpyHostToDevice, st) == hipSuccess &&
                   hipMemcpyAsync(d_win, wd.data(), sizeof(pf_win_dev) * W, hipMemcpyHostToDevice, st) == hipSuccess &&
-                  hipEventRecord(ev[0], st) == hipSuccess;
-        if (ok) ok = pf_inflate_launch((pf_ctx *)ctx, st, d_comp, d_blk, P.blk.data(), NB, d_arena, d_bst, ev[0], ev[1]) == PF_OK &&
-                     hipEventRecord(ev[2], st) == hipSuccess;
+                  hipEventRecord(ev[2], st) == hipSuccess;
         // ---- chain: count, offsets, write
         if (ok && NS_) {
             hipLaunchKernelGGL(pf_chain, dim3((NS_ + 63) / 64), dim3(64), 0, st, d_arena, d_sg, NS_, (uint64_t *)nullptr);
             ok = hipGetLastError() == hipSuccess;
         }
         std::vector<uint32_t> bst(NB);
-        ok = ok && hipMemcpyAsync(bst.data(), d_bst, 4ull * NB, hipMemcpyDeviceToHost, st) == hipSuccess &&
-             hipMemcpyAsync(sg.data(), d_sg, sizeof(pf_seg_dev) * NS_, hipMemcpyDeviceToHost, st) == hipSuccess &&
+        for (const Batch &B : batches)
+            ok = ok && hipMemcpyAsync(bst.data() + B.b0, B.d_st, 4ull * B.n, hipMemcpyDeviceToHost, st) == hipSuccess;
+        ok = ok && hipMemcpyAsync(sg.data(), d_sg, sizeof(pf_seg_dev) * NS_, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipStreamSynchronize(st) == hipSuccess;
         if (!ok) { evdone(); rc = PF_ERR_HIP; break; }
         for (uint32_t i = 0; i < NB; i++)
