@@ -261,8 +261,10 @@ extern "C" void pf_ctx_stage_trim(pf_ctx *c, size_t keep) {
     }
 }
 
+extern "C" void pf_fetch_cache_enable(pf_ctx_t *ctx, int on);
 extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     if (!c) return;
+    pf_fetch_cache_enable(c, 0);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);

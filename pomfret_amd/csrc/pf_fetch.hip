@@ -289,19 +289,32 @@ __global__ __launch_bounds__(256) void pf_select(const pf_win_dev *wins, uint32_
     if (write && W.skip) return;
     uint64_t done = 0;
     uint32_t cnt = 0, status = PF_WIN_OK;
+    uint32_t nxt = UINT32_MAX, nxt_run = UINT32_MAX;    // the chain record after the last one read
     bool stop = false;
     for (uint32_t c = W.c0; c < W.c1 && !stop; c++) {
         const pf_chunk_dev C = chunks[c];
         const uint64_t at = C.u > done ? C.u : done;
         if (at >= C.v) continue;
         const pf_run_dev Rn = runs[C.run];
-        // the chain record starting at `at` (a lower bound over the run's chain)
-        uint32_t lo = Rn.rec0, n = Rn.n_rec;
-        while (n > 0) {
-            const uint32_t h = n >> 1;
-            if (R.pos[lo + h] < at) { lo += h + 1; n -= h + 1; } else n = h;
-        }
         const uint32_t rend = Rn.rec0 + Rn.n_rec;
+        // the chain record starting at `at`: among the 64 after the last one
+        // read (consecutive chunks of a long query), else a lower bound over
+        // the run's chain
+        uint32_t lo = UINT32_MAX;
+        if (C.run == nxt_run) {
+            const uint32_t k = nxt + lane;
+            const uint64_t hit = __ballot(k < rend && R.pos[k] == at);
+            if (hit) lo = nxt + (uint32_t)__ffsll((long long)hit) - 1;
+        }
+        if (lo == UINT32_MAX) {
+            lo = Rn.rec0;
+            uint32_t n = Rn.n_rec;
+            while (n > 0) {
+                const uint32_t h = n >> 1;
+                if (R.pos[lo + h] < at) { lo += h + 1; n -= h + 1; } else n = h;
+            }
+        }
+        lo = uni(lo);
         uint32_t idx = lo;
         if (idx < rend ? R.pos[idx] != at : at != Rn.stop_pos) { status = PF_WIN_ERR; break; }
         for (;;) {
@@ -340,6 +353,8 @@ __global__ __launch_bounds__(256) void pf_select(const pf_win_dev *wins, uint32_
                 // the chunk ends before lane ni: either a record starting at or
                 // after v, or the chain's end
                 const uint32_t ke = idx + ni;
+                nxt = ke;
+                nxt_run = C.run;
                 if (ke >= rend) {
                     if (Rn.stop_pos < C.v) {                           // the chunk wants more records
                         if (Rn.stop == PF_CHAIN_CORRUPT) status = PF_WIN_ERR;

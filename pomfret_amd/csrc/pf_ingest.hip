@@ -163,6 +163,7 @@ out:
 #include <chrono>
 #include <mutex>
 #include <thread>
+#include <string>
 #include <errno.h>
 #include <fcntl.h>
 #include <unistd.h>
@@ -205,11 +206,96 @@ struct Range {
 struct Plan {
     std::vector<pf_bgzf_blk> blk;
     std::vector<uint64_t> caddr;            // file address of each block
+    std::vector<uint32_t> bsize;            // its BGZF size
     std::vector<Range> runs;
     uint8_t *comp = nullptr;                // compressed bytes of every run, back to back (pinned)
     uint64_t comp_n = 0;
     uint64_t arena = 0;                     // inflated bytes
 };
+
+// Whole-contig arenas kept on the device between the -u pre-pass and the
+// window jobs (HBM holds a contig's inflated BAM many times over): the
+// pre-pass fetches each contig whole, and a window job of that contig on the
+// same context then takes its blocks from the kept arena instead of reading
+// and inflating them again.  Keyed by context, file (path, size, mtime) and
+// contig; kept while the device keeps a reserve free; released by
+// pf_fetch_cache_clear (end of a methphase run, context destruction).
+struct ArenaCache {
+    const pf_ctx_t *ctx = nullptr;
+    std::string path;
+    uint64_t fsize = 0;
+    int64_t mt_s = 0, mt_ns = 0;
+    int32_t tid = -1;
+    uint8_t *d_arena = nullptr;             // arena bytes + 512 zero bytes
+    uint64_t arena = 0;
+    std::vector<uint64_t> caddr, out_off;   // per block: file address, arena offset
+    std::vector<uint32_t> bsize, isize, run; // its BGZF and inflated sizes, its run
+    std::vector<uint64_t> run_f1;           // per run: the end of the file range its scan covered
+};
+std::mutex g_cache_mu;
+std::vector<ArenaCache *> g_cache;
+std::vector<const pf_ctx_t *> g_keep_on;    // contexts whose -u pre-pass keeps its arenas
+
+bool cache_enabled(const pf_ctx_t *ctx) {
+    static const bool off = [] { const char *e = getenv("PF_FETCH_CACHE"); return e && !strcmp(e, "0"); }();
+    if (off) return false;
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    return std::find(g_keep_on.begin(), g_keep_on.end(), ctx) != g_keep_on.end();
+}
+
+const ArenaCache *cache_find(const pf_ctx_t *ctx, const char *path, const struct stat &s, int32_t tid) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    for (const ArenaCache *c : g_cache)
+        if (c->ctx == ctx && c->tid == tid && c->fsize == (uint64_t)s.st_size && c->mt_s == (int64_t)s.st_mtim.tv_sec &&
+            c->mt_ns == (int64_t)s.st_mtim.tv_nsec && c->path == path)
+            return c;
+    return nullptr;
+}
+
+// The plan's blocks from a kept arena: per run, the kept blocks from its
+// first address while they lie whole inside the run -- the blocks the scan of
+// the file bytes would find.  False when the kept arena does not cover a run
+// (its blocks stop before the run does, short of EOF).
+bool plan_from_cache_(const ArenaCache &C, Plan &P, uint64_t fsize);
+bool plan_from_cache(const ArenaCache &C, Plan &P, uint64_t fsize) {
+    if (plan_from_cache_(C, P, fsize)) return true;
+    P.blk.clear(); P.caddr.clear(); P.bsize.clear();     // the file path scans from scratch
+    for (Range &R : P.runs) { R.b0 = R.b1 = 0; R.end_addr = 0; R.to_eof = false; R.scan = 0; }
+    P.arena = 0;
+    return false;
+}
+bool plan_from_cache_(const ArenaCache &C, Plan &P, uint64_t fsize) {
+    P.blk.clear(); P.caddr.clear(); P.bsize.clear();
+    const size_t n = C.caddr.size();
+    for (uint32_t ri = 0; ri < P.runs.size(); ri++) {
+        Range &R = P.runs[ri];
+        R.b0 = (uint32_t)P.blk.size();
+        size_t i = (size_t)(std::lower_bound(C.caddr.begin(), C.caddr.end(), R.f0) - C.caddr.begin());
+        if (i >= n || C.caddr[i] != R.f0) return false;
+        uint64_t e = R.f0;
+        for (; i < n && C.caddr[i] == e && C.caddr[i] + C.bsize[i] <= R.f1; i++) {
+            pf_bgzf_blk b;
+            memset(&b, 0, sizeof b);
+            b.out_off = C.out_off[i];
+            b.isize = C.isize[i];
+            b.run = ri;
+            P.blk.push_back(b);
+            P.caddr.push_back(e);
+            P.bsize.push_back(C.bsize[i]);
+            e += C.bsize[i];
+        }
+        // past the run: the next block is known and does not fit, or the file
+        // ends, or the kept run's scan stopped at e within a range that
+        // reached at least as far as this run's
+        const bool next_known = i < n && C.caddr[i] == e;
+        if (!next_known && e < fsize && e + 18 <= R.f1 && !(e > R.f0 && R.f1 <= C.run_f1[C.run[i - 1]])) return false;
+        R.b1 = (uint32_t)P.blk.size();
+        R.end_addr = e;
+        R.to_eof = e >= fsize;
+    }
+    P.arena = C.arena;
+    return true;
+}
 
 // The compressed bytes are staged in the context's pinned buffer (grown on
 // demand and reused by every fetch of that context: pinning costs about as
@@ -296,7 +382,8 @@ struct FetchOut {
 // the caller needs from the gathered records.
 template <typename Sink>
 static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, const int64_t *beg, const int64_t *end,
-                     uint32_t reads, uint32_t max_win_recs, pf_bam_dev_fetch_own *F, Sink &&sink) {
+                     uint32_t reads, uint32_t max_win_recs, pf_bam_dev_fetch_own *F, Sink &&sink,
+                     ArenaCache *keep = nullptr) {
     const char *path = pf_bam_path(bam);
     if (!path || tid < 0) return PF_ERR_ARG;
     const double t_start = now_ms();
@@ -317,6 +404,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
     struct stat stt;
     if (fstat(fd, &stt) != 0) { close(fd); return -1; }
     const uint64_t fsize = (uint64_t)stt.st_size;
+    const ArenaCache *AC = cache_find(ctx, path, stt, tid);
     hipStream_t st = pf_ctx_stream((const pf_ctx *)ctx);
     if (hipSetDevice(pf_ctx_device((const pf_ctx *)ctx)) != hipSuccess) { close(fd); return PF_ERR_HIP; }
     memset(&F->pub, 0, sizeof F->pub);
@@ -342,25 +430,6 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         }
         uint64_t tot = 0;
         for (auto &R : P.runs) { R.buf0 = tot; tot += R.f1 - R.f0; }
-        // The pinned buffer holds the runs' bytes, then a two-half ring of
-        // block descriptors on their way to the device.
-        constexpr uint32_t RING = 16384;                                   // descriptors per half
-        // A launch waits for MINB blocks, and launches alternate between two
-        // streams so that one's tail overlaps the next (a wave decodes a block
-        // at a few MB/s: the rate comes from blocks in flight, about one per
-        // wave slot of the chip).
-        constexpr uint32_t MINB = 4096;
-        const uint64_t ring_at = (tot + 512 + 255) & ~255ull;
-        P.comp_n = tot + 512;
-        P.comp = pf_ctx_stage((pf_ctx *)ctx, ring_at + 2ull * RING * sizeof(pf_bgzf_blk));
-        uint8_t *d_comp = D.alloc<uint8_t>(P.comp_n);
-        if (!P.comp || !d_comp) { rc = PF_ERR_NOMEM; break; }
-        pf_bgzf_blk *ring = reinterpret_cast<pf_bgzf_blk *>(P.comp + ring_at);
-        // The inflated arena is sized from the compressed bytes (BAM inflates
-        // 1.5-3x); blocks past it wait for an exact arena after the reads.
-        const uint64_t acap = 4 * tot + (1ull << 20);
-        uint8_t *d_arena = D.alloc<uint8_t>(acap + 512);
-        if (!d_arena) { rc = PF_ERR_NOMEM; break; }
         hipStream_t cs = pf_ctx_stream2((const pf_ctx *)ctx), s3 = pf_ctx_stream3((const pf_ctx *)ctx);
         D.st2 = cs;
         D.st3 = s3;
@@ -382,6 +451,34 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         // per batch of blocks: its device descriptors and status words
         struct Batch { uint32_t b0, n; pf_bgzf_blk *d_blk; uint32_t *d_st; };
         std::vector<Batch> batches;
+        uint8_t *d_arena = nullptr;
+        // a whole-contig arena of this context holding every block of the plan
+        // (the -u pre-pass's): no reads, no inflate
+        const bool cached = AC && plan_from_cache(*AC, P, fsize);
+        if (cached) {
+            d_arena = AC->d_arena;
+            if (hipEventRecord(ev[0], st) != hipSuccess || hipEventRecord(ev[1], st) != hipSuccess) { rc = PF_ERR_HIP; break; }
+        }
+        if (!cached) {
+        // The pinned buffer holds the runs' bytes, then a two-half ring of
+        // block descriptors on their way to the device.
+        constexpr uint32_t RING = 16384;                                   // descriptors per half
+        // A launch waits for MINB blocks, and launches alternate between two
+        // streams so that one's tail overlaps the next (a wave decodes a block
+        // at a few MB/s: the rate comes from blocks in flight, about one per
+        // wave slot of the chip).
+        constexpr uint32_t MINB = 4096;
+        const uint64_t ring_at = (tot + 512 + 255) & ~255ull;
+        P.comp_n = tot + 512;
+        P.comp = pf_ctx_stage((pf_ctx *)ctx, ring_at + 2ull * RING * sizeof(pf_bgzf_blk));
+        uint8_t *d_comp = D.alloc<uint8_t>(P.comp_n);
+        if (!P.comp || !d_comp) { rc = PF_ERR_NOMEM; break; }
+        pf_bgzf_blk *ring = reinterpret_cast<pf_bgzf_blk *>(P.comp + ring_at);
+        // The inflated arena is sized from the compressed bytes (BAM inflates
+        // 1.5-3x); blocks past it wait for an exact arena after the reads.
+        const uint64_t acap = 4 * tot + (1ull << 20);
+        d_arena = D.alloc<uint8_t>(acap + 512);
+        if (!d_arena) { rc = PF_ERR_NOMEM; break; }
         uint32_t nb_sent = 0;                 // blocks whose inflate is enqueued
         uint32_t cur = 0;                     // first run not completely scanned
         bool spill = false;                   // the arena estimate was short
@@ -425,6 +522,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
                     P.arena += b.isize;
                     P.blk.push_back(b);
                     P.caddr.push_back(R.f0 + o);
+                    P.bsize.push_back(bsize);
                     o += bsize;
                 }
                 R.scan = o;
@@ -532,6 +630,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
                     hipEventRecord(ecp, s3) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess ||
                     hipEventRecord(ev[1], st) != hipSuccess))
             rc = PF_ERR_HIP;
+        }
         if (rc) break;
         const double t_read = now_ms() - t0;
         const uint32_t NB = (uint32_t)P.blk.size(), NR = (uint32_t)P.runs.size();
@@ -818,8 +917,8 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         pub.qname = F->qn.data();
         pub.hp_tag = F->s.hp_tag.data();
         pub.n_truncated = n_trunc;
-        pub.comp_bytes = tot;
-        pub.inflated_bytes = P.arena;
+        pub.comp_bytes = cached ? 0 : tot;           // (a kept arena: nothing read or inflated)
+        pub.inflated_bytes = cached ? 0 : P.arena;
         pub.n_blocks = NB;
         pub.n_chain_recs = NRec;
         pub.ms_read = t_read;
@@ -831,6 +930,32 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         pub.ms_total = now_ms() - t_start;
         pub.attempts = (uint32_t)attempt + 1;
         done = true;
+        if (keep && !cached) {
+            // an exact copy of the arena (the fetch's own is sized from the
+            // compressed bytes), if the device keeps its reserve
+            size_t fr = 0, tt = 0;
+            const uint64_t need = P.arena + 512;
+            uint8_t *k = nullptr;
+            if (hipMemGetInfo(&fr, &tt) == hipSuccess && fr > need && fr - need > std::max<size_t>(tt / 3, 32ull << 30) &&
+                hipMalloc(&k, need) == hipSuccess) {
+                if (hipMemcpyAsync(k, d_arena, need, hipMemcpyDeviceToDevice, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess) {
+                    keep->ctx = ctx; keep->path = path; keep->fsize = fsize; keep->tid = tid;
+                    keep->mt_s = (int64_t)stt.st_mtim.tv_sec; keep->mt_ns = (int64_t)stt.st_mtim.tv_nsec;
+                    keep->d_arena = k; keep->arena = P.arena;
+                    keep->caddr = P.caddr; keep->bsize = P.bsize;
+                    keep->out_off.resize(NB); keep->isize.resize(NB); keep->run.resize(NB);
+                    for (uint32_t i = 0; i < NB; i++) {
+                        keep->out_off[i] = P.blk[i].out_off; keep->isize[i] = P.blk[i].isize; keep->run[i] = P.blk[i].run;
+                    }
+                    keep->run_f1.resize(NR);
+                    for (uint32_t r = 0; r < NR; r++) keep->run_f1[r] = P.runs[r].f1;
+                } else {
+                    (void)hipFree(k);
+                }
+            }
+            (void)hipGetLastError();
+        }
         break;
     }
     close(fd);
@@ -960,6 +1085,7 @@ static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *ba
         const int64_t beg = (int64_t)k * step, end = k + 1 == NP ? INT64_MAX : (int64_t)(k + 1) * step;
         pf_bam_dev_fetch_own P;
         std::vector<uint32_t> take;                           // this piece's -u reads: selection positions
+        ArenaCache *keep = NP == 1 && cache_enabled(ctx) ? new ArenaCache() : nullptr;
         rc = dev_fetch(ctx, bam, tid, 1, &beg, &end, with_cov ? 0u : 1u, 0u, &P, [&](FetchOut &fo) -> int {
             const Small &S = *fo.S;
             uint64_t m = 0;                                   // records counted in an earlier piece
@@ -1024,7 +1150,14 @@ static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *ba
             pf_k4_reads_host h{start.data(), endp.data(), nins.data(), ncig.data(), mdl.data()};
             pf_k4_reads_dev dv{d_start, d_end, d_co, d_cig, d_so, d_len, d_seq, d_mo, d_md};
             return pf_haptag_core(ctx, K, (uint32_t)N, h, nullptr, &dv, F->read_hp.data() + h0, &prev_left);
-        });
+        }, keep);
+        if (keep && keep->d_arena && !rc) {
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            g_cache.push_back(keep);
+        } else if (keep) {
+            if (keep->d_arena) (void)hipFree(keep->d_arena);
+            delete keep;
+        }
         if (rc) break;
         // this piece's reads' qnames
         for (const uint32_t i : take) {
@@ -1146,4 +1279,31 @@ extern "C" int pf_bam_estimate_coverage_dev(pf_ctx_t *ctx, pf_bam_t *bam, int32_
     }
     if (!stopped && n_unplaced > 0 && last >= 0) covs[last] = 0;
     return PF_OK;
+}
+
+// release the kept whole-contig arenas of a context (all contexts: NULL)
+extern "C" void pf_fetch_cache_clear(pf_ctx_t *ctx) {
+    std::vector<ArenaCache *> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        std::vector<ArenaCache *> keep;
+        for (ArenaCache *c : g_cache) (ctx == nullptr || c->ctx == ctx ? drop : keep).push_back(c);
+        g_cache.swap(keep);
+    }
+    for (ArenaCache *c : drop) {
+        (void)hipFree(c->d_arena);
+        delete c;
+    }
+}
+
+// keep the -u pre-pass's whole-contig arenas of a context for its window jobs
+// (on), or stop and release them (off)
+extern "C" void pf_fetch_cache_enable(pf_ctx_t *ctx, int on) {
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto it = std::find(g_keep_on.begin(), g_keep_on.end(), ctx);
+        if (on && it == g_keep_on.end()) g_keep_on.push_back(ctx);
+        if (!on && it != g_keep_on.end()) g_keep_on.erase(it);
+    }
+    if (!on) pf_fetch_cache_clear(ctx);
 }

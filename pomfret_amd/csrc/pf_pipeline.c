@@ -1462,6 +1462,7 @@ int pf_mp_run_mine(pf_mp_plan_t *p, const pf_methphase_opts_t *run_opts, int kin
 }
 
 static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out);
+void pf_fetch_cache_enable(pf_ctx_t *ctx, int on);   /* pf_ingest.hip */
 
 /* one set of contexts for the whole run (coverage pass, -u pre-pass, window
  * jobs): a context's streams, pinned staging and kernels are set up once, not
@@ -1506,12 +1507,17 @@ static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     }
     pf_mp_plan_t *p = NULL;
     int rc = mp_plan(o, &p, 1);
+    /* the -u pre-pass's whole-contig arenas stay on the device for the window
+     * jobs of the same context (device fetch only) */
+    const int keep = !rc && o->untagged && !o->host_fetch && o->n_ctxs > 0;
+    for (int d = 0; keep && d < o->n_ctxs; d++) pf_fetch_cache_enable(o->ctxs[d], 1);
     if (!rc && o->untagged) {
         rc = run_on_devices(p, o, PF_JOB_HAPTAG);
         if (!rc) rc = pf_mp_merge_raw(p);
     }
     if (!rc && p->est_deferred) rc = finish_deferred_estimate(p, o->ctxs[0]);
     if (!rc) rc = run_on_devices(p, o, PF_JOB_WINDOWS);
+    for (int d = 0; keep && d < o->n_ctxs; d++) pf_fetch_cache_enable(o->ctxs[d], 0);
     if (!rc) rc = pf_mp_finish(p);
     if (rc) { pf_mp_free(p); return rc; }
     if (p->n_limit)
