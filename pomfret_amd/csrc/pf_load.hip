@@ -41,6 +41,9 @@
 
 #define DEV static __device__ __forceinline__
 #define NT_C 2u
+#ifndef PF_K0_SEQ_REREAD
+#define PF_K0_SEQ_REREAD 1                 // SEQ pass: trigger words re-read (1) or taken by ds_bpermute (0)
+#endif
 
 // Diagnostic build only (-DPF_K0_PROFILE): cycles per phase summed over the
 // records into ctr[8 + phase] (s_memtime, one fenced asm statement).
@@ -597,6 +600,24 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                 const uint32_t c0 = L.u.s.sc[i * 64 + Lw];
                 if (k >= c0) { k -= c0; hw = 1; }
             }
+#if PF_K0_SEQ_REREAD
+            // The trigger's word and its neighbour word (the context base at a
+            // word edge) are read again from SEQ: the block was just loaded, so
+            // the two 8-byte loads per trigger hit the caches.
+            bool edge = false;
+            uint2 xv = make_uint2(0, 0), nv = make_uint2(0, 0);
+            uint32_t w = 0;
+            if (act) {
+                w = b * BW + i * RW + 2 * Lw + hw;
+                const uint32_t wn = rev ? (w > 0 ? w - 1 : 0u) : (w + 1 < nwords ? w + 1 : w);
+                const uint2 *sq2 = reinterpret_cast<const uint2 *>(seq);
+                xv = sq2[w];
+                nv = sq2[wn];
+            }
+            if (act) {
+                const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(((uint64_t)xv.y << 32) | xv.x);
+                const uint64_t xn = nibswap(((uint64_t)nv.y << 32) | nv.x);
+#else
             // The trigger's word and its neighbour word (the context base at a
             // word edge) come from the registers of the lane that loaded them
             // (ds_bpermute), not from a second read of SEQ: lane Lw of row i
@@ -640,6 +661,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                 const uint32_t w = b * BW + i * RW + 2 * Lw + hw;
                 const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(((uint64_t)x1 << 32) | x0);
                 const uint64_t xn = nibswap(((uint64_t)n1 << 32) | n0);
+#endif
                 const uint32_t bi = sel_nibble(zero_nibbles(xw ^ pat), k);
                 const uint32_t p = w * 16 + bi;
                 uint32_t key = 0xFFFFFFFFu;
