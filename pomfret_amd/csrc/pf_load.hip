@@ -42,7 +42,7 @@
 #define DEV static __device__ __forceinline__
 #define NT_C 2u
 #ifndef PF_K0_SEQ_REREAD
-#define PF_K0_SEQ_REREAD 1                 // SEQ pass: trigger words re-read (1) or taken by ds_bpermute (0)
+#define PF_K0_SEQ_REREAD 0                 // SEQ pass: trigger words re-read (1: +4.6 GB HBM reads on the mix, no faster) or taken by ds_bpermute (0)
 #endif
 
 // Diagnostic build only (-DPF_K0_PROFILE): cycles per phase summed over the
