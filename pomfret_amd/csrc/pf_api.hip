@@ -786,6 +786,14 @@ extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cf
             for (uint32_t r = a->win_rec_off[w]; r < a->win_rec_off[w + 1]; r++) rw[r] = w;
         PUT(p32, rw.data(), n); ld.rec_win = p32;
         PUT(p32, a->win_rec_off, W + 1); ld.win_rec_off = p32;
+        // pack's workgroups: the windows with the most records first (the
+        // long copies start in the first wave of workgroups, not in the tail)
+        std::vector<uint32_t> wo(W);
+        for (uint32_t w = 0; w < W; w++) wo[w] = w;
+        std::stable_sort(wo.begin(), wo.end(), [&](uint32_t x, uint32_t y) {
+            return a->win_rec_off[x + 1] - a->win_rec_off[x] > a->win_rec_off[y + 1] - a->win_rec_off[y];
+        });
+        PUT(p32, wo.data(), W); ld.win_order = p32;
         ALLOC(p32, 2ull * W); ld.win_kept = p32; ld.win_calls = p32 + W;
         ALLOC(p64, W + 1); ld.win_call_off = p64;
         unsigned long long *pc; ALLOC(pc, PF_K0_NCTR); ld.ctr = pc; b->k0_ctr = pc;

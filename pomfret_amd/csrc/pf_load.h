@@ -63,6 +63,7 @@ struct pf_load_dev {
     uint32_t diag;                   /* measurement only (PF_K0_DIAG): 1 = trigger placement reads no SEQ word */
     const uint32_t *order;           /* [n_recs] record of each wave slot: longest reads first */
     const uint32_t *rec_win;         /* [n_recs] window of each record */
+    const uint32_t *win_order;       /* [W] pack's workgroups: windows with the most records first */
     const uint32_t *win_rec_off;     /* [W+1] records of each window */
     const uint16_t *flag;
     const uint8_t *mapq;

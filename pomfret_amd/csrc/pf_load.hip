@@ -1323,7 +1323,7 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
     __shared__ uint32_t sh32[2 * NW];
     __shared__ uint32_t l_n[NT];
     __shared__ uint64_t l_src[NT], l_dst[NT];
-    const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t w = d.win_order[blockIdx.x], tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t rb = d.win_read_off[w], re = d.win_read_off[w + 1];
     const bool last = w + 1 == d.n_windows;
     if (re == rb) {
