@@ -17,11 +17,14 @@ methphase` derives them without -c (cov_for_selection 7, cov_for_runtime 14,
 n_cand 16; blockjoin.c:4373-4375), loader defaults -q 10 -L 15000, ML bands
 100/156 (cli.c:52-63).  --coverage 30 --windows 256 is configs[1]'s shape.
 
-Multi-GPU (torchrun, one process per GPU): strong scaling by default -- the
-job's 1024 windows are dealt over the ranks, no collective in the data path;
-after each step the int8 decisions are gathered to every rank over RCCL (the
-drop-in's only exchange: the host that writes VCF/GTF needs all decisions).
---weak gives every rank its own --windows windows.
+Multi-GPU (torchrun, one process per GPU): weak scaling by default -- the
+path partitions into independent windows, and a real run (a whole genome:
+tens of thousands of windows) keeps every GPU's share large as N grows, so
+every rank owns a batch of --windows windows of its own (seeds differ per
+rank); no collective in the data path; after each step the int8 decisions
+are gathered to every rank over RCCL (the drop-in's only exchange: the host
+that writes VCF/GTF needs all decisions).  --strong deals one job's windows
+over the ranks instead (total work fixed).
 
 Prints ONE JSON line on rank 0.
 """
@@ -404,11 +407,12 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--windows", type=int, default=WORKLOAD["n_windows"],
-                    help="windows of the job (strong scaling, dealt over the ranks); per rank with --weak")
+                    help="windows per rank (weak scaling, the default); the job's windows with --strong")
     ap.add_argument("--coverage", type=int, default=WORKLOAD["coverage"])
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mix",
                     help="mix: log-uniform 5-500 kb gaps with skipped / site-less windows; fixed50: 50 kb gaps")
-    ap.add_argument("--weak", action="store_true", help="every rank owns --windows windows of its own")
+    ap.add_argument("--weak", action="store_true", help="every rank owns --windows windows of its own (default)")
+    ap.add_argument("--strong", action="store_true", help="one job of --windows windows dealt over the ranks")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-legs", action="store_true", help="skip the calls-level and PCIe-inclusive legs")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -428,14 +432,15 @@ def main():
     from pomfret_amd.synth import SynthSpec, make_batch
     from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
 
+    args.weak = not args.strong
     wl = dict(WORKLOADS[args.workload], n_windows=args.windows, coverage=args.coverage)
     cfg = Config.from_coverage(wl["coverage"], given=False)
     lcfg = LoadConfig()
     record_level = not args.calls_level
-    # Strong scaling (default): one job of wl["n_windows"] windows, dealt
-    # round-robin to the ranks (the synthetic windows are i.i.d.; the product's
-    # sharder, pomfret_amd.shard, balances real windows by LPT on their bytes).
-    # --weak: every rank owns wl["n_windows"] windows of its own.
+    # Weak scaling (default): every rank owns wl["n_windows"] windows of its
+    # own.  --strong: one job of wl["n_windows"] windows, dealt round-robin to
+    # the ranks (the synthetic windows are i.i.d.; the product's sharder,
+    # pomfret_amd.shard, balances real windows by LPT on their bytes).
     if args.weak:
         mine = list(range(wl["n_windows"]))
         seed = 1000 + rank
