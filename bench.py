@@ -420,6 +420,8 @@ def main():
                     help="windows of the end-to-end (BAM file -> decisions) leg; 0 skips it")
     ap.add_argument("--e2e-u-scale", type=float, default=1.0,
                     help="genome scale of the configs[3]-shaped -u leg (1.0: 96 Mb, ~1,000 windows); 0 skips it")
+    ap.add_argument("--split", type=int, default=1,
+                    help="also time the windows as this many batches on as many contexts of the GPU")
     ap.add_argument("--calls-level", action="store_true",
                     help="time the calls-level boundary (reads + 5mC calls resident, no K0)")
     args = ap.parse_args()
@@ -596,6 +598,46 @@ def main():
                      "what": "round 2's workload: 1024 windows x 50 kb gaps at 60x, records resident"}
         del a50
 
+    split_leg = None
+    if record_level and args.split > 1:
+        # the same windows as S batches, each on its own context of this GPU
+        # (own streams, own device buffers), launched together every step: one
+        # batch's K0/K12 fill the CUs the other's K3 tail leaves idle.  Windows
+        # are dealt to the batches heaviest first (record counts), round-robin.
+        nrec_w = np.diff(aln.win_rec_off.astype(np.int64))
+        order = np.argsort(-nrec_w, kind="stable")
+        parts = [sorted(order[s::args.split].tolist()) for s in range(args.split)]
+        sctx = [ctx] + [Context(local_rank) for _ in range(args.split - 1)]
+        sdb = [c.upload_aln(cfg, aln.select(p), lcfg) for c, p in zip(sctx, parts)]
+        souts = [[d.run(), d.run()] for d in sdb]
+        for _ in range(args.warmup):
+            for d, o in zip(sdb, souts):
+                d.run(o[0])
+        n_sr = sum(int(o[0].win_n_reads.sum()) for o in souts)
+        t1 = time.perf_counter()
+        for d in sdb:
+            d.launch()
+        for k in range(args.steps):
+            if k + 1 < args.steps:
+                for d in sdb:
+                    d.launch()
+            for d, o in zip(sdb, souts):
+                d.finish(o[k % 2])
+        el_s = time.perf_counter() - t1
+        dec = np.empty_like(out.decision)
+        for p, o in zip(parts, souts):
+            dec[np.asarray(p)] = o[(args.steps - 1) % 2].decision
+        split_leg = {"value": round(n_sr * args.steps / el_s, 1), "ms_per_step": round(el_s / args.steps * 1e3, 4),
+                     "batches": args.split, "reads": n_sr,
+                     "decisions_match": bool(np.array_equal(dec, out.decision)),
+                     "what": f"same windows as {args.split} batches on {args.split} contexts of this GPU, "
+                             "launched together every step"}
+        log(f"[bench] split: {json.dumps(split_leg)}")
+        for d in sdb:
+            d.free()
+        for c in sctx[1:]:
+            c.close()
+
     # PCIe-inclusive rate (never `value`): the one-shot boundary call hands
     # over host buffers -- upload (validation, pinned staging, H2D), run, D2H
     pcie = None
@@ -711,6 +753,7 @@ def main():
         "e2e_u": e2e_u,
         "calls_level": calls_leg,
         "fixed_gap50": fixed_leg,
+        "split": split_leg,
         "decisions": {"cis": int((out.decision == 0).sum()), "trans": int((out.decision == 1).sum()),
                       "none": int((out.decision < 0).sum())},
     }
