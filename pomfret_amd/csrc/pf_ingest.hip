@@ -243,10 +243,15 @@ bool cache_enabled(const pf_ctx_t *ctx) {
     return std::find(g_keep_on.begin(), g_keep_on.end(), ctx) != g_keep_on.end();
 }
 
+// An arena kept by any context of the same device serves this one: the
+// driver's contexts of one GPU (PF_DEV_CONTEXTS) share its HBM, and the -u
+// pre-pass that wrote the arenas has finished (its jobs joined) before the
+// window jobs look them up.
 const ArenaCache *cache_find(const pf_ctx_t *ctx, const char *path, const struct stat &s, int32_t tid) {
+    const int dev = pf_ctx_device((const pf_ctx *)ctx);
     std::lock_guard<std::mutex> lk(g_cache_mu);
     for (const ArenaCache *c : g_cache)
-        if (c->ctx == ctx && c->tid == tid && c->fsize == (uint64_t)s.st_size && c->mt_s == (int64_t)s.st_mtim.tv_sec &&
+        if ((c->ctx == ctx || pf_ctx_device((const pf_ctx *)c->ctx) == dev) && c->tid == tid && c->fsize == (uint64_t)s.st_size && c->mt_s == (int64_t)s.st_mtim.tv_sec &&
             c->mt_ns == (int64_t)s.st_mtim.tv_nsec && c->path == path)
             return c;
     return nullptr;

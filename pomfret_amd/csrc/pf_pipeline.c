@@ -1471,12 +1471,24 @@ int pf_methphase_main(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     if (!o || !out) return PF_ERR_ARG;
     *out = NULL;
     if (o->world > 1) return PF_ERR_ARG;           /* multi-process runs use the pf_mp_* steps */
-    const int nd = o->n_ctxs > 0 ? 0 : (o->n_devices > 0 ? o->n_devices : pf_device_count());
-    if (nd <= 0) return methphase_main_(o, out);
+    const int ng = o->n_ctxs > 0 ? 0 : (o->n_devices > 0 ? o->n_devices : pf_device_count());
+    if (ng <= 0) return methphase_main_(o, out);
+    /* PF_DEV_CONTEXTS contexts per GPU (default 2, at most 4), each on its own
+     * host thread over the shared job queue: one job's K0/K12 fill the CUs
+     * another job's K3 tail leaves idle (bench.py --split: 18.5 -> 17.0 ms on
+     * the 1024-window mix).  Two contexts are four streams, the box's
+     * GPU_MAX_HW_QUEUES; more would share hardware queues (4: 25 ms). */
+    int per = 2;
+    const char *e = getenv("PF_DEV_CONTEXTS");
+    if (e && *e) per = atoi(e);
+    if (per < 1) per = 1;
+    if (per > 4) per = 4;
+    const int nd = ng * per;
     pf_ctx_t **ctxs = (pf_ctx_t **)calloc((size_t)nd, sizeof(pf_ctx_t *));
     if (!ctxs) return PF_ERR_NOMEM;
     int rc = PF_OK;
-    for (int d = 0; d < nd && !rc; d++) rc = pf_ctx_create(o->devices ? o->devices[d] : d, &ctxs[d]);
+    /* device-major within each round, so the first jobs spread over the GPUs */
+    for (int d = 0; d < nd && !rc; d++) rc = pf_ctx_create(o->devices ? o->devices[d % ng] : d % ng, &ctxs[d]);
     if (!rc) {
         pf_methphase_opts_t oo = *o;
         oo.ctxs = ctxs;

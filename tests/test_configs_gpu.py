@@ -159,9 +159,10 @@ def _golden_check(out, gaps):
     assert gtf.replace("\t.\t+", ".\t+", 1) == open(os.path.join(GOLD, "output.mp.gtf")).read()
 
 
-def _cli(*args, timeout=300):
+def _cli(*args, timeout=300, env=None):
     exe = os.path.join(ROOT, "pomfret_amd", "pomfret-amd")
-    return subprocess.run([exe, *args], capture_output=True, text=True, timeout=timeout)
+    return subprocess.run([exe, *args], capture_output=True, text=True, timeout=timeout,
+                          env=dict(os.environ, **env) if env else None)
 
 
 def test_cli_methphase_example(oracle_lib, tmp_path):
@@ -180,14 +181,18 @@ def test_cli_methphase_example(oracle_lib, tmp_path):
     _golden_check(out, gaps)
 
 
-def test_cli_untagged_no_c(oracle_lib, tmp_path):
+@pytest.mark.parametrize("per_gpu", [None, "1", "3"])
+def test_cli_untagged_no_c(oracle_lib, tmp_path, per_gpu):
     """`pomfret-amd methphase -u` without -c: the K4 pre-pass, then the
-    per-contig parameters from the coverage estimate (4357-4374)."""
+    per-contig parameters from the coverage estimate (4357-4374).  per_gpu:
+    PF_DEV_CONTEXTS (default 2 contexts per GPU; the window jobs of one
+    context read the -u arenas another context of the GPU kept)."""
     from pomfret_amd import Config
     from pomfret_amd.bam import BamFile
     aln, recs, bam, vcf = fx.untagged(tmp_path, n_windows=2, coverage=40)
     out = str(tmp_path / "cli")
-    r = _cli("methphase", "-u", "-o", out, "--vcf", vcf, "--job-windows", "1", bam)
+    r = _cli("methphase", "-u", "-o", out, "--vcf", vcf, "--job-windows", "1", bam,
+             env={"PF_DEV_CONTEXTS": per_gpu} if per_gpu else None)
     assert r.returncode == 0, r.stderr
     with BamFile(bam) as b:
         cfg = Config.from_coverage(b.estimate_coverage()[0], given=False)
