@@ -10,7 +10,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-m3}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o bench --output-format csv -- python3 $R/bench.py --no-cpu --no-legs --steps 50 --e2e-windows 0 --e2e-u-scale 0 > $O/bench_prof.json 2> $O/bench_prof.err || exit 12
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o bench --output-format csv -- python3 $R/bench.py --no-cpu --no-legs --split 1 --steps 50 --e2e-windows 0 --e2e-u-scale 0 > $O/bench_prof.json 2> $O/bench_prof.err || exit 12
 echo trace done
 PF_SYNTH_WORKERS=16 timeout -k 10 300 python3 $R/tools/run_aln_once.py 1024 0 /tmp/aln1024.npz 60 > $O/gen.log 2>&1 || exit 13
 echo gen done
