@@ -1463,6 +1463,20 @@ int pf_mp_run_mine(pf_mp_plan_t *p, const pf_methphase_opts_t *run_opts, int kin
 
 static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out);
 void pf_fetch_cache_enable(pf_ctx_t *ctx, int on);   /* pf_ingest.hip */
+int pf_ctx_device(const pf_ctx_t *ctx);              /* pf_api.hip */
+
+/* the leading contexts of `ctxs` that are on distinct devices (the driver
+ * lists its contexts device-major: one per GPU, then the second per GPU) */
+static int distinct_device_prefix(pf_ctx_t *const *ctxs, int n) {
+    int k = 0;
+    for (; k < n; k++) {
+        const int dev = pf_ctx_device(ctxs[k]);
+        int seen = 0;
+        for (int j = 0; j < k && !seen; j++) seen = pf_ctx_device(ctxs[j]) == dev;
+        if (seen) break;
+    }
+    return k > 0 ? k : 1;
+}
 
 /* one set of contexts for the whole run (coverage pass, -u pre-pass, window
  * jobs): a context's streams, pinned staging and kernels are set up once, not
@@ -1524,7 +1538,13 @@ static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     const int keep = !rc && o->untagged && !o->host_fetch && o->n_ctxs > 0;
     for (int d = 0; keep && d < o->n_ctxs; d++) pf_fetch_cache_enable(o->ctxs[d], 1);
     if (!rc && o->untagged) {
-        rc = run_on_devices(p, o, PF_JOB_HAPTAG);
+        /* the -u pre-pass on one context per device: its whole-contig fetches
+         * are bound by the file reads, and a second context per GPU would only
+         * pin a second contig-sized staging buffer (e2e_u CLI 2.1 -> 2.9 s);
+         * the window jobs then run on every context and share the arenas */
+        pf_methphase_opts_t ou = *o;
+        if (o->n_ctxs > 1) ou.n_ctxs = distinct_device_prefix(o->ctxs, o->n_ctxs);
+        rc = run_on_devices(p, &ou, PF_JOB_HAPTAG);
         if (!rc) rc = pf_mp_merge_raw(p);
     }
     if (!rc && p->est_deferred) rc = finish_deferred_estimate(p, o->ctxs[0]);
