@@ -9,6 +9,10 @@ are already resident in HBM:
   K3 greedy + 2x2 tables (+ K3 fallback) -> D2H -> host Fisher test, join
   decisions and read tags (pf_methphase_launch + pf_methphase_finish, two
   steps in flight).
+The batch's windows run as `--split` (default 2) batches on as many contexts
+of the GPU, launched together every step -- what the driver does with its
+PF_DEV_CONTEXTS contexts per GPU; the single-batch run of the same step is
+timed too and gives the per-kernel figures and the roofline.
 `--calls-level` times the previous boundary instead (reads and 5mC calls
 resident, no K0).  Workload at N=1: BASELINE.json's target is quoted on HG002
 60x at 1 GPU, so the job is 1024 gap windows of 50 kb at 60x (HG002-like,
