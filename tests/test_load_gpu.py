@@ -137,3 +137,47 @@ def test_mm_parser_fuzz(oracle_lib, gpu_ctx, seed):
     db, b = _check_calls(oracle_lib, gpu_ctx, Config(), LOAD_CFG_SMALL, aln, f"mm-fuzz{seed}")
     assert 0 < db.n_reads < aln.n_recs
     db.free()
+
+
+def test_two_contexts_launched_together(oracle_lib, gpu_ctx):
+    """The bench's (and the driver's) two contexts per GPU: a record-level
+    batch's windows as two batches on two contexts of device 0, launched
+    together and pipelined two deep (pf_methphase_launch / _finish, as in
+    bench.py), give every window the one-context run's decision, join and
+    2x2 tables, and every read its tag."""
+    from pomfret_amd import Config, Context, LoadConfig
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    cfg = Config.from_coverage(60, given=False)
+    lcfg = LoadConfig()
+    aln = make_aln_batch(AlnSpec(n_windows=12, coverage=60, gap=50_000, seed=7, gap_mix=True,
+                                 skip_frac=0.1, nosite_frac=0.1))
+    ref = gpu_ctx.upload_aln(cfg, aln, lcfg).run()
+    nrec = np.diff(aln.win_rec_off.astype(np.int64))
+    order = np.argsort(-nrec, kind="stable")
+    parts = [np.sort(order[s::2]) for s in range(2)]
+    ctx2 = Context(0)
+    try:
+        dbs = [c.upload_aln(cfg, aln.select(p.tolist()), lcfg) for c, p in zip((gpu_ctx, ctx2), parts)]
+        outs = [[d.run(), d.run()] for d in dbs]
+        steps = 5
+        for d in dbs:
+            d.launch()
+        for k in range(steps):
+            if k + 1 < steps:
+                for d in dbs:
+                    d.launch()
+            for d, o in zip(dbs, outs):
+                d.finish(o[k % 2])
+        for p, o in zip(parts, outs):
+            got = o[(steps - 1) % 2]
+            assert np.array_equal(got.decision, ref.decision[p])
+            assert np.array_equal(got.dir_join, ref.dir_join[p])
+            assert np.array_equal(got.dir_table, ref.dir_table[p])
+            assert np.array_equal(got.win_n_reads, ref.win_n_reads[p])
+            ro = np.concatenate([[0], np.cumsum(ref.win_n_reads.astype(np.int64))])
+            want = np.concatenate([ref.read_hp[ro[w]:ro[w + 1]] for w in p])
+            assert np.array_equal(got.read_hp, want)
+        for d in dbs:
+            d.free()
+    finally:
+        ctx2.close()
