@@ -555,8 +555,9 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             return in->win_read_off[a + 1] - in->win_read_off[a] > in->win_read_off[c + 1] - in->win_read_off[c];
         });
         PUT(p, word.data(), word.size()); d.k12_order = p;
-        // Heavy problems: windows with at least twice the median reads (and
-        // >= 600).  They lead k3_order, and run in pf_k3_heavy on the
+        // Heavy problems: windows with at least 1.25x the median reads (and
+        // >= 600; 2x until the two-context sweep, profiles/r03/sweeps/
+        // heavy_x_two_ctx: 17.01 -> 16.92 ms/step, one batch 18.43 -> 18.16).  They lead k3_order, and run in pf_k3_heavy on the
         // context's second stream beside the main greedy kernel, starting at
         // once with the fallback's LDS budget instead of being deferred to the
         // fallback kernel after it (the serial tail of a gap mix: ~200 problems
@@ -567,7 +568,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
             std::nth_element(rw.begin(), rw.begin() + W / 2, rw.end());
             const char *hx = getenv("PF_K3_HEAVY_X");       // tuning: the multiple of the median
-            const double x = hx ? atof(hx) : 2.0;
+            const double x = hx ? atof(hx) : 1.25;
             const uint32_t thr = std::max<uint32_t>(hx ? 1u : 600u, (uint32_t)(x * rw[W / 2]));
             uint32_t nh = 0;
             while (nh < 2 * W && in->win_read_off[(ord[nh] >> 1) + 1] - in->win_read_off[ord[nh] >> 1] >= thr) nh++;
