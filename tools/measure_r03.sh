@@ -18,6 +18,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/fetch -o fetch
 echo fetch done
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/write -o write --output-format csv -- python3 $R/tools/run_aln_once.py 1024 3 /tmp/aln1024.npz 60 > $O/write.log 2>&1 || exit 15
 echo write done
+[ -x $R/tools/ubench/hbm_cal ] || hipcc --offload-arch=gfx950 -O2 -o $R/tools/ubench/hbm_cal $R/tools/ubench/hbm_cal.hip || exit 21
 rm -f /tmp/aln1024.npz
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/calf -o calf --output-format csv -- $R/tools/ubench/hbm_cal > $O/calf.log 2>&1 || exit 16
 timeout -k 10 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/calw -o calw --output-format csv -- $R/tools/ubench/hbm_cal > $O/calw.log 2>&1 || exit 17
