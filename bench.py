@@ -9,26 +9,29 @@ are already resident in HBM:
   K3 greedy + 2x2 tables (+ K3 fallback) -> D2H -> host Fisher test, join
   decisions and read tags (pf_methphase_launch + pf_methphase_finish, two
   steps in flight).
-The batch's windows run as `--split` (default 2) batches on as many contexts
-of the GPU, launched together every step -- what the driver does with its
-PF_DEV_CONTEXTS contexts per GPU; the single-batch run of the same step is
-timed too and gives the per-kernel figures and the roofline.
+The job: BASELINE.json's target is quoted on HG002 60x (a whole genome) at
+1 GPU, so the job is WGS-sized: --tiles (8) contigs, each carrying the same
+--windows (1024) distinct gap windows at 60x with SURVEY 8d's log-uniform
+5-500 kb gap mix (HG002-like, synthesised -- HG002 is not available offline),
+8192 windows in all; parameters as `pomfret methphase` derives them without
+-c (cov_for_selection 7, cov_for_runtime 14, n_cand 16; blockjoin.c:
+4373-4375), loader defaults -q 10 -L 15000, ML bands 100/156 (cli.c:52-63).
+A GPU's share of the job is a list of record-level batches (<= 1024 windows
+each) dealt over --split (2) contexts of the GPU -- what the driver does with
+its PF_DEV_CONTEXTS contexts per GPU -- and every step launches all of them.
+The first batch alone gives the per-kernel figures and the roofline.
 `--calls-level` times the previous boundary instead (reads and 5mC calls
-resident, no K0).  Workload at N=1: BASELINE.json's target is quoted on HG002
-60x at 1 GPU, so the job is 1024 gap windows of 50 kb at 60x (HG002-like,
-synthesised -- HG002 is not available offline), parameters as `pomfret
-methphase` derives them without -c (cov_for_selection 7, cov_for_runtime 14,
-n_cand 16; blockjoin.c:4373-4375), loader defaults -q 10 -L 15000, ML bands
-100/156 (cli.c:52-63).  --coverage 30 --windows 256 is configs[1]'s shape.
+resident, no K0).  --coverage 30 --windows 256 is configs[1]'s shape.
 
-Multi-GPU (torchrun, one process per GPU): weak scaling by default -- the
-path partitions into independent windows, and a real run (a whole genome:
-tens of thousands of windows) keeps every GPU's share large as N grows, so
-every rank owns a batch of --windows windows of its own (seeds differ per
-rank); no collective in the data path; after each step the int8 decisions
-are gathered to every rank over RCCL (the drop-in's only exchange: the host
-that writes VCF/GTF needs all decisions).  --strong deals one job's windows
-over the ranks instead (total work fixed).
+Multi-GPU (torchrun, one process per GPU): strong scaling by default -- the
+job's windows are dealt over the ranks by the product's LPT
+(pomfret_amd.shard.lpt_partition on the windows' SEQ + MM bytes), so the N=1
+line is the same job as the N=8 line; no collective in the data path; after
+each step the int8 decisions are all-gathered over RCCL (the drop-in's only
+exchange: the host that writes VCF/GTF needs all decisions).  --weak gives
+every rank a whole job of its own.  At N=1 the `strong_projection` leg times
+rank 0's share of the same job at N=2/4/8 on this GPU, and `critical_window`
+the heaviest window alone (the floor of any GPU's step).
 
 Prints ONE JSON line on rank 0.
 """
@@ -170,13 +173,14 @@ def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 2
     import oracle
     t0 = time.perf_counter()
     reps = 0
+    ref = None
     while reps < max_reps:
-        oracle.methphase_aln(cfg, lcfg, aln, n_threads=threads)
+        ref = oracle.methphase_aln(cfg, lcfg, aln, n_threads=threads)
         reps += 1
         if (time.perf_counter() - t0) * threads >= min_cpu_s and reps >= 2:
             break
     dt = time.perf_counter() - t0
-    return n_reads * reps / dt, dt, reps
+    return n_reads * reps / dt, dt, reps, ref
 
 
 def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu: bool = True):
@@ -405,28 +409,67 @@ def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bo
     return res
 
 
+def oracle_sample(aln, gaps, n_reads_w, n: int = 64):
+    """The cpu_baseline sample: the heaviest windows (most kept reads), the
+    widest gaps (>= 400 kb: K12's dense site path), then the first windows,
+    up to n windows in all (sorted)."""
+    heavy = np.argsort(-np.asarray(n_reads_w, np.int64), kind="stable")[:8]
+    wide = [int(w) for w in np.argsort(-np.asarray(gaps, np.int64), kind="stable")[:4] if gaps[w] >= 400_000]
+    pick = list(dict.fromkeys([int(w) for w in heavy] + wide))
+    for w in range(aln.n_windows):
+        if len(pick) >= n:
+            break
+        if w not in pick:
+            pick.append(w)
+    return sorted(pick[:n])
+
+
+def compare_with_oracle(out, wro, ref, sub, tags: bool = True):
+    """GPU result `out` of a batch (window read offsets `wro`) against the
+    oracle's result `ref` of the windows `sub`: decisions, 2x2 tables, joins,
+    site and read counts and read tags bit for bit, Fisher p at rtol 1e-6."""
+    wro = np.asarray(wro, np.int64)
+    sub = np.asarray(sub, np.int64)
+    bad = []
+    for f in ("decision", "dir_table", "dir_join", "dir_which_way", "win_n_sites", "win_n_reads", "dir_score"):
+        if not np.array_equal(getattr(out, f)[sub], getattr(ref, f)):
+            bad.append(f)
+    hp = np.concatenate([out.read_hp[wro[w]:wro[w + 1]] for w in sub]) if sub.size else np.zeros(0, np.uint8)
+    if tags and not np.array_equal(hp, ref.read_hp):
+        bad.append("read_hp")
+    p, q = out.dir_fisher_p[sub], ref.dir_fisher_p
+    if not np.all(np.abs(p - q) <= 1e-6 * np.abs(q)):
+        bad.append("dir_fisher_p")
+    return bad
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--windows", type=int, default=WORKLOAD["n_windows"],
-                    help="windows per rank (weak scaling, the default); the job's windows with --strong")
+                    help="base windows (distinct); the job is --tiles copies of them")
+    ap.add_argument("--tiles", type=int, default=8,
+                    help="the job: this many copies of the base windows, each copy a contig of its own "
+                         "(8 x 1024 = 8192 windows: a WGS-sized job)")
     ap.add_argument("--coverage", type=int, default=WORKLOAD["coverage"])
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="mix",
                     help="mix: log-uniform 5-500 kb gaps with skipped / site-less windows; fixed50: 50 kb gaps")
-    ap.add_argument("--weak", action="store_true", help="every rank owns --windows windows of its own (default)")
-    ap.add_argument("--strong", action="store_true", help="one job of --windows windows dealt over the ranks")
+    ap.add_argument("--weak", action="store_true",
+                    help="every rank runs a whole job of its own (seeds differ per rank) instead of its LPT "
+                         "share of one job")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--no-legs", action="store_true", help="skip the calls-level and PCIe-inclusive legs")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the calls-level, fixed-gap, projection, PCIe-inclusive and end-to-end legs")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e-windows", type=int, default=64,
                     help="windows of the end-to-end (BAM file -> decisions) leg; 0 skips it")
     ap.add_argument("--e2e-u-scale", type=float, default=1.0,
                     help="genome scale of the configs[3]-shaped -u leg (1.0: 96 Mb, ~1,000 windows); 0 skips it")
     ap.add_argument("--split", type=int, default=2,
-                    help="the windows as this many batches on as many contexts of the GPU, launched together "
-                         "(the headline; the single-batch run is kept for the per-kernel figures); 1: one batch")
+                    help="contexts per GPU (the driver's PF_DEV_CONTEXTS): the rank's batches are dealt over "
+                         "them and launched together every step")
     ap.add_argument("--calls-level", action="store_true",
                     help="time the calls-level boundary (reads + 5mC calls resident, no K0)")
     args = ap.parse_args()
@@ -436,33 +479,46 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     from pomfret_amd import Config, Context, LoadConfig, WindowBatch
+    from pomfret_amd.shard import aln_window_costs, group_copies, lpt_bound, lpt_partition, split_groups
     from pomfret_amd.synth import SynthSpec, make_batch
     from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
 
-    args.weak = not args.strong
     wl = dict(WORKLOADS[args.workload], n_windows=args.windows, coverage=args.coverage)
     cfg = Config.from_coverage(wl["coverage"], given=False)
     lcfg = LoadConfig()
     record_level = not args.calls_level
-    # Weak scaling (default): every rank owns wl["n_windows"] windows of its
-    # own.  --strong: one job of wl["n_windows"] windows, dealt round-robin to
-    # the ranks (the synthetic windows are i.i.d.; the product's sharder,
-    # pomfret_amd.shard, balances real windows by LPT on their bytes).
-    if args.weak:
-        mine = list(range(wl["n_windows"]))
-        seed = 1000 + rank
-    else:
-        mine = list(range(rank, wl["n_windows"], world))
-        seed = 1000
+    n_base, tiles = wl["n_windows"], max(1, args.tiles)
+    n_job = n_base * tiles
+    split = max(1, args.split)
+    seed = 1000 + (rank if args.weak else 0)
+    spec = AlnSpec(n_windows=n_base, coverage=wl["coverage"], gap=wl["gap"], seed=seed, gap_mix=wl["gap_mix"],
+                   skip_frac=wl["skip_frac"], nosite_frac=wl["nosite_frac"])
     t = time.perf_counter()
     if record_level:
         # generated (in worker processes) before anything touches the GPU
-        aln = make_aln_batch(AlnSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"], seed=seed,
-                                     gap_mix=wl["gap_mix"], skip_frac=wl["skip_frac"],
-                                     nosite_frac=wl["nosite_frac"]),
-                             windows=mine, workers=0 if world == 1 else max(1, CPU_SHARE // 2))
-        log(f"[bench] rank {rank}: generated {aln.n_windows} windows, {aln.n_recs} BAM records "
+        aln = make_aln_batch(spec, workers=0 if world == 1 else max(1, CPU_SHARE // 2))
+        log(f"[bench] rank {rank}: generated {aln.n_windows} base windows, {aln.n_recs} BAM records "
             f"({aln.nbytes() / 1e9:.2f} GB) in {time.perf_counter() - t:.1f}s")
+        base_costs = aln_window_costs(aln)
+    else:
+        cbatch = make_batch(SynthSpec(n_windows=n_base, coverage=wl["coverage"], gap=wl["gap"], seed=seed))
+        from pomfret_amd.shard import window_costs
+        base_costs = window_costs(cbatch)
+    gaps = (aln.win_end.astype(np.int64) - aln.win_start.astype(np.int64)) if record_level else None
+
+    # The job: `tiles` copies of the base windows, one contig each.  Strong
+    # scaling (default): the job's windows are dealt over the ranks by the
+    # product's LPT (pomfret_amd.shard, on the windows' SEQ + MM bytes); weak
+    # (--weak): every rank runs a whole job of its own.
+    job_costs = np.tile(base_costs, tiles)
+    if args.weak:
+        share = np.arange(n_job)
+        loads = None
+    else:
+        parts = lpt_partition(job_costs, world)
+        share = parts[rank]
+        loads = [float(job_costs[p].sum()) for p in parts]
+    groups = split_groups(group_copies(share, n_base), split, base_costs)
 
     dist = None
     if world > 1:
@@ -472,110 +528,124 @@ def main():
         torch.cuda.set_device(local_rank)
         tdist.init_process_group(backend="nccl")
         dist = tdist
-    ctx = Context(local_rank)
+    ctxs = [Context(local_rank) for _ in range(split)]
+    ctx = ctxs[0]
+    ident = np.arange(n_base)
+
+    def upload(c, basew):
+        if record_level:
+            if basew.shape[0] == n_base and np.array_equal(basew, ident):
+                return c.upload_aln(cfg, aln, lcfg), aln
+            sub = aln.select(basew)
+            return c.upload_aln(cfg, sub, lcfg), sub
+        return c.upload(cfg, cbatch.select(basew) if not np.array_equal(basew, ident) else cbatch), None
+
+    t = time.perf_counter()
+    dbs, subs = [], []
+    for gi, (_, basew) in enumerate(groups):
+        d, s = upload(ctxs[gi % split], basew)
+        dbs.append(d)
+        subs.append(s if gi == 0 else None)          # the first batch's records feed the byte model
+    log(f"[bench] rank {rank}: {len(share)} of {n_job} job windows as {len(dbs)} batches on {split} contexts "
+        f"(upload: validation, SEQ repack, H2D; no device work): {time.perf_counter() - t:.1f}s")
+    db = dbs[0]
+    aln0 = subs[0]
     if record_level:
-        t = time.perf_counter()
-        db = ctx.upload_aln(cfg, aln, lcfg)
-        log(f"[bench] upload (validation, SEQ repack, H2D; no device work): {time.perf_counter() - t:.1f}s")
         off, cpos, ccat, _, _ = db.debug_calls()
         rr = db.read_recs()
         # the loaded reads as a window batch (the byte model and the calls-level
         # leg): K0's calls, and the spans of the kept records (pos, bam_endpos)
-        wro = np.searchsorted(rr, aln.win_rec_off.astype(np.int64)).astype(np.uint32)
-        rs, re_ = record_spans(aln, rr)
-        batch = WindowBatch(win_start=aln.win_start, win_end=aln.win_end, win_read_off=wro,
+        wro = np.searchsorted(rr, aln0.win_rec_off.astype(np.int64)).astype(np.uint32)
+        rs, re_ = record_spans(aln0, rr)
+        batch = WindowBatch(win_start=aln0.win_start, win_end=aln0.win_end, win_read_off=wro,
                             read_start=rs, read_end=re_,
-                            read_hp=aln.hp[rr], read_call_off=off, call_pos=cpos, call_cat=ccat,
-                            win_cov_sel=aln.win_cov_sel, win_cov_rt=aln.win_cov_rt, win_n_cand=aln.win_n_cand)
+                            read_hp=aln0.hp[rr], read_call_off=off, call_pos=cpos, call_cat=ccat,
+                            win_cov_sel=aln0.win_cov_sel, win_cov_rt=aln0.win_cov_rt, win_n_cand=aln0.win_n_cand)
         del off, cpos, ccat
     else:
-        batch = make_batch(SynthSpec(n_windows=wl["n_windows"], coverage=wl["coverage"], gap=wl["gap"],
-                                     seed=seed)).select(mine)
-        log(f"[bench] rank {rank}: generated {batch.n_windows} windows, {batch.n_reads} reads, "
-            f"{batch.n_calls} calls in {time.perf_counter() - t:.1f}s")
-        db = ctx.upload(cfg, batch)
+        batch = cbatch.select(groups[0][1])
 
-    def timed(dbs, n_windows, n_reads, parts=None):
+    def timed(dbs_, steps=None):
         """W warmup runs, then exactly K timed steps between barrier + sync
-        pairs; returns (max-over-ranks seconds, total reads, per-kernel ms
-        summed over the steps, one step's result).  dbs: one batch, or the
-        batch's windows as several batches (parts: their window indices), each
-        on its own context, launched together every step."""
-        if not isinstance(dbs, (list, tuple)):
-            dbs = [dbs]
-        outs = [[d.run(), d.run()] for d in dbs]
+        pairs; returns (max-over-ranks seconds, reads over all ranks and
+        steps, per-kernel ms summed over the steps, one step's results per
+        batch).  dbs_: the batches, dealt over the contexts; every step
+        launches all of them (a context runs its batches in order on its
+        stream) and the steps are pipelined two deep."""
+        steps = args.steps if steps is None else steps
+        outs = [[d.run(), d.run()] for d in dbs_]
+        n_reads = sum(int(o[0].win_n_reads.sum()) for o in outs)
+        n_win = sum(d.n_windows for d in dbs_)
         for _ in range(args.warmup):
-            for d, o in zip(dbs, outs):
-                d.run(o[0])
-        if dist is not None:
+            for d in dbs_:
+                d.launch()
+            for d, o in zip(dbs_, outs):
+                d.finish(o[0])
+        use_dist = dist is not None and steps == args.steps
+        if use_dist:
             import torch
-            n_max = torch.tensor([n_windows], dtype=torch.int64, device=f"cuda:{local_rank}")
+            n_max = torch.tensor([n_win], dtype=torch.int64, device=f"cuda:{local_rank}")
             dist.all_reduce(n_max, op=dist.ReduceOp.MAX)
             dec_t = torch.full((int(n_max.item()),), -2, dtype=torch.int8, device=f"cuda:{local_rank}")
             gathered = torch.empty(world * dec_t.numel(), dtype=torch.int8, device=f"cuda:{local_rank}")
 
-        def merged(k):
-            if len(dbs) == 1:
-                return outs[0][k % 2].decision
-            dec = np.empty(n_windows, dtype=np.int8)
-            for p, o in zip(parts, outs):
-                dec[p] = o[k % 2].decision
-            return dec
-
         # Steps are pipelined two deep (pf_methphase_launch / _finish): the host
         # epilogue of step k (Fisher tests, decisions, read tags) overlaps the
         # kernels of step k+1; every step runs every kernel (K0 loader, scan +
-        # pack, K12, K2, K3), the D2H copy and the epilogue inside the timed region.
+        # pack, K12, K2, K3), the D2H copy and the epilogue inside the timed
+        # region.  After each step the int8 decisions are all-gathered over
+        # RCCL (the drop-in's only exchange: the writer needs every decision).
         def finish(k):
-            for d, o in zip(dbs, outs):
+            for d, o in zip(dbs_, outs):
                 d.finish(o[k % 2])
-            if dist is not None:
-                dec_t[:n_windows].copy_(torch.from_numpy(merged(k)))
+            if use_dist:
+                dec = np.concatenate([o[k % 2].decision for o in outs])
+                dec_t[:n_win].copy_(torch.from_numpy(dec))
                 dist.all_gather_into_tensor(gathered, dec_t)
 
-        if dist is not None:
+        if use_dist:
             dist.barrier()
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         kern_acc = {}
-        if args.steps:
-            for d in dbs:
+        if steps:
+            for d in dbs_:
                 d.launch()
-        for k in range(args.steps):
-            if k + 1 < args.steps:
-                for d in dbs:
+        for k in range(steps):
+            if k + 1 < steps:
+                for d in dbs_:
                     d.launch()
             finish(k)
-            for d in dbs:
-                for kn, v in d.ctx.kernel_times().items():
+            if len(dbs_) == 1:
+                for kn, v in dbs_[0].ctx.kernel_times().items():
                     kern_acc[kn] = kern_acc.get(kn, 0.0) + v
-        if dist is not None:
+        if use_dist:
             torch.cuda.synchronize()
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        if dist is not None:
+        total = float(n_reads) * steps
+        if use_dist:
             tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
             rt = torch.tensor([n_reads], dtype=torch.float64, device=f"cuda:{local_rank}")
             dist.all_reduce(rt)
-            total = float(rt.item()) * args.steps
-        else:
-            total = float(n_reads) * args.steps
-        out = outs[0][(args.steps - 1) % 2]
-        if len(dbs) > 1:
-            out = {"decision": merged(args.steps - 1)}
-        return elapsed, total, kern_acc, out
+            total = float(rt.item()) * steps
+        return elapsed, total, kern_acc, [o[(steps - 1) % 2] if steps else o[0] for o in outs]
 
-    elapsed, total_reads, kern_acc, out = timed(db, batch.n_windows, batch.n_reads)
-    value = total_reads / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
+    # 1. the first batch alone on one context: the per-kernel figures and the roofline
+    el1, tot1, kern_acc, outs1 = timed([db])
+    out = outs1[0]
+    single = {"value": round(tot1 / el1, 1), "ms_per_step": round(el1 / args.steps * 1e3, 4),
+              "windows": int(db.n_windows), "reads": int(out.win_n_reads.sum()),
+              "what": "the rank's first batch alone on one context (kernels and roofline measured here)"}
+    log(f"[bench] single batch: {json.dumps(single)}")
     stats = db.stats()
     kmean = {k: v / args.steps for k, v in kern_acc.items()}
     ab = algo_bytes(batch, stats, out.win_n_sites, db.heavy_problems())
     if record_level:
-        ab["pf_k0_load"] = k0_bytes(aln, rr, batch.n_calls)
-        ab["pf_k0_pack"] = pack_bytes(aln.n_recs, batch.n_reads, batch.n_calls)
+        ab["pf_k0_load"] = k0_bytes(aln0, rr, batch.n_calls)
+        ab["pf_k0_pack"] = pack_bytes(aln0.n_recs, batch.n_reads, batch.n_calls)
     else:
         kmean.pop("pf_k0_load", None)
         kmean.pop("pf_k0_pack", None)
@@ -589,118 +659,173 @@ def main():
     boundary = "records" if record_level else "calls"
     traffic = pmc_traffic(dom, dict(wl, windows_per_gpu=batch.n_windows), boundary)
 
+    # 2. the headline: the rank's whole share, every batch launched every step
+    elapsed, total_reads, _, job_outs = timed(dbs)
+    value = total_reads / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    job_reads = int(sum(int(o.win_n_reads.sum()) for o in job_outs))
+    # every copy of a base window must get the same decision and tags
+    dec_by_base = {}
+    consistent = True
+    for (_, basew), o in zip(groups, job_outs):
+        for w, dcs in zip(basew.tolist(), o.decision.tolist()):
+            if dec_by_base.setdefault(w, dcs) != dcs:
+                consistent = False
+    if 0 in range(len(groups)) and groups[0][1].shape[0] == n_base:
+        consistent = consistent and all(np.array_equal(o.decision, out.decision) and
+                                        np.array_equal(o.read_hp, out.read_hp)
+                                        for (_, bw), o in zip(groups, job_outs) if np.array_equal(bw, ident))
+    n_probs = 2 * len(share)
+    job = {"windows": int(n_job), "tiles": tiles, "base_windows": n_base, "windows_this_gpu": int(len(share)),
+           "greedy_problems_this_gpu": int(n_probs), "reads_this_gpu": job_reads,
+           "batches_this_gpu": len(dbs), "contexts": split, "copies_consistent": bool(consistent),
+           "deal": "weak: a whole job per rank" if args.weak else "LPT on SEQ + MM bytes (pomfret_amd.shard)"}
+    if loads is not None:
+        job["lpt_loads_max_over_mean"] = round(max(loads) / (sum(loads) / len(loads)), 4)
+        job["lpt_bound_ok"] = bool(max(loads) <= lpt_bound(job_costs, world) + 1e-6)
+    log(f"[bench] job: {json.dumps(job)}")
+
     calls_leg = None
-    if record_level and not args.no_legs:
+    if record_level and not args.no_legs and world == 1:
         # the same reads with K0's calls already resident (the calls-level
         # boundary, pf_batch_upload): K12 + K3 + epilogue only
         dbc = ctx.upload(cfg, batch)
-        el_c, tot_c, acc_c, out_c = timed(dbc, batch.n_windows, batch.n_reads)
+        el_c, tot_c, acc_c, out_c = timed([dbc])
         dbc.free()
         calls_leg = {"value": round(tot_c / el_c, 1), "ms_per_step": round(el_c / args.steps * 1e3, 4),
                      "kernels_ms": {k: round(v / args.steps, 4) for k, v in acc_c.items()
                                     if k not in ("pf_k0_load", "pf_k0_pack")},
-                     "decisions_match": bool(np.array_equal(out_c.decision, out.decision)),
-                     "what": "same reads, calls resident in HBM (no K0): the pre-K0 boundary"}
+                     "decisions_match": bool(np.array_equal(out_c[0].decision, out.decision)),
+                     "what": "the first batch's reads, calls resident in HBM (no K0): the pre-K0 boundary"}
+
+    proj = None
+    crit = None
+    if record_level and not args.no_legs and world == 1 and not args.weak:
+        # Strong scaling projected on this GPU: rank 0's LPT share of the same
+        # job at N GPUs, timed here (the ranks' shares are equal by the deal:
+        # max/mean load below), aggregate = job reads / that step time.
+        proj = {}
+        for n in (2, 4, 8):
+            parts_n = lpt_partition(job_costs, n)
+            g_n = split_groups(group_copies(parts_n[0], n_base), split, base_costs)
+            extra, dbs_n = [], []
+            for gi, (_, basew) in enumerate(g_n):
+                hit = next((d for d, (_, bw) in zip(dbs, groups) if np.array_equal(bw, basew)), None)
+                if hit is not None and hit not in dbs_n and hit.ctx is ctxs[gi % split]:
+                    dbs_n.append(hit)
+                else:
+                    d, _ = upload(ctxs[gi % split], basew)
+                    extra.append(d)
+                    dbs_n.append(d)
+            el_n, tot_n, _, o_n = timed(dbs_n)
+            reads_n = sum(int(o.win_n_reads.sum()) for o in o_n)
+            ld = [float(job_costs[p].sum()) for p in parts_n]
+            agg = reads_n * n * args.steps / el_n          # every rank runs a share like rank 0's
+            proj[str(n)] = {"ms_per_step": round(el_n / args.steps * 1e3, 4), "windows_rank0": int(len(parts_n[0])),
+                            "reads_rank0": int(reads_n), "projected_value": round(agg, 1),
+                            "projected_speedup": round(agg / value, 3),
+                            "lpt_loads_max_over_mean": round(max(ld) / (sum(ld) / n), 4)}
+            for d in extra:
+                d.free()
+            log(f"[bench] strong projection N={n}: {json.dumps(proj[str(n)])}")
+        # The floor of a GPU's step: the heaviest base window alone (its
+        # serial greedy chain; no GPU count takes it below this)
+        wmax = int(np.argmax(out.win_n_reads))
+        # both of its problems in pf_k3_heavy, as in the job's batches (alone in
+        # a batch the window is its own median: not "heavy" by the rule)
+        prev = os.environ.get("PF_K3_HEAVY")
+        os.environ["PF_K3_HEAVY"] = "2"
+        dbw, _ = upload(ctx, np.array([wmax]))
+        if prev is None:
+            os.environ.pop("PF_K3_HEAVY")
+        else:
+            os.environ["PF_K3_HEAVY"] = prev
+        el_w, _, acc_w, o_w = timed([dbw])
+        dbw.free()
+        crit = {"window": wmax, "reads": int(o_w[0].win_n_reads.sum()), "gap_bp": int(gaps[wmax]),
+                "ms_per_step": round(el_w / args.steps * 1e3, 4),
+                "kernels_ms": {k: round(v / args.steps, 4) for k, v in acc_w.items()},
+                "share_of_step_at_8": round(el_w / args.steps * 1e3 / proj["8"]["ms_per_step"], 4)}
+        log(f"[bench] critical window: {json.dumps(crit)}")
 
     fixed_leg = None
     if record_level and not args.no_legs and args.workload == "mix" and world == 1:
-        # round 2's headline workload (50 kb gaps, every window decided), same
-        # steps: the rate the gap mix is compared with
-        wl50 = dict(WORKLOADS["fixed50"], n_windows=wl["n_windows"], coverage=wl["coverage"])
+        # round 2's headline workload (50 kb gaps, every window decided), one
+        # 1024-window batch per context: the rate the gap mix is compared with
+        wl50 = dict(WORKLOADS["fixed50"], n_windows=n_base, coverage=wl["coverage"])
         a50 = make_aln_batch(AlnSpec(n_windows=wl50["n_windows"], coverage=wl50["coverage"], gap=wl50["gap"],
-                                     seed=seed), windows=mine)
+                                     seed=seed))
         db50 = ctx.upload_aln(cfg, a50, lcfg)
-        nr50 = int(db50.run().win_n_reads.sum())
-        el50, tot50, acc50, out50 = timed(db50, a50.n_windows, nr50)
+        el50, tot50, acc50, out50 = timed([db50])
         db50.free()
+        out50 = out50[0]
         fixed_leg = {"value": round(tot50 / el50, 1), "ms_per_step": round(el50 / args.steps * 1e3, 4),
-                     "reads": nr50, "records": int(a50.n_recs),
+                     "reads": int(out50.win_n_reads.sum()), "records": int(a50.n_recs),
                      "kernels_ms": {k: round(v / args.steps, 4) for k, v in acc50.items()},
                      "decisions": {"cis": int((out50.decision == 0).sum()), "trans": int((out50.decision == 1).sum()),
                                    "none": int((out50.decision < 0).sum())},
-                     "what": "round 2's workload: 1024 windows x 50 kb gaps at 60x, records resident"}
+                     "what": "round 2's workload: 1024 windows x 50 kb gaps at 60x, one batch, records resident"}
         del a50
-
-    split_leg = None
-    if record_level and args.split > 1:
-        # the same windows as S batches, each on its own context of this GPU
-        # (own streams, own device buffers), launched together every step: one
-        # batch's K0/K12 fill the CUs the other's K3 tail leaves idle.  Windows
-        # are dealt to the batches heaviest first (record counts), round-robin.
-        nrec_w = np.diff(aln.win_rec_off.astype(np.int64))
-        order = np.argsort(-nrec_w, kind="stable")
-        parts = [sorted(order[s::args.split].tolist()) for s in range(args.split)]
-        sctx = [ctx] + [Context(local_rank) for _ in range(args.split - 1)]
-        sdb = [c.upload_aln(cfg, aln.select(p), lcfg) for c, p in zip(sctx, parts)]
-        el_s, tot_s, _, out_s = timed(sdb, batch.n_windows, batch.n_reads, [np.asarray(p) for p in parts])
-        split_leg = {"value": round(tot_s / el_s, 1), "ms_per_step": round(el_s / args.steps * 1e3, 4),
-                     "batches": args.split,
-                     "decisions_match": bool(np.array_equal(out_s["decision"], out.decision)),
-                     "what": f"same windows as {args.split} batches on {args.split} contexts of this GPU "
-                             "(windows dealt heaviest first), launched together every step"}
-        log(f"[bench] split: {json.dumps(split_leg)}")
-        for d in sdb:
-            d.free()
-        for c in sctx[1:]:
-            c.close()
 
     # PCIe-inclusive rate (never `value`): the one-shot boundary call hands
     # over host buffers -- upload (validation, pinned staging, H2D), run, D2H
     pcie = None
-    if not args.no_legs:
+    if not args.no_legs and record_level:
         t1 = time.perf_counter()
         n_once = 2
         for _ in range(n_once):
-            db2 = ctx.upload_aln(cfg, aln, lcfg) if record_level else ctx.upload(cfg, batch)
+            db2 = ctx.upload_aln(cfg, aln0, lcfg)
             db2.run()
             db2.free()
-        what = ("upload(host BAM-record SoA: validation, SEQ repack, H2D) + run + free per call"
-                if record_level else "upload(host SoA -> HBM) + run + free per call")
         pcie = {"reads_per_s": round(batch.n_reads * n_once / (time.perf_counter() - t1), 1),
                 "ms_per_call": round((time.perf_counter() - t1) / n_once * 1e3, 3),
-                "what": what + ", rank 0"}
+                "what": "upload(host BAM-record SoA: validation, SEQ repack, H2D) + run + free per call, "
+                        "the first batch, rank 0"}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        # the box's CPU share per GPU (OMP_NUM_THREADS there); the reference's
-        # kt_for scales with threads, so the -t 32 figure of BASELINE's target
-        # would be at most twice this
+    if rank == 0 and world == 1 and not args.no_cpu and record_level:
         # BASELINE's target is phrased against the reference's -t 32: 32
         # threads when this host's affinity allows it (the GPU box's share is
-        # 16 cores per GPU: the 16-thread rate is reported beside it)
+        # 16 cores per GPU: the 16-thread rate is reported beside it).  The
+        # sample holds the heaviest and widest windows of the batch, and the
+        # oracle's result on it is compared with the GPU's.
         threads = args.cpu_threads or min(32, len(os.sched_getaffinity(0)))
-        sub = list(range(min(64, batch.n_windows)))
-        if record_level:
-            a_sub = aln.select(sub)
-            n_sub = int(batch.win_read_off[len(sub)])
-            v_cpu, dt, reps = cpu_baseline_aln(cfg, lcfg, a_sub, n_sub, threads, min_cpu_s=30.0)
-            # thread scaling of the same sample (windows are independent; the
-            # reference's -t N is kt_for over contigs)
-            v_half = cpu_baseline_aln(cfg, lcfg, a_sub, n_sub, max(1, threads // 2), min_cpu_s=15.0)[0]
-            what = "per-window loader + worker over the same BAM records, oracle/pf_oracle{_load,}.c"
-        else:
-            b_sub = batch.select(sub)
-            n_sub = b_sub.n_reads
-            v_cpu, dt, reps = cpu_baseline(cfg, b_sub, threads)
-            v_half = cpu_baseline(cfg, b_sub, max(1, threads // 2), min_cpu_s=10.0)[0]
-            what = "oracle/pf_oracle.c"
+        sub = oracle_sample(aln0, gaps, out.win_n_reads)
+        a_sub = aln0.select(sub)
+        n_sub = int(out.win_n_reads[sub].sum())
+        v_cpu, dt, reps, ref = cpu_baseline_aln(cfg, lcfg, a_sub, n_sub, threads, min_cpu_s=30.0)
+        # read tags: the oracle's loader, then its worker (methphase_aln leaves them unset)
+        import oracle
+        ref_t = oracle.methphase(cfg, oracle.load_reads(lcfg, a_sub)[0], n_threads=threads)
+        bad = sorted(set(compare_with_oracle(out, batch.win_read_off, ref, sub, tags=False))
+                     | set(compare_with_oracle(out, batch.win_read_off, ref_t, sub)))
+        v_half = cpu_baseline_aln(cfg, lcfg, a_sub, n_sub, max(1, threads // 2), min_cpu_s=15.0)[0]
         eff = v_cpu / (2 * v_half) if v_half else None
+        heavy_w = sorted({int(p) >> 1 for p in db.heavy_problems()} & set(sub))
         cpu = {"value": round(v_cpu, 1), "unit": "reads/s", "cores": threads, "kind": "port",
-               "sample": f"the first {len(sub)} windows of the workload x{reps} "
-                         f"({n_sub * reps} reads, {dt:.2f}s wall x {threads} threads "
-                         f"= {dt * threads:.0f} CPU-s), {what}; {threads} threads "
+               "sample": f"{len(sub)} windows of the first batch: the 8 with the most reads, the widest gaps "
+                         f"(>= 400 kb), then the first windows ({n_sub} reads, x{reps}: {dt:.2f}s wall x "
+                         f"{threads} threads = {dt * threads:.0f} CPU-s), per-window loader + worker over the "
+                         f"same BAM records, oracle/pf_oracle{{_load,}}.c; {threads} threads "
                          f"({len(os.sched_getaffinity(0))} in this process's affinity; the box's share per GPU "
                          f"is {CPU_SHARE})",
+               "matches": not bad, "mismatched": bad,
+               "compared": "decision, 2x2 tables, join, which_way, score, site/read counts, every read's tag "
+                           "(bit for bit); Fisher p (rtol 1e-6)",
+               "sample_windows": {"n": len(sub), "max_reads": int(out.win_n_reads[sub].max()),
+                                  "max_gap_bp": int(gaps[sub].max()), "heavy_problem_windows": len(heavy_w),
+                                  "windows_ge_400kb": int((gaps[sub] >= 400_000).sum())},
                "thread_scaling": {str(max(1, threads // 2)): round(v_half, 1), str(threads): round(v_cpu, 1),
                                   "efficiency": round(eff, 3) if eff else None},
                "t32_linear_estimate": round(v_cpu * 32 / threads, 1), "t32_measured": threads == 32}
+        log(f"[bench] cpu_baseline: {json.dumps(cpu)}")
 
     e2e = None
-    if rank == 0 and world == 1 and not args.no_legs and args.e2e_windows > 0:
+    if rank == 0 and world == 1 and not args.no_legs and args.e2e_windows > 0 and record_level:
         threads = args.cpu_threads or min(CPU_SHARE, len(os.sched_getaffinity(0)))
         # (round 2's 64-window BAM: the 50 kb workload, so the fetch rates compare across rounds)
         e2e = e2e_leg(ctx, cfg, lcfg, dict(WORKLOADS["fixed50"], coverage=wl["coverage"]),
-                      min(args.e2e_windows, wl["n_windows"]), threads,
+                      min(args.e2e_windows, n_base), threads,
                       os.environ.get("TMPDIR", "/tmp"), cpu=not args.no_cpu)
         log(f"[bench] e2e: {json.dumps(e2e)}")
 
@@ -714,16 +839,8 @@ def main():
             kernels[e2e_u["k4"]["kernel"]] = {"ms": e2e_u["k4"]["ms"], "algo_bytes": e2e_u["k4"]["algo_bytes"],
                                               "GBps": e2e_u["k4"]["GBps"], "leg": "e2e_u (largest contig)"}
 
-    single = None
-    if split_leg is not None:
-        # the headline is the split run (the driver's default: PF_DEV_CONTEXTS
-        # contexts per GPU); the per-kernel figures and the roofline come from
-        # the single-batch run, where each kernel runs alone on the GPU
-        single = {"value": round(value, 1), "ms_per_step": round(ms_per_step, 4),
-                  "what": "the windows as one batch on one context (kernels and roofline measured here)"}
-        value = split_leg["value"]
-        ms_per_step = split_leg["ms_per_step"]
-    par = f"windows dealt over dp{world}" + (" (weak: per-rank batches)" if args.weak else " (strong: one job)")
+    par = (f"job windows dealt over dp{world} by LPT (strong)" if not args.weak
+           else f"dp{world}, a whole job per rank (weak)")
     res = {
         "metric": "aligned reads/sec (methphase kernel)",
         "value": round(value, 1),
@@ -738,46 +855,50 @@ def main():
         "dtype": "u32/f32",
         "data": f"synthetic (seeded {wl['coverage']}x long-read pileups, HG002-like; HG002 not available offline)",
         "config": {
-            "workload": (f"HG002-like {wl['coverage']}x pre-haplotagged: "
-                         f"{wl['n_windows'] * (world if args.weak else 1)} gap windows, "
+            "workload": (f"HG002-like WGS-sized job at {wl['coverage']}x, pre-haplotagged: {n_job} gap windows = "
+                         f"{tiles} contigs x {n_base} distinct windows ("
                          + ("gaps log-uniform 5-500 kb (SURVEY 8d mix), "
-                            f"{wl['skip_frac']:.0%} skipped (left tags lost) + {wl['nosite_frac']:.0%} site-less windows "
-                            if wl["gap_mix"] else f"gaps {wl['gap'] // 1000} kb ")
-                         + f"in the job, {batch.n_windows} on this GPU; "
-                         + ("BAM records resident (every per-batch kernel in the step: K0 loader, scan + pack, "
-                            "K12, K2, K3)" if record_level else "reads + 5mC calls resident (no K0)")),
+                            f"{wl['skip_frac']:.0%} skipped (left tags lost) + {wl['nosite_frac']:.0%} site-less "
+                            "windows" if wl["gap_mix"] else f"gaps {wl['gap'] // 1000} kb")
+                         + f"); {len(share)} windows on this GPU"
+                         + (" (a whole job per rank)" if args.weak else "")
+                         + "; " + ("BAM records resident (every per-batch kernel in the step: K0 loader, scan + "
+                                   "pack, K12, K2, K3)" if record_level else "reads + 5mC calls resident (no K0)")),
             "boundary": boundary,
-            "records_per_gpu": aln.n_recs if record_level else None,
-            "windows_per_gpu": batch.n_windows, "reads_per_gpu": batch.n_reads,
-            "calls_per_gpu": batch.n_calls, "coverage": wl["coverage"],
+            "windows_job": n_job, "windows_per_gpu": int(len(share)),
+            "records_per_gpu": int(sum(int(np.diff(aln.win_rec_off.astype(np.int64))[bw].sum()) for _, bw in groups))
+            if record_level else None,
+            "reads_per_gpu": job_reads, "coverage": wl["coverage"],
             "cov_for_selection": cfg.cov_for_selection, "cov_for_runtime": cfg.cov_for_runtime,
             "n_cand": cfg.n_cand, "k": cfg.k, "k_span": cfg.k_span,
             "parallelism": par,
-            "batches_per_gpu": args.split,
+            "batches_per_gpu": len(dbs), "contexts_per_gpu": split,
         },
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": PEAK_HBM_GBPS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 5) if achieved else None,
-                     "traffic": traffic},
+                     "traffic": traffic, "measured_on": "single_batch"},
         "kernels": kernels,
         "cpu_baseline": cpu,
         "vs_cpu_baseline": round(value / cpu["value"], 2) if cpu else None,
-        # BASELINE's target is phrased against the reference's -t 32: the
-        # 16-thread port scaled linearly to 32 threads (an upper bound for it)
         "vs_cpu_t32_estimate": round(value / cpu["t32_linear_estimate"], 2) if cpu else None,
+        "job": job,
+        "single_batch": single,
+        "strong_projection": proj,
+        "critical_window": crit,
         "pcie_inclusive": pcie,
         "e2e": e2e,
         "e2e_u": e2e_u,
         "calls_level": calls_leg,
         "fixed_gap50": fixed_leg,
-        "split": split_leg,
-        "single_batch": single,
         "decisions": {"cis": int((out.decision == 0).sum()), "trans": int((out.decision == 1).sum()),
-                      "none": int((out.decision < 0).sum())},
+                      "none": int((out.decision < 0).sum()), "of": "the first batch"},
     }
     if rank == 0:
         print(json.dumps(res), flush=True)
-    db.free()
-    ctx.close()
+    for d in dbs:
+        d.free()
+    for c in ctxs:
+        c.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -462,7 +462,8 @@ class DeviceBatch:
         return out[:self.n_windows]
 
     def heavy_problems(self) -> np.ndarray:
-        """Greedy problems (w<<1 | dir) run in pf_k3_heavy (see pf_batch_heavy)."""
+        """Greedy problems (w<<1 | dir) run in pf_k3_heavy: the windows with at
+        least max(600, 1.25 x the median) records (see pf_batch_heavy)."""
         n = lib().pf_batch_heavy(self.handle, None, 0)
         out = np.zeros(max(n, 1), np.uint32)
         if n:

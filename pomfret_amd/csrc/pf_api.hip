@@ -9,6 +9,7 @@
 //             (deterministic: results never depend on arena sizes), then the
 //             host epilogue (Fisher test + join decision, pf_host.c).
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -49,7 +50,9 @@ struct pf_ctx {
     int device;
     hipStream_t stream;
     hipStream_t stream2;      /* the heavy greedy problems, beside the main greedy kernel; the fetch's copies */
-    hipStream_t stream3;      /* the fetch's second inflate stream */
+    hipStream_t stream3;      /* the fetch's second inflate stream (created by the first fetch, so a
+                                 context that only runs resident batches keeps two streams: with two
+                                 contexts per GPU, four streams for the box's four hardware queues) */
     hipEvent_t ev[PF_NKERN + 1];
     float last_ms[PF_NKERN];
     int have_times;
@@ -62,12 +65,29 @@ struct pf_ctx {
     size_t pin_cap = 0;
     void *stage = nullptr;    /* pinned staging of the device fetch's compressed bytes */
     size_t stage_cap = 0;
-    void *dws = nullptr;      /* device workspace of the inflate's first pass (tokens, tables) */
-    size_t dws_cap = 0;
-    uint32_t k3_lds_set = 0;  /* dynamic LDS limits set on the greedy kernels of this device */
-    uint32_t k3_lds_fb_set = 0;
-    uint32_t k3w_lds_set = 0;
 };
+
+// The greedy kernels' dynamic-LDS limits (hipFuncSetAttribute) hold per
+// function and device, for every context of the device: kept per device under
+// a lock and only ever raised, so one context's smaller batch never lowers the
+// limit another context's launch relies on.
+static std::mutex g_lds_mu;
+static uint32_t g_lds_set[64][3];             // [device][greedy, fallback + heavy, one-wave]
+static int raise_lds_limit(int dev, int which, const void *const *fns, int nf, uint32_t need) {
+    if (dev < 0 || dev >= 64) return PF_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_lds_mu);
+    if (need <= g_lds_set[dev][which]) return PF_OK;
+    for (int i = 0; i < nf; i++) {
+        const hipError_t e = hipFuncSetAttribute(fns[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)need);
+        if (e != hipSuccess) {
+            fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u B dynamic LDS): %s\n", need, hipGetErrorString(e));
+            (void)hipGetLastError();
+            return PF_ERR_HIP;
+        }
+    }
+    g_lds_set[dev][which] = need;
+    return PF_OK;
+}
 
 struct pf_dbatch {
     pf_ctx *ctx;
@@ -180,7 +200,7 @@ extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking));
+    c->stream3 = nullptr;
     c->heavy_ms = -1.0f;
     for (int i = 0; i <= PF_NKERN; i++) HIPCHK(hipEventCreate(&c->ev[i]));
     c->have_times = 0;
@@ -212,7 +232,12 @@ extern "C" int pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches) {
 extern "C" int pf_ctx_device(const pf_ctx *c) { return c->device; }
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c) { return c->stream; }
 extern "C" hipStream_t pf_ctx_stream2(const pf_ctx *c) { return c->stream2; }
-extern "C" hipStream_t pf_ctx_stream3(const pf_ctx *c) { return c->stream3; }
+extern "C" hipStream_t pf_ctx_stream3(const pf_ctx *c) {
+    // created on first use by the context's own (fetch) thread
+    pf_ctx *m = const_cast<pf_ctx *>(c);
+    if (!m->stream3 && hipStreamCreateWithFlags(&m->stream3, hipStreamNonBlocking) != hipSuccess) m->stream3 = nullptr;
+    return m->stream3 ? m->stream3 : m->stream;
+}
 
 // the context's pinned staging buffer for the device fetch's compressed bytes
 // (pf_ingest.hip), grown on demand; the caller owns the context's stream
@@ -232,22 +257,6 @@ extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n) {
         c->stage_cap = cap;
     }
     return static_cast<uint8_t *>(c->stage);
-}
-
-// the context's device workspace of at least n bytes (grown on demand, kept:
-// one fetch runs on a context at a time)
-extern "C" uint8_t *pf_ctx_devws(pf_ctx *c, size_t n) {
-    if (c->dws_cap < n) {
-        if (c->dws) { (void)hipStreamSynchronize(c->stream); (void)hipFree(c->dws); }
-        c->dws = nullptr;
-        c->dws_cap = 0;
-        void *p = nullptr;
-        const size_t cap = n + n / 8;
-        if (hipMalloc(&p, cap) != hipSuccess) return nullptr;
-        c->dws = p;
-        c->dws_cap = cap;
-    }
-    return static_cast<uint8_t *>(c->dws);
 }
 
 // release the staging buffer when it grew past `keep` bytes
@@ -270,10 +279,12 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamDestroy(c->stream2);
-    (void)hipStreamDestroy(c->stream3);
+    if (c->stream3) {
+        (void)hipStreamSynchronize(c->stream3);
+        (void)hipStreamDestroy(c->stream3);
+    }
     if (c->pin) (void)hipHostFree(c->pin);
     if (c->stage) (void)hipHostFree(c->stage);
-    if (c->dws) (void)hipFree(c->dws);
     delete c;
 }
 
@@ -964,30 +975,16 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(b->io, 0, PF_IO_HDR, st));
     if (b->W == 0) { HIPCHK(hipEventRecord(b->done[slot], st)); return PF_OK; }
-    // the greedy kernels' dynamic LDS limits, raised per context when a batch needs more
-    if (d.lds_w > 65536u && d.lds_w > c->k3w_lds_set) {
-        if (hipFuncSetAttribute((const void *)pf_k3_wave, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)d.lds_w) == hipSuccess)
-            c->k3w_lds_set = d.lds_w;
-        (void)hipGetLastError();
+    // the greedy kernels' dynamic LDS limits (per device, only raised)
+    if (d.lds_w > 65536u) {
+        const void *f[1] = {(const void *)pf_k3_wave};
+        (void)raise_lds_limit(c->device, 2, f, 1, d.lds_w);
     }
-    if (d.lds_bytes > c->k3_lds_set || d.lds_fb > c->k3_lds_fb_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)pf_k3_greedy,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)d.lds_bytes);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void *)pf_k3_fallback, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)d.lds_fb);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void *)pf_k3_heavy, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)d.lds_fb);
-        if (e != hipSuccess) {
-            fprintf(stderr, "[W::pomfret_amd] hipFuncSetAttribute(%u / %u B dynamic LDS): %s\n", d.lds_bytes,
-                    d.lds_fb, hipGetErrorString(e));
-            (void)hipGetLastError();
-        } else {
-            c->k3_lds_set = d.lds_bytes;
-            c->k3_lds_fb_set = d.lds_fb;
-        }
+    {
+        const void *f1[1] = {(const void *)pf_k3_greedy};
+        const void *f2[2] = {(const void *)pf_k3_fallback, (const void *)pf_k3_heavy};
+        if (raise_lds_limit(c->device, 0, f1, 1, d.lds_bytes) || raise_lds_limit(c->device, 1, f2, 2, d.lds_fb))
+            return PF_ERR_HIP;
     }
     HIPCHK(hipEventRecord(b->ev[slot][0], st));
     if (b->has_aln) {

@@ -681,7 +681,3 @@ __global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(
     inflate_blocks<false>(in, blk, nblk, arena, status);
 }
 
-__global__ __launch_bounds__(64 * INF_WAVES) __attribute__((amdgpu_waves_per_eu(INF_WPE, INF_WPE))) void pf_inflate_fallback(
-    const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena, uint32_t *status) {
-    inflate_blocks<true>(in, blk, nblk, arena, status);
-}

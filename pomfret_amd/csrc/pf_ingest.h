@@ -23,22 +23,10 @@ typedef struct pf_bgzf_blk {
 #define PF_INF_ESIZE 5u        // output differs from ISIZE
 #define PF_INF_EINPUT 6u       // stream runs past the payload
 #define PF_INF_ECRC 7u         // CRC32 mismatch
-#define PF_INF_FALLBACK 100u   // (internal) left by pf_inflate_tok for pf_inflate_fallback
+#define PF_INF_FALLBACK 100u   // (internal) a block left for inflate_blocks<true> (tools/ubench's two-pass decoder)
 
 __global__ void pf_inflate(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena,
                            uint32_t *status);
-// the same on the blocks whose status is PF_INF_FALLBACK only
-__global__ void pf_inflate_fallback(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint8_t *arena,
-                                    uint32_t *status);
-// the two-pass inflate (pf_inflate_simt.hip): Huffman decode one lane per
-// block into tokens, then LZ77 copies + CRC + store one workgroup per block.
-// Token area of block i of a launch: u32 index ((out_off - out_base) & ~3) + 4 i.
-#define PF_SI_META 20u                  // u32 per block of the meta array
-#define PF_SI_SCR 1152u                 // bytes per block of the first pass's scratch
-__global__ void pf_inflate_tok(const uint8_t *in, const pf_bgzf_blk *blk, uint32_t nblk, uint64_t out_base,
-                               uint32_t *tok, uint32_t *meta, uint8_t *scratch, uint32_t *status);
-__global__ void pf_inflate_lz(const pf_bgzf_blk *blk, uint32_t nblk, uint64_t out_base, const uint32_t *tok,
-                              const uint32_t *meta, uint8_t *arena, uint32_t *status);
 
 // ---- device fetch (pf_ingest.hip): runs of blocks, windows, chunks, records
 typedef struct pf_run_dev {

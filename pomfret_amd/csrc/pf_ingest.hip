@@ -61,48 +61,19 @@ int64_t pf_bgzf_scan(const uint8_t *comp, uint64_t len, uint64_t out_base, uint3
     return n;
 }
 
-extern "C" uint8_t *pf_ctx_devws(pf_ctx *c, size_t n);
-
-// Inflate blocks on the device: d_in / d_blk / d_arena / d_status resident
-// (h_blk: the host copy of the block table); status words set per block.
-// PF_INFLATE_IMPL=simt: the two-pass decoder (pf_inflate_simt.hip) in
-// launches of up to 32768 blocks, its workspace (tokens: 4 B per output byte
-// at most, tables) the context's; default: the one-wave-per-block pf_inflate.
+// Inflate blocks on the device: d_in / d_blk / d_arena / d_status resident;
+// status words set per block.  One wavefront per block (pf_inflate).  A
+// two-pass decoder (one lane per block for the Huffman decode, then the LZ77
+// copies) was built and measured slower; it lives in tools/ubench.
 int pf_inflate_launch(pf_ctx *ctx, hipStream_t st, const uint8_t *d_in, const pf_bgzf_blk *d_blk,
                       const pf_bgzf_blk *h_blk, uint32_t nblk, uint8_t *d_arena, uint32_t *d_status, hipEvent_t e0,
                       hipEvent_t e1) {
+    (void)ctx;
+    (void)h_blk;
     if (e0 && hipEventRecord(e0, st) != hipSuccess) return PF_ERR_HIP;
     if (!nblk) return e1 && hipEventRecord(e1, st) != hipSuccess ? PF_ERR_HIP : PF_OK;   // (the pair stays timeable)
-    static const int wave = [] {
-        const char *e = getenv("PF_INFLATE_IMPL");
-        return !(e && !strcmp(e, "simt"));
-    }();
-    if (wave) {
-        hipLaunchKernelGGL(pf_inflate, dim3((nblk + 3) / 4), dim3(256), 0, st, d_in, d_blk, nblk, d_arena, d_status);
-        if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
-    } else {
-        constexpr uint32_t BATCH = 32768;
-        for (uint32_t f = 0; f < nblk; f += BATCH) {
-            const uint32_t n = nblk - f < BATCH ? nblk - f : BATCH;
-            const uint64_t ob = h_blk[f].out_off, oe = h_blk[f + n - 1].out_off + h_blk[f + n - 1].isize;
-            const uint64_t tok_b = 4ull * ((oe - ob) + 4ull * n + 16) + 256;
-            const uint64_t meta_b = ((4ull * PF_SI_META * n) + 255) & ~255ull;
-            uint8_t *ws = pf_ctx_devws(ctx, tok_b + meta_b + (uint64_t)PF_SI_SCR * n);
-            if (!ws) return PF_ERR_NOMEM;
-            uint32_t *tok = reinterpret_cast<uint32_t *>(ws);
-            uint32_t *meta = reinterpret_cast<uint32_t *>(ws + tok_b);
-            uint8_t *scr = ws + tok_b + meta_b;
-            hipLaunchKernelGGL(pf_inflate_tok, dim3((n + 63) / 64), dim3(64), 0, st, d_in, d_blk + f, n, ob, tok, meta,
-                               scr, d_status + f);
-            if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
-            hipLaunchKernelGGL(pf_inflate_lz, dim3(n), dim3(256), 0, st, d_blk + f, n, ob, (const uint32_t *)tok,
-                               (const uint32_t *)meta, d_arena, d_status + f);
-            if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
-            hipLaunchKernelGGL(pf_inflate_fallback, dim3((n + 3) / 4), dim3(256), 0, st, d_in, d_blk + f, n, d_arena,
-                               d_status + f);
-            if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
-        }
-    }
+    hipLaunchKernelGGL(pf_inflate, dim3((nblk + 3) / 4), dim3(256), 0, st, d_in, d_blk, nblk, d_arena, d_status);
+    if (hipGetLastError() != hipSuccess) return PF_ERR_HIP;
     if (e1 && hipEventRecord(e1, st) != hipSuccess) return PF_ERR_HIP;
     return PF_OK;
 }

@@ -18,6 +18,9 @@ import numpy as np
 
 from .abi import WindowBatch
 
+__all__ = ["window_costs", "lpt_partition", "lpt_bound", "shard", "aln_window_costs", "shard_aln",
+           "group_copies", "split_groups", "gather_decisions"]
+
 
 def window_costs(batch: WindowBatch) -> np.ndarray:
     """LPT cost of each window, reads x calls: the greedy
@@ -62,6 +65,51 @@ def shard_aln(aln, rank: int, world: int):
     parts = lpt_partition(aln_window_costs(aln), world)
     idx = parts[rank]
     return idx, aln.select(idx)
+
+
+def lpt_bound(costs: np.ndarray, n_parts: int) -> float:
+    """Graham's bound on the largest LPT load: (4/3 - 1/(3m)) x OPT, with
+    OPT >= max(mean load, largest window)."""
+    c = np.asarray(costs, np.float64)
+    opt_lo = max(float(c.sum()) / n_parts, float(c.max()) if c.size else 0.0)
+    return (4.0 / 3.0 - 1.0 / (3.0 * n_parts)) * opt_lo
+
+
+def group_copies(share: np.ndarray, n_base: int):
+    """Device batches of a rank's share of a job made of copies (one per
+    contig) of `n_base` base windows: job window j is copy j // n_base of base
+    window j % n_base.  Batch k takes the k-th copy of every base window the
+    rank holds, in base-window order, so a rank that owns whole copies uploads
+    each as the base batch itself.  Returns [(job windows, base windows)]."""
+    share = np.sort(np.asarray(share, np.int64))
+    base = share % n_base
+    occ = np.zeros(share.shape[0], np.int64)
+    seen = {}
+    for i, b in enumerate(base.tolist()):
+        occ[i] = seen.get(b, 0)
+        seen[b] = occ[i] + 1
+    groups = []
+    for k in range(int(occ.max()) + 1 if share.size else 0):
+        m = np.flatnonzero(occ == k)
+        m = m[np.argsort(base[m], kind="stable")]
+        groups.append((share[m], base[m]))
+    return groups
+
+
+def split_groups(groups, n_min: int, base_costs: np.ndarray):
+    """At least n_min batches (one per context of the GPU): each group is
+    dealt heaviest first, round-robin, into ceil(n_min / len(groups)) parts."""
+    if not groups or len(groups) >= n_min:
+        return groups
+    k = -(-n_min // len(groups))
+    out = []
+    for jobw, basew in groups:
+        order = np.argsort(-np.asarray(base_costs, np.float64)[basew], kind="stable")
+        for s in range(k):
+            sel = np.sort(order[s::k])
+            if sel.size:
+                out.append((jobw[sel], basew[sel]))
+    return out
 
 
 def gather_decisions(n_windows: int, idx: np.ndarray, decision: np.ndarray, group=None):

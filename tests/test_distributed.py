@@ -206,3 +206,79 @@ def test_two_rank_multicontig(tmp_path, oracle_lib, untagged):
     assert open(out + ".mp.tsv").read() == ref["tsv"]
     assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
     assert (ref["decision"] >= 0).sum() >= 3
+
+
+def _job_deal(rank, world, n_base=48, tiles=8):
+    """bench.py's strong-scaling deal of a WGS-shaped job (tiles copies of the
+    base windows) for one rank: the share and its device batches."""
+    from pomfret_amd.shard import aln_window_costs, group_copies, lpt_partition, split_groups
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    aln = make_aln_batch(AlnSpec(n_windows=n_base, coverage=8, seed=1000, gap_mix=True, len_scale=0.15,
+                                 skip_frac=0.1, nosite_frac=0.05), workers=1)
+    base_costs = aln_window_costs(aln)
+    job_costs = np.tile(base_costs, tiles)
+    parts = lpt_partition(job_costs, world)
+    groups = split_groups(group_copies(parts[rank], n_base), 2, base_costs)
+    return job_costs, parts, groups
+
+
+def _deal_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, parts, groups = _job_deal(rank, world)
+        mine = [(j.tolist(), b.tolist()) for j, b in groups]
+        got = [None] * world
+        dist.all_gather_object(got, mine)
+        import json
+        with open(os.path.join(out_dir, f"deal{rank}.json"), "w") as f:
+            json.dump(dict(groups=got, share=parts[rank].tolist()), f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_strong_scaling_deal_two_ranks(tmp_path):
+    """bench.py --gpus N (strong, the default): the job's windows dealt by the
+    product's LPT on SEQ + MM bytes.  Over 2 gloo ranks every job window is
+    run exactly once, each rank's device batches cover its share exactly, and
+    the loads are within Graham's LPT bound on the gap mix."""
+    import json
+    from pomfret_amd.shard import lpt_bound
+    world, n_base, tiles = 2, 48, 8
+    mp.spawn(_deal_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    job_costs, parts, _ = _job_deal(0, world)
+    res = [json.load(open(tmp_path / f"deal{r}.json")) for r in range(world)]
+    assert res[0]["groups"] == res[1]["groups"]            # every rank sees the same deal
+    all_w = []
+    for r in range(world):
+        batches = res[0]["groups"][r]
+        jw = sorted(j for g in batches for j in g[0])
+        assert jw == sorted(res[r]["share"])
+        for j, b in batches:
+            assert [x % n_base for x in j] == b           # job window -> its base window
+            assert len(set(b)) == len(b)                  # one copy of a base window per batch
+        all_w += jw
+    assert sorted(all_w) == list(range(n_base * tiles))
+    loads = [job_costs[p].sum() for p in parts]
+    assert max(loads) <= lpt_bound(job_costs, world) + 1e-6
+    assert max(loads) / (sum(loads) / world) < 1.01      # identical copies: near-perfect balance
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_job_batches_by_copy(world):
+    """The batches of a rank's share: at N=1 the 8 copies are 8 whole base
+    batches (uploaded without a re-pack); at N=8 the one copy a rank holds is
+    split heaviest first over the two contexts."""
+    from pomfret_amd.shard import group_copies, lpt_partition, split_groups
+    n_base, tiles = 40, 8
+    costs = np.random.default_rng(3).lognormal(0, 1, n_base)
+    parts = lpt_partition(np.tile(costs, tiles), world)
+    for p in parts:
+        g = split_groups(group_copies(p, n_base), 2, costs)
+        assert sorted(np.concatenate([j for j, _ in g]).tolist()) == p.tolist()
+        if world <= 4:
+            assert len(g) == tiles // world
+            assert all(np.array_equal(b, np.arange(n_base)) for _, b in g)
+        else:
+            assert len(g) == 2 and sum(len(b) for _, b in g) == n_base

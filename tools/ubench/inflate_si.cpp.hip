@@ -1,6 +1,6 @@
 // A/B timing of the BGZF inflate kernels on the same blocks (a BAM file,
 // replicated): pf_inflate (one wave per block, pf_inflate.hip) against the
-// two-pass decoder (pf_inflate_simt.hip) at two table sizes; per variant the
+// two-pass decoder (inflate_simt.hip, measured slower and kept out of the product) at two table sizes; per variant the
 // first pass (Huffman -> tokens) and the second (LZ77 + CRC + store) timed
 // with events; outputs compared with the wave kernel's.
 // Usage: inflate_si <bgzf file> [copies]
@@ -14,6 +14,11 @@
 
 namespace w {
 #include "../../pomfret_amd/csrc/pf_inflate.hip"
+// the blocks the two-pass decoder left (PF_INF_FALLBACK), one wave each
+__global__ __launch_bounds__(64 * INF_WAVES) void pf_inflate_fallback(const uint8_t *in, const pf_bgzf_blk *blk,
+                                                                      uint32_t nblk, uint8_t *arena, uint32_t *status) {
+    inflate_blocks<true>(in, blk, nblk, arena, status);
+}
 }
 namespace vp {
 #define SI_PROF 1
@@ -23,7 +28,7 @@ namespace vp {
 #define SI_DCAP 32u
 #define SI_RS 8u
 #define SI_RP 4u
-#include "../../pomfret_amd/csrc/pf_inflate_simt.hip"
+#include "inflate_simt.hip"
 #undef SI_LR
 #undef SI_DR
 #undef SI_LCAP
@@ -40,7 +45,7 @@ namespace v1 {
 #define SI_DCAP 32u
 #define SI_RS 16u
 #define SI_RP 8u
-#include "../../pomfret_amd/csrc/pf_inflate_simt.hip"
+#include "inflate_simt.hip"
 #undef SI_LR
 #undef SI_DR
 #undef SI_LCAP
@@ -55,7 +60,7 @@ namespace v2 {
 #define SI_DCAP 32u
 #define SI_RS 16u
 #define SI_RP 8u
-#include "../../pomfret_amd/csrc/pf_inflate_simt.hip"
+#include "inflate_simt.hip"
 #undef SI_LR
 #undef SI_DR
 #undef SI_LCAP
@@ -70,7 +75,7 @@ namespace v3 {
 #define SI_DCAP 32u
 #define SI_RS 8u
 #define SI_RP 4u
-#include "../../pomfret_amd/csrc/pf_inflate_simt.hip"
+#include "inflate_simt.hip"
 #undef SI_LR
 #undef SI_DR
 #undef SI_LCAP

@@ -1,4 +1,5 @@
-// pf_inflate_simt.hip -- BGZF inflate in two passes: one LANE per block for
+// inflate_simt.hip -- (experiment, not in the product build: measured slower
+// than pf_inflate) BGZF inflate in two passes: one LANE per block for
 // the Huffman decode, one workgroup per block for the LZ77 copies.
 //
 // pf_inflate (pf_inflate.hip) runs one wavefront per block with the whole
@@ -44,6 +45,12 @@
 // first pass is skipped by the second.  A block whose literal/length tree has
 // more long codes than the LDS list holds (SI_LCAP; never seen on BAM data)
 // is flagged PF_INF_FALLBACK and decoded by pf_inflate_fallback instead.
+// the two-pass inflate's launch layout (was pf_ingest.h): token area of block
+// i of a launch: u32 index ((out_off - out_base) & ~3) + 4 i
+#ifndef PF_SI_META
+#define PF_SI_META 20u                  // u32 per block of the meta array
+#define PF_SI_SCR 1152u                 // bytes per block of the first pass's scratch
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "pf_ingest.h"
