@@ -183,7 +183,7 @@ def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 2
     return n_reads * reps / dt, dt, reps, ref
 
 
-def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu: bool = True):
+def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu: bool = True, cpu_threads: int = 0):
     """End to end from files (never `value`): the first n_windows windows of
     the workload written as a BAM + BAI (QUAL strings included, zlib level 6,
     tests/_bamio.py's writer), then per path the wall time from the BAM file to
@@ -194,8 +194,9 @@ def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu:
       host_fetch:   the host reader inflates and decodes (pf_bam_fetch_windows,
                     `threads` threads), upload_aln, K0..K3;
       cpu_port:     the host reader + the oracle's record-level path on
-                    `threads` threads (the reference's structure: htslib decode
-                    + the kt_for worker)."""
+                    `cpu_threads` threads (the reference's structure: htslib
+                    decode + the kt_for worker)."""
+    cpu_threads = cpu_threads or threads
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import _bamio
     from pomfret_amd.bam import BamFile
@@ -244,13 +245,16 @@ def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu:
                                  "fetch_ms": round((t1 - t0) * 1e3, 1), "upload_run_ms": round((t2 - t1) * 1e3, 1)}
             res["decisions_match"] = bool(np.array_equal(out.decision, dec_dev))
             # the pass over the whole BAM that runs without -c pay first
-            # (estimate_read_coverage_dirtyfast): device fetch vs the serial host pass
+            # (estimate_read_coverage_dirtyfast): device fetch vs the host pass
+            # with cpu_threads BGZF inflate threads (the reference's -t N: bgzf_mt)
             c0 = time.perf_counter()
             cov_d = b.estimate_coverage_device(ctx)
             c1 = time.perf_counter()
-            cov_h = b.estimate_coverage()
+            with BamFile(path, threads=cpu_threads) as bh:
+                cov_h = bh.estimate_coverage()
             c2 = time.perf_counter()
             res["coverage_estimate"] = {"device_ms": round((c1 - c0) * 1e3, 1), "host_ms": round((c2 - c1) * 1e3, 1),
+                                        "host_inflate_threads": cpu_threads,
                                         "match": cov_d == cov_h, "cov": int(cov_d[0])}
             # the whole driver, file to .mp.vcf/.mp.gtf (pf_methphase_main: VCF
             # gaps, plan, jobs, first-wins tables, writers), device fetch vs
@@ -279,13 +283,16 @@ def e2e_leg(ctx, cfg, lcfg, wl, n_windows: int, threads: int, workdir: str, cpu:
             os.unlink(vcf)
             if cpu:
                 import oracle
+                t5 = time.perf_counter()
+                got, _, _ = b.fetch_windows("chrS", ws, we, threads=cpu_threads)
                 t3 = time.perf_counter()
-                ref = oracle.methphase_aln(cfg, lcfg, got, n_threads=threads)
+                ref = oracle.methphase_aln(cfg, lcfg, got, n_threads=cpu_threads)
                 t4 = time.perf_counter()
-                res["cpu_port"] = {"reads_per_s": round(reads / ((t1 - t0) + (t4 - t3)), 1),
-                                   "ms": round(((t1 - t0) + (t4 - t3)) * 1e3, 1),
-                                   "what": f"host fetch ({threads} threads) + oracle record-level worker "
-                                           f"({threads} threads)"}
+                res["cpu_port"] = {"reads_per_s": round(reads / (t4 - t5), 1),
+                                   "ms": round((t4 - t5) * 1e3, 1), "threads": cpu_threads,
+                                   "fetch_ms": round((t3 - t5) * 1e3, 1), "worker_ms": round((t4 - t3) * 1e3, 1),
+                                   "what": f"host fetch ({cpu_threads} threads) + oracle record-level worker "
+                                           f"({cpu_threads} threads)"}
                 res["decisions_match"] = res["decisions_match"] and bool(np.array_equal(ref.decision, dec_dev))
     finally:
         os.unlink(path)
@@ -307,7 +314,7 @@ def k4_bytes(known, reads) -> int:
     return int(4 * cig.shape[0] + md.shape[0] + reads.n_reads + n_x + ins + 16 * v_span + reads.n_reads)
 
 
-def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bool = True):
+def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bool = True, cpu_threads: int = 0):
     """BASELINE configs[3]'s shape from files (never `value`): `pomfret
     methphase -u` without -c on a whole-genome-shaped 60x BAM (tests/_genome:
     4 contigs, reads uniform over each contig, ~1,000 phase-block gaps of
@@ -318,15 +325,17 @@ def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bo
                 init, the device coverage pass, the device -u pre-pass over
                 every primary read, the window jobs, the writers);
       driver:   the same driver in this process on a warm context;
-      cpu_port: the product's planner / writers with the host reader, the
-                serial host coverage pass and the oracle computing every job
-                (tests/_oracle_pipeline.methphase_files_port, `threads`
-                threads);
+      cpu_port: the product's planner / writers with the host reader (its
+                coverage pass and -u contig reads with BGZF inflate threads,
+                the reference's -t N bgzf_mt) and the oracle computing every
+                job (tests/_oracle_pipeline.methphase_files_port,
+                `cpu_threads` threads);
     outputs compared byte for byte.  Also the K4 kernel on the largest
     contig's reads (HIP events, SURVEY 8d's -u bytes)."""
     import subprocess
     sys.path.insert(0, os.path.join(HERE, "tests"))
     import _genome
+    cpu_threads = cpu_threads or threads
     from pomfret_amd.bam import BamFile, vcf_known_vars
     from pomfret_amd.pipeline import methphase_files
     spec = _genome.GenomeSpec()
@@ -394,11 +403,13 @@ def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bo
         if cpu:
             from _oracle_pipeline import methphase_files_port
             rp, ph = methphase_files_port(g["bam"], g["vcf"], prefix + ".port", None, lcfg, untagged=True,
-                                          threads=threads)
+                                          threads=cpu_threads)
             outs["cpu_port"] = take(prefix + ".port")
             res["cpu_port"] = {"s": round(ph["total_s"], 2), "records_per_s": round(res["records"] / ph["total_s"], 1),
                                "phases_s": {k: round(v, 2) for k, v in ph.items() if k != "total_s"},
-                               "what": f"host reader + serial host coverage pass + oracle jobs, {threads} threads"}
+                               "threads": cpu_threads,
+                               "what": f"host reader (coverage pass and -u contig reads with BGZF inflate threads) + "
+                                       f"oracle jobs, {cpu_threads} threads (-t {cpu_threads})"}
             res["vs_cpu_port"] = round(ph["total_s"] / (t1 - t0), 2)
         res["outputs_identical"] = all(o == outs["cli"] for o in outs.values())
         res["compared"] = sorted(outs)
@@ -826,14 +837,15 @@ def main():
         # (round 2's 64-window BAM: the 50 kb workload, so the fetch rates compare across rounds)
         e2e = e2e_leg(ctx, cfg, lcfg, dict(WORKLOADS["fixed50"], coverage=wl["coverage"]),
                       min(args.e2e_windows, n_base), threads,
-                      os.environ.get("TMPDIR", "/tmp"), cpu=not args.no_cpu)
+                      os.environ.get("TMPDIR", "/tmp"), cpu=not args.no_cpu,
+                      cpu_threads=args.cpu_threads or min(32, len(os.sched_getaffinity(0))))
         log(f"[bench] e2e: {json.dumps(e2e)}")
 
     e2e_u = None
     if rank == 0 and world == 1 and not args.no_legs and args.e2e_u_scale > 0:
         threads = args.cpu_threads or min(CPU_SHARE, len(os.sched_getaffinity(0)))
         e2e_u = e2e_u_leg(ctx, lcfg, threads, os.environ.get("TMPDIR", "/tmp"), scale=args.e2e_u_scale,
-                          cpu=not args.no_cpu)
+                          cpu=not args.no_cpu, cpu_threads=args.cpu_threads or min(32, len(os.sched_getaffinity(0))))
         log(f"[bench] e2e_u: {json.dumps(e2e_u)}")
         if e2e_u.get("k4"):
             kernels[e2e_u["k4"]["kernel"]] = {"ms": e2e_u["k4"]["ms"], "algo_bytes": e2e_u["k4"]["algo_bytes"],

@@ -516,6 +516,11 @@ void pf_bam_reads_free(pf_bam_reads_t *reads);
  * (estimate_read_coverage_dirtyfast, 951-1040): covs[tid] for
  * tid < pf_bam_n_targets (n >= that).  A full sequential pass over the BAM. */
 int  pf_bam_estimate_coverage(pf_bam_t *bam, int32_t *covs, int32_t n);
+/* BGZF inflate threads of the handle's sequential passes (the coverage
+ * estimate and pf_bam_fetch_contig_reads): the reference's -t N, which sets
+ * pomfret_n_bam_threads for bgzf_mt on every BAM it opens (cli.c:261-264,
+ * blockjoin.c:576-578).  n <= 1: single-threaded (the default). */
+void pf_bam_set_threads(pf_bam_t *bam, int n);
 /* The same estimate with the BAM's records inflated, chained and decoded on
  * ctx's device (the device fetch, pieces of <= piece_bytes compressed bytes
  * per call; 0 = 4 GiB), contig by contig through the index; identical covs

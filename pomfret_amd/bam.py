@@ -91,6 +91,8 @@ def _bind():
                                        C.c_int, C.POINTER(C.POINTER(PfRescueMap))]
     L.pf_rescue_map_free.argtypes = [C.POINTER(PfRescueMap)]
     L.pf_bam_estimate_coverage.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    L.pf_bam_set_threads.argtypes = [C.c_void_p, C.c_int]
+    L.pf_bam_set_threads.restype = None
     L.pf_bam_estimate_coverage_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64]
     L.pf_bam_n_no_coor.argtypes = [C.c_void_p]
     L.pf_bam_n_no_coor.restype = C.c_int64
@@ -116,7 +118,10 @@ def _arr(ptr, n, dt) -> np.ndarray:
 class BamFile:
     """An opened BAM + BAI (pf_bam_open).  bam=None opens the index alone."""
 
-    def __init__(self, bam: Optional[str], bai: Optional[str] = None):
+    def __init__(self, bam: Optional[str], bai: Optional[str] = None, threads: int = 1):
+        """threads: BGZF inflate threads of the sequential passes
+        (estimate_coverage, fetch_contig_reads; pf_bam_set_threads) -- the
+        reference's -t N for bgzf_mt (blockjoin.c:576-578)."""
         L = _bind()
         h = C.c_void_p()
         rc = L.pf_bam_open(bam.encode() if bam else None, bai.encode() if bai else None, C.byref(h))
@@ -125,6 +130,8 @@ class BamFile:
         _check(rc, "pf_bam_open")
         self.handle = h
         self.path = bam
+        if threads > 1:
+            L.pf_bam_set_threads(h, int(threads))
 
     def close(self):
         if self.handle:

@@ -36,7 +36,9 @@
 
 /* ------------------------------------------------------------------ */
 /* BGZF */
+struct bgzf_mt;
 typedef struct {
+    struct bgzf_mt *mt;      /* multi-threaded read-ahead (bgzf_mt), or NULL */
     FILE *f;
     uint8_t cbuf[65536 + 64];
     uint8_t ubuf[65536];
@@ -52,19 +54,19 @@ static uint32_t rd16(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1]
 static uint32_t rd32(const uint8_t *p) { return rd16(p) | (rd16(p + 2) << 16); }
 static uint64_t rd64(const uint8_t *p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
 
-/* load the block at compressed address addr; 0 ok, 1 clean EOF, <0 error */
-static int bgzf_load(bgzf_t *z, uint64_t addr) {
+/* read the block at compressed address addr into cbuf: its size, or 0 at a
+ * clean EOF, <0 on error */
+static int bgzf_read_raw(bgzf_t *z, uint64_t addr, uint8_t *h, uint32_t *xlen_out) {
     if (addr != z->fpos) {                    /* sequential blocks keep the stdio buffer */
         if (fseeko(z->f, (off_t)addr, SEEK_SET) != 0) return -1;
         z->fpos = addr;
     }
-    uint8_t *h = z->cbuf;
     size_t got = fread(h, 1, 18, z->f);
     z->fpos += got;
-    if (got == 0) { z->caddr = addr; z->next = addr; z->ulen = z->upos = 0; z->eof = 1; return 1; }
+    if (got == 0) return 0;
     if (got < 12 || h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return -2;
     const uint32_t xlen = rd16(h + 10);
-    if (xlen < 6 || 12 + xlen > sizeof z->cbuf) return -2;
+    if (xlen < 6 || 12 + xlen > 65536 + 64) return -2;
     if (got < 12 + (size_t)xlen) {
         const size_t k = fread(h + got, 1, 12 + xlen - got, z->f);
         z->fpos += k;
@@ -84,23 +86,214 @@ static int bgzf_load(bgzf_t *z, uint64_t addr) {
         z->fpos += k;
         if (k != bsize - got) return -2;
     }
+    *xlen_out = xlen;
+    return (int)bsize;
+}
+
+/* inflate + CRC check of one raw block (h, bsize): output bytes or -2 */
+static int bgzf_inflate_raw(const uint8_t *h, uint32_t bsize, uint32_t xlen, uint8_t *u) {
     const uint32_t isize = rd32(h + bsize - 4), crc = rd32(h + bsize - 8);
     if (isize > 65536) return -2;
     z_stream zs;
     memset(&zs, 0, sizeof zs);
     if (inflateInit2(&zs, -15) != Z_OK) return -3;
-    zs.next_in = h + 12 + xlen;
+    zs.next_in = (uint8_t *)h + 12 + xlen;
     zs.avail_in = bsize - 12 - xlen - 8;
-    zs.next_out = z->ubuf;
-    zs.avail_out = sizeof z->ubuf;
+    zs.next_out = u;
+    zs.avail_out = 65536;
     const int rc = inflate(&zs, Z_FINISH);
     const uint32_t out = (uint32_t)zs.total_out;
     inflateEnd(&zs);
     if (rc != Z_STREAM_END || out != isize) return -2;
-    if ((uint32_t)crc32(0L, z->ubuf, out) != crc) return -2;
+    if ((uint32_t)crc32(0L, u, out) != crc) return -2;
+    return (int)out;
+}
+
+/* Multi-threaded read-ahead (htslib's bgzf_mt, which the reference turns on
+ * with -t N for its whole-file passes, blockjoin.c:576-578): the reading
+ * thread reads the compressed blocks that follow the one it consumes into a
+ * ring, and n worker threads inflate them; blocks are handed out in file
+ * order.  A load at an address other than the ring's next block (a seek)
+ * drains the ring and restarts the read-ahead there. */
+typedef struct {
+    uint64_t caddr, next;
+    uint32_t bsize, xlen;
+    int ulen;                 /* inflated bytes, or < 0 on error */
+    int state;                /* 0 free, 1 read, 2 inflating, 3 done */
+    uint8_t c[65536 + 64];
+    uint8_t u[65536];
+} mt_blk_t;
+
+typedef struct bgzf_mt {
+    int nth, cap;
+    pthread_t *th;
+    pthread_mutex_t mu;
+    pthread_cond_t cv_job, cv_done;
+    mt_blk_t *ring;
+    uint64_t head, tail, job;     /* consume / read / next-to-inflate indices */
+    uint64_t raddr;               /* next compressed address to read */
+    int reof, rerr, stop;
+} bgzf_mt_t;
+
+static void *mt_worker(void *arg) {
+    bgzf_mt_t *M = (bgzf_mt_t *)arg;
+    pthread_mutex_lock(&M->mu);
+    for (;;) {
+        while (!M->stop && M->job == M->tail) pthread_cond_wait(&M->cv_job, &M->mu);
+        if (M->stop) break;
+        mt_blk_t *B = &M->ring[M->job % (uint64_t)M->cap];
+        M->job++;
+        B->state = 2;
+        pthread_mutex_unlock(&M->mu);
+        const int n = bgzf_inflate_raw(B->c, B->bsize, B->xlen, B->u);
+        pthread_mutex_lock(&M->mu);
+        B->ulen = n;
+        B->state = 3;
+        pthread_cond_broadcast(&M->cv_done);
+    }
+    pthread_mutex_unlock(&M->mu);
+    return NULL;
+}
+
+/* read ahead into the free slots (the consumer's thread; the lock is not held
+ * while reading) */
+static void mt_fill(bgzf_t *z) {
+    bgzf_mt_t *M = z->mt;
+    for (;;) {
+        pthread_mutex_lock(&M->mu);
+        const int room = !M->reof && M->tail - M->head < (uint64_t)M->cap;
+        mt_blk_t *B = room ? &M->ring[M->tail % (uint64_t)M->cap] : NULL;
+        pthread_mutex_unlock(&M->mu);
+        if (!B) return;
+        uint32_t xlen = 0;
+        const int bs = bgzf_read_raw(z, M->raddr, B->c, &xlen);
+        pthread_mutex_lock(&M->mu);
+        if (bs <= 0) {
+            M->reof = 1;
+            M->rerr = bs;                          /* 0: clean EOF */
+        } else {
+            B->caddr = M->raddr;
+            B->next = M->raddr + (uint64_t)bs;
+            B->bsize = (uint32_t)bs;
+            B->xlen = xlen;
+            B->state = 1;
+            M->raddr = B->next;
+            M->tail++;
+            pthread_cond_signal(&M->cv_job);
+        }
+        pthread_mutex_unlock(&M->mu);
+        if (bs <= 0) return;
+    }
+}
+
+/* wait for every inflate in flight, then empty the ring (lock held) */
+static void mt_drain(bgzf_mt_t *M) {
+    while (M->job != M->tail) pthread_cond_wait(&M->cv_done, &M->mu);
+    for (uint64_t i = M->head; i < M->tail; i++)
+        while (M->ring[i % (uint64_t)M->cap].state == 2) pthread_cond_wait(&M->cv_done, &M->mu);
+    for (int i = 0; i < M->cap; i++) M->ring[i].state = 0;
+    M->head = M->tail = M->job = 0;
+}
+
+static int bgzf_load_mt(bgzf_t *z, uint64_t addr) {
+    bgzf_mt_t *M = z->mt;
+    pthread_mutex_lock(&M->mu);
+    const int hit = M->tail > M->head && M->ring[M->head % (uint64_t)M->cap].caddr == addr;
+    const int at_end = M->tail == M->head && M->reof && M->raddr == addr;
+    if (!hit && !at_end) {
+        mt_drain(M);
+        M->raddr = addr;
+        M->reof = 0;
+        M->rerr = 0;
+    }
+    pthread_mutex_unlock(&M->mu);
+    mt_fill(z);
+    pthread_mutex_lock(&M->mu);
+    if (M->tail == M->head) {
+        const int err = M->rerr;
+        pthread_mutex_unlock(&M->mu);
+        if (err < 0) return err;
+        z->caddr = addr; z->next = addr; z->ulen = z->upos = 0; z->eof = 1;
+        return 1;
+    }
+    mt_blk_t *B = &M->ring[M->head % (uint64_t)M->cap];
+    while (B->state != 3) pthread_cond_wait(&M->cv_done, &M->mu);
+    pthread_mutex_unlock(&M->mu);
+    if (B->ulen < 0) return B->ulen;
+    memcpy(z->ubuf, B->u, (size_t)B->ulen);
+    z->caddr = B->caddr;
+    z->next = B->next;
+    z->ulen = B->ulen;
+    z->upos = 0;
+    z->eof = 0;
+    pthread_mutex_lock(&M->mu);
+    B->state = 0;
+    M->head++;
+    pthread_mutex_unlock(&M->mu);
+    mt_fill(z);
+    return 0;
+}
+
+/* n inflate threads for this reader (n <= 1: single-threaded) */
+static int bgzf_mt(bgzf_t *z, int n) {
+    if (n <= 1 || z->mt) return 0;
+    bgzf_mt_t *M = (bgzf_mt_t *)calloc(1, sizeof *M);
+    if (!M) return PF_ERR_NOMEM;
+    M->nth = n;
+    M->cap = 4 * n;
+    M->ring = (mt_blk_t *)calloc((size_t)M->cap, sizeof(mt_blk_t));
+    M->th = (pthread_t *)calloc((size_t)n, sizeof(pthread_t));
+    if (!M->ring || !M->th) { free(M->ring); free(M->th); free(M); return PF_ERR_NOMEM; }
+    pthread_mutex_init(&M->mu, NULL);
+    pthread_cond_init(&M->cv_job, NULL);
+    pthread_cond_init(&M->cv_done, NULL);
+    /* the ring starts where the single-threaded reader stands */
+    M->raddr = z->ulen > 0 && z->upos < z->ulen ? z->next : z->caddr;
+    int made = 0;
+    for (int i = 0; i < n; i++) made += pthread_create(&M->th[i], NULL, mt_worker, M) == 0;
+    if (made < n) {
+        pthread_mutex_lock(&M->mu);
+        M->stop = 1;
+        pthread_cond_broadcast(&M->cv_job);
+        pthread_mutex_unlock(&M->mu);
+        for (int i = 0; i < made; i++) pthread_join(M->th[i], NULL);
+        free(M->ring); free(M->th); free(M);
+        return PF_ERR_INTERNAL;
+    }
+    z->mt = M;
+    return 0;
+}
+
+static void bgzf_mt_free(bgzf_t *z) {
+    bgzf_mt_t *M = z->mt;
+    if (!M) return;
+    pthread_mutex_lock(&M->mu);
+    mt_drain(M);
+    M->stop = 1;
+    pthread_cond_broadcast(&M->cv_job);
+    pthread_mutex_unlock(&M->mu);
+    for (int i = 0; i < M->nth; i++) pthread_join(M->th[i], NULL);
+    pthread_mutex_destroy(&M->mu);
+    pthread_cond_destroy(&M->cv_job);
+    pthread_cond_destroy(&M->cv_done);
+    free(M->ring);
+    free(M->th);
+    free(M);
+    z->mt = NULL;
+}
+
+/* load the block at compressed address addr; 0 ok, 1 clean EOF, <0 error */
+static int bgzf_load(bgzf_t *z, uint64_t addr) {
+    if (z->mt) return bgzf_load_mt(z, addr);
+    uint32_t xlen = 0;
+    const int bsize = bgzf_read_raw(z, addr, z->cbuf, &xlen);
+    if (bsize == 0) { z->caddr = addr; z->next = addr; z->ulen = z->upos = 0; z->eof = 1; return 1; }
+    if (bsize < 0) return bsize;
+    const int out = bgzf_inflate_raw(z->cbuf, (uint32_t)bsize, xlen, z->ubuf);
+    if (out < 0) return out;
     z->caddr = addr;
-    z->next = addr + bsize;
-    z->ulen = (int)out;
+    z->next = addr + (uint64_t)bsize;
+    z->ulen = out;
     z->upos = 0;
     z->eof = 0;
     return 0;
@@ -145,6 +338,7 @@ static int64_t bgzf_read(bgzf_t *z, void *dst, size_t n) {
 }
 
 static void bgzf_close(bgzf_t *z) {
+    bgzf_mt_free(z);
     if (z->f) fclose(z->f);
     z->f = NULL;
     free(z->iobuf);
@@ -193,6 +387,7 @@ struct pf_bam {
     int32_t n_ref_idx;
     ref_idx_t *idx;
     int64_t n_no_coor;           /* the index's count of unplaced records; -1 when it has none */
+    int n_threads;               /* inflate threads of the whole-file / whole-contig passes */
 };
 
 static int cmp_bin(const void *a, const void *b) {
@@ -374,6 +569,7 @@ void pf_bam_close(pf_bam_t *b) {
 }
 
 const char *pf_bam_path(const pf_bam_t *b) { return b ? b->path : NULL; }
+void pf_bam_set_threads(pf_bam_t *b, int n) { if (b) b->n_threads = n; }
 int64_t pf_bam_n_no_coor(const pf_bam_t *b) { return b ? b->n_no_coor : -1; }
 
 int32_t pf_bam_n_targets(const pf_bam_t *b) { return b ? (b->path ? b->n_ref : b->n_ref_idx) : 0; }
@@ -989,6 +1185,7 @@ int pf_bam_fetch_contig_reads(pf_bam_t *b, const char *chrom, pf_bam_reads_t **o
     F.tid = tid;
     F.reads_mode = 1;
     int rc = bgzf_open(&F.z, b->path);
+    if (!rc) rc = bgzf_mt(&F.z, b->n_threads);
     /* sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX) */
     if (!rc) rc = fetch_region(&F, 0, INT64_MAX, &o->rb);
     bgzf_close(&F.z);
@@ -1426,7 +1623,8 @@ int pf_bam_estimate_coverage(pf_bam_t *b, int32_t *covs, int32_t n) {
     if (!z) return PF_ERR_NOMEM;
     int rc = bgzf_open(z, b->path);
     if (rc) { free(z); return rc; }
-    rc = bgzf_seek(z, b->data_off) ? PF_ERR_ARG : 0;
+    rc = bgzf_mt(z, b->n_threads);
+    if (!rc) rc = bgzf_seek(z, b->data_off) ? PF_ERR_ARG : 0;
     uint8_t *rec = NULL;
     size_t cap = 0;
     uint64_t *bins = NULL;

@@ -383,6 +383,7 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
 
     pf_bam_t *bam = NULL;
     rc = pf_bam_open(o->bam_path, NULL, &bam);
+    if (!rc) pf_bam_set_threads(bam, o->threads);
     if (rc) { pf_mp_free(p); return rc; }
     const int32_t nt = pf_bam_n_targets(bam);
     int32_t *covs = NULL;
@@ -698,6 +699,7 @@ int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
     pf_tags_t *seen = NULL;
     int rc = pf_vcf_known_vars(p->vcf_path, contig, &kt);
     if (!rc && kt->vars.n) rc = pf_bam_open(p->bam_path, NULL, &bam);
+    if (!rc && bam) pf_bam_set_threads(bam, p->o.threads);
     if (!rc && kt->vars.n && !p->o.host_fetch) {
         /* device fetch + K4 on the device (pf_haptag_bam) */
         pf_bam_dev_fetch_t *F = NULL;

@@ -98,11 +98,12 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
                 gtf=ep.gtf_text(contigs, blocks), tsv=ep.tsv_text(contigs, blocks), vcf=vcf, counts=counts)
 
 
-def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4, fetch_threads=1):
+def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4, fetch_threads=1, inflate_threads=1):
     """runner(plan, kind, j) for pomfret_amd.pipeline.methphase_files_dist /
     the Plan steps: a job's result computed by the oracle instead of the
     device (CPU tests of the product's plan / shard / merge / write).
-    fetch_threads: host reader threads per window job."""
+    fetch_threads: host reader threads per window job; inflate_threads: BGZF
+    inflate threads of a -u job's whole-contig read (bgzf_mt)."""
     import oracle
     from pomfret_amd import LoadConfig
     from pomfret_amd.bam import BamFile, vcf_known_vars
@@ -119,7 +120,7 @@ def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4, fetch_threads=
 
     def run(plan, kind, j):
         info = plan.job_info(kind, j)
-        with BamFile(bam_path) as bam:
+        with BamFile(bam_path, threads=inflate_threads if kind == JOB_HAPTAG else 1) as bam:
             if kind == JOB_HAPTAG:
                 kv = vcf_known_vars(vcf_path, info["contig_name"])
                 tab = {}
@@ -165,14 +166,17 @@ def methphase_files_port(bam_path, vcf_path, out_prefix, cfg, lcfg=None, untagge
     """The CPU port of the whole `pomfret methphase` driver -- the bench's CPU
     side of the file-to-output legs, and a CPU check of the product's
     planner / merge / writers.  The product's C plan and writers run with
-    --host-fetch semantics (the serial host coverage pass of
-    estimate_read_coverage_dirtyfast when cfg is None, blockjoin.c:951-1040;
-    the host BAM reader), and every job is computed by the oracle: the -u
-    pre-pass one contig per thread (the reference runs it serially while
-    loading the VCF, 2069-2080), then the window jobs in order, each fetched
-    with `threads` reader threads and run on `threads` oracle threads over
-    windows (the reference's kt_for runs contigs, 4560).  Writes the same
-    outputs as methphase_files.  -> (result dict, seconds per phase)."""
+    --host-fetch semantics and `threads` as the reference's -t N: the host
+    coverage pass of estimate_read_coverage_dirtyfast when cfg is None
+    (blockjoin.c:951-1040) reads the BAM with `threads` BGZF inflate threads
+    (bgzf_mt, 576-578; pf_bam_set_threads); every job is computed by the
+    oracle: the -u pre-pass one contig per thread, each contig's read with
+    threads / contigs inflate threads (the reference runs the contigs
+    serially with -t N inflate threads, 2069-2080, 1848), then the window
+    jobs in order, each fetched with `threads` reader threads and run on
+    `threads` oracle threads over windows (the reference's kt_for runs
+    contigs, 4560).  Writes the same outputs as methphase_files.  ->
+    (result dict, seconds per phase)."""
     import time
     from concurrent.futures import ThreadPoolExecutor
     from pomfret_amd.pipeline import JOB_HAPTAG, JOB_WINDOWS, MODE_METHPHASE, Plan, _result, make_opts
@@ -182,10 +186,11 @@ def methphase_files_port(bam_path, vcf_path, out_prefix, cfg, lcfg=None, untagge
                   job_windows=job_windows, host_fetch=True)
     plan = Plan(o)
     t1 = time.perf_counter()
-    run = oracle_job_runner(bam_path, vcf_path, lcfg, n_threads=threads, fetch_threads=threads)
+    nj = plan.n_jobs(JOB_HAPTAG) if untagged else 0
+    run = oracle_job_runner(bam_path, vcf_path, lcfg, n_threads=threads, fetch_threads=threads,
+                            inflate_threads=max(1, threads // max(1, min(threads, nj))))
     try:
         if untagged:
-            nj = plan.n_jobs(JOB_HAPTAG)
             with ThreadPoolExecutor(max(1, min(threads, nj))) as ex:
                 res = list(ex.map(lambda j: run(plan, JOB_HAPTAG, j), range(nj)))
             for j, r in enumerate(res):

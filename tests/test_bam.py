@@ -285,6 +285,12 @@ def test_u_ingest_round_trip(tmp_path):
     with BamFile(bam) as b:
         got, qn, info = b.fetch_contig_reads("chrU")
     assert info["n_truncated"] == 0
+    with BamFile(bam, threads=5) as b:                   # BGZF inflate threads: the same reads
+        got_t, qn_t, _ = b.fetch_contig_reads("chrU")
+        got_t2, qn_t2, _ = b.fetch_contig_reads("chrU")
+    assert qn_t == qn and qn_t2 == qn
+    for f in ("start", "end", "cigar", "seq", "md"):
+        assert np.array_equal(getattr(got_t, f), getattr(got, f)) and np.array_equal(getattr(got_t2, f), getattr(got, f))
     assert qn == [f"u{i}" for i in order]                 # the flag-256 record is skipped
     o = np.asarray(order)
     assert np.array_equal(got.start, reads.start[o]) and np.array_equal(got.end, reads.end[o])
@@ -497,6 +503,11 @@ def test_estimate_coverage(tmp_path):
         got = b.estimate_coverage()
         assert b.n_unplaced == 0
     assert got == _py_cov(seqfix, lens) and got[0] > 0
+    # with BGZF inflate threads (bgzf_mt, the reference's -t N): the same pass
+    for th in (2, 7):
+        with BamFile(p1, threads=th) as b:
+            assert b.estimate_coverage() == got
+            assert b.estimate_coverage() == got            # a second pass seeks back: the ring restarts
     # an unplaced read at the end reassigns refID: the last contig keeps 0
     un = Rec(-1, -1, "unplaced", flag=4, cigar=[], seq=bytes(50), l_seq=100)
     p2 = str(tmp_path / "cov2.bam")
