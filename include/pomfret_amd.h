@@ -474,6 +474,7 @@ typedef struct pf_bam_dev_fetch {
     double ms_read, ms_inflate, ms_chain, ms_decode, ms_select, ms_build, ms_total;
     uint32_t attempts;             /* plans tried (a record past the planned blocks widens the plan) */
     const uint8_t *read_hp;        /* pf_haptag_bam: [n_recs] each read's tag (NULL otherwise)  */
+    uint32_t from_arena;           /* 1: the blocks came from a kept -u arena (nothing read or inflated) */
 } pf_bam_dev_fetch_t;
 /* replace a record-level batch's per-record HP values (the -u table's tags,
  * blockjoin.c:1114-1122); n must equal its record count */
@@ -728,6 +729,10 @@ typedef struct pf_mp_stats {
     uint64_t comp_bytes[2], inflated_bytes[2];
     double run_ms[2];           /* pf_methphase_run / K4 wall, summed over jobs */
     uint64_t n_fetch[2];        /* device fetches */
+    /* window jobs of a run that keeps the -u pre-pass's arenas: fetches served
+     * from a kept arena, fetches that read and inflated the file again (their
+     * compressed bytes), and jobs a context took from another device's queue */
+    uint64_t arena_hits, arena_misses, reread_bytes, steals;
 } pf_mp_stats_t;
 int  pf_mp_stats(const pf_mp_plan_t *p, pf_mp_stats_t *s);
 

@@ -57,7 +57,8 @@ class PfBamDevFetch(C.Structure):
                 ("inflated_bytes", C.c_uint64), ("n_blocks", C.c_uint64), ("n_chain_recs", C.c_uint64),
                 ("ms_read", C.c_double), ("ms_inflate", C.c_double), ("ms_chain", C.c_double),
                 ("ms_decode", C.c_double), ("ms_select", C.c_double), ("ms_build", C.c_double),
-                ("ms_total", C.c_double), ("attempts", C.c_uint32), ("read_hp", C.c_void_p)]
+                ("ms_total", C.c_double), ("attempts", C.c_uint32), ("read_hp", C.c_void_p),
+                ("from_arena", C.c_uint32)]
 
 
 def _bind():

@@ -214,18 +214,39 @@ bool cache_enabled(const pf_ctx_t *ctx) {
     return std::find(g_keep_on.begin(), g_keep_on.end(), ctx) != g_keep_on.end();
 }
 
+// PF_FETCH_CACHE_SCOPE=ctx: an arena serves only the context that kept it,
+// and the driver treats every context as a device of its own (the -u
+// pre-pass runs on all of them): the multi-GPU affinity of window jobs,
+// rehearsed on one GPU (tests).
+extern "C" int pf_fetch_cache_scope_ctx(void) {
+    const char *e = getenv("PF_FETCH_CACHE_SCOPE");
+    return e && !strcmp(e, "ctx") ? 1 : 0;
+}
+
 // An arena kept by any context of the same device serves this one: the
 // driver's contexts of one GPU (PF_DEV_CONTEXTS) share its HBM, and the -u
 // pre-pass that wrote the arenas has finished (its jobs joined) before the
 // window jobs look them up.
 const ArenaCache *cache_find(const pf_ctx_t *ctx, const char *path, const struct stat &s, int32_t tid) {
     const int dev = pf_ctx_device((const pf_ctx *)ctx);
+    const bool by_ctx = pf_fetch_cache_scope_ctx() != 0;
     std::lock_guard<std::mutex> lk(g_cache_mu);
     for (const ArenaCache *c : g_cache)
-        if ((c->ctx == ctx || pf_ctx_device((const pf_ctx *)c->ctx) == dev) && c->tid == tid && c->fsize == (uint64_t)s.st_size && c->mt_s == (int64_t)s.st_mtim.tv_sec &&
+        if ((c->ctx == ctx || (!by_ctx && pf_ctx_device((const pf_ctx *)c->ctx) == dev)) && c->tid == tid &&
+            c->fsize == (uint64_t)s.st_size && c->mt_s == (int64_t)s.st_mtim.tv_sec &&
             c->mt_ns == (int64_t)s.st_mtim.tv_nsec && c->path == path)
             return c;
     return nullptr;
+}
+
+// The first of ctxs[0, n) that a kept arena of (path, contig tid) would
+// serve, or -1: the home of a window job of that contig (pf_pipeline.c).
+extern "C" int pf_fetch_cache_home(pf_ctx_t *const *ctxs, int n, const char *path, int32_t tid) {
+    struct stat s;
+    if (!path || stat(path, &s) != 0) return -1;
+    for (int i = 0; i < n; i++)
+        if (cache_find(ctxs[i], path, s, tid)) return i;
+    return -1;
 }
 
 // The plan's blocks from a kept arena: per run, the kept blocks from its
@@ -905,6 +926,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         pub.ms_build = ms_build;
         pub.ms_total = now_ms() - t_start;
         pub.attempts = (uint32_t)attempt + 1;
+        pub.from_arena = cached ? 1u : 0u;
         done = true;
         if (keep && !cached) {
             // an exact copy of the arena (the fetch's own is sized from the

@@ -208,6 +208,11 @@ typedef struct {
     uint32_t n_limit;          /* windows left undecided for a device limit */
 } job_t;
 
+/* pf_ingest.hip / pf_api.hip */
+int pf_fetch_cache_scope_ctx(void);
+int pf_fetch_cache_home(pf_ctx_t *const *ctxs, int n, const char *path, int32_t tid);
+int pf_ctx_device(const pf_ctx_t *ctx);
+
 struct pf_mp_plan {
     pf_methphase_opts_t o;
     char *bam_path, *vcf_path, *out_prefix;
@@ -230,6 +235,7 @@ struct pf_mp_plan {
     uint32_t n_limit;
     double report_counts[3];   /* correct, switch, fail */
     pf_mp_stats_t st;          /* measurement hook (pf_mp_stats) */
+    int keeps_arenas;          /* the -u pre-pass's arenas stay on the devices for the window jobs */
     pthread_mutex_t st_mu;
     /* -u without -c, one process: the coverage estimate comes from the -u
      * pre-pass's whole-contig fetches (pf_haptag_bam_cov), per VCF contig */
@@ -255,6 +261,10 @@ static void st_fetch(pf_mp_plan_t *p, int kind, const pf_bam_dev_fetch_t *F, dou
         s->comp_bytes[kind] += F->comp_bytes;
         s->inflated_bytes[kind] += F->inflated_bytes;
         s->n_fetch[kind]++;
+        if (kind == 0 && p->keeps_arenas) {
+            if (F->from_arena) s->arena_hits++;
+            else { s->arena_misses++; s->reread_bytes += F->comp_bytes; }
+        }
     }
     s->run_ms[kind] += run_ms;
     pthread_mutex_unlock(&p->st_mu);
@@ -1320,17 +1330,53 @@ static int finish_deferred_estimate(pf_mp_plan_t *p, pf_ctx_t *ctx) {
 /* ------------------------------------------------------------------ */
 /* in-process driver: one host thread per device                        */
 
+/* Job queues of a run: one per affinity group (a device, or with
+ * PF_FETCH_CACHE_SCOPE=ctx a context) holding the window jobs whose contig's
+ * -u arena that group kept, plus a shared queue (the other jobs, and every job
+ * of a run without kept arenas).  A worker takes from its group's queue,
+ * then from the shared one, then steals from the other groups' (the jobs of
+ * each queue in the plan's heaviest-first order). */
+typedef struct {
+    int n_groups;              /* affinity groups; queue n_groups is the shared one */
+    uint32_t *list;            /* the jobs, queue by queue */
+    uint32_t *off;             /* [n_groups + 2] */
+    atomic_uint *pos;          /* [n_groups + 1] next index of each queue */
+    int steal;                 /* 0: a worker never takes another group's jobs (PF_JOB_STEAL=0, tests) */
+} jobq_t;
+
 typedef struct {
     pf_mp_plan_t *p;
     pf_ctx_t *ctx;
     int device;
     int own_ctx;
     int kind;
-    atomic_uint *next;
-    const uint32_t *todo;
-    uint32_t n_todo;
+    jobq_t *q;
+    int group;                 /* its affinity group (-1: none) */
     int rc;
 } dev_worker_t;
+
+/* the worker's next job: 1 and *job, or 0 when every queue is drained */
+static int next_job(dev_worker_t *W, uint32_t *job) {
+    jobq_t *q = W->q;
+    const int G = q->n_groups;
+    for (int k = -1; k <= G; k++) {
+        /* own group first, then the shared queue, then the others in turn */
+        int g = k < 0 ? W->group : k == 0 ? G : (W->group + k) % (G > 0 ? G : 1);
+        if (g < 0 || (k > 0 && (g == W->group || G == 0 || !q->steal))) continue;
+        const uint32_t n = q->off[g + 1] - q->off[g];
+        if (atomic_load(&q->pos[g]) >= n) continue;
+        const uint32_t i = atomic_fetch_add(&q->pos[g], 1);
+        if (i >= n) continue;
+        *job = q->list[q->off[g] + i];
+        if (k > 0) {
+            pthread_mutex_lock(&W->p->st_mu);
+            W->p->st.steals++;
+            pthread_mutex_unlock(&W->p->st_mu);
+        }
+        return 1;
+    }
+    return 0;
+}
 
 typedef struct {
     const pf_mp_plan_t *p;
@@ -1354,12 +1400,9 @@ static void *dev_main(void *arg) {
         W->own_ctx = 1;
         if (rc) { W->rc = rc; return NULL; }
     }
+    uint32_t jb;
     if (W->kind == PF_JOB_HAPTAG) {
-        for (;;) {
-            const uint32_t i = atomic_fetch_add(W->next, 1);
-            if (i >= W->n_todo || rc) break;
-            rc = pf_mp_run_haptag_job(p, W->ctx, W->todo[i]);
-        }
+        while (!rc && next_job(W, &jb)) rc = pf_mp_run_haptag_job(p, W->ctx, jb);
         W->rc = rc;
         return NULL;
     }
@@ -1369,11 +1412,7 @@ static void *dev_main(void *arg) {
     rc = pf_bam_open(p->bam_path, NULL, &bam[0]);
     if (!rc) rc = pf_bam_open(p->bam_path, NULL, &bam[1]);
     if (!rc && !p->o.host_fetch) {              /* device fetch: host planning + reads, the rest on the GPU */
-        for (;;) {
-            const uint32_t k = atomic_fetch_add(W->next, 1);
-            if (k >= W->n_todo || rc) break;
-            rc = job_device_fetch(p, W->ctx, bam[0], &p->jobs[W->todo[k]]);
-        }
+        while (!rc && next_job(W, &jb)) rc = job_device_fetch(p, W->ctx, bam[0], &p->jobs[jb]);
         pf_bam_close(bam[0]);
         pf_bam_close(bam[1]);
         W->rc = rc;
@@ -1382,19 +1421,18 @@ static void *dev_main(void *arg) {
     prefetch_t cur, nxt;
     memset(&cur, 0, sizeof cur);
     memset(&nxt, 0, sizeof nxt);
-    uint32_t i = rc ? UINT32_MAX : atomic_fetch_add(W->next, 1);
     int have = 0, slot = 0;
-    if (i < W->n_todo) {
-        cur.p = p; cur.bam = bam[slot]; cur.J = &p->jobs[W->todo[i]];
+    if (!rc && next_job(W, &jb)) {
+        cur.p = p; cur.bam = bam[slot]; cur.J = &p->jobs[jb];
         job_fetch(p, cur.bam, cur.J, &cur.f);
         have = 1;
     }
     while (have && !rc) {
         pthread_t th;
         int spawned = 0;
-        const uint32_t k = atomic_fetch_add(W->next, 1);
-        if (k < W->n_todo) {
-            nxt.p = p; nxt.bam = bam[slot ^ 1]; nxt.J = &p->jobs[W->todo[k]];
+        const int more = next_job(W, &jb);
+        if (more) {
+            nxt.p = p; nxt.bam = bam[slot ^ 1]; nxt.J = &p->jobs[jb];
             nxt.f.recs = NULL; nxt.f.rc = 0;
             spawned = pthread_create(&th, NULL, prefetch_main, &nxt) == 0;
             if (!spawned) job_fetch(p, nxt.bam, nxt.J, &nxt.f);
@@ -1403,7 +1441,7 @@ static void *dev_main(void *arg) {
         if (cur.f.recs) pf_bam_records_free(cur.f.recs);
         cur.f.recs = NULL;
         if (spawned) pthread_join(th, NULL);
-        if (k < W->n_todo) { cur = nxt; slot ^= 1; }
+        if (more) { cur = nxt; slot ^= 1; }
         else have = 0;
     }
     if (have && cur.f.recs) pf_bam_records_free(cur.f.recs);
@@ -1434,11 +1472,47 @@ static int run_on_devices_(pf_mp_plan_t *p, const pf_methphase_opts_t *o, int ki
     if (nd <= 0) { free(todo); return PF_ERR_HIP; }
     dev_worker_t *W = (dev_worker_t *)calloc(nd, sizeof(dev_worker_t));
     pthread_t *th = (pthread_t *)calloc(nd, sizeof(pthread_t));
-    atomic_uint next;
-    atomic_init(&next, 0);
-    int rc = (!W || !th) ? PF_ERR_NOMEM : PF_OK;
+    /* affinity groups: window jobs of a run that kept the -u arenas go to the
+     * device (or context) holding their contig's arena */
+    jobq_t q;
+    memset(&q, 0, sizeof q);
+    int *gid = (int *)malloc(sizeof(int) * (size_t)nd);
+    int *home = (int *)malloc(sizeof(int) * (size_t)(nt ? nt : 1));
+    q.list = (uint32_t *)malloc(sizeof(uint32_t) * (nt ? nt : 1));
+    q.off = (uint32_t *)calloc((size_t)nd + 2, sizeof(uint32_t));
+    q.pos = (atomic_uint *)calloc((size_t)nd + 1, sizeof(atomic_uint));
+    int rc = (!W || !th || !gid || !home || !q.list || !q.off || !q.pos) ? PF_ERR_NOMEM : PF_OK;
+    const int affine = !rc && kind == PF_JOB_WINDOWS && p->keeps_arenas && o->n_ctxs > 0;
+    {
+        const char *e = getenv("PF_JOB_STEAL");
+        q.steal = !(e && !strcmp(e, "0"));
+    }
     for (int d = 0; d < nd && !rc; d++) {
-        W[d].p = p; W[d].kind = kind; W[d].next = &next; W[d].todo = todo; W[d].n_todo = nt;
+        gid[d] = -1;
+        if (!affine) continue;
+        const int by_ctx = pf_fetch_cache_scope_ctx();
+        for (int e = 0; e < d && gid[d] < 0; e++)
+            if (!by_ctx && pf_ctx_device(o->ctxs[e]) == pf_ctx_device(o->ctxs[d])) gid[d] = gid[e];
+        if (gid[d] < 0) gid[d] = q.n_groups++;
+    }
+    for (uint32_t i = 0; i < nt && !rc; i++) {
+        home[i] = q.n_groups;                       /* the shared queue */
+        if (affine) {
+            const int h = pf_fetch_cache_home(o->ctxs, nd, p->bam_path, p->tid[J[todo[i]].contig]);
+            if (h >= 0) home[i] = gid[h];
+        }
+        q.off[home[i] + 1]++;
+    }
+    for (int g = 0; g <= q.n_groups && !rc; g++) q.off[g + 1] += q.off[g];
+    if (!rc) {
+        uint32_t *fill = (uint32_t *)calloc((size_t)q.n_groups + 1, sizeof(uint32_t));
+        if (!fill) rc = PF_ERR_NOMEM;
+        for (uint32_t i = 0; i < nt && !rc; i++) q.list[q.off[home[i]] + fill[home[i]]++] = todo[i];
+        free(fill);
+        for (int g = 0; g <= q.n_groups; g++) atomic_init(&q.pos[g], 0);
+    }
+    for (int d = 0; d < nd && !rc; d++) {
+        W[d].p = p; W[d].kind = kind; W[d].q = &q; W[d].group = gid[d];
         W[d].ctx = o->n_ctxs > 0 ? o->ctxs[d] : NULL;
         W[d].device = o->devices ? o->devices[d] : d;
     }
@@ -1454,6 +1528,7 @@ static int run_on_devices_(pf_mp_plan_t *p, const pf_methphase_opts_t *o, int ki
         if (W[d].own_ctx && W[d].ctx) pf_ctx_destroy(W[d].ctx);
     }
     free(W); free(th); free(todo);
+    free(gid); free(home); free(q.list); free(q.off); free((void *)q.pos);
     return rc;
 }
 
@@ -1539,13 +1614,14 @@ static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
      * jobs of the same context (device fetch only) */
     const int keep = !rc && o->untagged && !o->host_fetch && o->n_ctxs > 0;
     for (int d = 0; keep && d < o->n_ctxs; d++) pf_fetch_cache_enable(o->ctxs[d], 1);
+    if (keep) p->keeps_arenas = 1;
     if (!rc && o->untagged) {
         /* the -u pre-pass on one context per device: its whole-contig fetches
          * are bound by the file reads, and a second context per GPU would only
          * pin a second contig-sized staging buffer (e2e_u CLI 2.1 -> 2.9 s);
          * the window jobs then run on every context and share the arenas */
         pf_methphase_opts_t ou = *o;
-        if (o->n_ctxs > 1) ou.n_ctxs = distinct_device_prefix(o->ctxs, o->n_ctxs);
+        if (o->n_ctxs > 1 && !pf_fetch_cache_scope_ctx()) ou.n_ctxs = distinct_device_prefix(o->ctxs, o->n_ctxs);
         rc = run_on_devices(p, &ou, PF_JOB_HAPTAG);
         if (!rc) rc = pf_mp_merge_raw(p);
     }

@@ -63,7 +63,8 @@ class PfMpStats(C.Structure):
     _fields_ = [("s_plan", C.c_double), ("s_estimate", C.c_double), ("s_haptag", C.c_double),
                 ("s_windows", C.c_double), ("s_finish", C.c_double), ("fetch_ms", (C.c_double * 7) * 2),
                 ("comp_bytes", C.c_uint64 * 2), ("inflated_bytes", C.c_uint64 * 2), ("run_ms", C.c_double * 2),
-                ("n_fetch", C.c_uint64 * 2)]
+                ("n_fetch", C.c_uint64 * 2), ("arena_hits", C.c_uint64), ("arena_misses", C.c_uint64),
+                ("reread_bytes", C.c_uint64), ("steals", C.c_uint64)]
 
 
 class PfMpJobResult(C.Structure):
@@ -325,6 +326,7 @@ class Plan:
         _check(lib().pf_mp_stats(self.h, C.byref(st)), "pf_mp_stats")
         names = ("read", "inflate", "chain", "decode", "select", "build", "total")
         out = {k: round(getattr(st, k), 4) for k in ("s_plan", "s_estimate", "s_haptag", "s_windows", "s_finish")}
+        out.update({k: int(getattr(st, k)) for k in ("arena_hits", "arena_misses", "reread_bytes", "steals")})
         for i, kind in enumerate(("windows", "haptag")):
             out[kind] = dict({f"{n}_ms": round(st.fetch_ms[i][j], 2) for j, n in enumerate(names)},
                              comp_bytes=int(st.comp_bytes[i]), inflated_bytes=int(st.inflated_bytes[i]),

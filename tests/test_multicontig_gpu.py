@@ -261,3 +261,42 @@ def test_two_ranks_on_one_device(gpu_ctx, tmp_path, untagged):
         assert got["raw_hp"] == one["raw_hp"]
     assert _outputs(str(tmp_path / "dist")) == _outputs(str(tmp_path / "one"))
     assert (one["decision"] >= 0).sum() >= 3
+
+
+@pytest.mark.parametrize("steal", [True, False], ids=["steal", "nosteal"])
+def test_untagged_window_jobs_follow_the_arenas(gpu_ctx, tmp_path, genome_small, monkeypatch, steal):
+    """The -u pre-pass keeps each contig's inflated arena on the device that
+    fetched it; window jobs are queued per device by that arena and a device
+    steals from another's queue only when its own and the shared one are
+    empty (VERDICT r03 "next round" 6; blockjoin.c:1841-1898, 4350-4426).
+    Rehearsed on one GPU with PF_FETCH_CACHE_SCOPE=ctx (an arena serves only
+    the context that kept it, and every context is a device of its own): the
+    outputs equal the one-context run byte for byte; every window fetch is an
+    arena hit or a miss, the misses are the stolen jobs (their compressed
+    bytes re-read), and with stealing off every fetch hits."""
+    from pomfret_amd import Context
+    from pomfret_amd.pipeline import methphase_files
+    g = genome_small
+    one = methphase_files(g["bam"], g["vcf"], str(tmp_path / "one"), None, ctx=gpu_ctx, untagged=True, tsv=True,
+                          job_windows=3)
+    monkeypatch.setenv("PF_FETCH_CACHE_SCOPE", "ctx")
+    if not steal:
+        monkeypatch.setenv("PF_JOB_STEAL", "0")
+    ctxs = [Context(0), Context(0)]
+    try:
+        two = methphase_files(g["bam"], g["vcf"], str(tmp_path / "two"), None, ctxs=ctxs, untagged=True, tsv=True,
+                              job_windows=3)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert np.array_equal(one["decision"], two["decision"])
+    assert list(one["qname_hp"].items()) == list(two["qname_hp"].items())
+    assert one["raw_hp"] == two["raw_hp"]
+    assert _outputs(str(tmp_path / "one")) == _outputs(str(tmp_path / "two"))
+    st = two["stats"]
+    n_fetch = st["windows"]["n_fetch"]
+    assert n_fetch > 4 and st["arena_hits"] + st["arena_misses"] == n_fetch
+    assert st["arena_misses"] == st["steals"]
+    assert (st["reread_bytes"] > 0) == (st["arena_misses"] > 0)
+    if not steal:
+        assert st["steals"] == 0 and st["arena_hits"] == n_fetch
