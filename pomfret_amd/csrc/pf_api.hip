@@ -38,7 +38,9 @@ __global__ void pf_selftest_wave(unsigned long long *bad);
 #define PF_SLOTS 2
 // I/O block header: status u32[4] | arena counters u64[3] (16) | K2, K3
 // fallback counters u32 (40, 44) | record level: staging bump pointer u64
-// (48), kept reads u32 (56), calls u64 (64), site slots u64 (72) | pad
+// (48), kept reads u32 (56), calls u64 (64), site slots u64 (72) | the heavy
+// kernel's deferral counter u32 (80) | the main greedy kernel's problem
+// counter u32 (84) | pad
 #define PF_IO_HDR 128ull
 
 // kernel timing slots: "pf_k0_pack" is the scan + pack pair
@@ -72,7 +74,7 @@ struct pf_ctx {
 // a lock and only ever raised, so one context's smaller batch never lowers the
 // limit another context's launch relies on.
 static std::mutex g_lds_mu;
-static uint32_t g_lds_set[64][3];             // [device][greedy, fallback + heavy, one-wave]
+static uint32_t g_lds_set[64][4];             // [device][greedy, fallback, one-wave, heavy]
 static int raise_lds_limit(int dev, int which, const void *const *fns, int nf, uint32_t need) {
     if (dev < 0 || dev >= 64) return PF_ERR_ARG;
     std::lock_guard<std::mutex> lk(g_lds_mu);
@@ -108,6 +110,7 @@ struct pf_dbatch {
     hipEvent_t ev[PF_SLOTS][PF_NKERN + 1];   // kernel boundaries per slot
     hipEvent_t done[PF_SLOTS];               // slot's D2H complete
     hipEvent_t hev[PF_SLOTS][2];             // pf_k3_heavy's boundaries on the context's second stream
+    hipEvent_t fev[PF_SLOTS][2];             // pf_k3_fallback's (after the join with the heavy kernel)
     uint32_t n_heavy = 0;                    // k3_order's first n_heavy problems run in pf_k3_heavy
     std::vector<uint32_t> h_heavy;           // and those problems
     bool heavy_launched[PF_SLOTS] = {false, false};
@@ -133,7 +136,7 @@ struct pf_dbatch {
 struct IoView {
     uint32_t *status;
     unsigned long long *ctr;     // keys, big, scr counters after a run
-    uint32_t *fb, *k3fb;
+    uint32_t *fb, *k3fb, *k3fbh;
     uint64_t stage, N, sites;    // record level: the staging arena, calls and site slots needed
     uint32_t R;
     int32_t *table;
@@ -149,6 +152,7 @@ static IoView io_view(const pf_dbatch *b, const uint8_t *h) {
     v.ctr = reinterpret_cast<unsigned long long *>(hh + 16);
     v.fb = reinterpret_cast<uint32_t *>(hh + 40);
     v.k3fb = reinterpret_cast<uint32_t *>(hh + 44);
+    v.k3fbh = reinterpret_cast<uint32_t *>(hh + 80);
     memcpy(&v.stage, hh + PF_IO_STAGE, 8);
     memcpy(&v.R, hh + PF_IO_R, 4);
     memcpy(&v.N, hh + PF_IO_N, 8);
@@ -386,7 +390,10 @@ extern "C" void pf_batch_free(pf_dbatch_t *b) {
         for (int i = 0; i < PF_SLOTS; i++) {
             for (int k = 0; k <= PF_NKERN; k++) (void)hipEventDestroy(b->ev[i][k]);
             (void)hipEventDestroy(b->done[i]);
-            for (int k = 0; k < 2; k++) (void)hipEventDestroy(b->hev[i][k]);
+            for (int k = 0; k < 2; k++) {
+                (void)hipEventDestroy(b->hev[i][k]);
+                (void)hipEventDestroy(b->fev[i][k]);
+            }
         }
     delete b;
 }
@@ -566,21 +573,29 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             return in->win_read_off[a + 1] - in->win_read_off[a] > in->win_read_off[c + 1] - in->win_read_off[c];
         });
         PUT(p, word.data(), word.size()); d.k12_order = p;
-        // Heavy problems: windows with at least 1.25x the median reads (and
-        // >= 600; 2x until the two-context sweep, profiles/r03/sweeps/
-        // heavy_x_two_ctx: 17.01 -> 16.92 ms/step, one batch 18.43 -> 18.16).  They lead k3_order, and run in pf_k3_heavy on the
-        // context's second stream beside the main greedy kernel, starting at
-        // once with the fallback's LDS budget instead of being deferred to the
-        // fallback kernel after it (the serial tail of a gap mix: ~200 problems
-        // of 1,000-1,400 reads, ~5 ms each).  PF_K3_HEAVY=n forces the n
-        // heaviest problems (tests; 0 disables the split).
+        // Heavy problems: the windows too large for the main kernel's LDS
+        // budget (below), run in pf_k3_heavy on the context's second stream
+        // beside the main kernel with a 72 KB budget, so that they start at
+        // once instead of being deferred to the fallback kernel after it.
+        // Round 3 sent the windows with >= 1.25x the median reads there (the
+        // main kernel then ran two 72 KB problems per CU); with round 4's
+        // compact layout (the candidate cache reads its per-read fields from
+        // HBM) the main kernel's 48 KB fit every window of the 60x gap mix
+        // (tools/k3_heavy_prof.py), so the split only takes windows from 2,000
+        // reads (1,100 under the 36 KB tier of 30x batches): one kernel, the
+        // heaviest problems first.  (A heavy kernel asking for 72 KB beside a
+        // main kernel of 48 KB problems waits for free CUs until the main
+        // kernel drains: profiles/r04/.)  PF_K3_HEAVY_X: a multiple of the median instead;
+        // PF_K3_HEAVY=n forces the n heaviest problems (tests; 0: none).
         if (W) {
             std::vector<uint32_t> rw(W);
             for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
+            std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
+            const uint32_t p90 = rw[(W * 9) / 10];
             std::nth_element(rw.begin(), rw.begin() + W / 2, rw.end());
             const char *hx = getenv("PF_K3_HEAVY_X");       // tuning: the multiple of the median
-            const double x = hx ? atof(hx) : 1.25;
-            const uint32_t thr = std::max<uint32_t>(hx ? 1u : 600u, (uint32_t)(x * rw[W / 2]));
+            const uint32_t thr = hx ? std::max<uint32_t>(1u, (uint32_t)(atof(hx) * rw[W / 2]))
+                                    : (p90 <= 400 ? 1100u : 2000u);
             uint32_t nh = 0;
             while (nh < 2 * W && in->win_read_off[(ord[nh] >> 1) + 1] - in->win_read_off[ord[nh] >> 1] >= thr) nh++;
             const char *hv = getenv("PF_K3_HEAVY");
@@ -590,7 +605,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         }
     }
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
-    ALLOC(d.k3_fb_list, std::max<uint32_t>(2 * W, 1));
+    ALLOC(d.k3_fb_list, std::max<uint32_t>(4 * W, 1));       // the main kernel's deferrals, then pf_k3_heavy's
     // one I/O block: the counters zeroed before a run (status, arena
     // counters, fallback counter) followed by everything copied back after it,
     // so a step costs one memset and one D2H copy
@@ -607,6 +622,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     }
     d.fb_ctr = reinterpret_cast<uint32_t *>(b->io + 40);
     d.k3_fb_ctr = reinterpret_cast<uint32_t *>(b->io + 44);
+    d.k3_next = reinterpret_cast<uint32_t *>(b->io + 84);
     d.table = reinterpret_cast<int32_t *>(b->io + PF_IO_HDR);
     d.win_S = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 32ull * W);
     d.win_nreads = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 36ull * W);
@@ -638,13 +654,20 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     // pays (30x: K3 2.43 -> 1.95 ms); for larger windows (60x) the heaviest
     // problems would be deferred to a serial tail, so 72 KB
     // (profiles/r02/k3_lds_sweep).  PF_K3_LDS (tests, tuning) sets both.
-    uint32_t lds_auto = 73728u;
+    // Round 4: the slim loop keeps no per-site divisor cache, u16 per-read
+    // fields and, when a window's slot lists miss LDS, only its candidates'
+    // lists (k3_greedy_slim CACHE); with the slim kernels' 3.7 KB of static
+    // LDS, 48 KB puts three problems on a CU and 36 KB four (LDS is granted
+    // in ~1 KB units: 49.5 KB already drops to two, tools/ubench/lds_occ.hip,
+    // profiles/r04/lds_occ.txt).  Profiled needs by window reads
+    // (tools/k3_heavy_prof.py): on the 60x gap mix every window below 1,284
+    // reads fits 44 KB, the largest 49 KB.
+    uint32_t lds_auto = 49152u;
     if (W) {
         std::vector<uint32_t> rw(W);
         for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
         std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
-        if (rw[(W * 9) / 10] <= 400) lds_auto = 40960u;
-        else if (rw[(W * 9) / 10] <= 800) lds_auto = 45056u;    // 60x: three per CU (u8 count pairs, round 3)
+        if (rw[(W * 9) / 10] <= 400) lds_auto = 36864u;
     }
     const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB"), *ldw = getenv("PF_K3W_LDS");
     // one-wave greedy kernel: ~25 KB leaves six problems per CU (a 60x
@@ -653,6 +676,11 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     d.lds_bytes = lds ? (uint32_t)atoi(lds) : lds_auto;
     d.lds_fb = ldf ? (uint32_t)atoi(ldf) : lds ? d.lds_bytes : 73728u;
     if (d.lds_fb < d.lds_bytes) d.lds_fb = d.lds_bytes;
+    {
+        const char *lh = getenv("PF_K3_LDS_HEAVY");
+        d.lds_heavy = lh ? (uint32_t)atoi(lh) : d.lds_fb;
+        if (d.lds_heavy < d.lds_bytes) d.lds_heavy = d.lds_bytes;
+    }
     // PF_K12_CAP / PF_K12_SMAX lower the fused kernel's limits (tests use them
     // to drive reads and windows through the fallback paths)
     const char *kc = getenv("PF_K12_CAP"), *ks = getenv("PF_K12_SMAX");
@@ -666,6 +694,10 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     // fold, or every iteration through the chunked record-row path (tests)
     const char *kp = getenv("PF_K3_PATH");
     d.k3_mode = !kp ? 0u : strcmp(kp, "fold") == 0 ? 1u : strcmp(kp, "rows") == 0 ? 2u : 0u;
+    {
+        const char *kc = getenv("PF_K3_CACHE");
+        d.k3_cache = kc && !strcmp(kc, "0") ? 0u : 1u;
+    }
     for (int i = 0; i < PF_SLOTS; i++)
         if (hipHostMalloc((void **)&b->h_io[i], b->io_bytes) != hipSuccess) return fail(PF_ERR_NOMEM);
     for (int i = 0; i < PF_SLOTS; i++) {
@@ -673,7 +705,8 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
             if (hipEventCreate(&b->ev[i][k]) != hipSuccess) return fail(PF_ERR_HIP);
         if (hipEventCreate(&b->done[i]) != hipSuccess) return fail(PF_ERR_HIP);
         for (int k = 0; k < 2; k++)
-            if (hipEventCreate(&b->hev[i][k]) != hipSuccess) return fail(PF_ERR_HIP);
+            if (hipEventCreate(&b->hev[i][k]) != hipSuccess || hipEventCreate(&b->fev[i][k]) != hipSuccess)
+                return fail(PF_ERR_HIP);
     }
     b->have_ev = 1;
     *out = b;
@@ -965,6 +998,27 @@ extern "C" int pf_batch_read_recs(const pf_dbatch_t *b, uint32_t *rec_of_read, u
     return PF_OK;
 }
 
+// workgroups of pf_k3_greedy the device holds at once with `lds` bytes of
+// dynamic LDS (occupancy x CUs; PF_K3_PERSIST caps it, tests)
+static uint32_t k3_resident(const pf_ctx *c, uint32_t lds) {
+    static std::mutex mu;
+    static std::vector<std::pair<uint64_t, uint32_t>> memo;
+    const uint64_t key = ((uint64_t)c->device << 32) | lds;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &e : memo) if (e.first == key) return e.second;
+    int per = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)pf_k3_greedy, PF_K3S_THREADS, lds) != hipSuccess ||
+        per <= 0)
+        per = 1;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0) ncu = 1;
+    (void)hipGetLastError();
+    uint32_t n = (uint32_t)per * (uint32_t)ncu;
+    const char *e = getenv("PF_K3_PERSIST");
+    if (e && atoi(e) > 0) n = std::min<uint32_t>(n, (uint32_t)atoi(e));
+    memo.push_back({key, n});
+    return n;
+}
+
 // enqueue one run of the kernels on the context's stream, timing events and
 // results into host slot `slot`.  stages < 3 are debug runs without the D2H:
 // 0 stops after the loader (K0, scan, pack), 1 after K12, 2 after K2.
@@ -982,8 +1036,10 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     }
     {
         const void *f1[1] = {(const void *)pf_k3_greedy};
-        const void *f2[2] = {(const void *)pf_k3_fallback, (const void *)pf_k3_heavy};
-        if (raise_lds_limit(c->device, 0, f1, 1, d.lds_bytes) || raise_lds_limit(c->device, 1, f2, 2, d.lds_fb))
+        const void *f2[1] = {(const void *)pf_k3_fallback};
+        const void *f3[1] = {(const void *)pf_k3_heavy};
+        if (raise_lds_limit(c->device, 0, f1, 1, d.lds_bytes) || raise_lds_limit(c->device, 1, f2, 1, d.lds_fb) ||
+            raise_lds_limit(c->device, 3, f3, 1, d.lds_heavy))
             return PF_ERR_HIP;
     }
     HIPCHK(hipEventRecord(b->ev[slot][0], st));
@@ -1029,23 +1085,40 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         // the heavy problems on the second stream, from the same point (K2 done)
         HIPCHK(hipStreamWaitEvent(c->stream2, b->ev[slot][4], 0));
         HIPCHK(hipEventRecord(b->hev[slot][0], c->stream2));
-        hipLaunchKernelGGL(pf_k3_heavy, dim3(nh), dim3(PF_K3_THREADS), d.lds_fb, c->stream2, d);
+        // its own deferral list: a problem beyond its budget runs in a fallback
+        // launch right behind it on the same stream, beside the main kernel
+        pf_dev_batch dh = d;
+        dh.k3_fb_list = d.k3_fb_list + 2ull * b->W;
+        dh.k3_fb_ctr = reinterpret_cast<uint32_t *>(b->io + 80);
+        hipLaunchKernelGGL(pf_k3_heavy, dim3(nh), dim3(PF_K3S_THREADS), d.lds_heavy, c->stream2, dh);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(nh, 512)), dim3(PF_K3_THREADS), d.lds_fb,
+                           c->stream2, dh);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(b->hev[slot][1], c->stream2));
     }
     if (c->k3_block) {
+        // persistent: as many workgroups as fit the device at this LDS budget,
+        // each taking the next problem (heaviest first) from a counter -- a
+        // free slot on any CU takes the next problem, instead of the problem
+        // dispatch order binding workgroups to XCDs round-robin
         pf_dev_batch dl = d;
         dl.k3_order = d.k3_order + nh;
-        if (2 * b->W > nh)
-            hipLaunchKernelGGL(pf_k3_greedy, dim3(2 * b->W - nh), dim3(PF_K3S_THREADS), d.lds_bytes, st, dl);
+        dl.k3_n = 2 * b->W - nh;
+        if (dl.k3_n) {
+            const uint32_t g = std::min<uint32_t>(dl.k3_n, k3_resident(c, d.lds_bytes));
+            hipLaunchKernelGGL(pf_k3_greedy, dim3(g), dim3(PF_K3S_THREADS), d.lds_bytes, st, dl);
+        }
     } else
         hipLaunchKernelGGL(pf_k3_wave, dim3(2 * b->W), dim3(64), d.lds_w, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][5], st));
-    // deferred problems (usually none): a grid-stride kernel over the main kernel's list
+    // the main kernel's deferred problems (usually none): a grid-stride kernel over its list
+    HIPCHK(hipEventRecord(b->fev[slot][0], st));
     hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_fb,
                        st, d);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(b->fev[slot][1], st));
     HIPCHK(hipEventRecord(b->ev[slot][6], st));
     if (nh) HIPCHK(hipStreamWaitEvent(st, b->hev[slot][1], 0));   // join: the heavy problems are done
     b->heavy_launched[slot] = nh != 0;
@@ -1162,6 +1235,7 @@ extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_
         if (b->W) {
             for (int i = 0; i < PF_NKERN; i++)
                 (void)hipEventElapsedTime(&c->last_ms[i], b->ev[slot][i], b->ev[slot][i + 1]);
+            (void)hipEventElapsedTime(&c->last_ms[PF_NKERN - 1], b->fev[slot][0], b->fev[slot][1]);
             c->heavy_ms = -1.0f;
             if (b->heavy_launched[slot]) (void)hipEventElapsedTime(&c->heavy_ms, b->hev[slot][0], b->hev[slot][1]);
             (void)hipGetLastError();               // a failed timing query must not fail a later launch check
@@ -1169,8 +1243,8 @@ extern "C" int pf_methphase_finish(pf_ctx_t *ctx, pf_dbatch_t *b, pf_window_out_
         }
         const uint32_t stt = b->W ? v.status[0] : 0;
         if (getenv("PF_DEBUG_FALLBACK"))
-            fprintf(stderr, "[D::pomfret_amd] status 0x%x, K2 fallback reads %u, K3 deferred problems %u\n", stt,
-                    *v.fb, *v.k3fb);
+            fprintf(stderr, "[D::pomfret_amd] status 0x%x, K2 fallback reads %u, K3 deferred problems %u (+%u heavy)\n",
+                    stt, *v.fb, *v.k3fb, *v.k3fbh);
         const int s = settle_status(b, stt, v, attempt);
         if (s < 0) return s;
         if (s == 0) break;

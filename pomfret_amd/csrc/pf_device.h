@@ -59,6 +59,8 @@ struct pf_dev_batch {
     const uint32_t *k3_order;          /* [2W] greedy problems (w<<1|dir), heaviest first */
     const uint32_t *k12_order;         /* [W] windows for K12's workgroups, heaviest first */
     uint32_t *k3_fb_list, *k3_fb_ctr;  /* problems the main greedy kernel defers to pf_k3_fallback */
+    uint32_t *k3_next;                 /* the persistent main greedy kernel's next problem (rank in k3_order) */
+    uint32_t k3_n;                     /* its problems: k3_order[0, k3_n) */
     uint32_t *site_pos, *st1_pos, *site_q1;
     uint8_t *len0, *len1;
     uint32_t *rev_ord;                 /* [R] window-local read index, ascending (end, idx) */
@@ -78,11 +80,13 @@ struct pf_dev_batch {
     unsigned long long *prof;          /* [W*2*8] diagnostic build only */
     uint32_t lds_bytes;                /* dynamic LDS of the main greedy kernel */
     uint32_t lds_fb;                   /* dynamic LDS of the fallback greedy kernel (>= lds_bytes) */
+    uint32_t lds_heavy;                /* dynamic LDS of pf_k3_heavy (the heavy problems' slim loop) */
     uint32_t lds_w;                    /* dynamic LDS of the one-wave greedy kernel */
     uint32_t k12_capw, k12_smax;       /* fused methmer phase limits (test overrides) */
     uint32_t k12_dense;                /* 1: every window takes K12's dense (HBM) site path (tests) */
     uint32_t k2_entcap;                /* fallback reads above this bound use HBM scratch */
     uint32_t k3_mode;                  /* test override: 0 exact pick, 1 always fold, 2 chunked record rows */
+    uint32_t k3_cache;                 /* 1: candidate slot-list cache when a window's lists miss LDS (PF_K3_CACHE=0: off) */
 };
 
 #endif

@@ -50,6 +50,12 @@ DEV unsigned long long k3_stamp_now() {
 }
 #define K3_STAMP(i) do { const unsigned long long t_ = k3_stamp_now(); \
     prof_acc[i] += t_ - prof_last; prof_last = t_; } while (0)
+// the chip-wide constant-rate clock (100 MHz), for the problems' start/end times
+DEV unsigned long long k3_realtime() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    return t;
+}
 #define K3_COUNT(i, v) do { prof_acc[i] += (v); } while (0)
 #define K12_STAMP(i) do { if (threadIdx.x == 0) { const unsigned long long t_ = k3_stamp_now(); \
     d.prof[64ull * d.W + (uint64_t)w * 16 + (i)] = t_ - k12_t0; k12_t0 = t_; } } while (0)
@@ -1243,6 +1249,7 @@ struct K3Ctl {
     uint32_t S, R, ntot, nc, L, done, failed, inserted, winner, tag;
     int32_t i_last;
     uint32_t min_i, max_i, fail, summ, nstrict, mxlen, cmax;
+    uint32_t path, need;                      // (profile build) the P2 variant taken and its LDS bytes
     uint32_t ins_n, ins_st, ins_mo, ins_tg;   // register variant: winner whose insert is pending
     unsigned long long scr;
     int32_t tab[4];
@@ -1256,6 +1263,16 @@ struct K3Cand {
     uint32_t kofs[PF_MAX_NCAND];
     unsigned long long key[PF_MAX_NCAND];
     uint8_t tag[PF_MAX_NCAND];
+};
+
+// the slim loop's static LDS (k3_greedy_slim): the per-wave queue scratch
+// (64 entries per wave), the push/positive count pairs [2][64] and the exact
+// hap sums [2][2][64] -- 3.5 KB instead of K3Cand's 7.2 KB, so more problems
+// fit a CU beside their dynamic budget
+struct K3CandSlim {
+    uint32_t read[PF_K3S_THREADS];
+    uint32_t pos[128];
+    unsigned long long key[256];
 };
 
 DEV uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
@@ -1325,8 +1342,13 @@ DEV void k3_dict_rewrite(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_
 }
 
 struct K3Mem {
-    uint32_t *sum, *cnt, *aux, *ord, *mn, *mst, *mo;
-    float4 *srec;            // per-site divisor cache (register variant)
+    uint32_t *sum, *cnt, *aux, *mo;
+    void *mn, *mst;          // methmers per read, first site index: u16 when m16 (the slim loop: S < 8192), else u32
+    bool m16;
+    uint16_t *ord;           // dir-1 scan order (window-local read indices, R < 2^16)
+    const uint64_t *gmo;     // mo == nullptr: the reads' key offsets in HBM (d.mmr_off, stride 2), minus kbase
+    const uint32_t *gmn, *gmst;   // mn == nullptr: the reads' methmer counts / first sites in HBM (stride 2)
+    uint64_t kbase;
     uint8_t *hp, *flg;
     uint64_t *untag;
     uint16_t *sl16;          // slot lists in LDS (u16), when they fit
@@ -1338,46 +1360,68 @@ struct K3Mem {
 
 #define K3_NOFF 13
 // P2 byte layout.  Returns the bytes needed with `rcw` records per wave;
-// slots (u16) are included only when with_slots.
+// slots (u16) are included only when with_slots, the per-read slot-list
+// offsets only when with_mo (the candidate cache reads them from HBM), and
+// aux_b bytes of T5 scratch (4R, or 0 when it lives in the cache region).
+// No per-site divisor cache: a term's divisor is its site's hap total, and
+// its reciprocal is taken beside the dependent count load.
 DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint32_t summ,
-                       bool with_slots, uint32_t rcw, uint64_t off[K3_NOFF], bool c8 = false) {
+                       bool with_slots, uint32_t rcw, uint64_t off[K3_NOFF], bool c8 = false, bool with_mo = true,
+                       uint64_t aux_b = ~0ull, bool with_mnst = true) {
     const uint32_t nwords = (R + 63) >> 6;
     off[0] = 0;                                        // sum   S*4
     off[1] = align16(off[0] + 4ull * S);               // cnt   ntot*4
     off[2] = align16(off[1] + (c8 ? 2ull : 4ull) * ntot);   // hp    R (cnt: u8 pairs when c8)
     off[3] = align16(off[2] + R);                      // flg   R
-    off[4] = align16(off[3] + R);                      // ord   R*4 (dir 1)
-    off[5] = align16(off[4] + (dir ? 4ull * R : 0));   // untag nwords*8
-    off[6] = align16(off[5] + 8ull * nwords);          // mn    R*4  methmers per read
-    off[7] = align16(off[6] + 4ull * R);               // mst   R*4  first site index
-    off[8] = align16(off[7] + 4ull * R);               // mo    R*4  slot-list offset
-    off[9] = align16(off[8] + 4ull * R);               // sl16  summ*2 (optional)
-    off[10] = align16(off[9] + (with_slots ? 2ull * summ : 0));   // srec  S*16
-    off[11] = off[10] + 16ull * S;                                 // records / aux
+    off[4] = align16(off[3] + R);                      // ord   R*2 (dir 1)
+    off[5] = align16(off[4] + (dir ? 2ull * R : 0));   // untag nwords*8
+    const uint64_t mw = !with_mnst ? 0ull : S < 8192u ? 2ull : 4ull;   // (u16 when every index fits: see k3_mem)
+    off[6] = align16(off[5] + 8ull * nwords);          // mn    R*2|4  methmers per read
+    off[7] = align16(off[6] + mw * R);                 // mst   R*2|4  first site index
+    off[8] = align16(off[7] + mw * R);                 // mo    R*4  slot-list offset (optional)
+    off[9] = align16(off[8] + (with_mo ? 4ull * R : 0));   // sl16  summ*2 (optional)
+    off[10] = align16(off[9] + (with_slots ? 2ull * summ : 0));
+    off[11] = off[10];                                 // records / aux
     const uint64_t rec = 12ull * PF_K3_WAVES * rcw;
-    const uint64_t aux = 4ull * R;
+    const uint64_t aux = aux_b == ~0ull ? 4ull * R : aux_b;
     off[12] = off[11] + (rec > aux ? rec : aux);
     return off[12];
 }
 
 DEV void k3_mem(uint8_t *base, const uint64_t off[K3_NOFF], uint32_t rcw, bool with_slots,
-                const uint32_t *kb, K3Mem &m) {
+                const uint32_t *kb, K3Mem &m, bool with_mo = true, uint32_t S = 0xFFFFFFFFu, bool with_mnst = true) {
     m.sum = reinterpret_cast<uint32_t *>(base + off[0]);
     m.cnt = reinterpret_cast<uint32_t *>(base + off[1]);
     m.hp = base + off[2];
     m.flg = base + off[3];
-    m.ord = reinterpret_cast<uint32_t *>(base + off[4]);
+    m.ord = reinterpret_cast<uint16_t *>(base + off[4]);
     m.untag = reinterpret_cast<uint64_t *>(base + off[5]);
-    m.mn = reinterpret_cast<uint32_t *>(base + off[6]);
-    m.mst = reinterpret_cast<uint32_t *>(base + off[7]);
-    m.mo = reinterpret_cast<uint32_t *>(base + off[8]);
+    m.mn = with_mnst ? base + off[6] : nullptr;
+    m.mst = with_mnst ? base + off[7] : nullptr;
+    m.gmn = m.gmst = nullptr;
+    m.m16 = S < 8192u;
+    m.mo = with_mo ? reinterpret_cast<uint32_t *>(base + off[8]) : nullptr;
+    m.gmo = nullptr;
+    m.kbase = 0;
     m.sl16 = with_slots ? reinterpret_cast<uint16_t *>(base + off[9]) : nullptr;
     m.kb = kb;
-    m.srec = reinterpret_cast<float4 *>(base + off[10]);
     m.recv = reinterpret_cast<float2 *>(base + off[11]);
     m.recc = reinterpret_cast<uint32_t *>(base + off[11] + 8ull * PF_K3_WAVES * rcw);
     m.aux = reinterpret_cast<uint32_t *>(base + off[11]);
     m.rcw = rcw;
+}
+
+DEV uint32_t k3_mn(const K3Mem &m, uint32_t i) {
+    if (!m.mn) return m.gmn[2ull * i];
+    return m.m16 ? (uint32_t)static_cast<const uint16_t *>(m.mn)[i] : static_cast<const uint32_t *>(m.mn)[i];
+}
+DEV uint32_t k3_mst(const K3Mem &m, uint32_t i) {
+    if (!m.mst) return m.gmst[2ull * i];
+    return m.m16 ? (uint32_t)static_cast<const uint16_t *>(m.mst)[i] : static_cast<const uint32_t *>(m.mst)[i];
+}
+// a read's slot-list offset in the HBM key arena (window base)
+DEV uint32_t k3_mo(const K3Mem &m, uint32_t rd) {
+    return m.mo ? m.mo[rd] : (uint32_t)(m.gmo[2ull * rd] - m.kbase);
 }
 
 #define FLG_LEFT 1u
@@ -1520,9 +1564,9 @@ DEV uint32_t k3_qbuild(const K3Mem &m, uint32_t nwords, int p, uint32_t dir, uin
     if (lane < cnt) {
         q_pos = qbuf[lane];
         q_rd = dir ? m.ord[q_pos] : q_pos;
-        q_n = m.mn[q_rd];
-        q_st = m.mst[q_rd];
-        q_mo = m.mo[q_rd];
+        q_n = k3_mn(m, q_rd);
+        q_st = k3_mst(m, q_rd);
+        q_mo = k3_mo(m, q_rd);
     }
     if (tot > 64) cont = (int)qbuf[63];
     else cont = dir == 0 ? (w0 + 64) * 64 - 1 : (w0 - 63) * 64;
@@ -1539,14 +1583,14 @@ DEV void k3_cand_fields(const K3Mem &m, uint32_t nc, uint32_t dir, uint32_t lane
     uint32_t lsum = 0;
     for (uint32_t c = lane; c < nc; c += 64) {
         const uint32_t rd = cd.read[c];
-        const uint32_t n = m.mn[rd], st = m.mst[rd];
+        const uint32_t n = k3_mn(m, rd), st = k3_mst(m, rd);
         const uint64_t lo = st > mn_ ? st : mn_;
         const uint64_t hi0 = (uint64_t)st + n;
         const uint64_t hi = hi0 < mx_ ? hi0 : mx_;
         const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0;
         cd.site0[c] = (uint32_t)lo;
         cd.len[c] = len;
-        cd.kofs[c] = m.mo[rd] + (len ? (uint32_t)(lo - st) : 0);
+        cd.kofs[c] = k3_mo(m, rd) + (len ? (uint32_t)(lo - st) : 0);
         lsum += len;
     }
     // lookups statistic: a wave sum without shuffles (ballot bit-slices)
@@ -1653,14 +1697,13 @@ DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
     for (uint32_t tb = tstart; tb < tpad; tb += 4 * step) {
         // unconditional loads (out-of-span lanes read entry 0 and are masked
         // afterwards)
-        uint32_t sl[4], cv[4];
-        float4 sr[4];
+        uint32_t sl[4], cv[4], sv[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const uint32_t t = tb + u * step;
             const bool ok = t < tend;
             sl[u] = k3_slot_raw<SLDS>(m, ok ? f_kofs + t : 0u);
-            sr[u] = m.srec[ok ? f_lo + t : 0u];
+            sv[u] = m.sum[ok ? f_lo + t : 0u];
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1673,11 +1716,12 @@ DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
         for (int u = 0; u < 4; u++) {
             const uint32_t t = tb + u * step;
             const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
+            const uint32_t h0 = sv[u] & 0xffffu, h1 = sv[u] >> 16;
             // key present at this site (inserted at least once) and sum != 0:
             // pushed; cnt > 0: positive (blockjoin.c:3505-3509, :3619-3624)
-            const bool p0 = cv[u] != 0 && sr[u].z != 0.f, p1 = cv[u] != 0 && sr[u].w != 0.f;
-            const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
-            const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
+            const bool p0 = cv[u] != 0 && h0 != 0, p1 = cv[u] != 0 && h1 != 0;
+            const float q0 = div_u16_y((float)a0, (float)h0, h0 ? __builtin_amdgcn_rcpf((float)h0) : 0.f);
+            const float q1 = div_u16_y((float)a1, (float)h1, h1 ? __builtin_amdgcn_rcpf((float)h1) : 0.f);
             lcode += (p0 ? 1u + (a0 ? 1u : 0u) : 0u) + ((p1 ? 1u + (a1 ? 1u : 0u) : 0u) << 16);
             if (t < tpad) row[t] = make_float2(q0, q1);
             e0 += (double)q0;                        // exact: see k3_pick_exact
@@ -1690,12 +1734,10 @@ DEV uint32_t k3_fill_rows(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
 #define K3_FADD(acc, x) asm("v_add_f32 %0, %0, %1" : "+v"(acc) : "v"(x))
 
 // insert_mmr_counts of one tagged read (hap tg) by the whole workgroup: its
-// sites are distinct, so a plain read-modify-write per site; only hap tg's
-// divisor entry changes (its total becomes >= 1, so no zero case)
+// sites are distinct, so a plain read-modify-write per site
 template <bool SLDS, int NT = PF_K3_THREADS, bool C8 = false>
 DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint32_t mo, uint32_t tg) {
-    const uint32_t inc = tg ? 0x10000u : 1u, sh = tg ? 16u : 0u;
-    float *srf = reinterpret_cast<float *>(m.srec) + tg;   // (h_tg, -, 1/h_tg, -) of site 0
+    const uint32_t inc = tg ? 0x10000u : 1u;
     for (uint32_t tb = 0; tb < n; tb += 2 * NT) {
         uint32_t sl[2], cc[2], sv[2];
         bool ok[2];
@@ -1717,13 +1759,9 @@ DEV void k3_insert_all(const K3Mem &m, uint32_t S, uint32_t n, uint32_t st, uint
         for (int u = 0; u < 2; u++) {
             if (ok[u]) {
                 const uint32_t site = st + tb + u * NT + threadIdx.x;
-                const uint32_t s2 = sv[u] + inc;
-                const float f = (float)((s2 >> sh) & 0xffffu);
                 if (C8) reinterpret_cast<uint16_t *>(m.cnt)[sl[u]] = (uint16_t)(cc[u] + (tg ? 0x100u : 1u));
                 else m.cnt[sl[u]] = cc[u] + inc;
-                m.sum[site] = s2;
-                srf[4 * site] = f;
-                srf[4 * site + 2] = __builtin_amdgcn_rcpf(f);
+                m.sum[site] = sv[u] + inc;
             }
         }
     }
@@ -1738,14 +1776,13 @@ DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
                           uint32_t step, double &e0, double &e1) {
     uint32_t lcode = 0;
     for (uint32_t tb = tstart; tb < tend; tb += 4 * step) {
-        uint32_t sl[4], cv[4];
-        float4 sr[4];
+        uint32_t sl[4], cv[4], sv[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const uint32_t t = tb + u * step;
             const bool ok = t < tend;
             sl[u] = k3_slot_raw<SLDS>(m, ok ? f_kofs + t : 0u);
-            sr[u] = m.srec[ok ? f_lo + t : 0u];
+            sv[u] = m.sum[ok ? f_lo + t : 0u];
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1757,16 +1794,17 @@ DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const uint32_t a0 = cv[u] & 0xffffu, a1 = cv[u] >> 16;
-            const float q0 = div_u16_y((float)a0, sr[u].x, sr[u].z);
-            const float q1 = div_u16_y((float)a1, sr[u].y, sr[u].w);
+            // the divisors: the site's hap totals (0 -> a zero reciprocal, so 0/h = 0)
+            const uint32_t h0 = sv[u] & 0xffffu, h1 = sv[u] >> 16;
+            const float q0 = div_u16_y((float)a0, (float)h0, h0 ? __builtin_amdgcn_rcpf((float)h0) : 0.f);
+            const float q1 = div_u16_y((float)a1, (float)h1, h1 ? __builtin_amdgcn_rcpf((float)h1) : 0.f);
             // push/positive counts (:3505-3509, :3619-3624): pushed = key present
-            // (cv != 0) and hap total != 0 (its cached reciprocal is then
-            // nonzero); positive = cnt > 0, which implies pushed.  Both haps
-            // packed per u32 half: min(cnt, 1) in one v_pk_min_u16.
-            uint32_t posc;
+            // (cv != 0) and hap total != 0; positive = cnt > 0, which implies
+            // pushed.  Both haps packed per u32 half: min(cnt, 1) and
+            // min(total, 1) in one v_pk_min_u16 each.
+            uint32_t posc, hm;
             asm("v_pk_min_u16 %0, %1, %2" : "=v"(posc) : "v"(cv[u]), "s"(0x00010001u));
-            const uint32_t hz = __float_as_uint(sr[u].z), hw = __float_as_uint(sr[u].w);
-            const uint32_t hm = (hz < 1u ? hz : 1u) | ((hw < 1u ? hw : 1u) << 16);
+            asm("v_pk_min_u16 %0, %1, %2" : "=v"(hm) : "v"(sv[u]), "s"(0x00010001u));
             lcode += posc + (cv[u] ? hm : 0u);
             e0 += (double)q0;
             e1 += (double)q1;
@@ -1781,22 +1819,22 @@ DEV uint32_t k3_fill_sums(const K3Mem &m, uint32_t f_lo, uint32_t f_kofs, uint32
 template <bool SLDS, bool C8 = false>
 DEV void k3_fold_direct(const K3Mem &m, uint32_t lo, uint32_t kofs, uint32_t len, float &s0, float &s1) {
     for (uint32_t t0 = 0; t0 < len; t0 += 8) {
-        uint32_t sl[8];
-        float4 sr[8];
+        uint32_t sl[8], sv[8];
         float q0[8], q1[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const uint32_t t = t0 + u;
             const bool ok = t < len;
             sl[u] = k3_slot_raw<SLDS>(m, ok ? kofs + t : 0u);
-            sr[u] = m.srec[ok ? lo + t : 0u];
+            sv[u] = m.sum[ok ? lo + t : 0u];
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             const bool ok = t0 + u < len && sl[u] != (SLDS ? 0xFFFFu : PF_NONE);
             const uint32_t c = ok ? k3_cnt_get<C8>(m, sl[u]) : 0u;
-            q0[u] = div_u16_y((float)(c & 0xffffu), sr[u].x, sr[u].z);
-            q1[u] = div_u16_y((float)(c >> 16), sr[u].y, sr[u].w);
+            const uint32_t h0 = sv[u] & 0xffffu, h1 = sv[u] >> 16;
+            q0[u] = div_u16_y((float)(c & 0xffffu), (float)h0, h0 ? __builtin_amdgcn_rcpf((float)h0) : 0.f);
+            q1[u] = div_u16_y((float)(c >> 16), (float)h1, h1 ? __builtin_amdgcn_rcpf((float)h1) : 0.f);
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -1888,12 +1926,19 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
         m.flg[i] = (uint8_t)f;
         m.hp[i] = d.read_hp[r];
         m.aux[i] = 0;
-        if (dir) m.ord[i] = d.rev_ord[r];
+        if (dir) m.ord[i] = (uint16_t)d.rev_ord[r];
         const uint64_t g = 2ull * r + dir;
-        m.mn[i] = d.mmr_n[g];
-        m.mst[i] = d.mmr_start[g];
-        sum_mmr += m.mn[i];
-        mx_mmr = m.mn[i] > mx_mmr ? m.mn[i] : mx_mmr;
+        const uint32_t n_ = d.mmr_n[g], st_ = d.mmr_start[g];
+        if (!m.mn) {
+        } else if (m.m16) {
+            static_cast<uint16_t *>(m.mn)[i] = (uint16_t)n_;
+            static_cast<uint16_t *>(m.mst)[i] = (uint16_t)st_;
+        } else {
+            static_cast<uint32_t *>(m.mn)[i] = n_;
+            static_cast<uint32_t *>(m.mst)[i] = st_;
+        }
+        sum_mmr += n_;
+        mx_mmr = n_ > mx_mmr ? n_ : mx_mmr;
     }
     if (tid == 0) {
         const uint32_t *a = d.site_pos + sb;
@@ -1915,7 +1960,7 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
         uint32_t carry = 0;
         for (uint32_t i0 = 0; i0 < R; i0 += NT) {
             const uint32_t i = i0 + tid;
-            const uint32_t v = i < R ? m.mn[i] : 0;
+            const uint32_t v = i < R ? k3_mn(m, i) : 0;
             uint32_t tot;
             const uint32_t ex = block_excl_scan<NT>(v, sh_scan, &tot);
             if (i < R) m.mo[i] = carry + ex;
@@ -1926,13 +1971,13 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
             const uint32_t g = 2 * (r0 + i) + dir;
             const uint32_t *src = kb + (d.mmr_off[g] - kbase);
             uint16_t *dst = m.sl16 + m.mo[i];
-            const uint32_t n = m.mn[i];
+            const uint32_t n = k3_mn(m, i);
             for (uint32_t t = lane; t < n; t += 64) {
                 const uint32_t v = src[t];
                 dst[t] = v == PF_NONE ? (uint16_t)0xFFFFu : (uint16_t)v;
             }
         }
-    } else {
+    } else if (m.mo) {
         for (uint32_t i = tid; i < R; i += NT)
             m.mo[i] = (uint32_t)(d.mmr_off[2ull * (r0 + i) + dir] - kbase);
     }
@@ -1943,7 +1988,7 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
     for (uint32_t i = wid; i < R; i += (NT / 64)) {
         const uint32_t hp = m.hp[i];
         if (!(m.flg[i] & refbit) || hp > 1) continue;
-        const uint32_t n = m.mn[i], st = m.mst[i], mo = m.mo[i];
+        const uint32_t n = k3_mn(m, i), st = k3_mst(m, i), mo = SLDS ? m.mo[i] : k3_mo(m, i);
         const uint32_t inc = hp ? 0x10000u : 1u;
         ref_ins += n;
         for (uint32_t t = lane; t < n; t += 64) {
@@ -1960,7 +2005,6 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
     if (sum_mmr) atomicAdd(&ctl.summ, sum_mmr);
     if (mx_mmr) atomicMax(&ctl.mxlen, mx_mmr);
     __syncthreads();
-    for (uint32_t j = tid; j < S; j += NT) m.srec[j] = site_rec(m.sum[j]);
     if (wid == 0) k3_range_update(m.sum, S, cov_rt, ctl, lane);
     // ---- step 1.5 (:4010-4025): all reads unphased, ref reads restored through
     // the (readID<<2)|hp round trip (hp >= 4 lands on readID|(hp>>2)); the last
@@ -2071,9 +2115,19 @@ DEV void k3_range_regs(const K3Mem &m, uint32_t S, int cov_rt, uint32_t lane, ui
 // redundantly -- identical register copies of the candidate list, the queue
 // and the range -- so nothing is published between waves; two barriers per
 // iteration: after the term fill (B) and after the winner's insert (X).
-template <bool SLDS, int NT = PF_K3_THREADS, bool C8 = false>
+//
+// CACHE: the window's slot lists do not fit LDS, so instead of reading them
+// from the HBM key arena in every fill and insert, the candidates' own lists
+// live in an LDS cache of n_cand + 1 slots of CL entries (u16, CL = the
+// longest list of the problem): a candidate's slot index rides in its lane
+// (c_cs), free slots in a wave-uniform mask.  The read the list appends in
+// this iteration is known at its top, so its list is loaded from HBM there
+// and stored into the free slot before the closing barrier -- the load's
+// latency hides behind the fill, the pick and the insert.  (The slots of a
+// fresh candidate list are filled in one cooperative copy.)
+template <bool SLDS, int NT = PF_K3_THREADS, bool C8 = false, bool CACHE = false, typename CD = K3Cand>
 DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, uint32_t S, uint32_t R,
-                        const K3Mem &m, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan, uint32_t *qb) {
+                        const K3Mem &m, K3Ctl &ctl, CD &cd, uint32_t *sh_scan, uint32_t *qb, uint32_t CL = 0) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
     const int cov_rt = d.win_par[w * 4 + 1];
     const uint32_t NC = (uint32_t)d.win_par[w * 4 + 2];
@@ -2082,14 +2136,18 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
 #ifdef PF_K3_PROFILE
     unsigned long long prof_acc[32] = {0};
     unsigned long long prof_last = k3_stamp_now();
+    prof_acc[24] = k3_realtime();
 #endif
-    k3_init<SLDS, NT, C8>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
+    k3_init<SLDS && !CACHE, NT, C8>(d, w, dir, r0, S, R, m, ctl, sh_scan, stx);
     K3_STAMP(0);
     int il = uni_i(ctl.i_last);
     uint32_t failed = 0;
     uint32_t umin = uni(ctl.min_i), umax = uni(ctl.max_i);
     uint32_t nc = 0;
     uint32_t c_pos = 0, c_rd = 0, c_n = 0, c_st = 0, c_mo = 0;
+    uint32_t c_cs = 0;                                   // CACHE: the candidate's cache slot
+    uint64_t fmask = 0;                                  // CACHE: free cache slots (wave-uniform)
+    const uint32_t NCS = NC + 1;
     uint32_t q_pos = 0, q_rd = 0, q_nn = 0, q_st = 0, q_mo = 0;
     uint32_t q_cnt = 0, q_head = 0;
     bool q_more = false;
@@ -2142,6 +2200,21 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             }
             if (done) break;
             need_collect = false;
+            if (CACHE) {
+                // a fresh list: candidate c in cache slot c; every list copied
+                // by the workgroup (wave v takes candidates v, v + NT/64, ...)
+                c_cs = lane;
+                fmask = (NCS >= 64 ? ~0ull : ((1ull << NCS) - 1ull)) & (nc >= 64 ? 0ull : ~((1ull << nc) - 1ull));
+                for (uint32_t c = wid; c < nc; c += NT / 64) {
+                    const uint32_t n_ = rdl(c_n, c), ko = rdl(c_mo, c);
+                    uint16_t *dst = m.sl16 + c * CL;
+                    for (uint32_t t = lane; t < n_; t += 64) {
+                        const uint32_t v = m.kb[ko + t];
+                        dst[t] = v == PF_NONE ? (uint16_t)0xFFFFu : (uint16_t)v;
+                    }
+                }
+                __syncthreads();
+            }
         }
         // ---- the next untagged read after the list, for this iteration's append
         int qn = -1;
@@ -2159,6 +2232,13 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 q_head++;
             }
         }
+        // CACHE: the appended read's list, loaded now, stored before (X)
+        uint32_t pf0 = PF_NONE, pf1 = PF_NONE, s_sp = 0;
+        if (CACHE && qn >= 0) {
+            s_sp = (uint32_t)__ffsll((unsigned long long)fmask) - 1u;
+            if (tid < q_n1) pf0 = m.kb[q_mo1 + tid];
+            if (tid + NT < q_n1) pf1 = m.kb[q_mo1 + tid + NT];
+        }
         // ---- lookup spans: sites in [min_i, max_i) (query_counts_of_mmrs, :3500-3501)
         uint32_t c_len, c_lo, c_kofs;
         {
@@ -2167,7 +2247,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             const uint32_t hi = hi0 < umax ? hi0 : umax;
             c_len = lane < nc && hi > lo && umin != 0xFFFFFFFFu ? hi - lo : 0;
             c_lo = lo;
-            c_kofs = c_mo + (c_len ? lo - c_st : 0);
+            c_kofs = (CACHE ? c_cs * CL : c_mo) + (c_len ? lo - c_st : 0);
         }
         lsum += c_len;
         if (nc >= NC) {
@@ -2244,7 +2324,8 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             continue;
         }
         // ---- the winner: tag, list minus the winner plus the queued read
-        const uint32_t rd = rdl(c_rd, cw), n = rdl(c_n, cw), st = rdl(c_st, cw), mo = rdl(c_mo, cw);
+        const uint32_t rd = rdl(c_rd, cw), n = rdl(c_n, cw), st = rdl(c_st, cw);
+        const uint32_t mo = CACHE ? rdl(c_cs, cw) * CL : rdl(c_mo, cw);
         const uint32_t pw = rdl(c_pos, cw);
         stx.inserts += n;
         if (wid == 0 && lane == 0) {
@@ -2252,16 +2333,19 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             m.untag[pw >> 6] &= ~(1ull << (pw & 63));
         }
         failed = 0;
+        if (CACHE) fmask |= 1ull << (mo / CL);           // the winner's slot: free after this insert
         {
             const int src = (int)lane + 1;
             const uint32_t a0 = (uint32_t)__shfl((int)c_pos, src, 64), a1 = (uint32_t)__shfl((int)c_rd, src, 64);
             const uint32_t a2 = (uint32_t)__shfl((int)c_n, src, 64), a3 = (uint32_t)__shfl((int)c_st, src, 64);
             const uint32_t a4 = (uint32_t)__shfl((int)c_mo, src, 64);
-            if (lane >= cw) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; }
+            const uint32_t a5 = CACHE ? (uint32_t)__shfl((int)c_cs, src, 64) : 0u;
+            if (lane >= cw) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; c_cs = a5; }
         }
         uint32_t ncn = nc - 1;
         if (qn >= 0) {
-            if (lane == ncn) { c_pos = (uint32_t)qn; c_rd = q_rd1; c_n = q_n1; c_st = q_st1; c_mo = q_mo1; }
+            if (lane == ncn) { c_pos = (uint32_t)qn; c_rd = q_rd1; c_n = q_n1; c_st = q_st1; c_mo = q_mo1; c_cs = s_sp; }
+            if (CACHE) fmask &= ~(1ull << s_sp);
             ncn++;
         }
         nc = ncn;
@@ -2271,6 +2355,12 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         // wave's fold, if the pick needed one, has read the tables)
         if (folded) __syncthreads();
         k3_insert_all<SLDS, NT, C8>(m, S, n, st, mo, tg);
+        if (CACHE && qn >= 0) {
+            // the appended read's list into its (free until now) cache slot
+            uint16_t *dst = m.sl16 + s_sp * CL;
+            if (tid < q_n1) dst[tid] = pf0 == PF_NONE ? (uint16_t)0xFFFFu : (uint16_t)pf0;
+            if (tid + NT < q_n1) dst[tid + NT] = pf1 == PF_NONE ? (uint16_t)0xFFFFu : (uint16_t)pf1;
+        }
         have_win = true;
         K3_STAMP(21);
         __syncthreads();                                           // (X)
@@ -2287,6 +2377,10 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
 #ifdef PF_K3_PROFILE
     if (lane == 0) {
         unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 32;
+        prof_acc[29] = ctl.path;
+        prof_acc[25] = k3_realtime();
+        prof_acc[30] = ctl.ntot;
+        prof_acc[31] = ctl.need;
         for (int i = 0; i < 32; i++) pp[i] = prof_acc[i];
     }
 #endif
@@ -2824,7 +2918,7 @@ DEV void k3_greedy_body(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
             const uint32_t rd = cd.read[cw];
             const uint32_t tg = cd.tag[cw];
             const uint32_t pw = cd.pos[cw];
-            const uint32_t n = m.mn[rd], st = m.mst[rd], mo = m.mo[rd];
+            const uint32_t n = k3_mn(m, rd), st = k3_mst(m, rd), mo = k3_mo(m, rd);
             const uint32_t inc = tg ? 0x10000u : 1u;
             stx.inserts += n;
             // the sites of one read are distinct: plain read-modify-write
@@ -2901,8 +2995,8 @@ DEV void k3_defer(const pf_dev_batch &d, uint32_t prob) {
 // false is the main kernel's slim build: slot dictionary and lists in LDS,
 // n_cand <= 64 (register candidate list), < 8192 sites (exact-interval pick
 // only); anything else is deferred to the FULL build.
-template <bool FULL, int NT = PF_K3_THREADS>
-DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl, K3Cand &cd, uint32_t *sh_scan,
+template <bool FULL, int NT = PF_K3_THREADS, typename CD = K3Cand>
+DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl, CD &cd, uint32_t *sh_scan,
                 const uint32_t lds, uint32_t *qb = nullptr) {
     // qb: per-wave queue scratch of the slim loop, 64 entries per wave; the
     // kernels that pass none (fallback, heavy: 256 threads) use cd.read
@@ -2955,9 +3049,14 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     }
     k3_dict<NT>(d, r0, R, S, dir, masks, mbase, sh_scan, ctl);
     const uint32_t ntot = uni(ctl.ntot);
-    // sum of methmers over the window's reads (slot-list size)
-    uint32_t summ = 0;
-    for (uint32_t i = tid; i < R; i += NT) summ += d.mmr_n[2ull * (r0 + i) + dir];
+    // sum of methmers over the window's reads (slot-list size) and the longest list
+    uint32_t summ = 0, lmx = 0;
+    for (uint32_t i = tid; i < R; i += NT) {
+        const uint32_t n_ = d.mmr_n[2ull * (r0 + i) + dir];
+        summ += n_;
+        lmx = n_ > lmx ? n_ : lmx;
+    }
+    if (lmx) atomicMax(&ctl.mxlen, lmx);
     uint32_t summ_tot;
     block_excl_scan<NT>(summ, sh_scan, &summ_tot);
 
@@ -2999,26 +3098,56 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     }
     const uint64_t slim_s = k3_layout(S, ntot, R, dir, summ_tot, true, 0, off, c8);
     const uint64_t slim_n = k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8);
-    const bool slim_fit = slim_ok && ((slots_ok && slim_s <= lds) || slim_n <= lds);
+    // the candidate slot-list cache (k3_greedy_slim CACHE) when the window's
+    // lists do not fit: n_cand + 1 slots of the longest list, u16 entries
+    const uint32_t CL = (uni(ctl.mxlen) + 1u) & ~1u;
+    const uint32_t NCc = (uint32_t)d.win_par[w * 4 + 2];
+    const bool cache_ok = slim_ok && slots_ok && NCc <= 63u && CL > 0 && CL <= 2u * NT && d.k3_cache != 0u;
+    // no per-read slot-list offsets (the cache copies from HBM), and the T5
+    // scratch of k3_init inside the cache region when it is large enough
+    const uint64_t cache_b = 2ull * (NCc + 1) * CL;
+    const bool aux_in_cache = cache_b >= 4ull * R;
+    const uint64_t slim_cn =
+        k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, aux_in_cache ? 0 : 4ull * R, false);
+    const uint64_t slim_c = align16(slim_cn) + cache_b;
+    const bool slim_fit = slim_ok && ((slots_ok && slim_s <= lds) || (cache_ok && slim_c <= lds) || slim_n <= lds);
     if (!FULL && !slim_fit) {
         k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
         return;
     }
     k3_dict_rewrite<NT>(d, r0, R, S, dir, masks, mbase);
     const uint32_t *kb = d.keys + kbase;
+#ifdef PF_K3_PROFILE
+    if (tid == 0) {
+        // 1 slot lists in LDS, 2 the candidate cache, 3 slot lists in HBM (slim loop); 4 the general body
+        ctl.path = !slim_fit ? 4u : (slots_ok && slim_s <= lds) ? 1u : (cache_ok && slim_c <= lds) ? 2u : 3u;
+        ctl.need = (uint32_t)(cache_ok ? slim_c : ctl.path == 1 ? slim_s : slim_n);   // the cache layout's need
+    }
+#endif
     if (slim_fit) {
         K3Mem m;
         uint32_t *qq = qb ? qb : cd.read;
         if (slots_ok && slim_s <= lds) {
             (void)k3_layout(S, ntot, R, dir, summ_tot, true, 0, off, c8);
-            k3_mem(smem, off, 0, true, kb, m);
-            if (c8) k3_greedy_slim<true, NT, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
-            else k3_greedy_slim<true, NT, false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
+            k3_mem(smem, off, 0, true, kb, m, true, S);
+            if (c8) k3_greedy_slim<true, NT, true, false, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
+            else k3_greedy_slim<true, NT, false, false, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
+        } else if (cache_ok && slim_c <= lds) {
+            (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, aux_in_cache ? 0 : 4ull * R, false);
+            k3_mem(smem, off, 0, false, kb, m, false, S, false);
+            m.gmo = d.mmr_off + 2ull * r0 + dir;
+            m.gmn = d.mmr_n + 2ull * r0 + dir;
+            m.gmst = d.mmr_start + 2ull * r0 + dir;
+            m.kbase = kbase;
+            m.sl16 = reinterpret_cast<uint16_t *>(smem + align16(slim_cn));
+            if (aux_in_cache) m.aux = reinterpret_cast<uint32_t *>(m.sl16);
+            if (c8) k3_greedy_slim<true, NT, true, true, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq, CL);
+            else k3_greedy_slim<true, NT, false, true, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq, CL);
         } else {
             (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8);
-            k3_mem(smem, off, 0, false, kb, m);
-            if (c8) k3_greedy_slim<false, NT, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
-            else k3_greedy_slim<false, NT, false>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
+            k3_mem(smem, off, 0, false, kb, m, true, S);
+            if (c8) k3_greedy_slim<false, NT, true, false, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
+            else k3_greedy_slim<false, NT, false, false, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
         }
         return;
     }
@@ -3032,7 +3161,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
             rcw = rcw > rcw_max ? rcw_max : rcw;
             (void)k3_layout(S, ntot, R, dir, summ_tot, true, rcw, off);
             K3Mem m;
-            k3_mem(smem, off, rcw, true, kb, m);
+            k3_mem(smem, off, rcw, true, kb, m, true, S);
             k3_greedy_body<true, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
         } else if (need_n <= lds) {
             (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw_min, off);
@@ -3040,7 +3169,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
             rcw = rcw > rcw_max ? rcw_max : rcw;
             (void)k3_layout(S, ntot, R, dir, summ_tot, false, rcw, off);
             K3Mem m;
-            k3_mem(smem, off, rcw, false, kb, m);
+            k3_mem(smem, off, rcw, false, kb, m, true, S);
             k3_greedy_body<false, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
         } else {
             const uint32_t rcw = rcw_min;
@@ -3055,7 +3184,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
             __syncthreads();
             if (uni(ctl.fail)) return;
             K3Mem m;
-            k3_mem(d.scr + ctl.scr, off, rcw, false, kb, m);
+            k3_mem(d.scr + ctl.scr, off, rcw, false, kb, m, true, S);
             k3_greedy_body<false, true>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan);
         }
     }
@@ -3068,29 +3197,38 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
 // in round 3 (50 kb batch 5.25 -> 4.96 ms, gap mix 7.3 -> 10.3 ms: register-
 // limited to two problems per CU; with 6 waves per SIMD forced, spills, 5.48 /
 // 11.2 ms) and 256 kept.
+// Persistent: the grid is what the device holds at once (pf_api.hip
+// k3_resident); each workgroup takes the next problem of k3_order (heaviest
+// first) from the counter d.k3_next until k3_n are taken -- list scheduling,
+// so a slot freed on any CU takes the next problem at once.  Every workgroup
+// leaves when the counter passes k3_n.
 __global__ __launch_bounds__(PF_K3S_THREADS) void pf_k3_greedy(pf_dev_batch d) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ K3Ctl ctl;
-    __shared__ K3Cand cd;
+    __shared__ K3CandSlim cd;
     __shared__ uint32_t sh_scan[PF_K3S_THREADS / 64 + 1];
-    if constexpr (PF_K3S_THREADS > PF_MAX_NCAND) {
-        __shared__ uint32_t qb[PF_K3S_THREADS];          // per-wave queue scratch beyond cd.read
-        k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes, qb);
-    } else {
-        // no extra static LDS: two 72 KB problems plus their static LDS fill a
-        // CU's 160 KB exactly (1 KB more halves the main kernel's occupancy)
-        k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_bytes);
+    __shared__ uint32_t s_rank;
+    static_assert(PF_K3S_THREADS <= PF_MAX_NCAND, "cd.read holds the per-wave queue scratch");
+    for (;;) {
+        if (threadIdx.x == 0) s_rank = atomicAdd(d.k3_next, 1u);
+        __syncthreads();
+        const uint32_t rank = uni(s_rank);
+        if (rank >= d.k3_n) break;
+        k3_run<false, PF_K3S_THREADS>(d, d.k3_order[rank], smem, ctl, cd, sh_scan, d.lds_bytes);
+        __syncthreads();                                 // every thread has read s_rank and left the problem
     }
 }
 
-// The heavy problems (k3_order's first n, pf_api.hip): the fallback's build
-// and LDS budget, launched on a second stream beside the main kernel.
-__global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_heavy(pf_dev_batch d) {
+// The heavy problems (k3_order's first n, pf_api.hip): the slim build with
+// the larger budget d.lds_heavy, launched on a second stream beside the main
+// kernel; a problem that does not fit is deferred to pf_k3_fallback like the
+// main kernel's.
+__global__ __launch_bounds__(PF_K3S_THREADS) void pf_k3_heavy(pf_dev_batch d) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ K3Ctl ctl;
-    __shared__ K3Cand cd;
-    __shared__ uint32_t sh_scan[PF_K3_WAVES + 1];
-    k3_run<true>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_fb);
+    __shared__ K3CandSlim cd;
+    __shared__ uint32_t sh_scan[PF_K3S_THREADS / 64 + 1];
+    k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_heavy);
 }
 
 // Problems the main kernel deferred (dictionary or tables beyond the LDS

@@ -51,13 +51,51 @@ for label, sel in (("heavy", [p for p in range(2 * W) if p in heavy]),
     print(f"{label}: {len(sel)} problems, {it:.0f} iterations, {allc / max(it, 1):.0f} cycles/iter")
     for k, n in SLIM.items():
         print(f"  {n:14s} {tot[k] / max(allc, 1) * 100:5.1f}%  {tot[k] / max(it, 1):8.0f} cyc/iter")
-    print("  per problem (w,dir): reads, sites, iters, lookups/iter, methmers, Mcycles")
+    print("  per problem (w,dir): reads, sites, iters, lookups/iter, methmers, Mcycles, path, KB")
     cyc = np.array([sum(prof[p >> 1, p & 1, k] for k in SLIM) for p in sel])
     print(f"  problem Mcycles: max {cyc.max() / 1e6:.2f}, p90 {np.percentile(cyc, 90) / 1e6:.2f}, "
           f"median {np.median(cyc) / 1e6:.2f}, sum {cyc.sum() / 1e9:.3f} G")
+    paths = prof[[p >> 1 for p in sel], [p & 1 for p in sel], 29].astype(int)
+    need = prof[[p >> 1 for p in sel], [p & 1 for p in sel], 31]
+    nt = prof[[p >> 1 for p in sel], [p & 1 for p in sel], 30]
+    print("  P2 path (1 LDS lists, 2 cache, 3 HBM lists, 4 body): " +
+          ", ".join(f"{k}: {int((paths == k).sum())}" for k in (1, 2, 3, 4)))
+    print(f"  LDS need of the slim layout taken: p50 {np.median(need) / 1024:.1f} KB, p90 "
+          f"{np.percentile(need, 90) / 1024:.1f} KB, max {need.max() / 1024:.1f} KB; slots p50 {np.median(nt):.0f} "
+          f"max {nt.max():.0f}")
     for p in sorted(sel, key=lambda p: -sum(prof[p >> 1, p & 1, k] for k in SLIM))[:8]:
         w, d = divmod(p, 2)
         print(f"    ({w},{d}) {st[w, d, 6]} {st[w, d, 7]} {st[w, d, 2]} {st[w, d, 0] / max(st[w, d, 2], 1):.0f} "
-              f"{st[w, d, 4]} {sum(prof[w, d, k] for k in SLIM) / 1e6:.2f}")
+              f"{st[w, d, 4]} {sum(prof[w, d, k] for k in SLIM) / 1e6:.2f} {int(prof[w, d, 29])} "
+              f"{prof[w, d, 31] / 1024:.1f}")
+# concurrency over time from the problems' start/end (s_memrealtime, 100 MHz)
+t0s = prof[:, :, 24].ravel()
+t1s = prof[:, :, 25].ravel()
+ok = (t0s > 0) & (t1s > t0s)
+if ok.any():
+    a0, a1 = t0s[ok], t1s[ok]
+    base = a0.min()
+    span = (a1.max() - base) / 100.0                     # microseconds
+    grid = np.linspace(0, a1.max() - base, 41)
+    conc = [int(((a0 - base <= g) & (a1 - base > g)).sum()) for g in grid]
+    dur = (a1 - a0) / 100.0
+    print(f"problems' span {span:.0f} us; duration us p50 {np.median(dur):.0f} max {dur.max():.0f}; "
+          f"concurrency over time (41 samples): {conc}")
+    print(f"  mean concurrency {np.mean(conc):.0f}; problem-us sum {dur.sum():.0f} -> mean "
+          f"{dur.sum() / max(span, 1):.0f}")
+# the candidate-cache layout's LDS need against the window's reads (all problems)
+allp = [(int(st[p >> 1, p & 1, 6]), prof[p >> 1, p & 1, 31] / 1024, sum(prof[p >> 1, p & 1, k] for k in SLIM) / 1e6)
+        for p in range(2 * W) if prof[p >> 1, p & 1, 31] > 0]
+if allp:
+    a = np.array(allp)
+    print("cache-layout need by reads (R bin: n, need p50 / p90 / max KB, Mcycles p50 / max):")
+    for lo, hi in ((0, 300), (300, 450), (450, 600), (600, 800), (800, 1000), (1000, 1200), (1200, 5000)):
+        sel = (a[:, 0] >= lo) & (a[:, 0] < hi)
+        if sel.any():
+            print(f"  [{lo},{hi}): {sel.sum():4d}  {np.median(a[sel, 1]):5.1f} / {np.percentile(a[sel, 1], 90):5.1f} / "
+                  f"{a[sel, 1].max():5.1f}   {np.median(a[sel, 2]):.2f} / {a[sel, 2].max():.2f}")
+    for b in (32, 36, 44, 48, 56):
+        print(f"  need > {b} KB: {(a[:, 1] > b).sum()} problems, min reads among them "
+              f"{int(a[a[:, 1] > b, 0].min()) if (a[:, 1] > b).any() else '-'}")
 db.free()
 ctx.close()
