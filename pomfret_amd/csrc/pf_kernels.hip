@@ -1250,6 +1250,7 @@ struct K3Ctl {
     int32_t i_last;
     uint32_t min_i, max_i, fail, summ, nstrict, mxlen, cmax;
     uint32_t path, need;                      // (profile build) the P2 variant taken and its LDS bytes
+    unsigned long long t_run;                 // (profile build) s_memrealtime at k3_run's start
     uint32_t ins_n, ins_st, ins_mo, ins_tg;   // register variant: winner whose insert is pending
     unsigned long long scr;
     int32_t tab[4];
@@ -1277,6 +1278,39 @@ struct K3CandSlim {
 
 DEV uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
+// Every methmer key of the problem's reads (direction dir) that `keep(i)`
+// selects: f(read i, index t, site st + t, arena offset, key).  A wave takes
+// eight reads at a time with all their scalar fields and key loads issued
+// before the first use, so a workgroup keeps 32 reads' loads in flight
+// instead of walking one read per wave through two dependent round trips
+// (the prologue of a 1,400-read problem was a quarter of its greedy loop).
+template <int NT, typename K, typename F>
+DEV void k3_each_key(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t dir, K &&keep, F &&f) {
+    constexpr uint32_t B = 8, NW = NT / 64;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t i0 = wid * B; i0 < R; i0 += NW * B) {
+        uint32_t n[B], st[B], key[B];
+        uint64_t off[B];
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++) {
+            const uint32_t i = i0 + u;
+            const bool ok = i < R && keep(i);
+            const uint64_t g = 2ull * (r0 + (ok ? i : 0u)) + dir;
+            n[u] = ok ? d.mmr_n[g] : 0u;
+            st[u] = d.mmr_start[g];
+            off[u] = d.mmr_off[g];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++) key[u] = lane < n[u] ? d.keys[off[u] + lane] : 0u;
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++)
+            if (lane < n[u]) f(i0 + u, lane, st[u] + lane, off[u] + lane, key[u]);
+#pragma unroll
+        for (uint32_t u = 0; u < B; u++)
+            for (uint32_t t = 64 + lane; t < n[u]; t += 64) f(i0 + u, t, st[u] + t, off[u] + t, d.keys[off[u] + t]);
+    }
+}
+
 // dictionary of methmer keys per site -> dense slot ids (replaces the per-site
 // key lists + linear search of insert_mmrs_to_counts / query_counts_of_mmrs)
 template <int NT = PF_K3_THREADS>
@@ -1286,17 +1320,11 @@ DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uin
     const uint32_t MW = (uint32_t)d.mw;
     for (uint32_t j = tid; j < S * MW; j += NT) masks[j] = 0;
     __syncthreads();
-    for (uint32_t i = wid; i < R; i += NT / 64) {
-        const uint32_t g = 2 * (r0 + i) + dir;
-        const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
-        const uint32_t *kp = d.keys + d.mmr_off[g];
-        for (uint32_t t = lane; t < n; t += 64) {
-            const uint32_t site = st + t;
-            const uint32_t key = kp[t];
-            if (site < S && key < 64u * MW)
-                atomicOr((unsigned long long *)&masks[(uint64_t)site * MW + (key >> 6)], 1ull << (key & 63));
-        }
-    }
+    k3_each_key<NT>(d, r0, R, dir, [](uint32_t) { return true; },
+                    [&](uint32_t, uint32_t, uint32_t site, uint64_t, uint32_t key) {
+                        if (site < S && key < 64u * MW)
+                            atomicOr((unsigned long long *)&masks[(uint64_t)site * MW + (key >> 6)], 1ull << (key & 63));
+                    });
     __syncthreads();
     uint32_t carry = 0;
     for (uint32_t p0 = 0; p0 < S; p0 += NT) {
@@ -1318,26 +1346,19 @@ DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uin
 template <int NT = PF_K3_THREADS>
 DEV void k3_dict_rewrite(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uint32_t dir,
                          const uint64_t *masks, const uint32_t *base) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t MW = (uint32_t)d.mw;
-    for (uint32_t i = wid; i < R; i += NT / 64) {
-        const uint32_t g = 2 * (r0 + i) + dir;
-        const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
-        uint32_t *kp = d.keys + d.mmr_off[g];
-        for (uint32_t t = lane; t < n; t += 64) {
-            const uint32_t site = st + t;
-            uint32_t slot = PF_NONE;
-            const uint32_t key = kp[t];
-            if (site < S && key < 64u * MW) {
-                const uint64_t *row = masks + (uint64_t)site * MW;
-                const uint32_t wi = key >> 6, b = key & 63;
-                slot = base[site];
-                for (uint32_t m = 0; m < wi; m++) slot += (uint32_t)__popcll(row[m]);
-                slot += (uint32_t)__popcll(row[wi] & ((1ull << b) - 1ull));
-            }
-            kp[t] = slot;
-        }
-    }
+    k3_each_key<NT>(d, r0, R, dir, [](uint32_t) { return true; },
+                    [&](uint32_t, uint32_t, uint32_t site, uint64_t koff, uint32_t key) {
+                        uint32_t slot = PF_NONE;
+                        if (site < S && key < 64u * MW) {
+                            const uint64_t *row = masks + (uint64_t)site * MW;
+                            const uint32_t wi = key >> 6, b = key & 63;
+                            slot = base[site];
+                            for (uint32_t m = 0; m < wi; m++) slot += (uint32_t)__popcll(row[m]);
+                            slot += (uint32_t)__popcll(row[wi] & ((1ull << b) - 1ull));
+                        }
+                        d.keys[koff] = slot;
+                    });
     __syncthreads();
 }
 
@@ -1985,21 +2006,29 @@ DEV void k3_init(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0, u
     // ---- reference reads seed the counts (insert_ref_reads_methmer_counts, :3776-3810)
     const uint32_t refbit = dir == 0 ? FLG_LEFT : FLG_RIGHT;
     uint32_t ref_ins = 0;
-    for (uint32_t i = wid; i < R; i += (NT / 64)) {
+    auto seed = [&](uint32_t i, uint32_t site, uint32_t slot) {
         const uint32_t hp = m.hp[i];
-        if (!(m.flg[i] & refbit) || hp > 1) continue;
-        const uint32_t n = k3_mn(m, i), st = k3_mst(m, i), mo = SLDS ? m.mo[i] : k3_mo(m, i);
-        const uint32_t inc = hp ? 0x10000u : 1u;
-        ref_ins += n;
-        for (uint32_t t = lane; t < n; t += 64) {
-            const uint32_t site = st + t;
-            const uint32_t slot = k3_slot<SLDS>(m, mo + t);
-            if (site < S && slot != PF_NONE) {
-                if (C8) atomicAdd(&m.cnt[slot >> 1], (hp ? 0x100u : 1u) << ((slot & 1u) * 16u));
-                else atomicAdd(&m.cnt[slot], inc);
-                atomicAdd(&m.sum[site], inc);
-            }
+        if (site < S && slot != PF_NONE) {
+            if (C8) atomicAdd(&m.cnt[slot >> 1], (hp ? 0x100u : 1u) << ((slot & 1u) * 16u));
+            else atomicAdd(&m.cnt[slot], hp ? 0x10000u : 1u);
+            atomicAdd(&m.sum[site], hp ? 0x10000u : 1u);
         }
+    };
+    auto is_ref = [&](uint32_t i) { return (m.flg[i] & refbit) && m.hp[i] <= 1; };
+    if (SLDS) {
+        for (uint32_t i = wid; i < R; i += (NT / 64)) {
+            if (!is_ref(i)) continue;
+            const uint32_t n = k3_mn(m, i), st = k3_mst(m, i), mo = m.mo[i];
+            ref_ins += n;
+            for (uint32_t t = lane; t < n; t += 64) seed(i, st + t, k3_slot<SLDS>(m, mo + t));
+        }
+    } else {
+        // the slot ids from the rewritten key arena, eight reads' loads in flight
+        k3_each_key<NT>(d, r0, R, dir, is_ref, [&](uint32_t i, uint32_t t, uint32_t site, uint64_t, uint32_t slot) {
+            if (t == 0) ref_ins += d.mmr_n[2ull * (r0 + i) + dir];
+            seed(i, site, slot);
+        });
+        ref_ins = (uint32_t)__builtin_amdgcn_readfirstlane((int)ref_ins);   // (lane 0 counted every read)
     }
     if (lane == 0 && ref_ins) atomicAdd((uint32_t *)&ctl.tab[0], ref_ins);
     if (sum_mmr) atomicAdd(&ctl.summ, sum_mmr);
@@ -2379,6 +2408,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         unsigned long long *pp = d.prof + ((uint64_t)w * 2 + dir) * 32;
         prof_acc[29] = ctl.path;
         prof_acc[25] = k3_realtime();
+        prof_acc[26] = ctl.t_run;
         prof_acc[30] = ctl.ntot;
         prof_acc[31] = ctl.need;
         for (int i = 0; i < 32; i++) pp[i] = prof_acc[i];
@@ -3013,6 +3043,9 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     const uint32_t r0 = d.win_read_off[w];
     const uint32_t MW = (uint32_t)d.mw;
     const uint64_t kbase = d.mmr_off[2ull * r0];
+#ifdef PF_K3_PROFILE
+    if (tid == 0) ctl.t_run = k3_realtime();
+#endif
 
     // ---- P1: slot dictionary
     const uint64_t need1 = align16(8ull * S * MW) + 4ull * S;

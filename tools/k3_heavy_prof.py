@@ -83,6 +83,11 @@ if ok.any():
           f"concurrency over time (41 samples): {conc}")
     print(f"  mean concurrency {np.mean(conc):.0f}; problem-us sum {dur.sum():.0f} -> mean "
           f"{dur.sum() / max(span, 1):.0f}")
+    tr = prof[:, :, 26].ravel()[ok]
+    if (tr > 0).any():
+        pro = (a0 - tr)[tr > 0] / 100.0
+        print(f"  prologue (k3_run start -> greedy init) us: p50 {np.median(pro):.1f} p90 {np.percentile(pro, 90):.1f} "
+              f"max {pro.max():.1f}, sum {pro.sum():.0f} = {pro.sum() / dur.sum() * 100:.1f}% of the greedy loops' sum")
 # the candidate-cache layout's LDS need against the window's reads (all problems)
 allp = [(int(st[p >> 1, p & 1, 6]), prof[p >> 1, p & 1, 31] / 1024, sum(prof[p >> 1, p & 1, k] for k in SLIM) / 1e6)
         for p in range(2 * W) if prof[p >> 1, p & 1, 31] > 0]
