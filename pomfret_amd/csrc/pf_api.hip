@@ -695,8 +695,11 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     const char *kp = getenv("PF_K3_PATH");
     d.k3_mode = !kp ? 0u : strcmp(kp, "fold") == 0 ? 1u : strcmp(kp, "rows") == 0 ? 2u : 0u;
     {
+        // the greedy loop's slot-list source: 1 auto (all lists in LDS when
+        // they fit, else the candidate cache, else HBM); tests force the
+        // others: 0 no cache, 2 the cache always, 3 HBM lists always
         const char *kc = getenv("PF_K3_CACHE");
-        d.k3_cache = kc && !strcmp(kc, "0") ? 0u : 1u;
+        d.k3_cache = !kc ? 1u : !strcmp(kc, "0") ? 0u : !strcmp(kc, "force") ? 2u : !strcmp(kc, "hbm") ? 3u : 1u;
     }
     for (int i = 0; i < PF_SLOTS; i++)
         if (hipHostMalloc((void **)&b->h_io[i], b->io_bytes) != hipSuccess) return fail(PF_ERR_NOMEM);

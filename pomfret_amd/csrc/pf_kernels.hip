@@ -3135,7 +3135,8 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     // lists do not fit: n_cand + 1 slots of the longest list, u16 entries
     const uint32_t CL = (uni(ctl.mxlen) + 1u) & ~1u;
     const uint32_t NCc = (uint32_t)d.win_par[w * 4 + 2];
-    const bool cache_ok = slim_ok && slots_ok && NCc <= 63u && CL > 0 && CL <= 2u * NT && d.k3_cache != 0u;
+    const bool cache_ok = slim_ok && slots_ok && NCc <= 63u && CL > 0 && CL <= 2u * NT && (d.k3_cache & 1u) != 0u;
+    const bool lists_ok = slots_ok && d.k3_cache < 2u;         // (tests force the cache / the HBM lists)
     // no per-read slot-list offsets (the cache copies from HBM), and the T5
     // scratch of k3_init inside the cache region when it is large enough
     const uint64_t cache_b = 2ull * (NCc + 1) * CL;
@@ -3143,7 +3144,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     const uint64_t slim_cn =
         k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, aux_in_cache ? 0 : 4ull * R, false);
     const uint64_t slim_c = align16(slim_cn) + cache_b;
-    const bool slim_fit = slim_ok && ((slots_ok && slim_s <= lds) || (cache_ok && slim_c <= lds) || slim_n <= lds);
+    const bool slim_fit = slim_ok && ((lists_ok && slim_s <= lds) || (cache_ok && slim_c <= lds) || slim_n <= lds);
     if (!FULL && !slim_fit) {
         k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
         return;
@@ -3153,14 +3154,14 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
 #ifdef PF_K3_PROFILE
     if (tid == 0) {
         // 1 slot lists in LDS, 2 the candidate cache, 3 slot lists in HBM (slim loop); 4 the general body
-        ctl.path = !slim_fit ? 4u : (slots_ok && slim_s <= lds) ? 1u : (cache_ok && slim_c <= lds) ? 2u : 3u;
+        ctl.path = !slim_fit ? 4u : (lists_ok && slim_s <= lds) ? 1u : (cache_ok && slim_c <= lds) ? 2u : 3u;
         ctl.need = (uint32_t)(cache_ok ? slim_c : ctl.path == 1 ? slim_s : slim_n);   // the cache layout's need
     }
 #endif
     if (slim_fit) {
         K3Mem m;
         uint32_t *qq = qb ? qb : cd.read;
-        if (slots_ok && slim_s <= lds) {
+        if (lists_ok && slim_s <= lds) {
             (void)k3_layout(S, ntot, R, dir, summ_tot, true, 0, off, c8);
             k3_mem(smem, off, 0, true, kb, m, true, S);
             if (c8) k3_greedy_slim<true, NT, true, false, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);

@@ -129,6 +129,25 @@ def test_lds_budget_variants(oracle_lib, gpu_ctx, monkeypatch, lds):
     db.free()
 
 
+@pytest.mark.parametrize("env", [{"PF_K3_CACHE": "force"}, {"PF_K3_CACHE": "hbm"}, {"PF_K3_PERSIST": "1"},
+                                 {"PF_K3_PERSIST": "7", "PF_K3_CACHE": "force"}],
+                         ids=["cache", "hbm_lists", "one_workgroup", "seven_workgroups_cache"])
+def test_slot_list_sources(oracle_lib, gpu_ctx, monkeypatch, env):
+    """The greedy loop's slot-list sources give the same bits on every case:
+    the candidate slot-list cache (round 4: the candidates' lists in LDS, the
+    appended read's list loaded an iteration ahead) forced for every problem,
+    the slot lists read from HBM, and the persistent main kernel with one
+    and with seven workgroups walking all the problems in turn (per-problem
+    state reset between problems)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for name, cfg, batch in CASES:
+        ref = oracle_lib.methphase(cfg, batch, n_threads=8)
+        db = gpu_ctx.upload(cfg, batch)
+        _compare(ref, db.run(), f"{name}/{env}")
+        db.free()
+
+
 @pytest.mark.parametrize("path", ["fold", "rows"])
 def test_greedy_pick_paths(oracle_lib, gpu_ctx, monkeypatch, path):
     """The greedy pick's alternatives give the same bits as the exact-interval
