@@ -179,8 +179,7 @@ struct Plan {
     std::vector<uint64_t> caddr;            // file address of each block
     std::vector<uint32_t> bsize;            // its BGZF size
     std::vector<Range> runs;
-    uint8_t *comp = nullptr;                // compressed bytes of every run, back to back (pinned)
-    uint64_t comp_n = 0;
+    uint64_t comp_n = 0;                    // compressed bytes of every run, back to back (d_comp), + pad
     uint64_t arena = 0;                     // inflated bytes
 };
 
@@ -465,17 +464,46 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         // at a few MB/s: the rate comes from blocks in flight, about one per
         // wave slot of the chip).
         constexpr uint32_t MINB = 4096;
-        const uint64_t ring_at = (tot + 512 + 255) & ~255ull;
-        P.comp_n = tot + 512;
-        P.comp = pf_ctx_stage((pf_ctx *)ctx, ring_at + 2ull * RING * sizeof(pf_bgzf_blk));
+        // The compressed bytes pass through a fixed pinned ring of NSLOT
+        // segment slots on their way to d_comp (round 4; round 3 pinned a
+        // buffer of the whole fetch, ~0.5 s for a 2 GB contig in a fresh
+        // process -- more than reading it).  A slot holds its segment's
+        // bytes behind the LB bytes before them (a copy of the previous
+        // segment's tail), so a block the previous scan left incomplete --
+        // it starts at most one BGZF block before the segment -- is scanned
+        // from one slot, header and footer.
+        constexpr uint64_t LB = 65536, PAD = 512;
+        uint64_t SEG = 64ull << 20, PIECE = 4ull << 20;
+        if (const char *e = getenv("PF_INGEST_SEG")) {     // tests: small segments (many slots, straddling blocks)
+            SEG = std::max<uint64_t>(strtoull(e, nullptr, 10), 4096);
+            PIECE = std::min(PIECE, SEG);
+        }
+        constexpr uint32_t NSLOT = 3;
+        const uint64_t slot_b = LB + SEG + PAD;
+        const uint64_t ring_at = NSLOT * slot_b;
+        P.comp_n = tot + PAD;
+        uint8_t *stage = pf_ctx_stage((pf_ctx *)ctx, ring_at + 2ull * RING * sizeof(pf_bgzf_blk));
         uint8_t *d_comp = D.alloc<uint8_t>(P.comp_n);
-        if (!P.comp || !d_comp) { rc = PF_ERR_NOMEM; break; }
-        pf_bgzf_blk *ring = reinterpret_cast<pf_bgzf_blk *>(P.comp + ring_at);
+        if (!stage || !d_comp) { rc = PF_ERR_NOMEM; break; }
+        pf_bgzf_blk *ring = reinterpret_cast<pf_bgzf_blk *>(stage + ring_at);
+        hipEvent_t eslot[NSLOT];
+        bool slot_used[NSLOT] = {};
+        int nes = 0;
+        for (auto &e : eslot) if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) nes++;
+        struct SlotEvGuard {
+            hipEvent_t *e; int n;
+            ~SlotEvGuard() { for (int i = 0; i < n; i++) (void)hipEventDestroy(e[i]); }
+        } sevg{eslot, nes};
+        if (nes != (int)NSLOT) { rc = PF_ERR_HIP; break; }
+        uint64_t win0 = 0;                    // the current slot holds global [win0 - LB, win1)
+        uint8_t *win_p = stage;               // host address of global win0 - LB
+        auto hp = [&](uint64_t x) { return win_p + (x + LB - win0); };
         // The inflated arena is sized from the compressed bytes (BAM inflates
         // 1.5-3x); blocks past it wait for an exact arena after the reads.
         const uint64_t acap = 4 * tot + (1ull << 20);
         d_arena = D.alloc<uint8_t>(acap + 512);
         if (!d_arena) { rc = PF_ERR_NOMEM; break; }
+        const double t_alloc = now_ms();                    // PF_INGEST_TRACE
         uint32_t nb_sent = 0;                 // blocks whose inflate is enqueued
         uint32_t cur = 0;                     // first run not completely scanned
         bool spill = false;                   // the arena estimate was short
@@ -487,13 +515,12 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
                 if (R.buf0 > front) return PF_OK;
                 if (R.scan == 0) R.b0 = (uint32_t)P.blk.size();
                 const uint64_t len = R.f1 - R.f0, avail = std::min(len, front - R.buf0);
-                const uint8_t *c = P.comp + R.buf0;
                 uint64_t o = R.scan;
                 bool end = false;
                 for (;;) {
                     if (o + 18 > len) { end = true; break; }
                     if (o + 18 > avail) break;
-                    const uint8_t *h = c + o;
+                    const uint8_t *h = hp(R.buf0 + o);
                     if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return PF_ERR_ARG;
                     const uint32_t xlen = rd16(h + 10);
                     if (o + 12 + xlen > len) { end = true; break; }
@@ -560,22 +587,34 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             }
             return PF_OK;
         };
-        // Parallel reads into the pinned buffer in segments of <= 64 MiB
+        // Parallel reads into the ring's slots in segments of <= 64 MiB
         // (pieces of <= 4 MiB on 16 threads); each segment's H2D copy runs on
         // the copy stream and its whole blocks are inflated on the main stream
-        // while the next segment is read.
+        // while the next segments are read.
         {
-            constexpr uint64_t SEG = 64ull << 20, PIECE = 4ull << 20;
             std::vector<std::pair<uint64_t, uint64_t>> pieces;     // (run, offset in run)
             for (uint32_t ri = 0; ri < P.runs.size(); ri++)
                 for (uint64_t o = 0; o < P.runs[ri].f1 - P.runs[ri].f0; o += PIECE) pieces.push_back({ri, o});
             std::atomic<int> bad{0};
             size_t pi = 0;
             uint64_t copied = 0;
+            double tr_read = 0, tr_copy = 0, tr_scan = 0, tr_send = 0;   // PF_INGEST_TRACE
+            uint32_t nseg = 0;
             while (pi < pieces.size() && !bad.load() && !rc) {
+                const double ta = now_ms();
                 size_t pe = pi;
                 const uint64_t seg0 = P.runs[pieces[pi].first].buf0 + pieces[pi].second;
                 while (pe < pieces.size() && P.runs[pieces[pe].first].buf0 + pieces[pe].second < seg0 + SEG) pe++;
+                const uint64_t seg1 = pe < pieces.size() ? P.runs[pieces[pe].first].buf0 + pieces[pe].second : tot;
+                // the slot: free once its last H2D copy is done; the previous
+                // segment's tail goes in front of the new bytes
+                const uint32_t sl = nseg++ % NSLOT;
+                uint8_t *sp = stage + (uint64_t)sl * slot_b;
+                if (slot_used[sl] && hipEventSynchronize(eslot[sl]) != hipSuccess) { bad.store(2); break; }
+                const uint64_t lb = std::min(LB, seg0);
+                if (lb) memcpy(sp + LB - lb, hp(seg0 - lb), lb);
+                win0 = seg0;
+                win_p = sp;
                 std::atomic<size_t> next{pi};
                 std::vector<std::thread> th;
                 const size_t nt = std::min<size_t>(16, pe - pi);
@@ -584,28 +623,38 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
                         for (size_t k; (k = next.fetch_add(1)) < pe;) {
                             const Range &R = P.runs[pieces[k].first];
                             const uint64_t o = pieces[k].second, n = std::min(PIECE, R.f1 - R.f0 - o);
-                            if (read_range(fd, R.f0 + o, n, P.comp + R.buf0 + o)) bad.store(1);
+                            if (read_range(fd, R.f0 + o, n, hp(R.buf0 + o))) bad.store(1);
                         }
                     });
                 for (auto &t : th) t.join();
+                const double tb = now_ms();
+                tr_read += tb - ta;
                 if (bad.load()) break;
-                const uint64_t seg1 = pe < pieces.size() ? P.runs[pieces[pe].first].buf0 + pieces[pe].second : tot;
-                if (pe == pieces.size()) memset(P.comp + tot, 0, 512);
-                const uint64_t cend = pe == pieces.size() ? tot + 512 : seg1;
-                if (hipMemcpyAsync(d_comp + copied, P.comp + copied, cend - copied, hipMemcpyHostToDevice, cs) !=
-                    hipSuccess) { bad.store(2); break; }
+                if (pe == pieces.size()) memset(hp(tot), 0, PAD);
+                const uint64_t cend = pe == pieces.size() ? tot + PAD : seg1;
+                if (hipMemcpyAsync(d_comp + copied, hp(copied), cend - copied, hipMemcpyHostToDevice, cs) !=
+                        hipSuccess || hipEventRecord(eslot[sl], cs) != hipSuccess) { bad.store(2); break; }
+                slot_used[sl] = true;
                 copied = cend;
                 pi = pe;
+                const double tc = now_ms();
                 rc = scan_to(seg1);
+                const double td = now_ms();
                 if (!rc && !spill) {
                     if (P.arena > acap) spill = true;
                     else rc = send(d_arena, false);
                 }
+                const double te = now_ms();
+                tr_copy += tc - tb; tr_scan += td - tc; tr_send += te - td;
             }
+            if (getenv("PF_INGEST_TRACE"))
+                fprintf(stderr, "[ingest] %zu pieces %.1f MB: plan + stage + alloc %.1f ms, read %.1f ms, copy enqueue "
+                        "%.1f, scan %.1f, send %.1f\n", pieces.size(), tot / 1e6, t_alloc - t0, tr_read, tr_copy,
+                        tr_scan, tr_send);
             if (!rc && bad.load()) rc = bad.load() == 1 ? -1 : PF_ERR_HIP;
             if (!rc && pieces.empty()) {
-                memset(P.comp + tot, 0, 512);
-                if (hipMemcpyAsync(d_comp, P.comp, 512, hipMemcpyHostToDevice, cs) != hipSuccess) rc = PF_ERR_HIP;
+                memset(stage, 0, PAD);
+                if (hipMemcpyAsync(d_comp, stage, PAD, hipMemcpyHostToDevice, cs) != hipSuccess) rc = PF_ERR_HIP;
             }
         }
         if (!rc) rc = scan_to(tot);
@@ -622,6 +671,8 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             d_arena = a2;
         }
         if (!rc) rc = send(d_arena, true);
+        // the slots' copies are done before the staging buffer is reused
+        if (!rc && hipStreamSynchronize(cs) != hipSuccess) rc = PF_ERR_HIP;
         if (!rc && batches.empty() && hipEventRecord(ev[0], st) != hipSuccess) rc = PF_ERR_HIP;
         if (!rc && (hipEventRecord(ecp, cs) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess ||
                     hipEventRecord(ecp, s3) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess ||
@@ -630,6 +681,7 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
         }
         if (rc) break;
         const double t_read = now_ms() - t0;
+        if (getenv("PF_INGEST_TRACE")) fprintf(stderr, "[ingest] t_read %.1f ms\n", t_read);
         const uint32_t NB = (uint32_t)P.blk.size(), NR = (uint32_t)P.runs.size();
         // ---- chunks -> arena positions; chain starts per run
         auto find_blk = [&](uint64_t addr) -> int64_t {

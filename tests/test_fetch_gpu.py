@@ -103,8 +103,14 @@ def _odd_records(tmp_path):
     return aln, bam
 
 
-def test_device_fetch_odd_records(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("seg", [None, "98304", "4096"])
+def test_device_fetch_odd_records(gpu_ctx, tmp_path, monkeypatch, seg):
+    """(seg: the staging ring's segment size forced small -- every slot
+    reused many times, blocks straddling segments scanned from the copied
+    tail of the previous one, the ~600 KB record over many segments.)"""
     from pomfret_amd import Config, LoadConfig
+    if seg:
+        monkeypatch.setenv("PF_INGEST_SEG", seg)
     aln, bam = _odd_records(tmp_path)
     cfg, lcfg = Config.from_coverage(20, given=False), LoadConfig()
     host, hqn, hinfo, db, dqn, dinfo = _both(gpu_ctx, bam, "chrS", aln.win_start, aln.win_end, cfg, lcfg)
@@ -162,7 +168,8 @@ def test_pipeline_device_vs_host_fetch(gpu_ctx, tmp_path, mode):
         assert open(pd + e, "rb").read() == open(ph + e, "rb").read(), e
 
 
-def test_haptag_bam_vs_host(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("seg", [None, "98304"])
+def test_haptag_bam_vs_host(gpu_ctx, tmp_path, monkeypatch, seg):
     """-u pre-pass through the device fetch (pf_haptag_bam) against the host
     reader + K4 (pf_bam_fetch_contig_reads + pf_haptag_reads): the same reads
     (qnames, BAM order, secondary/unmapped skipped) and tags."""
@@ -172,6 +179,8 @@ def test_haptag_bam_vs_host(gpu_ctx, tmp_path):
     from test_bam import _u_bam
     from pomfret_amd.bam import BamFile, vcf_known_vars
     from pomfret_amd.synth_u import USpec
+    if seg:
+        monkeypatch.setenv("PF_INGEST_SEG", seg)
     known, reads, order, bam, vcf = _u_bam(tmp_path, USpec(n_reads=600, ref_len=400_000))
     kv = vcf_known_vars(vcf, "chrU")
     with BamFile(bam) as b:
