@@ -366,6 +366,23 @@ def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bo
             raise RuntimeError(f"pomfret-amd failed ({p.returncode}): {p.stderr[-2000:]}")
         outs["cli"] = take(prefix + ".cli")
         log(f"[bench] e2e_u: cli {t1 - t0:.2f}s")
+        # what chromosome-scale contigs cost, on this genome: (a) no kept
+        # arenas (a contig whose inflated BAM would break the HBM reserve:
+        # its window jobs re-read and re-inflate their ranges), (b) the -u
+        # pre-pass in position pieces of 256 MiB compressed (a 60x chr1 is
+        # tens of GB: pieces of 4 GiB), outputs compared with the others
+        variants = {}
+        for key, extra in (("cli_no_kept_arenas", {"PF_FETCH_CACHE": "0"}),
+                           ("cli_pieces_256MiB", {"PF_FETCH_PIECE_BYTES": str(256 << 20)})):
+            tv = time.perf_counter()
+            pv = subprocess.run([c if c != prefix + ".cli" else prefix + "." + key for c in cmd], capture_output=True,
+                                text=True, env=dict(os.environ, **extra))
+            dv = time.perf_counter() - tv
+            if pv.returncode != 0:
+                raise RuntimeError(f"pomfret-amd ({key}) failed ({pv.returncode}): {pv.stderr[-2000:]}")
+            outs[key] = take(prefix + "." + key)
+            variants[key] = {"s": round(dv, 2), "env": extra}
+            log(f"[bench] e2e_u: {key} {dv:.2f}s")
         t0d = time.perf_counter()
         r = methphase_files(g["bam"], g["vcf"], prefix + ".drv", None, lcfg, ctx=ctx, untagged=True, threads=threads)
         t1d = time.perf_counter()
@@ -379,6 +396,7 @@ def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bo
         res["cli"] = {"s": round(t1 - t0, 2), "records_per_s": round(res["records"] / (t1 - t0), 1),
                       "what": " ".join(["pomfret-amd", "methphase", "-u", "-t", str(threads), "-o", "P",
                                         "--vcf", "V", "B"])}
+        res["cli_variants"] = variants
         res["driver"] = {"s": round(t1d - t0d, 2), "records_per_s": round(res["records"] / (t1d - t0d), 1),
                          "phases": r["stats"], "what": "methphase_files in this process, warm context"}
         # K4 on the largest contig (the -u pre-pass's kernel, warm)

@@ -478,6 +478,8 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             SEG = std::max<uint64_t>(strtoull(e, nullptr, 10), 4096);
             PIECE = std::min(PIECE, SEG);
         }
+        if (const char *e = getenv("PF_INGEST_PIECE"))     // tests: read pieces not dividing the segment
+            PIECE = std::min(SEG, std::max<uint64_t>(strtoull(e, nullptr, 10), 512));
         constexpr uint32_t NSLOT = 3;
         const uint64_t slot_b = LB + SEG + PAD;
         const uint64_t ring_at = NSLOT * slot_b;
@@ -602,9 +604,16 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             uint32_t nseg = 0;
             while (pi < pieces.size() && !bad.load() && !rc) {
                 const double ta = now_ms();
-                size_t pe = pi;
+                // whole pieces up to SEG bytes (a slot's capacity; pieces are
+                // run-relative, so a segment over several runs ends where the
+                // next piece would overflow the slot)
                 const uint64_t seg0 = P.runs[pieces[pi].first].buf0 + pieces[pi].second;
-                while (pe < pieces.size() && P.runs[pieces[pe].first].buf0 + pieces[pe].second < seg0 + SEG) pe++;
+                auto piece_end = [&](size_t k) {
+                    const Range &R = P.runs[pieces[k].first];
+                    return R.buf0 + pieces[k].second + std::min(PIECE, R.f1 - R.f0 - pieces[k].second);
+                };
+                size_t pe = pi + 1;
+                while (pe < pieces.size() && piece_end(pe) <= seg0 + SEG) pe++;
                 const uint64_t seg1 = pe < pieces.size() ? P.runs[pieces[pe].first].buf0 + pieces[pe].second : tot;
                 // the slot: free once its last H2D copy is done; the previous
                 // segment's tail goes in front of the new bytes

@@ -43,8 +43,15 @@ def _both(ctx, bam, chrom, ws, we, cfg, lcfg, **kw):
     return host, hqn, hinfo, db, dqn, dinfo
 
 
-def test_device_fetch_tagged(gpu_ctx, tmp_path):
+@pytest.mark.parametrize("ring", [None, ("196608", "77777"), ("98304", "98304")])
+def test_device_fetch_tagged(gpu_ctx, tmp_path, monkeypatch, ring):
+    """(ring: the staging ring's segment and read-piece sizes forced small;
+    the fetch's many runs make the pieces run-relative, so segments end where
+    the next piece would overflow a slot.)"""
     from pomfret_amd import Config, LoadConfig
+    if ring:
+        monkeypatch.setenv("PF_INGEST_SEG", ring[0])
+        monkeypatch.setenv("PF_INGEST_PIECE", ring[1])
     aln, recs, bam, vcf = tagged(tmp_path, n_windows=4, coverage=30)
     cfg, lcfg = Config.from_coverage(30, given=False), LoadConfig()
     # the gap windows, plus windows shifted into their neighbours' readback
