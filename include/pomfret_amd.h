@@ -275,10 +275,11 @@ int  pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n);
 int  pf_batch_stats(pf_dbatch_t *db, uint64_t *out, uint64_t n);
 
 /* The greedy problems (w<<1 | dir) this batch runs in pf_k3_heavy, the second
- * greedy kernel on the context's second stream (windows with at least
- * max(600, 1.25 x the batch's median) records; PF_K3_HEAVY_X changes the
- * multiple, PF_K3_HEAVY=n forces the n heaviest problems).  Returns their
- * count (<= cap copied). */
+ * greedy kernel on the context's second stream: windows with at least 2,000
+ * reads (1,100 when the batch's 90th-percentile window has <= 400 reads);
+ * every other problem, heaviest first, runs in the main kernel.
+ * PF_K3_HEAVY_X=x takes x times the median instead, PF_K3_HEAVY=n forces the
+ * n heaviest problems.  Returns their count (<= cap copied). */
 int  pf_batch_heavy(const pf_dbatch_t *db, uint32_t *probs, uint32_t cap);
 
 /* Parity/debug: run K1 only and copy window w's sites (ms->sites_real_poss,

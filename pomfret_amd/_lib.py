@@ -463,7 +463,8 @@ class DeviceBatch:
 
     def heavy_problems(self) -> np.ndarray:
         """Greedy problems (w<<1 | dir) run in pf_k3_heavy: the windows with at
-        least max(600, 1.25 x the median) records (see pf_batch_heavy)."""
+        least 2,000 reads (1,100 when the batch's 90th-percentile window has
+        <= 400), see pf_batch_heavy."""
         n = lib().pf_batch_heavy(self.handle, None, 0)
         out = np.zeros(max(n, 1), np.uint32)
         if n:
