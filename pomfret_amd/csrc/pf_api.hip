@@ -872,6 +872,31 @@ extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cf
         uint64_t *p64; PUT(p64, so_.data(), n + 1); ld.stage_off = p64;
         uint32_t *p32; ALLOC(p32, ld.stage_cap); ld.stage_pos = p32;
         uint8_t *p8; ALLOC(p8, ld.stage_cap); ld.stage_cat = p8;
+        // K0's per-slot record rows (the wave slots' order: longest first)
+        std::vector<uint32_t> ordh(n);
+        for (uint32_t r = 0; r < n; r++) ordh[r] = r;
+        std::stable_sort(ordh.begin(), ordh.end(), [&](uint32_t x, uint32_t y) { return a->l_qseq[x] > a->l_qseq[y]; });
+        std::vector<pf_k0_hdr> hdr(std::max<uint32_t>(n, 1));
+        for (uint32_t k = 0; k < n; k++) {
+            const uint32_t r = ordh[k];
+            pf_k0_hdr &h = hdr[k];
+            memset(&h, 0, sizeof h);
+            h.mm_off = a->mm_off[r]; h.mm_len = (uint32_t)(a->mm_off[r + 1] - a->mm_off[r]);
+            h.ml_off = a->ml_off[r]; h.ml_len = (uint32_t)(a->ml_off[r + 1] - a->ml_off[r]);
+            h.seq_off = seq_off[r];
+            h.cig_off = a->cigar_off[r]; h.ncig = (uint32_t)(a->cigar_off[r + 1] - a->cigar_off[r]);
+            h.stage_off = so_[r]; h.stage_len = (uint32_t)(so_[r + 1] - so_[r]);
+            h.scr_off = scr_off[r]; h.scr_len = (uint32_t)(scr_off[r + 1] - scr_off[r]);
+            h.l_qseq = a->l_qseq[r]; h.pos = a->pos[r]; h.rec = r; h.de = a->de[r];
+            h.flag_mapq = (uint32_t)a->flag[r] | ((uint32_t)a->mapq[r] << 16);
+        }
+        {
+            std::vector<uint32_t> slot_of(n);
+            for (uint32_t k = 0; k < n; k++) slot_of[ordh[k]] = k;
+            for (uint32_t w = 0; w < W; w++)
+                for (uint32_t r = a->win_rec_off[w]; r < a->win_rec_off[w + 1]; r++) hdr[slot_of[r]].rec_win = w;
+        }
+        pf_k0_hdr *ph; PUT(ph, hdr.data(), std::max<uint32_t>(n, 1)); ld.hdr = ph;
     }
     b->W = W; b->R = n; b->N = call_cap;
     b->n_recs = n;

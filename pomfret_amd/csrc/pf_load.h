@@ -55,6 +55,20 @@
 #define PF_IO_N     64            /* u64 calls (scan)                        */
 #define PF_IO_SITES 72            /* u64 site slots the windows need (scan)  */
 
+/* K0's fields of one record, one 128-byte row per wave slot (slots in the
+ * order[] order, longest reads first), so that a wave starts its record with
+ * one coalesced load instead of one cache line per field array at a random
+ * record index (round 4). */
+struct pf_k0_hdr {
+    uint64_t mm_off, ml_off, seq_off, cig_off, stage_off, scr_off;   /* words 0-11 */
+    uint32_t mm_len, ml_len, ncig, stage_len;                        /* 12-15 */
+    uint32_t scr_len, l_qseq, pos, rec;                              /* 16-19 */
+    float de;                                                        /* 20 */
+    uint32_t rec_win;                                                /* 21 */
+    uint32_t flag_mapq;                                              /* 22: flag | mapq << 16 */
+    uint32_t pad[9];
+};
+
 struct pf_load_dev {
     uint32_t n_recs, n_windows;
     uint32_t min_mapq, min_len;
@@ -62,6 +76,7 @@ struct pf_load_dev {
     uint32_t force_seq;              /* test override: every record through the sequential path */
     uint32_t diag;                   /* measurement only (PF_K0_DIAG): 1 = trigger placement reads no SEQ word */
     const uint32_t *order;           /* [n_recs] record of each wave slot: longest reads first */
+    const pf_k0_hdr *hdr;            /* [n_recs] K0's fields of each wave slot's record */
     const uint32_t *rec_win;         /* [n_recs] window of each record */
     const uint32_t *win_order;       /* [W] pack's workgroups: windows with the most records first */
     const uint32_t *win_rec_off;     /* [W+1] records of each window */

@@ -1041,18 +1041,40 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
     return true;
 }
 
+// a record's fields, read from its wave slot's row (pf_k0_hdr) with one
+// coalesced load and moved to scalar registers
+struct K0Rec {
+    uint32_t r, len, flag, mapq, pos, win, mlen, mln, ncig, slen, scr_len;
+    float de;
+    uint64_t mm_off, ml_off, seq_off, cig_off, s_lo, scr_off;
+};
+DEV K0Rec k0_rec(const pf_load_dev &d, uint32_t slot, uint32_t lane) {
+    const uint32_t *hw = reinterpret_cast<const uint32_t *>(d.hdr + slot);
+    const uint32_t v = hw[lane & 31u];
+    auto w32 = [&](uint32_t k) { return rdl(v, k); };
+    auto w64 = [&](uint32_t k) { return ((uint64_t)rdl(v, k + 1) << 32) | rdl(v, k); };
+    K0Rec R;
+    R.mm_off = w64(0); R.ml_off = w64(2); R.seq_off = w64(4); R.cig_off = w64(6); R.s_lo = w64(8); R.scr_off = w64(10);
+    R.mlen = w32(12); R.mln = w32(13); R.ncig = w32(14); R.slen = w32(15);
+    R.scr_len = w32(16); R.len = w32(17); R.pos = w32(18); R.r = w32(19);
+    R.de = __uint_as_float(w32(20)); R.win = w32(21);
+    const uint32_t fm = w32(22);
+    R.flag = fm & 0xFFFFu; R.mapq = fm >> 16;
+    return R;
+}
+
 template <typename TP>
-DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP TB, uint32_t cap, const K0Tgt &t,
+DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, TP TB, uint32_t cap, const K0Tgt &t,
                    bool okm) {
-    const uint32_t len = d.l_qseq[r];
-    const bool rev = (d.flag[r] & 16u) != 0;
-    const uint8_t *mmg = d.mm + d.mm_off[r];
-    const uint32_t mlen = (uint32_t)(d.mm_off[r + 1] - d.mm_off[r]);
-    const uint8_t *ml = d.ml + d.ml_off[r];
-    const uint32_t mln = (uint32_t)(d.ml_off[r + 1] - d.ml_off[r]);
-    const uint8_t *seq = d.seq + d.seq_off[r];
-    const uint32_t *cig = d.cigar + d.cigar_off[r];
-    const uint32_t ncig = (uint32_t)(d.cigar_off[r + 1] - d.cigar_off[r]);
+    const uint32_t r = R.r;
+    const uint32_t len = R.len;
+    const bool rev = (R.flag & 16u) != 0;
+    const uint8_t *mmg = d.mm + R.mm_off;
+    const uint8_t *ml = d.ml + R.ml_off;
+    const uint32_t mln = R.mln;
+    const uint8_t *seq = d.seq + R.seq_off;
+    const uint32_t *cig = d.cigar + R.cig_off;
+    const uint32_t ncig = R.ncig;
 
     bool okmm = okm;
     uint32_t nT = 0, mlq0 = 0xFFFFFFFFu, mlq1 = 0xFFFFFFFFu;
@@ -1114,7 +1136,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     // the arena's tail.  A full tail flags the batch: the bump pointer keeps
     // counting, so it ends at the size the run needs, and the host grows the
     // arena to that and re-runs.
-    const uint64_t s_lo = d.stage_off[r], s_hi = d.stage_off[r + 1];
+    const uint64_t s_lo = R.s_lo, s_hi = R.s_lo + R.slen;
     uint64_t cb = s_lo;
     if (implicit || (uint64_t)nT > s_hi - s_lo) {
         const uint64_t need = (uint64_t)nT + (uint64_t)(len + 1) / 2;
@@ -1132,7 +1154,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
     o.cat = d.stage_cat + cb;
     if (implicit && d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_IMPLICIT], 1ull);
 
-    const uint32_t qs = d.pos[r];
+    const uint32_t qs = R.pos;
     const bool stale = (cig[0] & 15u) == 4u && (TB[nT - 1] >> 2) <= (cig[0] >> 4);
     bool fatal = false, walked = false;
     uint32_t racc = 0;                                // this lane's share of bam_endpos (the wave walk)
@@ -1185,7 +1207,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, uint32_t r, uint32_t lane, TP T
         d.rec_last[r] = o.last;
         d.rec_coff[r] = cb;
         d.rec_n[r] = o.n;
-        const uint32_t w = d.rec_win[r];
+        const uint32_t w = R.win;
         atomicAdd(&d.win_kept[w], 1u);
         atomicAdd(&d.win_calls[w], o.n);
     }
@@ -1198,12 +1220,13 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_e
     const uint32_t wv = uni(threadIdx.x >> 6);
     const uint32_t slot = blockIdx.x * PF_K0_WAVES + wv;
     if (slot >= d.n_recs) return;
-    const uint32_t r = uni(d.order[slot]);
+    const K0Rec R = k0_rec(d, slot, lane);
+    const uint32_t r = R.r;
     K0W &L = lds[wv];
     // filters (1079-1085)
-    const uint32_t flag = d.flag[r];
-    const bool drop = (flag & 4u) || (flag & 256u) || (flag & 2048u) || (uint32_t)d.mapq[r] < d.min_mapq ||
-                      d.l_qseq[r] < 2u || d.l_qseq[r] < d.min_len || (double)d.de[r] > 0.1;
+    const uint32_t flag = R.flag;
+    const bool drop = (flag & 4u) || (flag & 256u) || (flag & 2048u) || R.mapq < d.min_mapq ||
+                      R.len < 2u || R.len < d.min_len || (double)R.de > 0.1;
     if (drop) {
         if (lane == 0) d.rec_n[r] = PF_NONE;
         return;
@@ -1218,16 +1241,13 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_e
     // bound: dorado's h + m entries make it twice the m list, so round 2 sent
     // ~45 % of 60x records to HBM, with every rank, key and binary search of
     // their trigger lists an L2 round trip).
-    const uint8_t *mmg = d.mm + d.mm_off[r];
+    const uint8_t *mmg = d.mm + R.mm_off;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
     K0Tgt t;
-    const bool okm = k0_mm_entries(reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis,
-                                   (uint32_t)(d.mm_off[r + 1] - d.mm_off[r]),
-                                   (uint32_t)(d.ml_off[r + 1] - d.ml_off[r]), lane, t);
-    const uint64_t s0 = d.scr_off[r], s1 = d.scr_off[r + 1];
-    if (s1 == s0 || !okm || uni(t.nd) <= (uint32_t)PF_K0_TCAP)
-        k0_record(d, L, r, lane, L.T, (uint32_t)PF_K0_TCAP, t, okm);
-    else k0_record(d, L, r, lane, d.scr + s0, (uint32_t)(s1 - s0), t, okm);
+    const bool okm = k0_mm_entries(reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis, R.mlen, R.mln, lane, t);
+    if (R.scr_len == 0 || !okm || uni(t.nd) <= (uint32_t)PF_K0_TCAP)
+        k0_record(d, L, R, lane, L.T, (uint32_t)PF_K0_TCAP, t, okm);
+    else k0_record(d, L, R, lane, d.scr + R.scr_off, R.scr_len, t, okm);
 }
 
 // ---------------------------------------------------------------------------
