@@ -822,11 +822,7 @@ extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cf
         PUT(p8, a->hp, n); ld.hp = p8;
         // K0's per-record output
         ALLOC(p32, n); ld.rec_n = p32;
-        ALLOC(p64, n); ld.rec_coff = p64;
-        ALLOC(p32, n); ld.rec_start = p32;
-        ALLOC(p32, n); ld.rec_end = p32;
-        ALLOC(p32, n); ld.rec_first = p32;
-        ALLOC(p32, n); ld.rec_last = p32;
+        ALLOC(p32, 8ull * n); ld.rec_out = p32;
         // window of each record, records per window, per-window totals (kept
         // then calls: one memset per run)
         std::vector<uint32_t> rw(n);

@@ -97,8 +97,8 @@ struct pf_load_dev {
     uint32_t *scr;
     /* K0 output, per record */
     uint32_t *rec_n;                 /* calls of each kept record, PF_NONE when dropped */
-    uint64_t *rec_coff;              /* its slice of the staging arena */
-    uint32_t *rec_start, *rec_end, *rec_first, *rec_last;
+    uint32_t *rec_out;               /* [8 n_recs] a kept record's row (one 32-byte store): start, end
+                                        (bam_endpos), first and last call, staging offset (lo, hi), 0, 0 */
     uint32_t *stage_pos;             /* staging arena: per-record call slices */
     uint8_t *stage_cat;
     const uint64_t *stage_off;       /* [n_recs+1] static slices: each record's trigger bound */

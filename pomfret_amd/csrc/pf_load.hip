@@ -1199,13 +1199,13 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     uint32_t rlen = racc;
     if (!walked)
         for (uint32_t c = lane; c < ncig; c += 64) rlen += k0_refc(cig[c]);
-    rlen = wscan(rlen, lane);
+    rlen = uni(__shfl(wscan(rlen, lane), 63, 64));
+    if (lane < 8) {                                   // the record's row: one 32-byte store
+        const uint32_t v = lane == 0 ? qs : lane == 1 ? qs + rlen : lane == 2 ? o.first : lane == 3 ? o.last
+                         : lane == 4 ? (uint32_t)cb : lane == 5 ? (uint32_t)(cb >> 32) : 0u;
+        d.rec_out[8ull * r + lane] = v;
+    }
     if (lane == 63) {
-        d.rec_start[r] = qs;
-        d.rec_end[r] = qs + rlen;
-        d.rec_first[r] = o.first;
-        d.rec_last[r] = o.last;
-        d.rec_coff[r] = cb;
         d.rec_n[r] = o.n;
         const uint32_t w = R.win;
         atomicAdd(&d.win_kept[w], 1u);
@@ -1364,10 +1364,12 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
         if (keep) {
             const uint32_t ri = rb + kc + ek;
             const uint64_t co = cb + ccarry + ec;
-            d.read_start[ri] = d.rec_start[r];
-            d.read_end[ri] = d.rec_end[r];
-            d.read_first[ri] = d.rec_first[r];
-            d.read_last[ri] = d.rec_last[r];
+            const uint4 ro = reinterpret_cast<const uint4 *>(d.rec_out)[2ull * r];
+            const uint2 rc = reinterpret_cast<const uint2 *>(d.rec_out)[4ull * r + 2];
+            d.read_start[ri] = ro.x;
+            d.read_end[ri] = ro.y;
+            d.read_first[ri] = ro.z;
+            d.read_last[ri] = ro.w;
             d.read_win[ri] = w;
             d.read_rec[ri] = r;
             const uint8_t h = d.hp[r];
@@ -1375,7 +1377,7 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
             d.hp_raw[ri] = h;
             d.read_call_off[ri] = co;
             l_n[ek] = n;
-            l_src[ek] = d.rec_coff[r];
+            l_src[ek] = ((uint64_t)rc.y << 32) | rc.x;
             l_dst[ek] = co;
         }
         __syncthreads();
