@@ -548,8 +548,10 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
         }
         uint32_t pref[ROWS];
         uint32_t run = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < ROWS; i++) {
+        // target counts per lane (word pair) of two rows at a time, one wave
+        // scan for both in 16-bit halves (a row counts at most 64 x 32 = 2048
+        // targets, so the low half never carries)
+        auto count = [&](uint32_t i, uint32_t &c0) {
             const uint32_t w = b * BW + i * RW + 2 * lane;
             const uint64_t xs[2] = {((uint64_t)v[i].y << 32) | v[i].x, ((uint64_t)v[i].w << 32) | v[i].z};
             uint32_t c[2];
@@ -562,12 +564,23 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                     c[h] = (uint32_t)__popcll(z);
                 }
             }
-            const uint32_t cp = c[0] + c[1];
-            const uint32_t inc = wscan(cp, lane);
+            c0 = c[0];
+            return c[0] + c[1];
+        };
+#pragma unroll
+        for (uint32_t i = 0; i < ROWS; i += 2) {
+            uint32_t c0a, c0b;
+            const uint32_t ca = count(i, c0a), cb = count(i + 1, c0b);
+            L.u.s.sc[i * 64 + lane] = (uint8_t)c0a;
+            L.u.s.sc[(i + 1) * 64 + lane] = (uint8_t)c0b;
+            const uint32_t inc = wscan(ca | (cb << 16), lane);
+            const uint32_t tot = uni(__shfl(inc, 63, 64));
             pref[i] = run;
-            L.u.s.sb[i * 64 + lane] = (uint16_t)(run + inc - cp);
-            L.u.s.sc[i * 64 + lane] = (uint8_t)c[0];
-            run += uni(__shfl(inc, 63, 64));
+            L.u.s.sb[i * 64 + lane] = (uint16_t)(run + (inc & 0xFFFFu) - ca);
+            run += tot & 0xFFFFu;
+            pref[i + 1] = run;
+            L.u.s.sb[(i + 1) * 64 + lane] = (uint16_t)(run + (inc >> 16) - cb);
+            run += tot >> 16;
         }
         const uint32_t btot = run;
         // the block's triggers: ranks < carry + btot, from ti on
