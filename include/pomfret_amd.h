@@ -273,6 +273,12 @@ int  pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms, int *n);
  * table, j=6 reads, j=7 sites.  n >= 16*n_windows.  These feed the
  * algorithmic-byte model of DESIGN.md. */
 int  pf_batch_stats(pf_dbatch_t *db, uint64_t *out, uint64_t n);
+/* The greedy loop's slot-list source per (window, direction) of the last
+ * run, out[w*2+dir]: 1 slot lists in LDS, 2 the candidate cache in LDS, 3
+ * slot lists in HBM (the slim loop), 4 the general body (fallback kernel),
+ * 5 the one-wave kernel (pf_k3_wave), 0 no greedy run (no sites).  n >= 2*n_windows.  Tests assert which
+ * variant PF_K3_CACHE forced. */
+int  pf_batch_k3_paths(pf_dbatch_t *db, uint8_t *out, uint64_t n);
 
 /* The greedy problems (w<<1 | dir) this batch runs in pf_k3_heavy, the second
  * greedy kernel on the context's second stream: windows with at least 2,000
@@ -334,10 +340,22 @@ typedef struct pf_gaps {
     uint32_t *drop_start, *drop_end;
 } pf_gaps_t;
 
-/* Parse a (bgzipped or plain) VCF.  Returns PF_OK, PF_ERR_ARG for the
- * reference's fatal input errors (unsorted POS, #CHROM header without 10
- * columns), PF_ERR_NOMEM, or -1 when the file cannot be read. */
+/* Parse a (bgzipped or plain) VCF.  Lines starting with '#' are skipped, as
+ * load_intervals_from_file does (:2023-2026).  Returns PF_OK, PF_ERR_ARG for
+ * the reference's fatal input error (a POS below the previous one,
+ * :1383-1387), PF_ERR_NOMEM, or -1 when the file cannot be read. */
 int  pf_vcf_gaps(const char *vcf_path, int32_t readback, pf_gaps_t **out);
+/* The same loader for any phase-block file main_blockjoin accepts
+ * (blockjoin.c:4661-4666: --tsv, then --gtf, then --vcf): PF_INTERVALS_VCF
+ * (PS blocks, as pf_vcf_gaps), PF_INTERVALS_GTF (block = GTF columns 4/5) or
+ * PF_INTERVALS_TSV (columns 2/3 of "chrom start end"), through insert_gtf_line
+ * (:1305-1345): a gap is [end of a block, start of the next block], the first
+ * block of each contig sets its abs_start (prev_end resets per new contig,
+ * :2098).  Plain or gzipped. */
+#define PF_INTERVALS_VCF 0
+#define PF_INTERVALS_GTF 1
+#define PF_INTERVALS_TSV 2
+int  pf_interval_gaps(const char *path, int32_t format, int32_t readback, pf_gaps_t **out);
 void pf_gaps_free(pf_gaps_t *gaps);
 
 /* `pomfret report` chunk windows of one contig (main_methreport,
@@ -581,13 +599,21 @@ void pf_rescue_map_free(pf_rescue_map_t *map);
  * 1937-1941, 2069-2080): GT "a|b" with a, b in {0,1}; SNP -> X at POS-1;
  * ref longer -> D at POS (len ref-alt, chars ref+1); alt longer -> I at
  * POS-1 (len alt-ref, chars alt+1); equal-length non-SNPs skipped; haptag =
- * GT[0].  Tokens split on runs of tabs as strtok_r does.  Returns PF_OK,
- * PF_ERR_ARG for a #CHROM header without exactly 10 columns, PF_ERR_NOMEM,
- * or -1 when the file cannot be read. */
+ * GT[0].  Tokens split on runs of tabs as strtok_r does; '#' lines skipped
+ * (:2023-2026).  Returns PF_OK, PF_ERR_NOMEM, or -1 when the file cannot be
+ * read. */
 typedef struct pf_known_table {
     pf_known_vars_t vars;
 } pf_known_table_t;
 int  pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t **out);
+/* The tables recover_variant_phase_in_dropped_intervals builds for the run's
+ * contigs (names: the phase-block file's contigs) in one pass over the VCF:
+ * the var_storage branch of load_intervals_from_file (2150-2163), where a
+ * line whose CHROM is not among `names` goes to the table the previous line
+ * went to (skipped before the first match).  With the VCF's own contigs as
+ * `names` (no --gtf / --tsv) out[c] equals pf_vcf_known_vars(names[c]).
+ * out[0..n) are set on PF_OK (free each with pf_known_table_free). */
+int  pf_vcf_known_vars_multi(const char *vcf_path, uint32_t n, const char *const *names, pf_known_table_t **out);
 void pf_known_table_free(pf_known_table_t *t);
 
 /* ------------------------------------------------------------------ */
@@ -648,6 +674,14 @@ typedef struct pf_methphase_opts {
     int32_t verbose;               /* < 0: no progress messages                                */
     int32_t host_fetch;            /* 1: records fetched and decoded on the host (pf_bam_fetch_windows
                                       + pf_batch_upload_aln); 0: the device fetch (pf_batch_upload_bam) */
+    /* --tsv / --gtf phase blocks (main_blockjoin 4661-4666: tsv, then gtf,
+     * then vcf).  NULL or PF_INTERVALS_VCF: the VCF's PS blocks.  With -u the
+     * VCF still names the contigs whose reads are pre-haplotagged (4446) and
+     * the file replaces the intervals (4460-4465); without vcf_path (methphase
+     * only, no -u) no VCF is written (4706). */
+    const char *interval_path;
+    int32_t interval_format;       /* PF_INTERVALS_GTF or PF_INTERVALS_TSV                     */
+    int32_t write_input_tagging;   /* -U (with -u): {prefix}.mp.input_haptag.tsv (4494-4517)  */
 } pf_methphase_opts_t;
 
 typedef struct pf_mp_plan pf_mp_plan_t;
@@ -742,6 +776,7 @@ int  pf_mp_stats(const pf_mp_plan_t *p, pf_mp_stats_t *s);
 
 #define PF_RETAG_METHPHASE 0       /* output_modify_bam (blockjoin.c:3022-3103)   */
 #define PF_RETAG_VARHAPTAG 1       /* main_varhaptag (4737-4836)                  */
+#define PF_RETAG_INPUT_HAPTAG 2    /* methphase -u -U: the TSV alone (4494-4517)  */
 
 /* Every record of bam_in, in file order (sam_itr_querys "."), with HP set
  * to the new haplotag + 1 as bam_aux_update_int does it (an existing
@@ -759,6 +794,9 @@ int  pf_mp_stats(const pf_mp_plan_t *p, pf_mp_stats_t *s);
  *     flip of blk's raw gap at the merged index - 1, carried over until the
  *     next interval is entered, across contigs too (get_flip_status_by_idx).
  *   PF_RETAG_VARHAPTAG: the new tag is raw's (absent: unphased).
+ *   PF_RETAG_INPUT_HAPTAG: as VARHAPTAG with no BAM (bam_out must be NULL)
+ *     and the -U header "#qname\treal_hp\ttagged_hp" ({prefix}.mp.input_haptag.tsv:
+ *     the HP tag's value, the -u table's tag + 1 or 255).
  * level: zlib level (htslib's "w" mode: -1, Z_DEFAULT_COMPRESSION).
  * The iteration stops, as htslib's does, at a record whose CIGAR query
  * length differs from l_qseq.  *n_records: records processed. */

@@ -50,6 +50,7 @@ def lib():
         L.orc_search_arr.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_int]
         L.orc_haptag_reads.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.orc_vcf_gaps.argtypes = [C.c_char_p, C.c_int, C.c_char_p]
+        L.orc_interval_gaps.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_char_p]
         L.orc_load_reads.argtypes = [C.c_void_p, C.c_void_p] + [C.c_void_p] * 8 + [C.c_uint64, C.c_void_p]
         L.orc_load_reads.restype = C.c_int
         L.orc_methphase_aln.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
@@ -127,8 +128,18 @@ def haptag_reads(known: KnownVars, reads: ReadAlnBatch) -> np.ndarray:
 
 
 def vcf_gaps(path: str, readback: int = 50_000):
+    return interval_gaps(path, 0, readback)
+
+
+INTERVALS_VCF, INTERVALS_GTF, INTERVALS_TSV = 0, 1, 2
+
+
+def interval_gaps(path: str, fmt: int = INTERVALS_VCF, readback: int = 50_000):
+    """load_intervals_from_file (blockjoin.c:1977-2176) for a VCF (PS
+    blocks, insert_vcf_line), a GTF (columns 4/5) or a 3-column TSV
+    (insert_gtf_line, :1305-1345), then merge_close_intervals(readback)."""
     with tempfile.NamedTemporaryFile("r", suffix=".txt", delete=True) as tf:
-        n = lib().orc_vcf_gaps(path.encode(), readback, tf.name.encode())
+        n = lib().orc_interval_gaps(path.encode(), int(fmt), readback, tf.name.encode())
         if n < 0:
             raise RuntimeError(f"vcf_gaps failed {n}")
         out, cur = [], None

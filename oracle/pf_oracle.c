@@ -1127,7 +1127,32 @@ static void insert_vcf_line(char *s, const char *chrom, o_ref_t *iv, uint32_t *p
     }
 }
 
+/* insert_gtf_line (:1305-1345): GTF columns 3/4 or TSV columns 1/2 (strtok
+ * tokens); a block's start closes the gap [prev_end, start] when a block was
+ * seen before on this contig, else it is the contig's abs_start; a block's end
+ * becomes prev_end */
+static void insert_gtf_line(char *s, const char *chrom, o_ref_t *iv, uint32_t *prev_end, int is_tsv) {
+    char *save = NULL;
+    char *tok = strtok_r(s, "\t", &save);
+    const int col_s = is_tsv ? 1 : 3, col_e = is_tsv ? 2 : 4;
+    int i = 0, use = 0;
+    while (tok) {
+        if (i == 0) use = strcmp(chrom, tok) == 0;
+        else if (i == col_s && use) {
+            if (*prev_end != UINT32_MAX) { VPUSH(iv->starts, *prev_end); VPUSH(iv->ends, (uint32_t)strtoul(tok, NULL, 10)); }
+            else iv->abs_start = (uint32_t)strtoul(tok, NULL, 10);
+        } else if (i == col_e && use) *prev_end = (uint32_t)strtoul(tok, NULL, 10);
+        tok = strtok_r(NULL, "\t", &save);
+        i++;
+    }
+}
+
 int orc_vcf_gaps(const char *vcf_path, int readback, const char *out_path) {
+    return orc_interval_gaps(vcf_path, 0, readback, out_path);
+}
+
+/* load_intervals_from_file (:1977-2176) for fmt 0 VCF, 1 GTF, 2 TSV */
+int orc_interval_gaps(const char *vcf_path, int fmt, int readback, const char *out_path) {
     gzFile fp = gzopen(vcf_path, "rb");
     if (!fp) return -1;
     size_t m = 1 << 16, n = 0;
@@ -1164,7 +1189,8 @@ int orc_vcf_gaps(const char *vcf_path, int readback, const char *out_path) {
             rp = ref_n++;
             prev_end = UINT32_MAX;     /* prev_group is NOT reset (:2098) */
         }
-        insert_vcf_line(line, refs[rp].name, &refs[rp], &prev_end, &prev_group);
+        if (fmt == 0) insert_vcf_line(line, refs[rp].name, &refs[rp], &prev_end, &prev_group);
+        else insert_gtf_line(line, refs[rp].name, &refs[rp], &prev_end, fmt == 2);
     }
     if (prev_end != UINT32_MAX && rp >= 0) refs[rp].abs_end = prev_end;
     free(all);

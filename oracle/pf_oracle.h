@@ -66,6 +66,8 @@ int orc_haptag_reads(const pf_known_vars_t *known, const pf_read_aln_batch_t *re
  * out_path: "contig\tabs_start\tabs_end\n" then "raw\ts\te", "gap\ts\te",
  * "dropped\ts\te".  Returns number of contigs or <0. */
 int orc_vcf_gaps(const char *vcf_path, int readback, const char *out_path);
+/* fmt 0 VCF, 1 GTF, 2 TSV (load_intervals_from_file, blockjoin.c:1977-2176) */
+int orc_interval_gaps(const char *path, int fmt, int readback, const char *out_path);
 
 /* Window loader (pf_oracle_load.c): filters + 5mC extraction of every
  * record (load_reads_given_interval, blockjoin.c:1043-1173).  Writes the kept

@@ -56,6 +56,7 @@ def lib():
                                            C.POINTER(C.c_float), C.POINTER(C.c_int)]
         L.pf_batch_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.pf_batch_heavy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
+        L.pf_batch_k3_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.pf_batch_debug_sites.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_uint32]
         L.pf_batch_debug_methmers.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
@@ -98,6 +99,7 @@ def _gaps_lib():
     L = lib()
     if not getattr(L, "_pf_gaps_typed", False):
         L.pf_vcf_gaps.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.POINTER(_PfGaps))]
+        L.pf_interval_gaps.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.POINTER(C.POINTER(_PfGaps))]
         L.pf_gaps_free.argtypes = [C.POINTER(_PfGaps)]
         L.pf_phase_blocks.argtypes = [C.POINTER(_PfGaps), C.c_void_p, C.POINTER(C.POINTER(_PfBlocks))]
         L.pf_blocks_free.argtypes = [C.POINTER(_PfBlocks)]
@@ -148,13 +150,18 @@ class _PfRescue(C.Structure):
     _fields_ = [("off", C.c_void_p), ("pos", C.c_void_p), ("hap_of_ref", C.c_void_p)]
 
 
-class Gaps:
-    """Phase-block gaps of a phased VCF (pf_vcf_gaps), owned C object."""
+INTERVALS_VCF, INTERVALS_GTF, INTERVALS_TSV = 0, 1, 2
 
-    def __init__(self, path: str, readback: int = 50_000):
+
+class Gaps:
+    """Phase-block gaps of a phased VCF (pf_vcf_gaps), or of a GTF / 3-column
+    TSV of phase blocks (pf_interval_gaps, fmt INTERVALS_GTF / _TSV), owned C
+    object."""
+
+    def __init__(self, path: str, readback: int = 50_000, fmt: int = INTERVALS_VCF):
         L = _gaps_lib()
         self._p = C.POINTER(_PfGaps)()
-        _check(L.pf_vcf_gaps(path.encode(), readback, C.byref(self._p)), "pf_vcf_gaps")
+        _check(L.pf_interval_gaps(path.encode(), int(fmt), readback, C.byref(self._p)), "pf_interval_gaps")
 
     def contigs(self):
         return _gaps_contigs(self._p)
@@ -234,7 +241,13 @@ class Blocks:
 def vcf_gaps(path: str, readback: int = 50_000):
     """Phase-block gaps of a phased VCF per contig (pf_vcf_gaps): a list of
     dict(name, abs_start, abs_end, raw, gaps, dropped) with (start, end) pairs."""
-    g = Gaps(path, readback)
+    return interval_gaps(path, INTERVALS_VCF, readback)
+
+
+def interval_gaps(path: str, fmt: int = INTERVALS_VCF, readback: int = 50_000):
+    """The gaps of any phase-block file `methphase` takes (pf_interval_gaps):
+    --vcf, --gtf or --tsv (blockjoin.c:1977-2176, 1305-1345)."""
+    g = Gaps(path, readback, fmt)
     res = g.contigs()
     g.close()
     return res
@@ -460,6 +473,14 @@ class DeviceBatch:
         out = np.zeros((max(self.n_windows, 1), 2, 8), np.uint64)
         _check(lib().pf_batch_stats(self.handle, out.ctypes.data, out.size), "pf_batch_stats")
         return out[:self.n_windows]
+
+    def k3_paths(self) -> np.ndarray:
+        """Per-(window, dir) slot-list source of the last run's greedy loop:
+        [W, 2] of 1 LDS lists, 2 candidate cache, 3 HBM lists, 4 general
+        body, 0 no sites (pf_batch_k3_paths)."""
+        out = np.zeros(max(2 * self.n_windows, 2), np.uint8)
+        _check(lib().pf_batch_k3_paths(self.handle, out.ctypes.data, out.size), "pf_batch_k3_paths")
+        return out[:2 * self.n_windows].reshape(-1, 2)
 
     def heavy_problems(self) -> np.ndarray:
         """Greedy problems (w<<1 | dir) run in pf_k3_heavy: the windows with at

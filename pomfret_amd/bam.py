@@ -326,6 +326,17 @@ class BamFile:
         return reads, qnames, info
 
 
+def _known_of(L, t) -> KnownVars:
+    try:
+        v = t.contents.vars
+        n = int(v.n)
+        off = _arr(v.char_off, n + 1, np.uint64)
+        return KnownVars(pos=_arr(v.pos, n, np.uint32), len=_arr(v.len, n, np.uint32), op=_arr(v.op, n, np.uint8),
+                         haptag=_arr(v.haptag, n, np.uint8), char_off=off, chars=_arr(v.chars, off[-1], np.uint8))
+    finally:
+        L.pf_known_table_free(t)
+
+
 def vcf_known_vars(vcf_path: str, contig: str) -> KnownVars:
     """The -u known-variant table of one contig (pf_vcf_known_vars)."""
     L = _bind()
@@ -334,15 +345,24 @@ def vcf_known_vars(vcf_path: str, contig: str) -> KnownVars:
     if rc == -1:
         raise FileNotFoundError(vcf_path)
     _check(rc, "pf_vcf_known_vars")
-    try:
-        v = out.contents.vars
-        n = int(v.n)
-        off = _arr(v.char_off, n + 1, np.uint64)
-        kv = KnownVars(pos=_arr(v.pos, n, np.uint32), len=_arr(v.len, n, np.uint32), op=_arr(v.op, n, np.uint8),
-                       haptag=_arr(v.haptag, n, np.uint8), char_off=off, chars=_arr(v.chars, off[-1], np.uint8))
-    finally:
-        L.pf_known_table_free(out)
-    return kv
+    return _known_of(L, out)
+
+
+def vcf_known_vars_multi(vcf_path: str, names) -> List[KnownVars]:
+    """The rescue's known tables for the phase-block file's contigs in one
+    pass (pf_vcf_known_vars_multi: a CHROM not among `names` goes to the
+    table the previous line went to, blockjoin.c:2150-2163)."""
+    L = _bind()
+    n = len(names)
+    enc = [x.encode() for x in names]
+    arr = (C.c_char_p * max(n, 1))(*enc)
+    outs = (C.POINTER(PfKnownTable) * max(n, 1))()
+    L.pf_vcf_known_vars_multi.argtypes = [C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    rc = L.pf_vcf_known_vars_multi(vcf_path.encode(), n, C.cast(arr, C.c_void_p), C.cast(outs, C.c_void_p))
+    if rc == -1:
+        raise FileNotFoundError(vcf_path)
+    _check(rc, "pf_vcf_known_vars_multi")
+    return [_known_of(L, outs[i]) for i in range(n)]
 
 
 def _qname_tags(table: Dict[str, int]):

@@ -236,10 +236,19 @@ extern "C" int pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches) {
 extern "C" int pf_ctx_device(const pf_ctx *c) { return c->device; }
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c) { return c->stream; }
 extern "C" hipStream_t pf_ctx_stream2(const pf_ctx *c) { return c->stream2; }
+static std::mutex g_stream3_mu;
 extern "C" hipStream_t pf_ctx_stream3(const pf_ctx *c) {
-    // created on first use by the context's own (fetch) thread
+    // created on first use, on the context's device (whatever device the
+    // calling thread has current), under a lock: any thread may ask first
     pf_ctx *m = const_cast<pf_ctx *>(c);
-    if (!m->stream3 && hipStreamCreateWithFlags(&m->stream3, hipStreamNonBlocking) != hipSuccess) m->stream3 = nullptr;
+    std::lock_guard<std::mutex> lk(g_stream3_mu);
+    if (!m->stream3) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != m->device) (void)hipSetDevice(m->device);
+        if (hipStreamCreateWithFlags(&m->stream3, hipStreamNonBlocking) != hipSuccess) m->stream3 = nullptr;
+        if (cur >= 0 && cur != m->device) (void)hipSetDevice(cur);
+    }
     return m->stream3 ? m->stream3 : m->stream;
 }
 
@@ -695,11 +704,15 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     const char *kp = getenv("PF_K3_PATH");
     d.k3_mode = !kp ? 0u : strcmp(kp, "fold") == 0 ? 1u : strcmp(kp, "rows") == 0 ? 2u : 0u;
     {
-        // the greedy loop's slot-list source: 1 auto (all lists in LDS when
-        // they fit, else the candidate cache, else HBM); tests force the
-        // others: 0 no cache, 2 the cache always, 3 HBM lists always
+        // the greedy loop's slot-list source (pf_kernels.hip k3_run: bit 0
+        // allows the candidate cache, a value >= 2 disallows the slot lists in
+        // LDS): auto (all lists in LDS when they fit, else the cache, else
+        // HBM); tests force the others: "0" no cache, "force" the cache
+        // always, "hbm" the HBM lists always
+        enum { K3C_NONE = 0u, K3C_AUTO = 1u, K3C_HBM = 2u, K3C_FORCE = 3u };
         const char *kc = getenv("PF_K3_CACHE");
-        d.k3_cache = !kc ? 1u : !strcmp(kc, "0") ? 0u : !strcmp(kc, "force") ? 2u : !strcmp(kc, "hbm") ? 3u : 1u;
+        d.k3_cache = !kc ? K3C_AUTO : !strcmp(kc, "0") ? K3C_NONE : !strcmp(kc, "force") ? K3C_FORCE
+                   : !strcmp(kc, "hbm") ? K3C_HBM : K3C_AUTO;
     }
     for (int i = 0; i < PF_SLOTS; i++)
         if (hipHostMalloc((void **)&b->h_io[i], b->io_bytes) != hipSuccess) return fail(PF_ERR_NOMEM);
@@ -1382,6 +1395,17 @@ extern "C" int pf_batch_stats(pf_dbatch_t *b, uint64_t *out, uint64_t n) {
     HIPCHK(hipSetDevice(b->ctx->device));
     HIPCHK(hipStreamSynchronize(b->ctx->stream));
     if (b->W) HIPCHK(hipMemcpy(out, b->d.stats, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < 2ull * b->W; i++) out[i * 8 + 2] &= (1ull << 56) - 1;   // the path byte: pf_batch_k3_paths
+    return PF_OK;
+}
+
+extern "C" int pf_batch_k3_paths(pf_dbatch_t *b, uint8_t *out, uint64_t n) {
+    if (!b || !out || n < 2ull * b->W) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    std::vector<uint64_t> st(16ull * b->W + 1);
+    if (b->W) HIPCHK(hipMemcpy(st.data(), b->d.stats, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < 2ull * b->W; i++) out[i] = (uint8_t)(st[i * 8 + 2] >> 56);
     return PF_OK;
 }
 

@@ -1992,10 +1992,12 @@ static int hp_update(const uint8_t *d, uint32_t bs, const rec_t *r, int64_t val,
 int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, const char *tsv_out, int mode,
                  const pf_gaps_t *g, const pf_blocks_t *blk, const pf_tags_t *methphased, const pf_tags_t *raw,
                  int level, uint64_t *n_records) {
-    if (!bam_in || (!bam_out && !tsv_out) || (mode != PF_RETAG_METHPHASE && mode != PF_RETAG_VARHAPTAG))
+    if (!bam_in || (!bam_out && !tsv_out) ||
+        (mode != PF_RETAG_METHPHASE && mode != PF_RETAG_VARHAPTAG && mode != PF_RETAG_INPUT_HAPTAG))
         return PF_ERR_ARG;
     if (mode == PF_RETAG_METHPHASE && (!g || !blk || !methphased)) return PF_ERR_ARG;
-    if (mode == PF_RETAG_VARHAPTAG && !raw) return PF_ERR_ARG;
+    if (mode != PF_RETAG_METHPHASE && !raw) return PF_ERR_ARG;
+    if (mode == PF_RETAG_INPUT_HAPTAG && (bam_out || !tsv_out)) return PF_ERR_ARG;
     if (n_records) *n_records = 0;
     bgzf_t *z = (bgzf_t *)malloc(sizeof(bgzf_t));
     bgzfw_t *w = bam_out ? (bgzfw_t *)calloc(1, sizeof(bgzfw_t)) : NULL;
@@ -2018,6 +2020,7 @@ int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, c
     if (!rc && tsv_out) {
         tsv = fopen(tsv_out, "w");
         if (!tsv) rc = -1;
+        else if (mode == PF_RETAG_INPUT_HAPTAG) fprintf(tsv, "#qname\treal_hp\ttagged_hp\n");   /* 4498 */
         else fprintf(tsv, "#qname\thaptag_input\thaptag_new\n");
     }
     /* header: copied as read, then flushed into its own block (bam_hdr_write) */
@@ -2111,8 +2114,8 @@ int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, c
             hp_raw = h;
         }
         int hp;
-        if (mode == PF_RETAG_VARHAPTAG) {
-            hp = hp_raw;                                 /* st->qname2haptag_raw, 4787-4795 */
+        if (mode != PF_RETAG_METHPHASE) {
+            hp = hp_raw;                                 /* st->qname2haptag_raw, 4787-4795 / 4504-4512 */
         } else {
             if (r.tid != prev_tid) { prev_unphased_idx = 1; prev_tid = r.tid; }
             /* check_if_in_phased_intervals (2406-2426) on the contig's merged gaps */

@@ -14,8 +14,11 @@
  * the BAM output OFF, cli.c:416) are kept.  Added: --gpus G (GPUs driven by
  * this process; default all visible), --host-fetch (records inflated and
  * decoded on the host instead of the device fetch) and --job-windows W (windows per device
- * job).  --gtf / --tsv phase-block inputs are not implemented (an error, not
- * a silent skip).
+ * job).  Phase blocks come from --tsv, else --gtf, else --vcf (main_blockjoin
+ * 4661-4666); with -u the VCF still supplies the variants and the contigs to
+ * pre-haplotag.  -U writes {prefix}.mp.input_haptag.tsv (4494-4517).  --dbg's
+ * {prefix}.mp.dbg.read2tag (2223-2248) lists a khash in bucket order, which
+ * no other implementation reproduces: it is not written (a warning says so).
  */
 #include <getopt.h>
 #include <stdio.h>
@@ -54,6 +57,9 @@ static void help_methphase(const char *prefix) {
     fprintf(stderr, "  -c     [opt] Read coverage (total, not per-haplotap). Will infer if not supplied.\n");
     fprintf(stderr, "  -o     [opt] Name prefix of output files. [%s]\n", prefix);
     fprintf(stderr, "  --vcf  [opt] Input, sorted vcf file containing phased variants. Plain or gz'd.\n");
+    fprintf(stderr, "  --gtf  [opt] Phase blocks as a GTF (e.g. whatshap stats --block-list). Overrides --vcf's.\n");
+    fprintf(stderr, "  --tsv  [opt] Phase blocks as a 3-column tsv (chrom, start, end). Overrides --gtf and --vcf.\n");
+    fprintf(stderr, "  -U,--write-input-tagging [opt] With -u, write {prefix}.mp.input_haptag.tsv.\n");
     fprintf(stderr, "  -u,--bam-is-untagged [opt] If present, will haplotag reads \n"
                     "               with phased variants in vcf first (on the GPU).\n");
     fprintf(stderr, "  -t     [opt] Host threads fetching reads, per GPU. [1]\n");
@@ -81,7 +87,7 @@ static const struct option longopts[] = {
 
 typedef struct {
     int help, threads, lo, hi, readlen, mapq, k, k_span, cov, cov_sel, n_cand, untagged, out_tsv, out_bam;
-    int chunk_size, chunk_stride, gpus, job_windows, verbose, host_fetch;
+    int chunk_size, chunk_stride, gpus, job_windows, verbose, host_fetch, write_input_tagging, dbg;
     char *prefix, *vcf, *gtf, *tsv, *bam;
 } cli_t;
 
@@ -113,10 +119,10 @@ static int parse(int argc, char **argv, cli_t *c) {
         case O_OTSV: c->out_tsv = 1; break;
         case 'T': case O_BAMT: break;
         case 'u': case O_UNTAG: c->untagged = 1; break;
-        case 'U': case O_WIT: break;
+        case 'U': case O_WIT: c->write_input_tagging = 1; break;
         case O_CSIZE: c->chunk_size = atoi(optarg); break;
         case O_CSTRIDE: c->chunk_stride = atoi(optarg); break;
-        case O_DBG: break;
+        case O_DBG: c->dbg = 1; break;
         case O_GPUS: c->gpus = atoi(optarg); break;
         case O_JOBW: c->job_windows = atoi(optarg); break;
         case O_HFETCH: c->host_fetch = 1; break;
@@ -157,10 +163,12 @@ static int sancheck(cli_t *c) {                       /* sancheck_cliopt, cli.c:
         fprintf(stderr, "[E::sancheck_cliopt] invalid chunk size or stride\n");
         return 1;
     }
-    if (c->gtf || c->tsv) {
-        fprintf(stderr, "[E::pomfret-amd] --gtf / --tsv phase-block inputs are not implemented; use --vcf\n");
-        return 1;
-    }
+    if ((c->gtf ? 1 : 0) + (c->tsv ? 1 : 0) + (c->vcf ? 1 : 0) > 1)
+        fprintf(stderr, "[M::sancheck_cliopt] multiple phase block files. Will not resolve conflict, only total "
+                        "override (order is always: tsv > gtf > vcf)\n");
+    if (c->dbg)
+        fprintf(stderr, "[W::pomfret-amd] --dbg: {prefix}.mp.dbg.read2tag (a hash table dump in bucket order) is "
+                        "not written\n");
     return 0;
 }
 
@@ -260,6 +268,11 @@ int main(int argc, char **argv) {
     o.job_windows = c.job_windows > 0 ? (uint32_t)c.job_windows : 0;
     o.host_fetch = c.host_fetch;
     o.verbose = c.verbose;
+    if (!report && (c.tsv || c.gtf)) {         /* tsv > gtf > vcf (4661-4666) */
+        o.interval_path = c.tsv ? c.tsv : c.gtf;
+        o.interval_format = c.tsv ? PF_INTERVALS_TSV : PF_INTERVALS_GTF;
+    }
+    o.write_input_tagging = c.write_input_tagging;
     pf_mp_plan_t *p = NULL;
     const int rc = pf_methphase_main(&o, &p);
     if (rc) {

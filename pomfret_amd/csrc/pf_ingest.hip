@@ -680,8 +680,9 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             d_arena = a2;
         }
         if (!rc) rc = send(d_arena, true);
-        // the slots' copies are done before the staging buffer is reused
-        if (!rc && hipStreamSynchronize(cs) != hipSuccess) rc = PF_ERR_HIP;
+        // the slots' copies are done before the staging buffer is reused --
+        // on the error exits too (the context keeps the stage for its next fetch)
+        if (hipStreamSynchronize(cs) != hipSuccess && !rc) rc = PF_ERR_HIP;
         if (!rc && batches.empty() && hipEventRecord(ev[0], st) != hipSuccess) rc = PF_ERR_HIP;
         if (!rc && (hipEventRecord(ecp, cs) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess ||
                     hipEventRecord(ecp, s3) != hipSuccess || hipStreamWaitEvent(st, ecp, 0) != hipSuccess ||

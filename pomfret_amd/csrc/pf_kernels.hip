@@ -1249,7 +1249,7 @@ struct K3Ctl {
     uint32_t S, R, ntot, nc, L, done, failed, inserted, winner, tag;
     int32_t i_last;
     uint32_t min_i, max_i, fail, summ, nstrict, mxlen, cmax;
-    uint32_t path, need;                      // (profile build) the P2 variant taken and its LDS bytes
+    uint32_t path, need;                      // the P2 variant taken (K3_PATH_*); (profile build) its LDS bytes
     unsigned long long t_run;                 // (profile build) s_memrealtime at k3_run's start
     uint32_t ins_n, ins_st, ins_mo, ins_tg;   // register variant: winner whose insert is pending
     unsigned long long scr;
@@ -2095,7 +2095,8 @@ DEV void k3_finish(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0,
     if (lane < 4) d.table[((uint64_t)w * 2 + dir) * 4 + lane] = (int32_t)tsum[lane];
     if (lane == 0) {
         unsigned long long *sp = d.stats + ((uint64_t)w * 2 + dir) * PF_NSTAT;
-        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
+        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[3] = stx.scanned;
+        sp[2] = stx.iters | ((unsigned long long)ctl.path << 56);      // the slot-list source in the top byte
         sp[4] = ctl.summ; sp[5] = tsum[4]; sp[6] = R; sp[7] = S;
     }
 }
@@ -3151,13 +3152,14 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     }
     k3_dict_rewrite<NT>(d, r0, R, S, dir, masks, mbase);
     const uint32_t *kb = d.keys + kbase;
-#ifdef PF_K3_PROFILE
     if (tid == 0) {
-        // 1 slot lists in LDS, 2 the candidate cache, 3 slot lists in HBM (slim loop); 4 the general body
+        // 1 slot lists in LDS, 2 the candidate cache, 3 slot lists in HBM (slim loop); 4 the general body;
+        // reported with the problem's stats (pf_batch_k3_paths)
         ctl.path = !slim_fit ? 4u : (lists_ok && slim_s <= lds) ? 1u : (cache_ok && slim_c <= lds) ? 2u : 3u;
+#ifdef PF_K3_PROFILE
         ctl.need = (uint32_t)(cache_ok ? slim_c : ctl.path == 1 ? slim_s : slim_n);   // the cache layout's need
-    }
 #endif
+    }
     if (slim_fit) {
         K3Mem m;
         uint32_t *qq = qb ? qb : cd.read;
@@ -3715,7 +3717,8 @@ DEV void k3w_finish(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_t r0
     if (lane < 4) d.table[((uint64_t)w * 2 + dir) * 4 + lane] = (int32_t)tsum[lane];
     if (lane == 0) {
         unsigned long long *sp = d.stats + ((uint64_t)w * 2 + dir) * PF_NSTAT;
-        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[2] = stx.iters; sp[3] = stx.scanned;
+        sp[0] = stx.lookups; sp[1] = stx.inserts; sp[3] = stx.scanned;
+        sp[2] = stx.iters | (5ull << 56);                              // the slot-list source: the one-wave kernel
         sp[4] = summ; sp[5] = tsum[4]; sp[6] = R; sp[7] = S;
     }
 }

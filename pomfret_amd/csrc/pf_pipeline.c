@@ -4,7 +4,10 @@
  *
  * Reference structure (line numbers: /root/reference/blockjoin.c):
  *   main_blockjoin (4643-4736) -> blockjoin_parallel (4427-4641):
- *     load_intervals_from_file + merge_close_intervals      -> pf_vcf_gaps
+ *     load_intervals_from_file + merge_close_intervals      -> pf_interval_gaps
+ *       (--tsv, then --gtf, then --vcf, 4661-4666; with -u the VCF names
+ *        the pre-pass contigs and a GTF/TSV then overrides the intervals,
+ *        4445-4465)
  *     (-u) pre_haplotagging_read_in_one_ref per contig (1841-1898),
  *          qname first-wins per contig, merged in contig order     -> K4 jobs
  *     estimate_read_coverage_dirtyfast when -c is absent (4547)     -> pf_bam_estimate_coverage_dev
@@ -216,8 +219,12 @@ int pf_ctx_device(const pf_ctx_t *ctx);
 struct pf_mp_plan {
     pf_methphase_opts_t o;
     char *bam_path, *vcf_path, *out_prefix;
-    pf_gaps_t *gaps;
+    pf_gaps_t *gaps;           /* the windows' phase blocks: --tsv / --gtf / --vcf */
     uint32_t n_contigs;
+    pf_gaps_t *ugaps_own;      /* -u with --gtf / --tsv: the VCF's own gaps */
+    const pf_gaps_t *ug;       /* contigs of the -u pre-pass (the VCF's): ugaps_own or gaps */
+    int32_t *utid;             /* [ug->n_contigs] their BAM tids or -1 */
+    char *interval_path;
     int32_t *tid;              /* [n_contigs] BAM tid or -1 */
     pf_cfg_t *cfg;             /* [n_contigs] */
     uint32_t n_windows;
@@ -304,7 +311,9 @@ void pf_mp_free(pf_mp_plan_t *p) {
     pf_tags_free(p->qname_hp);
     if (p->blocks) pf_blocks_free(p->blocks);
     if (p->gaps) pf_gaps_free(p->gaps);
-    free(p->bam_path); free(p->vcf_path); free(p->out_prefix);
+    if (p->ugaps_own) pf_gaps_free(p->ugaps_own);
+    free(p->utid);
+    free(p->bam_path); free(p->vcf_path); free(p->out_prefix); free(p->interval_path);
     free(p->ucov); free(p->utrunc); free(p->uhave);
     pthread_mutex_destroy(&p->st_mu);
     free(p);
@@ -360,9 +369,22 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
 
 int pf_mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out) { return mp_plan(o, out, 0); }
 
+/* the phase-block file the windows come from (main_blockjoin 4661-4666) */
+static int interval_file(const pf_methphase_opts_t *o, const char **path) {
+    if (o->interval_path && o->interval_format != PF_INTERVALS_VCF) { *path = o->interval_path; return o->interval_format; }
+    *path = o->vcf_path;
+    return PF_INTERVALS_VCF;
+}
+
 static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_est) {
-    if (!o || !out || !o->bam_path || !o->vcf_path) return PF_ERR_ARG;
+    if (!o || !out || !o->bam_path) return PF_ERR_ARG;
     if (o->mode != PF_MODE_METHPHASE && o->mode != PF_MODE_REPORT) return PF_ERR_ARG;
+    const char *ipath = NULL;
+    const int ifmt = interval_file(o, &ipath);
+    if (!ipath || ifmt < PF_INTERVALS_VCF || ifmt > PF_INTERVALS_TSV) return PF_ERR_ARG;
+    /* -u needs the VCF's variants; report reads only the VCF (main_methreport 4916-4919) */
+    if ((o->untagged || o->mode == PF_MODE_REPORT) && !o->vcf_path) return PF_ERR_ARG;
+    if (o->mode == PF_MODE_REPORT && ifmt != PF_INTERVALS_VCF) return PF_ERR_ARG;
     if (o->mode == PF_MODE_REPORT && (o->chunk_size <= 0 || o->chunk_stride <= 0)) return PF_ERR_ARG;
     *out = NULL;
     const double t_plan0 = now_s();
@@ -373,13 +395,21 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
     p->bam_path = dupstr(o->bam_path);
     p->vcf_path = dupstr(o->vcf_path);
     p->out_prefix = dupstr(o->out_prefix);
+    p->interval_path = dupstr(o->interval_path);
     p->o.bam_path = p->bam_path;
     p->o.vcf_path = p->vcf_path;
     p->o.out_prefix = p->out_prefix;
+    p->o.interval_path = p->interval_path;
     p->o.ctxs = NULL;
     p->o.n_ctxs = 0;
-    int rc = pf_vcf_gaps(o->vcf_path, PF_READBACK, &p->gaps);
+    /* -u: the VCF's contigs are pre-haplotagged (load_intervals_from_file with
+     * load_vcf_variants_too, 4446); a GTF / TSV then replaces the intervals
+     * (wipe_intervals_of_storage_t + reload, 4460-4465) */
+    int rc = PF_OK;
+    if (o->untagged && ifmt != PF_INTERVALS_VCF) rc = pf_vcf_gaps(o->vcf_path, PF_READBACK, &p->ugaps_own);
+    if (!rc) rc = pf_interval_gaps(ipath, ifmt, PF_READBACK, &p->gaps);
     if (rc) { pf_mp_free(p); return rc; }
+    p->ug = p->ugaps_own ? p->ugaps_own : p->gaps;
     const pf_gaps_t *g = p->gaps;
     const uint32_t C = g->n_contigs;
     p->n_contigs = C;
@@ -389,7 +419,11 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
     p->ucov = (int32_t *)calloc(C ? C : 1, sizeof(int32_t));
     p->utrunc = (int32_t *)calloc(C ? C : 1, sizeof(int32_t));
     p->uhave = (uint8_t *)calloc(C ? C : 1, 1);
-    if (!p->tid || !p->cfg || !p->win_off || !p->ucov || !p->utrunc || !p->uhave) { pf_mp_free(p); return PF_ERR_NOMEM; }
+    p->utid = (int32_t *)calloc(p->ug->n_contigs ? p->ug->n_contigs : 1, sizeof(int32_t));
+    if (!p->tid || !p->cfg || !p->win_off || !p->ucov || !p->utrunc || !p->uhave || !p->utid) {
+        pf_mp_free(p);
+        return PF_ERR_NOMEM;
+    }
 
     pf_bam_t *bam = NULL;
     rc = pf_bam_open(o->bam_path, NULL, &bam);
@@ -400,7 +434,7 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
     const int need_est = o->mode == PF_MODE_METHPHASE ? o->cov_for_selection <= 0 : o->cov <= 0;
     const double t_est0 = now_s();
     p->est_deferred = need_est && defer_est && o->mode == PF_MODE_METHPHASE && o->untagged && !o->host_fetch &&
-                      o->n_ctxs > 0;
+                      o->n_ctxs > 0 && p->ug == p->gaps;
     if (need_est) {
         covs = (int32_t *)calloc(nt > 0 ? nt : 1, sizeof(int32_t));
         if (!covs) rc = PF_ERR_NOMEM;
@@ -421,6 +455,7 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
     p->st.s_estimate = now_s() - t_est0;
     /* windows: merged gaps (methphase) or report chunks of the raw gaps */
     uint64_t nw = 0, cap = 0;
+    for (uint32_t c = 0; c < p->ug->n_contigs; c++) p->utid[c] = pf_bam_tid(bam, p->ug->names[c]);
     for (uint32_t c = 0; c < C && !rc; c++) {
         p->tid[c] = pf_bam_tid(bam, g->names[c]);
         pf_cfg_t *cf = &p->cfg[c];
@@ -511,18 +546,19 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
     }
     p->n_jobs = nj;
     rc = lpt(p->jobs, nj, o->world, &p->order);
-    /* -u pre-pass jobs: one per contig present in the BAM (cost: contig length) */
+    /* -u pre-pass jobs: one per VCF contig present in the BAM (cost: contig length) */
     if (!rc && o->untagged) {
-        p->ujobs = (job_t *)calloc(C ? C : 1, sizeof(job_t));
+        const uint32_t UC = p->ug->n_contigs;
+        p->ujobs = (job_t *)calloc(UC ? UC : 1, sizeof(job_t));
         if (!p->ujobs) rc = PF_ERR_NOMEM;
         uint32_t nu = 0;
         pf_bam_t *b2 = NULL;
         if (!rc) rc = pf_bam_open(o->bam_path, NULL, &b2);
-        for (uint32_t c = 0; c < C && !rc; c++) {
-            if (p->tid[c] < 0) continue;
+        for (uint32_t c = 0; c < UC && !rc; c++) {
+            if (p->utid[c] < 0) continue;
             job_t *J = &p->ujobs[nu++];
             J->contig = c;
-            J->cost = (double)pf_bam_target_len(b2, p->tid[c]);
+            J->cost = (double)pf_bam_target_len(b2, p->utid[c]);
         }
         if (b2) pf_bam_close(b2);
         p->n_ujobs = nu;
@@ -558,14 +594,15 @@ int pf_mp_job_info(const pf_mp_plan_t *p, int kind, uint32_t j, pf_mp_job_info_t
     uint32_t pos = 0;
     for (uint32_t i = 0; i < n; i++) if (ord[i] == j) { pos = i; break; }
     info->contig = J->contig;
-    info->contig_name = p->gaps->names[J->contig];
+    info->contig_name = (kind == PF_JOB_HAPTAG ? p->ug : p->gaps)->names[J->contig];
     info->w0 = J->w0;
     info->w1 = J->w1;
     info->rank = J->rank;
     info->lpt_pos = pos;
     info->cost = J->cost;
     info->done = J->done;
-    info->cfg = p->cfg[J->contig];
+    if (kind == PF_JOB_HAPTAG && p->ug != p->gaps) memset(&info->cfg, 0, sizeof info->cfg);
+    else info->cfg = p->cfg[J->contig];
     return PF_OK;
 }
 
@@ -700,7 +737,7 @@ static int ent_push(entlist_t *e, const char *nm, size_t l, uint8_t hp) {
 int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
     job_t *J = job_of(p, PF_JOB_HAPTAG, j);
     if (!J || !ctx) return PF_ERR_ARG;
-    const char *contig = p->gaps->names[J->contig];
+    const char *contig = p->ug->names[J->contig];
     pf_known_table_t *kt = NULL;
     pf_bam_t *bam = NULL;
     pf_bam_reads_t *rd = NULL;
@@ -767,15 +804,16 @@ int pf_mp_merge_raw(pf_mp_plan_t *p) {
     const double t0 = now_s();
     /* contig order, first wins across contigs (the -u table is one hash
      * filled contig by contig, 2069-2080) */
-    uint32_t *by_contig = (uint32_t *)malloc((p->n_contigs ? p->n_contigs : 1) * sizeof(uint32_t));
+    const uint32_t UC = p->ug->n_contigs;
+    uint32_t *by_contig = (uint32_t *)malloc((UC ? UC : 1) * sizeof(uint32_t));
     if (!by_contig) return PF_ERR_NOMEM;
-    for (uint32_t c = 0; c < p->n_contigs; c++) by_contig[c] = UINT32_MAX;
+    for (uint32_t c = 0; c < UC; c++) by_contig[c] = UINT32_MAX;
     for (uint32_t j = 0; j < p->n_ujobs; j++) {
         if (!p->ujobs[j].done) { free(by_contig); return PF_ERR_ARG; }
         by_contig[p->ujobs[j].contig] = j;
     }
     int rc = PF_OK;
-    for (uint32_t c = 0; c < p->n_contigs && !rc; c++) {
+    for (uint32_t c = 0; c < UC && !rc; c++) {
         if (by_contig[c] == UINT32_MAX) continue;
         const job_t *J = &p->ujobs[by_contig[c]];
         if (J->n_ent > UINT32_MAX) { rc = PF_ERR_LIMIT; break; }
@@ -1117,6 +1155,13 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
         rc = pf_write_tsv(p->gaps, p->blocks, fn);
         if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] tsv written.\n");
     }
+    /* -U: {prefix}.mp.input_haptag.tsv (4494-4517), every record of the BAM */
+    if (!rc && p->o.untagged && p->o.write_input_tagging) {
+        snprintf(fn, L, "%s.mp.input_haptag.tsv", p->out_prefix);
+        rc = pf_retag_bam(p->bam_path, NULL, NULL, fn, PF_RETAG_INPUT_HAPTAG, NULL, NULL, NULL, p->raw, -1, NULL);
+    }
+    /* the VCF only when --vcf was given (4706) */
+    if (rc || !p->vcf_path) { free(fn); return rc; }
     /* rescue of dropped-interval sites (recover_variant_phase_in_dropped_intervals) + VCF */
     const uint32_t C = p->n_contigs;
     uint64_t *roff = (uint64_t *)calloc(C + 1, sizeof(uint64_t));
@@ -1140,16 +1185,27 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
     const pf_known_vars_t **kvs = (const pf_known_vars_t **)calloc(C ? C : 1, sizeof(pf_known_vars_t *));
     pf_rescue_map_t **maps = (pf_rescue_map_t **)calloc(C ? C : 1, sizeof(pf_rescue_map_t *));
     if (!rc && (!rn_names || !rn_nd || !rn_c || !rn_ds || !rn_de || !kts || !kvs || !maps)) rc = PF_ERR_NOMEM;
-    for (uint32_t c = 0; c < C && !rc; c++) {
+    /* one pass over the VCF for every contig's known table, with the
+     * reference's attribution of lines to the phase-block file's contigs */
+    pf_known_table_t **kall = NULL;
+    int need = 0;
+    for (uint32_t c = 0; c < C; c++) need |= g->drop_off[c + 1] > g->drop_off[c] && p->tid[c] >= 0;
+    if (!rc && need) {
+        kall = (pf_known_table_t **)calloc(C, sizeof(pf_known_table_t *));
+        rc = kall ? pf_vcf_known_vars_multi(p->vcf_path, C, (const char *const *)g->names, kall) : PF_ERR_NOMEM;
+    }
+    for (uint32_t c = 0; c < C && !rc && need; c++) {
         const uint64_t nd = g->drop_off[c + 1] - g->drop_off[c];
         if (!nd || p->tid[c] < 0) continue;
-        rc = pf_vcf_known_vars(p->vcf_path, g->names[c], &kts[nr]);
-        if (rc) break;
+        kts[nr] = kall[c];
+        kall[c] = NULL;
         rn_names[nr] = g->names[c]; rn_nd[nr] = (uint32_t)nd; rn_c[nr] = c;
         rn_ds[nr] = g->drop_start + g->drop_off[c]; rn_de[nr] = g->drop_end + g->drop_off[c];
         kvs[nr] = &kts[nr]->vars;
         nr++;
     }
+    for (uint32_t c = 0; kall && c < C; c++) pf_known_table_free(kall[c]);
+    free(kall);
     if (!rc && nr) rc = pf_bam_open(p->bam_path, NULL, &bam);
     if (!rc && nr)
         rc = pf_rescue_dropped_multi(bam, nr, rn_names, rn_nd, rn_ds, rn_de, kvs, &tm, p->o.untagged ? &tr : NULL,
@@ -1610,6 +1666,22 @@ static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
     }
     pf_mp_plan_t *p = NULL;
     int rc = mp_plan(o, &p, 1);
+    if (!rc && o->mode == PF_MODE_METHPHASE) {
+        /* blockjoin_parallel's terminations (4450-4458, 4470-4477): counted on
+         * the raw gaps, before merging */
+        const pf_gaps_t *gs[2] = {o->untagged ? p->ug : NULL, p->gaps};
+        for (int k = 0; k < 2 && !rc; k++) {
+            if (!gs[k]) continue;
+            if (gs[k]->raw_off[gs[k]->n_contigs] == 0) {
+                fprintf(stderr, k == 0 ? "[E::blockjoin_parallel] Nothing loaded from vcf (ref_n=%u), cannot haptag "
+                                         "the input bam. Terminating.\n"
+                                       : "[E::blockjoin_parallel] No intervals loaded, terminating.%.0u\n",
+                        gs[k]->n_contigs);
+                rc = PF_ERR_ARG;
+            }
+        }
+        if (rc) { pf_mp_free(p); p = NULL; }
+    }
     /* the -u pre-pass's whole-contig arenas stay on the device for the window
      * jobs of the same context (device fetch only) */
     const int keep = !rc && o->untagged && !o->host_fetch && o->n_ctxs > 0;

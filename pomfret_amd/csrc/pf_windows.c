@@ -17,14 +17,26 @@
  *     reader only handles complete lines);
  *   - merging compares (start_i - end_j) as uint32 against the threshold, so
  *     an out-of-order start never merges.
+ * Every line starting with '#' is skipped before insert_vcf_line sees it
+ * (:2023-2026), so the #CHROM column check of insert_vcf_line (:1355-1371) is
+ * never reached on this path (the VCF writer keeps it, alter_vcf_line).
  * Fatal exits of the reference become error codes: PF_ERR_ARG for an
- * unsorted POS within a contig (:1383-1387) or a #CHROM header without
- * exactly 10 columns (:1361-1368), PF_ERR_NOMEM, -1 for an unreadable file.
- * Differences (reference UB): a PS value longer than 10 characters is cut at
- * 10 (the reference overflows char[11]); a sample column with fewer fields
- * than FORMAT's PS index counts as PS "." (the reference reads
- * uninitialised values); empty lines are skipped (the reference calls
- * strlen(NULL)).
+ * unsorted POS within a contig (:1383-1387), PF_ERR_NOMEM, -1 for an
+ * unreadable file.  Differences (reference UB): a PS value longer than 10
+ * characters is cut at 10 (the reference overflows char[11]); a sample
+ * column with fewer fields than FORMAT's PS index counts as PS "." (the
+ * reference reads uninitialised values); empty (or all-tab) lines are skipped
+ * (the reference calls strlen(NULL)).
+ *
+ * pf_interval_gaps: the same loader on a GTF (`--gtf`, e.g. whatshap stats
+ * --block-list output) or a 3-column TSV (`--tsv`): insert_gtf_line
+ * (:1305-1345) on columns 3/4 (GTF) or 1/2 (TSV) of the strtok tokens.  A
+ * block's start closes the gap [end of the previous block, this start] when
+ * the contig has seen a block, else it sets the contig's abs_start; its end
+ * becomes the previous end.  The previous end is reset at every new contig
+ * name (:2098), so unlike the VCF path every contig gets its own abs_start; a
+ * contig name seen again only switches back (its gaps continue from the
+ * other contig's last end, as the reference's shared prev_end does).
  *
  * pf_report_windows: the chunk windows of `pomfret report` (main_methreport,
  * :4963-4991): per contig, for each raw gap [start, end] in order with prev
@@ -66,7 +78,8 @@ typedef struct {
     contig_t *c;
     size_t n, m;
     int cur;            /* index of the contig lines are attributed to */
-    uint32_t prev_pos, prev_group;
+    uint32_t prev_pos, prev_group;   /* prev_pos is the GTF/TSV path's prev_end */
+    int fmt;            /* PF_INTERVALS_* */
 } gap_state_t;
 
 /* the idx-th ':'-separated field of [s, s+l) */
@@ -99,13 +112,21 @@ static int index_of_ps(const char *s, size_t l) {
 }
 
 static uint32_t parse_u32(const char *s, size_t l) {
-    /* strtoul semantics on a token: leading digits, truncated to 32 bits */
+    /* (uint32_t)strtoul(token, NULL, 10): leading white space, an optional
+     * sign (a '-' negates in unsigned arithmetic), the leading digits;
+     * ULONG_MAX on overflow */
     unsigned long v = 0;
+    int neg = 0, over = 0;
     size_t i = 0;
-    while (i < l && (s[i] == ' ' || s[i] == '\t')) i++;
-    if (i < l && s[i] == '+') i++;
-    for (; i < l && s[i] >= '0' && s[i] <= '9'; i++) v = v * 10 + (unsigned long)(s[i] - '0');
-    return (uint32_t)v;
+    while (i < l && (s[i] == ' ' || (s[i] >= '\t' && s[i] <= '\r'))) i++;
+    if (i < l && (s[i] == '+' || s[i] == '-')) neg = s[i++] == '-';
+    for (; i < l && s[i] >= '0' && s[i] <= '9'; i++) {
+        const unsigned long d = (unsigned long)(s[i] - '0');
+        if (v > (~0ul - d) / 10) over = 1;
+        v = v * 10 + d;
+    }
+    if (over) return (uint32_t)~0ul;
+    return (uint32_t)(neg ? 0ul - v : v);
 }
 
 static int new_contig(gap_state_t *g, const char *name, size_t l) {
@@ -129,13 +150,7 @@ static int new_contig(gap_state_t *g, const char *name, size_t l) {
 
 /* one complete data line (no '\n'); returns 0, PF_ERR_ARG or PF_ERR_NOMEM */
 static int gap_line(gap_state_t *g, const char *s, size_t l) {
-    if (l == 0) return 0;
-    if (s[0] == '#') {
-        if (l > 1 && s[1] == '#') return 0;
-        int n = 1;                                       /* #CHROM header: column count */
-        for (size_t i = 0; i < l; i++) n += s[i] == '\t';
-        return n == 10 ? 0 : PF_ERR_ARG;
-    }
+    if (l == 0 || s[0] == '#') return 0;                 /* :2023-2026 */
     /* split on tabs (empty tokens are skipped, as strtok does) */
     const char *tok[10];
     size_t tl[10];
@@ -165,8 +180,21 @@ static int gap_line(gap_state_t *g, const char *s, size_t l) {
         if (new_contig(g, tok[0], tl[0])) return PF_ERR_NOMEM;
         g->prev_pos = UINT32_MAX;
     }
-    /* insert_vcf_line (:1348-1430) */
     contig_t *c = &g->c[g->cur];
+    if (g->fmt != PF_INTERVALS_VCF) {                    /* insert_gtf_line (:1305-1345) */
+        const int cs = g->fmt == PF_INTERVALS_TSV ? 1 : 3, ce = cs + 1;
+        if (nt > cs) {
+            const uint32_t v = parse_u32(tok[cs], tl[cs]);
+            if (g->prev_pos != UINT32_MAX) {
+                if (u32v_push(&c->s, g->prev_pos) || u32v_push(&c->e, v)) return PF_ERR_NOMEM;
+            } else {
+                c->abs_start = v;
+            }
+        }
+        if (nt > ce) g->prev_pos = parse_u32(tok[ce], tl[ce]);
+        return 0;
+    }
+    /* insert_vcf_line (:1348-1430) */
     uint32_t pos = 0;
     if (nt > 1) {
         pos = parse_u32(tok[1], tl[1]);
@@ -206,12 +234,17 @@ static void free_state(gap_state_t *g) {
 }
 
 int pf_vcf_gaps(const char *vcf_path, int32_t readback, pf_gaps_t **out) {
-    if (!vcf_path || !out) return PF_ERR_ARG;
+    return pf_interval_gaps(vcf_path, PF_INTERVALS_VCF, readback, out);
+}
+
+int pf_interval_gaps(const char *path, int32_t format, int32_t readback, pf_gaps_t **out) {
+    if (!path || !out || format < PF_INTERVALS_VCF || format > PF_INTERVALS_TSV) return PF_ERR_ARG;
     *out = NULL;
-    gzFile fp = gzopen(vcf_path, "rb");
+    gzFile fp = gzopen(path, "rb");
     if (!fp) return -1;
     gap_state_t g;
     memset(&g, 0, sizeof(g));
+    g.fmt = format;
     g.cur = -1;
     g.prev_pos = UINT32_MAX;
     g.prev_group = UINT32_MAX;
@@ -356,7 +389,10 @@ int64_t pf_report_windows(uint32_t abs_start, const uint32_t *gap_start, const u
  * its chars from REF+1, an insertion its chars from ALT+1 (a multi-allelic
  * ALT is one string here too, commas included); chars are seq_nt4 codes
  * (A0 C1 G2 T3, else 4).  A sample column with fewer fields than FORMAT's
- * GT index is skipped (the reference reads uninitialised values). */
+ * GT index is skipped (the reference reads uninitialised values).  Lines
+ * starting with '#' never reach insert_variant_from_vcf_line on the paths
+ * that collect variants (load_intervals_from_file, :2023-2026), so its
+ * #CHROM column check (:1441-1455) is not applied. */
 typedef struct {
     u32v pos, len, hp;
     uint8_t *op;
@@ -389,17 +425,7 @@ static uint8_t nt4(char c) {
 }
 
 static int known_line(known_acc_t *K, const char *contig, const char *s, size_t l) {
-    if (l > 0 && s[0] == '#') {
-        if (l > 1 && s[1] == '#') return 0;
-        int n = 0;                                   /* strtok token count */
-        for (size_t i = 0; i < l;) {
-            while (i < l && s[i] == '\t') i++;
-            if (i >= l) break;
-            n++;
-            while (i < l && s[i] != '\t') i++;
-        }
-        return n == 10 ? 0 : PF_ERR_ARG;
-    }
+    if (l > 0 && s[0] == '#') return 0;              /* skipped by the caller (:2023-2026) */
     const char *tok[10];
     size_t tl[10];
     int nt = 0;
@@ -475,20 +501,38 @@ void pf_known_table_free(pf_known_table_t *t) {
     free(o);
 }
 
-int pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t **out) {
-    if (!vcf_path || !contig || !out) return PF_ERR_ARG;
-    *out = NULL;
-    gzFile fp = gzopen(vcf_path, "rb");
+/* the public view of an accumulated table */
+static int known_finish(struct pf_known_own *o) {
+    const size_t n = o->k.pos.n;
+    o->hp8 = (uint8_t *)malloc(n ? n : 1);
+    o->off = (uint64_t *)malloc((n + 1) * 8);
+    if (!o->hp8 || !o->off) return PF_ERR_NOMEM;
+    o->off[0] = 0;
+    for (size_t i = 0; i < n; i++) { o->hp8[i] = (uint8_t)o->k.hp.a[i]; o->off[i + 1] = o->k.off[i]; }
+    static const uint8_t dummy[8] = {0};
+    pf_known_vars_t *v = &o->pub.vars;
+    v->n = (uint32_t)n;
+    v->pos = n ? o->k.pos.a : (const uint32_t *)dummy;
+    v->len = n ? o->k.len.a : (const uint32_t *)dummy;
+    v->op = n ? o->k.op : dummy;
+    v->haptag = o->hp8;
+    v->char_off = o->off;
+    v->chars = o->k.n_ch ? o->k.ch : dummy;
+    return PF_OK;
+}
+
+/* every complete line of a (gzipped) text file through fn(arg, line, len) */
+static int each_line(const char *path, int (*fn)(void *, const char *, size_t), void *arg) {
+    gzFile fp = gzopen(path, "rb");
     if (!fp) return -1;
-    struct pf_known_own *o = (struct pf_known_own *)calloc(1, sizeof *o);
     size_t cap = 1 << 16, len = 0;
     char *buf = (char *)malloc(cap);
-    int rc = (buf && o) ? 0 : PF_ERR_NOMEM;
+    int rc = buf ? 0 : PF_ERR_NOMEM;
     while (!rc) {
         if (len == cap) {
-            char *p = (char *)realloc(buf, cap * 2);
-            if (!p) { rc = PF_ERR_NOMEM; break; }
-            buf = p;
+            char *q = (char *)realloc(buf, cap * 2);
+            if (!q) { rc = PF_ERR_NOMEM; break; }
+            buf = q;
             cap *= 2;
         }
         const int nr = gzread(fp, buf + len, (unsigned)(cap - len));
@@ -498,7 +542,7 @@ int pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t
         size_t start = 0;
         for (size_t i = 0; i < len && !rc; i++) {
             if (buf[i] == '\n') {
-                rc = known_line(&o->k, contig, buf + start, i - start);
+                rc = fn(arg, buf + start, i - start);
                 start = i + 1;
             }
         }
@@ -507,26 +551,73 @@ int pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t
     }
     gzclose(fp);
     free(buf);
-    if (!rc) {
-        const size_t n = o->k.pos.n;
-        o->hp8 = (uint8_t *)malloc(n ? n : 1);
-        o->off = (uint64_t *)malloc((n + 1) * 8);
-        if (!o->hp8 || !o->off) rc = PF_ERR_NOMEM;
-        else {
-            o->off[0] = 0;
-            for (size_t i = 0; i < n; i++) { o->hp8[i] = (uint8_t)o->k.hp.a[i]; o->off[i + 1] = o->k.off[i]; }
-            static const uint8_t dummy[8] = {0};
-            pf_known_vars_t *v = &o->pub.vars;
-            v->n = (uint32_t)n;
-            v->pos = n ? o->k.pos.a : (const uint32_t *)dummy;
-            v->len = n ? o->k.len.a : (const uint32_t *)dummy;
-            v->op = n ? o->k.op : dummy;
-            v->haptag = o->hp8;
-            v->char_off = o->off;
-            v->chars = o->k.n_ch ? o->k.ch : dummy;
-        }
+    return rc;
+}
+
+/* one pass for several contigs: a line goes to the table of the contig its
+ * CHROM names, or -- when that name is not in `names` -- to the table the
+ * previous line went to (none before the first match).  This is the
+ * var_storage branch of load_intervals_from_file (2150-2163) that
+ * recover_variant_phase_in_dropped_intervals drives (2639): i_ref_cache is
+ * only updated by a name it finds.  With every VCF contig in `names` each
+ * table is that contig's pf_vcf_known_vars. */
+typedef struct {
+    uint32_t n;
+    const char *const *names;
+    struct pf_known_own **o;
+    int32_t cache;
+    int sticky;         /* 0: a name not in `names` is skipped (one contig's table) */
+} known_multi_t;
+
+static int known_multi_line(void *arg, const char *s, size_t l) {
+    known_multi_t *M = (known_multi_t *)arg;
+    if (l == 0 || s[0] == '#') return 0;
+    size_t i = 0;
+    while (i < l && s[i] == '\t') i++;
+    if (i >= l) return 0;
+    size_t j = i;
+    while (j < l && s[j] != '\t') j++;
+    char nm[1024];
+    const size_t nl = j - i < sizeof nm - 1 ? j - i : sizeof nm - 1;
+    memcpy(nm, s + i, nl);
+    nm[nl] = 0;
+    int32_t hit = -1;
+    for (uint32_t c = 0; c < M->n && hit < 0; c++)
+        if (!strcmp(M->names[c], nm)) hit = (int32_t)c;
+    if (hit >= 0 || !M->sticky) M->cache = hit;
+    if (M->cache < 0) return 0;
+    return known_line(&M->o[M->cache]->k, nm, s, l);
+}
+
+int pf_vcf_known_vars_multi(const char *vcf_path, uint32_t n, const char *const *names, pf_known_table_t **out) {
+    if (!vcf_path || !out || (n && !names)) return PF_ERR_ARG;
+    struct pf_known_own **o = (struct pf_known_own **)calloc(n ? n : 1, sizeof *o);
+    int rc = o ? 0 : PF_ERR_NOMEM;
+    for (uint32_t c = 0; c < n && !rc; c++) {
+        out[c] = NULL;
+        if (!names[c]) rc = PF_ERR_ARG;
+        else if (!(o[c] = (struct pf_known_own *)calloc(1, sizeof **o))) rc = PF_ERR_NOMEM;
     }
-    if (rc) { pf_known_table_free(o ? &o->pub : NULL); return rc; }
+    known_multi_t M = {n, names, o, -1, 1};
+    if (!rc) rc = each_line(vcf_path, known_multi_line, &M);
+    for (uint32_t c = 0; c < n && !rc; c++) rc = known_finish(o[c]);
+    for (uint32_t c = 0; c < n && o; c++) {
+        if (rc) pf_known_table_free(o[c] ? &o[c]->pub : NULL);
+        else out[c] = &o[c]->pub;
+    }
+    free(o);
+    return rc;
+}
+
+int pf_vcf_known_vars(const char *vcf_path, const char *contig, pf_known_table_t **out) {
+    if (!vcf_path || !contig || !out) return PF_ERR_ARG;
+    *out = NULL;
+    struct pf_known_own *o = (struct pf_known_own *)calloc(1, sizeof *o);
+    if (!o) return PF_ERR_NOMEM;
+    known_multi_t M = {1, &contig, &o, -1, 0};
+    int rc = each_line(vcf_path, known_multi_line, &M);
+    if (!rc) rc = known_finish(o);
+    if (rc) { pf_known_table_free(&o->pub); return rc; }
     *out = &o->pub;
     return PF_OK;
 }

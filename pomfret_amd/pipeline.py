@@ -31,7 +31,8 @@ from typing import Callable, Dict, List, Optional
 
 import numpy as np
 
-from ._lib import PomfretError, _blocks_contigs, _check, _gaps_contigs, _PfBlocks, _PfGaps, lib
+from ._lib import (INTERVALS_GTF, INTERVALS_TSV, INTERVALS_VCF, PomfretError, _blocks_contigs, _check,  # noqa: F401
+                   _gaps_contigs, _PfBlocks, _PfGaps, lib)
 from .abi import Config, LoadConfig, PfCfg, PfLoadCfg
 
 MODE_METHPHASE, MODE_REPORT = 0, 1
@@ -46,7 +47,8 @@ class PfMethphaseOpts(C.Structure):
                 ("chunk_size", C.c_int32), ("chunk_stride", C.c_int32), ("threads", C.c_int32),
                 ("n_devices", C.c_int32), ("devices", C.c_void_p), ("ctxs", C.c_void_p), ("n_ctxs", C.c_int32),
                 ("rank", C.c_int32), ("world", C.c_int32), ("job_windows", C.c_uint32), ("verbose", C.c_int32),
-                ("host_fetch", C.c_int32)]
+                ("host_fetch", C.c_int32), ("interval_path", C.c_char_p), ("interval_format", C.c_int32),
+                ("write_input_tagging", C.c_int32)]
 
 
 class PfQnameTagsC(C.Structure):
@@ -199,14 +201,20 @@ def make_opts(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Opti
               lcfg: Optional[LoadConfig] = None, mode: int = MODE_METHPHASE, untagged: bool = False,
               tsv: bool = False, threads: int = 8, n_devices: int = 0, ctxs=None, rank: int = 0, world: int = 1,
               job_windows: int = 0, cov: int = 0, chunk_size: int = 50_000, chunk_stride: int = 1_000_000,
-              verbose: int = 0, host_fetch: bool = False):
+              verbose: int = 0, host_fetch: bool = False, intervals=None, write_input_tagging: bool = False):
     """pf_methphase_opts_t from Python values.  cfg None: per-contig
-    parameters from the BAM's coverage estimate (runs without -c)."""
+    parameters from the BAM's coverage estimate (runs without -c).
+    intervals: (path, INTERVALS_GTF | INTERVALS_TSV), the --gtf / --tsv phase
+    blocks (vcf_path may then be None unless untagged)."""
     lcfg = lcfg or LoadConfig()
     o = PfMethphaseOpts()
     o.mode = mode
     o.bam_path = bam_path.encode()
-    o.vcf_path = vcf_path.encode()
+    o.vcf_path = vcf_path.encode() if vcf_path else None
+    if intervals is not None:
+        o.interval_path = intervals[0].encode()
+        o.interval_format = int(intervals[1])
+    o.write_input_tagging = int(bool(write_input_tagging))
     o.out_prefix = out_prefix.encode() if out_prefix else None
     if cfg is not None:
         o.cov_for_selection, o.cov_for_runtime, o.n_cand = cfg.cov_for_selection, cfg.cov_for_runtime, cfg.n_cand
@@ -356,7 +364,8 @@ def _result(plan: Plan, mode: int) -> Dict:
 def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg: Optional[Config],
                     lcfg: Optional[LoadConfig] = None, device: int = 0, threads: int = 8, ctx=None,
                     untagged: bool = False, tsv: bool = False, n_devices: int = 1, job_windows: int = 0,
-                    host_fetch: bool = False, ctxs=None) -> Dict:
+                    host_fetch: bool = False, ctxs=None, intervals=None,
+                    write_input_tagging: bool = False) -> Dict:
     """`pomfret methphase` over every gap of vcf_path with the reads of
     bam_path, in this process (pf_methphase_main).  Writes out_prefix +
     .mp.gtf / .mp.vcf (and .mp.tsv with tsv=True, the reference's
@@ -366,7 +375,9 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
     queue (two contexts of one device exercise the multi-GPU dispatcher);
     else n_devices GPUs from `device` on (0: all visible).
     Returns dict(decision=int8[n_gaps], contigs=[...], qname_hp={qname: hp},
-    raw_hp={qname: hp} (the -u table), n_limit)."""
+    raw_hp={qname: hp} (the -u table), n_limit).  intervals=(path,
+    INTERVALS_GTF | INTERVALS_TSV): the --gtf / --tsv phase blocks instead of
+    the VCF's (vcf_path None: no VCF written); write_input_tagging: -U."""
     L = _bind()
     devs = None
     if ctx is not None:
@@ -375,7 +386,8 @@ def methphase_files(bam_path: str, vcf_path: str, out_prefix: Optional[str], cfg
         devs = (C.c_int32 * n_devices)(*range(device, device + n_devices))
     o = make_opts(bam_path, vcf_path, out_prefix, cfg, lcfg, untagged=untagged, tsv=tsv, threads=threads,
                   n_devices=0 if ctxs else n_devices, ctxs=ctxs or None,
-                  job_windows=job_windows, host_fetch=host_fetch)
+                  job_windows=job_windows, host_fetch=host_fetch, intervals=intervals,
+                  write_input_tagging=write_input_tagging)
     if devs is not None:
         o.devices = C.cast(devs, C.c_void_p)
     h = C.c_void_p()
@@ -415,7 +427,8 @@ def methphase_files_dist(bam_path: str, vcf_path: str, out_prefix: Optional[str]
                          lcfg: Optional[LoadConfig] = None, untagged: bool = False, tsv: bool = False,
                          threads: int = 8, ctx=None, group=None, job_windows: int = 0, mode: int = MODE_METHPHASE,
                          cov: int = 0, chunk_size: int = 50_000, chunk_stride: int = 1_000_000,
-                         runner: Optional[Callable] = None, writer: int = 0, host_fetch: bool = False) -> Dict:
+                         runner: Optional[Callable] = None, writer: int = 0, host_fetch: bool = False,
+                         intervals=None, write_input_tagging: bool = False) -> Dict:
     """One process per GPU (torch.distributed initialised; RCCL on GPUs,
     gloo on CPU).  Every rank plans the same jobs and runs the ones its
     static LPT shard owns on `ctx` (or its LOCAL_RANK device); -u tables are
@@ -428,7 +441,8 @@ def methphase_files_dist(bam_path: str, vcf_path: str, out_prefix: Optional[str]
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     o = make_opts(bam_path, vcf_path, out_prefix if rank == writer else None, cfg, lcfg, mode=mode,
                   untagged=untagged, tsv=tsv, threads=threads, rank=rank, world=world, job_windows=job_windows,
-                  cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride, host_fetch=host_fetch)
+                  cov=cov, chunk_size=chunk_size, chunk_stride=chunk_stride, host_fetch=host_fetch,
+                  intervals=intervals, write_input_tagging=write_input_tagging)
     plan = Plan(o)
     try:
         def run(kind):

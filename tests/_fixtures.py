@@ -116,3 +116,24 @@ def example(tmp_path, coverage=60, seed=6):
     bam = str(tmp_path / "phased.bam")
     write_bam(bam, [("chr6", 170_805_979)], recs)
     return aln, recs, bam, vcf, gaps
+
+
+def blocks_files(tmp_path, contig_gaps, name="blocks"):
+    """--gtf / --tsv fixtures: phase blocks whose gaps are `contig_gaps`
+    ({contig: [(s, e), ...]} in file order): blocks (s0 - 100 kb, s0), (e0,
+    s1), ..., (e_last, e_last + 100 kb), written as a whatshap stats
+    --block-list shaped GTF (blocks at columns 4/5) and as a 3-column TSV.
+    Returns (gtf_path, tsv_path)."""
+    gtf, tsv = [], []
+    for ctg, gaps in contig_gaps.items():
+        edges = [max(1, gaps[0][0] - 100_000)] + [x for g in gaps for x in g] + [gaps[-1][1] + 100_000]
+        for k in range(0, len(edges), 2):
+            bs, be = edges[k], edges[k + 1]
+            gtf.append(f'{ctg}\tPhasing\texon\t{bs}\t{be}\t.\t+\t.\tgene_id "{bs}"; transcript_id "{bs}.1";\n')
+            tsv.append(f"{ctg}\t{bs}\t{be}\n")
+    pg, pt = str(tmp_path / f"{name}.gtf"), str(tmp_path / f"{name}.tsv")
+    with open(pg, "w") as f:
+        f.write("".join(gtf))
+    with open(pt, "w") as f:
+        f.write("".join(tsv))
+    return pg, pt

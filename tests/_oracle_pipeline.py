@@ -22,11 +22,56 @@ if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
 
+def _text_lines(path):
+    """the complete lines of a plain or gzipped text file (a last line without
+    '\n' is never read, as the reference's buffered reader)"""
+    import gzip
+    raw = open(path, "rb").read()
+    if raw[:2] == b"\x1f\x8b":
+        raw = gzip.decompress(raw)
+    return raw.decode().split("\n")[:-1]
+
+
+def known_positions_multi(vcf_path, names):
+    """The known positions recover_variant_phase_in_dropped_intervals scans per
+    contig of the phase-block file (blockjoin.c:2618-2663): the var_storage
+    branch of load_intervals_from_file (2150-2163) puts a line into the table
+    of the contig its CHROM names, or -- a CHROM not among `names` -- into the
+    table of the last name it found (i_ref_cache is only updated on a hit)."""
+    from test_bam import _py_known
+    out = {n: [] for n in names}
+    cache = None
+    for s in _text_lines(vcf_path):
+        if not s or s.startswith("#"):
+            continue
+        tok = [t for t in s.split("\t") if t]
+        if not tok:
+            continue
+        if tok[0] in out:
+            cache = tok[0]
+        if cache is not None:
+            out[cache] += [k[0] for k in _py_known([s], tok[0])]
+    return out
+
+
+def input_haptag_text(bam_path, raw_hp):
+    """-U's {prefix}.mp.input_haptag.tsv (blockjoin.c:4494-4517): every record
+    in file order, its HP tag (get_hp_from_aln) + 1 and its -u tag + 1 (255
+    when the qname is not in the table)."""
+    from test_bamw import hp_tag_raw, parse_bam, qname
+    _, bodies, _, _ = parse_bam(bam_path)
+    rows = [f"{qname(b)}\t{hp_tag_raw(b) + 1}\t{raw_hp.get(qname(b), 254) + 1}\n" for b in bodies]
+    return "#qname\treal_hp\ttagged_hp\n" + "".join(rows)
+
+
 def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, recs_by_contig=None,
-                           n_threads=8):
-    """-> dict(decision, qname_hp, raw_hp, gtf, tsv, vcf, counts).  recs_by_contig
-    ({contig: [Rec]} as written) feeds the rescue restatement.  cfg None: no
-    -c, every contig's parameters from its coverage estimate."""
+                           n_threads=8, intervals=None):
+    """-> dict(decision, qname_hp, raw_hp, gtf, tsv, vcf, counts, input_haptag).
+    recs_by_contig ({contig: [Rec]} as written) feeds the rescue restatement.
+    cfg None: no -c, every contig's parameters from its coverage estimate.
+    intervals=(path, fmt): --gtf / --tsv phase blocks (oracle.interval_gaps);
+    with -u the VCF's contigs are still the pre-pass's (4446, 4460-4465);
+    vcf_path None: no VCF (4706)."""
     import oracle
     from oracle import epilogue as ep
     from pomfret_amd import Config, LoadConfig
@@ -34,7 +79,8 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
     from test_bam import _py_rescue
 
     lcfg = lcfg or LoadConfig()
-    contigs = oracle.vcf_gaps(vcf_path)
+    contigs = oracle.interval_gaps(*intervals) if intervals else oracle.vcf_gaps(vcf_path)
+    ucontigs = oracle.vcf_gaps(vcf_path) if untagged else []
     decision, qname_hp, raw_hp = [], {}, {}
     with BamFile(bam_path) as bam:
         covs = bam.estimate_coverage() if cfg is None else None
@@ -46,7 +92,7 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
             return Config.from_coverage(int(covs[bam.tid(name)]), given=False)
 
         if untagged:
-            for c in contigs:
+            for c in ucontigs:
                 if bam.tid(c["name"]) < 0:
                     continue
                 kv = vcf_known_vars(vcf_path, c["name"])
@@ -85,17 +131,20 @@ def methphase_files_oracle(bam_path, vcf_path, cfg, lcfg=None, untagged=False, r
                 for i in range(ro[w], ro[w + 1]):
                     qname_hp.setdefault(qn[int(recs_of_read[i])], int(res.read_hp[i]))
     blocks = ep.phase_blocks(contigs, decision)
-    rescue = []
-    for c in contigs:
-        if not c["dropped"] or recs_by_contig is None or c["name"] not in recs_by_contig:
-            rescue.append({})
-            continue
-        kv = vcf_known_vars(vcf_path, c["name"])
-        rescue.append(_py_rescue(recs_by_contig[c["name"]], kv.pos.tolist(), c["dropped"], qname_hp,
-                                 raw_hp if untagged else None))
-    vcf, counts = ep.vcf_bytes(vcf_path, contigs, blocks, rescue)
+    vcf, counts = None, None
+    if vcf_path:
+        known = known_positions_multi(vcf_path, [c["name"] for c in contigs])
+        rescue = []
+        for c in contigs:
+            if not c["dropped"] or recs_by_contig is None or c["name"] not in recs_by_contig:
+                rescue.append({})
+                continue
+            rescue.append(_py_rescue(recs_by_contig[c["name"]], known[c["name"]], c["dropped"], qname_hp,
+                                     raw_hp if untagged else None))
+        vcf, counts = ep.vcf_bytes(vcf_path, contigs, blocks, rescue)
     return dict(decision=np.asarray(decision, np.int8), qname_hp=qname_hp, raw_hp=raw_hp,
-                gtf=ep.gtf_text(contigs, blocks), tsv=ep.tsv_text(contigs, blocks), vcf=vcf, counts=counts)
+                gtf=ep.gtf_text(contigs, blocks), tsv=ep.tsv_text(contigs, blocks), vcf=vcf, counts=counts,
+                input_haptag=input_haptag_text(bam_path, raw_hp) if untagged else None)
 
 
 def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4, fetch_threads=1, inflate_threads=1):
@@ -162,7 +211,7 @@ def oracle_job_runner(bam_path, vcf_path, lcfg=None, n_threads=4, fetch_threads=
 
 
 def methphase_files_port(bam_path, vcf_path, out_prefix, cfg, lcfg=None, untagged=False, threads=16,
-                         tsv=False, job_windows=0):
+                         tsv=False, job_windows=0, intervals=None, write_input_tagging=False):
     """The CPU port of the whole `pomfret methphase` driver -- the bench's CPU
     side of the file-to-output legs, and a CPU check of the product's
     planner / merge / writers.  The product's C plan and writers run with
@@ -183,7 +232,8 @@ def methphase_files_port(bam_path, vcf_path, out_prefix, cfg, lcfg=None, untagge
 
     t0 = time.perf_counter()
     o = make_opts(bam_path, vcf_path, out_prefix, cfg, lcfg, untagged=untagged, tsv=tsv, threads=threads,
-                  job_windows=job_windows, host_fetch=True)
+                  job_windows=job_windows, host_fetch=True, intervals=intervals,
+                  write_input_tagging=write_input_tagging)
     plan = Plan(o)
     t1 = time.perf_counter()
     nj = plan.n_jobs(JOB_HAPTAG) if untagged else 0

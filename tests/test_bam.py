@@ -230,10 +230,38 @@ def test_vcf_known_vars_rules(tmp_path):
     assert [g[:3] for g in got] == [(99, 1, 1), (200, 3, 3), (299, 3, 2), (699, 2, 2), (899, 1, 1), (949, 1, 1)]
     assert got[1][4] == [1, 2, 3] and got[2][4] == [3, 3, 0] and got[3][4] == [4, 2]
     assert _kv_list(vcf_known_vars(str(p), "c2")) == _py_known(body, "c2")
+    # '#' lines never reach insert_variant_from_vcf_line on the paths that
+    # collect variants (load_intervals_from_file skips them, 2023-2026)
     bad = tmp_path / "b.vcf"
-    bad.write_text("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\n")
-    with pytest.raises(Exception):
-        vcf_known_vars(str(bad), "c1")
+    bad.write_text("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\n" + body[0] + "\n")
+    assert _kv_list(vcf_known_vars(str(bad), "c1")) == _py_known(body[:1], "c1")
+    with pytest.raises(FileNotFoundError):
+        vcf_known_vars(str(tmp_path / "missing.vcf"), "c1")
+
+
+def test_vcf_known_vars_multi_attribution(tmp_path):
+    """recover_variant_phase_in_dropped_intervals' tables over a GTF's contigs
+    (var_storage branch of load_intervals_from_file, blockjoin.c:2150-2163):
+    lines of a VCF contig the GTF lacks go to the last contig found (none
+    before the first hit); with every VCF contig named, each table is the
+    single-contig one."""
+    from pomfret_amd.bam import vcf_known_vars, vcf_known_vars_multi
+    from tests._oracle_pipeline import known_positions_multi
+    body = ["x0\t50\t.\tA\tG\t50\tPASS\t.\tGT\t0|1",     # before any hit: dropped
+            "c1\t100\t.\tA\tG\t50\tPASS\t.\tGT\t0|1",
+            "c1\t200\t.\tACGT\tA\t50\tPASS\t.\tGT\t1|0",
+            "c2\t30\t.\tA\tG\t50\tPASS\t.\tGT\t1|0",      # not in the GTF: appended to c1
+            "c2\t40\t.\tA\tG\t50\tPASS\t.\tGT\t0/1",      #   (unphased: rejected there too)
+            "c3\t70\t.\tC\tCTT\t50\tPASS\t.\tGT\t0|1",
+            "c2\t90\t.\tA\tT\t50\tPASS\t.\tGT\t0|1"]      # follows c3: appended to c3
+    p = tmp_path / "m.vcf"
+    p.write_text("##x\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS\n" + "\n".join(body) + "\n")
+    got = vcf_known_vars_multi(str(p), ["c3", "c1"])
+    ref = known_positions_multi(str(p), ["c3", "c1"])
+    assert [g.pos.tolist() for g in got] == [ref["c3"], ref["c1"]] == [[69, 89], [99, 200, 29]]
+    allc = vcf_known_vars_multi(str(p), ["x0", "c1", "c2", "c3"])
+    for name, kv in zip(["x0", "c1", "c2", "c3"], allc):
+        assert _kv_list(kv) == _kv_list(vcf_known_vars(str(p), name))
 
 
 def test_vcf_known_vars_example_fixture():

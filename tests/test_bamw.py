@@ -41,10 +41,12 @@ def read_bgzf_blocks(path):
 def parse_bam(path):
     """(header bytes, [record body bytes], [virtual offset of each record], block starts)"""
     blocks = read_bgzf_blocks(path)
-    starts, buf = [], b""
+    starts, parts, n = [], [], 0
     for off, data in blocks:
-        starts.append((off, len(buf)))
-        buf += data
+        starts.append((off, n))
+        parts.append(data)
+        n += len(data)
+    buf = b"".join(parts)
     lt = struct.unpack_from("<i", buf, 4)[0]
     o = 8 + lt
     nref = struct.unpack_from("<i", buf, o)[0]

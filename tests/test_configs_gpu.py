@@ -14,7 +14,8 @@ large or hand-made windows (VERDICT r01 "next round" 1 and 10):
     the documented differences of the older build;
   * the pre-haplotagged pipeline with output bytes and the qname table;
   * T8 (u16 site counters wrapping at 4096) and T6 (mmr_min_i wrapping to
-    UINT32_MAX) on hand-worked windows.
+    UINT32_MAX) on hand-worked windows;
+  * the CLI's --gtf / --tsv phase blocks and -U (VERDICT r04 "next round" 1).
 """
 import os
 import subprocess
@@ -332,3 +333,66 @@ def test_cli_write_bam_and_varhaptag(oracle_lib, tmp_path):
         h = ref["raw_hp"].get(qname(bi), 254)
         assert line == f"{qname(bi)}\t{hp_tag_raw(bi) + 1}\t{h + 1}"
         assert bo == aux_update_int(bi, h + 1)
+
+
+def _cli_blocks(aln, merge_pair):
+    from tests.test_pipeline import _shifted
+    return _shifted(aln, merge_pair=merge_pair)
+
+
+@pytest.mark.parametrize("fmt", ["gtf", "tsv"])
+def test_cli_gtf_tsv_blocks(oracle_lib, tmp_path, fmt):
+    """`pomfret-amd methphase --gtf blocks.gtf --vcf v.vcf` and `--tsv
+    blocks.tsv` (no --vcf: no VCF written, 4706): windows from the block file
+    (main_blockjoin 4661-4666), GTF / TSV / VCF bytes equal the oracle
+    pipeline's."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import INTERVALS_GTF, INTERVALS_TSV
+    aln, recs, bam, vcf = fx.tagged(tmp_path, n_windows=4)
+    cfg = Config.from_coverage(30, given=True)
+    for with_vcf in (True, False):
+        gtf, tsvp = fx.blocks_files(tmp_path, {"chrS": _cli_blocks(aln, not with_vcf)}, name=f"b{with_vcf}")
+        iv = (gtf, INTERVALS_GTF) if fmt == "gtf" else (tsvp, INTERVALS_TSV)
+        out = str(tmp_path / f"cli{int(with_vcf)}")
+        args = ["methphase", "-o", out, "-c", "30", f"--{fmt}", iv[0], "--output-tsv"]
+        if with_vcf:
+            args += ["--vcf", vcf]
+        r = _cli(*args, bam)
+        assert r.returncode == 0, r.stderr
+        ref = methphase_files_oracle(bam, vcf if with_vcf else None, cfg, recs_by_contig={"chrS": recs},
+                                     intervals=iv)
+        assert (ref["decision"] >= 0).sum() >= 2
+        assert open(out + ".mp.gtf").read() == ref["gtf"]
+        assert open(out + ".mp.tsv").read() == ref["tsv"]
+        if with_vcf:
+            assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+            assert "multiple phase block files" in r.stderr
+        else:
+            assert not os.path.exists(out + ".mp.vcf")
+
+
+def test_cli_untagged_gtf_input_tagging(oracle_lib, tmp_path):
+    """`pomfret-amd methphase -u -U --gtf blocks.gtf --vcf v.vcf`: K4 tags the
+    reads from the VCF's variants, the GTF's blocks (with a dropped interval
+    whose variants the rescue phases) define the windows, and -U writes
+    {prefix}.mp.input_haptag.tsv; every file equals the oracle pipeline's."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import INTERVALS_GTF
+    aln, recs, bam, vcf = fx.untagged(tmp_path, n_windows=2, coverage=30, len_scale=0.6)
+    gtf, _ = fx.blocks_files(tmp_path, {"chrS": _cli_blocks(aln, True)})
+    out = str(tmp_path / "u")
+    r = _cli("methphase", "-u", "-U", "-c", "30", "-o", out, "--gtf", gtf, "--vcf", vcf, "--output-tsv", bam)
+    assert r.returncode == 0, r.stderr
+    ref = methphase_files_oracle(bam, vcf, Config.from_coverage(30, given=True), untagged=True,
+                                 recs_by_contig={"chrS": recs}, intervals=(gtf, INTERVALS_GTF))
+    assert open(out + ".mp.gtf").read() == ref["gtf"]
+    assert open(out + ".mp.tsv").read() == ref["tsv"]
+    assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+    assert open(out + ".mp.input_haptag.tsv").read() == ref["input_haptag"]
+    # -U without -u writes nothing (4494), and an empty block file terminates (4474-4477)
+    r = _cli("methphase", "-U", "-c", "30", "-o", str(tmp_path / "t"), "--vcf", vcf, bam)
+    assert r.returncode == 0 and not os.path.exists(str(tmp_path / "t") + ".mp.input_haptag.tsv")
+    empty = str(tmp_path / "empty.gtf")
+    open(empty, "w").write("# nothing\n")
+    r = _cli("methphase", "-c", "30", "-o", str(tmp_path / "e"), "--gtf", empty, bam)
+    assert r.returncode == 1 and "No intervals loaded" in r.stderr

@@ -66,6 +66,9 @@ def test_headline_subset_natural_paths(oracle_lib, gpu_ctx, headline_subset, mon
     assert len(db.heavy_problems()) == 0
     st = db.stats()
     assert all(int(st[w, d, 4]) * 2 > 50688 for w in wide for d in (0, 1) if out.win_n_sites[w] > 0)
+    paths = db.k3_paths()
+    assert all(paths[w, d] == 2 for w in wide for d in (0, 1) if out.win_n_sites[w] > 0), paths[wide]
+    assert set(paths[out.win_n_sites > 0].ravel().tolist()) <= {1, 2}
     # the wide windows' call positions span beyond K12's 2^19-position bitmap:
     # their sites come from the dense path (pf_kernels.hip, range_ok)
     off, pos, _, _, _ = db.debug_calls()

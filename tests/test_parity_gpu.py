@@ -141,11 +141,26 @@ def test_slot_list_sources(oracle_lib, gpu_ctx, monkeypatch, env):
     state reset between problems)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
+    seen = set()
     for name, cfg, batch in CASES:
         ref = oracle_lib.methphase(cfg, batch, n_threads=8)
         db = gpu_ctx.upload(cfg, batch)
-        _compare(ref, db.run(), f"{name}/{env}")
+        out = db.run()
+        _compare(ref, out, f"{name}/{env}")
+        # the variant that ran (pf_batch_k3_paths): "force" never reads the
+        # slot lists from LDS, "hbm" never runs the cache
+        p = db.k3_paths()[out.win_n_sites > 0].ravel().tolist()
+        seen |= set(p)
+        mode = env.get("PF_K3_CACHE")
+        if mode == "force":
+            assert set(p) <= {2, 3, 4}, (name, p)
+        elif mode == "hbm":
+            assert set(p) <= {3, 4}, (name, p)
         db.free()
+    if env.get("PF_K3_CACHE") == "force":
+        assert 2 in seen
+    elif env.get("PF_K3_CACHE") == "hbm":
+        assert 3 in seen
 
 
 @pytest.mark.parametrize("path", ["fold", "rows"])

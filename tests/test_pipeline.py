@@ -149,3 +149,100 @@ def test_genome_port_matches_oracle(oracle_lib, tmp_path):
     assert open(out + ".mp.tsv").read() == ref["tsv"]
     assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
     assert ref["counts"][1] > 0 and set(ph) >= {"plan_s", "haptag_s", "windows_s", "total_s"}
+
+
+def _shifted(aln, merge_pair=True):
+    """GTF gaps that are not the VCF's: each window trimmed, plus (merge_pair)
+    a split of the first window into two raw gaps < READBACK apart, which
+    merge_close_intervals fuses back into one window with a dropped interval"""
+    g = [(int(s) + 1500, int(e) - 2500) for s, e in zip(aln.win_start, aln.win_end)]
+    if merge_pair:
+        s, e = g[0]
+        m = (s + e) // 2
+        g[0:1] = [(s, m - 200), (m + 200, e)]
+    return g
+
+
+@pytest.mark.parametrize("fmt", ["gtf", "tsv"])
+def test_plan_gtf_tsv_matches_oracle(oracle_lib, tmp_path, fmt):
+    """--gtf / --tsv phase blocks (main_blockjoin 4661-4666): windows from the
+    file, the VCF (when given) rewritten with those blocks and its variants in
+    the dropped interval rescued; without --vcf no VCF is written (4706)."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import INTERVALS_GTF, INTERVALS_TSV, Plan, make_opts
+    aln, recs, bam, vcf = fx.tagged(tmp_path, n_windows=4)
+    cfg = Config.from_coverage(30, given=False)
+    for with_vcf in (True, False):
+        # a dropped interval only without the VCF: this fixture's records carry
+        # no MD, which the rescue asserts on (1594-1596)
+        gtf, tsvp = fx.blocks_files(tmp_path, {"chrS": _shifted(aln, merge_pair=not with_vcf)}, name=f"b{with_vcf}")
+        iv = (gtf, INTERVALS_GTF) if fmt == "gtf" else (tsvp, INTERVALS_TSV)
+        out = str(tmp_path / f"o{int(with_vcf)}")
+        plan = Plan(make_opts(bam, vcf if with_vcf else None, out, cfg, tsv=True, intervals=iv))
+        _run_plan(plan, oracle_job_runner(bam, vcf))
+        ref = methphase_files_oracle(bam, vcf if with_vcf else None, cfg, recs_by_contig={"chrS": recs},
+                                     intervals=iv)
+        assert len(ref["decision"]) == 4 and (ref["decision"] >= 0).sum() >= 2
+        from pomfret_amd import _lib
+        assert len(_lib.interval_gaps(*iv)[0]["dropped"]) == (0 if with_vcf else 1)
+        assert np.array_equal(plan.decisions(), ref["decision"])
+        assert plan.qname_hp() == ref["qname_hp"]
+        assert open(out + ".mp.gtf").read() == ref["gtf"]
+        assert open(out + ".mp.tsv").read() == ref["tsv"]
+        if with_vcf:
+            assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]
+        else:
+            assert not os.path.exists(out + ".mp.vcf")
+        plan.close()
+
+
+def test_plan_untagged_gtf_input_tagging(oracle_lib, tmp_path):
+    """`-u --gtf blocks.gtf --vcf v.vcf -U`: the VCF's variants haplotag the
+    reads, the GTF's blocks define the windows (4445-4465), -U writes
+    {prefix}.mp.input_haptag.tsv (4494-4517)."""
+    from pomfret_amd import Config
+    from pomfret_amd.pipeline import INTERVALS_GTF, JOB_HAPTAG, Plan, make_opts
+    aln, recs, bam, vcf = fx.untagged(tmp_path, n_windows=2, coverage=30, len_scale=0.6)
+    gtf, _ = fx.blocks_files(tmp_path, {"chrS": _shifted(aln)})
+    cfg = Config.from_coverage(30, given=True)
+    out = str(tmp_path / "o")
+    plan = Plan(make_opts(bam, vcf, out, cfg, untagged=True, tsv=True, intervals=(gtf, INTERVALS_GTF),
+                          write_input_tagging=True))
+    assert plan.n_jobs(JOB_HAPTAG) == 1
+    _run_plan(plan, oracle_job_runner(bam, vcf))
+    ref = methphase_files_oracle(bam, vcf, cfg, untagged=True, recs_by_contig={"chrS": recs},
+                                 intervals=(gtf, INTERVALS_GTF))
+    _compare(out, plan, ref)
+    assert plan.raw_hp() == ref["raw_hp"] and len(ref["raw_hp"]) > 0
+    text = open(out + ".mp.input_haptag.tsv").read()
+    assert text == ref["input_haptag"]
+    assert text.count("\n") == len(recs) + 1 and "\t255\t" in text      # no HP tags in the input
+
+
+def test_plan_multicontig_gtf_lacks_a_vcf_contig(oracle_lib, tmp_path):
+    """A GTF without one of the VCF's contigs and in another contig order: the
+    -u pre-pass still runs over the VCF's contigs (first wins in VCF order),
+    the windows follow the GTF, and the rescue's known tables attribute the
+    missing contig's lines to the contig before it (2150-2163)."""
+    from pomfret_amd.pipeline import INTERVALS_GTF, JOB_HAPTAG, Plan, make_opts
+    from pomfret_amd import Config
+    bam, vcf, recs_by, alns = fx.multi_contig(tmp_path, untagged=True, len_scale=0.3)
+    ga = [(int(s), int(e)) for s, e in zip(alns["chrA"].win_start, alns["chrA"].win_end)]
+    gc = [(int(s) + 1000, int(e) - 1000) for s, e in zip(alns["chrC"].win_start, alns["chrC"].win_end)]
+    s, e = gc[1]
+    gc[1:2] = [(s, (s + e) // 2 - 100), ((s + e) // 2 + 100, e)]       # a dropped interval in chrC
+    gtf, _ = fx.blocks_files(tmp_path, {"chrC": gc, "chrA": ga})
+    cfg = Config.from_coverage(40, given=True)
+    out = str(tmp_path / "o")
+    plan = Plan(make_opts(bam, vcf, out, cfg, untagged=True, tsv=True, intervals=(gtf, INTERVALS_GTF),
+                          write_input_tagging=True))
+    names = sorted(plan.job_info(JOB_HAPTAG, j)["contig_name"] for j in range(plan.n_jobs(JOB_HAPTAG)))
+    assert names == ["chrA", "chrB", "chrC"]                  # the VCF's contigs, not the GTF's
+    _run_plan(plan, oracle_job_runner(bam, vcf))
+    ref = methphase_files_oracle(bam, vcf, cfg, untagged=True, recs_by_contig=recs_by,
+                                 intervals=(gtf, INTERVALS_GTF))
+    _compare(out, plan, ref)
+    assert plan.raw_hp() == ref["raw_hp"]
+    assert open(out + ".mp.input_haptag.tsv").read() == ref["input_haptag"]
+    from pomfret_amd import _lib
+    assert [c["name"] for c in _lib.interval_gaps(gtf, INTERVALS_GTF)] == ["chrC", "chrA"]
