@@ -167,7 +167,30 @@ def cpu_baseline(cfg, batch, threads: int, min_cpu_s: float = 20.0, max_reps: in
     return batch.n_reads * reps / dt, dt, reps
 
 
-def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 20.0, max_reps: int = 200):
+def effective_cores():
+    """(cores this process may run on, how that was found): the smaller of the
+    CPU affinity set and the cgroup CPU quota (cpu.max, v2; cfs_quota_us /
+    cfs_period_us, v1) -- `nproc` on the GPU box shows the whole machine."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    eff = aff if quota is None else max(1, min(aff, int(quota)))
+    return eff, {"affinity": aff, "cgroup_quota_cores": round(quota, 2) if quota is not None else None}
+
+
+def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 20.0, max_reps: int = 200,
+                     min_reps: int = 2):
     """Record-level CPU path of the oracle (per window: loader + worker, the
     reference's structure), `threads` pthreads over windows, bounded sample."""
     import oracle
@@ -177,7 +200,7 @@ def cpu_baseline_aln(cfg, lcfg, aln, n_reads, threads: int, min_cpu_s: float = 2
     while reps < max_reps:
         ref = oracle.methphase_aln(cfg, lcfg, aln, n_threads=threads)
         reps += 1
-        if (time.perf_counter() - t0) * threads >= min_cpu_s and reps >= 2:
+        if (time.perf_counter() - t0) * threads >= min_cpu_s and reps >= min_reps:
             break
     dt = time.perf_counter() - t0
     return n_reads * reps / dt, dt, reps, ref
@@ -438,6 +461,27 @@ def e2e_u_leg(ctx, lcfg, threads: int, workdir: str, scale: float = 1.0, cpu: bo
     return res
 
 
+def stagger_groups(groups, gctx, split: int, base_costs):
+    """The contexts out of phase: context c > 0 runs its first batch as two
+    halves (dealt heaviest first, round-robin), so its later batches start
+    half a batch after context 0's -- one context's K3 tail (few long greedy
+    problems) then runs beside another's K0 / K12 instead of beside its
+    twin's tail.  Same windows, same batches otherwise."""
+    out_g, out_c, done = [], [], set()
+    for g, c in zip(groups, gctx):
+        if c > 0 and c not in done and g[1].shape[0] >= 2:
+            done.add(c)
+            order = np.argsort(-np.asarray(base_costs, np.float64)[g[1]], kind="stable")
+            for h in (order[0::2], order[1::2]):
+                h = np.sort(h)
+                out_g.append((g[0][h], g[1][h]))
+                out_c.append(c)
+        else:
+            out_g.append(g)
+            out_c.append(c)
+    return out_g, out_c
+
+
 def oracle_sample(aln, gaps, n_reads_w, n: int = 64):
     """The cpu_baseline sample: the heaviest windows (most kept reads), the
     widest gaps (>= 400 kb: K12's dense site path), then the first windows,
@@ -499,6 +543,9 @@ def main():
     ap.add_argument("--split", type=int, default=2,
                     help="contexts per GPU (the driver's PF_DEV_CONTEXTS): the rank's batches are dealt over "
                          "them and launched together every step")
+    ap.add_argument("--stagger", type=int, default=0,
+                    help="1: every context but the first starts with its first batch cut in two halves, so "
+                         "the contexts' kernels run out of phase (round 5: 117.1 vs 114.0 ms per step, slower; off)")
     ap.add_argument("--calls-level", action="store_true",
                     help="time the calls-level boundary (reads + 5mC calls resident, no K0)")
     args = ap.parse_args()
@@ -510,7 +557,8 @@ def main():
     from pomfret_amd import Config, Context, LoadConfig, WindowBatch
     from pomfret_amd.shard import aln_window_costs, group_copies, lpt_bound, lpt_partition, split_groups
     from pomfret_amd.synth import SynthSpec, make_batch
-    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch
+    from dataclasses import replace
+    from pomfret_amd.synth_aln import AlnSpec, make_aln_batch, window_cost_estimates
 
     wl = dict(WORKLOADS[args.workload], n_windows=args.windows, coverage=args.coverage)
     cfg = Config.from_coverage(wl["coverage"], given=False)
@@ -548,6 +596,9 @@ def main():
         share = parts[rank]
         loads = [float(job_costs[p].sum()) for p in parts]
     groups = split_groups(group_copies(share, n_base), split, base_costs)
+    gctx = [gi % split for gi in range(len(groups))]
+    if args.stagger and split > 1 and len(groups) > split:
+        groups, gctx = stagger_groups(groups, gctx, split, base_costs)
 
     dist = None
     if world > 1:
@@ -572,7 +623,7 @@ def main():
     t = time.perf_counter()
     dbs, subs = [], []
     for gi, (_, basew) in enumerate(groups):
-        d, s = upload(ctxs[gi % split], basew)
+        d, s = upload(ctxs[gctx[gi]], basew)
         dbs.append(d)
         subs.append(s if gi == 0 else None)          # the first batch's records feed the byte model
     log(f"[bench] rank {rank}: {len(share)} of {n_job} job windows as {len(dbs)} batches on {split} contexts "
@@ -757,6 +808,37 @@ def main():
             for d in extra:
                 d.free()
             log(f"[bench] strong projection N={n}: {json.dumps(proj[str(n)])}")
+        # The same projection over DISTINCT windows: a job of
+        # `tiles` contigs with different seeds (a real WGS job has no copies),
+        # dealt by LPT on cost estimates (synth_aln.window_cost_estimate: the
+        # read bases, replayed from the generator's RNG without building the
+        # reads; correlation 0.99998 with the SEQ + MM bytes), then rank 0's
+        # share at N=8 generated and timed on this GPU.
+        n8 = 8
+        td = time.perf_counter()
+        djobs = [(replace(spec, seed=seed + 100 + t), w) for t in range(tiles) for w in range(n_base)]
+        dcost = window_cost_estimates(djobs, workers=CPU_SHARE)
+        parts_d = lpt_partition(dcost, n8)
+        ld_d = [float(dcost[p].sum()) for p in parts_d]
+        mine = sorted(parts_d[0].tolist())
+        a_d = make_aln_batch(spec, jobs=[djobs[i] for i in mine], workers=0)
+        dc_d = aln_window_costs(a_d)
+        g_d = split_groups([(np.arange(a_d.n_windows), np.arange(a_d.n_windows))], split, dc_d)
+        dbs_d = [ctxs[gi % split].upload_aln(cfg, a_d.select(bw) if bw.shape[0] != a_d.n_windows else a_d, lcfg)
+                 for gi, (_, bw) in enumerate(g_d)]
+        t_gen = time.perf_counter() - td
+        el_d, tot_d, _, o_d = timed(dbs_d)
+        reads_d = sum(int(o.win_n_reads.sum()) for o in o_d)
+        for d in dbs_d:
+            d.free()
+        del a_d, dbs_d
+        proj["8_distinct"] = {
+            "ms_per_step": round(el_d / args.steps * 1e3, 4), "windows_rank0": len(mine), "reads_rank0": reads_d,
+            "projected_value": round(reads_d * n8 * args.steps / el_d, 1),
+            "lpt_loads_max_over_mean": round(max(ld_d) / (sum(ld_d) / n8), 4),
+            "job": f"{tiles} contigs x {n_base} windows, seeds {seed + 100}..{seed + 99 + tiles} (no copies)",
+            "generate_s": round(t_gen, 1)}
+        log(f"[bench] strong projection N=8 distinct: {json.dumps(proj['8_distinct'])}")
         # The floor of a GPU's step: the heaviest base window alone (its
         # serial greedy chain; no GPU count takes it below this)
         wmax = int(np.argmax(out.win_n_reads))
@@ -813,40 +895,49 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and record_level:
-        # BASELINE's target is phrased against the reference's -t 32: 32
-        # threads when this host's affinity allows it (the GPU box's share is
-        # 16 cores per GPU: the 16-thread rate is reported beside it).  The
-        # sample holds the heaviest and widest windows of the batch, and the
-        # oracle's result on it is compared with the GPU's.
-        threads = args.cpu_threads or min(32, len(os.sched_getaffinity(0)))
+        # BASELINE's target is phrased against the reference's -t 32.  The
+        # port runs with min(32, effective cores) threads -- the effective
+        # cores are the affinity set capped by the cgroup quota (the GPU box
+        # grants 16 per GPU) -- over the whole first batch (1024 windows, so
+        # the threads are not tail-bound on a few heavy windows), once.  The
+        # port parallelises over windows; the reference's kt_for parallelises
+        # over contigs (blockjoin.c:4560), which favours the port.  The
+        # oracle's results are compared with the GPU's on every window of the
+        # batch, and the read tags on the heavy / wide sample.
+        eff, eff_how = effective_cores()
+        threads = args.cpu_threads or min(32, eff)
         sub = oracle_sample(aln0, gaps, out.win_n_reads)
-        a_sub = aln0.select(sub)
-        n_sub = int(out.win_n_reads[sub].sum())
-        v_cpu, dt, reps, ref = cpu_baseline_aln(cfg, lcfg, a_sub, n_sub, threads, min_cpu_s=30.0)
+        n_b0 = int(out.win_n_reads.sum())
+        allw = np.arange(aln0.n_windows)
+        v_cpu, dt, reps, ref = cpu_baseline_aln(cfg, lcfg, aln0, n_b0, threads, min_cpu_s=0.0, min_reps=1)
         # read tags: the oracle's loader, then its worker (methphase_aln leaves them unset)
         import oracle
+        a_sub = aln0.select(sub)
         ref_t = oracle.methphase(cfg, oracle.load_reads(lcfg, a_sub)[0], n_threads=threads)
-        bad = sorted(set(compare_with_oracle(out, batch.win_read_off, ref, sub, tags=False))
+        bad = sorted(set(compare_with_oracle(out, batch.win_read_off, ref, allw, tags=False))
                      | set(compare_with_oracle(out, batch.win_read_off, ref_t, sub)))
-        v_half = cpu_baseline_aln(cfg, lcfg, a_sub, n_sub, max(1, threads // 2), min_cpu_s=15.0)[0]
-        eff = v_cpu / (2 * v_half) if v_half else None
+        half = max(1, threads // 2)
+        v_half, dt_half = cpu_baseline_aln(cfg, lcfg, aln0, n_b0, half, min_cpu_s=0.0, min_reps=1)[:2]
+        eff_scal = v_cpu / (2 * v_half) if v_half else None
         heavy_w = sorted({int(p) >> 1 for p in db.heavy_problems()} & set(sub))
         cpu = {"value": round(v_cpu, 1), "unit": "reads/s", "cores": threads, "kind": "port",
-               "sample": f"{len(sub)} windows of the first batch: the 8 with the most reads, the widest gaps "
-                         f"(>= 400 kb), then the first windows ({n_sub} reads, x{reps}: {dt:.2f}s wall x "
-                         f"{threads} threads = {dt * threads:.0f} CPU-s), per-window loader + worker over the "
-                         f"same BAM records, oracle/pf_oracle{{_load,}}.c; {threads} threads "
-                         f"({len(os.sched_getaffinity(0))} in this process's affinity; the box's share per GPU "
-                         f"is {CPU_SHARE})",
+               "sample": f"the whole first batch: {aln0.n_windows} windows, {n_b0} reads, once ({dt:.2f}s wall x "
+                         f"{threads} threads); per-window loader + worker over the same BAM records, "
+                         f"oracle/pf_oracle{{_load,}}.c; pthreads over windows (the reference's kt_for runs "
+                         f"contigs, blockjoin.c:4560)",
+               "effective_cores": eff, "effective_cores_from": eff_how,
                "matches": not bad, "mismatched": bad,
-               "compared": "decision, 2x2 tables, join, which_way, score, site/read counts, every read's tag "
-                           "(bit for bit); Fisher p (rtol 1e-6)",
+               "compared": "every window of the batch: decision, 2x2 tables, join, which_way, score, site/read "
+                           f"counts (bit for bit), Fisher p (rtol 1e-6); every read's tag on {len(sub)} windows "
+                           "(the 8 with the most reads, the widest gaps >= 400 kb, then the first)",
                "sample_windows": {"n": len(sub), "max_reads": int(out.win_n_reads[sub].max()),
                                   "max_gap_bp": int(gaps[sub].max()), "heavy_problem_windows": len(heavy_w),
                                   "windows_ge_400kb": int((gaps[sub] >= 400_000).sum())},
-               "thread_scaling": {str(max(1, threads // 2)): round(v_half, 1), str(threads): round(v_cpu, 1),
-                                  "efficiency": round(eff, 3) if eff else None},
-               "t32_linear_estimate": round(v_cpu * 32 / threads, 1), "t32_measured": threads == 32}
+               "thread_scaling": {str(half): round(v_half, 1), str(threads): round(v_cpu, 1),
+                                  "efficiency": round(eff_scal, 3) if eff_scal else None,
+                                  "wall_s": {str(half): round(dt_half, 2), str(threads): round(dt, 2)}},
+               "t32_linear_estimate": round(v_cpu * 32 / threads, 1),
+               "t32_measured": threads == 32 and eff >= 32}
         log(f"[bench] cpu_baseline: {json.dumps(cpu)}")
 
     # The end-to-end legs time a file-to-output run as a user starts it: the
@@ -874,14 +965,14 @@ def main():
         e2e = e2e_leg(ctx, cfg, lcfg, dict(WORKLOADS["fixed50"], coverage=wl["coverage"]),
                       min(args.e2e_windows, n_base), threads,
                       os.environ.get("TMPDIR", "/tmp"), cpu=not args.no_cpu,
-                      cpu_threads=args.cpu_threads or min(32, len(os.sched_getaffinity(0))))
+                      cpu_threads=args.cpu_threads or min(32, effective_cores()[0]))
         log(f"[bench] e2e: {json.dumps(e2e)}")
 
     e2e_u = None
     if rank == 0 and world == 1 and not args.no_legs and args.e2e_u_scale > 0:
         threads = args.cpu_threads or min(CPU_SHARE, len(os.sched_getaffinity(0)))
         e2e_u = e2e_u_leg(ctx, lcfg, threads, os.environ.get("TMPDIR", "/tmp"), scale=args.e2e_u_scale,
-                          cpu=not args.no_cpu, cpu_threads=args.cpu_threads or min(32, len(os.sched_getaffinity(0))))
+                          cpu=not args.no_cpu, cpu_threads=args.cpu_threads or min(32, effective_cores()[0]))
         log(f"[bench] e2e_u: {json.dumps(e2e_u)}")
         if e2e_u.get("k4"):
             kernels[e2e_u["k4"]["kernel"]] = {"ms": e2e_u["k4"]["ms"], "algo_bytes": e2e_u["k4"]["algo_bytes"],

@@ -392,22 +392,75 @@ def _window_job(args):
     return make_aln_window(*args)
 
 
-def make_aln_batch(spec: AlnSpec, windows=None, workers: int = 0) -> AlnBatch:
+def window_cost_estimate(spec: AlnSpec, w: int) -> float:
+    """The read bases of window w without building its reads: the same
+    draws as make_aln_window up to the read spans (the RNG stream is
+    replayed), the sum of the kept reads' lengths.  Proportional, up to
+    clipping and indels, to the window's SEQ + MM bytes (shard.aln_window_costs),
+    for dealing distinct windows before generating them."""
+    rng = np.random.default_rng([spec.seed, w, 77])
+    gap = spec.gap
+    if spec.gap_mix:
+        gap = int(np.exp(rng.uniform(np.log(5_000), np.log(500_000))))
+    max_len = int(spec.max_len * spec.len_scale)
+    stride = max(spec.window_stride, gap + 2 * spec.readback + 2 * max_len + 10_000)
+    s = spec.base + (w % max(1, (400_000_000 - spec.base) // stride)) * stride
+    e = s + gap
+    if spec.windows_at:
+        s, e = (int(x) for x in spec.windows_at[w])
+    f_lo, f_hi = max(0, s - spec.readback), e + spec.readback
+    span_lo, span_hi = f_lo - max_len, f_hi + max_len
+    L = span_hi - span_lo + 16
+    rng.integers(0, 4, L)
+    n_cpg = rng.poisson(spec.cpg_rate * L)
+    cpg = np.unique(rng.integers(1, L - 3, size=n_cpg))
+    cpg = cpg[np.concatenate([[True], np.diff(cpg) >= 2])]
+    rng.random(cpg.shape[0])
+    rng.integers(0, 2, cpg.shape[0])
+    if spec.het_snv_rate > 0:
+        raise ValueError("window_cost_estimate: no -u windows")
+    mu, sig = _lognormal_params(spec.mean_len * spec.len_scale, spec.sd_len * spec.len_scale)
+    n_draw = int(spec.coverage * (span_hi - span_lo) / (spec.mean_len * spec.len_scale))
+    starts = rng.integers(span_lo, f_hi, size=n_draw, dtype=np.int64)
+    lens = np.clip(np.exp(rng.normal(mu, sig, n_draw)), spec.min_len * spec.len_scale, max_len).astype(np.int64)
+    ends = starts + lens
+    keep = (ends > f_lo) & (starts < f_hi) & (starts >= 0)
+    return float(lens[keep].sum())
+
+
+def _cost_job(args):
+    return window_cost_estimate(*args)
+
+
+def window_cost_estimates(jobs, workers: int = 16) -> np.ndarray:
+    """window_cost_estimate over (spec, w) pairs, in worker processes."""
+    jobs = list(jobs)
+    if workers > 1 and len(jobs) >= 16:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            return np.array(pool.map(_cost_job, jobs, chunksize=16), np.float64)
+    return np.array([window_cost_estimate(*j) for j in jobs], np.float64)
+
+
+def make_aln_batch(spec: AlnSpec, windows=None, workers: int = 0, jobs=None) -> AlnBatch:
     """workers: processes generating windows in parallel (0: up to 16 when
     there are many windows; every window is a pure function of its index,
-    so the result does not depend on it)."""
-    if windows is None:
-        windows = range(spec.n_windows)
-    windows = list(windows)
+    so the result does not depend on it).  jobs: (spec, window) pairs
+    instead of `windows` of `spec` (windows of several seeds in one batch)."""
+    if jobs is None:
+        if windows is None:
+            windows = range(spec.n_windows)
+        jobs = [(spec, w) for w in windows]
+    jobs = list(jobs)
     if workers == 0:
         env = os.environ.get("PF_SYNTH_WORKERS")
-        workers = int(env) if env else (min(16, os.cpu_count() or 1) if len(windows) >= 16 else 1)
+        workers = int(env) if env else (min(16, os.cpu_count() or 1) if len(jobs) >= 16 else 1)
     if workers > 1:
         import multiprocessing as mp
         with mp.get_context("fork").Pool(workers) as pool:
-            parts = pool.map(_window_job, [(spec, w) for w in windows], chunksize=1)
+            parts = pool.map(_window_job, jobs, chunksize=1)
     else:
-        parts = [make_aln_window(spec, w) for w in windows]
+        parts = [make_aln_window(*j) for j in jobs]
     recs = [r for p in parts for r in p["recs"]]
 
     def off(key, f=lambda x: x.shape[0]):

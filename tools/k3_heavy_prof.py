@@ -102,5 +102,25 @@ if allp:
     for b in (32, 36, 44, 48, 56):
         print(f"  need > {b} KB: {(a[:, 1] > b).sum()} problems, min reads among them "
               f"{int(a[a[:, 1] > b, 0].min()) if (a[:, 1] > b).any() else '-'}")
+# K12 phases (K12_STAMP, cycles) per window: mean, the slowest window, and the
+# kernel's window-cycles against its time (how many windows run at once)
+k12 = raw[W * 64:].reshape(W, 16).astype(float)
+names12 = ["-", "T7+range", "sites", "revbuf", "dir arrays", "reservation", "methmers"]
+tot12 = k12[:, 1:7].sum(axis=1)
+mx = int(tot12.argmax())
+print(f"K12 phases, cycles: mean over windows | slowest window ({mx}: {int(st[mx, 0, 6])} reads, "
+      f"{int(st[mx, 0, 7])} sites, gap {int(aln.win_end[mx]) - int(aln.win_start[mx])})")
+for j in range(1, 7):
+    print(f"  {names12[j]:12s} {k12[:, j].mean():10.0f} | {k12[mx, j]:10.0f}")
+print(f"  window cycles: sum {tot12.sum() / 1e9:.3f} G, max {tot12.max() / 1e6:.2f} M, p90 "
+      f"{np.percentile(tot12, 90) / 1e6:.2f} M, median {np.median(tot12) / 1e6:.2f} M")
+kt12 = kt.get("pf_k12_sites_methmers", 0.0)
+if kt12:
+    print(f"  K12 {kt12:.3f} ms; sum of window cycles / (ms x 2.4 GHz) = "
+          f"{tot12.sum() / (kt12 * 1e-3 * 2.4e9):.0f} windows at once on average (256 CUs)")
+k2n = ["lb + ranges", "chars", "entries", "emission", "calls: flags+sites", "core tails", "loop back-edge"]
+print("  K12 methmer phase, wave 0, cycles summed over its reads: mean over windows")
+for j in range(7):
+    print(f"    {k2n[j]:18s} {k12[:, 8 + j].mean():10.0f}")
 db.free()
 ctx.close()
