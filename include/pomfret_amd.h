@@ -516,6 +516,21 @@ int  pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, c
  * for `methphase -u` without -c: one pass over each contig instead of two. */
 int  pf_haptag_bam_cov(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, const char *chrom,
                        pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *truncated);
+/* Both with the contig's position pieces given: n_bounds strictly increasing
+ * positions > 0 split [0, HTS_POS_MAX) into n_bounds + 1 fetch regions (a
+ * read is taken in the piece its start falls in; the reads, tags and order
+ * are the one-piece fetch's).  With the fetch cache on (a -u pre-pass that
+ * keeps its arenas) every piece's arena is kept, and a later window fetch of
+ * the contig is served by the piece whose region holds all its windows.
+ * cov / truncated NULL: no coverage estimate.  The driver places the bounds
+ * between its windows' fetch regions (pf_pipeline.c). */
+int  pf_haptag_bam_pieces(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, const char *chrom,
+                          uint32_t n_bounds, const int64_t *bounds, pf_bam_dev_fetch_t **fetch_out, int32_t *cov,
+                          int32_t *truncated);
+/* The pieces the -u pre-pass fetches a contig in by default: K =
+ * ceil(compressed bytes of the contig's index chunks / piece_bytes) (0: the
+ * PF_FETCH_PIECE_BYTES variable or 4 GiB), each *step bases long. */
+uint64_t pf_bam_contig_pieces(pf_bam_t *bam, int32_t tid, uint64_t piece_bytes, int64_t *step);
 
 
 /* The -u pre-pass reads of one contig (pre_haplotagging_read_in_one_ref,

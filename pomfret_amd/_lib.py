@@ -330,11 +330,12 @@ class Context:
         return out[:n.value].tobytes(), st, ms.value
 
     def kernel_times(self):
-        names = (C.c_char_p * 8)()
-        ms = (C.c_float * 8)()
-        n = C.c_int(8)
+        cap = 16
+        names = (C.c_char_p * cap)()
+        ms = (C.c_float * cap)()
+        n = C.c_int(cap)
         _check(lib().pf_last_kernel_times(self.handle, names, ms, C.byref(n)), "kernel_times")
-        return {names[i].decode(): float(ms[i]) for i in range(n.value)}
+        return {names[i].decode(): float(ms[i]) for i in range(min(n.value, cap))}
 
     def selftest(self) -> int:
         """Mismatching (a, b) pairs of the kernels' 16-bit count division

@@ -24,6 +24,7 @@
 
 __global__ void pf_k12_sites_methmers(pf_dev_batch d);
 __global__ void pf_k2_methmers(pf_dev_batch d);
+__global__ void pf_k12_chunks(pf_dev_batch d);
 __global__ void pf_k3_greedy(pf_dev_batch d);
 __global__ void pf_k3_wave(pf_dev_batch d);
 __global__ void pf_k3_fallback(pf_dev_batch d);
@@ -34,18 +35,18 @@ __global__ void pf_k0_pack(pf_load_dev d);
 __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
-#define PF_NKERN 6
+#define PF_NKERN 7
 #define PF_SLOTS 2
 // I/O block header: status u32[4] | arena counters u64[3] (16) | K2, K3
 // fallback counters u32 (40, 44) | record level: staging bump pointer u64
 // (48), kept reads u32 (56), calls u64 (64), site slots u64 (72) | the heavy
 // kernel's deferral counter u32 (80) | the main greedy kernel's problem
-// counter u32 (84) | pad
+// counter u32 (84) | pf_k12_chunks' item count u32 (88) and next item u32 (92) | pad
 #define PF_IO_HDR 128ull
 
 // kernel timing slots: "pf_k0_pack" is the scan + pack pair
-static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k0_pack", "pf_k12_sites_methmers", "pf_k2_methmers",
-                                        "pf_k3_wave", "pf_k3_fallback"};
+static const char *k_names[PF_NKERN] = {"pf_k0_load", "pf_k0_pack", "pf_k12_sites_methmers", "pf_k12_chunks",
+                                        "pf_k2_methmers", "pf_k3_wave", "pf_k3_fallback"};
 #define PF_GROWABLE (PF_ST_KEYS_OVF | PF_ST_BIG_OVF | PF_ST_SCR_OVF | PF_ST_STAGE_OVF | PF_ST_CALL_OVF | PF_ST_SITES_OVF)
 
 struct pf_ctx {
@@ -614,6 +615,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         }
     }
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
+    ALLOC(d.k12c_list, 2ull * (R / PF_K12C_READS + W + 1));
     ALLOC(d.k3_fb_list, std::max<uint32_t>(4 * W, 1));       // the main kernel's deferrals, then pf_k3_heavy's
     // one I/O block: the counters zeroed before a run (status, arena
     // counters, fallback counter) followed by everything copied back after it,
@@ -632,6 +634,8 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     d.fb_ctr = reinterpret_cast<uint32_t *>(b->io + 40);
     d.k3_fb_ctr = reinterpret_cast<uint32_t *>(b->io + 44);
     d.k3_next = reinterpret_cast<uint32_t *>(b->io + 84);
+    d.k12c_ctr = reinterpret_cast<uint32_t *>(b->io + 88);
+    d.k12c_next = reinterpret_cast<uint32_t *>(b->io + 92);
     d.table = reinterpret_cast<int32_t *>(b->io + PF_IO_HDR);
     d.win_S = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 32ull * W);
     d.win_nreads = reinterpret_cast<uint32_t *>(b->io + PF_IO_HDR + 36ull * W);
@@ -695,6 +699,25 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     const char *kc = getenv("PF_K12_CAP"), *ks = getenv("PF_K12_SMAX");
     d.k12_capw = kc ? std::min<uint32_t>((uint32_t)atoi(kc), PF_K12_CAPW) : PF_K12_CAPW;
     d.k12_smax = ks ? std::min<uint32_t>((uint32_t)atoi(ks), PF_K12_SMAX) : PF_K12_SMAX;
+    {
+        // windows whose methmer phase K12 hands to pf_k12_chunks: those with
+        // at least 900 reads that alone exceed twice a CU's share of the
+        // batch's reads (records) -- a window that would be K12's tail.  On a
+        // 1024-window 60x batch none qualifies (K12 is throughput-bound
+        // there, and the chunks cost 0.1-0.2 ms); alone, the 500 kb window's
+        // K12 drops from 1.91 to 0.85 ms (profiles/r05/ab_chunk.txt).
+        // PF_K12C_MINR=n forces the bound (0: never).  And the window's
+        // sites must fit the kernel's LDS beside its wave buffers.
+        const char *km = getenv("PF_K12C_MINR");
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, b->ctx->device) != hipSuccess ||
+            ncu <= 0)
+            ncu = 256;
+        (void)hipGetLastError();
+        d.k12c_minr = km ? (uint32_t)atoi(km) : std::max<uint32_t>(900u, (uint32_t)(2ull * R / (uint32_t)ncu));
+        if (d.k12c_minr == 0) d.k12c_minr = 0xFFFFFFFFu;
+        d.k12c_smax = (uint32_t)((PF_K12C_LDS - PF_K12C_WAVES * PF_K12_WB * PF_K12_CAPW) / 14);
+    }
     const char *kd = getenv("PF_K12_DENSE");
     d.k12_dense = kd && atoi(kd) ? 1u : 0u;
     const char *ke = getenv("PF_K2_ENTCAP");
@@ -1103,12 +1126,24 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][3], st));
     if (stages < 2) return PF_OK;
+    // the heavy windows' methmer phase (usually a few windows): persistent,
+    // two workgroups per CU over K12's item list
+    if (d.k12c_minr != 0xFFFFFFFFu) {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0)
+            ncu = 1;
+        const uint32_t gc = std::min<uint32_t>(2u * (uint32_t)ncu, (uint32_t)(b->R / PF_K12C_READS + b->W + 1));
+        hipLaunchKernelGGL(pf_k12_chunks, dim3(gc), dim3(PF_K12C_WAVES * 64), PF_K12C_LDS, st, d);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(b->ev[slot][4], st));
+    if (stages < 2) return PF_OK;
     // fallback reads only (usually none): a grid-stride kernel over K12's list
     const uint64_t waves = 2ull * b->R;
     const uint32_t g2 = (uint32_t)std::min<uint64_t>((waves + PF_K2_WAVES - 1) / PF_K2_WAVES, 512);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][4], st));
+    HIPCHK(hipEventRecord(b->ev[slot][5], st));
     if (stages < 3) return PF_OK;
     // main greedy kernel: the 256-thread workgroup build; PF_K3_IMPL=wave runs
     // the one-wavefront build (measured slower on MI355X at 30x-60x: one wave
@@ -1120,7 +1155,7 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     const uint32_t nh = c->k3_block ? b->n_heavy : 0u;
     if (nh) {
         // the heavy problems on the second stream, from the same point (K2 done)
-        HIPCHK(hipStreamWaitEvent(c->stream2, b->ev[slot][4], 0));
+        HIPCHK(hipStreamWaitEvent(c->stream2, b->ev[slot][5], 0));
         HIPCHK(hipEventRecord(b->hev[slot][0], c->stream2));
         // its own deferral list: a problem beyond its budget runs in a fallback
         // launch right behind it on the same stream, beside the main kernel
@@ -1149,14 +1184,14 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     } else
         hipLaunchKernelGGL(pf_k3_wave, dim3(2 * b->W), dim3(64), d.lds_w, st, d);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(b->ev[slot][5], st));
+    HIPCHK(hipEventRecord(b->ev[slot][6], st));
     // the main kernel's deferred problems (usually none): a grid-stride kernel over its list
     HIPCHK(hipEventRecord(b->fev[slot][0], st));
     hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(2 * b->W, 512)), dim3(PF_K3_THREADS), d.lds_fb,
                        st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->fev[slot][1], st));
-    HIPCHK(hipEventRecord(b->ev[slot][6], st));
+    HIPCHK(hipEventRecord(b->ev[slot][7], st));
     if (nh) HIPCHK(hipStreamWaitEvent(st, b->hev[slot][1], 0));   // join: the heavy problems are done
     b->heavy_launched[slot] = nh != 0;
     HIPCHK(hipMemcpyAsync(b->h_io[slot], b->io, b->io_bytes, hipMemcpyDeviceToHost, st));
@@ -1434,7 +1469,7 @@ extern "C" int pf_last_kernel_times(pf_ctx_t *ctx, const char **names, float *ms
     int m = *n < tot ? *n : tot;
     for (int i = 0; i < m; i++) {
         if (i < PF_NKERN) {
-            if (names) names[i] = (i == 4 && ctx->k3_block) ? "pf_k3_greedy" : k_names[i];
+            if (names) names[i] = (i == 5 && ctx->k3_block) ? "pf_k3_greedy" : k_names[i];
             if (ms) ms[i] = ctx->have_times ? ctx->last_ms[i] : -1.0f;
         } else if (i == PF_NKERN && hv) {
             if (names) names[i] = "pf_k3_heavy";

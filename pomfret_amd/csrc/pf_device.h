@@ -28,6 +28,9 @@
 #define PF_K12_CAPW 512           /* per-wave site-entry buffer of the fused methmer phase */
 #define PF_K12_WB 8               /* bytes per wave-buffer entry: chars, crank, u16 irank, u32 staged key */
 #define PF_K12_SMAX 4600          /* sites whose arrays (14 B/site) fit LDS beside 16 such buffers */
+#define PF_K12C_READS 64          /* reads per item of pf_k12_chunks (the heavy windows' methmer phase) */
+#define PF_K12C_WAVES 8           /* its waves per workgroup */
+#define PF_K12C_LDS 61440         /* its dynamic LDS: 14 B per site + PF_K12C_WAVES wave buffers (2 per CU) */
 #define PF_NONE 0xFFFFFFFFu
 
 /* status bits */
@@ -54,6 +57,9 @@ struct pf_dev_batch {
     const uint32_t *call_pos;
     const uint8_t *call_cat;
     uint32_t *fb_list, *fb_ctr;        /* reads left to the K2 fallback kernel */
+    uint32_t *k12c_list, *k12c_ctr;    /* (window, first read) chunks of the heavy windows for pf_k12_chunks */
+    uint32_t *k12c_next;               /* pf_k12_chunks' next item */
+    uint32_t k12c_minr, k12c_smax;     /* windows with >= k12c_minr reads and <= k12c_smax sites go there */
     /* per-window results of K1 */
     uint32_t *win_S, *win_nreads;
     const uint32_t *k3_order;          /* [2W] greedy problems (w<<1|dir), heaviest first */

@@ -183,14 +183,19 @@ struct Plan {
     uint64_t arena = 0;                     // inflated bytes
 };
 
-// Whole-contig arenas kept on the device between the -u pre-pass and the
-// window jobs (HBM holds a contig's inflated BAM many times over): the
-// pre-pass fetches each contig whole, and a window job of that contig on the
-// same context then takes its blocks from the kept arena instead of reading
-// and inflating them again.  Keyed by context, file (path, size, mtime) and
-// contig; kept while the device keeps a reserve free; released by
-// pf_fetch_cache_clear (end of a methphase run, context destruction).
+// Contig arenas kept on the device between the -u pre-pass and the window
+// jobs (HBM holds a contig's inflated BAM many times over): the pre-pass
+// fetches each contig whole -- a chromosome-scale contig in position pieces of
+// about 4 GiB of compressed BAM, each kept as an arena of its own (round 5) --
+// and a window job of that contig on the same device then takes its blocks
+// from the kept arena whose position range holds every window of the job
+// (the driver cuts jobs at the pieces' bounds and places the bounds between
+// windows) instead of reading and inflating them again.  Keyed by context,
+// file (path, size, mtime), contig and position range; kept while the device
+// keeps a reserve free; released by pf_fetch_cache_clear (end of a methphase
+// run, context destruction).
 struct ArenaCache {
+    int64_t pbeg = 0, pend = INT64_MAX;     // the piece's fetch region [pbeg, pend) of the contig
     const pf_ctx_t *ctx = nullptr;
     std::string path;
     uint64_t fsize = 0;
@@ -207,7 +212,8 @@ std::vector<ArenaCache *> g_cache;
 std::vector<const pf_ctx_t *> g_keep_on;    // contexts whose -u pre-pass keeps its arenas
 
 bool cache_enabled(const pf_ctx_t *ctx) {
-    static const bool off = [] { const char *e = getenv("PF_FETCH_CACHE"); return e && !strcmp(e, "0"); }();
+    const char *e = getenv("PF_FETCH_CACHE");
+    const bool off = e && !strcmp(e, "0");
     if (off) return false;
     std::lock_guard<std::mutex> lk(g_cache_mu);
     return std::find(g_keep_on.begin(), g_keep_on.end(), ctx) != g_keep_on.end();
@@ -226,26 +232,33 @@ extern "C" int pf_fetch_cache_scope_ctx(void) {
 // driver's contexts of one GPU (PF_DEV_CONTEXTS) share its HBM, and the -u
 // pre-pass that wrote the arenas has finished (its jobs joined) before the
 // window jobs look them up.
-const ArenaCache *cache_find(const pf_ctx_t *ctx, const char *path, const struct stat &s, int32_t tid) {
+// ... whose piece holds the regions [lo, hi) of a fetch (lo > hi: any piece)
+const ArenaCache *cache_find(const pf_ctx_t *ctx, const char *path, const struct stat &s, int32_t tid, int64_t lo,
+                             int64_t hi) {
     const int dev = pf_ctx_device((const pf_ctx *)ctx);
     const bool by_ctx = pf_fetch_cache_scope_ctx() != 0;
     std::lock_guard<std::mutex> lk(g_cache_mu);
     for (const ArenaCache *c : g_cache)
         if ((c->ctx == ctx || (!by_ctx && pf_ctx_device((const pf_ctx *)c->ctx) == dev)) && c->tid == tid &&
+            (lo > hi || (c->pbeg <= lo && hi <= c->pend)) &&
             c->fsize == (uint64_t)s.st_size && c->mt_s == (int64_t)s.st_mtim.tv_sec &&
             c->mt_ns == (int64_t)s.st_mtim.tv_nsec && c->path == path)
             return c;
     return nullptr;
 }
 
-// The first of ctxs[0, n) that a kept arena of (path, contig tid) would
-// serve, or -1: the home of a window job of that contig (pf_pipeline.c).
-extern "C" int pf_fetch_cache_home(pf_ctx_t *const *ctxs, int n, const char *path, int32_t tid) {
+// The first of ctxs[0, n) that a kept arena of (path, contig tid) whose piece
+// holds [lo, hi) would serve, or -1: the home of a window job (pf_pipeline.c).
+extern "C" int pf_fetch_cache_home_range(pf_ctx_t *const *ctxs, int n, const char *path, int32_t tid, int64_t lo,
+                                         int64_t hi) {
     struct stat s;
     if (!path || stat(path, &s) != 0) return -1;
     for (int i = 0; i < n; i++)
-        if (cache_find(ctxs[i], path, s, tid)) return i;
+        if (cache_find(ctxs[i], path, s, tid, lo, hi)) return i;
     return -1;
+}
+extern "C" int pf_fetch_cache_home(pf_ctx_t *const *ctxs, int n, const char *path, int32_t tid) {
+    return pf_fetch_cache_home_range(ctxs, n, path, tid, 1, 0);
 }
 
 // The plan's blocks from a kept arena: per run, the kept blocks from its
@@ -400,7 +413,9 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
     struct stat stt;
     if (fstat(fd, &stt) != 0) { close(fd); return -1; }
     const uint64_t fsize = (uint64_t)stt.st_size;
-    const ArenaCache *AC = cache_find(ctx, path, stt, tid);
+    int64_t lo_all = INT64_MAX, hi_all = 0;               // the regions' union: the kept piece must hold it
+    for (uint32_t w = 0; w < W; w++) { lo_all = std::min(lo_all, beg[w]); hi_all = std::max(hi_all, end[w]); }
+    const ArenaCache *AC = W ? cache_find(ctx, path, stt, tid, lo_all, hi_all) : nullptr;
     hipStream_t st = pf_ctx_stream((const pf_ctx *)ctx);
     if (hipSetDevice(pf_ctx_device((const pf_ctx *)ctx)) != hipSuccess) { close(fd); return PF_ERR_HIP; }
     memset(&F->pub, 0, sizeof F->pub);
@@ -1081,7 +1096,7 @@ extern "C" int pf_batch_upload_bam(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_
 // [c0, c1) of the file): K pieces of equal reference length; a record belongs
 // to the piece its start falls in.  piece_bytes 0: PF_FETCH_PIECE_BYTES or
 // 4 GiB (tests force several pieces on small files with the variable).
-static uint64_t contig_pieces(pf_bam_t *bam, int32_t tid, uint64_t piece_bytes, int64_t *step) {
+extern "C" uint64_t pf_bam_contig_pieces(pf_bam_t *bam, int32_t tid, uint64_t piece_bytes, int64_t *step) {
     if (!piece_bytes)
         if (const char *e = getenv("PF_FETCH_PIECE_BYTES")) piece_bytes = strtoull(e, nullptr, 10);
     if (!piece_bytes) piece_bytes = 4ull << 30;
@@ -1119,7 +1134,8 @@ static void cov_add(std::vector<uint64_t> &bins, const Small &S, uint64_t i) {
 // when a truncated record ended the fetch (the estimate's serial pass stops
 // there).
 static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
-                           pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *trunc) {
+                           pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *trunc, uint32_t nb = 0,
+                           const int64_t *bounds = nullptr) {
     if (!ctx || !K || !bam || !chrom || !fetch_out) return PF_ERR_ARG;
     *fetch_out = nullptr;
     // sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX),
@@ -1130,7 +1146,11 @@ static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *ba
     const int32_t tid = pf_bam_tid(bam, chrom);
     if (tid < 0) return PF_ERR_ARG;
     int64_t step = 0;
-    const uint64_t NP = contig_pieces(bam, tid, 0, &step);
+    // the pieces' bounds: the caller's (the driver places them between its
+    // windows' fetch regions), else K pieces of equal reference length
+    const uint64_t NP = nb ? (uint64_t)nb + 1 : pf_bam_contig_pieces(bam, tid, 0, &step);
+    auto piece_beg = [&](uint64_t k) -> int64_t { return k == 0 ? 0 : nb ? bounds[k - 1] : (int64_t)k * step; };
+    auto piece_end = [&](uint64_t k) -> int64_t { return k + 1 == NP ? INT64_MAX : nb ? bounds[k] : (int64_t)(k + 1) * step; };
     const bool with_cov = cov != nullptr;
     std::vector<uint64_t> bins;
     if (with_cov) bins.assign(pf_bam_target_len(bam, tid) / 5000, 0);
@@ -1142,10 +1162,11 @@ static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *ba
     uint32_t attempts = 0;
     int rc = PF_OK;
     for (uint64_t k = 0; k < NP && !rc; k++) {
-        const int64_t beg = (int64_t)k * step, end = k + 1 == NP ? INT64_MAX : (int64_t)(k + 1) * step;
+        const int64_t beg = piece_beg(k), end = piece_end(k);
         pf_bam_dev_fetch_own P;
         std::vector<uint32_t> take;                           // this piece's -u reads: selection positions
-        ArenaCache *keep = NP == 1 && cache_enabled(ctx) ? new ArenaCache() : nullptr;
+        ArenaCache *keep = cache_enabled(ctx) ? new ArenaCache() : nullptr;
+        if (keep) { keep->pbeg = beg; keep->pend = end; }
         rc = dev_fetch(ctx, bam, tid, 1, &beg, &end, with_cov ? 0u : 1u, 0u, &P, [&](FetchOut &fo) -> int {
             const Small &S = *fo.S;
             uint64_t m = 0;                                   // records counted in an earlier piece
@@ -1269,6 +1290,15 @@ extern "C" int pf_haptag_bam_cov(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam
     return haptag_bam_impl(ctx, K, bam, chrom, fetch_out, cov, truncated);
 }
 
+extern "C" int pf_haptag_bam_pieces(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
+                                    uint32_t n_bounds, const int64_t *bounds, pf_bam_dev_fetch_t **fetch_out,
+                                    int32_t *cov, int32_t *truncated) {
+    if (n_bounds && !bounds) return PF_ERR_ARG;
+    for (uint32_t i = 0; i < n_bounds; i++)
+        if (bounds[i] <= (i ? bounds[i - 1] : 0)) return PF_ERR_ARG;     // strictly increasing, > 0
+    return haptag_bam_impl(ctx, K, bam, chrom, fetch_out, cov, truncated, n_bounds, bounds);
+}
+
 // estimate_read_coverage_dirtyfast (blockjoin.c:951-1040) through the device
 // fetch: the serial pass's records are, for a coordinate-sorted BAM, each
 // contig's records in index order followed by the unplaced tail, so the pass
@@ -1291,7 +1321,7 @@ static int est_contig(pf_ctx_t *ctx, pf_bam_t *bam, int32_t t, uint64_t piece_by
     if (nc == 0) return PF_OK;
     const uint32_t len = pf_bam_target_len(bam, t);
     int64_t step = 0;
-    const uint64_t K = contig_pieces(bam, t, piece_bytes, &step);
+    const uint64_t K = pf_bam_contig_pieces(bam, t, piece_bytes, &step);
     std::vector<uint64_t> bins(len / 5000, 0);
     for (uint64_t k = 0; k < K && !*stopped; k++) {
         const int64_t beg = (int64_t)k * step, end = k + 1 == K ? INT64_MAX : (int64_t)(k + 1) * step;

@@ -634,6 +634,90 @@ __global__ __launch_bounds__(PF_K2_WAVES * 64) void pf_k2_methmers(pf_dev_batch 
     }
 }
 
+// The methmer phase of one window over its reads i0, i0 + NW, ... < i1 (wave
+// wid of NW): one wavefront per read, both directions, the window's site
+// arrays in LDS (sp, st1, q1s, l0s, l1s; hsd when use_hash), the wave's
+// buffers at wb.  Used by K12 for its own reads and by pf_k12_chunks for the
+// read chunks of the windows K12 hands over.
+DEV void k12_methmers(const pf_dev_batch &d, uint32_t r0, uint32_t i0, uint32_t i1, uint32_t wid, uint32_t NW,
+                      uint32_t lane, uint32_t S, const uint32_t *sp, const uint32_t *st1, const uint32_t *q1s,
+                      const uint8_t *l0s, const uint8_t *l1s, const K2SiteHash &hsd, bool use_hash, uint8_t *wb,
+                      unsigned long long *k2acc) {
+        uint8_t *chars = wb, *crank = wb + PF_K12_CAPW;
+        uint16_t *irank = reinterpret_cast<uint16_t *>(wb + 2 * PF_K12_CAPW);
+        uint32_t *kst = reinterpret_cast<uint32_t *>(wb + 4 * PF_K12_CAPW);
+        // keys are staged in LDS and copied out at points where no prefetched
+        // load is younger than the copy: vmcnt counts loads and stores in
+        // issue order, so a load issued before a dynamic number of stores can
+        // only be waited for with vmcnt(0), which drains the stores too.  The
+        // dir-1 keys of read i are copied out after read i+1's prefetched
+        // calls have been consumed, just before read i+2's are issued.
+        uint32_t pend_n = 0;
+        uint64_t pend_off = 0;
+        // software pipeline over this wave's reads i, i+NW, ...: the scalars of
+        // read i+2NW and the calls of read i+NW are in flight while read i is
+        // processed
+        K2Read rdA, rdB;
+        uint32_t pA[K2_CR], tA[K2_CR], pB[K2_CR], tB[K2_CR];
+        const uint32_t iw = i0 + wid;
+        if (iw < i1) k2_load_scalars(d, r0 + iw, rdA);
+        if (iw + NW < i1) k2_load_scalars(d, r0 + iw + NW, rdB);
+        k2_issue_calls(d, iw < i1 ? rdA : K2Read{0, 0, 0, 0, 0, 0}, lane, pA, tA);
+        for (uint32_t i = iw; i < i1; i += NW) {
+            const uint32_t r = r0 + i;
+            K2_STAMP(6);
+            K2Read rd = rdA;
+            const uint64_t nc = rd.c1 - rd.c0;
+            const bool regs = rd.cap <= d.k12_capw && nc <= 64ull * K2_CR;
+            K2Calls cl;
+            if (regs) {
+                k2_finish_calls(rd.c0, rd.c1, lane, pA, tA, cl);
+                // last call position (sorted order) from the registers
+                uint32_t mc = 0;
+                if (nc) {
+                    const uint32_t ul = (uint32_t)((nc - 1) >> 6), ll = (uint32_t)((nc - 1) & 63);
+#pragma unroll
+                    for (int u = 0; u < K2_CR; u++)
+                        if ((uint32_t)u == ul) mc = rdl(cl.pos[u], ll);
+                }
+                rd.maxcall = mc;
+                k2_calls_sites(cl, sp, S, hsd, use_hash);
+            }
+            K2_STAMP(4);
+            k2_flush(d, kst, pend_off, pend_n, lane);
+            pend_n = 0;
+            K2Read rdC = {0, 0, 0, 0, 0, 0};
+            if (i + 2 * NW < i1) k2_load_scalars(d, r0 + i + 2 * NW, rdC);
+            k2_issue_calls(d, i + NW < i1 ? rdB : K2Read{0, 0, 0, 0, 0, 0}, lane, pB, tB);
+            K2_STAMP(8);
+            if (rd.cap > d.k12_capw) {
+                if (lane == 0) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r;
+            } else {
+                const uint64_t k0 = d.mmr_off[2ull * r], k1 = d.mmr_off[2ull * r + 1];
+                if (regs) {
+                    const uint32_t n0 = k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW,
+                                                rd, &cl, k0, k2acc, kst);
+                    k2_flush(d, kst, k0, n0, lane);
+                    K2_STAMP(5);
+                    pend_n = k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd,
+                                     &cl, k1, k2acc, kst);
+                    pend_off = k1;
+                    K2_STAMP(5);
+                } else {
+                    rd.maxcall = nc ? d.call_pos[rd.c1 - 1] : 0u;
+                    k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW, rd, nullptr, k0);
+                    k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd, nullptr, k1);
+                }
+            }
+            rdA = rdB;
+            rdB = rdC;
+#pragma unroll
+            for (int u = 0; u < K2_CR; u++) { pA[u] = pB[u]; tA[u] = tB[u]; }
+            K2_STAMP(7);
+        }
+        k2_flush(d, kst, pend_off, pend_n, lane);
+}
+
 // ========================================================================
 // K12: sites + directional methmer ranges + end-order + arena reservation,
 // then every read's methmers (both directions) from LDS-resident site arrays
@@ -1146,88 +1230,27 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     hsd.mask = HS - 1;
     hsd.pmin = pmin;
 
-    if (staged) {
+    if (staged && R >= d.k12c_minr && S <= d.k12c_smax) {
+        // a heavy window: its reads go to pf_k12_chunks in chunks of
+        // PF_K12C_READS, spread over the device, instead of this workgroup's
+        // 16 waves (round 5: the 500 kb window's methmer phase was 1.3 ms of
+        // its 1.9 ms here)
+        for (uint32_t c = tid; c * PF_K12C_READS < R; c += NT) {
+            const uint32_t k = atomicAdd(d.k12c_ctr, 1u);
+            d.k12c_list[2ull * k] = w;
+            d.k12c_list[2ull * k + 1] = c * PF_K12C_READS;
+        }
+    } else if (staged) {
         // per-wave buffers: chars, crank (u8), irank (u16), key staging (u32)
         uint8_t *wb = reinterpret_cast<uint8_t *>(tile) + arr_b + (use_hash ? 4u * HS : 0u) +
                       wid * (uint64_t)PF_K12_WB * PF_K12_CAPW;
-        uint8_t *chars = wb, *crank = wb + PF_K12_CAPW;
-        uint16_t *irank = reinterpret_cast<uint16_t *>(wb + 2 * PF_K12_CAPW);
-        uint32_t *kst = reinterpret_cast<uint32_t *>(wb + 4 * PF_K12_CAPW);
-        // keys are staged in LDS and copied out at points where no prefetched
-        // load is younger than the copy: vmcnt counts loads and stores in
-        // issue order, so a load issued before a dynamic number of stores can
-        // only be waited for with vmcnt(0), which drains the stores too.  The
-        // dir-1 keys of read i are copied out after read i+1's prefetched
-        // calls have been consumed, just before read i+2's are issued.
-        uint32_t pend_n = 0;
-        uint64_t pend_off = 0;
 #ifdef PF_K3_PROFILE
         unsigned long long k2a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
         unsigned long long *k2acc = wid == 0 ? k2a : nullptr;
 #else
         unsigned long long *k2acc = nullptr;
 #endif
-        // software pipeline over this wave's reads i, i+NW, ...: the scalars of
-        // read i+2NW and the calls of read i+NW are in flight while read i is
-        // processed
-        K2Read rdA, rdB;
-        uint32_t pA[K2_CR], tA[K2_CR], pB[K2_CR], tB[K2_CR];
-        if (wid < R) k2_load_scalars(d, r0 + wid, rdA);
-        if (wid + NW < R) k2_load_scalars(d, r0 + wid + NW, rdB);
-        k2_issue_calls(d, wid < R ? rdA : K2Read{0, 0, 0, 0, 0, 0}, lane, pA, tA);
-        for (uint32_t i = wid; i < R; i += NW) {
-            const uint32_t r = r0 + i;
-            K2_STAMP(6);
-            K2Read rd = rdA;
-            const uint64_t nc = rd.c1 - rd.c0;
-            const bool regs = rd.cap <= d.k12_capw && nc <= 64ull * K2_CR;
-            K2Calls cl;
-            if (regs) {
-                k2_finish_calls(rd.c0, rd.c1, lane, pA, tA, cl);
-                // last call position (sorted order) from the registers
-                uint32_t mc = 0;
-                if (nc) {
-                    const uint32_t ul = (uint32_t)((nc - 1) >> 6), ll = (uint32_t)((nc - 1) & 63);
-#pragma unroll
-                    for (int u = 0; u < K2_CR; u++)
-                        if ((uint32_t)u == ul) mc = rdl(cl.pos[u], ll);
-                }
-                rd.maxcall = mc;
-                k2_calls_sites(cl, sp, S, hsd, use_hash);
-            }
-            K2_STAMP(4);
-            k2_flush(d, kst, pend_off, pend_n, lane);
-            pend_n = 0;
-            K2Read rdC = {0, 0, 0, 0, 0, 0};
-            if (i + 2 * NW < R) k2_load_scalars(d, r0 + i + 2 * NW, rdC);
-            k2_issue_calls(d, i + NW < R ? rdB : K2Read{0, 0, 0, 0, 0, 0}, lane, pB, tB);
-            K2_STAMP(8);
-            if (rd.cap > d.k12_capw) {
-                if (lane == 0) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r;
-            } else {
-                const uint64_t k0 = d.mmr_off[2ull * r], k1 = d.mmr_off[2ull * r + 1];
-                if (regs) {
-                    const uint32_t n0 = k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW,
-                                                rd, &cl, k0, k2acc, kst);
-                    k2_flush(d, kst, k0, n0, lane);
-                    K2_STAMP(5);
-                    pend_n = k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd,
-                                     &cl, k1, k2acc, kst);
-                    pend_off = k1;
-                    K2_STAMP(5);
-                } else {
-                    rd.maxcall = nc ? d.call_pos[rd.c1 - 1] : 0u;
-                    k2_core(d, r, 0, lane, S, sp, sp, l0s, q1s, chars, crank, irank, PF_K12_CAPW, rd, nullptr, k0);
-                    k2_core(d, r, 1, lane, S, sp, st1, l1s, q1s, chars, crank, irank, PF_K12_CAPW, rd, nullptr, k1);
-                }
-            }
-            rdA = rdB;
-            rdB = rdC;
-#pragma unroll
-            for (int u = 0; u < K2_CR; u++) { pA[u] = pB[u]; tA[u] = tB[u]; }
-            K2_STAMP(7);
-        }
-        k2_flush(d, kst, pend_off, pend_n, lane);
+        k12_methmers(d, r0, 0, R, wid, NW, lane, S, sp, st1, q1s, l0s, l1s, hsd, use_hash, wb, k2acc);
 #ifdef PF_K3_PROFILE
         if (tid == 0) {
             for (int j = 0; j < 7; j++) d.prof[64ull * d.W + (uint64_t)w * 16 + 8 + j] = k2a[j];
@@ -1240,6 +1263,47 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     }
     __syncthreads();
     K12_STAMP(6);
+}
+
+// The methmer phase of the heavy windows K12 handed over: each item is
+// PF_K12C_READS reads of one window; a workgroup stages the window's site
+// arrays (14 B per site, written by K12) in LDS and runs k12_methmers over
+// the chunk with its PF_K12C_WAVES waves.  Persistent over the item counter.
+// No position hash (the heavy windows' calls span beyond K12's bitmap): the
+// calls' site indices come from binary searches in LDS, as K12's dense-path
+// windows do.
+__global__ __launch_bounds__(PF_K12C_WAVES * 64) void pf_k12_chunks(pf_dev_batch d) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint32_t s_item;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t n = *d.k12c_ctr;
+    for (;;) {
+        if (tid == 0) s_item = atomicAdd(d.k12c_next, 1u);
+        __syncthreads();
+        const uint32_t it = s_item;
+        if (it >= n) break;
+        const uint32_t w = d.k12c_list[2ull * it], c0 = d.k12c_list[2ull * it + 1];
+        const uint32_t r0 = d.win_read_off[w], R = d.win_read_off[w + 1] - r0;
+        const uint32_t S = d.win_S[w];
+        const uint64_t sb = d.win_site_off[w];
+        uint32_t *sp = reinterpret_cast<uint32_t *>(smem), *st1 = sp + S, *q1s = sp + 2 * S;
+        uint8_t *l0s = reinterpret_cast<uint8_t *>(sp + 3 * S), *l1s = l0s + S;
+        for (uint32_t p = tid; p < S; p += PF_K12C_WAVES * 64) {
+            sp[p] = d.site_pos[sb + p];
+            st1[p] = d.st1_pos[sb + p];
+            q1s[p] = d.site_q1[sb + p];
+            l0s[p] = d.len0[sb + p];
+            l1s[p] = d.len1[sb + p];
+        }
+        __syncthreads();
+        const uint32_t arr_b = (uint32_t)((14ull * S + 15) & ~15ull);
+        uint8_t *wb = smem + arr_b + wid * (uint64_t)PF_K12_WB * PF_K12_CAPW;
+        K2SiteHash hsd;
+        hsd.t = nullptr; hsd.mask = 0; hsd.pmin = 0;
+        const uint32_t c1 = min(R, c0 + PF_K12C_READS);
+        k12_methmers(d, r0, c0, c1, wid, PF_K12C_WAVES, lane, S, sp, st1, q1s, l0s, l1s, hsd, false, wb, nullptr);
+        __syncthreads();                                 // the site arrays are reused by the next item
+    }
 }
 
 // ========================================================================
@@ -1316,7 +1380,7 @@ DEV void k3_each_key(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t di
 template <int NT = PF_K3_THREADS>
 DEV void k3_dict(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_t S, uint32_t dir,
                  uint64_t *masks, uint32_t *base, uint32_t *sh_scan, K3Ctl &ctl) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t tid = threadIdx.x;
     const uint32_t MW = (uint32_t)d.mw;
     for (uint32_t j = tid; j < S * MW; j += NT) masks[j] = 0;
     __syncthreads();

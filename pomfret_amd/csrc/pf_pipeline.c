@@ -198,6 +198,8 @@ int pf_tags_view(const pf_tags_t *t, pf_qname_tags_t *out) {
 
 typedef struct {
     uint32_t contig, w0, w1;   /* windows [w0, w1) of the plan's global window list */
+    int64_t lo, hi;            /* window jobs: the union of the windows' fetch regions */
+    int32_t bc;                /* -u jobs: the window contig whose piece bounds the fetch uses (-1: none) */
     double cost;
     int32_t rank;
     int done;
@@ -214,6 +216,7 @@ typedef struct {
 /* pf_ingest.hip / pf_api.hip */
 int pf_fetch_cache_scope_ctx(void);
 int pf_fetch_cache_home(pf_ctx_t *const *ctxs, int n, const char *path, int32_t tid);
+int pf_fetch_cache_home_range(pf_ctx_t *const *ctxs, int n, const char *path, int32_t tid, int64_t lo, int64_t hi);
 int pf_ctx_device(const pf_ctx_t *ctx);
 
 struct pf_mp_plan {
@@ -224,6 +227,12 @@ struct pf_mp_plan {
     pf_gaps_t *ugaps_own;      /* -u with --gtf / --tsv: the VCF's own gaps */
     const pf_gaps_t *ug;       /* contigs of the -u pre-pass (the VCF's): ugaps_own or gaps */
     int32_t *utid;             /* [ug->n_contigs] their BAM tids or -1 */
+    /* -u pre-pass pieces of a chromosome-scale contig (window contig c's
+     * bounds bnd[bnd_off[c], bnd_off[c+1])): placed between the contig's
+     * windows' fetch regions, so every window job -- cut at the bounds --
+     * is served by one kept piece arena */
+    uint64_t *bnd_off;
+    int64_t *bnd;
     char *interval_path;
     int32_t *tid;              /* [n_contigs] BAM tid or -1 */
     pf_cfg_t *cfg;             /* [n_contigs] */
@@ -312,7 +321,7 @@ void pf_mp_free(pf_mp_plan_t *p) {
     if (p->blocks) pf_blocks_free(p->blocks);
     if (p->gaps) pf_gaps_free(p->gaps);
     if (p->ugaps_own) pf_gaps_free(p->ugaps_own);
-    free(p->utid);
+    free(p->utid); free(p->bnd_off); free(p->bnd);
     free(p->bam_path); free(p->vcf_path); free(p->out_prefix); free(p->interval_path);
     free(p->ucov); free(p->utrunc); free(p->uhave);
     pthread_mutex_destroy(&p->st_mu);
@@ -513,9 +522,65 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
     if (nw > UINT32_MAX) { pf_mp_free(p); return PF_ERR_LIMIT; }
     p->n_windows = (uint32_t)nw;
 
+    /* -u pre-pass pieces (device fetch): a contig past the piece size is
+     * fetched in position pieces whose arenas are kept one by one; each bound
+     * moves from k * step to the nearest position outside every window's
+     * fetch region (within half a step), so no window straddles two pieces */
+    p->bnd_off = (uint64_t *)calloc(C + 1, sizeof(uint64_t));
+    if (!p->bnd_off) { pf_mp_free(p); return PF_ERR_NOMEM; }
+    if (o->untagged && !o->host_fetch && o->mode == PF_MODE_METHPHASE) {
+        pf_bam_t *bb = NULL;
+        rc = pf_bam_open(o->bam_path, NULL, &bb);
+        uint64_t nb = 0, bcap = 0;
+        for (uint32_t c = 0; c < C && !rc; c++) {
+            p->bnd_off[c] = nb;
+            if (p->tid[c] < 0) continue;
+            int64_t step = 0;
+            const uint64_t K = pf_bam_contig_pieces(bb, p->tid[c], 0, &step);
+            if (K <= 1 || step <= 0) continue;
+            /* the windows' fetch regions, merged into clusters */
+            const uint64_t w0 = p->win_off[c], w1 = p->win_off[c + 1];
+            int64_t *ca = (int64_t *)malloc(2 * (w1 - w0 + 1) * sizeof(int64_t));
+            if (!ca) { rc = PF_ERR_NOMEM; break; }
+            uint64_t ncl = 0;
+            for (uint64_t w = w0; w < w1; w++) {          /* windows are in file order: starts ascending */
+                const int64_t a = p->win_start[w] > PF_READBACK ? (int64_t)p->win_start[w] - PF_READBACK : 0;
+                const int64_t b = (int64_t)p->win_end[w] + PF_READBACK;
+                if (ncl && a < ca[2 * ncl - 1]) { if (b > ca[2 * ncl - 1]) ca[2 * ncl - 1] = b; }
+                else { ca[2 * ncl] = a; ca[2 * ncl + 1] = b; ncl++; }
+            }
+            int64_t prev = 0;
+            for (uint64_t k = 1; k < K; k++) {
+                const int64_t t = (int64_t)k * step;
+                int64_t x = t;
+                for (uint64_t q = 0; q < ncl; q++) {
+                    if (ca[2 * q] < t && t < ca[2 * q + 1]) {
+                        const int64_t A = ca[2 * q], B = ca[2 * q + 1];
+                        x = (t - A <= B - t && A > prev) ? A : B;
+                        if (x - t > step / 2 || t - x > step / 2) x = t;
+                        break;
+                    }
+                }
+                if (x <= prev) continue;
+                if (nb == bcap) {
+                    bcap = bcap ? 2 * bcap : 64;
+                    int64_t *nbp = (int64_t *)realloc(p->bnd, bcap * sizeof(int64_t));
+                    if (!nbp) { rc = PF_ERR_NOMEM; break; }
+                    p->bnd = nbp;
+                }
+                p->bnd[nb++] = x;
+                prev = x;
+            }
+            free(ca);
+        }
+        p->bnd_off[C] = nb;
+        if (bb) pf_bam_close(bb);
+        if (rc) { pf_mp_free(p); return rc; }
+    }
+
     /* window jobs: runs of consecutive windows of one contig, at most
      * job_windows windows and, with several devices or ranks, small enough
-     * that every one gets several jobs */
+     * that every one gets several jobs; never across a -u piece bound */
     const uint32_t jw = o->job_windows ? o->job_windows : PF_JOB_WINDOWS_DEFAULT;
     double tot_span = 0;
     for (uint64_t w = 0; w < nw; w++) tot_span += (double)(p->win_end[w] - p->win_start[w]) + 2.0 * PF_READBACK;
@@ -526,11 +591,22 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
     if (!p->jobs) { pf_mp_free(p); return PF_ERR_NOMEM; }
     for (uint32_t c = 0; c < C; c++) {
         uint64_t w = p->win_off[c];
+        const int64_t *bd = p->bnd + p->bnd_off[c];
+        const uint64_t nbd = p->bnd_off[c + 1] - p->bnd_off[c];
+        /* the piece a window's fetch region starts in */
+        #define WIN_LO(w_) ((int64_t)(p->win_start[w_] > PF_READBACK ? p->win_start[w_] - PF_READBACK : 0))
+        #define WIN_HI(w_) ((int64_t)p->win_end[w_] + PF_READBACK)
         while (w < p->win_off[c + 1]) {
             const uint64_t w0 = w;
             double span = 0;
-            while (w < p->win_off[c + 1] && w - w0 < jw && (w == w0 || span < span_cap)) {
+            uint64_t pc = 0;
+            while (pc < nbd && bd[pc] <= WIN_LO(w0)) pc++;
+            int64_t lo = WIN_LO(w0), hi = WIN_HI(w0);
+            while (w < p->win_off[c + 1] && w - w0 < jw && (w == w0 || span < span_cap) &&
+                   (w == w0 || pc >= nbd || WIN_LO(w) < bd[pc])) {
                 span += (double)(p->win_end[w] - p->win_start[w]) + 2.0 * PF_READBACK;
+                if (WIN_LO(w) < lo) lo = WIN_LO(w);
+                if (WIN_HI(w) > hi) hi = WIN_HI(w);
                 w++;
             }
             if (nj == jcap) {
@@ -542,6 +618,7 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
             }
             job_t *J = &p->jobs[nj++];
             J->contig = c; J->w0 = (uint32_t)w0; J->w1 = (uint32_t)w; J->cost = span;
+            J->lo = lo; J->hi = hi; J->bc = -1;
         }
     }
     p->n_jobs = nj;
@@ -559,6 +636,9 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
             job_t *J = &p->ujobs[nu++];
             J->contig = c;
             J->cost = (double)pf_bam_target_len(b2, p->utid[c]);
+            J->bc = -1;                                          /* the window contig of the same name */
+            for (uint32_t wc = 0; wc < C; wc++)
+                if (!strcmp(g->names[wc], p->ug->names[c])) { J->bc = (int32_t)wc; break; }
         }
         if (b2) pf_bam_close(b2);
         p->n_ujobs = nu;
@@ -751,11 +831,15 @@ int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
         /* device fetch + K4 on the device (pf_haptag_bam) */
         pf_bam_dev_fetch_t *F = NULL;
         const double t0 = now_s();
+        /* the contig's pieces: the plan's bounds (between its windows), or
+         * the default equal-length pieces when it has none */
+        const uint64_t b0 = J->bc >= 0 ? p->bnd_off[J->bc] : 0, b1 = J->bc >= 0 ? p->bnd_off[J->bc + 1] : 0;
         if (p->est_deferred) {                  /* the contig's coverage estimate from the same fetch */
-            rc = pf_haptag_bam_cov(ctx, &kt->vars, bam, contig, &F, &p->ucov[J->contig], &p->utrunc[J->contig]);
+            rc = pf_haptag_bam_pieces(ctx, &kt->vars, bam, contig, (uint32_t)(b1 - b0), p->bnd + b0, &F,
+                                      &p->ucov[J->contig], &p->utrunc[J->contig]);
             if (!rc) p->uhave[J->contig] = 1;
         } else {
-            rc = pf_haptag_bam(ctx, &kt->vars, bam, contig, &F);
+            rc = pf_haptag_bam_pieces(ctx, &kt->vars, bam, contig, (uint32_t)(b1 - b0), p->bnd + b0, &F, NULL, NULL);
         }
         if (!rc) st_fetch(p, 1, F, (now_s() - t0) * 1e3 - F->ms_total);
         if (!rc && F->n_recs) {
@@ -1554,7 +1638,8 @@ static int run_on_devices_(pf_mp_plan_t *p, const pf_methphase_opts_t *o, int ki
     for (uint32_t i = 0; i < nt && !rc; i++) {
         home[i] = q.n_groups;                       /* the shared queue */
         if (affine) {
-            const int h = pf_fetch_cache_home(o->ctxs, nd, p->bam_path, p->tid[J[todo[i]].contig]);
+            const job_t *Jt = &J[todo[i]];
+            const int h = pf_fetch_cache_home_range(o->ctxs, nd, p->bam_path, p->tid[Jt->contig], Jt->lo, Jt->hi);
             if (h >= 0) home[i] = gid[h];
         }
         q.off[home[i] + 1]++;

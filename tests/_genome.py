@@ -292,6 +292,19 @@ def small_spec(seed: int = 7) -> GenomeSpec:
                                   min_len=7_500, max_len=75_000))
 
 
+def pieces_spec(seed: int = 5) -> GenomeSpec:
+    """One 3 Mb contig whose phase blocks (250-400 kb) leave room between the
+    windows' fetch regions (gap + 2 x 50 kb): the -u pre-pass's position
+    pieces (forced small with PF_FETCH_PIECE_BYTES) get bounds between
+    windows, so every window job is served by one kept piece arena."""
+    from pomfret_amd.synth_aln import AlnSpec
+    return GenomeSpec(contigs=(("chrP", 3_000_000),), coverage=30, block_min=250_000, block_max=400_000,
+                      short_block_frac=0.0, gap_min=5_000, gap_max=40_000, lead=60_000, seed=seed, qual=False,
+                      level=1, chunk_reads=400,
+                      aln=AlnSpec(het_snv_rate=0.001, untag_frac=0.0, mean_len=15_000, sd_len=7_500,
+                                  min_len=7_500, max_len=75_000))
+
+
 def report_spec(seed: int = 11) -> GenomeSpec:
     """BASELINE configs[4]'s shape at test scale: a 200x pileup over one
     contig with pre-haplotagged reads, phase blocks of 40-90 kb (the report's

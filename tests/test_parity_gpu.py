@@ -231,13 +231,18 @@ def test_wide_windows_parity(oracle_lib, gpu_ctx):
 
 
 @pytest.mark.parametrize("env", [{"PF_K12_CAP": "0"}, {"PF_K12_SMAX": "0"},
-                                 {"PF_K12_CAP": "0", "PF_K2_ENTCAP": "0"}, {"PF_K12_CAP": "40"}],
-                         ids=["all_reads_fallback", "no_lds_sites", "fallback_hbm_scratch", "mixed"])
+                                 {"PF_K12_CAP": "0", "PF_K2_ENTCAP": "0"}, {"PF_K12_CAP": "40"},
+                                 {"PF_K12C_MINR": "1"}, {"PF_K12C_MINR": "1", "PF_K12_CAP": "40"},
+                                 {"PF_K12C_MINR": "0"}],
+                         ids=["all_reads_fallback", "no_lds_sites", "fallback_hbm_scratch", "mixed",
+                              "all_windows_chunked", "chunked_and_fallback", "no_chunks"])
 def test_methmer_fallback_paths(oracle_lib, gpu_ctx, monkeypatch, env):
     """Reads the fused sites+methmers kernel hands to the K2 fallback kernel
     (site-entry bound above its wave buffer, windows whose sites do not fit
-    LDS, HBM scratch for very large reads) give the same bits, including every
-    read's methmer list."""
+    LDS, HBM scratch for very large reads), and windows it hands to
+    pf_k12_chunks (round 5: the heavy windows' methmer phase in 64-read
+    chunks over the device; PF_K12C_MINR=1 sends every window) give the same
+    bits, including every read's methmer list."""
     from pomfret_amd import Config
     for k, v in env.items():
         monkeypatch.setenv(k, v)
