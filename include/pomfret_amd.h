@@ -517,16 +517,20 @@ int  pf_haptag_bam(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, c
 int  pf_haptag_bam_cov(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, const char *chrom,
                        pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *truncated);
 /* Both with the contig's position pieces given: n_bounds strictly increasing
- * positions > 0 split [0, HTS_POS_MAX) into n_bounds + 1 fetch regions (a
- * read is taken in the piece its start falls in; the reads, tags and order
- * are the one-piece fetch's).  With the fetch cache on (a -u pre-pass that
+ * positions > 0 split [0, HTS_POS_MAX) into n_bounds + 1 pieces (a read is
+ * taken in the piece its start falls in; the reads, tags and order are the
+ * one-piece fetch's).  fetch_ends (optional, fetch_ends[k] >= bounds[k]):
+ * piece k fetches the region [bounds[k-1], fetch_ends[k]) -- reaching past
+ * its bound over the windows that start in it -- while its reads stay those
+ * starting before bounds[k].  With the fetch cache on (a -u pre-pass that
  * keeps its arenas) every piece's arena is kept, and a later window fetch of
- * the contig is served by the piece whose region holds all its windows.
- * cov / truncated NULL: no coverage estimate.  The driver places the bounds
- * between its windows' fetch regions (pf_pipeline.c). */
+ * the contig is served by the piece whose fetch region holds all its
+ * windows.  cov / truncated NULL: no coverage estimate.  The driver places
+ * the bounds between its windows' fetch regions where it can
+ * (pf_pipeline.c). */
 int  pf_haptag_bam_pieces(pf_ctx_t *ctx, const pf_known_vars_t *known, pf_bam_t *bam, const char *chrom,
-                          uint32_t n_bounds, const int64_t *bounds, pf_bam_dev_fetch_t **fetch_out, int32_t *cov,
-                          int32_t *truncated);
+                          uint32_t n_bounds, const int64_t *bounds, const int64_t *fetch_ends,
+                          pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *truncated);
 /* The pieces the -u pre-pass fetches a contig in by default: K =
  * ceil(compressed bytes of the contig's index chunks / piece_bytes) (0: the
  * PF_FETCH_PIECE_BYTES variable or 4 GiB), each *step bases long. */

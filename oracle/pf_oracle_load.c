@@ -15,9 +15,18 @@
  * specification that htslib implements -- PARITY UNPINNED for this part: no
  * reference test or fixture covers it.  Definitions where htslib's behaviour
  * on malformed input is not observable from the reference:
- *   - only the first MM entry with canonical base C, strand '+' and the
- *     single-letter code 'm' among its codes is read (other entries only
- *     advance the ML cursor); '-' strand entries are ignored;
+ *   - every MM entry with canonical base C and the single-letter code 'm'
+ *     among its codes gives 5mC calls, whatever its strand: htslib matches an
+ *     entry's canonical base against the read's base (complemented for a
+ *     reverse read) and reports the strand only as a field, so a `C-m` entry
+ *     counts the same C's as `C+m` (round 5; rounds 1-4 read the first C+
+ *     entry alone).  At one read position the calls come in MM order
+ *     (bam_mods_at_next_pos walks the entries in parse order) and the
+ *     reference pushes each (blockjoin.c:846-880); get_mod_poss_on_ref then
+ *     keeps the last one's quality (704-706).  Other entries (G-m, C+h, ...)
+ *     only advance the ML cursor.  A position with more than N_MODS = 10
+ *     modification codes (skipped whole at 840-844) is not restated: no
+ *     basecaller writes that many;
  *   - an entry whose deltas run past the last C of the read (G, counted from
  *     the end, for a reverse-strand read), or an ML array shorter than the MM
  *     tag needs, yields no calls (htslib reports a parse error; the reference
@@ -44,17 +53,24 @@ static inline uint8_t nib(const uint8_t *s, uint32_t i) { return (s[i >> 1] >> (
 /* 5mC triggers (read position in stored orientation, ML value) in ascending
  * position order, as the reference's mod_pos loop sees them (832-882).
  * Returns the number of triggers, 0 when there are none or on a parse error. */
+static int cmp_u64k(const void *a, const void *b) {
+    const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+    return x < y ? -1 : x > y;
+}
+
 static size_t mm_triggers(const char *mm, size_t mm_n, const uint8_t *ml, size_t ml_n, const uint8_t *seq,
                           uint32_t len, int rev, lv32 *tpos, lv8 *tq) {
     tpos->n = tq->n = 0;
     size_t ml_cur = 0, i = 0;
+    uint32_t n_ent = 0;                                 /* target entries so far (MM order) */
+    lv32 ent = {0};                                     /* each trigger's entry */
     while (i < mm_n) {
         size_t e = i;
         while (e < mm_n && mm[e] != ';') e++;
         /* header: base, strand, codes, optional '.'/'?' */
-        if (e - i < 3) return 0;
+        if (e - i < 3) goto fail;
         const char base = mm[i], strand = mm[i + 1];
-        if (strand != '+' && strand != '-') return 0;
+        if (strand != '+' && strand != '-') goto fail;
         size_t h = i + 2;
         int ncodes = 0, m_idx = -1;
         if (mm[h] >= '0' && mm[h] <= '9') {            /* ChEBI code */
@@ -67,33 +83,33 @@ static size_t mm_triggers(const char *mm, size_t mm_n, const uint8_t *ml, size_t
                 h++;
             }
         }
-        if (ncodes == 0) return 0;
+        if (ncodes == 0) goto fail;
         if (h < e && (mm[h] == '.' || mm[h] == '?')) h++;
         size_t nd = 0;
         for (size_t k = h; k < e; k++) nd += mm[k] == ',';
-        const int target = base == 'C' && strand == '+' && m_idx >= 0 && tpos->n == 0 && nd > 0;
+        const int target = base == 'C' && m_idx >= 0 && nd > 0 && n_ent < 255;
         if (target) {
-            if (ml_n && ml_cur + nd * (size_t)ncodes > ml_n) return 0;
+            if (ml_n && ml_cur + nd * (size_t)ncodes > ml_n) goto fail;
             /* ranks of the called C's among the read's C's (original orientation) */
             uint64_t rank = 0;
             lv32 ranks = {0};
             size_t k = h;
             for (size_t d = 0; d < nd; d++) {
-                if (k >= e || mm[k] != ',') { free(ranks.a); return 0; }
+                if (k >= e || mm[k] != ',') { free(ranks.a); goto fail; }
                 k++;
                 uint64_t v = 0;
                 size_t k0 = k;
                 while (k < e && mm[k] >= '0' && mm[k] <= '9') v = v * 10 + (uint64_t)(mm[k++] - '0');
-                if (k == k0 || v > 0xFFFFFFFFull) { free(ranks.a); return 0; }
+                if (k == k0 || v > 0xFFFFFFFFull) { free(ranks.a); goto fail; }
                 rank += v + (d ? 1 : 0);
-                if (rank > 0xFFFFFFFFull) { free(ranks.a); return 0; }
+                if (rank > 0xFFFFFFFFull) { free(ranks.a); goto fail; }
                 LPUSH(ranks, (uint32_t)rank);
             }
             /* count the target bases: C forward, G (= complement of C) reverse */
             const uint8_t tb = rev ? NT_G : NT_C;
             uint64_t n_t = 0;
             for (uint32_t p = 0; p < len; p++) n_t += nib(seq, p) == tb;
-            if (nd && ranks.a[nd - 1] >= n_t) { free(ranks.a); return 0; }
+            if (nd && ranks.a[nd - 1] >= n_t) { free(ranks.a); goto fail; }
             /* walk positions in stored order; a reverse read's C ranks count from the end */
             size_t d = rev ? nd : 0;
             uint64_t seen = 0;
@@ -106,20 +122,36 @@ static size_t mm_triggers(const char *mm, size_t mm_n, const uint8_t *ml, size_t
                         d--;
                         LPUSH(*tpos, p);
                         LPUSH(*tq, ml_n ? ml[ml_cur + d * ncodes + m_idx] : 255);
+                        LPUSH(ent, n_ent);
                     }
                 } else if (d < nd && ranks.a[d] == r) {
                     LPUSH(*tpos, p);
                     LPUSH(*tq, ml_n ? ml[ml_cur + d * ncodes + m_idx] : 255);
+                    LPUSH(ent, n_ent);
                     d++;
                 }
             }
             free(ranks.a);
+            n_ent++;
         }
         ml_cur += nd * (size_t)ncodes;
         i = e + 1;
     }
     if (ml_n && ml_cur > ml_n) { tpos->n = tq->n = 0; }
+    if (n_ent > 1 && tpos->n) {                        /* several entries: position order, ties in MM order */
+        uint64_t *k = (uint64_t *)malloc(tpos->n * sizeof(uint64_t));
+        for (size_t j = 0; j < tpos->n; j++)
+            k[j] = ((uint64_t)tpos->a[j] << 40) | ((uint64_t)ent.a[j] << 32) | ((uint64_t)tq->a[j] << 24) | j;
+        qsort(k, tpos->n, sizeof(uint64_t), cmp_u64k);
+        for (size_t j = 0; j < tpos->n; j++) { tpos->a[j] = (uint32_t)(k[j] >> 40); tq->a[j] = (uint8_t)(k[j] >> 24); }
+        free(k);
+    }
+    free(ent.a);
     return tpos->n;
+fail:
+    free(ent.a);
+    tpos->n = tq->n = 0;
+    return 0;
 }
 
 /* get_mod_poss_on_ref (605-792).  calls/quals are appended to out_pos/out_q.

@@ -446,7 +446,7 @@ class DeviceBatch:
         out = np.zeros(8, np.uint64)
         _check(lib().pf_batch_load_counters(self.handle, out.ctypes.data, 8), "pf_batch_load_counters")
         return dict(seq_path=int(out[0]), unsorted=int(out[1]), implicit=int(out[2]), bad_mm=int(out[3]),
-                    dup_chunks=int(out[4]))
+                    dup_chunks=int(out[4]), multi_cm=int(out[5]))
 
     def free(self):
         if self.handle:

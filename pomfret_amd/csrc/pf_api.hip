@@ -30,6 +30,7 @@ __global__ void pf_k3_wave(pf_dev_batch d);
 __global__ void pf_k3_fallback(pf_dev_batch d);
 __global__ void pf_k3_heavy(pf_dev_batch d);
 __global__ void pf_k0_load(pf_load_dev d);
+__global__ void pf_k0_multi(pf_load_dev d);
 __global__ void pf_k0_scan(pf_load_dev d);
 __global__ void pf_k0_pack(pf_load_dev d);
 __global__ void pf_selftest_div(unsigned long long *bad);
@@ -41,7 +42,8 @@ __global__ void pf_selftest_wave(unsigned long long *bad);
 // fallback counters u32 (40, 44) | record level: staging bump pointer u64
 // (48), kept reads u32 (56), calls u64 (64), site slots u64 (72) | the heavy
 // kernel's deferral counter u32 (80) | the main greedy kernel's problem
-// counter u32 (84) | pf_k12_chunks' item count u32 (88) and next item u32 (92) | pad
+// counter u32 (84) | pf_k12_chunks' item count u32 (88) and next item u32 (92) | K0's multi-entry
+// record count u32 (96) | pad
 #define PF_IO_HDR 128ull
 
 // kernel timing slots: "pf_k0_pack" is the scan + pack pair
@@ -877,6 +879,7 @@ extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cf
         ALLOC(p32, 2ull * W); ld.win_kept = p32; ld.win_calls = p32 + W;
         ALLOC(p64, W + 1); ld.win_call_off = p64;
         unsigned long long *pc; ALLOC(pc, PF_K0_NCTR); ld.ctr = pc; b->k0_ctr = pc;
+        uint32_t *ml_; ALLOC(ml_, std::max<uint32_t>(n, 1)); ld.multi_list = ml_;
         if (hipMemset(pc, 0, PF_K0_NCTR * 8) != hipSuccess) return fail(PF_ERR_HIP);
     }
     // ---- capacities: reads <= records; calls <= the records' trigger bounds
@@ -967,6 +970,7 @@ extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cf
     ld.call_pos = const_cast<uint32_t *>(d.call_pos);
     ld.call_cat = const_cast<uint8_t *>(d.call_cat);
     ld.stage_ctr = reinterpret_cast<unsigned long long *>(b->io + PF_IO_STAGE);
+    ld.multi_ctr = reinterpret_cast<uint32_t *>(b->io + 96);
     b->N = 0;                                   // calls: known once a run has finished
     *out = res;
     return PF_OK;
@@ -1108,6 +1112,10 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         HIPCHK(hipMemsetAsync(b->ld.win_kept, 0, 8ull * b->W, st));
         if (b->ld.n_recs) {
             hipLaunchKernelGGL(pf_k0_load, dim3((b->ld.n_recs + PF_K0_WAVES - 1) / PF_K0_WAVES),
+                               dim3(PF_K0_WAVES * 64), 0, st, b->ld);
+            HIPCHK(hipGetLastError());
+            // the records with several C m entries K0 handed over (usually none)
+            hipLaunchKernelGGL(pf_k0_multi, dim3(std::min<uint32_t>((b->ld.n_recs + PF_K0_WAVES - 1) / PF_K0_WAVES, 512)),
                                dim3(PF_K0_WAVES * 64), 0, st, b->ld);
             HIPCHK(hipGetLastError());
         }
@@ -1273,6 +1281,7 @@ static int settle_status(pf_dbatch *b, uint32_t stt, const IoView &v, int attemp
     if (stt == 0) return 0;
     if (stt & PF_ST_FATAL_CIGAR) return PF_ERR_ARG;   // the reference exits (blockjoin.c:776-779)
     if (stt & PF_ST_POS_LIMIT) return PF_ERR_LIMIT;    // pos<<3 packing (3398)
+    if (stt & PF_ST_MM_LIMIT) return PF_ERR_LIMIT;     // > PF_K0_MAXT C m entries in one MM tag
     if (attempt >= 6 || (stt & (PF_ST_INTERNAL | PF_ST_SITE_OVF)) || !(stt & PF_GROWABLE)) {
         fprintf(stderr, "[E::pomfret_amd] device status 0x%x\n", stt);
         return PF_ERR_INTERNAL;

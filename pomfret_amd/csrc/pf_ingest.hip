@@ -1135,7 +1135,7 @@ static void cov_add(std::vector<uint64_t> &bins, const Small &S, uint64_t i) {
 // there).
 static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
                            pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *trunc, uint32_t nb = 0,
-                           const int64_t *bounds = nullptr) {
+                           const int64_t *bounds = nullptr, const int64_t *fetch_ends = nullptr) {
     if (!ctx || !K || !bam || !chrom || !fetch_out) return PF_ERR_ARG;
     *fetch_out = nullptr;
     // sam_itr_querys(idx, hdr, chrom): the whole reference, [0, HTS_POS_MAX),
@@ -1151,6 +1151,10 @@ static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *ba
     const uint64_t NP = nb ? (uint64_t)nb + 1 : pf_bam_contig_pieces(bam, tid, 0, &step);
     auto piece_beg = [&](uint64_t k) -> int64_t { return k == 0 ? 0 : nb ? bounds[k - 1] : (int64_t)k * step; };
     auto piece_end = [&](uint64_t k) -> int64_t { return k + 1 == NP ? INT64_MAX : nb ? bounds[k] : (int64_t)(k + 1) * step; };
+    // a piece's fetch may reach past its bound (fetch_ends[k] >= bounds[k]:
+    // the driver's windows that start in the piece and end past the bound),
+    // so that its arena serves them; its reads stay those starting before the bound
+    auto fetch_end = [&](uint64_t k) -> int64_t { return k + 1 < NP && fetch_ends ? fetch_ends[k] : piece_end(k); };
     const bool with_cov = cov != nullptr;
     std::vector<uint64_t> bins;
     if (with_cov) bins.assign(pf_bam_target_len(bam, tid) / 5000, 0);
@@ -1162,16 +1166,18 @@ static int haptag_bam_impl(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *ba
     uint32_t attempts = 0;
     int rc = PF_OK;
     for (uint64_t k = 0; k < NP && !rc; k++) {
-        const int64_t beg = piece_beg(k), end = piece_end(k);
+        const int64_t beg = piece_beg(k), end = piece_end(k), fend = fetch_end(k);
         pf_bam_dev_fetch_own P;
         std::vector<uint32_t> take;                           // this piece's -u reads: selection positions
         ArenaCache *keep = cache_enabled(ctx) ? new ArenaCache() : nullptr;
-        if (keep) { keep->pbeg = beg; keep->pend = end; }
-        rc = dev_fetch(ctx, bam, tid, 1, &beg, &end, with_cov ? 0u : 1u, 0u, &P, [&](FetchOut &fo) -> int {
+        if (keep) { keep->pbeg = beg; keep->pend = fend; }
+        rc = dev_fetch(ctx, bam, tid, 1, &beg, &fend, with_cov ? 0u : 1u, 0u, &P, [&](FetchOut &fo) -> int {
             const Small &S = *fo.S;
             uint64_t m = 0;                                   // records counted in an earlier piece
             if (k) while (m < fo.n && (int32_t)S.pos[m] < beg) m++;
-            for (uint64_t i = m; i < fo.n; i++) {
+            uint64_t me = fo.n;                               // records of a later piece (an extended fetch)
+            if (fend > end) while (me > m && (int64_t)(int32_t)S.pos[me - 1] >= end) me--;
+            for (uint64_t i = m; i < me; i++) {
                 if (with_cov) {
                     cov_add(bins, S, i);
                     if (S.flag[i] & (4u | 256u | 2048u)) continue;              // primary mapped only (1869-1871)
@@ -1291,12 +1297,14 @@ extern "C" int pf_haptag_bam_cov(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam
 }
 
 extern "C" int pf_haptag_bam_pieces(pf_ctx_t *ctx, const pf_known_vars_t *K, pf_bam_t *bam, const char *chrom,
-                                    uint32_t n_bounds, const int64_t *bounds, pf_bam_dev_fetch_t **fetch_out,
-                                    int32_t *cov, int32_t *truncated) {
+                                    uint32_t n_bounds, const int64_t *bounds, const int64_t *fetch_ends,
+                                    pf_bam_dev_fetch_t **fetch_out, int32_t *cov, int32_t *truncated) {
     if (n_bounds && !bounds) return PF_ERR_ARG;
-    for (uint32_t i = 0; i < n_bounds; i++)
+    for (uint32_t i = 0; i < n_bounds; i++) {
         if (bounds[i] <= (i ? bounds[i - 1] : 0)) return PF_ERR_ARG;     // strictly increasing, > 0
-    return haptag_bam_impl(ctx, K, bam, chrom, fetch_out, cov, truncated, n_bounds, bounds);
+        if (fetch_ends && fetch_ends[i] < bounds[i]) return PF_ERR_ARG;
+    }
+    return haptag_bam_impl(ctx, K, bam, chrom, fetch_out, cov, truncated, n_bounds, bounds, fetch_ends);
 }
 
 // estimate_read_coverage_dirtyfast (blockjoin.c:951-1040) through the device

@@ -39,6 +39,7 @@
 #define PF_ST_STAGE_OVF  128u     /* K0's call staging arena is too small (grow, re-run) */
 #define PF_ST_CALL_OVF   256u     /* the batch call arrays are too small (grow, re-run) */
 #define PF_ST_SITES_OVF  512u     /* the batch site arrays are too small (grow, re-run) */
+#define PF_ST_MM_LIMIT  1024u     /* a record's MM tag has more than PF_K0_MAXT (8) C m entries */
 
 /* counters (ctr[]) */
 #define PF_K0C_SEQPATH  0         /* records walked by the sequential path */
@@ -46,6 +47,7 @@
 #define PF_K0C_IMPLICIT 2         /* records in implicit-canonical mode */
 #define PF_K0C_BADMM    3         /* records whose MM/ML could not be decoded */
 #define PF_K0C_DUPCHUNK 4         /* emission chunks with a duplicate position */
+#define PF_K0C_MULTICM  5         /* records with several C m entries (merged: duplex-style tags) */
 #define PF_K0_NCTR 16             /* [8..15]: per-phase cycles of the diagnostic build */
 
 /* I/O block header fields of the record-level path (byte offsets; the
@@ -107,6 +109,8 @@ struct pf_load_dev {
     uint32_t *win_kept, *win_calls;  /* [W] per-window totals (atomics, zeroed per run) */
     uint32_t *status;
     unsigned long long *ctr;         /* PF_K0_NCTR */
+    uint32_t *multi_list;            /* [n_recs] wave slots of records with several C m entries (pf_k0_multi) */
+    uint32_t *multi_ctr;             /* their count (I/O block header, zeroed per run) */
     /* scan + pack output: the batch's window / read / call arrays */
     uint8_t *io;                     /* I/O block (header totals, bump pointer) */
     uint64_t call_cap, sites_cap;

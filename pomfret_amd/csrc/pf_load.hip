@@ -177,6 +177,31 @@ struct K0Out {
 // bytes after it (the lane's word and the next) by a SWAR decimal parse, and
 // a count that may run past that window takes a byte loop.
 struct K0Tgt { uint32_t nd, nc, mi, th, te; uint64_t ml; };
+// The MM entries that give 5mC calls: every entry with canonical base C and
+// the code m among its codes, whatever its strand (htslib matches the
+// canonical base against the read's base and reports the strand as a field:
+// a C-m entry counts the same C's as C+m).  The first is kept in registers;
+// the others (rare: a duplex-style or repeated C m entry) go to the wave's
+// LDS, PF_K0_TW words each (no private array: dynamic indexing would put it
+// in scratch on every record).  Up to PF_K0_MAXT; more sets PF_ST_MM_LIMIT.
+#define PF_K0_MAXT 8
+#define PF_K0_TW 7
+struct K0Tgts { K0Tgt t0; uint32_t n, over; uint32_t *xt; };
+DEV void k0_tgt_put(uint32_t *xt, uint32_t e, const K0Tgt &t, uint32_t lane) {   // e >= 1, uniform
+    if (lane == 0) {
+        uint32_t *q = xt + PF_K0_TW * (e - 1);
+        q[0] = t.nd; q[1] = t.nc; q[2] = t.mi; q[3] = t.th; q[4] = t.te; q[5] = (uint32_t)t.ml;
+        q[6] = (uint32_t)(t.ml >> 32);
+    }
+}
+DEV K0Tgt k0_tgt_get(const K0Tgts &T, uint32_t e) {  // e uniform
+    if (e == 0) return T.t0;
+    const uint32_t *q = T.xt + PF_K0_TW * (e - 1);
+    K0Tgt t;
+    t.nd = q[0]; t.nc = q[1]; t.mi = q[2]; t.th = q[3]; t.te = q[4];
+    t.ml = ((uint64_t)q[6] << 32) | q[5];
+    return t;
+}
 
 DEV uint32_t bytes_eq(uint32_t w, uint32_t c) {      // 0x80 in each byte of w equal to c
     const uint32_t t = w ^ (c * 0x01010101u);
@@ -213,8 +238,10 @@ DEV uint32_t swar_dec(uint64_t y, uint32_t n) {      // bytes 0..n-1 of y (n in 
 struct K0Hdr { uint32_t base, strand, nc, h; int mi; };
 
 DEV bool k0_mm_entries(const uint32_t *gw, const uint8_t *mm, uint32_t mis, uint32_t mlen, uint32_t mln,
-                       uint32_t lane, K0Tgt &t) {
-    t.nd = 0;
+                       uint32_t lane, K0Tgts &T) {
+    T.n = 0;
+    T.over = 0;
+    T.t0.nd = 0;
     if (mlen == 0) return true;
     const uint32_t wend = mis + mlen;
     const uint32_t kmaxw = (wend - 1) / 4 + 1;       // the padded text holds this word
@@ -250,17 +277,20 @@ DEV bool k0_mm_entries(const uint32_t *gw, const uint8_t *mm, uint32_t mis, uint
         H.h = h; H.nc = nc; H.mi = mi;
     };
     uint64_t ml_cur = 0;
-    bool found = false;
     // entry [i, e) with `commas` commas
     auto close = [&](uint32_t i, uint32_t e, uint32_t commas) -> bool {
         if (e - i < 3) return false;
         if (H.strand != '+' && H.strand != '-') return false;
         if (H.nc == 0) return false;
         if (H.base == ',') commas--;                  // count the skip list's commas only
-        if (!found && H.base == 'C' && H.strand == '+' && H.mi >= 0 && commas > 0) {
-            found = true;
+        if (H.base == 'C' && H.mi >= 0 && commas > 0) {
             if (mln && ml_cur + (uint64_t)commas * H.nc > mln) return false;
+            if (T.n == PF_K0_MAXT) { T.over = 1; return true; }
+            K0Tgt t;
             t.nd = commas; t.nc = H.nc; t.mi = (uint32_t)H.mi; t.th = H.h; t.te = e; t.ml = ml_cur;
+            if (T.n == 0) T.t0 = t;
+            else k0_tgt_put(T.xt, T.n, t, lane);
+            T.n++;
         }
         ml_cur += (uint64_t)commas * H.nc;
         return true;
@@ -1076,9 +1106,107 @@ DEV K0Rec k0_rec(const pf_load_dev &d, uint32_t slot, uint32_t lane) {
     return R;
 }
 
+// Several C m entries (a duplex-style tag, or C+m twice): every entry's rank
+// list (the same C's counted: the ranks compare), each call's ML value in its
+// top byte, merged in rank order -- at one C the entries' calls in MM order,
+// as bam_mods_at_next_pos reports them and fill_read_meth_record_from_bam_line
+// pushes them (846-880) -- and cut to one call per C, the last entry's: the
+// one get_mod_poss_on_ref keeps (704-706 overwrite the quality of an equal
+// position; nothing else between the duplicates depends on them).  The lists
+// and the merge live in a tail slice of the staging arena (2 x the calls);
+// TB receives the merged list in the single-entry layout.  Rare (no config
+// has such tags): one wave, binary searches per call.
 template <typename TP>
-DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, TP TB, uint32_t cap, const K0Tgt &t,
+DEV bool k0_merge_targets(const pf_load_dev &d, K0W &L, const K0Tgts &T, uint32_t N, bool rev, TP TB,
+                          const uint32_t *gw, const uint8_t *mmg, uint32_t mis, const uint8_t *ml, uint32_t mln,
+                          uint32_t lane, uint32_t &nd_out, bool &past, bool &ovf) {
+    nd_out = 0;
+    ovf = false;
+    unsigned long long t0 = 0;
+    if (lane == 0) t0 = atomicAdd(d.stage_ctr, 2ull * N);
+    const uint64_t cb = d.stage_off[d.n_recs] + (((uint64_t)uni((uint32_t)(t0 >> 32)) << 32) | uni((uint32_t)t0));
+    if (cb + 2ull * N > d.stage_cap) {
+        if (lane == 0) atomicOr(d.status, PF_ST_STAGE_OVF);
+        ovf = true;
+        return false;
+    }
+    uint32_t *tmp = d.stage_pos + cb, *mrg = tmp + N;
+    k0_dw_table(L.u.mg.mV, lane);
+    wsync();
+    bool pst = false;
+    for (uint32_t e = 0, oe = 0; e < T.n; e++) {
+        const K0Tgt te = k0_tgt_get(T, e);
+        uint32_t *TBe = tmp + oe;
+        if (!k0_mm_ranks(gw, mmg, mis, te, rev, TBe, L.u.mg.mV, lane)) return false;
+        wsync();
+        for (uint32_t j = lane; j < te.nd; j += 64) {
+            const uint32_t q = mln ? (uint32_t)ml[te.ml + (uint64_t)j * te.nc + te.mi] : 255u;
+            const uint32_t sj = rev ? te.nd - 1 - j : j;
+            const uint32_t rk = TBe[sj];
+            pst |= rk >= (1u << 24);
+            TBe[sj] = (rk & 0xFFFFFFu) | (q << 24);
+        }
+        wsync();
+        oe += te.nd;
+    }
+    past = __ballot(pst) != 0;
+    if (past) return true;
+    // merged index: j plus, in every other list, the calls of a smaller rank
+    // (and of an equal rank in the earlier entries)
+    for (uint32_t e = 0, oe = 0; e < T.n; e++) {
+        const uint32_t ne = k0_tgt_get(T, e).nd;
+        for (uint32_t j = lane; j < ne; j += 64) {
+            const uint32_t v = tmp[oe + (rev ? ne - 1 - j : j)], rk = v & 0xFFFFFFu;
+            uint32_t pos = j;
+            for (uint32_t f = 0, of = 0; f < T.n; f++) {
+                const uint32_t nf = k0_tgt_get(T, f).nd;
+                if (f != e) {
+                    uint32_t lo = 0, hi = nf;              // first index whose rank is > (f < e) or >= rk
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        const uint32_t x = tmp[of + (rev ? nf - 1 - mid : mid)] & 0xFFFFFFu;
+                        if (f < e ? x <= rk : x < rk) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    pos += lo;
+                }
+                of += nf;
+            }
+            mrg[pos] = v;
+        }
+        oe += ne;
+    }
+    wsync();
+    // one call per C: the last of equal ranks
+    uint32_t kept = 0;
+    for (uint32_t k0 = 0; k0 < N; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const bool keep = k < N && (k + 1 == N || (mrg[k] & 0xFFFFFFu) != (mrg[k + 1] & 0xFFFFFFu));
+        kept += popc(__ballot(keep));
+    }
+    for (uint32_t k0 = 0, base = 0; k0 < N; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        const uint32_t v = k < N ? mrg[k] : 0u;
+        const bool keep = k < N && (k + 1 == N || (v & 0xFFFFFFu) != (mrg[k + 1] & 0xFFFFFFu));
+        const uint64_t b = __ballot(keep);
+        if (keep) {
+            const uint32_t j = base + popc(b & lanemask_lt(lane));
+            TB[rev ? kept - 1 - j : j] = v;
+        }
+        base += popc(b);
+    }
+    wsync();
+    nd_out = kept;
+    return true;
+}
+
+template <bool MULTI, typename TP>
+DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, TP TB, uint32_t cap, const K0Tgts &T,
                    bool okm) {
+    K0Tgt t = T.t0;
+    const bool multi = MULTI && T.n > 1;
+    uint32_t ndsum = t.nd;
+    for (uint32_t e = 1; e < T.n; e++) ndsum += k0_tgt_get(T, e).nd;
     const uint32_t r = R.r;
     const uint32_t len = R.len;
     const bool rev = (R.flag & 16u) != 0;
@@ -1096,8 +1224,8 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     {
         const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
         const uint32_t *gw = reinterpret_cast<const uint32_t *>(mmg - mis);
-        if (okmm && t.nd > cap) okmm = false;       // only a malformed tag lists more calls than its size allows
-        if (okmm && t.nd) {
+        if (okmm && ndsum > cap) okmm = false;      // only a malformed tag lists more calls than its size allows
+        if (okmm && t.nd && !multi) {
             // the first 512 ML values (8 per lane, packed) are loaded before
             // the rank pass and arrive while it runs
             if (mln) {
@@ -1117,7 +1245,19 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     }
     wsync();
     bool past = false;
-    if (okmm && t.nd) {                               // the C+m entry's ML values ride in the ranks' top byte
+    if constexpr (MULTI) {
+        if (okmm && multi) {
+            if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_MULTICM], 1ull);
+            bool ovf = false;
+            uint32_t ndm = 0;
+            const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
+            okmm = k0_merge_targets(d, L, T, ndsum, rev, TB, reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis,
+                                    ml, mln, lane, ndm, past, ovf);
+            if (ovf) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
+            t.nd = ndm;
+        }
+    }
+    if (!multi && okmm && t.nd) {                        // the C+m entry's ML values ride in the ranks' top byte
         uint32_t u = 0;
         for (uint32_t j = lane; j < t.nd; j += 64, u++) {
             const uint32_t q = !mln ? 255u : u < 8 ? ((u < 4 ? mlq0 : mlq1) >> (8 * (u & 3))) & 0xFFu
@@ -1227,15 +1367,13 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     K0_STAMP(3);
 }
 
-__global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_load(pf_load_dev d) {
-    __shared__ K0W lds[PF_K0_WAVES];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wv = uni(threadIdx.x >> 6);
-    const uint32_t slot = blockIdx.x * PF_K0_WAVES + wv;
-    if (slot >= d.n_recs) return;
+// One record on the wave: filters, the MM entries, the rest.  The main pass
+// hands a record with several C m entries to pf_k0_multi (rare; its merge
+// would cost the common path registers) and leaves its rec_n to it.
+template <bool MULTI>
+DEV void k0_one(const pf_load_dev &d, K0W &L, uint32_t slot, uint32_t lane) {
     const K0Rec R = k0_rec(d, slot, lane);
     const uint32_t r = R.r;
-    K0W &L = lds[wv];
     // filters (1079-1085)
     const uint32_t flag = R.flag;
     const bool drop = (flag & 4u) || (flag & 256u) || (flag & 2048u) || R.mapq < d.min_mapq ||
@@ -1248,7 +1386,7 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_e
     // filters / the MM phase / the SEQ pass, so that phase costs are kernel-time
     // differences (the s_memtime build's counter atomics distort them)
     if (d.diag == 4u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
-    // The tag's entries first: the C+m entry's skip count decides where the
+    // The tag's entries first: the C m entries' skip counts decide where the
     // trigger list lives -- the wave's LDS list when it fits (640), else the
     // record's HBM slice, which the upload sizes from the ML length (an upper
     // bound: dorado's h + m entries make it twice the m list, so round 2 sent
@@ -1256,11 +1394,42 @@ __global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_e
     // their trigger lists an L2 round trip).
     const uint8_t *mmg = d.mm + R.mm_off;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
-    K0Tgt t;
-    const bool okm = k0_mm_entries(reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis, R.mlen, R.mln, lane, t);
-    if (R.scr_len == 0 || !okm || uni(t.nd) <= (uint32_t)PF_K0_TCAP)
-        k0_record(d, L, R, lane, L.T, (uint32_t)PF_K0_TCAP, t, okm);
-    else k0_record(d, L, R, lane, d.scr + R.scr_off, R.scr_len, t, okm);
+    K0Tgts T;
+    T.xt = L.opE;                                     // free until the CIGAR walk (PF_K0_TW x 7 <= 64 words)
+    const bool okm = k0_mm_entries(reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis, R.mlen, R.mln, lane, T);
+    if (T.over) {                                     // more C m entries than this build merges
+        if (lane == 0) { atomicOr(d.status, PF_ST_MM_LIMIT); d.rec_n[r] = PF_NONE; }
+        return;
+    }
+    if (!MULTI && okm && T.n > 1) {
+        if (lane == 0) d.multi_list[atomicAdd(d.multi_ctr, 1u)] = slot;
+        return;
+    }
+    uint32_t ndsum = T.t0.nd;
+    for (uint32_t e = 1; e < T.n; e++) ndsum += k0_tgt_get(T, e).nd;
+    if (R.scr_len == 0 || !okm || uni(ndsum) <= (uint32_t)PF_K0_TCAP)
+        k0_record<MULTI>(d, L, R, lane, L.T, (uint32_t)PF_K0_TCAP, T, okm);
+    else k0_record<MULTI>(d, L, R, lane, d.scr + R.scr_off, R.scr_len, T, okm);
+}
+
+__global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_load(pf_load_dev d) {
+    __shared__ K0W lds[PF_K0_WAVES];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t slot = blockIdx.x * PF_K0_WAVES + wv;
+    if (slot >= d.n_recs) return;
+    k0_one<false>(d, lds[wv], slot, lane);
+}
+
+// The records pf_k0_load handed over (several C m entries): one wave each,
+// grid-stride over its list.
+__global__ __launch_bounds__(PF_K0_WAVES * 64) void pf_k0_multi(pf_load_dev d) {
+    __shared__ K0W lds[PF_K0_WAVES];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = uni(threadIdx.x >> 6);
+    const uint32_t n = *d.multi_ctr;
+    for (uint32_t i = blockIdx.x * PF_K0_WAVES + wv; i < n; i += gridDim.x * PF_K0_WAVES)
+        k0_one<true>(d, lds[wv], d.multi_list[i], lane);
 }
 
 // ---------------------------------------------------------------------------

@@ -232,7 +232,7 @@ struct pf_mp_plan {
      * windows' fetch regions, so every window job -- cut at the bounds --
      * is served by one kept piece arena */
     uint64_t *bnd_off;
-    int64_t *bnd;
+    int64_t *bnd, *bext;       /* bound k and how far piece k's fetch reaches past it */
     char *interval_path;
     int32_t *tid;              /* [n_contigs] BAM tid or -1 */
     pf_cfg_t *cfg;             /* [n_contigs] */
@@ -321,7 +321,7 @@ void pf_mp_free(pf_mp_plan_t *p) {
     if (p->blocks) pf_blocks_free(p->blocks);
     if (p->gaps) pf_gaps_free(p->gaps);
     if (p->ugaps_own) pf_gaps_free(p->ugaps_own);
-    free(p->utid); free(p->bnd_off); free(p->bnd);
+    free(p->utid); free(p->bnd_off); free(p->bnd); free(p->bext);
     free(p->bam_path); free(p->vcf_path); free(p->out_prefix); free(p->interval_path);
     free(p->ucov); free(p->utrunc); free(p->uhave);
     pthread_mutex_destroy(&p->st_mu);
@@ -565,10 +565,25 @@ static int mp_plan(const pf_methphase_opts_t *o, pf_mp_plan_t **out, int defer_e
                 if (nb == bcap) {
                     bcap = bcap ? 2 * bcap : 64;
                     int64_t *nbp = (int64_t *)realloc(p->bnd, bcap * sizeof(int64_t));
-                    if (!nbp) { rc = PF_ERR_NOMEM; break; }
-                    p->bnd = nbp;
+                    if (nbp) p->bnd = nbp;
+                    int64_t *nbe = nbp ? (int64_t *)realloc(p->bext, bcap * sizeof(int64_t)) : NULL;
+                    if (!nbp || !nbe) { rc = PF_ERR_NOMEM; break; }
+                    p->bext = nbe;
                 }
-                p->bnd[nb++] = x;
+                /* piece k-1 serves the windows whose fetch region starts
+                 * before x (the job cut below): its fetch reaches the
+                 * furthest of their ends, not the end of their cluster --
+                 * dense windows merge into one cluster per contig */
+                int64_t ext = x;
+                for (uint64_t w = w0; w < w1; w++) {
+                    const int64_t a = p->win_start[w] > PF_READBACK ? (int64_t)p->win_start[w] - PF_READBACK : 0;
+                    if (a >= x) break;
+                    const int64_t b = (int64_t)p->win_end[w] + PF_READBACK;
+                    if (b > ext) ext = b;
+                }
+                p->bnd[nb] = x;
+                p->bext[nb] = ext;
+                nb++;
                 prev = x;
             }
             free(ca);
@@ -835,11 +850,12 @@ int pf_mp_run_haptag_job(pf_mp_plan_t *p, pf_ctx_t *ctx, uint32_t j) {
          * the default equal-length pieces when it has none */
         const uint64_t b0 = J->bc >= 0 ? p->bnd_off[J->bc] : 0, b1 = J->bc >= 0 ? p->bnd_off[J->bc + 1] : 0;
         if (p->est_deferred) {                  /* the contig's coverage estimate from the same fetch */
-            rc = pf_haptag_bam_pieces(ctx, &kt->vars, bam, contig, (uint32_t)(b1 - b0), p->bnd + b0, &F,
-                                      &p->ucov[J->contig], &p->utrunc[J->contig]);
+            rc = pf_haptag_bam_pieces(ctx, &kt->vars, bam, contig, (uint32_t)(b1 - b0), b1 > b0 ? p->bnd + b0 : NULL,
+                                      b1 > b0 ? p->bext + b0 : NULL, &F, &p->ucov[J->contig], &p->utrunc[J->contig]);
             if (!rc) p->uhave[J->contig] = 1;
         } else {
-            rc = pf_haptag_bam_pieces(ctx, &kt->vars, bam, contig, (uint32_t)(b1 - b0), p->bnd + b0, &F, NULL, NULL);
+            rc = pf_haptag_bam_pieces(ctx, &kt->vars, bam, contig, (uint32_t)(b1 - b0), b1 > b0 ? p->bnd + b0 : NULL,
+                                      b1 > b0 ? p->bext + b0 : NULL, &F, NULL, NULL);
         }
         if (!rc) st_fetch(p, 1, F, (now_s() - t0) * 1e3 - F->ms_total);
         if (!rc && F->n_recs) {

@@ -85,6 +85,25 @@ HANDMADE = [
     # combined codes: ML interleaved per position (h, m)
     ("combined_hm", dict(seq="ACGTTCGA", cigar="8M", mm="C+hm?,0,0;", ml=[1, 2, 3, 4], pos=100),
      [(101, 1), (105, 1)]),
+    # several C m entries (duplex-style tags; round 5): htslib matches each
+    # entry's canonical base against the read's base, whatever the strand, so
+    # C-m counts the same C's as C+m; at one C the calls come in MM order and
+    # get_mod_poss_on_ref keeps the last one's quality (846-880, 704-706)
+    ("duplex_c_minus", dict(seq="ACGTTCGA", cigar="8M", mm="C+m?,0;C-m?,0,0;", ml=[200, 10, 30], pos=100),
+     [(101, 1), (105, 1)]),
+    # G-m (the usual duplex encoding: the opposite strand's C) is not a C
+    # entry: only its ML values are skipped
+    ("duplex_g_minus", dict(seq="ACGTTCGA", cigar="8M", mm="C+m?,0,0;G-m?,0,1;", ml=[200, 10, 5, 6], pos=100),
+     [(101, 0), (105, 1)]),
+    # a second C+m entry: its calls merge into the first's by position
+    ("repeated_c_plus", dict(seq="ACGTTCGA", cigar="8M", mm="C+m?,1;C+m?,0;", ml=[180, 20], pos=100),
+     [(101, 1), (105, 0)]),
+    # reverse read: both entries count the stored G's from the end
+    ("duplex_rev", dict(seq="ACGTTCGA", cigar="8M", mm="C+m?,0;C-m?,1;", ml=[50, 220], pos=200, flag=16),
+     [(201, 0), (205, 1)]),
+    ("duplex_same_c_rev", dict(seq="ACGTTCGA", cigar="8M", mm="C+m?,0,0;C-m?,0;", ml=[50, 220, 130], pos=200,
+                               flag=16),
+     [(201, 0), (205, 2)]),
     # no ML tag: quality 255 (HTS_MOD_UNKNOWN as uint8_t) -> methylated
     ("no_ml", dict(seq="ACGTTCGA", cigar="8M", mm="C+m.,0,0;", pos=100), [(101, 0), (105, 0)]),
     # a call on the last base of an M op followed by a deletion keeps the

@@ -11,6 +11,8 @@ import os
 import numpy as np
 import pytest
 
+from pomfret_amd.abi import LoadConfig
+
 from tests._aln_cases import HANDMADE, LOAD_CFG_SMALL, aln_cases, handmade_batch, mm_fuzz_batch, records_batch
 
 pytestmark = pytest.mark.gpu
@@ -55,6 +57,56 @@ def test_handmade_records(oracle_lib, gpu_ctx):
     assert db.n_reads == len(kept)
     c = db.load_counters()
     assert c["seq_path"] >= 2 and c["implicit"] >= 2 and c["bad_mm"] >= 2
+    # the duplex-style records (several C m entries) went through pf_k0_multi
+    n_multi = sum(1 for h in HANDMADE if h[1].get("mm", "").count("C+m") + h[1].get("mm", "").count("C-m") > 1)
+    assert n_multi == 4 and c["multi_cm"] >= n_multi
+    db.free()
+
+
+def test_multi_entry_records_at_scale(oracle_lib, gpu_ctx):
+    """Every record of a synthetic batch re-tagged with a second C m entry
+    (a C-m copy of half its calls with other ML values, placed before or after
+    the C+m entry): K0 hands them to pf_k0_multi, which merges the entries'
+    calls; the calls equal the oracle's (htslib semantics, parity unpinned:
+    no reference fixture holds such a tag)."""
+    from pomfret_amd import Config
+    from tests._aln_cases import synth_aln
+    aln = synth_aln(3, 30, 91)
+    rng = np.random.default_rng(5)
+    mm_new, ml_new = [], []
+    for r in range(aln.n_recs):
+        mm = bytes(aln.mm[aln.mm_off[r]:aln.mm_off[r + 1]]).decode()
+        ml = aln.ml[aln.ml_off[r]:aln.ml_off[r + 1]].tolist()
+        ents = [e for e in mm.split(";") if e]
+        # the entry holding 5mC and its ML slice
+        pos, o = None, 0
+        for e in ents:
+            hdr, *sk = e.split(",")
+            nc = len(hdr.rstrip("?.")) - 2
+            if hdr.startswith("C+") and "m" in hdr[2:]:
+                pos = (e, o, nc, sk)
+            o += len(sk) * nc
+        if pos is None or len(pos[3]) < 2:
+            mm_new.append(mm); ml_new.append(ml)
+            continue
+        e, o, nc, sk = pos
+        # the C-m copy: every other call of the C+m entry (re-based skip counts)
+        ranks = np.cumsum(np.array(sk, np.int64) + 1) - 1
+        sub = ranks[::2]
+        skips = np.diff(np.concatenate([[-1], sub])) - 1
+        extra = "C-m?," + ",".join(str(x) for x in skips.tolist()) + ";"
+        qx = rng.integers(0, 256, len(sub)).tolist()
+        if r % 2:
+            mm_new.append(mm + extra); ml_new.append(ml + qx)
+        else:
+            mm_new.append(extra + mm); ml_new.append(qx + ml)
+    enc = [np.frombuffer(m.encode(), np.uint8) for m in mm_new]
+    aln.mm = np.concatenate(enc)
+    aln.mm_off = np.concatenate([[0], np.cumsum([len(x) for x in enc])]).astype(np.uint64)
+    aln.ml = np.concatenate([np.asarray(x, np.uint8) for x in ml_new])
+    aln.ml_off = np.concatenate([[0], np.cumsum([len(x) for x in ml_new])]).astype(np.uint64)
+    db, _ = _check_calls(oracle_lib, gpu_ctx, Config(), LoadConfig(), aln, "multi-entry")
+    assert db.load_counters()["multi_cm"] >= aln.n_recs // 2
     db.free()
 
 

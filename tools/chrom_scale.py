@@ -78,6 +78,7 @@ def run_genome(tag, contigs, workdir, threads, cpu_threads, ctx, cpu):
                          "windows": int(r["decision"].shape[0]), "joined": int((r["decision"] >= 0).sum()),
                          "arena_hits": st["arena_hits"], "arena_misses": st["arena_misses"],
                          "reread_bytes": st["reread_bytes"], "window_fetches": st["windows"]["n_fetch"],
+                         "haptag_comp_over_bam": round(st["haptag"]["comp_bytes"] / res["bam_bytes"], 3),
                          "phases": st}
         log(f"[cs] {tag}: driver {dd:.2f}s, hits {st['arena_hits']} misses {st['arena_misses']}")
         if cpu:
