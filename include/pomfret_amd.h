@@ -279,6 +279,10 @@ int  pf_batch_stats(pf_dbatch_t *db, uint64_t *out, uint64_t n);
  * 5 the one-wave kernel (pf_k3_wave), 0 no greedy run (no sites).  n >= 2*n_windows.  Tests assert which
  * variant PF_K3_CACHE forced. */
 int  pf_batch_k3_paths(pf_dbatch_t *db, uint8_t *out, uint64_t n);
+/* The greedy launch this batch was given: out[0] the main kernel's dynamic
+ * LDS per problem, out[1] its persistent workgroups (problems at once on the
+ * device), out[2] pf_k3_heavy's dynamic LDS, out[3] its problems.  n >= 4. */
+int  pf_batch_k3_budget(const pf_dbatch_t *db, uint32_t *out, uint64_t n);
 
 /* The greedy problems (w<<1 | dir) this batch runs in pf_k3_heavy, the second
  * greedy kernel on the context's second stream: windows with at least 2,000

@@ -57,6 +57,7 @@ def lib():
         L.pf_batch_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.pf_batch_heavy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
         L.pf_batch_k3_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.pf_batch_k3_budget.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.pf_batch_debug_sites.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_uint32]
         L.pf_batch_debug_methmers.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
@@ -482,6 +483,14 @@ class DeviceBatch:
         out = np.zeros(max(2 * self.n_windows, 2), np.uint8)
         _check(lib().pf_batch_k3_paths(self.handle, out.ctypes.data, out.size), "pf_batch_k3_paths")
         return out[:2 * self.n_windows].reshape(-1, 2)
+
+    def k3_budget(self) -> dict:
+        """The greedy launch of this batch (pf_batch_k3_budget): the main
+        kernel's dynamic LDS per problem and its resident workgroups, the
+        heavy kernel's LDS and problem count."""
+        out = np.zeros(4, np.uint32)
+        _check(lib().pf_batch_k3_budget(self.handle, out.ctypes.data, out.size), "pf_batch_k3_budget")
+        return {"lds": int(out[0]), "resident": int(out[1]), "lds_heavy": int(out[2]), "n_heavy": int(out[3])}
 
     def heavy_problems(self) -> np.ndarray:
         """Greedy problems (w<<1 | dir) run in pf_k3_heavy: the windows with at

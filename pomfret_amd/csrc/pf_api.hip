@@ -508,6 +508,31 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
 // and b->R / b->N are capacities; the read, call and site arrays are only
 // allocated -- K0, scan and pack fill them on every run -- and the site
 // slots are sized from win_calls, an upper bound of each window's calls.
+// The main greedy kernel's largest dynamic LDS that still holds four
+// problems per CU (its 128 VGPRs allow four waves per SIMD): a quarter of the
+// CU's LDS less the kernel's static LDS.  A workgroup's LDS is granted in
+// 1 KB units and a quarter of 160 KB is whole units, so the sum may reach it
+// exactly (tools/ubench/lds_occ.hip, profiles/r05/lds_occ.txt); the
+// occupancy query does not model the units and over-reports past it.
+static uint32_t k3_lds_four(int device) {
+    static std::mutex mu;
+    static std::vector<std::pair<int, uint32_t>> memo;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &e : memo) if (e.first == device) return e.second;
+    hipFuncAttributes fa;
+    int per_cu = 0;
+    const uint32_t st = hipFuncGetAttributes(&fa, (const void *)pf_k3_greedy) == hipSuccess ? (uint32_t)fa.sharedSizeBytes
+                                                                                              : 4096u;
+    if (hipDeviceGetAttribute(&per_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, device) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 163840;
+    (void)hipGetLastError();
+    const uint32_t quarter = ((uint32_t)per_cu / 4u) & ~1023u;
+    const uint32_t best = quarter > st + 32768u ? (quarter - st) & ~15u : 36864u;
+    memo.push_back({device, best});
+    return best;
+}
+
 static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t *first, const uint32_t *last,
                        const uint32_t *cpos, const uint8_t *ccat, const uint64_t *win_calls, pf_dbatch_t **out) {
     const pf_cfg_t *cfg = &b->cfg;
@@ -648,6 +673,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     ALLOC(d.len0, site_total);
     ALLOC(d.len1, site_total);
     ALLOC(d.rev_ord, R);
+    ALLOC(d.k3_side, 14ull * R + 16);
     ALLOC(d.mmr_n, 2ull * R);
     ALLOC(d.mmr_start, 2ull * R);
     ALLOC(d.mmr_off, 2ull * R);
@@ -677,12 +703,21 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     // profiles/r04/lds_occ.txt).  Profiled needs by window reads
     // (tools/k3_heavy_prof.py): on the 60x gap mix every window below 1,284
     // reads fits 44 KB, the largest 49 KB.
+    // Round 5: the side arrays of the candidate-cache layout live in HBM
+    // (k3_side_mem) and the main kernel fits 128 VGPRs, so at the four-per-CU
+    // budget (k3_lds_four, ~37 KB) every problem of the 60x gap mix fits
+    // (largest 36.0 KB, at 1,431 reads; tools/k3_heavy_prof.py): four
+    // problems per CU when no window passes PF_K3_FOUR_RMAX reads (1,500), or
+    // when 90 % of the windows are small (the heavy kernel takes the rest).
     uint32_t lds_auto = 49152u;
     if (W) {
         std::vector<uint32_t> rw(W);
         for (uint32_t w = 0; w < W; w++) rw[w] = in->win_read_off[w + 1] - in->win_read_off[w];
+        const uint32_t rmax = *std::max_element(rw.begin(), rw.end());
         std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
-        if (rw[(W * 9) / 10] <= 400) lds_auto = 36864u;
+        const char *fr = getenv("PF_K3_FOUR_RMAX");
+        const uint32_t four_rmax = fr ? (uint32_t)atoi(fr) : 1500u;
+        if (rw[(W * 9) / 10] <= 400 || rmax <= four_rmax) lds_auto = k3_lds_four(b->ctx->device);
     }
     const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB"), *ldw = getenv("PF_K3W_LDS");
     // one-wave greedy kernel: ~25 KB leaves six problems per CU (a 60x
@@ -1074,6 +1109,22 @@ static uint32_t k3_resident(const pf_ctx *c, uint32_t lds) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)pf_k3_greedy, PF_K3S_THREADS, lds) != hipSuccess ||
         per <= 0)
         per = 1;
+    // the residency model beside the query (LDS granted in 1 KB units, one
+    // wave per SIMD per workgroup, 512 VGPRs per SIMD lane): the larger wins
+    // -- a workgroup beyond what the device holds starts when one leaves and
+    // finds the problem counter spent, so over-counting costs nothing
+    {
+        hipFuncAttributes fa;
+        int lds_cu = 0;
+        if (hipFuncGetAttributes(&fa, (const void *)pf_k3_greedy) == hipSuccess &&
+            hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, c->device) == hipSuccess &&
+            lds_cu > 0 && fa.numRegs > 0) {
+            const uint32_t wg_lds = ((uint32_t)fa.sharedSizeBytes + lds + 1023u) & ~1023u;
+            const uint32_t by_lds = wg_lds ? (uint32_t)lds_cu / wg_lds : 8u;
+            const uint32_t by_vgpr = std::min<uint32_t>(8u, 512u / (((uint32_t)fa.numRegs + 7u) & ~7u));
+            per = std::max<int>(per, (int)std::min(by_lds, by_vgpr));
+        }
+    }
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || ncu <= 0) ncu = 1;
     (void)hipGetLastError();
     uint32_t n = (uint32_t)per * (uint32_t)ncu;
@@ -1450,6 +1501,16 @@ extern "C" int pf_batch_k3_paths(pf_dbatch_t *b, uint8_t *out, uint64_t n) {
     std::vector<uint64_t> st(16ull * b->W + 1);
     if (b->W) HIPCHK(hipMemcpy(st.data(), b->d.stats, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
     for (uint64_t i = 0; i < 2ull * b->W; i++) out[i] = (uint8_t)(st[i * 8 + 2] >> 56);
+    return PF_OK;
+}
+
+extern "C" int pf_batch_k3_budget(const pf_dbatch_t *b, uint32_t *out, uint64_t n) {
+    if (!b || !out || n < 4) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    out[0] = b->d.lds_bytes;
+    out[1] = k3_resident(b->ctx, b->d.lds_bytes);
+    out[2] = b->d.lds_heavy;
+    out[3] = b->n_heavy;
     return PF_OK;
 }
 

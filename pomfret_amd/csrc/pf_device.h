@@ -78,6 +78,9 @@ struct pf_dev_batch {
     uint32_t *keys; uint64_t keys_cap; unsigned long long *keys_ctr;
     uint8_t *big; uint64_t big_cap; unsigned long long *big_ctr;
     uint8_t *scr; uint64_t scr_cap; unsigned long long *scr_ctr;
+    /* the slim greedy loop's per-read side arrays in HBM, when its slot lists
+     * miss LDS (k3_side_mem): hp, flg [2R] bytes, ord [R] u16, aux [2R] u32 */
+    uint8_t *k3_side;
     /* outputs */
     int32_t *table;                    /* [W*2*4] */
     uint8_t *hp_fwd;                   /* [R] */

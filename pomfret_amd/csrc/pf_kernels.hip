@@ -135,6 +135,11 @@ DEV uint32_t wave_max_dpp(uint32_t x) {
     const uint32_t ab = a > b ? a : b, ce = c > e ? c : e;
     return ab > ce ? ab : ce;
 }
+// lane i <- lane i + 1 (DPP wave_shl:1; lane 63 gets 0): no LDS round trip,
+// unlike a ds_bpermute shuffle
+DEV uint32_t wave_shl1(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xF, 0xF, false);
+}
 // (float)cnt/sum of query_counts_of_mmrs (blockjoin.c:3508-3509) for 16-bit
 // counts (0 <= a <= 65535, 1 <= b <= 65535), correctly
 // rounded: one Newton correction of the hardware reciprocal.  Exact here since
@@ -1313,7 +1318,7 @@ struct K3Ctl {
     uint32_t S, R, ntot, nc, L, done, failed, inserted, winner, tag;
     int32_t i_last;
     uint32_t min_i, max_i, fail, summ, nstrict, mxlen, cmax;
-    uint32_t path, need;                      // the P2 variant taken (K3_PATH_*); (profile build) its LDS bytes
+    uint32_t path, need, cacheb;              // the P2 variant taken (K3_PATH_*); (profile build) its LDS bytes, cache part
     unsigned long long t_run;                 // (profile build) s_memrealtime at k3_run's start
     uint32_t ins_n, ins_st, ins_mo, ins_tg;   // register variant: winner whose insert is pending
     unsigned long long scr;
@@ -1452,14 +1457,15 @@ struct K3Mem {
 // its reciprocal is taken beside the dependent count load.
 DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint32_t summ,
                        bool with_slots, uint32_t rcw, uint64_t off[K3_NOFF], bool c8 = false, bool with_mo = true,
-                       uint64_t aux_b = ~0ull, bool with_mnst = true) {
+                       uint64_t aux_b = ~0ull, bool with_mnst = true, bool with_side = true) {
     const uint32_t nwords = (R + 63) >> 6;
+    const uint64_t sd = with_side ? 1ull : 0ull;       // hp, flg, ord in LDS (else k3_side_mem)
     off[0] = 0;                                        // sum   S*4
     off[1] = align16(off[0] + 4ull * S);               // cnt   ntot*4
     off[2] = align16(off[1] + (c8 ? 2ull : 4ull) * ntot);   // hp    R (cnt: u8 pairs when c8)
-    off[3] = align16(off[2] + R);                      // flg   R
-    off[4] = align16(off[3] + R);                      // ord   R*2 (dir 1)
-    off[5] = align16(off[4] + (dir ? 2ull * R : 0));   // untag nwords*8
+    off[3] = align16(off[2] + sd * R);                 // flg   R
+    off[4] = align16(off[3] + sd * R);                 // ord   R*2 (dir 1)
+    off[5] = align16(off[4] + (dir ? 2ull * sd * R : 0));   // untag nwords*8
     const uint64_t mw = !with_mnst ? 0ull : S < 8192u ? 2ull : 4ull;   // (u16 when every index fits: see k3_mem)
     off[6] = align16(off[5] + 8ull * nwords);          // mn    R*2|4  methmers per read
     off[7] = align16(off[6] + mw * R);                 // mst   R*2|4  first site index
@@ -1494,6 +1500,18 @@ DEV void k3_mem(uint8_t *base, const uint64_t off[K3_NOFF], uint32_t rcw, bool w
     m.recc = reinterpret_cast<uint32_t *>(base + off[11] + 8ull * PF_K3_WAVES * rcw);
     m.aux = reinterpret_cast<uint32_t *>(base + off[11]);
     m.rcw = rcw;
+}
+
+// the per-read side arrays (hp, flg, ord, aux) of problem (r0, dir) in the
+// batch's HBM buffer d.k3_side: touched by the problem set-up, one store per
+// iteration (the winner's hp), a load per 64 queued reads (ord) and the
+// finish -- LDS left to the tables the greedy loop reads in every iteration
+DEV void k3_side_mem(const pf_dev_batch &d, uint32_t r0, uint32_t dir, K3Mem &m) {
+    const uint64_t RB = d.R;
+    m.hp = d.k3_side + dir * RB + r0;
+    m.flg = d.k3_side + 2 * RB + dir * RB + r0;
+    m.ord = reinterpret_cast<uint16_t *>(d.k3_side + 4 * RB) + r0;
+    m.aux = reinterpret_cast<uint32_t *>(d.k3_side + ((6 * RB + 3) & ~3ull)) + dir * RB + r0;
 }
 
 DEV uint32_t k3_mn(const K3Mem &m, uint32_t i) {
@@ -2249,6 +2267,12 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     uint32_t *qbuf = qb + 64 * wid;                      // per-wave queue scratch
     uint32_t lsum = 0;
     bool need_collect = true, have_win = false;
+    // the range walk runs after the first insert (the initial range is not a
+    // walk's result) and then only when the insert touched a site that ended
+    // the last walk: umin - 1 or umin on the left (it stopped at an uncovered
+    // site; coverage only grows, and only by inserts), umax or umax + 1 on the
+    // right -- the walk's result is otherwise what it was
+    bool rng_walk = true;
     // per-candidate totals, double-buffered by iteration parity: exact fp64
     // hap sums [2][128] and push/positive count pairs [2][64]
     double *accd = reinterpret_cast<double *>(cd.key);
@@ -2259,7 +2283,8 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
     __syncthreads();
     for (;;) {
         // ---- range after the last insert (update_available_methmer_range)
-        if (have_win) k3_range_regs(m, S, cov_rt, lane, umin, umax);
+        if (have_win && rng_walk) k3_range_regs(m, S, cov_rt, lane, umin, umax);
+        K3_STAMP(4);
         // ---- candidate list: full collection from i_last (:4037-4051)
         if (need_collect) {
             bool done = false;
@@ -2310,6 +2335,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 __syncthreads();
             }
         }
+        K3_STAMP(5);
         // ---- the next untagged read after the list, for this iteration's append
         int qn = -1;
         uint32_t q_rd1 = 0, q_n1 = 0, q_st1 = 0, q_mo1 = 0;
@@ -2326,6 +2352,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
                 q_head++;
             }
         }
+        K3_STAMP(6);
         // CACHE: the appended read's list, loaded now, stored before (X)
         uint32_t pf0 = PF_NONE, pf1 = PF_NONE, s_sp = 0;
         if (CACHE && qn >= 0) {
@@ -2429,12 +2456,18 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         failed = 0;
         if (CACHE) fmask |= 1ull << (mo / CL);           // the winner's slot: free after this insert
         {
-            const int src = (int)lane + 1;
-            const uint32_t a0 = (uint32_t)__shfl((int)c_pos, src, 64), a1 = (uint32_t)__shfl((int)c_rd, src, 64);
-            const uint32_t a2 = (uint32_t)__shfl((int)c_n, src, 64), a3 = (uint32_t)__shfl((int)c_st, src, 64);
-            const uint32_t a4 = (uint32_t)__shfl((int)c_mo, src, 64);
-            const uint32_t a5 = CACHE ? (uint32_t)__shfl((int)c_cs, src, 64) : 0u;
+            // the list closes over the winner: lanes >= cw take their upper
+            // neighbour's entry (DPP, no LDS round trip)
+            const uint32_t a0 = wave_shl1(c_pos), a1 = wave_shl1(c_rd), a2 = wave_shl1(c_n), a3 = wave_shl1(c_st);
+            const uint32_t a4 = CACHE ? 0u : wave_shl1(c_mo);
+            const uint32_t a5 = CACHE ? wave_shl1(c_cs) : 0u;
             if (lane >= cw) { c_pos = a0; c_rd = a1; c_n = a2; c_st = a3; c_mo = a4; c_cs = a5; }
+        }
+        // touched sites [st, st + n) against the last walk's end sites
+        {
+            const uint32_t te = st + n;
+            auto hit = [&](uint32_t a) { return a != 0xFFFFFFFFu && a >= st && a < te; };
+            rng_walk = !have_win || hit(umin) || hit(umin - 1u) || hit(umax) || hit(umax + 1u);
         }
         uint32_t ncn = nc - 1;
         if (qn >= 0) {
@@ -2476,6 +2509,7 @@ DEV void k3_greedy_slim(const pf_dev_batch &d, uint32_t w, uint32_t dir, uint32_
         prof_acc[26] = ctl.t_run;
         prof_acc[30] = ctl.ntot;
         prof_acc[31] = ctl.need;
+        prof_acc[27] = ctl.cacheb;
         for (int i = 0; i < 32; i++) pp[i] = prof_acc[i];
     }
 #endif
@@ -3202,12 +3236,10 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     const uint32_t NCc = (uint32_t)d.win_par[w * 4 + 2];
     const bool cache_ok = slim_ok && slots_ok && NCc <= 63u && CL > 0 && CL <= 2u * NT && (d.k3_cache & 1u) != 0u;
     const bool lists_ok = slots_ok && d.k3_cache < 2u;         // (tests force the cache / the HBM lists)
-    // no per-read slot-list offsets (the cache copies from HBM), and the T5
-    // scratch of k3_init inside the cache region when it is large enough
+    // no per-read slot-list offsets (the cache copies from HBM), and the
+    // per-read side arrays and the T5 scratch of k3_init in HBM (k3_side_mem)
     const uint64_t cache_b = 2ull * (NCc + 1) * CL;
-    const bool aux_in_cache = cache_b >= 4ull * R;
-    const uint64_t slim_cn =
-        k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, aux_in_cache ? 0 : 4ull * R, false);
+    const uint64_t slim_cn = k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, 0, false, false);
     const uint64_t slim_c = align16(slim_cn) + cache_b;
     const bool slim_fit = slim_ok && ((lists_ok && slim_s <= lds) || (cache_ok && slim_c <= lds) || slim_n <= lds);
     if (!FULL && !slim_fit) {
@@ -3222,6 +3254,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
         ctl.path = !slim_fit ? 4u : (lists_ok && slim_s <= lds) ? 1u : (cache_ok && slim_c <= lds) ? 2u : 3u;
 #ifdef PF_K3_PROFILE
         ctl.need = (uint32_t)(cache_ok ? slim_c : ctl.path == 1 ? slim_s : slim_n);   // the cache layout's need
+        ctl.cacheb = (uint32_t)cache_b;
 #endif
     }
     if (slim_fit) {
@@ -3233,14 +3266,14 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
             if (c8) k3_greedy_slim<true, NT, true, false, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
             else k3_greedy_slim<true, NT, false, false, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq);
         } else if (cache_ok && slim_c <= lds) {
-            (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, aux_in_cache ? 0 : 4ull * R, false);
+            (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, 0, false, false);
             k3_mem(smem, off, 0, false, kb, m, false, S, false);
+            k3_side_mem(d, r0, dir, m);
             m.gmo = d.mmr_off + 2ull * r0 + dir;
             m.gmn = d.mmr_n + 2ull * r0 + dir;
             m.gmst = d.mmr_start + 2ull * r0 + dir;
             m.kbase = kbase;
             m.sl16 = reinterpret_cast<uint16_t *>(smem + align16(slim_cn));
-            if (aux_in_cache) m.aux = reinterpret_cast<uint32_t *>(m.sl16);
             if (c8) k3_greedy_slim<true, NT, true, true, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq, CL);
             else k3_greedy_slim<true, NT, false, true, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq, CL);
         } else {
@@ -3302,7 +3335,9 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
 // first) from the counter d.k3_next until k3_n are taken -- list scheduling,
 // so a slot freed on any CU takes the next problem at once.  Every workgroup
 // leaves when the counter passes k3_n.
-__global__ __launch_bounds__(PF_K3S_THREADS) void pf_k3_greedy(pf_dev_batch d) {
+// At most 128 VGPRs (four waves per SIMD): four problems per CU when the LDS
+// budget allows it (pf_api.hip k3_lds_four; round 4's 132 VGPRs held three).
+__global__ __launch_bounds__(PF_K3S_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void pf_k3_greedy(pf_dev_batch d) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ K3Ctl ctl;
     __shared__ K3CandSlim cd;
@@ -4254,6 +4289,8 @@ __global__ __launch_bounds__(64) void pf_selftest_wave(unsigned long long *bad) 
     {
         const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
         if (lane > 0) nb += sh != v[lane - 1];
+        const uint32_t sl = wave_shl1(x);
+        nb += sl != (lane < 63 ? v[lane + 1] : 0u);
     }
     nb += wave_max_dpp(x) != mx;
     for (uint32_t ncp = 1; ncp <= 64; ncp <<= 1) {

@@ -237,6 +237,7 @@ DEV uint32_t swar_dec(uint64_t y, uint32_t n) {      // bytes 0..n-1 of y (n in 
 // byte from memory: one dependent round trip per row and per header byte.
 struct K0Hdr { uint32_t base, strand, nc, h; int mi; };
 
+template <bool MULTI>
 DEV bool k0_mm_entries(const uint32_t *gw, const uint8_t *mm, uint32_t mis, uint32_t mlen, uint32_t mln,
                        uint32_t lane, K0Tgts &T) {
     T.n = 0;
@@ -285,11 +286,12 @@ DEV bool k0_mm_entries(const uint32_t *gw, const uint8_t *mm, uint32_t mis, uint
         if (H.base == ',') commas--;                  // count the skip list's commas only
         if (H.base == 'C' && H.mi >= 0 && commas > 0) {
             if (mln && ml_cur + (uint64_t)commas * H.nc > mln) return false;
+            if (!MULTI && T.n) { T.n = 2; return true; }   // the main pass hands the record over
             if (T.n == PF_K0_MAXT) { T.over = 1; return true; }
             K0Tgt t;
             t.nd = commas; t.nc = H.nc; t.mi = (uint32_t)H.mi; t.th = H.h; t.te = e; t.ml = ml_cur;
             if (T.n == 0) T.t0 = t;
-            else k0_tgt_put(T.xt, T.n, t, lane);
+            else if constexpr (MULTI) k0_tgt_put(T.xt, T.n, t, lane);
             T.n++;
         }
         ml_cur += (uint64_t)commas * H.nc;
@@ -1204,9 +1206,12 @@ template <bool MULTI, typename TP>
 DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, TP TB, uint32_t cap, const K0Tgts &T,
                    bool okm) {
     K0Tgt t = T.t0;
-    const bool multi = MULTI && T.n > 1;
+    bool multi = false;
     uint32_t ndsum = t.nd;
-    for (uint32_t e = 1; e < T.n; e++) ndsum += k0_tgt_get(T, e).nd;
+    if constexpr (MULTI) {                            // the main pass only sees records of one C m entry
+        multi = T.n > 1;
+        for (uint32_t e = 1; e < T.n; e++) ndsum += k0_tgt_get(T, e).nd;
+    }
     const uint32_t r = R.r;
     const uint32_t len = R.len;
     const bool rev = (R.flag & 16u) != 0;
@@ -1396,7 +1401,7 @@ DEV void k0_one(const pf_load_dev &d, K0W &L, uint32_t slot, uint32_t lane) {
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(mmg) & 3u);
     K0Tgts T;
     T.xt = L.opE;                                     // free until the CIGAR walk (PF_K0_TW x 7 <= 64 words)
-    const bool okm = k0_mm_entries(reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis, R.mlen, R.mln, lane, T);
+    const bool okm = k0_mm_entries<MULTI>(reinterpret_cast<const uint32_t *>(mmg - mis), mmg, mis, R.mlen, R.mln, lane, T);
     if (T.over) {                                     // more C m entries than this build merges
         if (lane == 0) { atomicOr(d.status, PF_ST_MM_LIMIT); d.rec_n[r] = PF_NONE; }
         return;
@@ -1406,7 +1411,8 @@ DEV void k0_one(const pf_load_dev &d, K0W &L, uint32_t slot, uint32_t lane) {
         return;
     }
     uint32_t ndsum = T.t0.nd;
-    for (uint32_t e = 1; e < T.n; e++) ndsum += k0_tgt_get(T, e).nd;
+    if constexpr (MULTI)
+        for (uint32_t e = 1; e < T.n; e++) ndsum += k0_tgt_get(T, e).nd;
     if (R.scr_len == 0 || !okm || uni(ndsum) <= (uint32_t)PF_K0_TCAP)
         k0_record<MULTI>(d, L, R, lane, L.T, (uint32_t)PF_K0_TCAP, T, okm);
     else k0_record<MULTI>(d, L, R, lane, d.scr + R.scr_off, R.scr_len, T, okm);

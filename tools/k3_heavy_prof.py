@@ -18,7 +18,7 @@ from pomfret_amd import Config, Context, LoadConfig  # noqa: E402
 from pomfret_amd.synth_aln import AlnSpec, make_aln_batch  # noqa: E402
 
 # stamp slots of k3_greedy_slim (K3_STAMP indices)
-SLIM = {0: "init", 2: "upkeep+spans", 10: "fill", 3: "barrier B", 19: "pick", 20: "list shift",
+SLIM = {0: "init", 4: "range", 5: "collect", 6: "queue", 2: "prefetch+spans", 10: "fill", 3: "barrier B", 19: "pick", 20: "list shift",
         21: "insert", 8: "barrier X"}
 SPEC = dict(n_windows=1024, coverage=60, gap=50_000, seed=1000, gap_mix=True, skip_frac=0.10, nosite_frac=0.05)
 WIDE = [218, 422, 691, 580, 52, 884]
@@ -31,6 +31,7 @@ db = ctx.upload_aln(cfg, aln, lcfg)
 db.run()
 db.run()
 kt = ctx.kernel_times()
+print("greedy launch", db.k3_budget())
 W = aln.n_windows
 lib = L.lib()
 lib.pf_batch_prof.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
@@ -99,7 +100,13 @@ if allp:
         if sel.any():
             print(f"  [{lo},{hi}): {sel.sum():4d}  {np.median(a[sel, 1]):5.1f} / {np.percentile(a[sel, 1], 90):5.1f} / "
                   f"{a[sel, 1].max():5.1f}   {np.median(a[sel, 2]):.2f} / {a[sel, 2].max():.2f}")
-    for b in (32, 36, 44, 48, 56):
+    big = sorted(range(2 * W), key=lambda p: -prof[p >> 1, p & 1, 31])[:8]
+    print("  largest needs (w,dir): reads sites slots need KB = cache KB + rest KB")
+    for p in big:
+        w, d = divmod(p, 2)
+        print(f"    ({w},{d}) {st[w, d, 6]} {st[w, d, 7]} {prof[w, d, 30]:.0f} {prof[w, d, 31] / 1024:.1f} = "
+              f"{prof[w, d, 27] / 1024:.1f} + {(prof[w, d, 31] - prof[w, d, 27]) / 1024:.1f}")
+    for b in (32, 34, 36, 40, 44, 48):
         print(f"  need > {b} KB: {(a[:, 1] > b).sum()} problems, min reads among them "
               f"{int(a[a[:, 1] > b, 0].min()) if (a[:, 1] > b).any() else '-'}")
 # K12 phases (K12_STAMP, cycles) per window: mean, the slowest window, and the
