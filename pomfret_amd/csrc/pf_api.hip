@@ -707,8 +707,11 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     // (k3_side_mem) and the main kernel fits 128 VGPRs, so at the four-per-CU
     // budget (k3_lds_four, ~37 KB) every problem of the 60x gap mix fits
     // (largest 36.0 KB, at 1,431 reads; tools/k3_heavy_prof.py): four
-    // problems per CU when no window passes PF_K3_FOUR_RMAX reads (1,500), or
-    // when 90 % of the windows are small (the heavy kernel takes the rest).
+    // problems per CU when no window passes PF_K3_FOUR_RMAX records (1,600:
+    // the mix's largest windows hold 1,503-1,514 records for at most 1,431
+    // kept reads; a problem past the budget is deferred to the fallback
+    // kernel, exact but after the main kernel), or when 90 % of the windows
+    // are small (the heavy kernel takes the rest).
     uint32_t lds_auto = 49152u;
     if (W) {
         std::vector<uint32_t> rw(W);
@@ -716,7 +719,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         const uint32_t rmax = *std::max_element(rw.begin(), rw.end());
         std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
         const char *fr = getenv("PF_K3_FOUR_RMAX");
-        const uint32_t four_rmax = fr ? (uint32_t)atoi(fr) : 1500u;
+        const uint32_t four_rmax = fr ? (uint32_t)atoi(fr) : 1600u;
         if (rw[(W * 9) / 10] <= 400 || rmax <= four_rmax) lds_auto = k3_lds_four(b->ctx->device);
     }
     const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB"), *ldw = getenv("PF_K3W_LDS");
