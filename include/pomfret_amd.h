@@ -276,8 +276,10 @@ int  pf_batch_stats(pf_dbatch_t *db, uint64_t *out, uint64_t n);
 /* The greedy loop's slot-list source per (window, direction) of the last
  * run, out[w*2+dir]: 1 slot lists in LDS, 2 the candidate cache in LDS, 3
  * slot lists in HBM (the slim loop), 4 the general body (fallback kernel),
- * 5 the one-wave kernel (pf_k3_wave), 0 no greedy run (no sites).  n >= 2*n_windows.  Tests assert which
- * variant PF_K3_CACHE forced. */
+ * 5 the one-wave kernel (pf_k3_wave), 6 the candidate cache with the count
+ * table in HBM (a problem a few KB past the main kernel's budget), 0 no
+ * greedy run (no sites).  n >= 2*n_windows.  Tests assert which variant
+ * PF_K3_CACHE / PF_K3_GCNT forced. */
 int  pf_batch_k3_paths(pf_dbatch_t *db, uint8_t *out, uint64_t n);
 /* The greedy launch this batch was given: out[0] the main kernel's dynamic
  * LDS per problem, out[1] its persistent workgroups (problems at once on the

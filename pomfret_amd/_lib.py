@@ -479,7 +479,8 @@ class DeviceBatch:
     def k3_paths(self) -> np.ndarray:
         """Per-(window, dir) slot-list source of the last run's greedy loop:
         [W, 2] of 1 LDS lists, 2 candidate cache, 3 HBM lists, 4 general
-        body, 0 no sites (pf_batch_k3_paths)."""
+        body, 5 one-wave kernel, 6 candidate cache with the count table in
+        HBM, 0 no sites (pf_batch_k3_paths)."""
         out = np.zeros(max(2 * self.n_windows, 2), np.uint8)
         _check(lib().pf_batch_k3_paths(self.handle, out.ctypes.data, out.size), "pf_batch_k3_paths")
         return out[:2 * self.n_windows].reshape(-1, 2)

@@ -776,6 +776,11 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         const char *kc = getenv("PF_K3_CACHE");
         d.k3_cache = !kc ? K3C_AUTO : !strcmp(kc, "0") ? K3C_NONE : !strcmp(kc, "force") ? K3C_FORCE
                    : !strcmp(kc, "hbm") ? K3C_HBM : K3C_AUTO;
+        // path 6 (the candidate cache with the count table in HBM) for every
+        // candidate-cache problem with u8 count pairs, not only those past
+        // the budget: PF_K3_GCNT=force (tests)
+        const char *kg = getenv("PF_K3_GCNT");
+        d.k3_gcnt = kg && !strcmp(kg, "force") ? 1u : 0u;
     }
     for (int i = 0; i < PF_SLOTS; i++)
         if (hipHostMalloc((void **)&b->h_io[i], b->io_bytes) != hipSuccess) return fail(PF_ERR_NOMEM);

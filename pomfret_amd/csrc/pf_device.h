@@ -96,6 +96,7 @@ struct pf_dev_batch {
     uint32_t k2_entcap;                /* fallback reads above this bound use HBM scratch */
     uint32_t k3_mode;                  /* test override: 0 exact pick, 1 always fold, 2 chunked record rows */
     uint32_t k3_cache;                 /* 1: candidate slot-list cache when a window's lists miss LDS (PF_K3_CACHE=0: off) */
+    uint32_t k3_gcnt;                  /* 1: path 6 (cache + count table in HBM) for every cache problem (PF_K3_GCNT=force) */
 };
 
 #endif

@@ -1457,12 +1457,12 @@ struct K3Mem {
 // its reciprocal is taken beside the dependent count load.
 DEV uint64_t k3_layout(uint32_t S, uint32_t ntot, uint32_t R, uint32_t dir, uint32_t summ,
                        bool with_slots, uint32_t rcw, uint64_t off[K3_NOFF], bool c8 = false, bool with_mo = true,
-                       uint64_t aux_b = ~0ull, bool with_mnst = true, bool with_side = true) {
+                       uint64_t aux_b = ~0ull, bool with_mnst = true, bool with_side = true, bool with_cnt = true) {
     const uint32_t nwords = (R + 63) >> 6;
     const uint64_t sd = with_side ? 1ull : 0ull;       // hp, flg, ord in LDS (else k3_side_mem)
     off[0] = 0;                                        // sum   S*4
-    off[1] = align16(off[0] + 4ull * S);               // cnt   ntot*4
-    off[2] = align16(off[1] + (c8 ? 2ull : 4ull) * ntot);   // hp    R (cnt: u8 pairs when c8)
+    off[1] = align16(off[0] + 4ull * S);               // cnt   ntot*4 (in HBM when !with_cnt: path 6)
+    off[2] = align16(off[1] + (with_cnt ? (c8 ? 2ull : 4ull) * ntot : 0ull));   // hp    R (cnt: u8 pairs when c8)
     off[3] = align16(off[2] + sd * R);                 // flg   R
     off[4] = align16(off[3] + sd * R);                 // ord   R*2 (dir 1)
     off[5] = align16(off[4] + (dir ? 2ull * sd * R : 0));   // untag nwords*8
@@ -3241,25 +3241,62 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     const uint64_t cache_b = 2ull * (NCc + 1) * CL;
     const uint64_t slim_cn = k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, 0, false, false);
     const uint64_t slim_c = align16(slim_cn) + cache_b;
-    const bool slim_fit = slim_ok && ((lists_ok && slim_s <= lds) || (cache_ok && slim_c <= lds) || slim_n <= lds);
+    const bool slim_fit0 = slim_ok && ((lists_ok && slim_s <= lds) || (cache_ok && slim_c <= lds) || slim_n <= lds);
+    // path 6 (round 5): a candidate-cache problem past the budget (the main
+    // kernel's four-per-CU budget leaves the largest windows of a batch a few
+    // KB short) keeps its count table -- the bulk of its need -- in HBM
+    // scratch: it runs at once, heaviest first, instead of in the fallback
+    // kernel after the main one.  u8 count pairs only (c8); PF_K3_GCNT=force
+    // takes it for every such problem (tests)
+    const uint64_t cnt_b = align16(2ull * ntot);
+    const uint64_t slim_g =
+        align16(k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, 0, false, false, false)) + cache_b;
+    const bool gcnt = !FULL && cache_ok && c8 && slim_g <= lds && (!slim_fit0 || d.k3_gcnt != 0u);
+    const bool slim_fit = slim_fit0 || gcnt;
     if (!FULL && !slim_fit) {
         k3_defer(d, prob);           // keys still intact: the fallback rebuilds the dictionary
         return;
+    }
+    if (gcnt) {
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)cnt_b);
+            ctl.fail = 0;
+            if (o + cnt_b > d.scr_cap) { ctl.fail = 1; atomicOr(d.status, PF_ST_SCR_OVF); }   // the host grows it, re-runs
+            ctl.scr = o;
+        }
+        __syncthreads();
+        if (uni(ctl.fail)) return;
     }
     k3_dict_rewrite<NT>(d, r0, R, S, dir, masks, mbase);
     const uint32_t *kb = d.keys + kbase;
     if (tid == 0) {
         // 1 slot lists in LDS, 2 the candidate cache, 3 slot lists in HBM (slim loop); 4 the general body;
         // reported with the problem's stats (pf_batch_k3_paths)
-        ctl.path = !slim_fit ? 4u : (lists_ok && slim_s <= lds) ? 1u : (cache_ok && slim_c <= lds) ? 2u : 3u;
+        ctl.path = !slim_fit ? 4u : gcnt ? 6u : (lists_ok && slim_s <= lds) ? 1u : (cache_ok && slim_c <= lds) ? 2u : 3u;
 #ifdef PF_K3_PROFILE
-        ctl.need = (uint32_t)(cache_ok ? slim_c : ctl.path == 1 ? slim_s : slim_n);   // the cache layout's need
+        ctl.need = (uint32_t)(cache_ok ? slim_c : ctl.path == 1 ? slim_s : slim_n);   // the cache layout's need (path 6: with its counts)
         ctl.cacheb = (uint32_t)cache_b;
 #endif
     }
     if (slim_fit) {
         K3Mem m;
         uint32_t *qq = qb ? qb : cd.read;
+        if constexpr (!FULL) {
+            if (gcnt) {
+                (void)k3_layout(S, ntot, R, dir, summ_tot, false, 0, off, c8, false, 0, false, false, false);
+                k3_mem(smem, off, 0, false, kb, m, false, S, false);
+                k3_side_mem(d, r0, dir, m);
+                m.cnt = reinterpret_cast<uint32_t *>(d.scr + ctl.scr);
+                m.gmo = d.mmr_off + 2ull * r0 + dir;
+                m.gmn = d.mmr_n + 2ull * r0 + dir;
+                m.gmst = d.mmr_start + 2ull * r0 + dir;
+                m.kbase = kbase;
+                m.sl16 = reinterpret_cast<uint16_t *>(smem + (slim_g - cache_b));
+                k3_greedy_slim<true, NT, true, true, CD>(d, w, dir, r0, S, R, m, ctl, cd, sh_scan, qq, CL);
+                return;
+            }
+        }
         if (lists_ok && slim_s <= lds) {
             (void)k3_layout(S, ntot, R, dir, summ_tot, true, 0, off, c8);
             k3_mem(smem, off, 0, true, kb, m, true, S);

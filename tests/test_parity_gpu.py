@@ -130,15 +130,21 @@ def test_lds_budget_variants(oracle_lib, gpu_ctx, monkeypatch, lds):
 
 
 @pytest.mark.parametrize("env", [{"PF_K3_CACHE": "force"}, {"PF_K3_CACHE": "hbm"}, {"PF_K3_PERSIST": "1"},
-                                 {"PF_K3_PERSIST": "7", "PF_K3_CACHE": "force"}],
-                         ids=["cache", "hbm_lists", "one_workgroup", "seven_workgroups_cache"])
+                                 {"PF_K3_PERSIST": "7", "PF_K3_CACHE": "force"},
+                                 {"PF_K3_CACHE": "force", "PF_K3_GCNT": "force"},
+                                 {"PF_K3_LDS": "24576", "PF_K3_LDS_FB": "73728"}],
+                         ids=["cache", "hbm_lists", "one_workgroup", "seven_workgroups_cache", "cache_counts_hbm",
+                              "budget_24k"])
 def test_slot_list_sources(oracle_lib, gpu_ctx, monkeypatch, env):
     """The greedy loop's slot-list sources give the same bits on every case:
     the candidate slot-list cache (round 4: the candidates' lists in LDS, the
     appended read's list loaded an iteration ahead) forced for every problem,
     the slot lists read from HBM, and the persistent main kernel with one
     and with seven workgroups walking all the problems in turn (per-problem
-    state reset between problems)."""
+    state reset between problems).  Round 5: the candidate cache with the
+    count table in HBM (path 6) forced for every cache problem with u8 count
+    pairs, and a 24 KB budget under which problems past it take path 6 by
+    themselves."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     seen = set()
@@ -153,11 +159,13 @@ def test_slot_list_sources(oracle_lib, gpu_ctx, monkeypatch, env):
         seen |= set(p)
         mode = env.get("PF_K3_CACHE")
         if mode == "force":
-            assert set(p) <= {2, 3, 4}, (name, p)
+            assert set(p) <= {2, 3, 4, 6}, (name, p)
         elif mode == "hbm":
             assert set(p) <= {3, 4}, (name, p)
         db.free()
-    if env.get("PF_K3_CACHE") == "force":
+    if env.get("PF_K3_GCNT") == "force":
+        assert 6 in seen, seen
+    elif env.get("PF_K3_CACHE") == "force":
         assert 2 in seen
     elif env.get("PF_K3_CACHE") == "hbm":
         assert 3 in seen
