@@ -707,11 +707,14 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     // (k3_side_mem) and the main kernel fits 128 VGPRs, so at the four-per-CU
     // budget (k3_lds_four, ~37 KB) every problem of the 60x gap mix fits
     // (largest 36.0 KB, at 1,431 reads; tools/k3_heavy_prof.py): four
-    // problems per CU when no window passes PF_K3_FOUR_RMAX records (1,600:
-    // the mix's largest windows hold 1,503-1,514 records for at most 1,431
-    // kept reads; a problem past the budget is deferred to the fallback
-    // kernel, exact but after the main kernel), or when 90 % of the windows
-    // are small (the heavy kernel takes the rest).
+    // problems per CU when no window passes PF_K3_FOUR_RMAX records (2,000,
+    // where the heavy split starts), or when 90 % of the windows are small
+    // (the heavy kernel takes the rest).  A problem past the budget takes
+    // path 6 (its count table in HBM, k3_run): forced on every problem of the
+    // mix it costs 14 % of K3 (4.10 -> 4.68 ms, profiles/r05/ab_k3_path6_forced.txt),
+    // so four per CU with every problem on it still matches three per CU
+    // without it (4.66 ms); the mix's largest windows hold 1,503-1,514
+    // records for at most 1,431 kept reads and all fit the budget.
     uint32_t lds_auto = 49152u;
     if (W) {
         std::vector<uint32_t> rw(W);
@@ -719,7 +722,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
         const uint32_t rmax = *std::max_element(rw.begin(), rw.end());
         std::nth_element(rw.begin(), rw.begin() + (W * 9) / 10, rw.end());
         const char *fr = getenv("PF_K3_FOUR_RMAX");
-        const uint32_t four_rmax = fr ? (uint32_t)atoi(fr) : 1600u;
+        const uint32_t four_rmax = fr ? (uint32_t)atoi(fr) : 2000u;
         if (rw[(W * 9) / 10] <= 400 || rmax <= four_rmax) lds_auto = k3_lds_four(b->ctx->device);
     }
     const char *lds = getenv("PF_K3_LDS"), *ldf = getenv("PF_K3_LDS_FB"), *ldw = getenv("PF_K3W_LDS");
