@@ -69,6 +69,36 @@ for label, sel in (("heavy", [p for p in range(2 * W) if p in heavy]),
         print(f"    ({w},{d}) {st[w, d, 6]} {st[w, d, 7]} {st[w, d, 2]} {st[w, d, 0] / max(st[w, d, 2], 1):.0f} "
               f"{st[w, d, 4]} {sum(prof[w, d, k] for k in SLIM) / 1e6:.2f} {int(prof[w, d, 29])} "
               f"{prof[w, d, 31] / 1024:.1f}")
+# the heaviest-first order against the measured per-problem cycles: list
+# scheduling of those cycles over the resident slots (the main kernel's
+# persistent grid) in three orders -- reads (k3_order today), methmers (the
+# window's total over its reads), the measured cycles themselves (ideal)
+if sel_all := [p for p in range(2 * W) if prof[p >> 1, p & 1, 29] > 0]:
+    import heapq
+    cyc_all = np.array([sum(prof[p >> 1, p & 1, k] for k in SLIM) for p in sel_all])
+    reads_all = np.array([float(st[p >> 1, p & 1, 6]) for p in sel_all])
+    mm_all = np.array([float(st[p >> 1, p & 1, 4]) for p in sel_all])
+    slots = int(db.k3_budget()["resident"])
+    def makespan(order):
+        h = [0.0] * slots
+        for i in order:
+            t = heapq.heappop(h)
+            heapq.heappush(h, t + cyc_all[i])
+        return max(h)
+    rw_ = np.diff(aln.win_rec_off.astype(np.int64))
+    bases_w = np.add.reduceat(aln.l_qseq.astype(np.float64), aln.win_rec_off[:-1].astype(np.int64)) * (rw_ > 0)
+    bases_all = np.array([bases_w[p >> 1] for p in sel_all])
+    rec_all = np.array([float(rw_[p >> 1]) for p in sel_all])
+    print(f"  corr(cycles, bases) {np.corrcoef(cyc_all, bases_all)[0, 1]:.3f}, corr(cycles, records) "
+          f"{np.corrcoef(cyc_all, rec_all)[0, 1]:.3f}, corr(cycles, records^1.5) "
+          f"{np.corrcoef(cyc_all, rec_all ** 1.5)[0, 1]:.3f}, corr(cycles, records x bases) "
+          f"{np.corrcoef(cyc_all, rec_all * bases_all)[0, 1]:.3f}")
+    for lab, key in (("reads", -reads_all), ("methmers", -mm_all), ("bases", -bases_all),
+                     ("records x bases", -rec_all * bases_all), ("measured cycles", -cyc_all)):
+        o = np.lexsort((np.arange(len(key)), key))
+        print(f"  list schedule over {slots} slots by {lab:16s}: makespan {makespan(o) / 1e6:.2f} Mcycles")
+    print(f"  corr(cycles, reads) {np.corrcoef(cyc_all, reads_all)[0, 1]:.3f}, corr(cycles, methmers) "
+          f"{np.corrcoef(cyc_all, mm_all)[0, 1]:.3f}")
 # concurrency over time from the problems' start/end (s_memrealtime, 100 MHz)
 t0s = prof[:, :, 24].ravel()
 t1s = prof[:, :, 25].ravel()
