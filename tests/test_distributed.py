@@ -183,20 +183,23 @@ def _mc_worker(rank, world, port, tmp, untagged):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("untagged", [False, True])
-def test_two_rank_multicontig(tmp_path, oracle_lib, untagged):
+def test_two_rank_multicontig(tmp_path, oracle_lib, untagged, world):
     """Four BAM contigs, three in the VCF (one without reads, header order
-    different from the VCF's), qnames shared across contigs, no -c: the two
+    different from the VCF's), qnames shared across contigs, no -c: the
     ranks' jobs merged on the writer equal the single-process oracle pipeline
     -- per-contig parameters (4358-4390), contig-order first-wins merge
-    (4579-4595), the shared -u raw table (1880), PS 0 on later contigs."""
+    (4579-4595), the shared -u raw table (1880), PS 0 on later contigs.  At
+    world 4 the ranks outnumber the contigs with reads: shares are uneven and
+    may be empty (the case an 8-GPU run meets on a small job)."""
     import json
     from tests import _fixtures as fx
     from tests._oracle_pipeline import methphase_files_oracle
     bam, vcf, recs_by, _ = fx.multi_contig(tmp_path, untagged=untagged)
-    mp.spawn(_mc_worker, args=(2, _free_port(), str(tmp_path), untagged), nprocs=2, join=True)
+    mp.spawn(_mc_worker, args=(world, _free_port(), str(tmp_path), untagged), nprocs=world, join=True)
     ref = methphase_files_oracle(bam, vcf, None, untagged=untagged, recs_by_contig=recs_by)
-    for r in range(2):
+    for r in range(world):
         got = json.load(open(tmp_path / f"res{r}.json"))
         assert got["decision"] == ref["decision"].tolist()
         assert [tuple(x) for x in got["qname_hp"]] == list(ref["qname_hp"].items())
