@@ -431,6 +431,10 @@ typedef struct pf_bam pf_bam_t;
  * file cannot be opened. */
 int  pf_bam_open(const char *bam_path, const char *bai_path, pf_bam_t **out);
 void pf_bam_close(pf_bam_t *bam);
+/* The host BGZF reader's block decoder: 1 = libdeflate (loaded at run time,
+ * as htslib links it), 0 = zlib (libdeflate absent, or PF_HOST_ZLIB set in
+ * the environment before the first block).  Diagnostics only. */
+int  pf_host_inflater(void);
 int32_t pf_bam_n_targets(const pf_bam_t *bam);
 const char *pf_bam_target_name(const pf_bam_t *bam, int32_t tid);
 uint32_t pf_bam_target_len(const pf_bam_t *bam, int32_t tid);

@@ -1247,6 +1247,10 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
     const size_t L = strlen(p->out_prefix) + 32;
     char *fn = (char *)malloc(L);
     if (!fn) return PF_ERR_NOMEM;
+    /* PF_MP_TRACE: the writers' steps on stderr (seconds) */
+    const int trace = getenv("PF_MP_TRACE") != NULL;
+    double tw = now_s();
+#define WTRACE(what) do { if (trace) { const double t_ = now_s(); fprintf(stderr, "[writers] %s %.3fs\n", what, t_ - tw); tw = t_; } } while (0)
     snprintf(fn, L, "%s.mp.gtf", p->out_prefix);
     int rc = pf_write_gtf(p->gaps, p->blocks, fn);
     if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] gtf written.\n");
@@ -1260,6 +1264,7 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
         snprintf(fn, L, "%s.mp.input_haptag.tsv", p->out_prefix);
         rc = pf_retag_bam(p->bam_path, NULL, NULL, fn, PF_RETAG_INPUT_HAPTAG, NULL, NULL, NULL, p->raw, -1, NULL);
     }
+    WTRACE("gtf/tsv/input_haptag");
     /* the VCF only when --vcf was given (4706) */
     if (rc || !p->vcf_path) { free(fn); return rc; }
     /* rescue of dropped-interval sites (recover_variant_phase_in_dropped_intervals) + VCF */
@@ -1306,6 +1311,7 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
     }
     for (uint32_t c = 0; kall && c < C; c++) pf_known_table_free(kall[c]);
     free(kall);
+    WTRACE("known-variant tables");
     if (!rc && nr) rc = pf_bam_open(p->bam_path, NULL, &bam);
     if (!rc && nr)
         rc = pf_rescue_dropped_multi(bam, nr, rn_names, rn_nd, rn_ds, rn_de, kvs, &tm, p->o.untagged ? &tr : NULL,
@@ -1334,12 +1340,14 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
     }
     free(rn_names); free(rn_nd); free(rn_c); free(rn_ds); free(rn_de); free(kts); free(kvs); free(maps);
     if (bam) pf_bam_close(bam);
+    WTRACE("rescue (dropped intervals)");
     if (!rc) {
         pf_rescue_t res = {roff, rpos ? rpos : (const uint32_t *)roff, rhap ? rhap : (const uint8_t *)roff};
         snprintf(fn, L, "%s.mp.vcf", p->out_prefix);
         if (p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] writing vcf...\n");
         rc = pf_write_vcf(p->vcf_path, p->gaps, p->blocks, &res, fn, NULL);
         if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] vcf written.\n");
+        WTRACE("vcf");
     }
     if (!rc && p->o.write_bam) {                    /* output_modify_bam + sam_index_build3 (4719-4731) */
         char *fb = (char *)malloc(L + 8);
@@ -1355,6 +1363,7 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
     }
     free(roff); free(rpos); free(rhap); free(fn);
     return rc;
+#undef WTRACE
 }
 
 /* varhaptag (main_varhaptag, 4737-4836): the -u pre-pass on the devices,

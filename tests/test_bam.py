@@ -69,6 +69,48 @@ def test_fetch_windows_matches_overlap_rule(tmp_path):
     _check_fetch(p, allr, refs, "chrB", [int(aln.win_start[0])], [int(aln.win_end[0])], 50_000)
 
 
+_FETCH_DIGEST = r"""
+import hashlib, sys
+from pomfret_amd._lib import lib
+from pomfret_amd.bam import BamFile
+p, chrom, s, e = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+h = hashlib.sha256()
+with BamFile(p) as b:
+    got, qn, info = b.fetch_windows(chrom, [s], [e], readback=50_000, threads=2)
+for f in ("pos", "flag", "cigar", "seq", "mm", "ml", "de", "hp", "cigar_off", "seq_off"):
+    h.update(getattr(got, f).tobytes())
+h.update("\n".join(qn).encode())
+print(lib().pf_host_inflater(), got.n_recs, h.hexdigest())
+"""
+
+
+def test_host_inflaters_agree(tmp_path):
+    """The host BGZF reader decodes with libdeflate when the system has it and
+    with zlib otherwise (or under PF_HOST_ZLIB): both fetch the same bytes."""
+    import subprocess
+    import sys
+    aln, recs = _aln_records(n_windows=2, seed=4)
+    p = str(tmp_path / "z.bam")
+    write_bam(p, [("c1", 40_000_000)], recs)
+    s, e = int(aln.win_start[0]), int(aln.win_end[-1])
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for name, extra in (("default", {}), ("zlib", {"PF_HOST_ZLIB": "1"})):
+        env = {k: v for k, v in os.environ.items() if k != "PF_HOST_ZLIB"}
+        env.update(extra)
+        env["PYTHONPATH"] = repo + os.pathsep + env.get("PYTHONPATH", "")
+        r = subprocess.run([sys.executable, "-c", _FETCH_DIGEST, p, "c1", str(s), str(e)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out[name] = r.stdout.split()
+    assert out["zlib"][0] == "0"
+    have_ldf = any(os.path.exists(os.path.join(d, "libdeflate.so.0"))
+                   for d in ("/usr/lib/x86_64-linux-gnu", "/usr/lib64", "/usr/lib"))
+    assert out["default"][0] == ("1" if have_ldf else "0")
+    assert int(out["default"][1]) > 0
+    assert out["default"][1:] == out["zlib"][1:]
+
+
 def test_fetched_fields_equal_the_written_records(tmp_path):
     aln, recs = _aln_records(n_windows=2, seed=9)
     refs = [("c1", 40_000_000)]
