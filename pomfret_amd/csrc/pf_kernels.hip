@@ -783,14 +783,16 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     if (tid == 0) { sh_misc[4] = 0; d.win_nreads[w] = R; }
     __syncthreads();
 
-    // ---- fast path: LDS hash of call positions (meth/unmeth only) + a bitmap of
-    // qualifying positions over [pmin, pmin + 64*BW): a site's index (its rank in
-    // position order) is a prefix popcount, so no sort is needed.
-    constexpr uint32_t HN = 8192, HMAX = 6144, BW = 8192;
-    uint32_t *hkeys = tile, *hcnt = tile + HN;
-    uint64_t *bmap = reinterpret_cast<uint64_t *>(tile + 2 * HN);
+    // ---- fast path: a bitmap of the positions with >= 2 meth/unmeth calls over
+    // [pmin, pmin + 64*BW), one counter per such position indexed by its rank
+    // among them (a prefix popcount: no hash, no probing), then the bitmap of
+    // qualifying positions, whose prefix popcount is a site's index, so no
+    // sort is needed.
+    constexpr uint32_t BW = 8192, RMAX = 12288;
+    static_assert(BW / 2 + RMAX <= PF_K1_TILE / 2, "word ranks + counters fit the first half of the tile");
+    uint64_t *bmap = reinterpret_cast<uint64_t *>(tile + PF_K1_TILE / 2);
     const bool range_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64 && !d.k12_dense;
-    bool hash_ok = false;
+    bool fast = false;
     // the window's calls are one contiguous run: flat passes, four
     // independent (cat, pos) loads in flight per thread
     const uint64_t C0 = d.read_call_off[r0], C1 = d.read_call_off[r0 + R];
@@ -798,10 +800,10 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     // needs >= cov_sel calls of each kind, so no other position can qualify.
     // Pass B counts only those.  Sequencing errors put CpG calls at positions
     // that one read alone covers; with real reads they outnumber the sites, and
-    // filtering them keeps the table small and its probes short.
+    // filtering them keeps the counters few.
     if (range_ok) {
         {
-            uint64_t *once = reinterpret_cast<uint64_t *>(tile);   // over the hash table
+            uint64_t *once = reinterpret_cast<uint64_t *>(tile);   // the first half of the tile
             for (uint32_t j = tid; j < BW; j += NT) { once[j] = 0; bmap[j] = 0; }
             __syncthreads();
             for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
@@ -824,78 +826,82 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
             }
             __syncthreads();
         }
-        // more repeated positions than the hash may hold: the dense path,
-        // without pass B (an overflowing table leaves every later key probing
-        // a full table, the whole workgroup contending on the reservation
-        // counter: 5-7 M cycles on a 500 kb gap)
+        // more repeated positions than counters: the dense path
+        constexpr uint32_t PW = BW / NT;                 // bitmap words per thread
         uint32_t rep = 0, rep_tot = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < BW / NT; j++) rep += (uint32_t)__popcll(bmap[tid * (BW / NT) + j]);
-        block_excl_scan<NT>(rep, sh_scan, &rep_tot);
-        if (rep_tot <= HMAX) {
-        for (uint32_t j = tid; j < HN; j += NT) { hkeys[j] = PF_NONE; hcnt[j] = 0; }
-        if (tid == 0) { sh_misc[5] = 0; sh_misc[6] = 0; }
-        __syncthreads();
-        for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
-            uint32_t cat4[4], pos4[4];
+        for (uint32_t j = 0; j < PW; j++) rep += (uint32_t)__popcll(bmap[tid * PW + j]);
+        const uint32_t rep_ex = block_excl_scan<NT>(rep, sh_scan, &rep_tot);
+        if (rep_tot <= RMAX) {
+            // over the freed once-bitmap: each word's rank base (u16), then the
+            // counters (meth in the low half, unmeth in the high half)
+            uint16_t *wrank = reinterpret_cast<uint16_t *>(tile);
+            uint32_t *rcnt = tile + BW / 2;
+            {
+                uint32_t rk = rep_ex;
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint64_t c = cb + (uint64_t)u * NT;
-                const bool ok = c < C1;
-                cat4[u] = ok ? d.call_cat[c] : 2u;
-                pos4[u] = ok ? d.call_pos[c] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t cat = cat4[u];
-                if (cat >= 2) continue;
-                const uint32_t pos = pos4[u];
-                if (!((bmap[(pos - pmin) >> 6] >> ((pos - pmin) & 63)) & 1ull)) continue;
-                const uint32_t inc = cat == 0 ? 1u : 0x10000u;
-                uint32_t h = (pos * 2654435761u) >> 19;
-                for (;;) {
-                    const uint32_t k = __hip_atomic_load(&hkeys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (k == pos) { atomicAdd(&hcnt[h], inc); break; }
-                    if (k == PF_NONE) {
-                        // reserve before inserting: at most HMAX keys ever enter the
-                        // table, so probing always terminates
-                        if (atomicAdd(&sh_misc[5], 1u) >= HMAX) { sh_misc[6] = 1; break; }
-                        const uint32_t old = atomicCAS(&hkeys[h], PF_NONE, pos);
-                        if (old == PF_NONE || old == pos) { atomicAdd(&hcnt[h], inc); break; }
-                    }
-                    h = (h + 1) & (HN - 1);
+                for (uint32_t j = 0; j < PW; j++) {
+                    const uint32_t wi = tid * PW + j;
+                    wrank[wi] = (uint16_t)rk;
+                    rk += (uint32_t)__popcll(bmap[wi]);
                 }
             }
-        }
-        __syncthreads();
-        hash_ok = sh_misc[6] == 0;
-        if (hash_ok) {                                 // bmap becomes the qualifying bitmap
-            for (uint32_t j = tid; j < BW; j += NT) bmap[j] = 0;
+            for (uint32_t j = tid; j < rep_tot; j += NT) rcnt[j] = 0;
             __syncthreads();
-        }
+            for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
+                uint32_t cat4[4], pos4[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t c = cb + (uint64_t)u * NT;
+                    const bool ok = c < C1;
+                    cat4[u] = ok ? d.call_cat[c] : 2u;
+                    pos4[u] = ok ? d.call_pos[c] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (cat4[u] >= 2) continue;
+                    const uint32_t o = pos4[u] - pmin;
+                    const uint64_t bits = bmap[o >> 6];
+                    const uint64_t below = (1ull << (o & 63)) - 1ull;
+                    if (!((bits >> (o & 63)) & 1ull)) continue;
+                    const uint32_t ix = (uint32_t)wrank[o >> 6] + (uint32_t)__popcll(bits & below);
+                    atomicAdd(&rcnt[ix], cat4[u] == 0 ? 1u : 0x10000u);
+                }
+            }
+            __syncthreads();
+            // bmap becomes the qualifying bitmap, each thread over its own words
+            // counts are uint16 holding count<<4 in the reference: count mod 4096 (blockjoin.c:3236)
+            {
+                uint32_t rk = rep_ex;
+#pragma unroll
+                for (uint32_t j = 0; j < PW; j++) {
+                    const uint32_t wi = tid * PW + j;
+                    uint64_t bits = bmap[wi], q = 0;
+                    while (bits) {
+                        const uint32_t b = (uint32_t)__ffsll((unsigned long long)bits) - 1;
+                        bits &= bits - 1;
+                        const uint32_t v = rcnt[rk++];
+                        if ((int)(v & 4095u) >= cov && (int)((v >> 16) & 4095u) >= cov) q |= 1ull << b;
+                    }
+                    bmap[wi] = q;
+                }
+            }
+            __syncthreads();
+            fast = true;
         }
     }
-    if (hash_ok) {
-        for (uint32_t j = tid; j < HN; j += NT) {
-            const uint32_t k = hkeys[j];
-            if (k == PF_NONE) continue;
-            const uint32_t v = hcnt[j];
-            if ((int)(v & 4095u) >= cov && (int)((v >> 16) & 4095u) >= cov) {
-                const uint32_t o = k - pmin;
-                atomicOr((unsigned long long *)&bmap[o >> 6], 1ull << (o & 63));
-            } else hcnt[j] = PF_NONE;
-        }
-        __syncthreads();
+    if (fast) {
+        constexpr uint32_t PW = BW / NT;
         uint32_t mycount = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < BW / NT; j++) mycount += (uint32_t)__popcll(bmap[tid * (BW / NT) + j]);
+        for (uint32_t j = 0; j < PW; j++) mycount += (uint32_t)__popcll(bmap[tid * PW + j]);
         uint32_t total;
         const uint32_t excl = block_excl_scan<NT>(mycount, sh_scan, &total);
         sh_tbase[tid] = excl;
         {
             uint32_t rank = excl;
-            for (uint32_t j = 0; j < BW / NT; j++) {
-                const uint32_t wi = tid * (BW / NT) + j;
+            for (uint32_t j = 0; j < PW; j++) {
+                const uint32_t wi = tid * PW + j;
                 uint64_t bits = bmap[wi];
                 while (bits) {
                     const uint32_t b = __ffsll((unsigned long long)bits) - 1;
@@ -921,7 +927,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     // binary searches per read and tile); device-scope atomics on an HBM
     // counter array were tried this round: ~15 cycles per call at L2, 6-9 M
     // cycles on a 500 kb gap -- both ~10x this.
-    if (!hash_ok) {
+    if (!fast) {
         constexpr uint32_t CHB = 14, CH = 1u << CHB, MAXCH = 8191;
         static_assert(CH + 2 * (MAXCH + 1) <= PF_K1_TILE, "chunk counters + chunk offsets fit the tile");
         uint32_t *ccnt = tile, *coff = tile + CH, *cfill = coff + MAXCH + 1;
@@ -1218,7 +1224,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     // sites), which linear probing makes long at high load
     uint32_t HS = 1;
     while (HS < S * 4) HS <<= 1;
-    const bool use_hash = staged && hash_ok && arr_b + 4u * HS + 16u * PF_K12_WB * PF_K12_CAPW <= 4u * PF_K1_TILE;
+    const bool use_hash = staged && fast && arr_b + 4u * HS + 16u * PF_K12_WB * PF_K12_CAPW <= 4u * PF_K1_TILE;
     uint32_t *hst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(tile) + arr_b);
     if (use_hash) {
         for (uint32_t j = tid; j < HS; j += NT) hst[j] = PF_NONE;

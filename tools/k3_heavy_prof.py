@@ -155,19 +155,19 @@ kt12 = kt.get("pf_k12_sites_methmers", 0.0)
 if kt12:
     print(f"  K12 {kt12:.3f} ms; sum of window cycles / (ms x 2.4 GHz) = "
           f"{tot12.sum() / (kt12 * 1e-3 * 2.4e9):.0f} windows at once on average (256 CUs)")
-# the sites phase by path: k12[:, 0] is the dense path's cycles (0: the hash path)
+# the sites phase by path: k12[:, 0] is the dense path's cycles (0: the fast path)
 dense = k12[:, 0] > 0
 rw = np.diff(aln.win_rec_off.astype(np.int64))
-for lab, sel in (("hash path", ~dense), ("dense path", dense)):
+for lab, sel in (("fast path", ~dense), ("dense path", dense)):
     if sel.any():
         print(f"  sites phase, {lab}: {int(sel.sum())} windows, cycles mean {k12[sel, 2].mean():.0f} "
               f"p50 {np.median(k12[sel, 2]):.0f} max {k12[sel, 2].max():.0f}; share of all sites cycles "
               f"{k12[sel, 2].sum() / k12[:, 2].sum():.2f}; records p50 {np.median(rw[sel]):.0f}; "
               f"methmers phase mean {k12[sel, 6].mean():.0f}")
-# sites-phase cycles per record (hash path): how they scale
+# sites-phase cycles per record (fast path): how they scale
 if (~dense).any():
     cpr = k12[~dense, 2] / np.maximum(rw[~dense], 1)
-    print(f"  hash-path sites cycles per record: p10 {np.percentile(cpr, 10):.0f} p50 {np.median(cpr):.0f} "
+    print(f"  fast-path sites cycles per record: p10 {np.percentile(cpr, 10):.0f} p50 {np.median(cpr):.0f} "
           f"p90 {np.percentile(cpr, 90):.0f}")
 k2n = ["lb + ranges", "chars", "entries", "emission", "calls: flags+sites", "core tails", "loop back-edge"]
 print("  K12 methmer phase, wave 0, cycles summed over its reads: mean over windows")
