@@ -793,6 +793,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     uint64_t *bmap = reinterpret_cast<uint64_t *>(tile + PF_K1_TILE / 2);
     const bool range_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64 && !d.k12_dense;
     bool fast = false;
+    [[maybe_unused]] uint32_t rep_seen = 0;             // the profile's dense-path reason
     // the window's calls are one contiguous run: flat passes, four
     // independent (cat, pos) loads in flight per thread
     const uint64_t C0 = d.read_call_off[r0], C1 = d.read_call_off[r0 + R];
@@ -832,6 +833,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
 #pragma unroll
         for (uint32_t j = 0; j < PW; j++) rep += (uint32_t)__popcll(bmap[tid * PW + j]);
         const uint32_t rep_ex = block_excl_scan<NT>(rep, sh_scan, &rep_tot);
+        rep_seen = rep_tot;
         if (rep_tot <= RMAX) {
             // over the freed once-bitmap: each word's rank base (u16), then the
             // counters (meth in the low half, unmeth in the high half)
@@ -1070,7 +1072,13 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
             }
         }
 #ifdef PF_K3_PROFILE
-        if (tid == 0) d.prof[64ull * d.W + (uint64_t)w * 16] = k3_stamp_now() - dz0;   // the dense path
+        // the dense path: cycles | repeated positions << 32 (0: the span was beyond
+        // the bitmap) | span in KiB << 52 | the bitmap's range held << 63
+        if (tid == 0)
+            d.prof[64ull * d.W + (uint64_t)w * 16] = ((k3_stamp_now() - dz0) & 0xFFFFFFFFull) |
+                                                     ((uint64_t)min(rep_seen, 0xFFFFFu) << 32) |
+                                                     ((uint64_t)min((pmax - pmin) >> 10, 0x7FFu) << 52) |
+                                                     ((uint64_t)range_ok << 63);
 #endif
     }
     K12_STAMP(2);

@@ -155,8 +155,20 @@ kt12 = kt.get("pf_k12_sites_methmers", 0.0)
 if kt12:
     print(f"  K12 {kt12:.3f} ms; sum of window cycles / (ms x 2.4 GHz) = "
           f"{tot12.sum() / (kt12 * 1e-3 * 2.4e9):.0f} windows at once on average (256 CUs)")
-# the sites phase by path: k12[:, 0] is the dense path's cycles (0: the fast path)
-dense = k12[:, 0] > 0
+# the sites phase by path: k12[:, 0] packs the dense path's cycles (0: the fast
+# path), its repeated positions (bits 32-51), the span in KiB (52-62) and
+# whether the span fit the bitmap (63)
+d0 = raw[W * 64:].reshape(W, 16)[:, 0].astype(np.uint64)
+dense = d0 > 0
+k12[:, 0] = (d0 & np.uint64(0xFFFFFFFF)).astype(float)
+if dense.any():
+    rep = ((d0 >> np.uint64(32)) & np.uint64(0xFFFFF)).astype(np.int64)[dense]
+    spk = ((d0 >> np.uint64(52)) & np.uint64(0x7FF)).astype(np.int64)[dense]
+    inr = (d0 >> np.uint64(63)).astype(bool)[dense]
+    print(f"  dense windows: {int(inr.sum())} within the bitmap's span (repeated positions p50 "
+          f"{int(np.median(rep[inr])) if inr.any() else 0}, min {int(rep[inr].min()) if inr.any() else 0}), "
+          f"{int((~inr).sum())} beyond it (span KiB p50 {int(np.median(spk[~inr])) if (~inr).any() else 0}, "
+          f"min {int(spk[~inr].min()) if (~inr).any() else 0}, max {int(spk[~inr].max()) if (~inr).any() else 0})")
 rw = np.diff(aln.win_rec_off.astype(np.int64))
 for lab, sel in (("fast path", ~dense), ("dense path", dense)):
     if sel.any():
