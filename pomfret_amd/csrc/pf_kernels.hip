@@ -731,7 +731,6 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     __shared__ uint32_t tile[PF_K1_TILE];
     __shared__ uint32_t sh_scan[PF_K1_THREADS / 64 + 1];
     __shared__ uint32_t sh_misc[8];
-    __shared__ uint32_t sh_tbase[PF_K1_THREADS];
     __shared__ unsigned long long sh_base[2];
     constexpr uint32_t NT = PF_K1_THREADS, NW = NT / 64;
     // windows heaviest first (k12_order): the big windows of a gap mix start
@@ -784,15 +783,19 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     __syncthreads();
 
     // ---- fast path: a bitmap of the positions with >= 2 meth/unmeth calls over
-    // [pmin, pmin + 64*BW), one counter per such position indexed by its rank
-    // among them (a prefix popcount: no hash, no probing), then the bitmap of
-    // qualifying positions, whose prefix popcount is a site's index, so no
-    // sort is needed.
-    constexpr uint32_t BW = 8192, RMAX = 12288;
+    // a segment [base, base + 64*BW) of the window's positions, one counter per
+    // such position indexed by its rank among them (a prefix popcount: no
+    // hash, no probing), then the bitmap of qualifying positions, whose prefix
+    // popcount is a site's index, so no sort is needed.  A span of up to two
+    // segments (1 Mb; the mix's widest windows span 512-760 kb) takes them one
+    // after the other, each over all of the window's calls, the site ranks
+    // carried in position order.
+    constexpr uint32_t BW = 8192, RMAX = 12288, SEGB = BW * 64, MAXSEG = 2;
     static_assert(BW / 2 + RMAX <= PF_K1_TILE / 2, "word ranks + counters fit the first half of the tile");
     uint64_t *bmap = reinterpret_cast<uint64_t *>(tile + PF_K1_TILE / 2);
-    const bool range_ok = (uint64_t)(pmax - pmin) < (uint64_t)BW * 64 && !d.k12_dense;
-    bool fast = false;
+    const uint32_t nseg = d.k12_dense ? 0u : (uint32_t)min<uint64_t>(((uint64_t)(pmax - pmin) + SEGB) / SEGB, MAXSEG + 1);
+    const bool range_ok = nseg >= 1 && nseg <= MAXSEG;
+    bool fast = range_ok;
     [[maybe_unused]] uint32_t rep_seen = 0;             // the profile's dense-path reason
     // the window's calls are one contiguous run: flat passes, four
     // independent (cat, pos) loads in flight per thread
@@ -802,7 +805,8 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     // Pass B counts only those.  Sequencing errors put CpG calls at positions
     // that one read alone covers; with real reads they outnumber the sites, and
     // filtering them keeps the counters few.
-    if (range_ok) {
+    for (uint32_t seg = 0; fast && seg < nseg; seg++) {
+        const uint32_t base = pmin + seg * SEGB;
         {
             uint64_t *once = reinterpret_cast<uint64_t *>(tile);   // the first half of the tile
             for (uint32_t j = tid; j < BW; j += NT) { once[j] = 0; bmap[j] = 0; }
@@ -818,8 +822,8 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
-                    if (cat4[u] >= 2) continue;
-                    const uint32_t o = pos4[u] - pmin;
+                    const uint32_t o = pos4[u] - base;
+                    if (cat4[u] >= 2 || o >= SEGB) continue;
                     const unsigned long long bit = 1ull << (o & 63);
                     if (atomicOr((unsigned long long *)&once[o >> 6], bit) & bit)
                         atomicOr((unsigned long long *)&bmap[o >> 6], bit);
@@ -833,89 +837,92 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
 #pragma unroll
         for (uint32_t j = 0; j < PW; j++) rep += (uint32_t)__popcll(bmap[tid * PW + j]);
         const uint32_t rep_ex = block_excl_scan<NT>(rep, sh_scan, &rep_tot);
-        rep_seen = rep_tot;
-        if (rep_tot <= RMAX) {
-            // over the freed once-bitmap: each word's rank base (u16), then the
-            // counters (meth in the low half, unmeth in the high half)
-            uint16_t *wrank = reinterpret_cast<uint16_t *>(tile);
-            uint32_t *rcnt = tile + BW / 2;
-            {
-                uint32_t rk = rep_ex;
-#pragma unroll
-                for (uint32_t j = 0; j < PW; j++) {
-                    const uint32_t wi = tid * PW + j;
-                    wrank[wi] = (uint16_t)rk;
-                    rk += (uint32_t)__popcll(bmap[wi]);
-                }
-            }
-            for (uint32_t j = tid; j < rep_tot; j += NT) rcnt[j] = 0;
-            __syncthreads();
-            for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
-                uint32_t cat4[4], pos4[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint64_t c = cb + (uint64_t)u * NT;
-                    const bool ok = c < C1;
-                    cat4[u] = ok ? d.call_cat[c] : 2u;
-                    pos4[u] = ok ? d.call_pos[c] : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    if (cat4[u] >= 2) continue;
-                    const uint32_t o = pos4[u] - pmin;
-                    const uint64_t bits = bmap[o >> 6];
-                    const uint64_t below = (1ull << (o & 63)) - 1ull;
-                    if (!((bits >> (o & 63)) & 1ull)) continue;
-                    const uint32_t ix = (uint32_t)wrank[o >> 6] + (uint32_t)__popcll(bits & below);
-                    atomicAdd(&rcnt[ix], cat4[u] == 0 ? 1u : 0x10000u);
-                }
-            }
-            __syncthreads();
-            // bmap becomes the qualifying bitmap, each thread over its own words
-            // counts are uint16 holding count<<4 in the reference: count mod 4096 (blockjoin.c:3236)
-            {
-                uint32_t rk = rep_ex;
-#pragma unroll
-                for (uint32_t j = 0; j < PW; j++) {
-                    const uint32_t wi = tid * PW + j;
-                    uint64_t bits = bmap[wi], q = 0;
-                    while (bits) {
-                        const uint32_t b = (uint32_t)__ffsll((unsigned long long)bits) - 1;
-                        bits &= bits - 1;
-                        const uint32_t v = rcnt[rk++];
-                        if ((int)(v & 4095u) >= cov && (int)((v >> 16) & 4095u) >= cov) q |= 1ull << b;
-                    }
-                    bmap[wi] = q;
-                }
-            }
-            __syncthreads();
-            fast = true;
+        rep_seen = rep_tot > rep_seen ? rep_tot : rep_seen;
+        if (rep_tot > RMAX) {
+            fast = false;                                // uniform: a block-wide total
+            break;
         }
-    }
-    if (fast) {
-        constexpr uint32_t PW = BW / NT;
-        uint32_t mycount = 0;
+        // over the freed once-bitmap: each word's rank base (u16), then the
+        // counters (meth in the low half, unmeth in the high half)
+        uint16_t *wrank = reinterpret_cast<uint16_t *>(tile);
+        uint32_t *rcnt = tile + BW / 2;
+        {
+            uint32_t rk = rep_ex;
 #pragma unroll
-        for (uint32_t j = 0; j < PW; j++) mycount += (uint32_t)__popcll(bmap[tid * PW + j]);
+            for (uint32_t j = 0; j < PW; j++) {
+                const uint32_t wi = tid * PW + j;
+                wrank[wi] = (uint16_t)rk;
+                rk += (uint32_t)__popcll(bmap[wi]);
+            }
+        }
+        for (uint32_t j = tid; j < rep_tot; j += NT) rcnt[j] = 0;
+        __syncthreads();
+        for (uint64_t cb = C0 + tid; cb < C1; cb += 4ull * NT) {
+            uint32_t cat4[4], pos4[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint64_t c = cb + (uint64_t)u * NT;
+                const bool ok = c < C1;
+                cat4[u] = ok ? d.call_cat[c] : 2u;
+                pos4[u] = ok ? d.call_pos[c] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t o = pos4[u] - base;
+                if (cat4[u] >= 2 || o >= SEGB) continue;
+                const uint64_t bits = bmap[o >> 6];
+                const uint64_t below = (1ull << (o & 63)) - 1ull;
+                if (!((bits >> (o & 63)) & 1ull)) continue;
+                const uint32_t ix = (uint32_t)wrank[o >> 6] + (uint32_t)__popcll(bits & below);
+                atomicAdd(&rcnt[ix], cat4[u] == 0 ? 1u : 0x10000u);
+            }
+        }
+        __syncthreads();
+        // bmap becomes the qualifying bitmap, each thread over its own words
+        // counts are uint16 holding count<<4 in the reference: count mod 4096 (blockjoin.c:3236)
+        uint32_t mycount = 0;
+        {
+            uint32_t rk = rep_ex;
+#pragma unroll
+            for (uint32_t j = 0; j < PW; j++) {
+                const uint32_t wi = tid * PW + j;
+                uint64_t bits = bmap[wi], q = 0;
+                while (bits) {
+                    const uint32_t b = (uint32_t)__ffsll((unsigned long long)bits) - 1;
+                    bits &= bits - 1;
+                    const uint32_t v = rcnt[rk++];
+                    if ((int)(v & 4095u) >= cov && (int)((v >> 16) & 4095u) >= cov) q |= 1ull << b;
+                }
+                bmap[wi] = q;
+                mycount += (uint32_t)__popcll(q);
+            }
+        }
+        // the segment's sites, ranked after the earlier segments'
         uint32_t total;
         const uint32_t excl = block_excl_scan<NT>(mycount, sh_scan, &total);
-        sh_tbase[tid] = excl;
+        const uint32_t carry = sh_misc[4];
         {
-            uint32_t rank = excl;
+            uint32_t rank = carry + excl;
             for (uint32_t j = 0; j < PW; j++) {
                 const uint32_t wi = tid * PW + j;
                 uint64_t bits = bmap[wi];
                 while (bits) {
                     const uint32_t b = __ffsll((unsigned long long)bits) - 1;
                     bits &= bits - 1;
-                    if (rank < scap) d.site_pos[sb + rank] = pmin + wi * 64 + b;
+                    if (rank < scap) d.site_pos[sb + rank] = base + wi * 64 + b;
                     else atomicOr(d.status, PF_ST_SITE_OVF);
                     rank++;
                 }
             }
         }
         __syncthreads();
-        if (tid == 0) sh_misc[4] = total;
+        if (tid == 0) sh_misc[4] = carry + total;
+        __syncthreads();
+    }
+    if (range_ok && !fast) {
+        // a segment had too many repeated positions: the dense path restarts
+        // the window's sites from rank 0
+        if (tid == 0) sh_misc[4] = 0;
         __syncthreads();
     }
     // ---- general path (a position range beyond the bitmaps, or more repeated
@@ -1232,7 +1239,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     // sites), which linear probing makes long at high load
     uint32_t HS = 1;
     while (HS < S * 4) HS <<= 1;
-    const bool use_hash = staged && fast && arr_b + 4u * HS + 16u * PF_K12_WB * PF_K12_CAPW <= 4u * PF_K1_TILE;
+    const bool use_hash = staged && fast && nseg == 1 && arr_b + 4u * HS + 16u * PF_K12_WB * PF_K12_CAPW <= 4u * PF_K1_TILE;
     uint32_t *hst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(tile) + arr_b);
     if (use_hash) {
         for (uint32_t j = tid; j < HS; j += NT) hst[j] = PF_NONE;
