@@ -647,7 +647,7 @@ __global__ __launch_bounds__(PF_K2_WAVES * 64) void pf_k2_methmers(pf_dev_batch 
 DEV void k12_methmers(const pf_dev_batch &d, uint32_t r0, uint32_t i0, uint32_t i1, uint32_t wid, uint32_t NW,
                       uint32_t lane, uint32_t S, const uint32_t *sp, const uint32_t *st1, const uint32_t *q1s,
                       const uint8_t *l0s, const uint8_t *l1s, const K2SiteHash &hsd, bool use_hash, uint8_t *wb,
-                      unsigned long long *k2acc) {
+                      unsigned long long *k2acc, uint32_t *rctr) {
         uint8_t *chars = wb, *crank = wb + PF_K12_CAPW;
         uint16_t *irank = reinterpret_cast<uint16_t *>(wb + 2 * PF_K12_CAPW);
         uint32_t *kst = reinterpret_cast<uint32_t *>(wb + 4 * PF_K12_CAPW);
@@ -659,16 +659,25 @@ DEV void k12_methmers(const pf_dev_batch &d, uint32_t r0, uint32_t i0, uint32_t 
         // calls have been consumed, just before read i+2's are issued.
         uint32_t pend_n = 0;
         uint64_t pend_off = 0;
-        // software pipeline over this wave's reads i, i+NW, ...: the scalars of
-        // read i+2NW and the calls of read i+NW are in flight while read i is
-        // processed
+        // software pipeline over this wave's reads: the scalars of the read
+        // after next and the calls of the next read are in flight while a read
+        // is processed.  A wave's first read is i0 + wid; later ones are taken
+        // from the workgroup's counter (*rctr, set to i0 + NW by the caller),
+        // one read ahead, so that the waves finish together however the
+        // reads' lengths fall (round-robin left the window to its slowest wave)
+        auto take = [&]() -> uint32_t {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(rctr, 1u);
+            return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        };
         K2Read rdA, rdB;
         uint32_t pA[K2_CR], tA[K2_CR], pB[K2_CR], tB[K2_CR];
         const uint32_t iw = i0 + wid;
+        uint32_t iB = iw < i1 ? take() : i1;
         if (iw < i1) k2_load_scalars(d, r0 + iw, rdA);
-        if (iw + NW < i1) k2_load_scalars(d, r0 + iw + NW, rdB);
+        if (iB < i1) k2_load_scalars(d, r0 + iB, rdB);
         k2_issue_calls(d, iw < i1 ? rdA : K2Read{0, 0, 0, 0, 0, 0}, lane, pA, tA);
-        for (uint32_t i = iw; i < i1; i += NW) {
+        for (uint32_t i = iw; i < i1;) {
             const uint32_t r = r0 + i;
             K2_STAMP(6);
             K2Read rd = rdA;
@@ -692,8 +701,9 @@ DEV void k12_methmers(const pf_dev_batch &d, uint32_t r0, uint32_t i0, uint32_t 
             k2_flush(d, kst, pend_off, pend_n, lane);
             pend_n = 0;
             K2Read rdC = {0, 0, 0, 0, 0, 0};
-            if (i + 2 * NW < i1) k2_load_scalars(d, r0 + i + 2 * NW, rdC);
-            k2_issue_calls(d, i + NW < i1 ? rdB : K2Read{0, 0, 0, 0, 0, 0}, lane, pB, tB);
+            const uint32_t iC = iB < i1 ? take() : i1;
+            if (iC < i1) k2_load_scalars(d, r0 + iC, rdC);
+            k2_issue_calls(d, iB < i1 ? rdB : K2Read{0, 0, 0, 0, 0, 0}, lane, pB, tB);
             K2_STAMP(8);
             if (rd.cap > d.k12_capw) {
                 if (lane == 0) d.fb_list[atomicAdd(d.fb_ctr, 1u)] = r;
@@ -716,6 +726,8 @@ DEV void k12_methmers(const pf_dev_batch &d, uint32_t r0, uint32_t i0, uint32_t 
             }
             rdA = rdB;
             rdB = rdC;
+            i = iB;
+            iB = iC;
 #pragma unroll
             for (int u = 0; u < K2_CR; u++) { pA[u] = pB[u]; tA[u] = tB[u]; }
             K2_STAMP(7);
@@ -1241,6 +1253,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     while (HS < S * 4) HS <<= 1;
     const bool use_hash = staged && fast && nseg == 1 && arr_b + 4u * HS + 16u * PF_K12_WB * PF_K12_CAPW <= 4u * PF_K1_TILE;
     uint32_t *hst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(tile) + arr_b);
+    if (tid == 0) sh_misc[5] = NW;                       // the methmer phase's read counter
     if (use_hash) {
         for (uint32_t j = tid; j < HS; j += NT) hst[j] = PF_NONE;
         __syncthreads();
@@ -1276,7 +1289,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
 #else
         unsigned long long *k2acc = nullptr;
 #endif
-        k12_methmers(d, r0, 0, R, wid, NW, lane, S, sp, st1, q1s, l0s, l1s, hsd, use_hash, wb, k2acc);
+        k12_methmers(d, r0, 0, R, wid, NW, lane, S, sp, st1, q1s, l0s, l1s, hsd, use_hash, wb, k2acc, &sh_misc[5]);
 #ifdef PF_K3_PROFILE
         if (tid == 0) {
             for (int j = 0; j < 7; j++) d.prof[64ull * d.W + (uint64_t)w * 16 + 8 + j] = k2a[j];
@@ -1300,7 +1313,7 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
 // windows do.
 __global__ __launch_bounds__(PF_K12C_WAVES * 64) void pf_k12_chunks(pf_dev_batch d) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ uint32_t s_item;
+    __shared__ uint32_t s_item, s_rctr;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t n = *d.k12c_ctr;
     for (;;) {
@@ -1309,6 +1322,7 @@ __global__ __launch_bounds__(PF_K12C_WAVES * 64) void pf_k12_chunks(pf_dev_batch
         const uint32_t it = s_item;
         if (it >= n) break;
         const uint32_t w = d.k12c_list[2ull * it], c0 = d.k12c_list[2ull * it + 1];
+        if (tid == 0) s_rctr = c0 + PF_K12C_WAVES;
         const uint32_t r0 = d.win_read_off[w], R = d.win_read_off[w + 1] - r0;
         const uint32_t S = d.win_S[w];
         const uint64_t sb = d.win_site_off[w];
@@ -1327,7 +1341,8 @@ __global__ __launch_bounds__(PF_K12C_WAVES * 64) void pf_k12_chunks(pf_dev_batch
         K2SiteHash hsd;
         hsd.t = nullptr; hsd.mask = 0; hsd.pmin = 0;
         const uint32_t c1 = min(R, c0 + PF_K12C_READS);
-        k12_methmers(d, r0, c0, c1, wid, PF_K12C_WAVES, lane, S, sp, st1, q1s, l0s, l1s, hsd, false, wb, nullptr);
+        k12_methmers(d, r0, c0, c1, wid, PF_K12C_WAVES, lane, S, sp, st1, q1s, l0s, l1s, hsd, false, wb, nullptr,
+                     &s_rctr);
         __syncthreads();                                 // the site arrays are reused by the next item
     }
 }
