@@ -29,6 +29,7 @@ __global__ void pf_k3_greedy(pf_dev_batch d);
 __global__ void pf_k3_wave(pf_dev_batch d);
 __global__ void pf_k3_fallback(pf_dev_batch d);
 __global__ void pf_k3_heavy(pf_dev_batch d);
+__global__ void pf_k3_kdict(pf_dev_batch d);
 __global__ void pf_k0_load(pf_load_dev d);
 __global__ void pf_k0_multi(pf_load_dev d);
 __global__ void pf_k0_scan(pf_load_dev d);
@@ -436,7 +437,9 @@ extern "C" int pf_batch_upload(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_wind
     if (!ctx || !cfg || !in || !out) return PF_ERR_ARG;
     *out = nullptr;
     if (cfg->k < 1 || cfg->k_span < 0) return PF_ERR_ARG;
-    if (cfg->k > 5) return PF_ERR_UNSUPPORTED;     // slot dictionary: 4^k keys per site
+    // k <= 15: the reference's limit (2-bit methmer characters in a u32 and
+    // `char mmr[16]`, cli.c:243, blockjoin.c:3186-3194, 3403)
+    if (cfg->k > 15) return PF_ERR_UNSUPPORTED;
     const uint32_t W = in->n_windows, R = in->n_reads;
     const uint64_t N = in->n_calls;
     if (W && (!in->win_start || !in->win_end || !in->win_read_off)) return PF_ERR_ARG;
@@ -569,7 +572,13 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     d.W = W; d.R = R; d.N = N;
     d.k = cfg->k; d.k_span = cfg->k_span;
     d.hard_cov = cfg->hard_cov > 0 ? cfg->hard_cov : 15;
-    d.mw = mask_words(cfg->k);
+    // k > 5: per-site hash tables (pf_k3_kdict) instead of 4^k-bit masks;
+    // PF_K3_KDICT=1 takes them at any k (tests: the same slots)
+    {
+        const char *kd = getenv("PF_K3_KDICT");
+        d.kdict = cfg->k > 5 || (kd && atoi(kd) == 1) ? 1u : 0u;
+    }
+    d.mw = d.kdict ? 0 : mask_words(cfg->k);
     int rc = 0;
 #define PUT(field, src, n) do { rc = dev_put(b, &field, src, n); if (rc) return fail(rc); } while (0)
 #define ALLOC(field, n) do { rc = dev_alloc(b, &field, n); if (rc) return fail(rc); } while (0)
@@ -644,6 +653,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     ALLOC(d.fb_list, std::max<uint32_t>(R, 1));
     ALLOC(d.k12c_list, 2ull * (R / PF_K12C_READS + W + 1));
     ALLOC(d.k3_fb_list, std::max<uint32_t>(4 * W, 1));       // the main kernel's deferrals, then pf_k3_heavy's
+    ALLOC(d.k3_ntot, std::max<uint32_t>(2 * W, 1));
     // one I/O block: the counters zeroed before a run (status, arena
     // counters, fallback counter) followed by everything copied back after it,
     // so a step costs one memset and one D2H copy
@@ -815,7 +825,7 @@ extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cf
     if (!ctx || !cfg || !lc || !a || !fill || !out) return PF_ERR_ARG;
     *out = nullptr;
     if (cfg->k < 1 || cfg->k_span < 0) return PF_ERR_ARG;
-    if (cfg->k > 5) return PF_ERR_UNSUPPORTED;
+    if (cfg->k > 15) return PF_ERR_UNSUPPORTED;     // as pf_batch_upload
     const uint32_t W = a->n_windows, n = a->n_recs;
     if (W && (!a->win_start || !a->win_end || !a->win_rec_off)) return PF_ERR_ARG;
     if (W && (a->win_rec_off[0] != 0 || a->win_rec_off[W] != n)) return PF_ERR_ARG;
@@ -1213,6 +1223,11 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     const uint32_t g2 = (uint32_t)std::min<uint64_t>((waves + PF_K2_WAVES - 1) / PF_K2_WAVES, 512);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
+    // k > 5: the slot dictionaries, one workgroup per problem (timed with K2)
+    if (d.kdict && b->W) {
+        hipLaunchKernelGGL(pf_k3_kdict, dim3(2 * b->W), dim3(PF_K3_THREADS), 0, st, d);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(b->ev[slot][5], st));
     if (stages < 3) return PF_OK;
     // main greedy kernel: the 256-thread workgroup build; PF_K3_IMPL=wave runs

@@ -98,6 +98,7 @@ static int bgzf_read_raw(bgzf_t *z, uint64_t addr, uint8_t *h, uint32_t *xlen_ou
  * PF_HOST_ZLIB set, blocks go through zlib.  Both decode the same bytes. */
 typedef struct {
     void *(*alloc)(void);
+    void (*free)(void *);
     int (*decompress)(void *, const void *, size_t, void *, size_t, size_t *);
     uint32_t (*crc)(uint32_t, const void *, size_t);
 } ldf_t;
@@ -110,7 +111,7 @@ static void ldf_init(void) {
     void *L = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
     if (!L) return;
     void (*fr)(void *) = (void (*)(void *))dlsym(L, "libdeflate_free_decompressor");
-    ldf_t t = {(void *(*)(void))dlsym(L, "libdeflate_alloc_decompressor"),
+    ldf_t t = {(void *(*)(void))dlsym(L, "libdeflate_alloc_decompressor"), fr,
                (int (*)(void *, const void *, size_t, void *, size_t, size_t *))dlsym(L, "libdeflate_deflate_decompress"),
                (uint32_t (*)(uint32_t, const void *, size_t))dlsym(L, "libdeflate_crc32")};
     if (!fr || !t.alloc || !t.decompress || !t.crc || pthread_key_create(&g_ldf_key, fr)) return;
@@ -122,7 +123,10 @@ static void *ldf_dec(void) {
     pthread_once(&g_ldf_once, ldf_init);
     if (!g_ldf.alloc) return NULL;
     void *d = pthread_getspecific(g_ldf_key);
-    if (!d && (d = g_ldf.alloc()) != NULL && pthread_setspecific(g_ldf_key, d)) return NULL;
+    if (!d && (d = g_ldf.alloc()) != NULL && pthread_setspecific(g_ldf_key, d)) {
+        g_ldf.free(d);                        /* not registered: this thread decodes through zlib */
+        return NULL;
+    }
     return d;
 }
 

@@ -97,6 +97,11 @@ struct pf_dev_batch {
     uint32_t k3_mode;                  /* test override: 0 exact pick, 1 always fold, 2 chunked record rows */
     uint32_t k3_cache;                 /* 1: candidate slot-list cache when a window's lists miss LDS (PF_K3_CACHE=0: off) */
     uint32_t k3_gcnt;                  /* 1: path 6 (cache + count table in HBM) for every cache problem (PF_K3_GCNT=force) */
+    /* k > 5 (or PF_K3_KDICT=1): the slot dictionary is built by pf_k3_kdict
+     * before the greedy kernels (per-site hash tables in HBM scratch instead
+     * of 4^k-bit masks), which rewrite no keys and read ntot from k3_ntot */
+    uint32_t kdict;
+    uint32_t *k3_ntot;                 /* [2W] slots of each problem (kdict) */
 };
 
 #endif

@@ -1467,6 +1467,136 @@ DEV void k3_dict_rewrite(const pf_dev_batch &d, uint32_t r0, uint32_t R, uint32_
     __syncthreads();
 }
 
+// ---- k > 5: the slot dictionary from per-site hash tables (pf_k3_kdict).
+// insert_mmrs_to_counts (blockjoin.c:3453-3486) keeps, per site, a linear list
+// of the distinct methmer keys it has seen, and query_counts_of_mmrs
+// (3669-3691) searches it; the greedy kernels index the counts by a dense
+// slot id per (site, key) instead.  For k <= 5 k3_dict numbers the slots from
+// a 4^k-bit mask per site.  Past that the masks outgrow any memory (4^15 bits
+// a site at the reference's documented maximum, cli.c:243), so this kernel --
+// one workgroup per problem, launched before the greedy kernels -- gives each
+// site an open-addressing table of 2^ceil(log2(2 cov)) keys in HBM scratch
+// (cov: the methmers at the site, <= half full), ranks each site's distinct
+// keys, and rewrites every key into base[site] + its rank: the numbering the
+// masks give, so both dictionaries yield the same slots (PF_K3_KDICT=1 forces
+// this one at any k; tests compare the two).  The greedy kernels then skip
+// their dictionary phase and read the problem's slot count from k3_ntot.
+DEV uint32_t kd_hash(uint32_t key) {
+    const uint32_t h = key * 0x9E3779B1u;
+    return h ^ (h >> 15);
+}
+DEV void kd_sync() {                    // HBM tables written by other waves of the workgroup
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__global__ __launch_bounds__(PF_K3_THREADS) void pf_k3_kdict(pf_dev_batch d) {
+    constexpr uint32_t NT = PF_K3_THREADS, NW = NT / 64;
+    __shared__ uint32_t sh_scan[NW + 1];
+    __shared__ unsigned long long s_o;
+    __shared__ uint32_t s_fail;
+    const uint32_t prob = blockIdx.x, w = prob >> 1, dir = prob & 1;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t S = d.win_S[w];
+    if (S == 0) {
+        if (tid == 0) d.k3_ntot[prob] = 0;
+        return;
+    }
+    const uint32_t R = d.win_nreads[w], r0 = d.win_read_off[w];
+    auto alloc = [&](uint64_t bytes) -> bool {     // workgroup-uniform scratch allocation
+        if (tid == 0) {
+            const unsigned long long o = atomicAdd(d.scr_ctr, (unsigned long long)bytes);
+            s_fail = o + bytes > d.scr_cap;
+            if (s_fail) atomicOr(d.status, PF_ST_SCR_OVF);   // the host grows the scratch and re-runs
+            s_o = o;
+        }
+        __syncthreads();
+        return s_fail == 0;
+    };
+    // per site: the methmer coverage (a difference array first), then the
+    // table's capacity; its table offset; its distinct keys, then its base
+    if (!alloc(align16(12ull * (S + 1)))) { if (tid == 0) d.k3_ntot[prob] = PF_NONE; return; }
+    uint32_t *cap = reinterpret_cast<uint32_t *>(d.scr + s_o), *toff = cap + (S + 1), *base = toff + (S + 1);
+    for (uint32_t j = tid; j <= S; j += NT) cap[j] = 0;
+    kd_sync();
+    for (uint32_t i = tid; i < R; i += NT) {
+        const uint64_t g = 2ull * (r0 + i) + dir;
+        const uint32_t n = d.mmr_n[g], st = d.mmr_start[g];
+        if (n && st < S) {
+            atomicAdd(&cap[st], 1u);
+            atomicAdd(&cap[st + n < S ? st + n : S], 0xFFFFFFFFu);
+        }
+    }
+    kd_sync();
+    // contiguous runs of sites per thread: coverage, capacity, table offsets
+    const uint32_t per = (S + NT - 1) / NT, j0 = min(tid * per, S), j1 = min(j0 + per, S);
+    uint32_t part = 0, tot = 0;
+    for (uint32_t j = j0; j < j1; j++) part += cap[j];
+    uint32_t run = block_excl_scan<NT>(part, sh_scan, &tot), csum = 0;
+    for (uint32_t j = j0; j < j1; j++) {
+        run += cap[j];
+        const uint32_t c = run ? 1u << (32 - __builtin_clz(2u * run - 1u)) : 0u;   // >= 2 cov, a power of 2
+        cap[j] = c;
+        csum += c;
+    }
+    uint32_t T = 0;
+    uint32_t o = block_excl_scan<NT>(csum, sh_scan, &T);
+    for (uint32_t j = j0; j < j1; j++) { toff[j] = o; o += cap[j]; }
+    if (!alloc(align16(8ull * T))) { if (tid == 0) d.k3_ntot[prob] = PF_NONE; return; }   // keys not rewritten
+    uint32_t *tbl = reinterpret_cast<uint32_t *>(d.scr + s_o), *rk = tbl + T;   // key + 1 (0: empty), rank
+    for (uint32_t j = tid; j < T; j += NT) tbl[j] = 0;
+    kd_sync();
+    k3_each_key<NT>(d, r0, R, dir, [](uint32_t) { return true; },
+                    [&](uint32_t, uint32_t, uint32_t site, uint64_t, uint32_t key) {
+                        if (site >= S) return;
+                        const uint32_t m = cap[site] - 1u, ob = toff[site];
+                        for (uint32_t h = kd_hash(key) & m;; h = (h + 1u) & m) {
+                            const uint32_t prev = atomicCAS(&tbl[ob + h], 0u, key + 1u);
+                            if (prev == 0u || prev == key + 1u) break;
+                        }
+                    });
+    kd_sync();
+    // one wave per site: each distinct key's rank among the site's keys
+    for (uint32_t s = wid; s < S; s += NW) {
+        const uint32_t c = cap[s], ob = toff[s];
+        uint32_t nd = 0;
+        for (uint32_t a0 = 0; a0 < c; a0 += 64) {
+            const uint32_t v = a0 + lane < c ? tbl[ob + a0 + lane] : 0u;
+            uint32_t r = 0;
+            for (uint32_t b0 = 0; b0 < c; b0 += 64) {
+                const uint32_t u = b0 + lane < c ? tbl[ob + b0 + lane] : 0u;
+                for (uint64_t m = __ballot(u != 0u); m; m &= m - 1) {
+                    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)u, __builtin_ctzll(m));
+                    r += x < v ? 1u : 0u;
+                }
+            }
+            if (v) rk[ob + a0 + lane] = r;
+            nd += (uint32_t)__popcll(__ballot(v != 0u));
+        }
+        if (lane == 0) base[s] = nd;
+    }
+    kd_sync();
+    part = 0;
+    for (uint32_t j = j0; j < j1; j++) part += base[j];
+    uint32_t ntot = 0;
+    run = block_excl_scan<NT>(part, sh_scan, &ntot);
+    for (uint32_t j = j0; j < j1; j++) { const uint32_t x = base[j]; base[j] = run; run += x; }
+    if (tid == 0) d.k3_ntot[prob] = ntot;
+    kd_sync();
+    k3_each_key<NT>(d, r0, R, dir, [](uint32_t) { return true; },
+                    [&](uint32_t, uint32_t, uint32_t site, uint64_t koff, uint32_t key) {
+                        uint32_t slot = PF_NONE;
+                        if (site < S) {
+                            const uint32_t m = cap[site] - 1u, ob = toff[site];
+                            uint32_t h = kd_hash(key) & m;
+                            while (tbl[ob + h] != key + 1u) h = (h + 1u) & m;   // inserted above: found
+                            slot = base[site] + rk[ob + h];
+                        }
+                        d.keys[koff] = slot;
+                    });
+}
+
 struct K3Mem {
     uint32_t *sum, *cnt, *aux, *mo;
     void *mn, *mst;          // methmers per read, first site index: u16 when m16 (the slim loop: S < 8192), else u32
@@ -3182,8 +3312,9 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     if (tid == 0) ctl.t_run = k3_realtime();
 #endif
 
-    // ---- P1: slot dictionary
-    const uint64_t need1 = align16(8ull * S * MW) + 4ull * S;
+    // ---- P1: slot dictionary (built by pf_k3_kdict when d.kdict)
+    const bool kd = d.kdict != 0u;
+    const uint64_t need1 = kd ? 0ull : align16(8ull * S * MW) + 4ull * S;
     const bool p1_lds = need1 <= lds;
     // the slim loop: register candidate list (n_cand <= 64), exact-interval
     // pick (< 8192 sites), dictionary in LDS
@@ -3215,8 +3346,9 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
         masks = reinterpret_cast<uint64_t *>(g);
         mbase = reinterpret_cast<uint32_t *>(g + align16(8ull * S * MW));
     }
-    k3_dict<NT>(d, r0, R, S, dir, masks, mbase, sh_scan, ctl);
-    const uint32_t ntot = uni(ctl.ntot);
+    if (!kd) k3_dict<NT>(d, r0, R, S, dir, masks, mbase, sh_scan, ctl);
+    const uint32_t ntot = kd ? uni(d.k3_ntot[prob]) : uni(ctl.ntot);
+    if (kd && ntot == PF_NONE) return;               // pf_k3_kdict ran out of scratch: the host re-runs
     // sum of methmers over the window's reads (slot-list size) and the longest list
     uint32_t summ = 0, lmx = 0;
     for (uint32_t i = tid; i < R; i += NT) {
@@ -3304,7 +3436,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
         __syncthreads();
         if (uni(ctl.fail)) return;
     }
-    k3_dict_rewrite<NT>(d, r0, R, S, dir, masks, mbase);
+    if (!kd) k3_dict_rewrite<NT>(d, r0, R, S, dir, masks, mbase);
     const uint32_t *kb = d.keys + kbase;
     if (tid == 0) {
         // 1 slot lists in LDS, 2 the candidate cache, 3 slot lists in HBM (slim loop); 4 the general body;
@@ -4254,7 +4386,7 @@ DEV void k3w_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl
     const uint64_t kbase = d.mmr_off[2ull * r0];
     // the wave build: n_cand <= 64 (register candidate list), < 8192 sites
     // (exact-interval pick), the dictionary in LDS, the exact or fold pick
-    if (d.win_par[w * 4 + 2] > 64 || S >= 8192u || d.k3_mode > 1u || k3w_p1_bytes(S, MW) > lds) {
+    if (d.win_par[w * 4 + 2] > 64 || S >= 8192u || d.k3_mode > 1u || d.kdict || k3w_p1_bytes(S, MW) > lds) {
         k3_defer(d, prob);
         return;
     }

@@ -63,6 +63,25 @@ DEV unsigned long long k0_now() {
 #define K0_T0 do { } while (0)
 #endif
 #define NT_G 4u
+// Out-of-line code (pf_k0_load is ~77 KB inlined, past the 64 KB instruction
+// cache two CUs share): bit 0 the record path of HBM trigger lists (long
+// records), bit 1 the cold paths (SWAR parse, lane-0 walk, implicit chunks)
+#ifndef PF_K0_NOINL
+#define PF_K0_NOINL 0
+#endif
+#if PF_K0_NOINL & 1
+#define DEV_HBM static __device__ __attribute__((noinline))
+#else
+#define DEV_HBM DEV
+#endif
+#if PF_K0_NOINL & 2
+#define DEV_COLD static __device__ __attribute__((noinline))
+#else
+#define DEV_COLD DEV
+#endif
+#ifndef PF_K0_WPE
+#define PF_K0_WPE 8                        // pf_k0_load's waves per SIMD (register budget: 512 / WPE VGPRs)
+#endif
 
 DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 DEV uint64_t lanemask_lt(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -369,7 +388,7 @@ DEV void k0_dw_table(uint32_t *tbl, uint32_t lane) {
 }
 
 template <typename TP>
-DEV bool k0_mm_ranks_swar(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const K0Tgt &t, bool rev, TP TB,
+DEV_COLD bool k0_mm_ranks_swar(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const K0Tgt &t, bool rev, TP TB,
                           uint32_t lane);
 
 template <typename TP>
@@ -453,7 +472,7 @@ DEV bool k0_mm_ranks(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const 
 
 // Per-comma SWAR parse (rounds 1-2): the fallback for counts of 8+ digits.
 template <typename TP>
-DEV bool k0_mm_ranks_swar(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const K0Tgt &t, bool rev, TP TB,
+DEV_COLD bool k0_mm_ranks_swar(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const K0Tgt &t, bool rev, TP TB,
                      uint32_t lane) {
     if (mm[t.th] != ',') return false;
     const uint32_t wend = mis + t.te;
@@ -803,7 +822,7 @@ DEV void k0_emit_lanes(const pf_load_dev &d, K0Out &o, bool keep, uint32_t v, ui
 // Lane 0 walks the record with the reference loop itself (605-792): used for
 // the stale-trigger case of a leading soft clip, and by tests for everything.
 template <int MODE, typename TP>
-DEV void k0_walk_seq(const uint32_t *cig, uint32_t ncig, uint32_t qs, bool rev, TP TB, uint32_t nT,
+DEV_COLD void k0_walk_seq(const uint32_t *cig, uint32_t ncig, uint32_t qs, bool rev, TP TB, uint32_t nT,
                      const uint8_t *seqi, uint32_t len, K0Out &o, bool &fatal) {
     const uint32_t cgoffset = rev ? 0xFFFFFFFFu : 0u;
     uint32_t i_read = 0, i_ref = qs, it = 0;
@@ -886,7 +905,7 @@ DEV uint32_t k0_tlb(TP TB, uint32_t n, uint32_t x) {
 // Explicit triggers with p <= a_end and CpGs in [a_cur, a_end) that the
 // reference's scan visits, merged in push order, then emitted.
 template <int MODE, typename TP>
-DEV void k0_chunk_implicit(const pf_load_dev &d, K0W &L, uint32_t nv, uint32_t c0, uint32_t a_cur, uint32_t a_end,
+DEV_COLD void k0_chunk_implicit(const pf_load_dev &d, K0W &L, uint32_t nv, uint32_t c0, uint32_t a_cur, uint32_t a_end,
                            uint32_t i_ref, uint32_t cgoffset, bool rev, TP TB, uint32_t nT, uint32_t &tc,
                            const uint8_t *seq, uint32_t len, uint32_t lane, K0Out &o) {
     K0Merge &M = L.u.mg;
@@ -1372,6 +1391,12 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     K0_STAMP(3);
 }
 
+// a record whose trigger list is past the wave's LDS list: its HBM slice
+template <bool MULTI>
+DEV_HBM void k0_record_hbm(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, const K0Tgts &T, bool okm) {
+    k0_record<MULTI>(d, L, R, lane, d.scr + R.scr_off, R.scr_len, T, okm);
+}
+
 // One record on the wave: filters, the MM entries, the rest.  The main pass
 // hands a record with several C m entries to pf_k0_multi (rare; its merge
 // would cost the common path registers) and leaves its rec_n to it.
@@ -1415,10 +1440,10 @@ DEV void k0_one(const pf_load_dev &d, K0W &L, uint32_t slot, uint32_t lane) {
         for (uint32_t e = 1; e < T.n; e++) ndsum += k0_tgt_get(T, e).nd;
     if (R.scr_len == 0 || !okm || uni(ndsum) <= (uint32_t)PF_K0_TCAP)
         k0_record<MULTI>(d, L, R, lane, L.T, (uint32_t)PF_K0_TCAP, T, okm);
-    else k0_record<MULTI>(d, L, R, lane, d.scr + R.scr_off, R.scr_len, T, okm);
+    else k0_record_hbm<MULTI>(d, L, R, lane, T, okm);
 }
 
-__global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_load(pf_load_dev d) {
+__global__ __launch_bounds__(PF_K0_WAVES * 64) __attribute__((amdgpu_waves_per_eu(PF_K0_WPE))) void pf_k0_load(pf_load_dev d) {
     __shared__ K0W lds[PF_K0_WAVES];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = uni(threadIdx.x >> 6);

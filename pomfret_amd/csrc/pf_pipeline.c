@@ -1243,31 +1243,11 @@ static int write_report(pf_mp_plan_t *p) {
     return fclose(fo) ? -1 : PF_OK;
 }
 
-static int write_methphase_outputs(pf_mp_plan_t *p) {
-    const size_t L = strlen(p->out_prefix) + 32;
-    char *fn = (char *)malloc(L);
-    if (!fn) return PF_ERR_NOMEM;
-    /* PF_MP_TRACE: the writers' steps on stderr (seconds) */
-    const int trace = getenv("PF_MP_TRACE") != NULL;
-    double tw = now_s();
+/* the rescue of dropped-interval sites (recover_variant_phase_in_dropped_intervals)
+ * and {prefix}.mp.vcf: only with --vcf (4706-4712) */
+static int write_rescued_vcf(pf_mp_plan_t *p, char *fn, size_t L, int trace, double tw) {
+    int rc = 0;
 #define WTRACE(what) do { if (trace) { const double t_ = now_s(); fprintf(stderr, "[writers] %s %.3fs\n", what, t_ - tw); tw = t_; } } while (0)
-    snprintf(fn, L, "%s.mp.gtf", p->out_prefix);
-    int rc = pf_write_gtf(p->gaps, p->blocks, fn);
-    if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] gtf written.\n");
-    if (!rc && p->o.write_tsv) {
-        snprintf(fn, L, "%s.mp.tsv", p->out_prefix);
-        rc = pf_write_tsv(p->gaps, p->blocks, fn);
-        if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] tsv written.\n");
-    }
-    /* -U: {prefix}.mp.input_haptag.tsv (4494-4517), every record of the BAM */
-    if (!rc && p->o.untagged && p->o.write_input_tagging) {
-        snprintf(fn, L, "%s.mp.input_haptag.tsv", p->out_prefix);
-        rc = pf_retag_bam(p->bam_path, NULL, NULL, fn, PF_RETAG_INPUT_HAPTAG, NULL, NULL, NULL, p->raw, -1, NULL);
-    }
-    WTRACE("gtf/tsv/input_haptag");
-    /* the VCF only when --vcf was given (4706) */
-    if (rc || !p->vcf_path) { free(fn); return rc; }
-    /* rescue of dropped-interval sites (recover_variant_phase_in_dropped_intervals) + VCF */
     const uint32_t C = p->n_contigs;
     uint64_t *roff = (uint64_t *)calloc(C + 1, sizeof(uint64_t));
     uint32_t *rpos = NULL;
@@ -1349,6 +1329,36 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
         if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] vcf written.\n");
         WTRACE("vcf");
     }
+    free(roff); free(rpos); free(rhap);
+    return rc;
+#undef WTRACE
+}
+
+static int write_methphase_outputs(pf_mp_plan_t *p) {
+    const size_t L = strlen(p->out_prefix) + 32;
+    char *fn = (char *)malloc(L);
+    if (!fn) return PF_ERR_NOMEM;
+    /* PF_MP_TRACE: the writers' steps on stderr (seconds) */
+    const int trace = getenv("PF_MP_TRACE") != NULL;
+    double tw = now_s();
+#define WTRACE(what) do { if (trace) { const double t_ = now_s(); fprintf(stderr, "[writers] %s %.3fs\n", what, t_ - tw); tw = t_; } } while (0)
+    snprintf(fn, L, "%s.mp.gtf", p->out_prefix);
+    int rc = pf_write_gtf(p->gaps, p->blocks, fn);
+    if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] gtf written.\n");
+    if (!rc && p->o.write_tsv) {
+        snprintf(fn, L, "%s.mp.tsv", p->out_prefix);
+        rc = pf_write_tsv(p->gaps, p->blocks, fn);
+        if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] tsv written.\n");
+    }
+    /* -U: {prefix}.mp.input_haptag.tsv (4494-4517), every record of the BAM */
+    if (!rc && p->o.untagged && p->o.write_input_tagging) {
+        snprintf(fn, L, "%s.mp.input_haptag.tsv", p->out_prefix);
+        rc = pf_retag_bam(p->bam_path, NULL, NULL, fn, PF_RETAG_INPUT_HAPTAG, NULL, NULL, NULL, p->raw, -1, NULL);
+    }
+    WTRACE("gtf/tsv/input_haptag");
+    /* the VCF only when --vcf was given (4706); the BAM whenever --write-bam
+     * was (4714-4731), with or without a VCF */
+    if (!rc && p->vcf_path) rc = write_rescued_vcf(p, fn, L, trace, tw);
     if (!rc && p->o.write_bam) {                    /* output_modify_bam + sam_index_build3 (4719-4731) */
         char *fb = (char *)malloc(L + 8);
         if (!fb) rc = PF_ERR_NOMEM;
@@ -1361,7 +1371,7 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
         }
         free(fb);
     }
-    free(roff); free(rpos); free(rhap); free(fn);
+    free(fn);
     return rc;
 #undef WTRACE
 }
@@ -1783,10 +1793,11 @@ static int methphase_main_(const pf_methphase_opts_t *o, pf_mp_plan_t **out) {
         for (int k = 0; k < 2 && !rc; k++) {
             if (!gs[k]) continue;
             if (gs[k]->raw_off[gs[k]->n_contigs] == 0) {
-                fprintf(stderr, k == 0 ? "[E::blockjoin_parallel] Nothing loaded from vcf (ref_n=%u), cannot haptag "
-                                         "the input bam. Terminating.\n"
-                                       : "[E::blockjoin_parallel] No intervals loaded, terminating.%.0u\n",
-                        gs[k]->n_contigs);
+                if (k == 0)
+                    fprintf(stderr, "[E::blockjoin_parallel] Nothing loaded from vcf (ref_n=%u), cannot haptag "
+                                    "the input bam. Terminating.\n", gs[k]->n_contigs);
+                else
+                    fprintf(stderr, "[E::blockjoin_parallel] No intervals loaded, terminating.\n");
                 rc = PF_ERR_ARG;
             }
         }

@@ -345,9 +345,12 @@ def test_cli_gtf_tsv_blocks(oracle_lib, tmp_path, fmt):
     """`pomfret-amd methphase --gtf blocks.gtf --vcf v.vcf` and `--tsv
     blocks.tsv` (no --vcf: no VCF written, 4706): windows from the block file
     (main_blockjoin 4661-4666), GTF / TSV / VCF bytes equal the oracle
-    pipeline's."""
-    from pomfret_amd import Config
+    pipeline's.  The no-VCF run also takes --write-bam, which the reference
+    honours with or without a VCF (4714-4731): its records carry the HP tags
+    output_modify_bam gives over the oracle's tables."""
+    from pomfret_amd import Config, _lib
     from pomfret_amd.pipeline import INTERVALS_GTF, INTERVALS_TSV
+    from tests.test_bamw import _restate_methphase, aux_update_int, parse_bam
     aln, recs, bam, vcf = fx.tagged(tmp_path, n_windows=4)
     cfg = Config.from_coverage(30, given=True)
     for with_vcf in (True, False):
@@ -357,6 +360,8 @@ def test_cli_gtf_tsv_blocks(oracle_lib, tmp_path, fmt):
         args = ["methphase", "-o", out, "-c", "30", f"--{fmt}", iv[0], "--output-tsv"]
         if with_vcf:
             args += ["--vcf", vcf]
+        else:
+            args += ["--write-bam"]
         r = _cli(*args, bam)
         assert r.returncode == 0, r.stderr
         ref = methphase_files_oracle(bam, vcf if with_vcf else None, cfg, recs_by_contig={"chrS": recs},
@@ -369,6 +374,15 @@ def test_cli_gtf_tsv_blocks(oracle_lib, tmp_path, fmt):
             assert "multiple phase block files" in r.stderr
         else:
             assert not os.path.exists(out + ".mp.vcf")
+            g = _lib.Gaps(iv[0], fmt=iv[1])
+            b = _lib.Blocks(g, ref["decision"])
+            _, bodies_in, _, _ = parse_bam(bam)
+            _, bodies_out, _, _ = parse_bam(out + ".mp.bam")
+            hp = _restate_methphase(bodies_in, [0] * len(bodies_in), g.contigs(), b.contigs(), ref["qname_hp"],
+                                    None, tid_names=("chrS",))
+            assert len(bodies_out) == len(bodies_in)
+            assert all(bo == aux_update_int(bi, h + 1) for bi, bo, h in zip(bodies_in, bodies_out, hp))
+            assert os.path.getsize(out + ".mp.bam.bai") > 0
 
 
 def test_cli_untagged_gtf_input_tagging(oracle_lib, tmp_path):

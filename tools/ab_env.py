@@ -14,13 +14,19 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import WORKLOAD  # noqa: E402
 from pomfret_amd import Config, Context, LoadConfig  # noqa: E402
-from pomfret_amd.synth_aln import AlnSpec, make_aln_batch  # noqa: E402
+from pomfret_amd.synth_aln import AlnSpec, load_aln, make_aln_batch, save_aln  # noqa: E402
 
 runs = int(os.environ.get("AB_RUNS", "5"))
 nw = int(os.environ.get("AB_WINDOWS", "1024"))
 wl = WORKLOAD
-aln = make_aln_batch(AlnSpec(n_windows=nw, coverage=60, seed=1000, gap=wl["gap"], gap_mix=wl["gap_mix"],
-                             skip_frac=wl["skip_frac"], nosite_frac=wl["nosite_frac"]), workers=16)
+cache = os.environ.get("AB_CACHE")           # a .npz: generated once, loaded by later runs
+if cache and os.path.exists(cache):
+    aln = load_aln(cache)
+else:
+    aln = make_aln_batch(AlnSpec(n_windows=nw, coverage=60, seed=1000, gap=wl["gap"], gap_mix=wl["gap_mix"],
+                                 skip_frac=wl["skip_frac"], nosite_frac=wl["nosite_frac"]), workers=16)
+    if cache:
+        save_aln(cache, aln)
 cfg, lcfg = Config.from_coverage(60, given=False), LoadConfig()
 ctx = Context(0)
 ref = None
@@ -53,7 +59,9 @@ for spec in sys.argv[1:]:
             same = all(np.array_equal(getattr(out, f), getattr(ref, f)) for f in FIELDS)
         else:
             same = None
-        res[label] = dict(wall_ms=round(wall, 3), same=same, **{k: round(v, 4) for k, v in acc.items() if v > 0.01})
+        import hashlib
+        dig = hashlib.sha1(b"".join(np.ascontiguousarray(getattr(out, f)).tobytes() for f in FIELDS)).hexdigest()[:12]
+        res[label] = dict(wall_ms=round(wall, 3), same=same, digest=dig, **{k: round(v, 4) for k, v in acc.items() if v > 0.01})
         db.free()
     print(name, res, flush=True)
     for k, v in saved.items():
