@@ -572,8 +572,16 @@ def main():
                    skip_frac=wl["skip_frac"], nosite_frac=wl["nosite_frac"])
     t = time.perf_counter()
     if record_level:
-        # generated (in worker processes) before anything touches the GPU
-        aln = make_aln_batch(spec, workers=0 if world == 1 else max(1, CPU_SHARE // 2))
+        # generated (in worker processes) before anything touches the GPU;
+        # PF_BENCH_ALN_CACHE: a batch saved beforehand (tools/run_aln_once.py,
+        # same spec), so that a traced run forks no generator workers
+        cache = os.environ.get("PF_BENCH_ALN_CACHE")
+        if cache and os.path.exists(cache) and not args.weak:
+            from pomfret_amd.synth_aln import load_aln
+            aln = load_aln(cache)
+            assert aln.n_windows == n_base, "PF_BENCH_ALN_CACHE holds another batch"
+        else:
+            aln = make_aln_batch(spec, workers=0 if world == 1 else max(1, CPU_SHARE // 2))
         log(f"[bench] rank {rank}: generated {aln.n_windows} base windows, {aln.n_recs} BAM records "
             f"({aln.nbytes() / 1e9:.2f} GB) in {time.perf_counter() - t:.1f}s")
         base_costs = aln_window_costs(aln)

@@ -281,6 +281,13 @@ int  pf_batch_stats(pf_dbatch_t *db, uint64_t *out, uint64_t n);
  * greedy run (no sites).  n >= 2*n_windows.  Tests assert which variant
  * PF_K3_CACHE / PF_K3_GCNT forced. */
 int  pf_batch_k3_paths(pf_dbatch_t *db, uint8_t *out, uint64_t n);
+/* K12's sites path per window of the last run, out[w]: 1 or 2 the fast
+ * path (seen-twice bitmaps and rank counters) over one or two 512 kb
+ * segments, 3 the dense path (per-chunk histograms in HBM: spans past 1 Mb,
+ * or more repeated positions than a segment's counters), 0 no K12 sites pass
+ * (no calls, or the left-coverage check of blockjoin.c:1161).  n >= n_windows.
+ * Tests assert which path the wide headline windows took. */
+int  pf_batch_k12_paths(pf_dbatch_t *db, uint8_t *out, uint64_t n);
 /* The greedy launch this batch was given: out[0] the main kernel's dynamic
  * LDS per problem, out[1] its persistent workgroups (problems at once on the
  * device), out[2] pf_k3_heavy's dynamic LDS, out[3] its problems.  n >= 4. */

@@ -57,6 +57,7 @@ def lib():
         L.pf_batch_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.pf_batch_heavy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
         L.pf_batch_k3_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.pf_batch_k12_paths.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.pf_batch_k3_budget.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.pf_batch_debug_sites.argtypes = [C.c_void_p, C.c_uint32, C.c_int, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_uint32]
@@ -474,6 +475,13 @@ class DeviceBatch:
         """Per-(window, dir) counters of the last run: [W, 2, 8] (see pf_batch_stats)."""
         out = np.zeros((max(self.n_windows, 1), 2, 8), np.uint64)
         _check(lib().pf_batch_stats(self.handle, out.ctypes.data, out.size), "pf_batch_stats")
+        return out[:self.n_windows]
+
+    def k12_paths(self) -> np.ndarray:
+        """Per-window sites path of the last run's K12: 1 / 2 the fast path
+        over one / two segments, 3 the dense path, 0 none (pf_batch_k12_paths)."""
+        out = np.zeros(max(self.n_windows, 1), np.uint8)
+        _check(lib().pf_batch_k12_paths(self.handle, out.ctypes.data, out.size), "pf_batch_k12_paths")
         return out[:self.n_windows]
 
     def k3_paths(self) -> np.ndarray:

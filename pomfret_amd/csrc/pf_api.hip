@@ -654,6 +654,7 @@ static int batch_build(pf_dbatch *b, const pf_window_batch_t *in, const uint32_t
     ALLOC(d.k12c_list, 2ull * (R / PF_K12C_READS + W + 1));
     ALLOC(d.k3_fb_list, std::max<uint32_t>(4 * W, 1));       // the main kernel's deferrals, then pf_k3_heavy's
     ALLOC(d.k3_ntot, std::max<uint32_t>(2 * W, 1));
+    ALLOC(d.k12_path, std::max<uint32_t>(W, 1));
     // one I/O block: the counters zeroed before a run (status, arena
     // counters, fallback counter) followed by everything copied back after it,
     // so a step costs one memset and one D2H copy
@@ -1202,6 +1203,7 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     }
     HIPCHK(hipEventRecord(b->ev[slot][2], st));
     if (stages < 1) return PF_OK;
+    HIPCHK(hipMemsetAsync(d.k12_path, 0, b->W, st));
     hipLaunchKernelGGL(pf_k12_sites_methmers, dim3(b->W), dim3(PF_K1_THREADS), 0, st, d);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(b->ev[slot][3], st));
@@ -1223,8 +1225,9 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     const uint32_t g2 = (uint32_t)std::min<uint64_t>((waves + PF_K2_WAVES - 1) / PF_K2_WAVES, 512);
     if (g2) hipLaunchKernelGGL(pf_k2_methmers, dim3(g2), dim3(PF_K2_WAVES * 64), 0, st, d);
     HIPCHK(hipGetLastError());
-    // k > 5: the slot dictionaries, one workgroup per problem (timed with K2)
-    if (d.kdict && b->W) {
+    // k > 5: the slot dictionaries, one workgroup per problem (timed with K2;
+    // not in a stage-limited debug run, whose keys stay keys)
+    if (d.kdict && b->W && stages >= 3) {
         hipLaunchKernelGGL(pf_k3_kdict, dim3(2 * b->W), dim3(PF_K3_THREADS), 0, st, d);
         HIPCHK(hipGetLastError());
     }
@@ -1527,6 +1530,14 @@ extern "C" int pf_batch_k3_paths(pf_dbatch_t *b, uint8_t *out, uint64_t n) {
     std::vector<uint64_t> st(16ull * b->W + 1);
     if (b->W) HIPCHK(hipMemcpy(st.data(), b->d.stats, 16ull * b->W * sizeof(uint64_t), hipMemcpyDeviceToHost));
     for (uint64_t i = 0; i < 2ull * b->W; i++) out[i] = (uint8_t)(st[i * 8 + 2] >> 56);
+    return PF_OK;
+}
+
+extern "C" int pf_batch_k12_paths(pf_dbatch_t *b, uint8_t *out, uint64_t n) {
+    if (!b || !out || n < b->W) return PF_ERR_ARG;
+    HIPCHK(hipSetDevice(b->ctx->device));
+    HIPCHK(hipStreamSynchronize(b->ctx->stream));
+    if (b->W) HIPCHK(hipMemcpy(out, b->d.k12_path, b->W, hipMemcpyDeviceToHost));
     return PF_OK;
 }
 

@@ -101,6 +101,8 @@ struct pf_dev_batch {
      * before the greedy kernels (per-site hash tables in HBM scratch instead
      * of 4^k-bit masks), which rewrite no keys and read ntot from k3_ntot */
     uint32_t kdict;
+    uint8_t *k12_path;                 /* [W] K12's sites path of the last run: 1 / 2 the fast path over 1 / 2
+                                          segments, 3 the dense path, 0 none (no calls, left coverage) */
     uint32_t *k3_ntot;                 /* [2W] slots of each problem (kdict) */
 };
 

@@ -133,6 +133,7 @@ out:
 #include <atomic>
 #include <chrono>
 #include <mutex>
+#include <map>
 #include <thread>
 #include <string>
 #include <errno.h>
@@ -209,6 +210,36 @@ struct ArenaCache {
 };
 std::mutex g_cache_mu;
 std::vector<ArenaCache *> g_cache;
+std::map<int, uint64_t> g_kept_dev;         // bytes of kept arenas per device (PF_ARENA_KEEP_MAX)
+
+// PF_ARENA_KEEP_MAX (bytes; K/M/G suffixes): at most this many bytes of kept
+// arenas per device -- a smaller HBM, to measure the window jobs' re-reads of
+// the contigs past the budget (tools/genome_scale.py).  Unset: no cap beyond
+// the free-memory reserve.
+uint64_t arena_keep_max() {
+    const char *e = getenv("PF_ARENA_KEEP_MAX");
+    if (!e || !*e) return UINT64_MAX;
+    char *end = nullptr;
+    double v = strtod(e, &end);
+    if (end && (*end == 'K' || *end == 'k')) v *= 1024.0;
+    if (end && (*end == 'M' || *end == 'm')) v *= 1024.0 * 1024.0;
+    if (end && (*end == 'G' || *end == 'g')) v *= 1024.0 * 1024.0 * 1024.0;
+    return v < 0 ? 0ull : (uint64_t)v;
+}
+// reserve `need` bytes of the device's arena budget (false: past it)
+bool arena_budget_take(int dev, uint64_t need) {
+    const uint64_t cap = arena_keep_max();
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    uint64_t &k = g_kept_dev[dev];
+    if (cap != UINT64_MAX && k + need > cap) return false;
+    k += need;
+    return true;
+}
+void arena_budget_give(int dev, uint64_t n) {
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    uint64_t &k = g_kept_dev[dev];
+    k = k > n ? k - n : 0ull;
+}
 std::vector<const pf_ctx_t *> g_keep_on;    // contexts whose -u pre-pass keeps its arenas
 
 bool cache_enabled(const pf_ctx_t *ctx) {
@@ -1011,8 +1042,10 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
             size_t fr = 0, tt = 0;
             const uint64_t need = P.arena + 512;
             uint8_t *k = nullptr;
+            const int kdev = pf_ctx_device((const pf_ctx *)ctx);
+            bool took = false;
             if (hipMemGetInfo(&fr, &tt) == hipSuccess && fr > need && fr - need > std::max<size_t>(tt / 3, 32ull << 30) &&
-                hipMalloc(&k, need) == hipSuccess) {
+                (took = arena_budget_take(kdev, need)) && hipMalloc(&k, need) == hipSuccess) {
                 if (hipMemcpyAsync(k, d_arena, need, hipMemcpyDeviceToDevice, st) == hipSuccess &&
                     hipStreamSynchronize(st) == hipSuccess) {
                     keep->ctx = ctx; keep->path = path; keep->fsize = fsize; keep->tid = tid;
@@ -1027,8 +1060,10 @@ static int dev_fetch(pf_ctx_t *ctx, pf_bam_t *bam, int32_t tid, uint32_t W, cons
                     for (uint32_t r = 0; r < NR; r++) keep->run_f1[r] = P.runs[r].f1;
                 } else {
                     (void)hipFree(k);
+                    k = nullptr;
                 }
             }
+            if (took && !k) arena_budget_give(kdev, need);
             (void)hipGetLastError();
         }
         break;
@@ -1389,6 +1424,7 @@ extern "C" void pf_fetch_cache_clear(pf_ctx_t *ctx) {
         g_cache.swap(keep);
     }
     for (ArenaCache *c : drop) {
+        if (c->d_arena) arena_budget_give(pf_ctx_device((const pf_ctx *)c->ctx), c->arena + 512);
         (void)hipFree(c->d_arena);
         delete c;
     }

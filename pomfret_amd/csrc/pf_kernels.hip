@@ -1103,7 +1103,10 @@ __global__ __launch_bounds__(PF_K1_THREADS) void pf_k12_sites_methmers(pf_dev_ba
     K12_STAMP(2);
     uint32_t S = sh_misc[4];
     if (S > scap) S = scap;
-    if (tid == 0) d.win_S[w] = S;
+    if (tid == 0) {
+        d.win_S[w] = S;
+        d.k12_path[w] = fast ? (uint8_t)nseg : (uint8_t)3;
+    }
 
     // ---- revbuf order: reads ascending by (end<<32 | idx) (blockjoin.c:1126, 1140)
     {
@@ -3349,6 +3352,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
     if (!kd) k3_dict<NT>(d, r0, R, S, dir, masks, mbase, sh_scan, ctl);
     const uint32_t ntot = kd ? uni(d.k3_ntot[prob]) : uni(ctl.ntot);
     if (kd && ntot == PF_NONE) return;               // pf_k3_kdict ran out of scratch: the host re-runs
+    if (kd && tid == 0) ctl.ntot = ntot;             // the greedy loop's init reads it (k3_init; a barrier follows)
     // sum of methmers over the window's reads (slot-list size) and the longest list
     uint32_t summ = 0, lmx = 0;
     for (uint32_t i = tid; i < R; i += NT) {

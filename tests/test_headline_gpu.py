@@ -73,14 +73,19 @@ def test_headline_subset_natural_paths(oracle_lib, gpu_ctx, headline_subset, mon
     paths = db.k3_paths()
     assert all(paths[w, d] == 2 for w in wide for d in (0, 1) if out.win_n_sites[w] > 0), paths[wide]
     assert set(paths[out.win_n_sites > 0].ravel().tolist()) <= {1, 2}
-    # the wide windows' call positions span beyond K12's 2^19-position bitmap:
-    # their sites come from the dense path (pf_kernels.hip, range_ok)
+    # the wide windows' call positions span beyond one 2^19-position segment
+    # of K12's bitmaps: since round 5 they take the fast path over two
+    # segments, one after the other (pf_batch_k12_paths 2), and no window of
+    # the mix goes to the dense path (3)
+    k12 = db.k12_paths()
     off, pos, _, _, _ = db.debug_calls()
     ro = np.searchsorted(db.read_recs(), aln.win_rec_off.astype(np.int64))
     for w in wide:
         c0, c1 = int(off[ro[w]]), int(off[ro[w + 1]])
         if c1 > c0 and out.win_n_sites[w] > 0:
             assert int(pos[c0:c1].max()) - int(pos[c0:c1].min()) >= 1 << 19, w
+            assert k12[w] == 2, (w, int(k12[w]))
+    assert set(k12[out.win_n_sites > 0].tolist()) <= {1, 2}, np.unique(k12, return_counts=True)
     # at 60x no position is covered by 256 reads (so by 256 reads' methmer
     # spans): every problem's slot table holds u8 count pairs (k3_run's bound)
     wro = wb.win_read_off.astype(np.int64)

@@ -97,7 +97,9 @@ def test_large_k_record_level(oracle_lib, gpu_ctx):
     cfg = _cfg(8)
     db = gpu_ctx.upload_aln(cfg, aln, LoadConfig())
     out = db.run()
-    ref = oracle_lib.methphase_aln(cfg, LoadConfig(), aln, n_threads=8)
+    # the oracle's loader, then its window worker (methphase_aln leaves the read tags unset)
+    wb = oracle_lib.load_reads(LoadConfig(), aln)[0]
+    ref = oracle_lib.methphase(cfg, wb, n_threads=8)
     _compare(ref, out, "aln k8")
     db.free()
 

@@ -132,9 +132,10 @@ def test_lds_budget_variants(oracle_lib, gpu_ctx, monkeypatch, lds):
 @pytest.mark.parametrize("env", [{"PF_K3_CACHE": "force"}, {"PF_K3_CACHE": "hbm"}, {"PF_K3_PERSIST": "1"},
                                  {"PF_K3_PERSIST": "7", "PF_K3_CACHE": "force"},
                                  {"PF_K3_CACHE": "force", "PF_K3_GCNT": "force"},
-                                 {"PF_K3_LDS": "24576", "PF_K3_LDS_FB": "73728"}],
+                                 {"PF_K3_LDS": "24576", "PF_K3_LDS_FB": "73728"},
+                                 {"PF_K3_KDICT": "1", "PF_K3_PERSIST": "7"}],
                          ids=["cache", "hbm_lists", "one_workgroup", "seven_workgroups_cache", "cache_counts_hbm",
-                              "budget_24k"])
+                              "budget_24k", "hash_dictionary"])
 def test_slot_list_sources(oracle_lib, gpu_ctx, monkeypatch, env):
     """The greedy loop's slot-list sources give the same bits on every case:
     the candidate slot-list cache (round 4: the candidates' lists in LDS, the
@@ -144,7 +145,9 @@ def test_slot_list_sources(oracle_lib, gpu_ctx, monkeypatch, env):
     state reset between problems).  Round 5: the candidate cache with the
     count table in HBM (path 6) forced for every cache problem with u8 count
     pairs, and a 24 KB budget under which problems past it take path 6 by
-    themselves."""
+    themselves.  Round 6: the hash-table slot dictionary of k > 5
+    (pf_k3_kdict) at the cases' own k, with seven persistent workgroups
+    taking problem after problem (its slot count must reach each one)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     seen = set()
@@ -200,6 +203,9 @@ def test_dense_site_path(oracle_lib, gpu_ctx, monkeypatch, name, cfg, batch):
     db = gpu_ctx.upload(cfg, batch)
     out = db.run()
     _compare(ref, out, name + "/dense")
+    # every window with a sites pass took the dense path (pf_batch_k12_paths)
+    k12 = db.k12_paths()
+    assert set(k12[k12 > 0].tolist()) <= {3} and (k12 == 3).sum() >= (out.win_n_sites > 0).sum()
     db.free()
 
 
