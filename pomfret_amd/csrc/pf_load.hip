@@ -79,6 +79,13 @@ DEV unsigned long long k0_now() {
 #else
 #define DEV_COLD DEV
 #endif
+// SEQ-pass trigger placement (round 6): 1 = the block's trigger range by a
+// wave-parallel search (2 round trips instead of ~10 dependent ones) and each
+// trigger's word pair by two 8-wide LDS reads with packed compares (group,
+// then pair) instead of a 6-step binary search; 0 = round 5
+#ifndef PF_K0_PLACE
+#define PF_K0_PLACE 1
+#endif
 #ifndef PF_K0_WPE
 #define PF_K0_WPE 8                        // pf_k0_load's waves per SIMD (register budget: 512 / WPE VGPRs)
 #endif
@@ -566,6 +573,23 @@ DEV uint32_t sel_nibble(uint64_t m, uint32_t k) {
     if (k >= c) base += 1;
     return base;
 }
+// how many of the 8 u16 values of q (each < 2^15) are <= f: the sign bits of
+// the packed differences q - (f + 1)
+typedef short k0_s16x2 __attribute__((ext_vector_type(2)));
+DEV uint32_t le8_u16(uint4 q, uint32_t f) {
+    const uint32_t F1 = (f + 1u) * 0x10001u;
+    auto neg = [&](uint32_t x) {
+        const k0_s16x2 a = __builtin_bit_cast(k0_s16x2, x), b = __builtin_bit_cast(k0_s16x2, F1);
+        return __builtin_bit_cast(uint32_t, (k0_s16x2)(a - b)) & 0x80008000u;
+    };
+    return (uint32_t)__builtin_popcount(neg(q.x)) + (uint32_t)__builtin_popcount(neg(q.y)) +
+           (uint32_t)__builtin_popcount(neg(q.z)) + (uint32_t)__builtin_popcount(neg(q.w));
+}
+// u16 element e (0..7) of q
+DEV uint32_t u16_at(uint4 q, uint32_t e) {
+    const uint32_t d = e < 2 ? q.x : e < 4 ? q.y : e < 6 ? q.z : q.w;
+    return (e & 1u) ? d >> 16 : d & 0xFFFFu;
+}
 DEV uint64_t valid_nibbles(uint32_t nv) { return nv >= 16 ? 0x1111111111111111ull : ((1ull << (4 * nv)) - 1) & 0x1111111111111111ull; }
 
 template <typename TP>
@@ -627,15 +651,43 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             const uint32_t inc = wscan(ca | (cb << 16), lane);
             const uint32_t tot = uni(__shfl(inc, 63, 64));
             pref[i] = run;
-            L.u.s.sb[i * 64 + lane] = (uint16_t)(run + (inc & 0xFFFFu) - ca);
+            const uint32_t ba = run + (inc & 0xFFFFu) - ca;
+            L.u.s.sb[i * 64 + lane] = (uint16_t)ba;
             run += tot & 0xFFFFu;
             pref[i + 1] = run;
-            L.u.s.sb[(i + 1) * 64 + lane] = (uint16_t)(run + (inc >> 16) - cb);
+            const uint32_t bb2 = run + (inc >> 16) - cb;
+            L.u.s.sb[(i + 1) * 64 + lane] = (uint16_t)bb2;
             run += tot >> 16;
+#if PF_K0_PLACE
+            if ((lane & 7u) == 0) {                   // group bases: every 8th pair's (opA is free until the walk)
+                uint16_t *gb = reinterpret_cast<uint16_t *>(L.opA);
+                gb[i * 8 + (lane >> 3)] = (uint16_t)ba;
+                gb[(i + 1) * 8 + (lane >> 3)] = (uint16_t)bb2;
+            }
+#endif
         }
         const uint32_t btot = run;
         // the block's triggers: ranks < carry + btot, from ti on
         uint32_t tend = ti;
+#if PF_K0_PLACE
+        {
+            // the answer lies in [lo, lo + n]: strided probes narrow it to a
+            // stride, then one probe per lane (ranks increase with j)
+            const uint32_t lim = carry + btot;
+            uint32_t lo = ti, n = nd - ti;
+            while (n > 64) {
+                const uint32_t sd = (n + 63) / 64, off = lane * sd;
+                const bool in = off < n && (TB[slot(min(lo + off, nd - 1))] & 0xFFFFFFu) < lim;
+                const uint32_t c = popc(__ballot(in));
+                if (c == 0) { n = 0; break; }
+                const uint32_t nlo = lo + (c - 1) * sd + 1;
+                n = min(c * sd, n) - (c - 1) * sd - 1;
+                lo = nlo;
+            }
+            const bool in = lane < n && (TB[slot(min(lo + lane, nd - 1))] & 0xFFFFFFu) < lim;   // (nd > ti >= 0)
+            tend = uni(lo + popc(__ballot(in)));
+        }
+#else
         {
             uint32_t n = nd - ti;
             while (n > 0) {
@@ -644,6 +696,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             }
             tend = uni(tend);
         }
+#endif
         wsync();
         for (uint32_t j0 = ti; j0 < tend; j0 += 64) {
             const uint32_t j = j0 + lane;
@@ -657,10 +710,21 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
 #pragma unroll
                 for (uint32_t q = 1; q < ROWS; q++) i += pref[q] <= f ? 1u : 0u;
                 const uint16_t *sbi = L.u.s.sb + i * 64;
+#if PF_K0_PLACE
+                // last pair with base <= f: its group of 8 (the row's group
+                // bases; the first is the row's own base, <= f), then the pair
+                const uint4 G = *reinterpret_cast<const uint4 *>(reinterpret_cast<const uint16_t *>(L.opA) + i * 8);
+                const uint32_t g = le8_u16(G, f) - 1u;
+                const uint4 P = *reinterpret_cast<const uint4 *>(sbi + 8 * g);
+                const uint32_t c = le8_u16(P, f) - 1u;
+                Lw = 8 * g + c;
+                k = f - u16_at(P, c);
+#else
                 uint32_t lo = 0, n = 64;                        // last pair with base <= f
                 while (n > 0) { const uint32_t h = n >> 1; if (sbi[lo + h] <= f) { lo += h + 1; n -= h + 1; } else n = h; }
                 Lw = lo - 1;
                 k = f - sbi[Lw];
+#endif
                 const uint32_t c0 = L.u.s.sc[i * 64 + Lw];
                 if (k >= c0) { k -= c0; hw = 1; }
             }

@@ -118,7 +118,7 @@ def test_cli_large_k(oracle_lib, tmp_path, k):
     assert r.returncode == 0, r.stderr
     cfg = dataclasses.replace(Config.from_coverage(30, given=True), k=k)
     ref = methphase_files_oracle(bam, vcf, cfg, recs_by_contig={"chrS": recs})
-    assert (ref["decision"] >= 0).sum() >= 2
+    assert (ref["decision"] >= 0).sum() >= 1     # longer methmers join fewer of these 4 windows
     assert open(out + ".mp.gtf").read() == ref["gtf"]
     assert open(out + ".mp.tsv").read() == ref["tsv"]
     assert open(out + ".mp.vcf", "rb").read() == ref["vcf"]

@@ -11,7 +11,7 @@ if [ -n "$2" ]; then
   timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu $2 > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 11; }
   tail -3 $O/pytest.log
 fi
-bash tools/ab_libs.sh $T/ab libpomfret_amd.so libpomfret_amd_w6.so libpomfret_amd_w7.so || exit 12
+bash tools/ab_libs.sh $T/ab ${AB_LIBS:-libpomfret_amd.so} || exit 12
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 60 rocprofv3 -L > $O/avail.txt 2>&1
 grep -o "SQC_ICACHE[A-Z_]*\|SQ_IFETCH[A-Z_]*" $O/avail.txt | sort -u > $O/icache_counters.txt
