@@ -1003,7 +1003,7 @@ def main():
         "data": f"synthetic (seeded {wl['coverage']}x long-read pileups, HG002-like; HG002 not available offline)",
         "config": {
             "workload": (f"HG002-like WGS-sized job at {wl['coverage']}x, pre-haplotagged: {n_job} gap windows = "
-                         (f"{tiles} copies of {n_base} distinct windows (" if tiles > 1 else f"{n_base} distinct windows (")
+                         + (f"{tiles} copies of {n_base} distinct windows (" if tiles > 1 else f"{n_base} distinct windows (")
                          + ("gaps log-uniform 5-500 kb (SURVEY 8d mix), "
                             f"{wl['skip_frac']:.0%} skipped (left tags lost) + {wl['nosite_frac']:.0%} site-less "
                             "windows" if wl["gap_mix"] else f"gaps {wl['gap'] // 1000} kb")

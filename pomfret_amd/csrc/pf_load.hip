@@ -698,7 +698,9 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
         }
 #endif
         wsync();
-        for (uint32_t j0 = ti; j0 < tend; j0 += 64) {
+        // PF_K0_DIAG=5 (measurement only): the count and the trigger-range
+        // search without the placement
+        for (uint32_t j0 = ti; j0 < (d.diag == 5u ? ti : tend); j0 += 64) {
             const uint32_t j = j0 + lane;
             const bool act = j < tend;
             uint32_t e = 0, i = 8, Lw = 0, hw = 0, k = 0;
@@ -1362,7 +1364,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     if (d.diag == 2u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
     if (okmm && t.nd && !past) nT = k0_seq_pass(d, L, seq, len, rev, t, TB, lane, implicit);
     K0_STAMP(1);
-    if (d.diag == 3u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
+    if (d.diag == 3u || d.diag == 5u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
     if (!okmm && d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_BADMM], 1ull);
     nT = uni(nT);
 

@@ -26,7 +26,8 @@ no-cache window rate, and the BAM reads priced at the page-cache rate the runs
 saw and at the measured O_DIRECT rate (the node's storage is shared by its 8
 GPUs).
 
-usage: python tools/genome_scale.py [--no-cpu] > profiles/r06/genome_scale.json"""
+usage: python tools/genome_scale.py [--no-cpu] > profiles/r06/genome_scale.json
+       python tools/genome_scale.py --project saved.json   (the projection again)"""
 import json
 import mmap
 import os
@@ -76,7 +77,9 @@ def odirect_read_gbps(path, limit=8 << 30):
     return round(n / dt / 1e9, 2) if n else "unavailable: read nothing"
 
 
-def hbm_total_bytes():
+def hbm_total_bytes(out=None):
+    if out and out.get("hbm_total_bytes"):
+        return int(out["hbm_total_bytes"])
     try:
         import torch
         return int(torch.cuda.get_device_properties(0).total_memory)
@@ -85,6 +88,11 @@ def hbm_total_bytes():
 
 
 def main():
+    if "--project" in sys.argv:            # recompute the projection of a saved run
+        out = json.load(open(sys.argv[sys.argv.index("--project") + 1]))
+        out["hg002_60x_projection"] = project(out, out["genome"]["genome_mb"])
+        print(json.dumps(out), flush=True)
+        return
     cpu = "--no-cpu" not in sys.argv
     eff, _ = effective_cores()
     threads = min(16, eff)
@@ -184,12 +192,13 @@ def project(out, mb):
     t_fin = per_mb(keep["s_finish"])
     read_ms = keep["haptag"]["read_ms"]
     pc_gbps = keep["haptag"]["comp_bytes"] / (read_ms / 1e3) / 1e9 if read_ms else None
-    hbm = hbm_total_bytes()
+    hbm = hbm_total_bytes(out)
+    out["hbm_total_bytes"] = hbm
     budget = hbm - max(hbm / 3, 32 * 2**30)                       # pf_ingest.hip's keep rule leaves this free
     od = out["odirect_read_gbps"] if isinstance(out["odirect_read_gbps"], float) else None
     res = {"kind": "PROJECTION from the per-Mb rates measured above, not a measurement",
-           "genome_mb": HG002_MB, "bam_gb": round(bam_mb * HG002_MB / 1e3, 1),
-           "inflated_gb": round(infl_mb * HG002_MB / 1e3, 1),
+           "genome_mb": HG002_MB, "bam_gb": round(bam_mb * HG002_MB / 1e9, 1),
+           "inflated_gb": round(infl_mb * HG002_MB / 1e9, 1),
            "arena_budget_gb_per_gpu": round(budget / 1e9, 1),
            "page_cache_read_gbps_measured": round(pc_gbps, 2) if pc_gbps else None,
            "odirect_read_gbps_measured": od,
@@ -197,7 +206,7 @@ def project(out, mb):
                         "windows_miss": round(t_win_miss, 6), "writers": round(t_fin, 6)}}
     for n in (1, 8):
         share = HG002_MB / n
-        kept = min(1.0, budget / (infl_mb * 1e6 * share)) if infl_mb else 1.0
+        kept = min(1.0, budget / (infl_mb * share)) if infl_mb else 1.0     # infl_mb: bytes per Mb
         win = share * (kept * t_win_hit + (1 - kept) * t_win_miss)
         pre = share * t_pre
         t_pc = HG002_MB * t_plan + pre + win + HG002_MB * t_fin

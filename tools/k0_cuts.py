@@ -35,7 +35,7 @@ save_aln(path, make_aln_batch(AlnSpec(n_windows=nw, coverage=w["coverage"], gap=
                                       gap_mix=w["gap_mix"], skip_frac=w["skip_frac"],
                                       nosite_frac=w["nosite_frac"]), workers=8))
 res = {}
-for mode in ("4", "2", "3", "0"):
+for mode in ("4", "2", "5", "3", "0"):
     env = dict(os.environ, PF_K0_DIAG=mode)
     out = subprocess.run([sys.executable, __file__, str(nw), wl, runs, path], env=env, capture_output=True,
                          text=True, timeout=300)
@@ -45,5 +45,6 @@ for mode in ("4", "2", "3", "0"):
     m, t = out.stdout.split()[-2:]
     res[m] = float(t)
     print(f"PF_K0_DIAG={m}: K0 {float(t):.3f} ms", flush=True)
-print(f"filters+launch {res['4']:.3f}  MM/ML {res['2'] - res['4']:.3f}  SEQ {res['3'] - res['2']:.3f}  "
+print(f"filters+launch {res['4']:.3f}  MM/ML {res['2'] - res['4']:.3f}  SEQ {res['3'] - res['2']:.3f} "
+      f"(count+range {res['5'] - res['2']:.3f}, placement {res['3'] - res['5']:.3f})  "
       f"CIGAR+emit+end {res['0'] - res['3']:.3f} ms")
