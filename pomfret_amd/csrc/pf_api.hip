@@ -1250,7 +1250,7 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         pf_dev_batch dh = d;
         dh.k3_fb_list = d.k3_fb_list + 2ull * b->W;
         dh.k3_fb_ctr = reinterpret_cast<uint32_t *>(b->io + 80);
-        hipLaunchKernelGGL(pf_k3_heavy, dim3(nh), dim3(PF_K3S_THREADS), d.lds_heavy, c->stream2, dh);
+        hipLaunchKernelGGL(pf_k3_heavy, dim3(nh), dim3(PF_K3H_THREADS), d.lds_heavy, c->stream2, dh);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(nh, 512)), dim3(PF_K3_THREADS), d.lds_fb,
                            c->stream2, dh);

@@ -24,6 +24,9 @@
 #define PF_K3_THREADS 256
 #define PF_K3_WAVES (PF_K3_THREADS / PF_WAVE)
 #define PF_K3S_THREADS 256         /* the main (slim) greedy kernel (512 measured: DESIGN.md 8) */
+#ifndef PF_K3H_THREADS
+#define PF_K3H_THREADS 256         /* pf_k3_heavy (512 measured in round 6: critical window 3.37 -> 3.65 ms, profiles/r06/ab_k3_heavy512.txt) */
+#endif
 #define PF_MAX_NCAND 256
 #define PF_K12_CAPW 512           /* per-wave site-entry buffer of the fused methmer phase */
 #define PF_K12_WB 8               /* bytes per wave-buffer entry: chars, crank, u16 irank, u32 staged key */

@@ -1378,11 +1378,13 @@ struct K3Cand {
 // (64 entries per wave), the push/positive count pairs [2][64] and the exact
 // hap sums [2][2][64] -- 3.5 KB instead of K3Cand's 7.2 KB, so more problems
 // fit a CU beside their dynamic budget
-struct K3CandSlim {
-    uint32_t read[PF_K3S_THREADS];
+template <int NTH>
+struct K3CandSlimT {
+    uint32_t read[NTH];
     uint32_t pos[128];
     unsigned long long key[256];
 };
+using K3CandSlim = K3CandSlimT<PF_K3S_THREADS>;
 
 DEV uint64_t align16(uint64_t x) { return (x + 15) & ~15ull; }
 
@@ -3298,7 +3300,7 @@ DEV void k3_run(const pf_dev_batch &d, uint32_t prob, uint8_t *smem, K3Ctl &ctl,
                 const uint32_t lds, uint32_t *qb = nullptr) {
     // qb: per-wave queue scratch of the slim loop, 64 entries per wave; the
     // kernels that pass none (fallback, heavy: 256 threads) use cd.read
-    static_assert(NT <= PF_MAX_NCAND || NT == PF_K3S_THREADS, "cd.read holds 64 entries per wave");
+    static_assert(sizeof(cd.read) / sizeof(cd.read[0]) >= (size_t)NT, "cd.read holds 64 entries per wave");
     const uint32_t tid = threadIdx.x;
     const uint32_t w = prob >> 1, dir = prob & 1;
     const uint32_t S = d.win_S[w];
@@ -3567,12 +3569,15 @@ __global__ __launch_bounds__(PF_K3S_THREADS) __attribute__((amdgpu_waves_per_eu(
 // the larger budget d.lds_heavy, launched on a second stream beside the main
 // kernel; a problem that does not fit is deferred to pf_k3_fallback like the
 // main kernel's.
-__global__ __launch_bounds__(PF_K3S_THREADS) void pf_k3_heavy(pf_dev_batch d) {
+// Round 6: PF_K3H_THREADS (512) threads per problem -- a heavy problem's
+// chain is its window's critical path, and the term fill, the winner's insert
+// and the range walk split over twice the waves (the pick runs in every wave).
+__global__ __launch_bounds__(PF_K3H_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void pf_k3_heavy(pf_dev_batch d) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ K3Ctl ctl;
-    __shared__ K3CandSlim cd;
-    __shared__ uint32_t sh_scan[PF_K3S_THREADS / 64 + 1];
-    k3_run<false, PF_K3S_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_heavy);
+    __shared__ K3CandSlimT<PF_K3H_THREADS> cd;
+    __shared__ uint32_t sh_scan[PF_K3H_THREADS / 64 + 1];
+    k3_run<false, PF_K3H_THREADS>(d, d.k3_order[blockIdx.x], smem, ctl, cd, sh_scan, d.lds_heavy);
 }
 
 // Problems the main kernel deferred (dictionary or tables beyond the LDS
