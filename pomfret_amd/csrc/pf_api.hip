@@ -1184,6 +1184,9 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         // K0: filters + 5mC extraction of every record into staging slices
         HIPCHK(hipMemsetAsync(b->ld.win_kept, 0, 8ull * b->W, st));
         if (b->ld.n_recs) {
+            // one workgroup per four wave slots (round 6 measured persistent
+            // grids, slots from a counter or dealt statically: 9.2 / 8.0 ms
+            // against 5.7 ms, profiles/r06/ab_k0_persist_*.txt)
             hipLaunchKernelGGL(pf_k0_load, dim3((b->ld.n_recs + PF_K0_WAVES - 1) / PF_K0_WAVES),
                                dim3(PF_K0_WAVES * 64), 0, st, b->ld);
             HIPCHK(hipGetLastError());

@@ -86,6 +86,11 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_PLACE
 #define PF_K0_PLACE 1
 #endif
+// CIGAR walk (round 6): 1 = each trigger's operation by two 8-wide LDS reads
+// (the tile's group ends, then the group) instead of a 6-step binary search
+#ifndef PF_K0_WALK2
+#define PF_K0_WALK2 1
+#endif
 #ifndef PF_K0_WPE
 #define PF_K0_WPE 8                        // pf_k0_load's waves per SIMD (register budget: 512 / WPE VGPRs)
 #endif
@@ -1093,12 +1098,15 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
         j = 1;
     }
     bool trunc = false;
-    uint32_t cn = j + lane < ncig ? cig[j + lane] : 4u;   // next tile in flight
+    // the next tile in flight (three in flight measured in round 6: no faster)
+    auto ld_tile = [&](uint32_t t) { return t + lane < ncig ? cig[t + lane] : 4u; };
+    uint32_t cn = ld_tile(j);
+    auto next_tile = [&]() { cn = j + 64 < ncig ? ld_tile(j + 64) : 4u; };   // cn is tile j + 64 then
     while (j < ncig && !trunc && (tc < nT || implicit)) {
         // ---- 64 CIGAR operations: read starts, reference offsets, ends
         const uint32_t g = j + lane;
         const uint32_t c = cn;
-        if (j + 64 < ncig) cn = j + 64 + lane < ncig ? cig[j + 64 + lane] : 4u;
+        next_tile();
         racc += k0_refc(c);                           // past the end: 4u (S), nothing
         const uint32_t op = c & 15u, ln = c >> 4;
         const uint64_t stop = __ballot(op == 3u || op == 4u);     // past the end acts as a stop
@@ -1113,10 +1121,16 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
         const uint32_t dl = !valid ? 0u : op == 2u ? ln : op == 1u ? 0u - ln : 0u;
         const uint32_t rin = wscan(rl, lane), din = wscan(dl, lane);
         const uint32_t a = a_cur + rin - rl, off = off_cur + din - dl;
-        L.opE[lane] = valid ? a + rl : 0xFFFFFFFFu;
+        const uint32_t oe = valid ? a + rl : 0xFFFFFFFFu;
+        L.opE[lane] = oe;
         L.opA[lane] = a;
         L.opOff[lane] = off;
         L.opT[lane] = (uint8_t)op;
+#if PF_K0_WALK2
+        // the 8 groups' last ends (explicit mode only: the implicit chunks use
+        // the merge lists this shares)
+        if (!implicit && (lane & 7u) == 7u) L.u.mg.eP[lane >> 3] = oe;
+#endif
         const uint32_t a_end = a_cur + uni(__shfl(rin, 63, 64));
         const uint32_t off_end = off_cur + uni(__shfl(din, 63, 64));
         wsync();
@@ -1132,7 +1146,20 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
                 bool keep = false;
                 uint32_t v = 0;
                 if (in) {
+#if PF_K0_WALK2
+                    // first operation with end >= p (ends past nv are ~0): the
+                    // groups whose last end is < p, then within the group
+                    auto lt8 = [&](uint4 x, uint4 y) {
+                        return (x.x < p ? 1u : 0u) + (x.y < p ? 1u : 0u) + (x.z < p ? 1u : 0u) + (x.w < p ? 1u : 0u) +
+                               (y.x < p ? 1u : 0u) + (y.y < p ? 1u : 0u) + (y.z < p ? 1u : 0u) + (y.w < p ? 1u : 0u);
+                    };
+                    const uint4 *gl = reinterpret_cast<const uint4 *>(L.u.mg.eP);
+                    const uint32_t g = lt8(gl[0], gl[1]);              // < 8: the last end of the tile is >= p
+                    const uint4 *ge = reinterpret_cast<const uint4 *>(L.opE + 8 * g);
+                    const uint32_t oi = 8 * g + lt8(ge[0], ge[1]);
+#else
                     const uint32_t oi = lb64<false>(L.opE, nv, p);
+#endif
                     keep = L.opT[oi] == 0;
                     v = i_ref + p + cgoffset + L.opOff[oi];
                 }
@@ -1153,11 +1180,10 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
     // fatal operations past the last consumed trigger are still reached
     // by the reference's loop (it walks every op up to N/S); the end position
     // counts every operation (the tile at j is already in flight in cn)
-    bool first = true;
     for (; j < ncig; j += 64) {
         const uint32_t g = j + lane;
-        const uint32_t c = first ? cn : g < ncig ? cig[g] : 4u;
-        first = false;
+        const uint32_t c = cn;
+        next_tile();
         racc += k0_refc(c);
         if (trunc) continue;
         const uint32_t op = c & 15u;
