@@ -718,6 +718,8 @@ typedef struct pf_methphase_opts {
     const char *interval_path;
     int32_t interval_format;       /* PF_INTERVALS_GTF or PF_INTERVALS_TSV                     */
     int32_t write_input_tagging;   /* -U (with -u): {prefix}.mp.input_haptag.tsv (4494-4517)  */
+    int32_t bam_threads;           /* -T / --bam-threads: --write-bam's BGZF compression threads
+                                      (<= 0: `threads`, as -t sets threads_bam, cli.c:261-264)  */
 } pf_methphase_opts_t;
 
 typedef struct pf_mp_plan pf_mp_plan_t;
@@ -839,6 +841,13 @@ int  pf_mp_stats(const pf_mp_plan_t *p, pf_mp_stats_t *s);
 int  pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, const char *tsv_out, int mode,
                   const pf_gaps_t *g, const pf_blocks_t *blk, const pf_tags_t *methphased, const pf_tags_t *raw,
                   int level, uint64_t *n_records);
+/* The same with `threads` BGZF compression threads for bam_out (-T /
+ * --bam-threads: htslib's bgzf_mt for the output, cli.c:261-264, 3036):
+ * blocks deflated in parallel, written in order; the BAM and BAI bytes do not
+ * depend on the thread count. */
+int  pf_retag_bam_threads(const char *bam_in, const char *bam_out, const char *bai_out, const char *tsv_out, int mode,
+                          const pf_gaps_t *g, const pf_blocks_t *blk, const pf_tags_t *methphased,
+                          const pf_tags_t *raw, int level, int threads, uint64_t *n_records);
 
 /* Host helper: htslib kt_fisher_exact semantics. Returns the probability of
  * the observed table. */

@@ -407,22 +407,23 @@ RETAG_METHPHASE, RETAG_VARHAPTAG = 0, 1
 
 
 def retag_bam(bam_in: str, bam_out: Optional[str], bai_out: Optional[str], tsv_out: Optional[str], mode: int,
-              gaps=None, blocks=None, methphased=None, raw=None, level: int = -1) -> int:
-    """pf_retag_bam: --write-bam (mode RETAG_METHPHASE, output_modify_bam) or
-    varhaptag (RETAG_VARHAPTAG) output of bam_in.  gaps / blocks: _lib.Gaps /
-    _lib.Blocks; methphased / raw: pipeline.Tags (or None).  Returns the
-    number of records written."""
+              gaps=None, blocks=None, methphased=None, raw=None, level: int = -1, threads: int = 1) -> int:
+    """pf_retag_bam_threads: --write-bam (mode RETAG_METHPHASE,
+    output_modify_bam) or varhaptag (RETAG_VARHAPTAG) output of bam_in.  gaps /
+    blocks: _lib.Gaps / _lib.Blocks; methphased / raw: pipeline.Tags (or
+    None); threads: BGZF compression threads (-T).  Returns the number of
+    records written."""
     from ._lib import _PfBlocks, _PfGaps
     L = _bind()
     if not getattr(L, "_retag_typed", False):
-        L.pf_retag_bam.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int,
-                                   C.POINTER(_PfGaps), C.POINTER(_PfBlocks), C.c_void_p, C.c_void_p, C.c_int,
-                                   C.POINTER(C.c_uint64)]
+        L.pf_retag_bam_threads.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_int,
+                                           C.POINTER(_PfGaps), C.POINTER(_PfBlocks), C.c_void_p, C.c_void_p, C.c_int,
+                                           C.c_int, C.POINTER(C.c_uint64)]
         L._retag_typed = True
     n = C.c_uint64()
     enc = lambda s: s.encode() if s else None  # noqa: E731
-    _check(L.pf_retag_bam(enc(bam_in), enc(bam_out), enc(bai_out), enc(tsv_out), int(mode),
-                          gaps._p if gaps is not None else None, blocks._p if blocks is not None else None,
-                          methphased.h if methphased is not None else None, raw.h if raw is not None else None,
-                          int(level), C.byref(n)), "pf_retag_bam")
+    _check(L.pf_retag_bam_threads(enc(bam_in), enc(bam_out), enc(bai_out), enc(tsv_out), int(mode),
+                                  gaps._p if gaps is not None else None, blocks._p if blocks is not None else None,
+                                  methphased.h if methphased is not None else None, raw.h if raw is not None else None,
+                                  int(level), int(threads), C.byref(n)), "pf_retag_bam_threads")
     return int(n.value)

@@ -1784,43 +1784,186 @@ int pf_bam_estimate_coverage(pf_bam_t *b, int32_t *covs, int32_t n) {
 static const uint8_t BGZF_EOF[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0,
                                      0, 0, 0, 0, 0, 0, 0, 0};
 
+/* one BGZF block: n bytes of ubuf deflated into cbuf; its size, or 0 on error */
+static uint32_t bgzf_block(const uint8_t *ubuf, int n, int level, uint8_t *cbuf) {
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return 0;
+    zs.next_in = (Bytef *)ubuf;
+    zs.avail_in = (uInt)n;
+    zs.next_out = cbuf + 18;
+    zs.avail_out = (uInt)(65536 - 18 - 8);
+    const int rc = deflate(&zs, Z_FINISH);
+    const uint32_t clen = (uint32_t)zs.total_out;
+    deflateEnd(&zs);
+    if (rc != Z_STREAM_END) return 0;
+    const uint32_t bsize = 18 + clen + 8;
+    const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0};
+    memcpy(cbuf, hdr, 16);
+    cbuf[16] = (uint8_t)((bsize - 1) & 0xff);
+    cbuf[17] = (uint8_t)((bsize - 1) >> 8);
+    const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), ubuf, (uInt)n);
+    uint8_t *t = cbuf + 18 + clen;
+    for (int i = 0; i < 4; i++) { t[i] = (uint8_t)(crc >> (8 * i)); t[4 + i] = (uint8_t)((uint32_t)n >> (8 * i)); }
+    return bsize;
+}
+
+/* -T / --bam-threads (htslib's bgzf_mt for the output, cli.c:261-264): blocks
+ * are queued, deflated by a pool of threads in batches and written in order.
+ * Each block is deflated alone with the same parameters, so the file is the
+ * same bytes at any thread count.  The index's virtual offsets are taken in
+ * block-number space while writing (bgzfw_tell) and moved to file addresses
+ * when the last block is written (bgzfw_vmap). */
+#define BGZFW_BATCH 16                /* queued blocks per thread */
+typedef struct {
+    int nt, nq, cap;                  /* threads, queued blocks, queue capacity */
+    uint8_t *u, *c;                   /* cap x BGZF_BLK input, cap x 65536 output */
+    int *un;
+    uint32_t *cs;
+    pthread_t *th;
+    int made;
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    uint64_t gen;                     /* batch generation */
+    int next, left, quit, level;
+} bgzfw_pool_t;
+
 typedef struct {
     FILE *f;
     uint8_t ubuf[BGZF_BLK];
     uint8_t cbuf[65536];
     int n;
-    uint64_t caddr;              /* compressed address of the block being filled */
+    uint64_t caddr;              /* compressed address of the block being filled (threaded: its number) */
     int level;
     int err;
+    bgzfw_pool_t *pool;          /* NULL: deflated in this thread as it fills */
+    uint64_t *baddr;             /* threaded: file address of block i (i <= the blocks written) */
+    uint64_t nb, mb;
 } bgzfw_t;
+
+static void *bgzfw_worker(void *arg) {
+    bgzfw_pool_t *P = (bgzfw_pool_t *)arg;
+    uint64_t seen = 0;
+    pthread_mutex_lock(&P->mu);
+    for (;;) {
+        while (!P->quit && P->gen == seen) pthread_cond_wait(&P->go, &P->mu);
+        if (P->quit) break;
+        seen = P->gen;
+        while (P->next < P->nq) {
+            const int i = P->next++;
+            pthread_mutex_unlock(&P->mu);
+            P->cs[i] = bgzf_block(P->u + (size_t)i * BGZF_BLK, P->un[i], P->level, P->c + (size_t)i * 65536);
+            pthread_mutex_lock(&P->mu);
+            if (--P->left == 0) pthread_cond_signal(&P->done);
+        }
+    }
+    pthread_mutex_unlock(&P->mu);
+    return NULL;
+}
+
+/* deflate the queued blocks (the pool and this thread), write them in order */
+static int bgzfw_drain(bgzfw_t *w) {
+    bgzfw_pool_t *P = w->pool;
+    if (!P->nq) return 0;
+    pthread_mutex_lock(&P->mu);
+    P->next = 0;
+    P->left = P->nq;
+    P->gen++;
+    pthread_cond_broadcast(&P->go);
+    while (P->next < P->nq) {                         /* this thread takes blocks too */
+        const int i = P->next++;
+        pthread_mutex_unlock(&P->mu);
+        P->cs[i] = bgzf_block(P->u + (size_t)i * BGZF_BLK, P->un[i], P->level, P->c + (size_t)i * 65536);
+        pthread_mutex_lock(&P->mu);
+        P->left--;
+    }
+    while (P->left > 0) pthread_cond_wait(&P->done, &P->mu);
+    pthread_mutex_unlock(&P->mu);
+    for (int i = 0; i < P->nq && !w->err; i++) {
+        if (!P->cs[i]) { w->err = PF_ERR_INTERNAL; break; }
+        if (fwrite(P->c + (size_t)i * 65536, 1, P->cs[i], w->f) != P->cs[i]) { w->err = -1; break; }
+        if (w->nb + 1 >= w->mb) {
+            const uint64_t m = w->mb ? 2 * w->mb : 1024;
+            uint64_t *a = (uint64_t *)realloc(w->baddr, m * sizeof(uint64_t));
+            if (!a) { w->err = PF_ERR_NOMEM; break; }
+            w->baddr = a;
+            w->mb = m;
+        }
+        w->baddr[w->nb + 1] = w->baddr[w->nb] + P->cs[i];
+        w->nb++;
+    }
+    P->nq = 0;
+    return w->err;
+}
 
 static int bgzfw_flush(bgzfw_t *w) {
     if (w->err) return w->err;
     if (w->n == 0) return 0;
-    z_stream zs;
-    memset(&zs, 0, sizeof zs);
-    if (deflateInit2(&zs, w->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return w->err = PF_ERR_NOMEM;
-    zs.next_in = w->ubuf;
-    zs.avail_in = (uInt)w->n;
-    zs.next_out = w->cbuf + 18;
-    zs.avail_out = (uInt)(sizeof w->cbuf - 18 - 8);
-    const int rc = deflate(&zs, Z_FINISH);
-    const uint32_t clen = (uint32_t)zs.total_out;
-    deflateEnd(&zs);
-    if (rc != Z_STREAM_END) return w->err = PF_ERR_INTERNAL;
-    const uint32_t bsize = 18 + clen + 8;
-    uint8_t *h = w->cbuf;
-    const uint8_t hdr[16] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0};
-    memcpy(h, hdr, 16);
-    h[16] = (uint8_t)((bsize - 1) & 0xff);
-    h[17] = (uint8_t)((bsize - 1) >> 8);
-    const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), w->ubuf, (uInt)w->n);
-    uint8_t *t = h + 18 + clen;
-    for (int i = 0; i < 4; i++) { t[i] = (uint8_t)(crc >> (8 * i)); t[4 + i] = (uint8_t)((uint32_t)w->n >> (8 * i)); }
-    if (fwrite(h, 1, bsize, w->f) != bsize) return w->err = -1;
+    if (w->pool) {
+        bgzfw_pool_t *P = w->pool;
+        memcpy(P->u + (size_t)P->nq * BGZF_BLK, w->ubuf, (size_t)w->n);
+        P->un[P->nq++] = w->n;
+        w->caddr++;
+        w->n = 0;
+        return P->nq == P->cap ? bgzfw_drain(w) : 0;
+    }
+    const uint32_t bsize = bgzf_block(w->ubuf, w->n, w->level, w->cbuf);
+    if (!bsize) return w->err = PF_ERR_INTERNAL;
+    if (fwrite(w->cbuf, 1, bsize, w->f) != bsize) return w->err = -1;
     w->caddr += bsize;
     w->n = 0;
     return 0;
+}
+
+/* threads > 1: start the pool (on failure the writer stays single-threaded) */
+static void bgzfw_start_pool(bgzfw_t *w, int threads) {
+    if (threads <= 1) return;
+    bgzfw_pool_t *P = (bgzfw_pool_t *)calloc(1, sizeof(bgzfw_pool_t));
+    if (!P) return;
+    P->nt = threads;
+    P->cap = BGZFW_BATCH * threads;
+    P->level = w->level;
+    P->u = (uint8_t *)malloc((size_t)P->cap * BGZF_BLK);
+    P->c = (uint8_t *)malloc((size_t)P->cap * 65536);
+    P->un = (int *)malloc((size_t)P->cap * sizeof(int));
+    P->cs = (uint32_t *)malloc((size_t)P->cap * sizeof(uint32_t));
+    P->th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    w->baddr = (uint64_t *)calloc(1024, sizeof(uint64_t));
+    w->mb = 1024;
+    if (!P->u || !P->c || !P->un || !P->cs || !P->th || !w->baddr || pthread_mutex_init(&P->mu, NULL)) goto fail;
+    pthread_cond_init(&P->go, NULL);
+    pthread_cond_init(&P->done, NULL);
+    for (int i = 0; i < threads - 1; i++) P->made += pthread_create(&P->th[i], NULL, bgzfw_worker, P) == 0;
+    w->pool = P;
+    w->baddr[0] = w->caddr;                           /* the first queued block's file address */
+    w->caddr = 0;                                     /* block numbers from here */
+    return;
+fail:
+    free(P->u); free(P->c); free(P->un); free(P->cs); free(P->th); free(P);
+    free(w->baddr); w->baddr = NULL; w->mb = 0;
+}
+
+static void bgzfw_stop_pool(bgzfw_t *w) {
+    bgzfw_pool_t *P = w->pool;
+    if (!P) return;
+    pthread_mutex_lock(&P->mu);
+    P->quit = 1;
+    pthread_cond_broadcast(&P->go);
+    pthread_mutex_unlock(&P->mu);
+    for (int i = 0; i < P->made; i++) pthread_join(P->th[i], NULL);
+    pthread_mutex_destroy(&P->mu);
+    pthread_cond_destroy(&P->go);
+    pthread_cond_destroy(&P->done);
+    free(P->u); free(P->c); free(P->un); free(P->cs); free(P->th); free(P);
+    w->pool = NULL;
+}
+
+/* a virtual offset of the threaded writer (block number << 16 | offset) as a
+ * file one (after the last drain); the single-threaded writer's as is */
+static uint64_t bgzfw_vmap(const bgzfw_t *w, uint64_t v) {
+    if (!w->baddr || v == ~0ull) return v;
+    const uint64_t b = v >> 16;
+    return b <= w->nb ? (w->baddr[b] << 16) | (v & 0xffffu) : v;
 }
 
 static int bgzfw_write(bgzfw_t *w, const void *src, size_t n) {
@@ -2043,6 +2186,12 @@ static int hp_update(const uint8_t *d, uint32_t bs, const rec_t *r, int64_t val,
 int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, const char *tsv_out, int mode,
                  const pf_gaps_t *g, const pf_blocks_t *blk, const pf_tags_t *methphased, const pf_tags_t *raw,
                  int level, uint64_t *n_records) {
+    return pf_retag_bam_threads(bam_in, bam_out, bai_out, tsv_out, mode, g, blk, methphased, raw, level, 1, n_records);
+}
+
+int pf_retag_bam_threads(const char *bam_in, const char *bam_out, const char *bai_out, const char *tsv_out, int mode,
+                         const pf_gaps_t *g, const pf_blocks_t *blk, const pf_tags_t *methphased, const pf_tags_t *raw,
+                         int level, int threads, uint64_t *n_records) {
     if (!bam_in || (!bam_out && !tsv_out) ||
         (mode != PF_RETAG_METHPHASE && mode != PF_RETAG_VARHAPTAG && mode != PF_RETAG_INPUT_HAPTAG))
         return PF_ERR_ARG;
@@ -2108,6 +2257,7 @@ int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, c
         }
         if (!rc && w) rc = bgzfw_flush(w);
     }
+    if (!rc && w) bgzfw_start_pool(w, threads);       /* the header's block is written: numbers start at 0 */
     if (!rc && w) {
         X.n_ref = n_ref;
         X.r = (iref_t *)calloc(n_ref ? (size_t)n_ref : 1, sizeof(iref_t));
@@ -2223,9 +2373,24 @@ int pf_retag_bam(const char *bam_in, const char *bam_out, const char *bai_out, c
     if (!rc && w) {
         rc = bgzfw_flush(w);
         if (!rc) bai_finish(&X, bgzfw_tell(w));
+        if (!rc && w->pool) rc = bgzfw_drain(w);
+        if (!rc && w->baddr) {                        /* block numbers -> file addresses */
+            for (int32_t t = 0; t < X.n_ref; t++) {
+                iref_t *r = &X.r[t];
+                for (size_t i = 0; i < r->n; i++) { r->c[i].u = bgzfw_vmap(w, r->c[i].u); r->c[i].v = bgzfw_vmap(w, r->c[i].v); }
+                for (size_t i = 0; i < r->nl; i++) r->lin[i] = bgzfw_vmap(w, r->lin[i]);
+                r->off_beg = bgzfw_vmap(w, r->off_beg);
+                r->off_end = bgzfw_vmap(w, r->off_end);
+            }
+        }
         if (!rc && fwrite(BGZF_EOF, 1, sizeof BGZF_EOF, w->f) != sizeof BGZF_EOF) rc = -1;
     }
-    if (w) { if (w->f && fclose(w->f) && !rc) rc = -1; free(w); }
+    if (w) {
+        bgzfw_stop_pool(w);
+        if (w->f && fclose(w->f) && !rc) rc = -1;
+        free(w->baddr);
+        free(w);
+    }
     if (!rc && bam_out && bai_out) rc = bai_write(&X, bai_out);
     if (tsv && fclose(tsv) && !rc) rc = -1;
     for (int32_t t = 0; t < X.n_ref; t++) { free(X.r[t].c); free(X.r[t].lin); }

@@ -65,6 +65,7 @@ static void help_methphase(const char *prefix) {
     fprintf(stderr, "  -t     [opt] Host threads fetching reads, per GPU. [1]\n");
     fprintf(stderr, "  --output-tsv [opt] Also write {prefix}.mp.tsv.\n");
     fprintf(stderr, "  --write-bam  [opt] Also write {prefix}.mp.bam (+ .bai) with the new HP tags.\n");
+    fprintf(stderr, "  -T,--bam-threads [opt] Compression threads of the output BAM. [-t]\n");
     fprintf(stderr, "  --gpus [opt] GPUs to use. [all visible]\n");
     fprintf(stderr, "  --host-fetch [opt] Inflate and decode BAM records (and the coverage pass) on the host instead of the GPU.\n");
 }
@@ -87,7 +88,7 @@ static const struct option longopts[] = {
 
 typedef struct {
     int help, threads, lo, hi, readlen, mapq, k, k_span, cov, cov_sel, n_cand, untagged, out_tsv, out_bam;
-    int chunk_size, chunk_stride, gpus, job_windows, verbose, host_fetch, write_input_tagging, dbg;
+    int chunk_size, chunk_stride, gpus, job_windows, verbose, host_fetch, write_input_tagging, dbg, bam_threads;
     char *prefix, *vcf, *gtf, *tsv, *bam;
 } cli_t;
 
@@ -117,7 +118,7 @@ static int parse(int argc, char **argv, cli_t *c) {
         case O_TSV: c->tsv = optarg; break;
         case O_WBAM: c->out_bam = 1; break;
         case O_OTSV: c->out_tsv = 1; break;
-        case 'T': case O_BAMT: break;
+        case 'T': case O_BAMT: c->bam_threads = atoi(optarg); break;
         case 'u': case O_UNTAG: c->untagged = 1; break;
         case 'U': case O_WIT: c->write_input_tagging = 1; break;
         case O_CSIZE: c->chunk_size = atoi(optarg); break;
@@ -264,6 +265,7 @@ int main(int argc, char **argv) {
     o.chunk_size = c.chunk_size;
     o.chunk_stride = c.chunk_stride;
     o.threads = c.threads;
+    o.bam_threads = c.bam_threads;                  /* -T; else -t (cli.c:261-264) */
     o.n_devices = c.gpus;
     o.job_windows = c.job_windows > 0 ? (uint32_t)c.job_windows : 0;
     o.host_fetch = c.host_fetch;

@@ -1243,6 +1243,11 @@ static int write_report(pf_mp_plan_t *p) {
     return fclose(fo) ? -1 : PF_OK;
 }
 
+/* the output BAM's compression threads: -T, else -t (cli.c:261-264) */
+static int bam_threads(const pf_methphase_opts_t *o) {
+    return o->bam_threads > 0 ? o->bam_threads : o->threads > 0 ? o->threads : 1;
+}
+
 /* the rescue of dropped-interval sites (recover_variant_phase_in_dropped_intervals)
  * and {prefix}.mp.vcf: only with --vcf (4706-4712) */
 static int write_rescued_vcf(pf_mp_plan_t *p, char *fn, size_t L, int trace, double tw) {
@@ -1365,8 +1370,8 @@ static int write_methphase_outputs(pf_mp_plan_t *p) {
         if (!rc) {
             snprintf(fn, L, "%s.mp.bam", p->out_prefix);
             snprintf(fb, L + 8, "%s.mp.bam.bai", p->out_prefix);
-            rc = pf_retag_bam(p->bam_path, fn, fb, NULL, PF_RETAG_METHPHASE, p->gaps, p->blocks, p->qname_hp,
-                              p->o.untagged ? p->raw : NULL, -1, NULL);
+            rc = pf_retag_bam_threads(p->bam_path, fn, fb, NULL, PF_RETAG_METHPHASE, p->gaps, p->blocks, p->qname_hp,
+                                      p->o.untagged ? p->raw : NULL, -1, bam_threads(&p->o), NULL);
             if (!rc && p->o.verbose >= 0) fprintf(stderr, "[M::main_blockjoin] bam written and indexed.\n");
         }
         free(fb);
@@ -1385,8 +1390,8 @@ static int varhaptag_outputs(pf_mp_plan_t *p) {
     if (!rc) {
         snprintf(ft, L, "%s.varhaptag.tsv", p->out_prefix);
         snprintf(fb, L, "%s.bai", p->out_prefix);
-        rc = pf_retag_bam(p->bam_path, p->o.write_bam ? p->out_prefix : NULL, p->o.write_bam ? fb : NULL, ft,
-                          PF_RETAG_VARHAPTAG, NULL, NULL, NULL, p->raw, -1, NULL);
+        rc = pf_retag_bam_threads(p->bam_path, p->o.write_bam ? p->out_prefix : NULL, p->o.write_bam ? fb : NULL, ft,
+                                  PF_RETAG_VARHAPTAG, NULL, NULL, NULL, p->raw, -1, bam_threads(&p->o), NULL);
     }
     free(ft); free(fb);
     return rc;

@@ -48,7 +48,7 @@ class PfMethphaseOpts(C.Structure):
                 ("n_devices", C.c_int32), ("devices", C.c_void_p), ("ctxs", C.c_void_p), ("n_ctxs", C.c_int32),
                 ("rank", C.c_int32), ("world", C.c_int32), ("job_windows", C.c_uint32), ("verbose", C.c_int32),
                 ("host_fetch", C.c_int32), ("interval_path", C.c_char_p), ("interval_format", C.c_int32),
-                ("write_input_tagging", C.c_int32)]
+                ("write_input_tagging", C.c_int32), ("bam_threads", C.c_int32)]
 
 
 class PfQnameTagsC(C.Structure):

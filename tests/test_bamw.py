@@ -274,3 +274,36 @@ def test_varhaptag_tsv_and_bam(tmp_path):
     os.remove(out)
     retag_bam(bam, None, None, out + ".2.tsv", RETAG_VARHAPTAG, raw=rt)
     assert open(out + ".2.tsv").read() == open(out + ".varhaptag.tsv").read() and not os.path.exists(out)
+
+
+@pytest.mark.parametrize("threads", [2, 3, 8])
+def test_write_bam_threads_same_bytes(tmp_path, threads):
+    """-T / --bam-threads: the BGZF blocks deflated by a thread pool in batches
+    and written in order, the index's virtual offsets taken in block-number
+    space and moved to file addresses at the end -- the BAM and the BAI are
+    the same bytes as the single-threaded writer's (several batches here), and
+    the index answers queries."""
+    from pomfret_amd import _lib
+    from pomfret_amd.bam import RETAG_METHPHASE, BamFile, retag_bam
+    from pomfret_amd.pipeline import Tags
+    from tests import _fixtures as fx
+    aln, recs, bam, vcf = fx.tagged(tmp_path, n_windows=4)
+    g = _lib.Gaps(vcf)
+    rng = random.Random(11)
+    b = _lib.Blocks(g, [rng.choice([-1, 0, 1]) for _ in range(g.n_windows)])
+    table = {r.qname: rng.choice([0, 1]) for r in recs if rng.random() < 0.5}
+    t = Tags()
+    t.put_first(list(table), list(table.values()))
+    outs = []
+    for th in (1, threads):
+        out = str(tmp_path / f"o{th}.mp.bam")
+        n = retag_bam(bam, out, out + ".bai", None, RETAG_METHPHASE, g, b, t, None, threads=th)
+        assert n == len(recs)
+        outs.append((open(out, "rb").read(), open(out + ".bai", "rb").read()))
+    assert len(read_bgzf_blocks(str(tmp_path / "o1.mp.bam"))) > 16 * threads + 2    # more than one batch
+    assert outs[0][0] == outs[1][0]
+    assert outs[0][1] == outs[1][1]
+    with BamFile(str(tmp_path / f"o{threads}.mp.bam")) as bo:
+        s, e = int(aln.win_start[1]), int(aln.win_end[1])
+        got, qn, _ = bo.fetch_windows("chrS", [s], [e], readback=0)
+        assert len(qn) > 0
