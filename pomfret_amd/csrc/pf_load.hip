@@ -91,6 +91,12 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_WALK2
 #define PF_K0_WALK2 1
 #endif
+// SEQ pass (round 6): 1 = the placement writes the CpG triggers compacted
+// (forward reads from the bottom of the list, reverse reads from the top)
+// instead of a compaction pass over the whole list afterwards
+#ifndef PF_K0_FUSEC
+#define PF_K0_FUSEC 1
+#endif
 #ifndef PF_K0_WPE
 #define PF_K0_WPE 8                        // pf_k0_load's waves per SIMD (register budget: 512 / WPE VGPRs)
 #endif
@@ -599,7 +605,7 @@ DEV uint64_t valid_nibbles(uint32_t nv) { return nv >= 16 ? 0x1111111111111111ul
 
 template <typename TP>
 DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint32_t len, bool rev, const K0Tgt &t,
-                         TP TB, uint32_t lane, bool &implicit) {
+                         TP TB, uint32_t lane, bool &implicit, uint32_t &tb_off) {
     // Blocks of 1024 16-base words (16384 bases), read by 8 coalesced
     // wave-instructions of 1 KiB (lane L holds words 2L, 2L+1 of each 128-word
     // row i).  Target counts per word pair, one scan per row, and each pair's
@@ -616,8 +622,9 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
     const uint32_t nblk = (nwords + BW - 1) / BW;
     const uint32_t nd = t.nd;
     auto slot = [&](uint32_t j) { return rev ? nd - 1 - j : j; };   // rank order -> TB index
-    uint32_t carry = 0, ti = 0;
+    uint32_t carry = 0, ti = 0, nout = 0;             // nout: CpG triggers written (PF_K0_FUSEC)
     bool imp = false;
+    tb_off = 0;
     for (uint32_t bb = 0; bb < nblk && ti < nd; bb++) {
         const uint32_t b = rev ? nblk - 1 - bb : bb;
         uint4 v[ROWS];
@@ -709,6 +716,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             const uint32_t j = j0 + lane;
             const bool act = j < tend;
             uint32_t e = 0, i = 8, Lw = 0, hw = 0, k = 0;
+            uint32_t key = 0xFFFFFFFFu;
             if (act) {
                 e = TB[slot(j)];
                 const uint32_t rr = (e & 0xFFFFFFu) - carry;
@@ -799,7 +807,6 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
 #endif
                 const uint32_t bi = sel_nibble(zero_nibbles(xw ^ pat), k);
                 const uint32_t p = w * 16 + bi;
-                uint32_t key = 0xFFFFFFFFu;
                 if (p > 0 && p < len - 1) {
                     bool ctx;
                     if (!rev) ctx = (bi < 15 ? (uint32_t)(xw >> (4 * (bi + 1))) & 15u
@@ -811,8 +818,22 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                         key = (p << 2) | (q < d.lo ? 1u : q >= d.hi ? 0u : 2u);
                     } else imp = true;
                 }
-                TB[slot(j)] = key;
             }
+#if PF_K0_FUSEC
+            // the CpG triggers in rank order, compacted as they are placed: a
+            // forward read's list grows from TB[0], a reverse read's (ranks
+            // from the end) from TB[nd - 1] down, so either ends in ascending
+            // position; every write lands on a slot this batch or an earlier
+            // one has read (x <= j)
+            const uint64_t kb = __ballot(act && key != 0xFFFFFFFFu);
+            if (act && key != 0xFFFFFFFFu) {
+                const uint32_t x = nout + popc(kb & lanemask_lt(lane));
+                TB[rev ? nd - 1 - x : x] = key;
+            }
+            nout += popc(kb);
+#else
+            if (act) TB[slot(j)] = key;
+#endif
         }
         wsync();
         ti = tend;
@@ -821,8 +842,10 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
     implicit = __ballot(imp) != 0;
     if (ti < nd) return 0;                            // skip counts beyond the read
     wsync();
+#if PF_K0_FUSEC
+    tb_off = rev ? nd - nout : 0u;
+#else
     // compaction in place (order kept)
-    uint32_t nout = 0;
     for (uint32_t c0 = 0; c0 < nd; c0 += 64) {
         const uint32_t jj = c0 + lane;
         const uint32_t key = jj < nd ? TB[jj] : 0xFFFFFFFFu;
@@ -831,6 +854,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
         nout += popc(pb);
     }
     wsync();
+#endif
     return nout;
 }
 
@@ -1388,7 +1412,9 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     }
     K0_STAMP(0);
     if (d.diag == 2u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
-    if (okmm && t.nd && !past) nT = k0_seq_pass(d, L, seq, len, rev, t, TB, lane, implicit);
+    uint32_t tb_off = 0;
+    if (okmm && t.nd && !past) nT = k0_seq_pass(d, L, seq, len, rev, t, TB, lane, implicit, tb_off);
+    TB = TB + uni(tb_off);                            // the compacted triggers start here
     K0_STAMP(1);
     if (d.diag == 3u || d.diag == 5u) { if (lane == 0) d.rec_n[r] = PF_NONE; return; }
     if (!okmm && d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_BADMM], 1ull);
