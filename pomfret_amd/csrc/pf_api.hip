@@ -1037,6 +1037,7 @@ extern "C" int pf_aln_build(pf_ctx_t *ctx, const pf_cfg_t *cfg, const pf_load_cf
 
 // host arrays -> device: the large arrays through the context's pinned
 // staging, SEQ repacked into 16-byte aligned, zero-padded slices on the way
+// (an odd length's pad nibble cleared too: pf_load.h)
 struct HostFill {
     const pf_aln_batch_t *a;
 };
@@ -1060,6 +1061,7 @@ static int host_fill(void *user, pf_ctx_t *ctx, pf_load_dev *ld, const uint64_t 
                     if (rel < sb) {
                         const uint64_t k = std::min(sb - rel, x1 - x);
                         memcpy(buf + (x - lo), a->seq + a->seq_off[r] + rel, k);
+                        if ((a->l_qseq[r] & 1u) && rel + k == sb) buf[x - lo + k - 1] &= 0xF0u;   // the pad nibble
                         x += k;
                     } else {
                         memset(buf + (x - lo), 0, x1 - x);

@@ -414,7 +414,8 @@ DEV void wcopy32(uint32_t *dst, const uint8_t *a, uint64_t src, uint64_t nw, uin
 }
 
 // the large arrays of the selected records (one wave each) at the batch's
-// offsets; SEQ slices are zero padded to their aligned size
+// offsets; SEQ slices are zero padded to their aligned size, an odd length's
+// pad nibble included (K0's counts rely on it: pf_load.h)
 __global__ __launch_bounds__(256) void pf_gather_big(const uint8_t *arena, const uint32_t *sel, uint64_t n, pf_recs_dev R,
                                                      const uint64_t *cig_off, uint32_t *cig, const uint64_t *seq_off,
                                                      uint8_t *seq, const uint64_t *mm_off, uint8_t *mm,
@@ -426,11 +427,13 @@ __global__ __launch_bounds__(256) void pf_gather_big(const uint8_t *arena, const
     const uint32_t k = sel[i];
     if (cig) wcopy32(cig + cig_off[i], arena, R.cig[k], R.ncig[k], lane);
     if (seq) {
-        const uint64_t sb = ((uint64_t)R.l_qseq[k] + 1) / 2, s0 = seq_off[i], s1 = seq_off[i + 1];
+        // whole bytes, then an odd length's last base with its pad nibble cleared
+        const uint64_t lq = R.l_qseq[k], full = lq / 2, sb = (lq + 1) / 2, s0 = seq_off[i], s1 = seq_off[i + 1];
         uint8_t *dst = seq + s0;
-        const uint64_t nw = (s0 & 3u) ? 0 : sb / 4;          // unaligned slices (the -u reads): bytes
+        const uint64_t nw = (s0 & 3u) ? 0 : full / 4;        // unaligned slices (the -u reads): bytes
         wcopy32(reinterpret_cast<uint32_t *>(dst), arena, R.seq[k], nw, lane);
-        for (uint64_t j = 4 * nw + lane; j < s1 - s0; j += 64) dst[j] = j < sb ? arena[R.seq[k] + j] : 0;
+        for (uint64_t j = 4 * nw + lane; j < s1 - s0; j += 64)
+            dst[j] = j < full ? arena[R.seq[k] + j] : j < sb ? (uint8_t)(arena[R.seq[k] + j] & 0xF0u) : 0;
     }
     if (mm && mm_off[i + 1] > mm_off[i]) wcopy(mm + mm_off[i], arena, R.mm[k], mm_off[i + 1] - mm_off[i], lane);
     if (ml && ml_off[i + 1] > ml_off[i]) wcopy(ml + ml_off[i], arena, R.ml[k], ml_off[i + 1] - ml_off[i], lane);

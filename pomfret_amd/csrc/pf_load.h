@@ -131,7 +131,9 @@ struct pf_load_dev {
 #ifdef __cplusplus
 /* placement of a record-level batch's large arrays (pf_aln_build, pf_api.hip):
  * fill() writes ld->cigar / mm / ml (sized by the batch's offsets) and the
- * SEQ slices (seq_off[r], 16-byte aligned, zero padded; seq_bytes total) */
+ * SEQ slices (seq_off[r], 16-byte aligned, zero padded; seq_bytes total).
+ * The pad nibble of an odd-length SEQ is written as 0 as well, so no nibble
+ * past l_qseq is C or G: K0's SEQ counts have no per-word tail test. */
 struct pf_ctx;
 struct pf_dbatch;
 typedef struct pf_aln_fill {

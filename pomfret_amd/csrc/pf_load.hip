@@ -97,6 +97,12 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_FUSEC
 #define PF_K0_FUSEC 1
 #endif
+// SEQ count without a per-word tail test (round 6): every nibble past the
+// record's SEQ is 0 in the slice, the odd-length pad nibble included (both
+// producers clear it: pf_load.h), and 0 is never a target
+#ifndef PF_K0_PADFIX
+#define PF_K0_PADFIX 1
+#endif
 #ifndef PF_K0_WPE
 #define PF_K0_WPE 8                        // pf_k0_load's waves per SIMD (register budget: 512 / WPE VGPRs)
 #endif
@@ -566,11 +572,16 @@ DEV_COLD bool k0_mm_ranks_swar(const uint32_t *gw, const uint8_t *mm, uint32_t m
 DEV uint64_t nibswap(uint64_t w) {                   // base i -> bits 4i..4i+3
     return ((w & 0x0F0F0F0F0F0F0F0Full) << 4) | ((w >> 4) & 0x0F0F0F0F0F0F0F0Full);
 }
-DEV uint64_t zero_nibbles(uint64_t x) {             // bit 4i set iff nibble i of x == 0
-    uint64_t a = (x | (x >> 1)) & 0x5555555555555555ull;
-    a = (a | (a >> 2)) & 0x1111111111111111ull;
-    return ~a & 0x1111111111111111ull;
+// bit 4i+3 set iff nibble i of x == 0: a nibble's low 3 bits + 7 carry into
+// its bit 3 unless they are 0 (no carry leaves the nibble), so bit 3 of the
+// sum | x is 0 exactly for a zero nibble (5 ops per 32 bits)
+DEV uint64_t zero_nibbles_hi(uint64_t x) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t zl = ~(((lo & 0x77777777u) + 0x77777777u) | lo) & 0x88888888u;
+    const uint32_t zh = ~(((hi & 0x77777777u) + 0x77777777u) | hi) & 0x88888888u;
+    return ((uint64_t)zh << 32) | zl;
 }
+DEV uint64_t zero_nibbles(uint64_t x) { return zero_nibbles_hi(x) >> 3; }   // bit 4i set iff nibble i of x == 0
 // index of the k-th (k < popcount) set nibble flag (bits 4i) of m, branch-free
 DEV uint32_t sel_nibble(uint64_t m, uint32_t k) {
     uint32_t lo = (uint32_t)m, base = 0;
@@ -644,12 +655,17 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             uint32_t c[2];
 #pragma unroll
             for (uint32_t h = 0; h < 2; h++) {
+#if PF_K0_PADFIX
+                (void)w;
+                c[h] = (uint32_t)__popcll(zero_nibbles_hi(xs[h] ^ pat));   // past the read: 0 nibbles, no targets
+#else
                 c[h] = 0;
                 if (w + h < nwords) {
-                    uint64_t z = zero_nibbles(xs[h] ^ pat);
-                    if ((w + h) * 16 + 16 > len) z = zero_nibbles(nibswap(xs[h]) ^ pat) & valid_nibbles(len - (w + h) * 16);
-                    c[h] = (uint32_t)__popcll(z);
+                    if ((w + h) * 16 + 16 > len)
+                        c[h] = (uint32_t)__popcll(zero_nibbles(nibswap(xs[h]) ^ pat) & valid_nibbles(len - (w + h) * 16));
+                    else c[h] = (uint32_t)__popcll(zero_nibbles_hi(xs[h] ^ pat));
                 }
+#endif
             }
             c0 = c[0];
             return c[0] + c[1];

@@ -26,7 +26,9 @@ def _compare(host, hqn, hinfo, db, dqn, dinfo):
     so = d["seq_off"]
     for i in range(host.n_recs):
         nb = (int(host.l_qseq[i]) + 1) // 2
-        a = host.seq[host.seq_off[i]:host.seq_off[i] + nb]
+        a = host.seq[host.seq_off[i]:host.seq_off[i] + nb].copy()
+        if host.l_qseq[i] & 1:
+            a[-1] &= 0xF0                              # the slice's pad nibble is 0 (pf_load.h)
         b = d["seq"][so[i]:so[i] + nb]
         assert np.array_equal(a, b), i
         assert not d["seq"][so[i] + nb:so[i + 1]].any()

@@ -190,6 +190,26 @@ def test_scratch_trigger_lists(oracle_lib, gpu_ctx):
     db.free()
 
 
+@pytest.mark.parametrize("pad", [0x2, 0x4, 0xF])
+def test_odd_length_pad_nibble(oracle_lib, gpu_ctx, pad):
+    """SEQ of an odd-length record ends in a pad nibble the SAM spec leaves
+    unspecified; htslib's loops (and the oracle's) stop at l_qseq, so the pad
+    is never a base.  Pads set to C (2), G (4) and N (15) - the bases K0's
+    count and placement look for - leave the calls unchanged."""
+    from pomfret_amd import Config, LoadConfig
+    from tests._aln_cases import synth_aln
+    aln = synth_aln(3, 30, 23)
+    lq = np.asarray(aln.l_qseq, np.int64)
+    odd = np.flatnonzero(lq & 1)
+    assert odd.size > 10
+    seq = aln.seq.copy()
+    last = aln.seq_off[odd].astype(np.int64) + (lq[odd] >> 1)
+    seq[last] = (seq[last] & 0xF0) | pad
+    aln.seq = seq
+    db, _ = _check_calls(oracle_lib, gpu_ctx, Config(), LoadConfig(), aln, f"pad{pad}")
+    db.free()
+
+
 @pytest.mark.parametrize("seed", [17, 18, 19])
 def test_mm_parser_fuzz(oracle_lib, gpu_ctx, seed):
     """MM/ML texts of 1-6 KB with every layout and malformation of
