@@ -103,6 +103,14 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_PADFIX
 #define PF_K0_PADFIX 1
 #endif
+// SEQ placement (round 6): 1 = a trigger takes its own word only (4
+// ds_bpermute per row); the neighbour word, needed for the context base of a
+// trigger at the word's last (forward) / first (reverse) base, is fetched
+// afterwards for those triggers alone (1 in 16); 0 = every trigger takes its
+// word and the neighbour pair (6 ds_bpermute and 2 readlanes per row)
+#ifndef PF_K0_NBRARE
+#define PF_K0_NBRARE 1
+#endif
 #ifndef PF_K0_WPE
 #define PF_K0_WPE 8                        // pf_k0_load's waves per SIMD (register budget: 512 / WPE VGPRs)
 #endif
@@ -403,12 +411,13 @@ DEV uint32_t pack4(uint32_t f) {                     // 0x80 byte flags -> 4-bit
 }
 // digit x 10^e table (index digit << 3 | e, digits 0..9), in the wave's
 // spare LDS during the MM phase
+DEV uint32_t k0_dw(uint32_t i) {                     // (i >> 3) x 10^(i & 7), branch-free
+    const uint32_t e = i & 7u;
+    return (i >> 3) * ((e & 1u) ? 10u : 1u) * ((e & 2u) ? 100u : 1u) * ((e & 4u) ? 10000u : 1u);
+}
 DEV void k0_dw_table(uint32_t *tbl, uint32_t lane) {
-    for (uint32_t i = lane; i < 80; i += 64) {
-        uint32_t v = i >> 3;
-        for (uint32_t e = 0; e < (i & 7u); e++) v *= 10u;
-        tbl[i] = v;
-    }
+    tbl[lane] = k0_dw(lane);
+    if (lane < 16u) tbl[64u + lane] = k0_dw(64u + lane);
 }
 
 template <typename TP>
@@ -776,6 +785,74 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             if (act) {
                 const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(((uint64_t)xv.y << 32) | xv.x);
                 const uint64_t xn = nibswap(((uint64_t)nv.y << 32) | nv.x);
+#elif PF_K0_NBRARE
+            // The trigger's word comes from the registers of the lane that
+            // loaded it (ds_bpermute): lane Lw of row i holds words 2Lw (x, y)
+            // and 2Lw+1 (z, w).
+            uint32_t x0 = 0, x1 = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < ROWS; q++) {
+                const bool mine = i == q;
+                if (!__ballot(mine)) continue;
+                const int sl = (int)((mine ? Lw : lane) << 2);
+                const uint32_t a0 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].x);
+                const uint32_t a1 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].y);
+                const uint32_t a2 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].z);
+                const uint32_t a3 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)v[q].w);
+                if (mine) {
+                    x0 = hw ? a2 : a0;
+                    x1 = hw ? a3 : a1;
+                }
+            }
+            const uint32_t w = b * BW + i * RW + 2 * Lw + hw;
+            const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(((uint64_t)x1 << 32) | x0);
+            const uint32_t bi = act ? sel_nibble(zero_nibbles(xw ^ pat), k) : 0u;
+            // The context base: inside the word, or -- for the word's last base
+            // (forward) / first base (reverse) -- the neighbour word's first /
+            // last base: the pair's other word, the next / previous pair (lane
+            // Lw +- 1), the next / previous row's edge pair, or past the
+            // block's edge a byte of SEQ.
+            const bool atedge = act && (rev ? bi == 0 : bi == 15);
+            uint32_t cb = (uint32_t)(xw >> (4 * ((rev ? bi - 1u : bi + 1u) & 15u))) & 15u;   // edge lanes: below
+            if (__ballot(atedge)) {
+                const uint32_t p = w * 16 + bi;
+                const bool inpair = rev ? hw != 0 : hw == 0;     // the pair's other word
+                uint32_t n0 = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < ROWS; q++) {
+                    const bool mine = atedge && i == q;
+                    if (!__ballot(mine)) continue;
+                    // the word holding the context base: forward the next word's
+                    // first base (byte 0 high nibble), reverse the previous
+                    // word's last base (byte 7 low nibble)
+                    const uint32_t nl = inpair ? Lw : rev ? Lw - 1u : Lw + 1u;   // out of the row: 64 or ~0
+                    const int snl = (int)(((mine && nl < 64u) ? nl : lane) << 2);
+                    // forward: the low dword of word 2nl+1 (z, the pair's other
+                    // word) or of word 2nl (x, the next pair); reverse: the high
+                    // dword of word 2nl (y) or 2nl+1 (w).  ds_bpermute's source
+                    // operand is one VGPR for all lanes, so both are taken.
+                    const uint32_t e0 = (uint32_t)__builtin_amdgcn_ds_bpermute(snl, (int)(rev ? v[q].y : v[q].z));
+                    const uint32_t e1 = (uint32_t)__builtin_amdgcn_ds_bpermute(snl, (int)(rev ? v[q].w : v[q].x));
+                    uint32_t r = 0;
+                    bool redge = true;                          // past the block
+                    if (!rev && q + 1 < ROWS) { r = rdl(v[q + 1 < ROWS ? q + 1 : q].x, 0); redge = false; }
+                    if (rev && q > 0) { r = rdl(v[q > 0 ? q - 1 : q].w, 63); redge = false; }
+                    if (mine) {
+                        if (inpair) n0 = e0;
+                        else if (nl < 64u) n0 = e1;
+                        else if (!redge) n0 = r;
+                        else n0 = 0xFFFFFFFFu;                  // marker: read SEQ
+                    }
+                }
+                if (atedge) {
+                    // forward: byte 0 of the next word, high nibble; reverse:
+                    // byte 7 of the previous word (byte 3 of its high dword),
+                    // low nibble
+                    if (n0 == 0xFFFFFFFFu) cb = p > 0 && p < len - 1 ? (rev ? nib(seq, p - 1) : nib(seq, p + 1)) : 0u;
+                    else cb = rev ? (n0 >> 24) & 15u : (n0 >> 4) & 15u;
+                }
+            }
+            if (act) {
 #else
             // The trigger's word and its neighbour word (the context base at a
             // word edge) come from the registers of the lane that loaded them
@@ -821,14 +898,20 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
                 const uint64_t xw = d.diag == 1u ? 0x2222222222222222ull : nibswap(((uint64_t)x1 << 32) | x0);
                 const uint64_t xn = nibswap(((uint64_t)n1 << 32) | n0);
 #endif
+#if !PF_K0_NBRARE || PF_K0_SEQ_REREAD
                 const uint32_t bi = sel_nibble(zero_nibbles(xw ^ pat), k);
+#endif
                 const uint32_t p = w * 16 + bi;
                 if (p > 0 && p < len - 1) {
                     bool ctx;
+#if PF_K0_NBRARE && !PF_K0_SEQ_REREAD
+                    ctx = cb == (rev ? NT_C : NT_G);
+#else
                     if (!rev) ctx = (bi < 15 ? (uint32_t)(xw >> (4 * (bi + 1))) & 15u
                                              : edge ? nib(seq, p + 1) : (uint32_t)xn & 15u) == NT_G;
                     else ctx = (bi > 0 ? (uint32_t)(xw >> (4 * (bi - 1))) & 15u
                                        : edge ? nib(seq, p - 1) : (uint32_t)(xn >> 60) & 15u) == NT_C;
+#endif
                     if (ctx) {
                         const uint32_t q = e >> 24;
                         key = (p << 2) | (q < d.lo ? 1u : q >= d.hi ? 0u : 2u);

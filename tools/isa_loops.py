@@ -4,7 +4,10 @@ persistent problem loop is depth 1), its instructions with all its child
 loops', SALU, LDS, and the SGPR-spill traffic -- v_writelane into, and
 v_readlane out of, the VGPRs the compiler spills SGPRs to.
 
-    python tools/isa_loops.py <listing.s> <kernel-name-substring> [top]
+    python tools/isa_loops.py <listing.s> <kernel-name-substring> [top] [depth]
+
+(depth: the loop depth grouped on, 2 by default -- under a persistent loop;
+1 for a kernel without one)
 """
 import collections
 import re
@@ -17,7 +20,7 @@ def kernel_body(lines, name):
     return lines[st:en]
 
 
-def loop_stats(body):
+def loop_stats(body, depth=2):
     spillv = {m.group(1) for l in body for m in [re.match(r"\s*v_writelane_b32 (v\d+),", l)] if m}
     top2, stats, hdr = {}, collections.defaultdict(collections.Counter), ("none", 0)
     for i, l in enumerate(body):
@@ -34,10 +37,10 @@ def loop_stats(body):
             elif h:
                 lab, d = l.split(":")[0][2:], int(h.group(1))
                 hdr = (lab, d)
-                if d == 2:
+                if d == depth:
                     top2[lab] = lab
                 for p, pd in re.findall(r"Parent Loop (BB\d+_\d+) Depth=(\d+)", txt):
-                    if int(pd) == 2:
+                    if int(pd) == depth:
                         top2[lab] = p
             else:
                 hdr = ("none", 0)
@@ -54,15 +57,15 @@ def loop_stats(body):
         c["spill_stores"] += op == "v_writelane_b32"
     agg = collections.defaultdict(collections.Counter)
     for (h, d), c in stats.items():
-        if d >= 2:
+        if d >= depth:
             agg[top2.get(h, "?")].update(c)
     return sorted(spillv), agg
 
 
 if __name__ == "__main__":
     body = kernel_body(open(sys.argv[1]).read().split("\n"), sys.argv[2])
-    spillv, agg = loop_stats(body)
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 12
+    spillv, agg = loop_stats(body, int(sys.argv[4]) if len(sys.argv) > 4 else 2)
     print(f"{sys.argv[2]}: SGPR spill VGPRs {spillv}")
     for h, c in sorted(agg.items(), key=lambda x: -x[1]["instrs"])[:top]:
         print(f"  loop {h:10s} " + " ".join(f"{k} {c[k]}" for k in ("instrs", "salu", "lds", "spill_reloads", "spill_stores")))
