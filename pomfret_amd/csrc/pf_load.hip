@@ -111,6 +111,12 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_NBRARE
 #define PF_K0_NBRARE 1
 #endif
+// emission (round 6): 1 = when the kept calls are lanes 0..n-1, each call's
+// predecessor by DPP wave_shr:1 instead of a ds_bpermute from the previous
+// kept lane
+#ifndef PF_K0_EMITDPP
+#define PF_K0_EMITDPP 1
+#endif
 #ifndef PF_K0_WPE
 #define PF_K0_WPE 8                        // pf_k0_load's waves per SIMD (register budget: 512 / WPE VGPRs)
 #endif
@@ -989,9 +995,20 @@ DEV void k0_emit_lanes(const pf_load_dev &d, K0Out &o, bool keep, uint32_t v, ui
     const uint32_t cnt = popc(bk);
     const uint64_t below = bk & lanemask_lt(lane);
     const uint32_t idx = popc(below);
-    const uint32_t pl = below ? 63u - (uint32_t)__clzll(below) : lane;
-    const uint32_t vprev_l = (uint32_t)__shfl((int)v, (int)pl, 64);
-    const uint32_t vprev = below ? vprev_l : o.last;
+    uint32_t vprev;
+#if PF_K0_EMITDPP
+    if ((bk & (bk + 1u)) == 0) {
+        // the kept lanes are lanes 0..cnt-1 (the walk's usual case): the
+        // previous call is the previous lane's (DPP wave_shr:1), lane 0's the
+        // last one pushed
+        vprev = (uint32_t)__builtin_amdgcn_update_dpp((int)o.last, (int)v, 0x138, 0xF, 0xF, false);
+    } else
+#endif
+    {
+        const uint32_t pl = below ? 63u - (uint32_t)__clzll(below) : lane;
+        const uint32_t vprev_l = (uint32_t)__shfl((int)v, (int)pl, 64);
+        vprev = below ? vprev_l : o.last;
+    }
     const bool has_prev = below != 0 || o.n > 0;
     if (__ballot(keep && has_prev && v == vprev)) {
         if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_DUPCHUNK], 1ull);
