@@ -111,6 +111,11 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_NBRARE
 #define PF_K0_NBRARE 1
 #endif
+// MM entries (round 6): 1 = a one-code header ("C+m?") parsed from one
+// 4-byte window instead of byte by byte
+#ifndef PF_K0_HDRFAST
+#define PF_K0_HDRFAST 1
+#endif
 // emission (round 6): 1 = when the kept calls are lanes 0..n-1, each call's
 // predecessor by DPP wave_shr:1 instead of a ds_bpermute from the previous
 // kept lane
@@ -315,7 +320,33 @@ DEV bool k0_mm_entries(const uint32_t *gw, const uint8_t *mm, uint32_t mis, uint
         return mm[x];
     };
     K0Hdr H;
+#if PF_K0_HDRFAST
+    auto dword_at = [&](uint32_t kx) -> uint32_t {    // text dword kx (uniform)
+        if (kx - k0 < 64) return rdl(w, kx - k0);
+        if (kx - k0 < 128) return rdl(pw, kx - k0 - 64);
+        return gw[min(kx, kmaxw)];
+    };
+#endif
     auto header = [&](uint32_t i) {                   // base, strand, codes, '.'/'?' (the entry's ';' stops every loop)
+#if PF_K0_HDRFAST
+        // one code ("C+m?", "C+h.", "C+m,"): bytes i..i+3 at once; anything
+        // else (several codes, a ChEBI number, a header at the text's end)
+        // takes the byte loop below, which gives the same fields
+        if (i + 3 < mlen) {
+            const uint32_t x = mis + i, kx = x >> 2, sh = 8u * (x & 3u);
+            const uint32_t lo = dword_at(kx);
+            const uint32_t b4 = sh ? (lo >> sh) | (dword_at(kx + 1) << (32u - sh)) : lo;
+            const uint32_t c2 = (b4 >> 16) & 0xFFu, c3 = b4 >> 24;
+            if (is_alpha(c2) && !is_alpha(c3)) {
+                H.base = b4 & 0xFFu;
+                H.strand = (b4 >> 8) & 0xFFu;
+                H.nc = 1;
+                H.mi = c2 == 'm' ? 0 : -1;
+                H.h = i + 3 + ((c3 == '.' || c3 == '?') ? 1u : 0u);
+                return;
+            }
+        }
+#endif
         H.base = byte_at(i);
         H.strand = i + 1 < mlen ? byte_at(i + 1) : 0u;
         uint32_t h = i + 2, nc = 0;
