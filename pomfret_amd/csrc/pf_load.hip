@@ -129,6 +129,10 @@ DEV unsigned long long k0_now() {
 DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 DEV uint64_t lanemask_lt(uint32_t lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 DEV uint32_t popc(uint64_t m) { return (uint32_t)__popcll(m); }
+// set bits of b below this lane (popc(b & lanemask_lt(lane)) in two mbcnt)
+DEV uint32_t below_cnt(uint64_t b) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
 DEV uint32_t rdl(uint32_t x, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l); }
 
 DEV void wsync() {
@@ -723,7 +727,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             L.u.s.sc[i * 64 + lane] = (uint8_t)c0a;
             L.u.s.sc[(i + 1) * 64 + lane] = (uint8_t)c0b;
             const uint32_t inc = wscan(ca | (cb << 16), lane);
-            const uint32_t tot = uni(__shfl(inc, 63, 64));
+            const uint32_t tot = rdl(inc, 63);
             pref[i] = run;
             const uint32_t ba = run + (inc & 0xFFFFu) - ca;
             L.u.s.sb[i * 64 + lane] = (uint16_t)ba;
@@ -963,7 +967,7 @@ DEV uint32_t k0_seq_pass(const pf_load_dev &d, K0W &L, const uint8_t *seq, uint3
             // one has read (x <= j)
             const uint64_t kb = __ballot(act && key != 0xFFFFFFFFu);
             if (act && key != 0xFFFFFFFFu) {
-                const uint32_t x = nout + popc(kb & lanemask_lt(lane));
+                const uint32_t x = nout + below_cnt(kb);
                 TB[rev ? nd - 1 - x : x] = key;
             }
             nout += popc(kb);
@@ -1024,8 +1028,7 @@ DEV void k0_emit_lanes(const pf_load_dev &d, K0Out &o, bool keep, uint32_t v, ui
     const uint64_t bk = __ballot(keep);
     if (!bk) return;
     const uint32_t cnt = popc(bk);
-    const uint64_t below = bk & lanemask_lt(lane);
-    const uint32_t idx = popc(below);
+    const uint32_t idx = below_cnt(bk);                // kept lanes below this one
     uint32_t vprev;
 #if PF_K0_EMITDPP
     if ((bk & (bk + 1u)) == 0) {
@@ -1036,25 +1039,30 @@ DEV void k0_emit_lanes(const pf_load_dev &d, K0Out &o, bool keep, uint32_t v, ui
     } else
 #endif
     {
+        const uint64_t below = bk & lanemask_lt(lane);
         const uint32_t pl = below ? 63u - (uint32_t)__clzll(below) : lane;
         const uint32_t vprev_l = (uint32_t)__shfl((int)v, (int)pl, 64);
         vprev = below ? vprev_l : o.last;
     }
-    const bool has_prev = below != 0 || o.n > 0;
-    if (__ballot(keep && has_prev && v == vprev)) {
-        if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_DUPCHUNK], 1ull);
-        if (keep) { sv[idx] = v; sc[idx] = (uint8_t)(cat | (imp ? 0x80u : 0u)); }
-        wsync();
-        K0Out s = o;
-        if (lane == 0)
-            for (uint32_t q = 0; q < cnt; q++) k0_emit_one<MODE>(s, sv[q], sc[q] & 3u, (sc[q] & 0x80u) != 0);
-        k0_bcast(o, s);
-        wsync();
-        return;
+    const bool has_prev = idx > 0 || o.n > 0;
+    // one ballot for the three rare cases: a repeated position, a position
+    // below its predecessor, a position past 2^29
+    if (__ballot(keep && ((has_prev && v <= vprev) || v >= (1u << 29)))) {
+        if (__ballot(keep && has_prev && v == vprev)) {
+            if (d.ctr && lane == 0) atomicAdd(&d.ctr[PF_K0C_DUPCHUNK], 1ull);
+            if (keep) { sv[idx] = v; sc[idx] = (uint8_t)(cat | (imp ? 0x80u : 0u)); }
+            wsync();
+            K0Out s = o;
+            if (lane == 0)
+                for (uint32_t q = 0; q < cnt; q++) k0_emit_one<MODE>(s, sv[q], sc[q] & 3u, (sc[q] & 0x80u) != 0);
+            k0_bcast(o, s);
+            wsync();
+            return;
+        }
+        if (__ballot(keep && has_prev && v < vprev)) o.sorted = 0;
+        if (__ballot(keep && v >= (1u << 29))) o.lim = 1;
     }
     if (MODE && keep) { o.pos[o.n + idx] = v; o.cat[o.n + idx] = (uint8_t)cat; }
-    if (__ballot(keep && has_prev && v < vprev)) o.sorted = 0;
-    if (__ballot(keep && v >= (1u << 29))) o.lim = 1;
     const uint32_t fl = (uint32_t)__ffsll((long long)bk) - 1, ll = 63u - (uint32_t)__clzll(bk);
     if (o.n == 0) o.first = rdl(v, fl);
     o.last = rdl(v, ll);
@@ -1218,7 +1226,7 @@ DEV_COLD void k0_chunk_implicit(const pf_load_dev &d, K0W &L, uint32_t nv, uint3
             M.iP[inc - kept + i] = pp[i];
             M.iV[inc - kept + i] = vv[i];
         }
-        ni = uni(__shfl(inc, 63, 64));
+        ni = rdl(inc, 63);
     }
     wsync();
     const uint32_t nm = ne + ni;
@@ -1302,8 +1310,8 @@ DEV bool k0_walk(const pf_load_dev &d, K0W &L, const uint32_t *cig, uint32_t nci
         // the merge lists this shares)
         if (!implicit && (lane & 7u) == 7u) L.u.mg.eP[lane >> 3] = oe;
 #endif
-        const uint32_t a_end = a_cur + uni(__shfl(rin, 63, 64));
-        const uint32_t off_end = off_cur + uni(__shfl(din, 63, 64));
+        const uint32_t a_end = a_cur + rdl(rin, 63);
+        const uint32_t off_end = off_cur + rdl(din, 63);
         wsync();
         if (!implicit) {
             // the triggers this tile consumes (p <= a_end), 64 at a time
@@ -1641,7 +1649,7 @@ DEV void k0_record(const pf_load_dev &d, K0W &L, const K0Rec &R, uint32_t lane, 
     uint32_t rlen = racc;
     if (!walked)
         for (uint32_t c = lane; c < ncig; c += 64) rlen += k0_refc(cig[c]);
-    rlen = uni(__shfl(wscan(rlen, lane), 63, 64));
+    rlen = rdl(wscan(rlen, lane), 63);
     if (lane < 8) {                                   // the record's row: one 32-byte store
         const uint32_t v = lane == 0 ? qs : lane == 1 ? qs + rlen : lane == 2 ? o.first : lane == 3 ? o.last
                          : lane == 4 ? (uint32_t)cb : lane == 5 ? (uint32_t)(cb >> 32) : 0u;
