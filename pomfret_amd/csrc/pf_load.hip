@@ -111,6 +111,11 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_NBRARE
 #define PF_K0_NBRARE 1
 #endif
+// MM ranks (round 6): 1 = one text load per lane and row, the neighbour
+// words' non-digit flags by DPP; 0 = three loads per lane and row
+#ifndef PF_K0_RANKDPP
+#define PF_K0_RANKDPP 1
+#endif
 // MM entries (round 6): 1 = a one-code header ("C+m?") parsed from one
 // 4-byte window instead of byte by byte
 #ifndef PF_K0_HDRFAST
@@ -480,13 +485,29 @@ DEV bool k0_mm_ranks(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const 
     // masked below
     const uint32_t kmaxw = (wend - 1) / 4 + 2;
     auto ld = [&](uint32_t k) { return gw[min(k, kmaxw)]; };
+#if PF_K0_RANKDPP
+    // one load per lane and row, two rows in flight; the next two words'
+    // non-digit flags come from lanes + 1, + 2 (DPP wave_shl:1), the row's
+    // last lanes taking the next row's first two
+    uint32_t w = ld(k0s + lane), pw = ld(k0s + lane + 64);
+    uint32_t nd0 = pack4(nondigit4(w));
+#else
     uint32_t w = ld(k0s + lane), wn = ld(k0s + lane + 1), wn2 = ld(k0s + lane + 2);
+#endif
     for (uint32_t k0 = k0s; 4 * k0 < wend; k0 += 64) {
         const uint32_t k = k0 + lane;
+#if PF_K0_RANKDPP
+        const uint32_t ppw = ld(k + 128);             // two rows ahead, in flight
+        const uint32_t ndn = pack4(nondigit4(pw));
+        const uint32_t nd1 = (uint32_t)__builtin_amdgcn_update_dpp((int)rdl(ndn, 0), (int)nd0, 0x130, 0xF, 0xF, false);
+        const uint32_t nd2 = (uint32_t)__builtin_amdgcn_update_dpp((int)rdl(ndn, 1), (int)nd1, 0x130, 0xF, 0xF, false);
+        const uint32_t ndm = nd0 | (nd1 << 4) | (nd2 << 8);
+#else
         const uint32_t pw = ld(k + 64), pwn = ld(k + 65), pwn2 = ld(k + 66);   // the next row, in flight
+        const uint32_t ndm = pack4(nondigit4(w)) | (pack4(nondigit4(wn)) << 4) | (pack4(nondigit4(wn2)) << 8);
+#endif
         const int32_t b = (int32_t)(4 * k) - (int32_t)mis;
         const uint32_t nlo = (uint32_t)min(max((int32_t)lo - b, 0), 4);
-        const uint32_t ndm = pack4(nondigit4(w)) | (pack4(nondigit4(wn)) << 4) | (pack4(nondigit4(wn2)) << 8);
         const uint32_t cw = pack4(bytes_eq(w, ','));
         uint32_t M, vb, cb;
         for (;;) {
@@ -506,8 +527,10 @@ DEV bool k0_mm_ranks(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const 
         x8 &= x8 >> 4;                                // bit j: bytes j..j+7 all digits
         const uint32_t db = D & vb;                   // the word's digits
         const bool badc = (cb & (M >> 1)) != 0;       // a comma not followed by a digit
-        if (__ballot((x8 & db) != 0)) return k0_mm_ranks_swar(gw, mm, mis, t, rev, TB, lane);
-        if (__ballot(badc)) return false;
+        if (__ballot((x8 & db) != 0 || badc)) {       // rare: one ballot for both
+            if (__ballot((x8 & db) != 0)) return k0_mm_ranks_swar(gw, mm, mis, t, rev, TB, lane);
+            return false;
+        }
         uint32_t c[4];
 #pragma unroll
         for (uint32_t j = 0; j < 4; j++) {            // branch-free: every lane weighs all 4 bytes
@@ -535,7 +558,11 @@ DEV bool k0_mm_ranks(const uint32_t *gw, const uint8_t *mm, uint32_t mis, const 
         if (__ballot(ovf)) return false;
         carry += (uint64_t)rdl(sincl, 63);
         kk += rdl(cincl, 63);
+#if PF_K0_RANKDPP
+        w = pw; pw = ppw; nd0 = ndn;
+#else
         w = pw; wn = pwn; wn2 = pwn2;
+#endif
     }
     if (kk != t.nd) return false;                     // commas after a stray byte
     const uint64_t last = carry + (t.nd - 1);
