@@ -116,6 +116,11 @@ DEV unsigned long long k0_now() {
 #ifndef PF_K0_RANKDPP
 #define PF_K0_RANKDPP 1
 #endif
+// pack (round 6): 1 = each wave's next 512-call chunk loaded before the
+// current chunk is stored
+#ifndef PF_PACK_PIPE
+#define PF_PACK_PIPE 1
+#endif
 // MM entries (round 6): 1 = a one-code header ("C+m?") parsed from one
 // 4-byte window instead of byte by byte
 #ifndef PF_K0_HDRFAST
@@ -1851,7 +1856,11 @@ __global__ __launch_bounds__(PF_SCAN_THREADS) void pf_k0_scan(pf_load_dev d) {
 // pack: one workgroup per window.  Kept records become reads in record
 // order; their scalars move to the read arrays and their calls from the
 // staging slices to the window's contiguous run (one wave per read).
+#if PF_PACK_PIPE
+__global__ __launch_bounds__(PF_PACK_THREADS) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_pack(pf_load_dev d) {
+#else
 __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
+#endif
     constexpr uint32_t NT = PF_PACK_THREADS, NW = NT / 64;
     __shared__ uint32_t sh32[2 * NW];
     __shared__ uint32_t l_n[NT];
@@ -1894,6 +1903,47 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
             l_dst[ek] = co;
         }
         __syncthreads();
+#if PF_PACK_PIPE
+        // one wave per read, 256-call chunks (4 calls per lane); the next
+        // chunk's loads are issued before this chunk's stores, so a wave's
+        // chunks overlap one memory round trip with the next (two chunks in
+        // registers: the kernel keeps 8 waves per SIMD)
+        {
+            constexpr uint32_t U = 4;
+            uint32_t j = wid, c0 = 0;
+            uint32_t pv[U];
+            uint8_t cv[U];
+            auto load = [&](uint32_t jj, uint32_t cc, uint32_t *p8, uint8_t *q8) {
+                const uint32_t cn = l_n[jj];
+                const uint64_t s = l_src[jj];
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    const uint32_t c = cc + u * 64 + lane;
+                    p8[u] = c < cn ? d.stage_pos[s + c] : 0u;
+                    q8[u] = c < cn ? d.stage_cat[s + c] : (uint8_t)0;
+                }
+            };
+            if (j < tk) load(j, 0, pv, cv);
+            while (j < tk) {
+                uint32_t jn = j, cn0 = c0 + U * 64;
+                if (cn0 >= l_n[j]) { jn = j + NW; cn0 = 0; }
+                uint32_t pn[U];
+                uint8_t qn[U];
+                if (jn < tk) load(jn, cn0, pn, qn);
+                const uint32_t cn = l_n[j];
+                const uint64_t t = l_dst[j];
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) {
+                    const uint32_t c = c0 + u * 64 + lane;
+                    if (c < cn) { d.call_pos[t + c] = pv[u]; d.call_cat[t + c] = cv[u]; }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) { pv[u] = pn[u]; cv[u] = qn[u]; }
+                j = jn;
+                c0 = cn0;
+            }
+        }
+#else
         // one wave per read, 8 calls per lane in flight (loads before stores)
         for (uint32_t j = wid; j < tk; j += NW) {
             const uint32_t cn = l_n[j];
@@ -1914,6 +1964,7 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
                 }
             }
         }
+#endif
         __syncthreads();
         kc += tk;
         ccarry += tc;
