@@ -17,8 +17,9 @@ The job: BASELINE.json's target is quoted on HG002 60x (a whole genome) at
 -c (cov_for_selection 7, cov_for_runtime 14, n_cand 16; blockjoin.c:
 4373-4375), loader defaults -q 10 -L 15000, ML bands 100/156 (cli.c:52-63).
 A GPU's share of the job is a list of record-level batches (<= 1024 windows
-each) dealt over --split (2) contexts of the GPU -- what the driver does with
-its PF_DEV_CONTEXTS contexts per GPU -- and every step launches all of them.
+each, and at least --min-batches (2)) dealt over --split (4) contexts of the
+GPU -- what the driver does with its PF_DEV_CONTEXTS contexts per GPU -- and
+every step launches all of them.
 The first batch alone gives the per-kernel figures and the roofline.
 `--calls-level` times the previous boundary instead (reads and 5mC calls
 resident, no K0).  --coverage 30 --windows 256 is configs[1]'s shape.
@@ -540,9 +541,13 @@ def main():
                     help="windows of the end-to-end (BAM file -> decisions) leg; 0 skips it")
     ap.add_argument("--e2e-u-scale", type=float, default=1.0,
                     help="genome scale of the configs[3]-shaped -u leg (1.0: 96 Mb, ~1,000 windows); 0 skips it")
-    ap.add_argument("--split", type=int, default=2,
+    ap.add_argument("--split", type=int, default=4,
                     help="contexts per GPU (the driver's PF_DEV_CONTEXTS): the rank's batches are dealt over "
-                         "them and launched together every step")
+                         "them and launched together every step (round 6: 4, since a context's second stream "
+                         "is created on first use and four contexts fit the device's four hardware queues)")
+    ap.add_argument("--min-batches", type=int, default=2,
+                    help="a share of fewer batches is cut into this many (a 1024-window share at N=8: two "
+                         "512-window batches, not four of 256)")
     ap.add_argument("--stagger", type=int, default=0,
                     help="1: every context but the first starts with its first batch cut in two halves, so "
                          "the contexts' kernels run out of phase (round 5: 117.1 vs 114.0 ms per step, slower; off)")
@@ -603,7 +608,8 @@ def main():
         parts = lpt_partition(job_costs, world)
         share = parts[rank]
         loads = [float(job_costs[p].sum()) for p in parts]
-    groups = split_groups(group_copies(share, n_base), split, base_costs)
+    min_batches = max(1, min(args.min_batches, split))
+    groups = split_groups(group_copies(share, n_base), min_batches, base_costs)
     gctx = [gi % split for gi in range(len(groups))]
     if args.stagger and split > 1 and len(groups) > split:
         groups, gctx = stagger_groups(groups, gctx, split, base_costs)
@@ -795,7 +801,7 @@ def main():
         proj = {}
         for n in (2, 4, 8):
             parts_n = lpt_partition(job_costs, n)
-            g_n = split_groups(group_copies(parts_n[0], n_base), split, base_costs)
+            g_n = split_groups(group_copies(parts_n[0], n_base), min_batches, base_costs)
             extra, dbs_n = [], []
             for gi, (_, basew) in enumerate(g_n):
                 hit = next((d for d, (_, bw) in zip(dbs, groups) if np.array_equal(bw, basew)), None)
@@ -831,7 +837,7 @@ def main():
         mine = sorted(parts_d[0].tolist())
         a_d = make_aln_batch(spec, jobs=[djobs[i] for i in mine], workers=0)
         dc_d = aln_window_costs(a_d)
-        g_d = split_groups([(np.arange(a_d.n_windows), np.arange(a_d.n_windows))], split, dc_d)
+        g_d = split_groups([(np.arange(a_d.n_windows), np.arange(a_d.n_windows))], min_batches, dc_d)
         dbs_d = [ctxs[gi % split].upload_aln(cfg, a_d.select(bw) if bw.shape[0] != a_d.n_windows else a_d, lcfg)
                  for gi, (_, bw) in enumerate(g_d)]
         t_gen = time.perf_counter() - td

@@ -207,7 +207,7 @@ extern "C" int pf_ctx_create(int device, pf_ctx_t **out) {
     pf_ctx *c = new pf_ctx();
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    c->stream2 = nullptr;                             // on first use (pf_ctx_stream2)
     c->stream3 = nullptr;
     c->heavy_ms = -1.0f;
     for (int i = 0; i <= PF_NKERN; i++) HIPCHK(hipEventCreate(&c->ev[i]));
@@ -239,8 +239,23 @@ extern "C" int pf_selftest(pf_ctx_t *ctx, uint64_t *mismatches) {
 
 extern "C" int pf_ctx_device(const pf_ctx *c) { return c->device; }
 extern "C" hipStream_t pf_ctx_stream(const pf_ctx *c) { return c->stream; }
-extern "C" hipStream_t pf_ctx_stream2(const pf_ctx *c) { return c->stream2; }
 static std::mutex g_stream3_mu;
+// The second stream (the heavy greedy problems, the fetch's copies) is created
+// on first use: HIP gives each stream a hardware queue until the device's
+// queues (GPU_MAX_HW_QUEUES, 4 here) run out and then shares them, so an idle
+// second stream per context would take a queue another context's work needs.
+extern "C" hipStream_t pf_ctx_stream2(const pf_ctx *c) {
+    pf_ctx *m = const_cast<pf_ctx *>(c);
+    std::lock_guard<std::mutex> lk(g_stream3_mu);
+    if (!m->stream2) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != m->device) (void)hipSetDevice(m->device);
+        if (hipStreamCreateWithFlags(&m->stream2, hipStreamNonBlocking) != hipSuccess) m->stream2 = nullptr;
+        if (cur >= 0 && cur != m->device) (void)hipSetDevice(cur);
+    }
+    return m->stream2 ? m->stream2 : m->stream;
+}
 extern "C" hipStream_t pf_ctx_stream3(const pf_ctx *c) {
     // created on first use, on the context's device (whatever device the
     // calling thread has current), under a lock: any thread may ask first
@@ -262,7 +277,7 @@ extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n) {
     if (c->stage_cap < n) {
         if (c->stage) {
             (void)hipStreamSynchronize(c->stream);
-            (void)hipStreamSynchronize(c->stream2);
+            if (c->stream2) (void)hipStreamSynchronize(c->stream2);
             (void)hipHostFree(c->stage);
         }
         c->stage = nullptr;
@@ -280,7 +295,7 @@ extern "C" uint8_t *pf_ctx_stage(pf_ctx *c, size_t n) {
 extern "C" void pf_ctx_stage_trim(pf_ctx *c, size_t keep) {
     if (c->stage && c->stage_cap > keep) {
         (void)hipStreamSynchronize(c->stream);
-        (void)hipStreamSynchronize(c->stream2);
+        if (c->stream2) (void)hipStreamSynchronize(c->stream2);
         (void)hipHostFree(c->stage);
         c->stage = nullptr;
         c->stage_cap = 0;
@@ -295,7 +310,10 @@ extern "C" void pf_ctx_destroy(pf_ctx_t *c) {
     (void)hipStreamSynchronize(c->stream);
     for (int i = 0; i <= PF_NKERN; i++) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
-    (void)hipStreamDestroy(c->stream2);
+    if (c->stream2) {
+        (void)hipStreamSynchronize(c->stream2);
+        (void)hipStreamDestroy(c->stream2);
+    }
     if (c->stream3) {
         (void)hipStreamSynchronize(c->stream3);
         (void)hipStreamDestroy(c->stream3);
@@ -1248,19 +1266,20 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
     const uint32_t nh = c->k3_block ? b->n_heavy : 0u;
     if (nh) {
         // the heavy problems on the second stream, from the same point (K2 done)
-        HIPCHK(hipStreamWaitEvent(c->stream2, b->ev[slot][5], 0));
-        HIPCHK(hipEventRecord(b->hev[slot][0], c->stream2));
+        hipStream_t s2 = pf_ctx_stream2(c);
+        HIPCHK(hipStreamWaitEvent(s2, b->ev[slot][5], 0));
+        HIPCHK(hipEventRecord(b->hev[slot][0], s2));
         // its own deferral list: a problem beyond its budget runs in a fallback
         // launch right behind it on the same stream, beside the main kernel
         pf_dev_batch dh = d;
         dh.k3_fb_list = d.k3_fb_list + 2ull * b->W;
         dh.k3_fb_ctr = reinterpret_cast<uint32_t *>(b->io + 80);
-        hipLaunchKernelGGL(pf_k3_heavy, dim3(nh), dim3(PF_K3H_THREADS), d.lds_heavy, c->stream2, dh);
+        hipLaunchKernelGGL(pf_k3_heavy, dim3(nh), dim3(PF_K3H_THREADS), d.lds_heavy, s2, dh);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(pf_k3_fallback, dim3(std::min<uint32_t>(nh, 512)), dim3(PF_K3_THREADS), d.lds_fb,
-                           c->stream2, dh);
+                           s2, dh);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(b->hev[slot][1], c->stream2));
+        HIPCHK(hipEventRecord(b->hev[slot][1], s2));
     }
     if (c->k3_block) {
         // persistent: as many workgroups as fit the device at this LDS budget,
