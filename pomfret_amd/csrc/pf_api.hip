@@ -34,6 +34,7 @@ __global__ void pf_k0_load(pf_load_dev d);
 __global__ void pf_k0_multi(pf_load_dev d);
 __global__ void pf_k0_scan(pf_load_dev d);
 __global__ void pf_k0_pack(pf_load_dev d);
+__global__ void pf_k0_pack_small(pf_load_dev d);
 __global__ void pf_selftest_div(unsigned long long *bad);
 __global__ void pf_selftest_wave(unsigned long long *bad);
 
@@ -1221,7 +1222,8 @@ static int enqueue(pf_dbatch *b, int slot, int stages = 3) {
         // window offsets, then the batch's read and call arrays
         hipLaunchKernelGGL(pf_k0_scan, dim3(1), dim3(PF_SCAN_THREADS), 0, st, b->ld);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(pf_k0_pack, dim3(b->W), dim3(PF_PACK_THREADS), 0, st, b->ld);
+        if (b->W >= PF_PACK_PIPE_MIN) hipLaunchKernelGGL(pf_k0_pack, dim3(b->W), dim3(PF_PACK_THREADS), 0, st, b->ld);
+        else hipLaunchKernelGGL(pf_k0_pack_small, dim3(b->W), dim3(PF_PACK_THREADS), 0, st, b->ld);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(b->ev[slot][2], st));

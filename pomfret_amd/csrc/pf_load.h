@@ -30,6 +30,13 @@
 #define PF_K0_EC (PF_K0_CB / 2)   /* explicit / implicit calls per chunk (CpGs are >= 2 apart) */
 #define PF_K0_SEQ_ALIGN 16        /* per-record SEQ slices are 16-byte aligned and padded */
 #define PF_PACK_THREADS 1024
+/* pf_k0_pack's pipelined copy pays in batches that fill the device with pack
+ * workgroups (a 1024-window batch: 0.755 -> 0.628 ms); in the 512-window
+ * batches of an 8-GPU rank its 256-call chunks lost (the N=8 step 12.63 ->
+ * 13.0 ms), so smaller batches run pf_k0_pack_small (512-call chunks) */
+#ifndef PF_PACK_PIPE_MIN
+#define PF_PACK_PIPE_MIN 768u
+#endif
 #define PF_SCAN_THREADS 1024
 
 /* status bits of K0 and the pack step (share the batch status word with

@@ -121,6 +121,9 @@ DEV unsigned long long k0_now() {
 #ifndef PF_PACK_PIPE
 #define PF_PACK_PIPE 1
 #endif
+#ifndef PF_PACK_U
+#define PF_PACK_U 4                        // calls per lane per chunk of the pipelined pack
+#endif
 // MM entries (round 6): 1 = a one-code header ("C+m?") parsed from one
 // 4-byte window instead of byte by byte
 #ifndef PF_K0_HDRFAST
@@ -1856,11 +1859,8 @@ __global__ __launch_bounds__(PF_SCAN_THREADS) void pf_k0_scan(pf_load_dev d) {
 // pack: one workgroup per window.  Kept records become reads in record
 // order; their scalars move to the read arrays and their calls from the
 // staging slices to the window's contiguous run (one wave per read).
-#if PF_PACK_PIPE
-__global__ __launch_bounds__(PF_PACK_THREADS) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_pack(pf_load_dev d) {
-#else
-__global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
-#endif
+template <bool PIPE>
+DEV void k0_pack(pf_load_dev d) {
     constexpr uint32_t NT = PF_PACK_THREADS, NW = NT / 64;
     __shared__ uint32_t sh32[2 * NW];
     __shared__ uint32_t l_n[NT];
@@ -1903,13 +1903,13 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
             l_dst[ek] = co;
         }
         __syncthreads();
-#if PF_PACK_PIPE
+        if constexpr (PIPE) {
         // one wave per read, 256-call chunks (4 calls per lane); the next
         // chunk's loads are issued before this chunk's stores, so a wave's
         // chunks overlap one memory round trip with the next (two chunks in
         // registers: the kernel keeps 8 waves per SIMD)
         {
-            constexpr uint32_t U = 4;
+            constexpr uint32_t U = PF_PACK_U;
             uint32_t j = wid, c0 = 0;
             uint32_t pv[U];
             uint8_t cv[U];
@@ -1943,7 +1943,7 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
                 c0 = cn0;
             }
         }
-#else
+        } else {
         // one wave per read, 8 calls per lane in flight (loads before stores)
         for (uint32_t j = wid; j < tk; j += NW) {
             const uint32_t cn = l_n[j];
@@ -1964,10 +1964,16 @@ __global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack(pf_load_dev d) {
                 }
             }
         }
-#endif
+        }
         __syncthreads();
         kc += tk;
         ccarry += tc;
     }
     if (last && tid == 0) d.read_call_off[re] = d.win_call_off[d.n_windows];
 }
+// a batch of PF_PACK_PIPE_MIN+ windows takes the pipelined copy (two
+// workgroups per CU held by the register budget), a smaller one the plain one
+__global__ __launch_bounds__(PF_PACK_THREADS) __attribute__((amdgpu_waves_per_eu(8))) void pf_k0_pack(pf_load_dev d) {
+    k0_pack<PF_PACK_PIPE != 0>(d);
+}
+__global__ __launch_bounds__(PF_PACK_THREADS) void pf_k0_pack_small(pf_load_dev d) { k0_pack<false>(d); }
